@@ -1,0 +1,113 @@
+"""Model tables for the Allsteps walker (compiled from the reference MJCF by ``mjcf.py``).
+
+``load_model()`` flattens ``walker3d.json`` into the fixed-size arrays of the C-ABI model struct
+(``include/allsteps.h`` :c:type:`as_model_t`): links in topological (parent-before-child) order,
+link 0 the floating root, link i >= 1 carrying hinge dof i-1; geoms ordered feet first so that the
+contact cap (``AS_MAX_CONTACTS``) never drops a foot contact in favour of another body's.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+MAX_LINKS = 32
+MAX_GEOMS = 32
+HERE = os.path.dirname(os.path.abspath(__file__))
+WALKER_JSON = os.path.join(HERE, "walker3d.json")
+
+
+def load_json(path: str = WALKER_JSON) -> dict:
+    with open(path) as f:
+        return json.load(f)
+
+
+def load_model(path: str = WALKER_JSON) -> dict:
+    """Return the flat model tables (numpy, float32 / int32) used by the kernels and the oracle."""
+    j = load_json(path)
+    links = j["links"]
+    nl = len(links)
+    if nl > MAX_LINKS:
+        raise ValueError(f"model has {nl} links > {MAX_LINKS}")
+    m = {
+        "num_links": nl,
+        "num_hinges": nl - 1,
+        "parent": np.full(MAX_LINKS, -1, np.int32),
+        "offset_pos": np.zeros((MAX_LINKS, 3), np.float32),
+        "offset_quat": np.zeros((MAX_LINKS, 4), np.float32),
+        "axis": np.zeros((MAX_LINKS, 3), np.float32),
+        "anchor": np.zeros((MAX_LINKS, 3), np.float32),
+        "mass": np.zeros(MAX_LINKS, np.float32),
+        "com": np.zeros((MAX_LINKS, 3), np.float32),
+        "inertia": np.zeros((MAX_LINKS, 6), np.float32),
+        "armature": np.zeros(MAX_LINKS, np.float32),
+        "lower": np.zeros(MAX_LINKS, np.float32),
+        "upper": np.zeros(MAX_LINKS, np.float32),
+        "cfg_dof_link": np.zeros(MAX_LINKS, np.int32),
+        "gear": np.zeros(MAX_LINKS, np.float32),
+    }
+    m["offset_quat"][:, 0] = 1.0
+    for i, L in enumerate(links):
+        if L["parent"] >= i:
+            raise ValueError("links must be in topological order")
+        m["parent"][i] = L["parent"]
+        m["offset_pos"][i] = L["offset_pos"]
+        m["offset_quat"][i] = L["offset_quat"]
+        m["mass"][i] = L["mass"]
+        m["com"][i] = L["com"]
+        I = np.array(L["inertia"])
+        m["inertia"][i] = [I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]]
+        if L["joint"] is not None:
+            jt = L["joint"]
+            m["axis"][i] = jt["axis"]
+            m["anchor"][i] = jt["anchor"]
+            m["armature"][i] = jt["armature"]
+            m["lower"][i], m["upper"][i] = jt["range"]
+    m["cfg_dof_link"][: nl - 1] = j["cfg_dof_link"]
+    m["gear"][: nl - 1] = j["gears"]
+
+    # geoms: feet first (right then left), then every other geom in link order
+    bl = j["body_link"]
+    foot_link = [bl["right_foot"], bl["left_foot"]]
+    geoms = []
+    for i, L in enumerate(links):
+        for g in L["geoms"]:
+            foot = foot_link.index(i) if i in foot_link else -1
+            geoms.append((0 if foot >= 0 else 1, foot, i, g))
+    geoms.sort(key=lambda t: (t[0], t[1], t[2]))
+    if len(geoms) > MAX_GEOMS:
+        raise ValueError("too many geoms")
+    m["num_geoms"] = len(geoms)
+    m["geom_link"] = np.zeros(MAX_GEOMS, np.int32)
+    m["geom_type"] = np.zeros(MAX_GEOMS, np.int32)
+    m["geom_foot"] = np.full(MAX_GEOMS, -1, np.int32)
+    m["geom_radius"] = np.zeros(MAX_GEOMS, np.float32)
+    m["geom_p0"] = np.zeros((MAX_GEOMS, 3), np.float32)
+    m["geom_p1"] = np.zeros((MAX_GEOMS, 3), np.float32)
+    m["geom_name"] = []
+    for k, (_, foot, li, g) in enumerate(geoms):
+        m["geom_link"][k] = li
+        m["geom_type"][k] = 0 if g["type"] == "sphere" else 1
+        m["geom_foot"][k] = foot
+        m["geom_radius"][k] = g["radius"]
+        m["geom_p0"][k] = g["p0"]
+        m["geom_p1"][k] = g["p1"]
+        m["geom_name"].append(g["name"])
+    m["torso_link"] = bl["torso"]
+    m["foot_link"] = np.array(foot_link, np.int32)
+    m["link_names"] = [L["name"] for L in links]
+    m["dof_names"] = list(j["cfg_dof_order"])
+    m["total_mass"] = float(j["total_mass"])
+    return m
+
+
+def joint_limits_cfg(m: dict) -> np.ndarray:
+    """(21, 2) joint position limits in cfg/PhysX dof order (ArticulationData.joint_pos_limits)."""
+    nh = m["num_hinges"]
+    lim = np.zeros((nh, 2), np.float32)
+    for k in range(nh):
+        li = m["cfg_dof_link"][k]
+        lim[k] = (m["lower"][li], m["upper"][li])
+    return lim

@@ -1,0 +1,659 @@
+/*
+ * physics.c -- CPU restatement of the articulated-body step that replaces PhysX
+ * (TEST INFRASTRUCTURE; see oracle.h).
+ *
+ * The reference steps PhysX 5 (isaacsim 4.5 / omni.physx, external, absent offline) through
+ * isaaclab/sim/simulation_context.py:453-478 with the articulation configured at
+ * isaaclab_assets/robots/walker3d.py:21-46 (self-collision on, 4 position / 0 velocity solver
+ * iterations, gyroscopic forces on, max_depenetration_velocity 10, implicit actuators with
+ * kp = kd = 0 so the effort target is the joint torque).  PARITY UNPINNED against PhysX.
+ *
+ * Algorithm (one substep, dt = 1/240; DESIGN.md §Dynamics is the spec the HIP kernel follows):
+ *   1. FK of all links, spatial quantities in a world-aligned frame with origin at the root link
+ *      origin (O).  Generalised velocity u = [v_com0 (3), w0 (3), qd hinges (nh)].
+ *   2. RNEA with qdd = 0 -> bias C(q, u) (Coriolis, centrifugal, gyroscopic, gravity).
+ *   3. CRBA -> joint-space inertia H (+ armature on the hinge diagonal), Cholesky H = L L^T.
+ *   4. u* = u + dt H^-1 (tau - C).
+ *   5. Contacts (robot spheres/capsules vs the 20 axis-aligned stone boxes, speculative margin)
+ *      and joint-limit rows; projected Gauss-Seidel on impulses (normal >= 0, box friction,
+ *      Baumgarte bias capped at max_depenetration_velocity), pgs_iters sweeps.
+ *   6. Semi-implicit integration: hinges q += dt u, root COM += dt v, orientation by exp map.
+ *   The per-(foot, stone) normal impulse of the last substep gives the contact-sensor flags
+ *   (contact_sensor.py:320-343: force_matrix_w = impulse / dt, tested > 1e-4 at
+ *   allsteps_env.py:421-425).
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+#define NV_MAX (OR_NDOF_ROOT + OR_MAX_LINKS)
+#define F(arr, f, n, e) (arr)[(size_t)(f) * (n) + (e)]
+
+typedef struct {
+  int nl, nv;
+  float R[OR_MAX_LINKS][9];  /* link rotation (world) */
+  float p[OR_MAX_LINKS][3];  /* link origin, relative to O */
+  float c[OR_MAX_LINKS][3];  /* link COM, relative to O */
+  float S[NV_MAX][6];        /* motion subspace [w; v_O] per dof */
+  float Ic[OR_MAX_LINKS][10];/* spatial inertia at O: m, h(3), Io(6) (xx yy zz xy xz yz) */
+  float Ib[OR_MAX_LINKS][10];/* single-body spatial inertia at O */
+} kin_t;
+
+static void quat_to_mat(const float q[4], float R[9]) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1.f - 2.f * (y * y + z * z); R[1] = 2.f * (x * y - w * z);       R[2] = 2.f * (x * z + w * y);
+  R[3] = 2.f * (x * y + w * z);       R[4] = 1.f - 2.f * (x * x + z * z); R[5] = 2.f * (y * z - w * x);
+  R[6] = 2.f * (x * z - w * y);       R[7] = 2.f * (y * z + w * x);       R[8] = 1.f - 2.f * (x * x + y * y);
+}
+
+static void axis_angle_mat(const float a[3], float ang, float R[9]) {
+  float c = cosf(ang), s = sinf(ang), t = 1.f - c;
+  R[0] = c + t * a[0] * a[0];        R[1] = t * a[0] * a[1] - s * a[2]; R[2] = t * a[0] * a[2] + s * a[1];
+  R[3] = t * a[0] * a[1] + s * a[2]; R[4] = c + t * a[1] * a[1];        R[5] = t * a[1] * a[2] - s * a[0];
+  R[6] = t * a[0] * a[2] - s * a[1]; R[7] = t * a[1] * a[2] + s * a[0]; R[8] = c + t * a[2] * a[2];
+}
+
+static void matmul3(const float A[9], const float B[9], float C[9]) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+static void matvec3(const float A[9], const float v[3], float o[3]) {
+  o[0] = A[0] * v[0] + A[1] * v[1] + A[2] * v[2];
+  o[1] = A[3] * v[0] + A[4] * v[1] + A[5] * v[2];
+  o[2] = A[6] * v[0] + A[7] * v[1] + A[8] * v[2];
+}
+
+static void cross(const float a[3], const float b[3], float o[3]) {
+  float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+
+static float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static float dot6(const float a[6], const float b[6]) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+/* Io w for symmetric (xx yy zz xy xz yz) */
+static void sym_mul(const float I[6], const float w[3], float o[3]) {
+  o[0] = I[0] * w[0] + I[3] * w[1] + I[4] * w[2];
+  o[1] = I[3] * w[0] + I[1] * w[1] + I[5] * w[2];
+  o[2] = I[4] * w[0] + I[5] * w[1] + I[2] * w[2];
+}
+
+/* spatial inertia (m, h, Io) times motion [w; v] -> force [Io w + h x v; m v - h x w] */
+static void inertia_mul(const float I[10], const float V[6], float out[6]) {
+  float Iw[3], hv[3], hw[3];
+  sym_mul(I + 4, V, Iw);
+  cross(I + 1, V + 3, hv);
+  cross(I + 1, V, hw);
+  for (int k = 0; k < 3; ++k) {
+    out[k] = Iw[k] + hv[k];
+    out[3 + k] = I[0] * V[3 + k] - hw[k];
+  }
+}
+
+/* [w;v] x_m [w2;v2] = [w x w2; w x v2 + v x w2] */
+static void crm(const float V[6], const float M[6], float o[6]) {
+  float a[3], b[3], c[3];
+  cross(V, M, a);
+  cross(V, M + 3, b);
+  cross(V + 3, M, c);
+  for (int k = 0; k < 3; ++k) { o[k] = a[k]; o[3 + k] = b[k] + c[k]; }
+}
+
+/* [w;v] x_f [n;f] = [w x n + v x f; w x f] */
+static void crf(const float V[6], const float Fv[6], float o[6]) {
+  float a[3], b[3], c[3];
+  cross(V, Fv, a);
+  cross(V + 3, Fv + 3, b);
+  cross(V, Fv + 3, c);
+  for (int k = 0; k < 3; ++k) { o[k] = a[k] + b[k]; o[3 + k] = c[k]; }
+}
+
+/* FK + motion subspace + spatial inertias. q_int: hinge angles in link order (link i -> q_int[i-1]). */
+static void kinematics(const or_model_t* m, const float root_quat[4], const float* q_int, kin_t* K) {
+  const int nl = m->num_links;
+  K->nl = nl;
+  K->nv = OR_NDOF_ROOT + m->num_hinges;
+  quat_to_mat(root_quat, K->R[0]);
+  K->p[0][0] = K->p[0][1] = K->p[0][2] = 0.f;
+  for (int i = 1; i < nl; ++i) {
+    int pa = m->parent[i];
+    float Roff[9], Rj[9], Rl[9], t[3], Ro[3], tmp[3];
+    quat_to_mat(m->offset_quat[i], Roff);
+    axis_angle_mat(m->axis[i], q_int[i - 1], Rj);
+    matmul3(Roff, Rj, Rl);
+    /* joint translation t_j = o - Rj o; local origin = offset_pos + Roff t_j */
+    matvec3(Rj, m->anchor[i], Ro);
+    for (int k = 0; k < 3; ++k) t[k] = m->anchor[i][k] - Ro[k];
+    matvec3(Roff, t, tmp);
+    for (int k = 0; k < 3; ++k) tmp[k] += m->offset_pos[i][k];
+    matmul3(K->R[pa], Rl, K->R[i]);
+    float wp[3];
+    matvec3(K->R[pa], tmp, wp);
+    for (int k = 0; k < 3; ++k) K->p[i][k] = K->p[pa][k] + wp[k];
+  }
+  for (int i = 0; i < nl; ++i) {
+    float cw[3];
+    matvec3(K->R[i], m->com[i], cw);
+    for (int k = 0; k < 3; ++k) K->c[i][k] = K->p[i][k] + cw[k];
+    /* world inertia about COM: R I R^T */
+    const float* Il = m->inertia[i];
+    float Im[9] = {Il[0], Il[3], Il[4], Il[3], Il[1], Il[5], Il[4], Il[5], Il[2]};
+    float T[9], Iw[9], Rt[9];
+    const float* R = K->R[i];
+    Rt[0] = R[0]; Rt[1] = R[3]; Rt[2] = R[6]; Rt[3] = R[1]; Rt[4] = R[4]; Rt[5] = R[7];
+    Rt[6] = R[2]; Rt[7] = R[5]; Rt[8] = R[8];
+    matmul3(R, Im, T);
+    matmul3(T, Rt, Iw);
+    float mass = m->mass[i], *c = K->c[i];
+    float cc = dot3(c, c);
+    float* B = K->Ib[i];
+    B[0] = mass;
+    B[1] = mass * c[0]; B[2] = mass * c[1]; B[3] = mass * c[2];
+    B[4] = Iw[0] + mass * (cc - c[0] * c[0]);
+    B[5] = Iw[4] + mass * (cc - c[1] * c[1]);
+    B[6] = Iw[8] + mass * (cc - c[2] * c[2]);
+    B[7] = Iw[1] - mass * c[0] * c[1];
+    B[8] = Iw[2] - mass * c[0] * c[2];
+    B[9] = Iw[5] - mass * c[1] * c[2];
+  }
+  /* motion subspace */
+  const float* c0 = K->c[0];
+  for (int k = 0; k < 3; ++k) {
+    float* Sl = K->S[k];
+    float* Sa = K->S[3 + k];
+    for (int j = 0; j < 6; ++j) Sl[j] = Sa[j] = 0.f;
+    Sl[3 + k] = 1.f;
+    float e[3] = {0.f, 0.f, 0.f};
+    e[k] = 1.f;
+    Sa[k] = 1.f;
+    cross(c0, e, Sa + 3);
+  }
+  for (int i = 1; i < nl; ++i) {
+    float a[3], o[3], Ro[3];
+    matvec3(K->R[i], m->axis[i], a);
+    matvec3(K->R[i], m->anchor[i], Ro);
+    for (int k = 0; k < 3; ++k) o[k] = K->p[i][k] + Ro[k];
+    float* S = K->S[OR_NDOF_ROOT + i - 1];
+    S[0] = a[0]; S[1] = a[1]; S[2] = a[2];
+    cross(o, a, S + 3);
+  }
+  /* composite inertias (world frame: plain sums over the subtree) */
+  for (int i = 0; i < nl; ++i) memcpy(K->Ic[i], K->Ib[i], sizeof(float) * 10);
+  for (int i = nl - 1; i >= 1; --i)
+    for (int k = 0; k < 10; ++k) K->Ic[m->parent[i]][k] += K->Ic[i][k];
+}
+
+/* dofs influencing link i: hinge dofs on the path to the root (deepest first), then root dofs */
+static int chain_dofs(const or_model_t* m, int link, int* out) {
+  int n = 0;
+  for (int l = link; l > 0; l = m->parent[l]) out[n++] = OR_NDOF_ROOT + l - 1;
+  for (int k = OR_NDOF_ROOT - 1; k >= 0; --k) out[n++] = k;
+  return n;
+}
+
+static void crba(const or_model_t* m, const kin_t* K, float* H) {
+  const int nv = K->nv;
+  memset(H, 0, sizeof(float) * (size_t)nv * nv);
+  int chain[NV_MAX];
+  for (int j = 0; j < nv; ++j) {
+    int link = j < OR_NDOF_ROOT ? 0 : j - OR_NDOF_ROOT + 1;
+    float Fj[6];
+    inertia_mul(K->Ic[link], K->S[j], Fj);
+    int nc = chain_dofs(m, link, chain);
+    for (int t = 0; t < nc; ++t) {
+      int k = chain[t];
+      if (k > j) continue; /* fill lower triangle (k <= j) and mirror */
+      float h = dot6(K->S[k], Fj);
+      H[j * nv + k] = h;
+      H[k * nv + j] = h;
+    }
+  }
+  for (int i = 1; i < m->num_links; ++i) {
+    int j = OR_NDOF_ROOT + i - 1;
+    H[j * nv + j] += m->armature[i];
+  }
+}
+
+static void link_velocities(const or_model_t* m, const kin_t* K, const float* u, float V[][6]) {
+  const float* c0 = K->c[0];
+  float wxc[3];
+  cross(c0, u + 3, wxc);
+  for (int k = 0; k < 3; ++k) { V[0][k] = u[3 + k]; V[0][3 + k] = u[k] + wxc[k]; }
+  for (int i = 1; i < K->nl; ++i) {
+    float qd = u[OR_NDOF_ROOT + i - 1];
+    const float* S = K->S[OR_NDOF_ROOT + i - 1];
+    for (int k = 0; k < 6; ++k) V[i][k] = V[m->parent[i]][k] + S[k] * qd;
+  }
+}
+
+static void rnea_bias(const or_model_t* m, const kin_t* K, const float* u, float gravity, float* C) {
+  float V[OR_MAX_LINKS][6], A[OR_MAX_LINKS][6], Fl[OR_MAX_LINKS][6];
+  link_velocities(m, K, u, V);
+  /* A_0 = [0; v_c0 x w] */
+  float vxw[3];
+  cross(u, u + 3, vxw);
+  for (int k = 0; k < 3; ++k) { A[0][k] = 0.f; A[0][3 + k] = vxw[k]; }
+  for (int i = 1; i < K->nl; ++i) {
+    float qd = u[OR_NDOF_ROOT + i - 1];
+    const float* S = K->S[OR_NDOF_ROOT + i - 1];
+    float Sq[6], cr[6];
+    for (int k = 0; k < 6; ++k) Sq[k] = S[k] * qd;
+    crm(V[i], Sq, cr);
+    for (int k = 0; k < 6; ++k) A[i][k] = A[m->parent[i]][k] + cr[k];
+  }
+  for (int i = 0; i < K->nl; ++i) {
+    float IA[6], IV[6], x[6];
+    inertia_mul(K->Ib[i], A[i], IA);
+    inertia_mul(K->Ib[i], V[i], IV);
+    crf(V[i], IV, x);
+    float mg[3] = {0.f, 0.f, m->mass[i] * gravity};
+    float cxmg[3];
+    cross(K->c[i], mg, cxmg);
+    for (int k = 0; k < 3; ++k) {
+      Fl[i][k] = IA[k] + x[k] - cxmg[k];
+      Fl[i][3 + k] = IA[3 + k] + x[3 + k] - mg[k];
+    }
+  }
+  for (int i = K->nl - 1; i >= 1; --i)
+    for (int k = 0; k < 6; ++k) Fl[m->parent[i]][k] += Fl[i][k];
+  for (int j = 0; j < K->nv; ++j) {
+    int link = j < OR_NDOF_ROOT ? 0 : j - OR_NDOF_ROOT + 1;
+    C[j] = dot6(K->S[j], Fl[link]);
+  }
+}
+
+static void cholesky(float* H, int n) {
+  for (int j = 0; j < n; ++j) {
+    float s = H[j * n + j];
+    for (int k = 0; k < j; ++k) s -= H[j * n + k] * H[j * n + k];
+    float d = sqrtf(s > 1e-12f ? s : 1e-12f);
+    H[j * n + j] = d;
+    float inv = 1.0f / d;
+    for (int i = j + 1; i < n; ++i) {
+      float t = H[i * n + j];
+      for (int k = 0; k < j; ++k) t -= H[i * n + k] * H[j * n + k];
+      H[i * n + j] = t * inv;
+    }
+  }
+}
+
+static void chol_solve(const float* L, int n, const float* b, float* x) {
+  float y[NV_MAX];
+  for (int i = 0; i < n; ++i) {
+    float s = b[i];
+    for (int k = 0; k < i; ++k) s -= L[i * n + k] * y[k];
+    y[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    float s = y[i];
+    for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+}
+
+/* ---------------------------------------------------------------- collision (boxes, spheres, capsules) */
+
+/* signed distance from p to an axis-aligned box (center c, half extents h); normal out of box */
+static float sd_box(const float p[3], const float c[3], const float h[3], float nrm[3]) {
+  float d[3], s[3];
+  for (int k = 0; k < 3; ++k) {
+    float r = p[k] - c[k];
+    s[k] = r >= 0.f ? 1.f : -1.f;
+    d[k] = fabsf(r) - h[k];
+  }
+  float o0 = d[0] > 0.f ? d[0] : 0.f, o1 = d[1] > 0.f ? d[1] : 0.f, o2 = d[2] > 0.f ? d[2] : 0.f;
+  float out = sqrtf(o0 * o0 + o1 * o1 + o2 * o2);
+  if (out > 0.f) {
+    float inv = 1.0f / out;
+    nrm[0] = s[0] * o0 * inv; nrm[1] = s[1] * o1 * inv; nrm[2] = s[2] * o2 * inv;
+    return out;
+  }
+  int ax = 0;
+  if (d[1] > d[ax]) ax = 1;
+  if (d[2] > d[ax]) ax = 2;
+  nrm[0] = nrm[1] = nrm[2] = 0.f;
+  nrm[ax] = s[ax];
+  return d[ax];
+}
+
+typedef struct {
+  int n;
+  int link[OR_MAX_CONTACTS], stone[OR_MAX_CONTACTS], foot[OR_MAX_CONTACTS];
+  float pt[OR_MAX_CONTACTS][3], nrm[OR_MAX_CONTACTS][3], sep[OR_MAX_CONTACTS];
+} contacts_t;
+
+static void add_contact(contacts_t* C, int link, int stone, int foot, const float P[3], const float nrm[3], float sep,
+                        float r) {
+  if (C->n >= OR_MAX_CONTACTS) return;
+  int c = C->n++;
+  C->link[c] = link; C->stone[c] = stone; C->foot[c] = foot; C->sep[c] = sep;
+  for (int k = 0; k < 3; ++k) { C->nrm[c][k] = nrm[k]; C->pt[c][k] = P[k] - nrm[k] * r; }
+}
+
+#define GOLDEN_ITERS 14
+
+static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, const float* stones_rel, int nst,
+                    contacts_t* C) {
+  C->n = 0;
+  const float* h = sim->stone_half;
+  /* broadphase: stones whose box is within 1.8 m of the root link origin (O) */
+  int cand[OR_MAX_STONES], nc = 0;
+  for (int s = 0; s < nst; ++s) {
+    const float* c = stones_rel + 3 * s;
+    float o = 0.f;
+    for (int k = 0; k < 3; ++k) {
+      float d = fabsf(c[k]) - h[k];
+      if (d > 0.f) o += d * d;
+    }
+    if (o < 1.8f * 1.8f) cand[nc++] = s;
+  }
+  for (int g = 0; g < m->num_geoms; ++g) {
+    int l = m->geom_link[g];
+    float r = m->geom_radius[g];
+    float a[3], b[3], t0[3], t1[3];
+    matvec3(K->R[l], m->geom_p0[g], t0);
+    matvec3(K->R[l], m->geom_p1[g], t1);
+    for (int k = 0; k < 3; ++k) { a[k] = K->p[l][k] + t0[k]; b[k] = K->p[l][k] + t1[k]; }
+    float L = sqrtf((b[0] - a[0]) * (b[0] - a[0]) + (b[1] - a[1]) * (b[1] - a[1]) + (b[2] - a[2]) * (b[2] - a[2]));
+    for (int ci = 0; ci < nc; ++ci) {
+      int s = cand[ci];
+      const float* c = stones_rel + 3 * s;
+      float nr[3];
+      if (m->geom_type[g] == 0) {
+        float sd = sd_box(a, c, h, nr) - r;
+        if (sd < sim->margin) add_contact(C, l, s, m->geom_foot[g], a, nr, sd, r);
+        continue;
+      }
+      /* capsule: bounding test on the segment midpoint */
+      float mid[3] = {0.5f * (a[0] + b[0]), 0.5f * (a[1] + b[1]), 0.5f * (a[2] + b[2])};
+      if (sd_box(mid, c, h, nr) > 0.5f * L + r + sim->margin) continue;
+      float n0[3], n1[3];
+      float s0 = sd_box(a, c, h, n0) - r;
+      float s1 = sd_box(b, c, h, n1) - r;
+      /* golden-section minimisation of the (convex) sd along the segment */
+      const float gr = 0.6180339887f;
+      float lo = 0.f, hi = 1.f;
+      float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
+      float P1[3], P2[3], tn[3];
+      for (int k = 0; k < 3; ++k) { P1[k] = a[k] + x1 * (b[k] - a[k]); P2[k] = a[k] + x2 * (b[k] - a[k]); }
+      float f1 = sd_box(P1, c, h, tn), f2 = sd_box(P2, c, h, tn);
+      for (int it = 0; it < GOLDEN_ITERS; ++it) {
+        if (f1 < f2) {
+          hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
+          for (int k = 0; k < 3; ++k) P1[k] = a[k] + x1 * (b[k] - a[k]);
+          f1 = sd_box(P1, c, h, tn);
+        } else {
+          lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
+          for (int k = 0; k < 3; ++k) P2[k] = a[k] + x2 * (b[k] - a[k]);
+          f2 = sd_box(P2, c, h, tn);
+        }
+      }
+      float ts = 0.5f * (lo + hi), Ps[3], ns[3];
+      for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (b[k] - a[k]);
+      float ss = sd_box(Ps, c, h, ns) - r;
+      if (s0 < sim->margin) add_contact(C, l, s, m->geom_foot[g], a, n0, s0, r);
+      if (s1 < sim->margin) add_contact(C, l, s, m->geom_foot[g], b, n1, s1, r);
+      float smin = s0 < s1 ? s0 : s1;
+      if (ss < sim->margin && ss < smin - 0.002f) add_contact(C, l, s, m->geom_foot[g], Ps, ns, ss, r);
+    }
+  }
+}
+
+/* ---------------------------------------------------------------- one env step (decimation substeps) */
+
+typedef struct {
+  int nrow;
+  int type[OR_MAX_ROWS];     /* 0 normal, 1 tangent, 2 limit */
+  int contact[OR_MAX_ROWS];
+  float target[OR_MAX_ROWS];
+  float J[OR_MAX_ROWS][NV_MAX];
+  float W[OR_MAX_ROWS][NV_MAX];
+  float Ad[OR_MAX_ROWS];
+  float lam[OR_MAX_ROWS];
+} rows_t;
+
+static void contact_row(const or_model_t* m, const kin_t* K, int link, const float P[3], const float d[3], float* J) {
+  float f6[6];
+  cross(P, d, f6);
+  f6[3] = d[0]; f6[4] = d[1]; f6[5] = d[2];
+  for (int j = 0; j < K->nv; ++j) J[j] = 0.f;
+  int chain[NV_MAX];
+  int nc = chain_dofs(m, link, chain);
+  for (int t = 0; t < nc; ++t) J[chain[t]] = dot6(K->S[chain[t]], f6);
+}
+
+static void tangents(const float n[3], float t1[3], float t2[3]) {
+  float e[3] = {1.f, 0.f, 0.f};
+  if (fabsf(n[0]) > 0.9f) { e[0] = 0.f; e[1] = 1.f; }
+  cross(n, e, t1);
+  float inv = 1.0f / sqrtf(dot3(t1, t1));
+  for (int k = 0; k < 3; ++k) t1[k] *= inv;
+  cross(n, t1, t2);
+}
+
+static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3], float root_quat[4], float* q_int,
+                    float* u, const float* tau_int, const float* stones_w, int nst, uint32_t mask[2]) {
+  kin_t K;
+  kinematics(m, root_quat, q_int, &K);
+  const int nv = K.nv, nh = m->num_hinges;
+  const float dt = sim->dt;
+  float H[NV_MAX * NV_MAX], C[NV_MAX], b[NV_MAX], acc[NV_MAX];
+  crba(m, &K, H);
+  rnea_bias(m, &K, u, sim->gravity, C);
+  for (int j = 0; j < nv; ++j) b[j] = (j < OR_NDOF_ROOT ? 0.f : tau_int[j - OR_NDOF_ROOT]) - C[j];
+  cholesky(H, nv);
+  chol_solve(H, nv, b, acc);
+  for (int j = 0; j < nv; ++j) u[j] += dt * acc[j];
+
+  /* constraints */
+  float stones_rel[OR_MAX_STONES * 3];
+  for (int s = 0; s < nst; ++s)
+    for (int k = 0; k < 3; ++k) stones_rel[3 * s + k] = stones_w[3 * s + k] - root_pos[k];
+  contacts_t Cn;
+  collide(m, sim, &K, stones_rel, nst, &Cn);
+  static __thread rows_t Rw;
+  rows_t* R = &Rw;
+  R->nrow = 0;
+  for (int c = 0; c < Cn.n && R->nrow + 3 <= OR_MAX_ROWS; ++c) {
+    float t1[3], t2[3];
+    tangents(Cn.nrm[c], t1, t2);
+    const float* dirs[3] = {Cn.nrm[c], t1, t2};
+    for (int d = 0; d < 3; ++d) {
+      int r = R->nrow++;
+      R->type[r] = d == 0 ? 0 : 1;
+      R->contact[r] = c;
+      contact_row(m, &K, Cn.link[c], Cn.pt[c], dirs[d], R->J[r]);
+      float s = Cn.sep[c];
+      if (d == 0)
+        R->target[r] = s < 0.f ? fminf(sim->baumgarte * fmaxf(-s - sim->slop, 0.f) / dt, sim->max_depen_vel)
+                               : -s / dt;
+      else
+        R->target[r] = 0.f;
+    }
+  }
+  for (int i = 1; i <= nh && R->nrow < OR_MAX_ROWS; ++i) {
+    int j = OR_NDOF_ROOT + i - 1;
+    float qv = q_int[i - 1], pred = qv + dt * u[j];
+    for (int side = 0; side < 2 && R->nrow < OR_MAX_ROWS; ++side) {
+      float err = side == 0 ? m->lower[i] - qv : qv - m->upper[i];
+      int viol = side == 0 ? pred < m->lower[i] : pred > m->upper[i];
+      if (!viol) continue;
+      int r = R->nrow++;
+      R->type[r] = 2;
+      R->contact[r] = -1;
+      for (int k = 0; k < nv; ++k) R->J[r][k] = 0.f;
+      R->J[r][j] = side == 0 ? 1.f : -1.f;
+      R->target[r] = err > 0.f ? fminf(sim->baumgarte * err / dt, sim->max_depen_vel) : err / dt;
+    }
+  }
+  for (int r = 0; r < R->nrow; ++r) {
+    chol_solve(H, nv, R->J[r], R->W[r]);
+    float a = 0.f;
+    for (int k = 0; k < nv; ++k) a += R->J[r][k] * R->W[r][k];
+    R->Ad[r] = 1.0f / (a + 1e-9f);
+    R->lam[r] = 0.f;
+  }
+  for (int it = 0; it < sim->pgs_iters; ++it) {
+    for (int r = 0; r < R->nrow; ++r) {
+      float v = 0.f;
+      for (int k = 0; k < nv; ++k) v += R->J[r][k] * u[k];
+      float l0 = R->lam[r];
+      float l1;
+      if (R->type[r] == 1) {
+        int rn = r - (r % 3 == 1 ? 1 : 2); /* normal row of this contact */
+        float lim = sim->friction * R->lam[rn];
+        l1 = l0 - v * R->Ad[r];
+        l1 = l1 < -lim ? -lim : (l1 > lim ? lim : l1);
+      } else {
+        l1 = l0 + (R->target[r] - v) * R->Ad[r];
+        l1 = l1 > 0.f ? l1 : 0.f;
+      }
+      float dl = l1 - l0;
+      R->lam[r] = l1;
+      for (int k = 0; k < nv; ++k) u[k] += R->W[r][k] * dl;
+    }
+  }
+  /* contact sensor flags of this substep: |sum_n lambda_n n| / dt > eps per (foot, stone) */
+  mask[0] = mask[1] = 0u;
+  for (int c = 0; c < Cn.n; ++c) {
+    if (Cn.foot[c] < 0) continue;
+    if (3 * c >= R->nrow) break;
+    float fx = 0.f, fy = 0.f, fz = 0.f;
+    for (int c2 = 0; c2 < Cn.n && 3 * c2 < R->nrow; ++c2) {
+      if (Cn.foot[c2] != Cn.foot[c] || Cn.stone[c2] != Cn.stone[c]) continue;
+      float l = R->lam[3 * c2];
+      fx += l * Cn.nrm[c2][0]; fy += l * Cn.nrm[c2][1]; fz += l * Cn.nrm[c2][2];
+    }
+    float fn = sqrtf(fx * fx + fy * fy + fz * fz) / dt;
+    if (fn > 1e-4f) mask[Cn.foot[c]] |= 1u << Cn.stone[c];
+  }
+  /* clamp joint speeds, integrate */
+  for (int i = 0; i < nh; ++i) {
+    float* v = &u[OR_NDOF_ROOT + i];
+    if (*v > sim->max_joint_vel) *v = sim->max_joint_vel;
+    if (*v < -sim->max_joint_vel) *v = -sim->max_joint_vel;
+    q_int[i] += dt * *v;
+  }
+  float c0w[3];
+  for (int k = 0; k < 3; ++k) c0w[k] = root_pos[k] + K.c[0][k] + dt * u[k];
+  const float* w = u + 3;
+  float wn = sqrtf(dot3(w, w));
+  float th = wn * dt, dq[4];
+  if (th > 1e-12f) {
+    float s = sinf(0.5f * th) / wn;
+    dq[0] = cosf(0.5f * th); dq[1] = w[0] * s; dq[2] = w[1] * s; dq[3] = w[2] * s;
+  } else {
+    dq[0] = 1.f; dq[1] = 0.5f * dt * w[0]; dq[2] = 0.5f * dt * w[1]; dq[3] = 0.5f * dt * w[2];
+  }
+  const float* q0 = root_quat;
+  float nq[4] = {dq[0] * q0[0] - dq[1] * q0[1] - dq[2] * q0[2] - dq[3] * q0[3],
+                 dq[0] * q0[1] + dq[1] * q0[0] + dq[2] * q0[3] - dq[3] * q0[2],
+                 dq[0] * q0[2] - dq[1] * q0[3] + dq[2] * q0[0] + dq[3] * q0[1],
+                 dq[0] * q0[3] + dq[1] * q0[2] - dq[2] * q0[1] + dq[3] * q0[0]};
+  float qn = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+  for (int k = 0; k < 4; ++k) root_quat[k] = nq[k] * qn;
+  float Rn[9], cl[3];
+  quat_to_mat(root_quat, Rn);
+  matvec3(Rn, m->com[0], cl);
+  for (int k = 0; k < 3; ++k) root_pos[k] = c0w[k] - cl[k];
+}
+
+void or_fk_bodies(const or_model_t* m, const float root_pos[3], const float root_quat[4], const float* q_cfg,
+                  float body_pos[9]) {
+  float q_int[OR_MAX_LINKS];
+  for (int k = 0; k < m->num_hinges; ++k) q_int[m->cfg_dof_link[k] - 1] = q_cfg[k];
+  kin_t K;
+  kinematics(m, root_quat, q_int, &K);
+  int ls[3] = {m->torso_link, m->foot_link[0], m->foot_link[1]};
+  for (int b = 0; b < 3; ++b)
+    for (int k = 0; k < 3; ++k) body_pos[3 * b + k] = root_pos[k] + K.p[ls[b]][k];
+}
+
+void or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st, int e,
+                     const float* act_clamped) {
+  const int n = st->n, nh = m->num_hinges;
+  float rp[3], rq[4], q_int[OR_MAX_LINKS], u[NV_MAX], tau[OR_MAX_LINKS], stones[OR_MAX_STONES * 3];
+  for (int k = 0; k < 3; ++k) rp[k] = F(st->root_pos, k, n, e);
+  for (int k = 0; k < 4; ++k) rq[k] = F(st->root_quat, k, n, e);
+  for (int k = 0; k < 3; ++k) { u[k] = F(st->root_lin, k, n, e); u[3 + k] = F(st->root_ang, k, n, e); }
+  /* ENV:270-274 _apply_action: tau = gain[curriculum] * gear * a (ImplicitActuator pass-through) */
+  float gain = task->gain_curriculum[st->curriculum[0]];
+  for (int k = 0; k < nh; ++k) {
+    int i = m->cfg_dof_link[k] - 1;
+    q_int[i] = F(st->q, k, n, e);
+    u[OR_NDOF_ROOT + i] = F(st->qd, k, n, e);
+    tau[i] = gain * m->gear[k] * act_clamped[k];
+  }
+  const int nst = task->num_steps;
+  for (int s = 0; s < nst; ++s)
+    for (int k = 0; k < 3; ++k) stones[3 * s + k] = F(st->stones, s * 3 + k, n, e);
+  uint32_t mask[2] = {0u, 0u};
+  for (int s = 0; s < sim->substeps; ++s) substep(m, sim, rp, rq, q_int, u, tau, stones, nst, mask);
+  for (int k = 0; k < 3; ++k) {
+    F(st->root_pos, k, n, e) = rp[k];
+    F(st->root_lin, k, n, e) = u[k];
+    F(st->root_ang, k, n, e) = u[3 + k];
+  }
+  for (int k = 0; k < 4; ++k) F(st->root_quat, k, n, e) = rq[k];
+  for (int k = 0; k < nh; ++k) {
+    int i = m->cfg_dof_link[k] - 1;
+    F(st->q, k, n, e) = q_int[i];
+    F(st->qd, k, n, e) = u[OR_NDOF_ROOT + i];
+  }
+  F(st->contact_mask, 0, n, e) = mask[0];
+  F(st->contact_mask, 1, n, e) = mask[1];
+  float bp[9], qc[OR_MAX_LINKS];
+  for (int k = 0; k < nh; ++k) qc[k] = F(st->q, k, n, e);
+  or_fk_bodies(m, rp, rq, qc, bp);
+  for (int c = 0; c < 9; ++c) F(st->body_pos, c, n, e) = bp[c];
+}
+
+/* ---------------------------------------------------------------- env-level API */
+
+void or_env_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
+                 const float* actions, const float* reset_draws, uint64_t seed, float* obs, float* rew,
+                 uint8_t* term, uint8_t* trunc, int32_t* any_reset, int nthreads) {
+  const int n = st->n;
+  (void)nthreads;
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
+  for (int e = 0; e < n; ++e) {
+    float a[OR_MAX_LINKS];
+    for (int k = 0; k < m->num_hinges; ++k) {
+      float x = actions[(size_t)e * m->num_hinges + k];
+      a[k] = x < -1.f ? -1.f : (x > 1.f ? 1.f : x);
+    }
+    or_physics_step(m, sim, task, st, e, a);
+  }
+  or_task_post_physics(m, task, st, actions, NULL, NULL, reset_draws, seed, NULL, NULL, obs, rew, term, trunc,
+                       any_reset);
+}
+
+void or_env_reset_all(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
+                      const float* reset_draws, uint64_t seed, float* obs) {
+  (void)sim;
+  or_task_reset_all(m, task, st, reset_draws, seed, obs);
+}
+
+/* ---------------------------------------------------------------- known-answer test hooks */
+
+void or_mass_matrix(const or_model_t* m, const float root_pos[3], const float root_quat[4], const float* q_int,
+                    float* H, float* com0) {
+  (void)root_pos;
+  kin_t K;
+  kinematics(m, root_quat, q_int, &K);
+  crba(m, &K, H);
+  for (int k = 0; k < 3; ++k) com0[k] = K.c[0][k];
+}
+
+void or_bias_forces(const or_model_t* m, const float root_pos[3], const float root_quat[4], const float* q_int,
+                    const float* u, float gravity, float* C) {
+  (void)root_pos;
+  kin_t K;
+  kinematics(m, root_quat, q_int, &K);
+  rnea_bias(m, &K, u, gravity, C);
+}

@@ -1,0 +1,548 @@
+"""Generate golden fixtures from the reference Allsteps task logic (run in the build container).
+
+    python tests/golden/gen_golden.py            # writes tests/golden/*.npz
+
+The reference task module (``allsteps_env.py``) and ``isaaclab/utils/math.py`` are imported from
+``/root/reference`` with stub Isaac modules (``refload.py``).  PhysX is absent, so
+the robot / sensor data are synthetic: a seeded generator produces root states, joint states,
+torso/foot positions and per-(foot, stone) contact force matrices chosen to exercise every branch
+of the task logic (target reaches, stop-frame progression, falls, speed and height terminations,
+time-outs, the curriculum bump, mirrored resets, the foot-state double tick and stale contacts).
+All ``torch.rand`` draws the reference makes are intercepted and stored, so the restatement can
+replay them exactly ("inject the draws").
+
+Fixtures (all float32 / int64 / bool numpy arrays, ``np.load(allow_pickle=False)``):
+  footsteps.npz   -- _generate_foot_steps_allsteps at curriculum levels 0/3/9 (+ draws)
+  math.npz        -- euler_xyz_from_quat, quat_rotate_inverse, subtract_frame_transforms,
+                     scale/unscale_transform on random and edge-case inputs
+  task_seq.npz    -- a 40-step post-physics sequence of DirectRLEnv.step (dones -> rewards ->
+                     reset -> obs) on 24 envs, every input and output per step
+  mirror.npz      -- get_symmetric_states_rl_games / _rsl_rl
+  rlg_wrapper.npz -- RlGamesVecEnvWrapper.step I/O on a fake env
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import refload  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from allsteps_isaaclab_amd.model.mjcf import CFG_DOF_ORDER, CFG_GEARS  # noqa: E402
+
+import json  # noqa: E402
+
+MODEL = json.load(open(os.path.join(os.path.dirname(os.path.dirname(HERE)),
+                                    "allsteps_isaaclab_amd", "model", "walker3d.json")))
+
+BODY_NAMES = ["walker3d", "head", "torso", "waist", "right_upper_arm", "left_upper_arm", "pelvis",
+              "right_lower_arm", "left_lower_arm", "right_thigh", "left_thigh", "right_hand",
+              "left_hand", "right_shin", "left_shin", "right_foot", "left_foot"]
+
+
+class RandRecorder:
+    """Proxy for the ``torch`` module global of a reference module: records every torch.rand."""
+
+    def __init__(self, gen: torch.Generator):
+        self._gen = gen
+        self.draws: list[torch.Tensor] = []
+
+    def __getattr__(self, name):
+        return getattr(torch, name)
+
+    def rand(self, *size, device=None, dtype=None, **kw):
+        if len(size) == 1 and isinstance(size[0], (tuple, list, torch.Size)):
+            size = tuple(size[0])
+        t = torch.rand(*size, generator=self._gen, dtype=torch.float32)
+        self.draws.append(t.clone())
+        return t
+
+
+def joint_limits() -> np.ndarray:
+    lim = np.zeros((21, 2), np.float32)
+    for k, name in enumerate(CFG_DOF_ORDER):
+        li = MODEL["cfg_dof_link"][k]
+        lim[k] = MODEL["links"][li]["joint"]["range"]
+    return lim
+
+
+def make_cfg():
+    # values from allsteps_env_cfg.py:54-58,90,95-97,133-155,212-234
+    return types.SimpleNamespace(
+        num_steps=20, step_radius=0.25, joint_gears=list(CFG_GEARS), force_scale=1.5,
+        torso_name="torso", foot_names=["right_foot", "left_foot"],
+        hip_y_names=["right_hip_y", "left_hip_y"],
+        right_body_names=["right_shoulder_x", "right_shoulder_y", "right_shoulder_z", "right_elbow",
+                          "right_hip_x", "right_hip_y", "right_hip_z", "right_knee", "right_ankle"],
+        left_body_names=["left_shoulder_x", "left_shoulder_y", "left_shoulder_z", "left_elbow",
+                         "left_hip_x", "left_hip_y", "left_hip_z", "left_knee", "left_ankle"],
+        negation_body_names=["abdomen_z", "abdomen_x"],
+        energy_cost_scale=0.009, actions_cost_scale=0.01, alive_reward_scale=2.0, dof_vel_scale=0.1,
+        joint_at_limit_cost_scale=0.1, death_cost=-1.0, termination_height_absolute=0.4,
+        angular_velocity_scale=0.25, initial_joint_angle_range=[-0.1, 0.1],
+        initial_joint_angle_clip_range=[-0.95, 0.95], camera_pos=(1.5, -4.0, 1.5),
+    )
+
+
+class FakeData:
+    def __init__(self, n: int):
+        self.body_names = list(BODY_NAMES)
+        self.joint_names = list(CFG_DOF_ORDER)
+        self.root_state_w = torch.zeros(n, 13)
+        self.root_state_w[:, 3] = 1.0
+        self.body_pos_w = torch.zeros(n, len(BODY_NAMES), 3)
+        self.joint_pos = torch.zeros(n, 21)
+        self.joint_vel = torch.zeros(n, 21)
+        lim = torch.from_numpy(joint_limits())
+        self.joint_pos_limits = lim.unsqueeze(0).repeat(n, 1, 1)
+        self.default_joint_pos = torch.zeros(n, 21)
+        self.default_joint_vel = torch.zeros(n, 21)
+        self.default_root_state = torch.zeros(n, 13)
+        self.default_root_state[:, :3] = torch.tensor([0.2, 0.0, 1.5])  # walker3d.py:37
+        self.default_root_state[:, 3] = 1.0
+
+    root_pos_w = property(lambda s: s.root_state_w[:, :3])
+    root_quat_w = property(lambda s: s.root_state_w[:, 3:7])
+    root_lin_vel_w = property(lambda s: s.root_state_w[:, 7:10])
+    root_ang_vel_w = property(lambda s: s.root_state_w[:, 10:13])
+
+
+def fake_fk(root_pos: torch.Tensor, q: torch.Tensor):
+    """Deterministic synthetic 'FK' for post-reset body positions (recorded; not physics)."""
+    torso = root_pos.clone()
+    rf = root_pos + torch.stack([0.05 * q[:, 12], -0.11 + 0.02 * q[:, 11], -1.27 + 0.03 * q[:, 17]], -1)
+    lf = root_pos + torch.stack([0.05 * q[:, 15], 0.11 + 0.02 * q[:, 14], -1.27 + 0.03 * q[:, 18]], -1)
+    return torso, rf, lf
+
+
+class FakeRobot:
+    def __init__(self, n: int, record: list):
+        self.data = FakeData(n)
+        self._ALL_INDICES = torch.arange(n, dtype=torch.long)
+        self._record = record
+
+    def reset(self, env_ids):
+        pass
+
+    def write_root_pose_to_sim(self, pose, env_ids):
+        self.data.root_state_w[env_ids, :7] = pose
+
+    def write_root_velocity_to_sim(self, vel, env_ids):
+        self.data.root_state_w[env_ids, 7:] = vel
+
+    def write_joint_state_to_sim(self, pos, vel, joint_ids, env_ids):
+        self.data.joint_pos[env_ids] = pos
+        self.data.joint_vel[env_ids] = vel
+        torso, rf, lf = fake_fk(self.data.root_state_w[env_ids, :3], pos)
+        bi = BODY_NAMES.index
+        self.data.body_pos_w[env_ids, bi("torso")] = torso
+        self.data.body_pos_w[env_ids, bi("right_foot")] = rf
+        self.data.body_pos_w[env_ids, bi("left_foot")] = lf
+
+
+class FakeSensor:
+    def __init__(self, n: int):
+        self.data = types.SimpleNamespace(force_matrix_w=torch.zeros(n, 1, 20, 3))
+
+
+def build_env(mod, n: int, gen: torch.Generator):
+    E = mod.AllstepsEnv
+    env = object.__new__(E)
+    env.cfg = make_cfg()
+    env.num_envs = n
+    env.device = "cpu"
+    env.step_dt = (1 / 240) * 4  # simulation_cfg dt * decimation (direct_rl_env.py step_dt)
+    env.max_episode_length = math.ceil(15.0 / ((1 / 240) * 4))
+    env.episode_length_buf = torch.zeros(n, dtype=torch.long)
+    env.reset_terminated = torch.zeros(n, dtype=torch.bool)
+    env.reset_time_outs = torch.zeros(n, dtype=torch.bool)
+    env.actions = torch.zeros(n, 21)
+    rec: list = []
+    env.robot = FakeRobot(n, rec)
+    env.sensor = FakeSensor(n)
+    env.sensor_left = FakeSensor(n)
+    env.sensor_right = FakeSensor(n)
+    env.scene = types.SimpleNamespace(env_origins=torch.zeros(n, 3))
+    env.sim = types.SimpleNamespace(set_camera_view=lambda **k: None)
+    env.steps = types.SimpleNamespace(write_object_pose_to_sim=lambda *a, **k: None)
+    env.marker = types.SimpleNamespace(visualize=lambda **k: None)
+    # replicate AllstepsEnv.__init__ (allsteps_env.py:40-96) without DirectRLEnv.__init__
+    env.dist_range = torch.tensor([0.75, 0.9], dtype=torch.float32)
+    env.pitch_range = torch.tensor([-30, 30], dtype=torch.float32)
+    env.yaw_range = torch.tensor([-20, 20], dtype=torch.float32)
+    env.tilt_range = torch.tensor([-15, 15], dtype=torch.float32)
+    env.max_curriculum = torch.tensor(9, dtype=torch.int64)
+    env.termination_curriculum = torch.linspace(0.75, 0.45, int(env.max_curriculum) + 1)
+    env.applied_gain_curriculum = torch.linspace(1.2, 1.2, int(env.max_curriculum) + 1)
+    env.curriculum = torch.zeros(n, dtype=torch.int64)
+    env.num_steps = 20
+    env.init_step_separation = 0.75
+    env.step_radius = 0.25
+    env.target_dim = 3
+    env.curriculum_progess_theshold = 12
+    env.foot_sep = 0.16
+    env.mirrored = False
+    env.stop_frames = 2
+    env.look_ahead = 2
+    env.look_behind = 1
+    env.steps_pos = torch.zeros(n, 20, 3)
+    env.steps_dphi = torch.zeros(n, 20)
+    env.targets_w = torch.zeros(n, 3, 3)
+    env.targets_b = torch.zeros(n, 3, 3)
+    env.pre_defined_swing_leg = torch.ones(n, 20, dtype=torch.int64)
+    env.swing_leg = torch.zeros(n, dtype=torch.int64)
+    env.curr_target_index = torch.ones(n, dtype=torch.int64)
+    env.prev_target_index = torch.clamp(env.curr_target_index - 1, 0, 19)
+    env.next_target_index = torch.clamp(env.curr_target_index + 1, 0, 19)
+    env.target_reach_count = torch.zeros(n, dtype=torch.int64)
+    env.foot_contact = torch.zeros(n, 2)
+    env.joint_gears = torch.tensor(env.cfg.joint_gears, dtype=torch.float32)
+    env.force_scale = env.cfg.force_scale
+    env.foot_names = env.cfg.foot_names
+    env.foot_indices = [BODY_NAMES.index(x) for x in env.foot_names]
+    env.torso_index = BODY_NAMES.index("torso")
+    J = CFG_DOF_ORDER.index
+    env.hip_y_index = torch.tensor([J(x) for x in env.cfg.hip_y_names])
+    env.right_body_indices = torch.tensor([J(x) for x in env.cfg.right_body_names])
+    env.left_body_indices = torch.tensor([J(x) for x in env.cfg.left_body_names])
+    env.negation_body_indices = torch.tensor([J(x) for x in env.cfg.negation_body_names])
+    env.potentials = torch.zeros(n)
+    env.old_potentials = env.potentials.clone()
+    env.old_obs = None
+    env.curriculum_counter = 0
+    return env
+
+
+# ----------------------------------------------------------------------------------------------
+def gen_footsteps(mod, out: dict):
+    n = 8
+    for level in (0, 3, 9):
+        g = torch.Generator().manual_seed(1000 + level)
+        rec = RandRecorder(g)
+        env = build_env(mod, n, g)
+        env.curriculum = torch.full((n,), level, dtype=torch.int64)
+        saved = mod.torch
+        mod.torch = rec
+        try:
+            pos, dphi, swing = env._generate_foot_steps_allsteps()
+        finally:
+            mod.torch = saved
+        assert len(rec.draws) == 5
+        out[f"fs{level}_draws"] = torch.stack(rec.draws).numpy()  # (5, n, 20)
+        out[f"fs{level}_pos"] = pos.numpy()
+        out[f"fs{level}_dphi"] = dphi.numpy()
+        out[f"fs{level}_swing"] = swing.numpy()
+
+
+def gen_math(math_mod, out: dict):
+    g = torch.Generator().manual_seed(7)
+    n = 256
+    q = torch.randn(n, 4, generator=g)
+    q[0] = torch.tensor([1.0, 0, 0, 0])
+    q[1] = torch.tensor([1.0, -0.0, -0.0, -0.0])
+    q[2] = torch.tensor([0.70710677, 0.0, 0.70710677, 0.0])   # |sin_pitch| >= 1 branch
+    q[3] = torch.tensor([0.70710677, 0.0, -0.70710677, 0.0])
+    q[4] = torch.tensor([0.9995, -0.03, -0.01, 0.0])          # small negative roll/pitch -> ~2pi
+    q[5:] = q[5:] / q[5:].norm(dim=-1, keepdim=True)
+    q[4] = q[4] / q[4].norm()
+    v = torch.randn(n, 3, generator=g) * 3.0
+    t01 = torch.randn(n, 3, generator=g) * 5.0
+    t02 = torch.randn(n, 3, generator=g) * 5.0
+    qs = q.clone()
+    qs[128:] *= 1.7  # non-unit quats for subtract_frame_transforms' normalize()
+    r, p, y = math_mod.euler_xyz_from_quat(q)
+    out["m_q"] = q.numpy()
+    out["m_v"] = v.numpy()
+    out["m_roll"], out["m_pitch"], out["m_yaw"] = r.numpy(), p.numpy(), y.numpy()
+    out["m_qri"] = math_mod.quat_rotate_inverse(q, v).numpy()
+    out["m_qr"] = math_mod.quat_rotate(q, v).numpy()
+    out["m_t01"], out["m_t02"], out["m_qs"] = t01.numpy(), t02.numpy(), qs.numpy()
+    out["m_sft"] = math_mod.subtract_frame_transforms(t01=t01, q01=qs, t02=t02)[0].numpy()
+    lim = torch.from_numpy(joint_limits())
+    x = (torch.rand(n, 21, generator=g) * 2 - 1) * 2.5
+    out["m_x"] = x.numpy()
+    out["m_lim"] = lim.numpy()
+    out["m_scale"] = math_mod.scale_transform(x, lim[:, 0], lim[:, 1]).numpy()
+    out["m_unscale"] = math_mod.unscale_transform(x, lim[:, 0], lim[:, 1]).numpy()
+
+
+def _random_quat(g, n, scale):
+    ang = (torch.rand(n, 3, generator=g) * 2 - 1) * scale
+    cr, sr = torch.cos(ang[:, 0] / 2), torch.sin(ang[:, 0] / 2)
+    cp, sp = torch.cos(ang[:, 1] / 2), torch.sin(ang[:, 1] / 2)
+    cy, sy = torch.cos(ang[:, 2] / 2), torch.sin(ang[:, 2] / 2)
+    w = cr * cp * cy + sr * sp * sy
+    x = sr * cp * cy - cr * sp * sy
+    y = cr * sp * cy + sr * cp * sy
+    z = cr * cp * sy - sr * sp * cy
+    return torch.stack([w, x, y, z], -1)
+
+
+def synth_physics(env, g: torch.Generator, t: int, calm: bool = False):
+    """Overwrite the fake robot/sensor data with a synthetic post-physics state."""
+    n = env.num_envs
+    d = env.robot.data
+    u = lambda *s: torch.rand(*s, generator=g)  # noqa: E731
+    idx = env.curr_target_index.clone()
+    tgt = env.steps_pos[torch.arange(n), idx]  # (n,3)
+    # root: walking along the stones, z mostly healthy
+    root = tgt.clone()
+    root[:, 0] += (u(n) - 0.7) * 0.8
+    root[:, 1] += (u(n) - 0.5) * 0.3
+    root[:, 2] = 1.25 + (u(n) - 0.5) * 0.3
+    low = (u(n) < 0.06) & (not calm)
+    root[low, 2] = 0.3 + u(int(low.sum())) * 0.2            # died: z < 0.4
+    quat = _random_quat(g, n, 0.6)
+    quat[u(n) < 0.2] = torch.tensor([1.0, 0.0, 0.0, 0.0])
+    linv = (u(n, 3) - 0.5) * 3.0
+    fast = (u(n) < 0.04) & (not calm)
+    linv[fast] *= 8.0                                        # so_fast: |v| > 5
+    angv = (u(n, 3) - 0.5) * 4.0
+    d.root_state_w[:, :3] = root
+    d.root_state_w[:, 3:7] = quat
+    d.root_state_w[:, 7:10] = linv
+    d.root_state_w[:, 10:13] = angv
+    lim = d.joint_pos_limits
+    qn = (u(n, 21) * 2 - 1) * 1.05                          # some beyond +-0.99 normalized
+    d.joint_pos[:] = qn * (lim[..., 1] - lim[..., 0]) * 0.5 + (lim[..., 1] + lim[..., 0]) * 0.5
+    d.joint_vel[:] = (u(n, 21) - 0.5) * 120.0                 # some clamp at +-5 after *0.1
+    # feet: the swing foot near the current target with prob 0.6
+    bi = BODY_NAMES.index
+    swing = env.swing_leg.clone()
+    feet = torch.zeros(n, 2, 3)
+    for f in range(2):
+        near = (u(n) < 0.6) & (swing == f)
+        off = (u(n, 3) - 0.5) * torch.tensor([0.6, 0.6, 0.1])
+        feet[:, f] = root + torch.tensor([0.0, -0.11 if f == 0 else 0.11, -1.2]) + off
+        feet[near, f] = tgt[near] + (u(int(near.sum()), 3) - 0.5) * torch.tensor([0.4, 0.4, 0.05])
+    h_fall = (u(n) < 0.08) & (not calm)
+    feet[h_fall, :, 2] = root[h_fall, 2:3] - 0.3             # fell: h < threshold
+    d.body_pos_w[:, bi("torso")] = root
+    d.body_pos_w[:, bi("right_foot")] = feet[:, 0]
+    d.body_pos_w[:, bi("left_foot")] = feet[:, 1]
+    # contact force matrices (N,1,20,3): current-target entries for each foot, around the 1e-4 edge
+    for f, sens in ((0, env.sensor_right), (1, env.sensor_left)):
+        fm = torch.zeros(n, 1, 20, 3)
+        on = u(n) < 0.55
+        mag = torch.where(u(n) < 0.15, torch.tensor(5e-5) + u(n) * 1e-4, u(n) * 400.0)
+        dirn = torch.nn.functional.normalize(torch.randn(n, 3, generator=g) * 0.1 + torch.tensor([0, 0, 1.0]), dim=-1)
+        fm[on, 0, idx[on]] = dirn[on] * mag[on, None]
+        # noise on other stones (ignored by the task logic)
+        other = (idx + 1) % 20
+        fm[:, 0, other] = torch.where((u(n) < 0.3)[:, None], dirn * 30.0, torch.zeros(n, 3))
+        # next-stone contact, visible to tick #2 after a progression
+        nxt = torch.clamp(idx + 1, 0, 19)
+        hit = u(n) < 0.3
+        fm[hit, 0, nxt[hit]] = dirn[hit] * 50.0
+        stone1 = u(n) < 0.2                                  # reset envs re-read stone 1 (stale)
+        fm[stone1, 0, 1] = dirn[stone1] * 20.0
+        sens.data.force_matrix_w = fm
+
+
+def gen_task_seq(mod, math_mod, out: dict):
+    n, T = 24, 40
+    g = torch.Generator().manual_seed(42)
+    env = build_env(mod, n, g)
+    # level-0 stones (RNG-independent) via the reference generator itself
+    rec0 = RandRecorder(torch.Generator().manual_seed(0))
+    saved = mod.torch
+    mod.torch = rec0
+    try:
+        pos, _, _ = env._generate_foot_steps_allsteps()
+    finally:
+        mod.torch = saved
+    env.steps_pos[:] = pos
+    # initial task state: varied indices / counts / swing legs / episode lengths
+    env.curr_target_index[:] = torch.randint(1, 20, (n,), generator=g)
+    env.curr_target_index[:4] = 19
+    env.curr_target_index[4:18] = torch.randint(14, 20, (14,), generator=g)  # mean > 12 -> curriculum bump
+    env.prev_target_index[:] = torch.clamp(env.curr_target_index - 1, 0, 19)
+    env.next_target_index[:] = torch.clamp(env.curr_target_index + 1, 0, 19)
+    env.target_reach_count[:] = torch.randint(0, 2, (n,), generator=g)
+    env.swing_leg[:] = torch.randint(0, 2, (n,), generator=g)
+    env.episode_length_buf[:] = torch.randint(0, 40, (n,), generator=g)
+    env.episode_length_buf[:3] = torch.tensor([895, 897, 898])   # time-outs inside the sequence
+    env.potentials[:] = -(torch.rand(n, generator=g) * 50)
+    env.old_potentials[:] = env.potentials - 0.5
+    init = {
+        "idx": env.curr_target_index.clone(), "prev": env.prev_target_index.clone(),
+        "next": env.next_target_index.clone(), "count": env.target_reach_count.clone(),
+        "swing": env.swing_leg.clone(), "ep_len": env.episode_length_buf.clone(),
+        "pot": env.potentials.clone(), "old_pot": env.old_potentials.clone(),
+        "curriculum": env.curriculum.clone(),
+    }
+    rec = RandRecorder(g)
+    saved_env_torch, saved_math_torch = mod.torch, math_mod.torch
+    mod.torch = rec
+    math_mod.torch = rec
+    bi = BODY_NAMES.index
+    S = {k: [] for k in [
+        "actions", "root_state", "joint_pos", "joint_vel", "torso", "rfoot", "lfoot", "fm_r", "fm_l",
+        "terminated", "truncated", "reward", "obs", "any_reset", "reset_draws",
+        "post_root_state", "post_joint_pos", "post_joint_vel", "post_torso", "post_rfoot", "post_lfoot",
+        "idx", "prev", "next", "count", "swing", "pot", "old_pot", "ep_len", "curriculum",
+        "foot_contact"]}
+    try:
+        for t in range(T):
+            synth_physics(env, g, t, calm=(8 <= t < 14) or (26 <= t < 31))
+            d = env.robot.data
+            act = (torch.rand(n, 21, generator=g) * 2 - 1) * 1.3   # some outside [-1,1] (clamped)
+            S["actions"].append(act.clone())
+            S["root_state"].append(d.root_state_w.clone())
+            S["joint_pos"].append(d.joint_pos.clone())
+            S["joint_vel"].append(d.joint_vel.clone())
+            S["torso"].append(d.body_pos_w[:, bi("torso")].clone())
+            S["rfoot"].append(d.body_pos_w[:, bi("right_foot")].clone())
+            S["lfoot"].append(d.body_pos_w[:, bi("left_foot")].clone())
+            S["fm_r"].append(env.sensor_right.data.force_matrix_w[:, 0].clone())
+            S["fm_l"].append(env.sensor_left.data.force_matrix_w[:, 0].clone())
+            # --- DirectRLEnv.step post-physics (direct_rl_env.py:322-381) ---
+            env._pre_physics_step(act)
+            env.episode_length_buf += 1
+            env.reset_terminated[:], env.reset_time_outs[:] = env._get_dones()
+            reset_buf = env.reset_terminated | env.reset_time_outs
+            rew = env._get_rewards()
+            ids = reset_buf.nonzero(as_tuple=False).squeeze(-1)
+            draws = torch.zeros(n, 22)
+            nd = len(rec.draws)
+            if len(ids) > 0:
+                env._reset_idx(ids)
+                new = rec.draws[nd:]
+                assert len(new) == 2, len(new)
+                draws[ids, 0] = new[0]
+                draws[ids, 1:] = new[1]
+            obs = env._get_observations()["policy"]
+            S["terminated"].append(env.reset_terminated.clone())
+            S["truncated"].append(env.reset_time_outs.clone())
+            S["reward"].append(rew.clone())
+            S["obs"].append(obs.clone())
+            S["any_reset"].append(torch.tensor(len(ids) > 0))
+            S["reset_draws"].append(draws)
+            S["post_root_state"].append(d.root_state_w.clone())
+            S["post_joint_pos"].append(d.joint_pos.clone())
+            S["post_joint_vel"].append(d.joint_vel.clone())
+            S["post_torso"].append(d.body_pos_w[:, bi("torso")].clone())
+            S["post_rfoot"].append(d.body_pos_w[:, bi("right_foot")].clone())
+            S["post_lfoot"].append(d.body_pos_w[:, bi("left_foot")].clone())
+            S["idx"].append(env.curr_target_index.clone())
+            S["prev"].append(env.prev_target_index.clone())
+            S["next"].append(env.next_target_index.clone())
+            S["count"].append(env.target_reach_count.clone())
+            S["swing"].append(env.swing_leg.clone())
+            S["pot"].append(env.potentials.clone())
+            S["old_pot"].append(env.old_potentials.clone())
+            S["ep_len"].append(env.episode_length_buf.clone())
+            S["curriculum"].append(env.curriculum.clone())
+            S["foot_contact"].append(env.foot_contact.clone())
+    finally:
+        mod.torch, math_mod.torch = saved_env_torch, saved_math_torch
+    for k, v in S.items():
+        out["seq_" + k] = torch.stack(v).numpy()
+    for k, v in init.items():
+        out["init_" + k] = v.numpy()
+    out["steps_pos"] = env.steps_pos.numpy()
+    out["joint_limits"] = joint_limits()
+    n_resets = int(torch.stack(S["any_reset"]).sum())
+    print(f"task_seq: {T} steps, {n_resets} steps with resets, "
+          f"terminated={int(torch.stack(S['terminated']).sum())}, truncated={int(torch.stack(S['truncated']).sum())}, "
+          f"final curriculum={int(env.curriculum[0])}, idx advances="
+          f"{int((torch.stack(S['idx'])[1:] != torch.stack(S['idx'])[:-1]).sum())}")
+
+
+def gen_mirror(mod, out: dict):
+    g = torch.Generator().manual_seed(11)
+    env = types.SimpleNamespace()
+    J = CFG_DOF_ORDER.index
+    cfg = make_cfg()
+    uw = types.SimpleNamespace(
+        right_body_indices=torch.tensor([J(x) for x in cfg.right_body_names]),
+        left_body_indices=torch.tensor([J(x) for x in cfg.left_body_names]),
+        negation_body_indices=torch.tensor([J(x) for x in cfg.negation_body_names]),
+        observation_space=types.SimpleNamespace(shape=(64, 59)),
+        action_space=types.SimpleNamespace(shape=(64, 21)),
+    )
+    env.unwrapped = uw
+    env.device = "cpu"
+    obs = torch.randn(64, 59, generator=g)
+    act = torch.randn(64, 21, generator=g)
+    mus = torch.randn(64, 21, generator=g)
+    o, a, m = mod.get_symmetric_states_rl_games(obs, act, env, False, mus)
+    o2, a2 = mod.get_symmetric_states_rsl_rl(obs, act, env)
+    out.update(mir_obs=obs.numpy(), mir_act=act.numpy(), mir_mus=mus.numpy(), mir_out_obs=o.numpy(),
+               mir_out_act=a.numpy(), mir_out_mus=m.numpy(), mir_rsl_obs=o2.numpy(), mir_rsl_act=a2.numpy())
+
+
+def gen_rlg_wrapper(out: dict):
+    class FakeDirect:
+        pass
+
+    rlg, Box = refload.load_rl_games_wrapper(FakeDirect)
+    g = torch.Generator().manual_seed(5)
+    n = 16
+
+    class FakeEnv(FakeDirect):
+        def __init__(self):
+            self.num_envs = n
+            self.device = "cpu"
+            self.render_mode = None
+            self.cfg = types.SimpleNamespace(is_finite_horizon=False)
+            self.single_observation_space = {"policy": Box(-math.inf, math.inf, (59,))}
+            self.single_action_space = Box(-math.inf, math.inf, (21,))
+            self.seen_actions = None
+
+        @property
+        def unwrapped(self):
+            return self
+
+        def reset(self):
+            return {"policy": torch.randn(n, 59, generator=g) * 20}, {}
+
+        def step(self, a):
+            self.seen_actions = a.clone()
+            obs = torch.randn(n, 59, generator=g) * 20
+            rew = torch.randn(n, generator=g)
+            term = torch.rand(n, generator=g) < 0.3
+            trunc = torch.rand(n, generator=g) < 0.3
+            self.last = (obs, rew, term, trunc)
+            return {"policy": obs}, rew, term, trunc, {}
+
+    rlg.gymnasium.spaces.Box = Box
+    fe = FakeEnv()
+    w = rlg.RlGamesVecEnvWrapper(fe, "cpu", math.inf, 1.0)
+    acts = torch.randn(n, 21, generator=g) * 2
+    o, r, d, ex = w.step(acts)
+    obs, rew, term, trunc = fe.last
+    out.update(rlg_actions=acts.numpy(), rlg_seen_actions=fe.seen_actions.numpy(), rlg_env_obs=obs.numpy(),
+               rlg_env_rew=rew.numpy(), rlg_env_term=term.numpy(), rlg_env_trunc=trunc.numpy(),
+               rlg_obs=o.numpy(), rlg_rew=r.numpy(), rlg_dones=d.numpy(), rlg_time_outs=ex["time_outs"].numpy())
+    w2 = rlg.RlGamesVecEnvWrapper(fe, "cpu", 10.0, 0.5)
+    o2, _, _, _ = w2.step(acts)
+    out.update(rlg_clip_obs10=o2.numpy(), rlg_clip_env_obs=fe.last[0].numpy(),
+               rlg_seen_actions_05=fe.seen_actions.numpy())
+
+
+def main():
+    torch.set_num_threads(1)
+    mod, math_mod = refload.load_allsteps_env()
+    fs, mt, ts, mi, rg = {}, {}, {}, {}, {}
+    gen_footsteps(mod, fs)
+    gen_math(math_mod, mt)
+    gen_task_seq(mod, math_mod, ts)
+    gen_mirror(mod, mi)
+    gen_rlg_wrapper(rg)
+    for name, d in (("footsteps", fs), ("math", mt), ("task_seq", ts), ("mirror", mi), ("rlg_wrapper", rg)):
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **d)
+        print(f"wrote {path} ({os.path.getsize(path)} B, {len(d)} arrays)")
+
+
+if __name__ == "__main__":
+    main()
