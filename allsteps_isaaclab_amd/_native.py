@@ -1,0 +1,286 @@
+"""ctypes binding of ``liballsteps_hip.so`` (the C ABI of ``include/allsteps.h``).
+
+The product path has no fallback: if the HIP library is missing or no gfx950 device is present the
+calls raise :class:`NativeError` -- nothing silently runs on the CPU.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "liballsteps_hip.so")
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(os.path.dirname(PKG), "include")
+
+MAXL, MAXG = 32, 32
+ABI_VERSION = 1
+
+EXPORTED_SYMBOLS = [
+    "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
+    "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
+    "as_set_seed", "as_profile", "as_profile_read",
+]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class AsModel(C.Structure):
+    _fields_ = [
+        ("num_links", C.c_int32), ("num_hinges", C.c_int32), ("parent", C.c_int32 * MAXL),
+        ("offset_pos", (C.c_float * 3) * MAXL), ("offset_quat", (C.c_float * 4) * MAXL),
+        ("axis", (C.c_float * 3) * MAXL), ("anchor", (C.c_float * 3) * MAXL), ("mass", C.c_float * MAXL),
+        ("com", (C.c_float * 3) * MAXL), ("inertia", (C.c_float * 6) * MAXL), ("armature", C.c_float * MAXL),
+        ("lower", C.c_float * MAXL), ("upper", C.c_float * MAXL), ("cfg_dof_link", C.c_int32 * MAXL),
+        ("gear", C.c_float * MAXL), ("num_geoms", C.c_int32), ("geom_link", C.c_int32 * MAXG),
+        ("geom_type", C.c_int32 * MAXG), ("geom_foot", C.c_int32 * MAXG), ("geom_radius", C.c_float * MAXG),
+        ("geom_p0", (C.c_float * 3) * MAXG), ("geom_p1", (C.c_float * 3) * MAXG), ("torso_link", C.c_int32),
+        ("foot_link", C.c_int32 * 2),
+    ]
+
+
+class AsSim(C.Structure):
+    _fields_ = [
+        ("dt", C.c_float), ("substeps", C.c_int32), ("gravity", C.c_float), ("friction", C.c_float),
+        ("margin", C.c_float), ("baumgarte", C.c_float), ("slop", C.c_float), ("max_depen_vel", C.c_float),
+        ("pgs_iters", C.c_int32), ("stone_half", C.c_float * 3), ("max_joint_vel", C.c_float),
+    ]
+
+
+class AsTask(C.Structure):
+    _fields_ = [
+        ("num_steps", C.c_int32), ("step_radius", C.c_float), ("stop_frames", C.c_int32), ("eps", C.c_float),
+        ("alive", C.c_float), ("energy", C.c_float), ("action", C.c_float), ("joint_limit", C.c_float),
+        ("death", C.c_float), ("dof_vel_scale", C.c_float), ("fall_abs", C.c_float), ("step_dt", C.c_float),
+        ("max_episode_length", C.c_int32), ("max_curriculum", C.c_int32), ("curriculum_threshold", C.c_int32),
+        ("term_curriculum", C.c_float * 10), ("gain_curriculum", C.c_float * 10), ("init_root", C.c_float * 3),
+        ("init_q", C.c_float * 21), ("right_idx", C.c_int32 * 9), ("left_idx", C.c_int32 * 9),
+        ("neg_idx", C.c_int32 * 2), ("noise_lo", C.c_float), ("noise_hi", C.c_float), ("clip_lo", C.c_float),
+        ("clip_hi", C.c_float),
+    ]
+
+
+VP = C.c_void_p
+
+
+class AsState(C.Structure):
+    _fields_ = [(name, VP) for name in (
+        "root_pos", "root_quat", "root_lin", "root_ang", "q", "qd", "stones", "pot", "old_pot", "foot_contact",
+        "body_pos", "idx", "prev", "next", "count", "swing", "ep_len", "episode", "contact_mask", "curriculum")]
+
+
+# (field, rows, dtype) of the SoA state, in as_state_t order
+STATE_LAYOUT = [
+    ("root_pos", 3, "f"), ("root_quat", 4, "f"), ("root_lin", 3, "f"), ("root_ang", 3, "f"), ("q", 21, "f"),
+    ("qd", 21, "f"), ("stones", 60, "f"), ("pot", 1, "f"), ("old_pot", 1, "f"), ("foot_contact", 2, "f"),
+    ("body_pos", 9, "f"), ("idx", 1, "i"), ("prev", 1, "i"), ("next", 1, "i"), ("count", 1, "i"),
+    ("swing", 1, "i"), ("ep_len", 1, "i"), ("episode", 1, "i"), ("contact_mask", 2, "i"),
+]
+
+_LIB = None
+
+
+def lib_path() -> str:
+    return os.environ.get("ALLSTEPS_HIP_LIB", LIB_PATH)
+
+
+def load() -> C.CDLL:
+    """Load liballsteps_hip.so (raises NativeError if it is missing: build it with build_native())."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        raise NativeError(f"{path} not found: the HIP extension is not built "
+                          f"(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    L = C.CDLL(path)
+    V, I32, I64, U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
+    L.as_create.argtypes = [I32, V, V, V, V, U64, I32, I64, C.POINTER(V)]
+    L.as_destroy.argtypes = [V]
+    L.as_reset_all.argtypes = [V, V, V, V]
+    L.as_step.argtypes = [V, V, V, V, V, V, V, V]
+    L.as_physics_step.argtypes = [V, V, V]
+    L.as_task_step.argtypes = [V, V, V, V, V, V, V, V]
+    L.as_set_seed.argtypes = [V, U64]
+    L.as_profile.argtypes = [V, I32]
+    L.as_profile_read.argtypes = [V, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(I32)]
+    L.as_generate_stones.argtypes = [V, I32, V, V]
+    L.as_step_counters.argtypes = [V, C.POINTER(V)]
+    L.as_get_curriculum_host.argtypes = [V, C.POINTER(I32)]
+    L.as_last_error.restype = C.c_char_p
+    for name in EXPORTED_SYMBOLS:
+        if name != "as_last_error":
+            getattr(L, name).restype = C.c_int
+    if L.as_abi_version() != ABI_VERSION:
+        raise NativeError(f"ABI version mismatch: library {L.as_abi_version()} != {ABI_VERSION}")
+    _LIB = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().as_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed ({rc}): {msg}")
+
+
+def build_native(verbose: bool = False) -> str:
+    """Compile liballsteps_hip.so for gfx950 in-tree (hipcc)."""
+    import subprocess
+
+    srcs = [os.path.join(CSRC, f) for f in ("allsteps_kernels.hip", "allsteps_abi.hip")]
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+           "-I", INCLUDE, "-o", LIB_PATH] + srcs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+# ------------------------------------------------------------------------------------------ structs
+
+def make_model(m: dict) -> AsModel:
+    M = AsModel()
+    M.num_links = m["num_links"]
+    M.num_hinges = m["num_hinges"]
+    for name in ("parent", "cfg_dof_link", "geom_link", "geom_type", "geom_foot"):
+        getattr(M, name)[:] = [int(x) for x in m[name]]
+    for name in ("mass", "armature", "lower", "upper", "gear", "geom_radius"):
+        getattr(M, name)[:] = [float(x) for x in m[name]]
+    for name in ("offset_pos", "offset_quat", "axis", "anchor", "com", "inertia", "geom_p0", "geom_p1"):
+        arr = getattr(M, name)
+        for i, row in enumerate(m[name]):
+            arr[i][:] = [float(x) for x in row]
+    M.num_geoms = m["num_geoms"]
+    M.torso_link = int(m["torso_link"])
+    M.foot_link[:] = [int(x) for x in m["foot_link"]]
+    return M
+
+
+def linspace_f32(start: float, end: float, steps: int) -> np.ndarray:
+    """float32 torch.linspace (ATen RangeFactories: start+i*step for the first half, end-(n-1-i)*step after)."""
+    s, e = np.float32(start), np.float32(end)
+    step = (e - s) / np.float32(steps - 1)
+    return np.array([s + step * np.float32(i) if i < steps // 2 else e - step * np.float32(steps - i - 1)
+                     for i in range(steps)], np.float32)
+
+
+def make_task(cfg, dof_names: list) -> AsTask:
+    from .envs.allsteps_env_cfg import running_start_pose
+
+    T = AsTask()
+    T.num_steps = cfg.num_steps
+    T.step_radius = cfg.step_radius
+    T.stop_frames = cfg.stop_frames
+    T.eps = cfg.epsilon
+    T.alive, T.energy, T.action = cfg.alive_reward_scale, cfg.energy_cost_scale, cfg.actions_cost_scale
+    T.joint_limit, T.death = cfg.joint_at_limit_cost_scale, cfg.death_cost
+    T.dof_vel_scale, T.fall_abs = cfg.dof_vel_scale, cfg.termination_height_absolute
+    T.step_dt = float(np.float32(cfg.sim.dt * cfg.decimation))
+    T.max_episode_length = cfg.max_episode_length
+    T.max_curriculum = cfg.max_curriculum
+    T.curriculum_threshold = cfg.curriculum_progress_threshold
+    T.term_curriculum[:] = [float(x) for x in linspace_f32(0.75, 0.45, cfg.max_curriculum + 1)]
+    T.gain_curriculum[:] = [float(x) for x in linspace_f32(1.2, 1.2, cfg.max_curriculum + 1)]
+    T.init_root[:] = list(cfg.init_root_pos)
+    T.init_q[:] = [float(np.float32(x)) for x in running_start_pose()]
+    J = dof_names.index
+    T.right_idx[:] = [J(x) for x in cfg.right_body_names]
+    T.left_idx[:] = [J(x) for x in cfg.left_body_names]
+    T.neg_idx[:] = [J(x) for x in cfg.negation_body_names]
+    T.noise_lo, T.noise_hi = cfg.initial_joint_angle_range
+    T.clip_lo, T.clip_hi = cfg.initial_joint_angle_clip_range
+    return T
+
+
+def make_sim(cfg) -> AsSim:
+    S = AsSim()
+    s = cfg.sim
+    S.dt = s.dt
+    S.substeps = cfg.decimation
+    S.gravity = s.gravity[2]
+    S.friction = s.friction
+    S.margin = s.contact_margin
+    S.baumgarte = s.baumgarte
+    S.slop = s.slop
+    S.max_depen_vel = s.max_depenetration_velocity
+    S.pgs_iters = s.solver_position_iteration_count
+    sz = cfg.step_size
+    S.stone_half[:] = [sz[0] / 2, sz[1] / 2, sz[2] / 2]
+    S.max_joint_vel = s.max_joint_velocity
+    return S
+
+
+class NativeEnv:
+    """Owns an ``as_env_t`` handle over caller-owned (torch) SoA state tensors."""
+
+    def __init__(self, n: int, model: dict, cfg, state: dict, seed: int, device_index: int, env_offset: int = 0):
+        self.L = load()
+        self.n = n
+        self._model = make_model(model)
+        self._sim = make_sim(cfg)
+        self._task = make_task(cfg, model["dof_names"])
+        self._state_tensors = state  # keep alive
+        S = AsState()
+        for name, _, _ in STATE_LAYOUT:
+            setattr(S, name, state[name].data_ptr())
+        S.curriculum = state["curriculum"].data_ptr()
+        self._state = S
+        h = C.c_void_p()
+        check(self.L.as_create(n, C.byref(self._model), C.byref(self._sim), C.byref(self._task), C.byref(S),
+                               seed & 0xFFFFFFFFFFFFFFFF, device_index, env_offset, C.byref(h)), "as_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.as_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def step(self, actions, obs, rew, term, trunc, reset_draws=None, stream=None):
+        check(self.L.as_step(self.h, actions.data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),
+                             trunc.data_ptr(), reset_draws.data_ptr() if reset_draws is not None else None,
+                             stream), "as_step")
+
+    def task_step(self, actions, obs, rew, term, trunc, reset_draws=None, stream=None):
+        check(self.L.as_task_step(self.h, actions.data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),
+                                  trunc.data_ptr(), reset_draws.data_ptr() if reset_draws is not None else None,
+                                  stream), "as_task_step")
+
+    def set_seed(self, seed: int):
+        check(self.L.as_set_seed(self.h, seed & 0xFFFFFFFFFFFFFFFF), "as_set_seed")
+
+    def reset_all(self, obs, reset_draws=None, stream=None):
+        check(self.L.as_reset_all(self.h, obs.data_ptr(),
+                                  reset_draws.data_ptr() if reset_draws is not None else None, stream),
+              "as_reset_all")
+
+    def physics_step(self, actions, stream=None):
+        check(self.L.as_physics_step(self.h, actions.data_ptr(), stream), "as_physics_step")
+
+    def generate_stones(self, level: int, draws=None, stream=None):
+        check(self.L.as_generate_stones(self.h, level, draws.data_ptr() if draws is not None else None, stream),
+              "as_generate_stones")
+
+    def profile(self, max_launches: int):
+        check(self.L.as_profile(self.h, max_launches), "as_profile")
+
+    def profile_read(self):
+        a, b, k = C.c_double(), C.c_double(), C.c_int32()
+        check(self.L.as_profile_read(self.h, C.byref(a), C.byref(b), C.byref(k)), "as_profile_read")
+        return a.value, b.value, k.value
+
+    def counters_ptr(self) -> int:
+        p = C.c_void_p()
+        check(self.L.as_step_counters(self.h, C.byref(p)), "as_step_counters")
+        return p.value

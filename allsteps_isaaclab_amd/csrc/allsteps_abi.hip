@@ -1,0 +1,256 @@
+// allsteps_abi.hip -- extern "C" implementation of include/allsteps.h.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/allsteps.h"
+#include "allsteps_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return fail(AS_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+}  // namespace
+
+struct as_env {
+  int32_t n;
+  int32_t device;
+  uint64_t seed;
+  int64_t env_offset;
+  as_state_t st;
+  as::Consts* consts_dev;
+  int32_t* counters_dev;
+  int32_t num_steps;
+  // optional per-launch timing (as_profile): event triples around k_step / k_obs
+  std::vector<hipEvent_t> ev;
+  int32_t prof_cap = 0, prof_n = 0;
+};
+
+extern "C" {
+
+int as_abi_version(void) { return AS_ABI_VERSION; }
+
+const char* as_last_error(void) { return g_err.c_str(); }
+
+int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, const as_task_t* task,
+              const as_state_t* state, uint64_t seed, int32_t device, int64_t env_id_offset, as_env_t** out) {
+  if (!out || !model || !sim || !task || !state) return fail(AS_ERR_INVALID, "as_create: null argument");
+  *out = nullptr;
+  if (num_envs <= 0) return fail(AS_ERR_INVALID, "as_create: num_envs must be > 0");
+  if (model->num_links < 1 || model->num_links > as::kMaxLinks)
+    return fail(AS_ERR_INVALID, "as_create: num_links out of range (1.." + std::to_string(as::kMaxLinks) + ")");
+  if (model->num_hinges != model->num_links - 1 || model->num_hinges > AS_ACT_DIM)
+    return fail(AS_ERR_INVALID, "as_create: num_hinges must be num_links-1 <= 21");
+  if (model->num_geoms < 0 || model->num_geoms > AS_MAX_GEOMS) return fail(AS_ERR_INVALID, "as_create: num_geoms");
+  if (task->num_steps < 1 || task->num_steps > AS_NUM_STONES) return fail(AS_ERR_INVALID, "as_create: num_steps");
+  if (sim->substeps < 1 || sim->pgs_iters < 0) return fail(AS_ERR_INVALID, "as_create: substeps/pgs_iters");
+  const void* ptrs[] = {state->root_pos, state->root_quat, state->root_lin, state->root_ang, state->q,
+                        state->qd, state->stones, state->pot, state->old_pot, state->foot_contact,
+                        state->body_pos, state->idx, state->prev, state->next, state->count, state->swing,
+                        state->ep_len, state->episode, state->contact_mask, state->curriculum};
+  for (const void* p : ptrs)
+    if (!p) return fail(AS_ERR_INVALID, "as_create: null state field");
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(AS_ERR_NO_DEVICE, "as_create: no HIP device");
+  if (device < 0 || device >= ndev) return fail(AS_ERR_INVALID, "as_create: bad device index");
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(AS_ERR_NO_DEVICE, std::string("as_create: device is ") + prop.gcnArchName + ", built for gfx950");
+
+  // tree plan
+  as::Consts h{};
+  h.model = *model;
+  h.sim = *sim;
+  h.task = *task;
+  h.nv = 6 + model->num_hinges;
+  h.max_depth = 0;
+  for (int i = 0; i < model->num_links; ++i) {
+    int pa = model->parent[i];
+    if (i == 0 ? pa != -1 : (pa < 0 || pa >= i)) return fail(AS_ERR_INVALID, "as_create: parent not topological");
+    h.depth[i] = i == 0 ? 0 : h.depth[pa] + 1;
+    if (h.depth[i] > h.max_depth) h.max_depth = h.depth[i];
+  }
+  for (int i = model->num_links - 1; i >= 1; --i) {
+    int pa = model->parent[i];
+    if (h.nchild[pa] >= as::kMaxChildren) return fail(AS_ERR_INVALID, "as_create: too many children per link");
+    h.child[pa][h.nchild[pa]++] = i;  // descending index order
+  }
+  for (int k = 0; k < model->num_hinges; ++k) {
+    int li = model->cfg_dof_link[k];
+    if (li < 1 || li >= model->num_links) return fail(AS_ERR_INVALID, "as_create: cfg_dof_link");
+  }
+
+  as_env* env = new as_env();
+  env->n = num_envs;
+  env->device = device;
+  env->seed = seed;
+  env->env_offset = env_id_offset;
+  env->st = *state;
+  env->num_steps = task->num_steps;
+  if (hipMalloc(&env->consts_dev, sizeof(as::Consts)) != hipSuccess ||
+      hipMalloc(&env->counters_dev, 4 * sizeof(int32_t)) != hipSuccess) {
+    delete env;
+    return fail(AS_ERR_HIP, "as_create: hipMalloc failed");
+  }
+  HIP_TRY(hipMemcpy(env->consts_dev, &h, sizeof(as::Consts), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(env->counters_dev, 0, 4 * sizeof(int32_t)));
+  *out = env;
+  return AS_OK;
+}
+
+int as_destroy(as_env_t* env) {
+  if (!env) return AS_OK;
+  (void)hipSetDevice(env->device);
+  for (hipEvent_t e : env->ev) (void)hipEventDestroy(e);
+  (void)hipFree(env->consts_dev);
+  (void)hipFree(env->counters_dev);
+  delete env;
+  return AS_OK;
+}
+
+static int run(as_env_t* env, int mode, const float* actions, float* obs, float* reward, uint8_t* term,
+               uint8_t* trunc, const float* reset_draws, void* stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipMemsetAsync(env->counters_dev, 0, 4 * sizeof(int32_t), s));
+  as::StepArgs a{};
+  a.consts = env->consts_dev;
+  a.st = env->st;
+  a.n = env->n;
+  a.mode = mode;
+  a.actions = actions;
+  a.reward = reward;
+  a.terminated = term;
+  a.truncated = trunc;
+  a.reset_draws = reset_draws;
+  a.counters = env->counters_dev;
+  a.seed = env->seed;
+  a.env_offset = env->env_offset;
+  const bool prof = env->prof_n < env->prof_cap;
+  if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n], s));
+  HIP_TRY(as::launch_step(a, s));
+  if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 1], s));
+  if (mode == as::kModePhysics) {
+    if (prof) {
+      HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 2], s));
+      ++env->prof_n;
+    }
+    return AS_OK;
+  }
+  as::ObsArgs o{};
+  o.consts = env->consts_dev;
+  o.st = env->st;
+  o.n = env->n;
+  o.counters = env->counters_dev;
+  o.obs = obs;
+  HIP_TRY(as::launch_obs(o, s));
+  if (prof) {
+    HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 2], s));
+    ++env->prof_n;
+  }
+  return AS_OK;
+}
+
+int as_profile(as_env_t* env, int32_t max_launches) {
+  if (!env || max_launches < 0) return fail(AS_ERR_INVALID, "as_profile: bad argument");
+  HIP_TRY(hipSetDevice(env->device));
+  for (hipEvent_t e : env->ev) HIP_TRY(hipEventDestroy(e));
+  env->ev.assign(3 * (size_t)max_launches, nullptr);
+  for (auto& e : env->ev) HIP_TRY(hipEventCreate(&e));
+  env->prof_cap = max_launches;
+  env->prof_n = 0;
+  return AS_OK;
+}
+
+int as_profile_read(as_env_t* env, double* step_kernel_ms, double* obs_kernel_ms, int32_t* launches) {
+  if (!env || !step_kernel_ms || !obs_kernel_ms || !launches) return fail(AS_ERR_INVALID, "as_profile_read: null");
+  double a = 0.0, b = 0.0;
+  if (env->prof_n > 0) HIP_TRY(hipEventSynchronize(env->ev[3 * env->prof_n - 1]));
+  for (int i = 0; i < env->prof_n; ++i) {
+    float t1 = 0.f, t2 = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t1, env->ev[3 * i], env->ev[3 * i + 1]));
+    HIP_TRY(hipEventElapsedTime(&t2, env->ev[3 * i + 1], env->ev[3 * i + 2]));
+    a += t1;
+    b += t2;
+  }
+  *step_kernel_ms = a;
+  *obs_kernel_ms = b;
+  *launches = env->prof_n;
+  env->prof_n = 0;
+  return AS_OK;
+}
+
+int as_step(as_env_t* env, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
+            const float* reset_draws, void* stream) {
+  if (!env || !actions || !obs || !reward || !terminated || !truncated)
+    return fail(AS_ERR_INVALID, "as_step: null argument");
+  return run(env, as::kModeStep, actions, obs, reward, terminated, truncated, reset_draws, stream);
+}
+
+int as_task_step(as_env_t* env, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                 uint8_t* truncated, const float* reset_draws, void* stream) {
+  if (!env || !actions || !obs || !reward || !terminated || !truncated)
+    return fail(AS_ERR_INVALID, "as_task_step: null argument");
+  return run(env, as::kModeTask, actions, obs, reward, terminated, truncated, reset_draws, stream);
+}
+
+int as_set_seed(as_env_t* env, uint64_t seed) {
+  if (!env) return fail(AS_ERR_INVALID, "as_set_seed: null handle");
+  env->seed = seed;
+  return AS_OK;
+}
+
+int as_reset_all(as_env_t* env, float* obs, const float* reset_draws, void* stream) {
+  if (!env || !obs) return fail(AS_ERR_INVALID, "as_reset_all: null argument");
+  return run(env, as::kModeReset, nullptr, obs, nullptr, nullptr, nullptr, reset_draws, stream);
+}
+
+int as_physics_step(as_env_t* env, const float* actions, void* stream) {
+  if (!env || !actions) return fail(AS_ERR_INVALID, "as_physics_step: null argument");
+  return run(env, as::kModePhysics, actions, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* stream) {
+  if (!env) return fail(AS_ERR_INVALID, "as_generate_stones: null handle");
+  if (level < 0) return fail(AS_ERR_INVALID, "as_generate_stones: level < 0");
+  as::StonesArgs a{};
+  a.consts = env->consts_dev;
+  a.stones = env->st.stones;
+  a.n = env->n;
+  a.level = level;
+  a.draws = draws;
+  a.seed = env->seed;
+  a.env_offset = env->env_offset;
+  HIP_TRY(as::launch_stones(a, reinterpret_cast<hipStream_t>(stream)));
+  return AS_OK;
+}
+
+int as_step_counters(as_env_t* env, const int32_t** counters_dev) {
+  if (!env || !counters_dev) return fail(AS_ERR_INVALID, "as_step_counters: null argument");
+  *counters_dev = env->counters_dev;
+  return AS_OK;
+}
+
+int as_get_curriculum_host(as_env_t* env, int32_t* level_host) {
+  if (!env || !level_host) return fail(AS_ERR_INVALID, "as_get_curriculum_host: null argument");
+  HIP_TRY(hipMemcpy(level_host, env->st.curriculum, sizeof(int32_t), hipMemcpyDeviceToHost));
+  return AS_OK;
+}
+
+}  // extern "C"

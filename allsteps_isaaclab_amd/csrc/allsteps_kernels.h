@@ -1,0 +1,67 @@
+// allsteps_kernels.h -- host/device interface of the step kernels (internal to liballsteps_hip.so).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/allsteps.h"
+
+namespace as {
+
+constexpr int kMaxLinks = 24;  // LDS sizing of the step kernel (walker: 22 links)
+constexpr int kMaxChildren = 4;
+
+enum { kModeStep = 0, kModeReset = 1, kModePhysics = 2, kModeTask = 3 };
+
+// Everything the kernels read that does not change per step: model tables + the tree plan
+// derived from them on the host (depth levels and child lists for the level-synchronous passes).
+struct Consts {
+  as_model_t model;
+  as_sim_t sim;
+  as_task_t task;
+  int32_t nv;
+  int32_t max_depth;
+  int32_t depth[kMaxLinks];
+  int32_t nchild[kMaxLinks];
+  int32_t child[kMaxLinks][kMaxChildren];  // descending link index
+};
+
+struct StepArgs {
+  const Consts* consts;
+  as_state_t st;
+  int32_t n;
+  int32_t mode;
+  const float* actions;
+  float* reward;
+  uint8_t* terminated;
+  uint8_t* truncated;
+  const float* reset_draws;
+  int32_t* counters;  // [0] any reset, [1] sum of curr_target_index (zeroed before the launch)
+  uint64_t seed;
+  int64_t env_offset;
+};
+
+struct ObsArgs {
+  const Consts* consts;
+  as_state_t st;
+  int32_t n;
+  const int32_t* counters;
+  float* obs;
+};
+
+struct StonesArgs {
+  const Consts* consts;
+  float* stones;
+  int32_t n;
+  int32_t level;
+  const float* draws;
+  uint64_t seed;
+  int64_t env_offset;
+};
+
+hipError_t launch_step(const StepArgs& a, hipStream_t stream);
+hipError_t launch_obs(const ObsArgs& a, hipStream_t stream);
+hipError_t launch_stones(const StonesArgs& a, hipStream_t stream);
+size_t step_lds_bytes();
+
+}  // namespace as

@@ -1,0 +1,1009 @@
+// allsteps_kernels.hip -- MI355X (gfx950) step kernels for Allsteps-v0.
+//
+// k_step (K1): one env per 32-lane group (two envs per 64-lane wave, one wave per workgroup).
+//   For each env: load the SoA state once, run `decimation` physics substeps
+//   (FK -> RNEA bias -> CRBA inertia -> Cholesky -> unconstrained velocity -> stone contacts +
+//   joint limits -> projected Gauss-Seidel -> semi-implicit integration), then the task epilogue of
+//   DirectRLEnv.step (direct_rl_env.py:349-364): episode counter, foot-state tick #1, targets,
+//   potentials, dones, rewards, and -- for envs that are done -- the in-kernel reset
+//   (allsteps_env.py:469-565) with Philox draws and an FK of the new pose.  All per-env scratch
+//   lives in LDS; the state is read and written exactly once per env step.
+// k_obs (K2): one env per lane.  If any env reset this step (device counter written by K1), the
+//   second _compute_useful_values over ALL envs (allsteps_env.py:567: foot-state tick #2 with the
+//   stale last-substep contacts, targets, potentials) and the curriculum gate
+//   (allsteps_env.py:471-479); then the observation (allsteps_env.py:326-345).
+// k_stones: _generate_foot_steps_allsteps (allsteps_env.py:125-174), one env per lane.
+//
+// The algorithm is specified in DESIGN.md §Dynamics; oracle/physics.c is its serial restatement.
+#include <hip/hip_runtime.h>
+
+#include "../../include/allsteps.h"
+#include "allsteps_device.h"
+#include "allsteps_kernels.h"
+
+namespace as {
+
+constexpr int G = 32;              // lanes per env
+constexpr int EPB = 2;             // envs per 64-lane workgroup
+constexpr int LMAX = kMaxLinks;    // links (walker: 22)
+constexpr int NVMAX = 6 + LMAX - 1;// generalized velocities
+constexpr int LDH = 31;            // odd row stride: conflict-free column access
+constexpr int MAXC = AS_MAX_CONTACTS;
+constexpr int MAXR = AS_MAX_ROWS;
+constexpr int NST = AS_NUM_STONES;
+constexpr int GOLDEN_ITERS = 14;
+
+static_assert(NVMAX <= G, "one lane per generalized velocity");
+static_assert(LMAX <= G, "one lane per link");
+
+// ------------------------------------------------------------------------------------------------
+// per-env LDS scratch
+struct EnvS {
+  float R[LMAX][9];
+  float p[LMAX][3];
+  float c[LMAX][3];
+  float Rl[LMAX][12];   // local joint transform (R 9, p 3)
+  float Ib[LMAX][10];
+  float Ic[LMAX][10];
+  float S[NVMAX][6];
+  float V[LMAX][6];
+  float A[LMAX][6];
+  float F[LMAX][6];
+  float H[NVMAX * LDH];
+  float J[MAXR * LDH];
+  float W[MAXR * LDH];
+  float rtarget[MAXR], rAd[MAXR], rlam[MAXR];
+  int rtype[MAXR];
+  float cpt[MAXC][3], cn[MAXC][3], csep[MAXC];
+  int clink[MAXC], cstone[MAXC], cfoot[MAXC];
+  float u[NVMAX], b[NVMAX], acc[NVMAX];
+  float qi[LMAX];       // hinge angles, link order (link i -> qi[i-1])
+  float tau[LMAX];
+  float act[AS_ACT_DIM];
+  float stones[NST * 3];
+  float root_pos[3], root_quat[4];
+  int cand[NST];
+  int pair_ok[64];
+  int ncand, ncontact, nrow, npair;
+  uint32_t mask[2];
+  // task scratch
+  float red[4];
+};
+
+struct Smem {
+  EnvS env[EPB];
+  int maxrow;
+};
+
+__device__ __forceinline__ float wave32_sum(float v) {
+  // butterfly over the 32 lanes of this env group (xor < 32 stays inside the half-wave)
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// FK: local joint transforms (parallel), then level-synchronous composition.
+__device__ void fk(const Consts& K, EnvS& s, int lane) {
+  const as_model_t& m = K.model;
+  const int nl = m.num_links;
+  for (int i = lane; i < nl; i += G) {
+    if (i == 0) {
+      quat_to_mat(s.root_quat, s.R[0]);
+      s.p[0][0] = s.p[0][1] = s.p[0][2] = 0.f;
+    } else {
+      float Roff[9], Rj[9], Ro[3], t[3], tmp[3];
+      quat_to_mat(m.offset_quat[i], Roff);
+      axis_angle_mat(m.axis[i], s.qi[i - 1], Rj);
+      matmul3(Roff, Rj, s.Rl[i]);
+      matvec3(Rj, m.anchor[i], Ro);
+      for (int k = 0; k < 3; ++k) t[k] = m.anchor[i][k] - Ro[k];
+      matvec3(Roff, t, tmp);
+      for (int k = 0; k < 3; ++k) s.Rl[i][9 + k] = tmp[k] + m.offset_pos[i][k];
+    }
+  }
+  __syncthreads();
+  for (int d = 1; d <= K.max_depth; ++d) {
+    for (int i = lane; i < nl; i += G) {
+      if (K.depth[i] != d) continue;
+      int pa = m.parent[i];
+      matmul3(s.R[pa], s.Rl[i], s.R[i]);
+      float wp[3];
+      matvec3(s.R[pa], s.Rl[i] + 9, wp);
+      for (int k = 0; k < 3; ++k) s.p[i][k] = s.p[pa][k] + wp[k];
+    }
+    __syncthreads();
+  }
+}
+
+// Per-link world quantities: COM, spatial inertia at O, motion subspace.
+__device__ void link_quantities(const Consts& K, EnvS& s, int lane) {
+  const as_model_t& m = K.model;
+  const int nl = m.num_links;
+  for (int i = lane; i < nl; i += G) {
+    const float* R = s.R[i];
+    float cw[3];
+    matvec3(R, m.com[i], cw);
+    float c[3] = {s.p[i][0] + cw[0], s.p[i][1] + cw[1], s.p[i][2] + cw[2]};
+    s.c[i][0] = c[0]; s.c[i][1] = c[1]; s.c[i][2] = c[2];
+    const float* Il = m.inertia[i];
+    float Im[9] = {Il[0], Il[3], Il[4], Il[3], Il[1], Il[5], Il[4], Il[5], Il[2]};
+    float Rt[9] = {R[0], R[3], R[6], R[1], R[4], R[7], R[2], R[5], R[8]};
+    float T[9], Iw[9];
+    matmul3(R, Im, T);
+    matmul3(T, Rt, Iw);
+    float mass = m.mass[i], cc = dot3(c, c);
+    float* B = s.Ib[i];
+    B[0] = mass;
+    B[1] = mass * c[0]; B[2] = mass * c[1]; B[3] = mass * c[2];
+    B[4] = Iw[0] + mass * (cc - c[0] * c[0]);
+    B[5] = Iw[4] + mass * (cc - c[1] * c[1]);
+    B[6] = Iw[8] + mass * (cc - c[2] * c[2]);
+    B[7] = Iw[1] - mass * c[0] * c[1];
+    B[8] = Iw[2] - mass * c[0] * c[2];
+    B[9] = Iw[5] - mass * c[1] * c[2];
+    for (int k = 0; k < 10; ++k) s.Ic[i][k] = B[k];
+    if (i > 0) {
+      float a[3], Ro[3], o[3];
+      matvec3(R, m.axis[i], a);
+      matvec3(R, m.anchor[i], Ro);
+      for (int k = 0; k < 3; ++k) o[k] = s.p[i][k] + Ro[k];
+      float* S = s.S[6 + i - 1];
+      S[0] = a[0]; S[1] = a[1]; S[2] = a[2];
+      cross3(o, a, S + 3);
+    }
+  }
+  __syncthreads();
+  if (lane < 6) {  // root columns need c0
+    float* S = s.S[lane];
+    for (int j = 0; j < 6; ++j) S[j] = 0.f;
+    int k = lane % 3;
+    if (lane < 3) {
+      S[3 + k] = 1.f;
+    } else {
+      float e[3] = {0.f, 0.f, 0.f};
+      e[k] = 1.f;
+      S[k] = 1.f;
+      cross3(s.c[0], e, S + 3);
+    }
+  }
+  __syncthreads();
+}
+
+// Velocities, bias accelerations (qdd = 0), RNEA forces, composite inertias, C, H.
+__device__ void dynamics(const Consts& K, EnvS& s, int lane, float gravity) {
+  const as_model_t& m = K.model;
+  const int nl = m.num_links, nv = K.nv;
+  // level 0: root
+  if (lane == 0) {
+    const float* u = s.u;
+    float wxc[3], vxw[3];
+    cross3(s.c[0], u + 3, wxc);
+    cross3(u, u + 3, vxw);
+    for (int k = 0; k < 3; ++k) {
+      s.V[0][k] = u[3 + k];
+      s.V[0][3 + k] = u[k] + wxc[k];
+      s.A[0][k] = 0.f;
+      s.A[0][3 + k] = vxw[k];
+    }
+  }
+  __syncthreads();
+  for (int d = 1; d <= K.max_depth; ++d) {
+    for (int i = lane; i < nl; i += G) {
+      if (K.depth[i] != d) continue;
+      int pa = m.parent[i];
+      float qd = s.u[6 + i - 1];
+      const float* S = s.S[6 + i - 1];
+      float Sq[6], cr[6];
+      for (int k = 0; k < 6; ++k) {
+        Sq[k] = S[k] * qd;
+        s.V[i][k] = s.V[pa][k] + Sq[k];
+      }
+      crm(s.V[i], Sq, cr);
+      for (int k = 0; k < 6; ++k) s.A[i][k] = s.A[pa][k] + cr[k];
+    }
+    __syncthreads();
+  }
+  for (int i = lane; i < nl; i += G) {
+    float IA[6], IV[6], x[6];
+    inertia_mul(s.Ib[i], s.A[i], IA);
+    inertia_mul(s.Ib[i], s.V[i], IV);
+    crf(s.V[i], IV, x);
+    float mg[3] = {0.f, 0.f, m.mass[i] * gravity};
+    float cxmg[3];
+    cross3(s.c[i], mg, cxmg);
+    for (int k = 0; k < 3; ++k) {
+      s.F[i][k] = IA[k] + x[k] - cxmg[k];
+      s.F[i][3 + k] = IA[3 + k] + x[3 + k] - mg[k];
+    }
+  }
+  __syncthreads();
+  // inward accumulation: parents add their children (descending child index = oracle order)
+  for (int d = K.max_depth - 1; d >= 0; --d) {
+    for (int i = lane; i < nl; i += G) {
+      if (K.depth[i] != d) continue;
+      for (int t = 0; t < K.nchild[i]; ++t) {
+        int ch = K.child[i][t];
+        for (int k = 0; k < 6; ++k) s.F[i][k] += s.F[ch][k];
+        for (int k = 0; k < 10; ++k) s.Ic[i][k] += s.Ic[ch][k];
+      }
+    }
+    __syncthreads();
+  }
+  // bias C, b = tau - C, and the joint-space inertia rows (lane = dof j)
+  if (lane < nv) {
+    const int j = lane;
+    const int link = j < 6 ? 0 : j - 5;
+    float Cj = dot6(s.S[j], s.F[link]);
+    s.b[j] = (j < 6 ? 0.f : s.tau[j - 6]) - Cj;
+    float Fj[6];
+    inertia_mul(s.Ic[link], s.S[j], Fj);
+    float* Hrow = s.H + j * LDH;
+    for (int k = 0; k <= j; ++k) Hrow[k] = 0.f;
+    for (int l = link; l > 0; l = m.parent[l]) {
+      int k = 6 + l - 1;
+      if (k <= j) Hrow[k] = dot6(s.S[k], Fj);
+    }
+    for (int k = 0; k < 6; ++k)
+      if (k <= j) Hrow[k] = dot6(s.S[k], Fj);
+    if (j >= 6) Hrow[j] += m.armature[j - 5];
+  }
+  __syncthreads();
+}
+
+// Left-looking Cholesky H = L L^T in place (lower triangle), lanes over rows.
+__device__ void cholesky(const Consts& K, EnvS& s, int lane) {
+  const int nv = K.nv;
+  float* H = s.H;
+  for (int j = 0; j < nv; ++j) {
+    if (lane == j) {
+      float acc = H[j * LDH + j];
+      for (int k = 0; k < j; ++k) acc -= H[j * LDH + k] * H[j * LDH + k];
+      H[j * LDH + j] = sqrtf(acc > 1e-12f ? acc : 1e-12f);
+    }
+    __syncthreads();
+    if (lane > j && lane < nv) {
+      const int i = lane;
+      float t = H[i * LDH + j];
+      for (int k = 0; k < j; ++k) t -= H[i * LDH + k] * H[j * LDH + k];
+      H[i * LDH + j] = t * (1.0f / H[j * LDH + j]);
+    }
+    __syncthreads();
+  }
+}
+
+// Solve H x = b for one RHS held in LDS (x may alias b), column-oriented, lanes over rows.
+__device__ void chol_solve_lds(const Consts& K, EnvS& s, int lane, float* b, float* x) {
+  const int nv = K.nv;
+  const float* L = s.H;
+  for (int j = 0; j < nv; ++j) {  // forward: y_j = b_j / L_jj ; b_i -= L_ij y_j
+    float yj = b[j] / L[j * LDH + j];
+    __syncthreads();
+    if (lane == j) b[j] = yj;
+    if (lane > j && lane < nv) b[lane] -= L[lane * LDH + j] * yj;
+    __syncthreads();
+  }
+  for (int j = nv - 1; j >= 0; --j) {  // backward: x_j = y_j / L_jj ; y_i -= L_ji x_j
+    float xj = b[j] / L[j * LDH + j];
+    __syncthreads();
+    if (lane == j) x[j] = xj;
+    if (lane < j) b[lane] -= L[j * LDH + lane] * xj;
+    __syncthreads();
+  }
+}
+
+// Per-lane serial solve of H w = J_r (row r), reading L (broadcast) and writing W_r.
+__device__ void chol_solve_row(int nv, const float* L, const float* Jr, float* Wr) {
+  float y[NVMAX];
+#pragma unroll
+  for (int i = 0; i < NVMAX; ++i) {
+    if (i < nv) {
+      float acc = Jr[i];
+      for (int k = 0; k < i; ++k) acc -= L[i * LDH + k] * y[k];
+      y[i] = acc / L[i * LDH + i];
+    }
+  }
+#pragma unroll
+  for (int i = NVMAX - 1; i >= 0; --i) {
+    if (i < nv) {
+      float acc = y[i];
+      for (int k = nv - 1; k > i; --k) acc -= L[k * LDH + i] * Wr[k];
+      Wr[i] = acc / L[i * LDH + i];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// contacts: robot geoms vs axis-aligned stone boxes
+
+__device__ void emit_contact(EnvS& s, int slot, int link, int stone, int foot, const float* P, const float* n,
+                             float sep, float r) {
+  if (slot >= MAXC) return;
+  s.clink[slot] = link; s.cstone[slot] = stone; s.cfoot[slot] = foot; s.csep[slot] = sep;
+  for (int k = 0; k < 3; ++k) { s.cn[slot][k] = n[k]; s.cpt[slot][k] = P[k] - n[k] * r; }
+}
+
+__device__ void collide(const Consts& K, EnvS& s, int lane) {
+  const as_model_t& m = K.model;
+  const float* h = K.sim.stone_half;
+  const int nst = K.task.num_steps;
+  // broadphase: stones within 1.8 m of the root link origin
+  bool isc = false;
+  float rel[3] = {0.f, 0.f, 0.f};
+  if (lane < nst) {
+    float o = 0.f;
+    for (int k = 0; k < 3; ++k) {
+      rel[k] = s.stones[3 * lane + k] - s.root_pos[k];
+      float d = fabsf(rel[k]) - h[k];
+      if (d > 0.f) o += d * d;
+    }
+    isc = o < 1.8f * 1.8f;
+  }
+  // compact candidates in stone order (ballot over this env's half-wave)
+  uint64_t bal = __ballot(isc);
+  const int half = (threadIdx.x >> 5) & 1;
+  uint32_t mine = (uint32_t)(bal >> (32 * half));
+  if (isc) {
+    int pos = __popc(mine & ((1u << lane) - 1u));
+    s.cand[pos] = lane;
+  }
+  if (lane == 0) { s.ncand = __popc(mine); s.ncontact = 0; }
+  __syncthreads();
+  const int ncand = s.ncand, ng = m.num_geoms;
+  const int npairs = ng * ncand;
+  // pass over pairs in (geom, stone) order, 32 at a time; each pair emits 0..3 contacts
+  int base = 0;
+  for (int p0 = 0; p0 < npairs; p0 += G) {
+    int p = p0 + lane;
+    int cnt = 0;
+    int link = 0, stone = 0, foot = -1;
+    float P[3][3], N[3][3], SEP[3], rr = 0.f;
+    if (p < npairs) {
+      int g = p / ncand, st = s.cand[p % ncand];
+      link = m.geom_link[g]; stone = st; foot = m.geom_foot[g];
+      float r = m.geom_radius[g];
+      rr = r;
+      float a[3], bb[3], t0[3], t1[3];
+      matvec3(s.R[link], m.geom_p0[g], t0);
+      matvec3(s.R[link], m.geom_p1[g], t1);
+      for (int k = 0; k < 3; ++k) { a[k] = s.p[link][k] + t0[k]; bb[k] = s.p[link][k] + t1[k]; }
+      float c[3];
+      for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * st + k] - s.root_pos[k];
+      float nr[3];
+      if (m.geom_type[g] == 0) {
+        float sd = sd_box(a, c, h, nr) - r;
+        if (sd < K.sim.margin) {
+          for (int k = 0; k < 3; ++k) { P[0][k] = a[k]; N[0][k] = nr[k]; }
+          SEP[0] = sd;
+          cnt = 1;
+        }
+      } else {
+        float L = sqrtf((bb[0] - a[0]) * (bb[0] - a[0]) + (bb[1] - a[1]) * (bb[1] - a[1]) +
+                        (bb[2] - a[2]) * (bb[2] - a[2]));
+        float mid[3] = {0.5f * (a[0] + bb[0]), 0.5f * (a[1] + bb[1]), 0.5f * (a[2] + bb[2])};
+        if (sd_box(mid, c, h, nr) <= 0.5f * L + r + K.sim.margin) {
+          float n0[3], n1[3], tn[3];
+          float s0 = sd_box(a, c, h, n0) - r;
+          float s1 = sd_box(bb, c, h, n1) - r;
+          const float gr = 0.6180339887f;
+          float lo = 0.f, hi = 1.f;
+          float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
+          float P1[3], P2[3];
+          for (int k = 0; k < 3; ++k) { P1[k] = a[k] + x1 * (bb[k] - a[k]); P2[k] = a[k] + x2 * (bb[k] - a[k]); }
+          float f1 = sd_box(P1, c, h, tn), f2 = sd_box(P2, c, h, tn);
+          for (int it = 0; it < GOLDEN_ITERS; ++it) {
+            if (f1 < f2) {
+              hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
+              for (int k = 0; k < 3; ++k) P1[k] = a[k] + x1 * (bb[k] - a[k]);
+              f1 = sd_box(P1, c, h, tn);
+            } else {
+              lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
+              for (int k = 0; k < 3; ++k) P2[k] = a[k] + x2 * (bb[k] - a[k]);
+              f2 = sd_box(P2, c, h, tn);
+            }
+          }
+          float ts = 0.5f * (lo + hi), Ps[3], ns[3];
+          for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (bb[k] - a[k]);
+          float ss = sd_box(Ps, c, h, ns) - r;
+          if (s0 < K.sim.margin) {
+            for (int k = 0; k < 3; ++k) { P[cnt][k] = a[k]; N[cnt][k] = n0[k]; }
+            SEP[cnt++] = s0;
+          }
+          if (s1 < K.sim.margin) {
+            for (int k = 0; k < 3; ++k) { P[cnt][k] = bb[k]; N[cnt][k] = n1[k]; }
+            SEP[cnt++] = s1;
+          }
+          float smin = fminf(s0, s1);
+          if (ss < K.sim.margin && ss < smin - 0.002f) {
+            for (int k = 0; k < 3; ++k) { P[cnt][k] = Ps[k]; N[cnt][k] = ns[k]; }
+            SEP[cnt++] = ss;
+          }
+        }
+      }
+    }
+    // exclusive prefix sum of cnt over the 32 lanes of this env (in pair order)
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      int v = __shfl_up(incl, o, 32);
+      if (lane >= o) incl += v;
+    }
+    int total = __shfl(incl, 31, 32);
+    int slot = base + incl - cnt;
+    for (int t = 0; t < cnt; ++t) emit_contact(s, slot + t, link, stone, foot, P[t], N[t], SEP[t], rr);
+    base += total;
+  }
+  __syncthreads();
+  if (lane == 0) s.ncontact = base < MAXC ? base : MAXC;
+  __syncthreads();
+}
+
+// Jacobian row of direction d at point P on link `link` (lanes are rows; serial over dofs)
+__device__ void build_contact_row(const Consts& K, const EnvS& s, int link, const float* P, const float* d,
+                                  float* Jr) {
+  const as_model_t& m = K.model;
+  float f6[6];
+  cross3(P, d, f6);
+  f6[3] = d[0]; f6[4] = d[1]; f6[5] = d[2];
+  for (int j = 0; j < K.nv; ++j) Jr[j] = 0.f;
+  for (int l = link; l > 0; l = m.parent[l]) Jr[6 + l - 1] = dot6(s.S[6 + l - 1], f6);
+  for (int k = 0; k < 6; ++k) Jr[k] = dot6(s.S[k], f6);
+}
+
+__device__ void tangents(const float* n, float* t1, float* t2) {
+  float e[3] = {1.f, 0.f, 0.f};
+  if (fabsf(n[0]) > 0.9f) { e[0] = 0.f; e[1] = 1.f; }
+  cross3(n, e, t1);
+  float inv = 1.0f / sqrtf(dot3(t1, t1));
+  for (int k = 0; k < 3; ++k) t1[k] *= inv;
+  cross3(n, t1, t2);
+}
+
+// ------------------------------------------------------------------------------------------------
+__device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* mask_out) {
+  const as_model_t& m = K.model;
+  const float dt = K.sim.dt;
+  const int nv = K.nv, nh = m.num_hinges;
+  fk(K, s, lane);
+  link_quantities(K, s, lane);
+  dynamics(K, s, lane, K.sim.gravity);
+  cholesky(K, s, lane);
+  chol_solve_lds(K, s, lane, s.b, s.acc);
+  if (lane < nv) s.u[lane] += dt * s.acc[lane];
+  __syncthreads();
+  // ---- constraints
+  collide(K, s, lane);
+  const int nc = s.ncontact;
+  // contact rows: lane c builds the three rows of contact c
+  if (lane < nc && 3 * lane + 3 <= MAXR) {
+    float t1[3], t2[3];
+    tangents(s.cn[lane], t1, t2);
+    const float* dirs[3] = {s.cn[lane], t1, t2};
+    for (int d = 0; d < 3; ++d) {
+      int r = 3 * lane + d;
+      s.rtype[r] = d == 0 ? 0 : 1;
+      build_contact_row(K, s, s.clink[lane], s.cpt[lane], dirs[d], s.J + r * LDH);
+      float sp = s.csep[lane];
+      s.rtarget[r] = d == 0 ? (sp < 0.f ? fminf(K.sim.baumgarte * fmaxf(-sp - K.sim.slop, 0.f) / dt, K.sim.max_depen_vel)
+                                        : -sp / dt)
+                            : 0.f;
+    }
+  }
+  int crow = 3 * nc < MAXR ? 3 * nc : MAXR;
+  // joint-limit rows: lane h (hinge) emits lower then upper, in hinge order
+  int lo_v = 0, hi_v = 0;
+  float err_lo = 0.f, err_hi = 0.f;
+  if (lane < nh) {
+    int i = lane + 1;
+    float qv = s.qi[lane], pred = qv + dt * s.u[6 + lane];
+    err_lo = m.lower[i] - qv;
+    err_hi = qv - m.upper[i];
+    lo_v = pred < m.lower[i];
+    hi_v = pred > m.upper[i];
+  }
+  int cnt = lo_v + hi_v;
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    int v = __shfl_up(incl, o, 32);
+    if (lane >= o) incl += v;
+  }
+  int total = __shfl(incl, 31, 32);
+  int slot = crow + incl - cnt;
+  for (int sd = 0; sd < 2; ++sd) {
+    int viol = sd == 0 ? lo_v : hi_v;
+    if (!viol) continue;
+    if (slot < MAXR) {
+      float* Jr = s.J + slot * LDH;
+      for (int k = 0; k < nv; ++k) Jr[k] = 0.f;
+      Jr[6 + lane] = sd == 0 ? 1.f : -1.f;
+      float err = sd == 0 ? err_lo : err_hi;
+      s.rtype[slot] = 2;
+      s.rtarget[slot] = err > 0.f ? fminf(K.sim.baumgarte * err / dt, K.sim.max_depen_vel) : err / dt;
+    }
+    ++slot;
+  }
+  const int nrow = crow + total < MAXR ? crow + total : MAXR;
+  if (lane == 0) s.nrow = nrow;
+  __syncthreads();
+  // W_r = H^-1 J_r^T and the effective masses (lanes over rows)
+  for (int r = lane; r < nrow; r += G) {
+    const float* Jr = s.J + r * LDH;
+    float* Wr = s.W + r * LDH;
+    chol_solve_row(nv, s.H, Jr, Wr);
+    float a = 0.f;
+    for (int k = 0; k < nv; ++k) a += Jr[k] * Wr[k];
+    s.rAd[r] = 1.0f / (a + 1e-9f);
+    s.rlam[r] = 0.f;
+  }
+  if (threadIdx.x == 0) sm.maxrow = max(sm.env[0].nrow, sm.env[1].nrow);
+  __syncthreads();
+  // ---- projected Gauss-Seidel; lane j holds u_j
+  const int maxrow = sm.maxrow;
+  float uj = lane < nv ? s.u[lane] : 0.f;
+  for (int it = 0; it < K.sim.pgs_iters; ++it) {
+    for (int r = 0; r < maxrow; ++r) {
+      bool act = r < nrow;
+      float Jrj = (act && lane < nv) ? s.J[r * LDH + lane] : 0.f;
+      float v = wave32_sum(Jrj * uj);
+      if (act) {
+        float l0 = s.rlam[r], l1;
+        if (s.rtype[r] == 1) {
+          int rn = r - (r % 3 == 1 ? 1 : 2);
+          float lim = K.sim.friction * s.rlam[rn];
+          l1 = fminf(fmaxf(l0 - v * s.rAd[r], -lim), lim);
+        } else {
+          l1 = fmaxf(l0 + (s.rtarget[r] - v) * s.rAd[r], 0.f);
+        }
+        float dl = l1 - l0;
+        if (lane < nv) uj += s.W[r * LDH + lane] * dl;
+        __syncthreads();  // every lane has read rlam before it changes
+        if (lane == 0) s.rlam[r] = l1;
+      } else {
+        __syncthreads();
+      }
+      __syncthreads();
+    }
+  }
+  if (lane < nv) s.u[lane] = uj;
+  __syncthreads();
+  // ---- contact-sensor flags of this substep (force_matrix_w = impulse / dt, > eps)
+  if (lane == 0) {
+    uint32_t mk[2] = {0u, 0u};
+    for (int c = 0; c < nc; ++c) {
+      if (s.cfoot[c] < 0 || 3 * c >= nrow) continue;
+      float fx = 0.f, fy = 0.f, fz = 0.f;
+      for (int c2 = 0; c2 < nc && 3 * c2 < nrow; ++c2) {
+        if (s.cfoot[c2] != s.cfoot[c] || s.cstone[c2] != s.cstone[c]) continue;
+        float l = s.rlam[3 * c2];
+        fx += l * s.cn[c2][0]; fy += l * s.cn[c2][1]; fz += l * s.cn[c2][2];
+      }
+      if (sqrtf(fx * fx + fy * fy + fz * fz) / dt > 1e-4f) mk[s.cfoot[c]] |= 1u << s.cstone[c];
+    }
+    mask_out[0] = mk[0];
+    mask_out[1] = mk[1];
+  }
+  // ---- integrate
+  if (lane < nh) {
+    float v = fminf(fmaxf(s.u[6 + lane], -K.sim.max_joint_vel), K.sim.max_joint_vel);
+    s.u[6 + lane] = v;
+    s.qi[lane] += dt * v;
+  }
+  if (lane == 0) {
+    const float* u = s.u;
+    float c0w[3];
+    for (int k = 0; k < 3; ++k) c0w[k] = s.root_pos[k] + s.c[0][k] + dt * u[k];
+    const float* w = u + 3;
+    float wn = sqrtf(dot3(w, w));
+    float th = wn * dt, dq[4];
+    if (th > 1e-12f) {
+      float sn, cs;
+      sincosf(0.5f * th, &sn, &cs);
+      float sc = sn / wn;
+      dq[0] = cs; dq[1] = w[0] * sc; dq[2] = w[1] * sc; dq[3] = w[2] * sc;
+    } else {
+      dq[0] = 1.f; dq[1] = 0.5f * dt * w[0]; dq[2] = 0.5f * dt * w[1]; dq[3] = 0.5f * dt * w[2];
+    }
+    const float* q0 = s.root_quat;
+    float nq[4] = {dq[0] * q0[0] - dq[1] * q0[1] - dq[2] * q0[2] - dq[3] * q0[3],
+                   dq[0] * q0[1] + dq[1] * q0[0] + dq[2] * q0[3] - dq[3] * q0[2],
+                   dq[0] * q0[2] - dq[1] * q0[3] + dq[2] * q0[0] + dq[3] * q0[1],
+                   dq[0] * q0[3] + dq[1] * q0[2] - dq[2] * q0[1] + dq[3] * q0[0]};
+    float qn = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+    for (int k = 0; k < 4; ++k) s.root_quat[k] = nq[k] * qn;
+    float Rn[9], cl[3];
+    quat_to_mat(s.root_quat, Rn);
+    matvec3(Rn, m.com[0], cl);
+    for (int k = 0; k < 3; ++k) s.root_pos[k] = c0w[k] - cl[k];
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// task logic helpers (allsteps_env.py)
+
+struct Useful {
+  float h, roll, pitch, body_dist, dist_f[2];
+  int reached;
+};
+
+// allsteps_env.py:418-457 foot-state tick + 459-467 targets + 407-416 potentials (one env, serial)
+__device__ void compute_useful(const Consts& K, const float* root_pos, const float* root_quat, const float* bp,
+                               const float* stones_env /* [20][3] or strided via lambda */, int stride,
+                               uint32_t mask_r, uint32_t mask_l, int& idx, int& prev, int& next, int& count,
+                               int& swing, float& pot, float& old_pot, float* foot_contact, bool tick, Useful& u) {
+  const as_task_t& T = K.task;
+  const int N = T.num_steps;
+  float lower = fminf(bp[8], bp[5]);   // minimum(left_z, right_z)
+  u.h = bp[2] - lower;
+  euler_rp_from_quat(root_quat, &u.roll, &u.pitch);
+  u.reached = 0;
+  if (tick) {
+    float cf0 = ((mask_r >> idx) & 1u) ? 1.f : 0.f;
+    float cf1 = ((mask_l >> idx) & 1u) ? 1.f : 0.f;
+    foot_contact[0] = cf0;
+    foot_contact[1] = cf1;
+    float tx = stones_env[(idx * 3 + 0) * stride], ty = stones_env[(idx * 3 + 1) * stride];
+    for (int f = 0; f < 2; ++f) {
+      float dx = bp[3 + 3 * f] - tx, dy = bp[3 + 3 * f + 1] - ty;
+      u.dist_f[f] = sqrtf(dx * dx + dy * dy);
+    }
+    float cfs = swing == 0 ? cf0 : cf1;
+    u.reached = (cfs > 0.f) && (u.dist_f[swing] < T.step_radius);
+    if (u.reached) count += 1;
+    if (count >= T.stop_frames) {
+      swing ^= 1;
+      int ni = min(max(idx + 1, 0), N - 1);
+      idx = ni;
+      prev = min(max(ni - 1, 0), N - 1);
+      next = min(max(ni + 1, 0), N - 1);
+      count = 0;
+    }
+  }
+  float dx = stones_env[(next * 3 + 0) * stride] - root_pos[0];
+  float dy = stones_env[(next * 3 + 1) * stride] - root_pos[1];
+  u.body_dist = sqrtf(dx * dx + dy * dy);
+  old_pot = pot;
+  pot = -(u.body_dist) / T.step_dt;
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_step(StepArgs P) {
+  __shared__ Smem sm;
+  __shared__ Consts K;
+  {  // stage the constants in LDS
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(P.consts);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&K);
+    for (int i = threadIdx.x; i < (int)(sizeof(Consts) / 4); i += 64) dst[i] = src[i];
+  }
+  const int el = threadIdx.x >> 5, lane = threadIdx.x & 31;
+  const int n = P.n;
+  const int e_raw = blockIdx.x * EPB + el;
+  const bool valid = e_raw < n;
+  const int e = valid ? e_raw : n - 1;
+  EnvS& s = sm.env[el];
+  const as_state_t& st = P.st;
+  __syncthreads();
+  const as_model_t& m = K.model;
+  const int nh = m.num_hinges;
+  const as_task_t& T = K.task;
+  // ---- load
+  if (lane < 3) {
+    s.root_pos[lane] = st.root_pos[lane * n + e];
+    s.u[lane] = st.root_lin[lane * n + e];
+    s.u[3 + lane] = st.root_ang[lane * n + e];
+  }
+  if (lane < 4) s.root_quat[lane] = st.root_quat[lane * n + e];
+  const int cur = st.curriculum[0];
+  const float gain = T.gain_curriculum[cur];
+  if (lane < nh) {
+    int i = m.cfg_dof_link[lane] - 1;
+    s.qi[i] = st.q[lane * n + e];
+    s.u[6 + i] = st.qd[lane * n + e];
+    float a = 0.f;
+    if (P.mode != kModeReset) a = P.actions[(size_t)e * nh + lane];
+    a = fminf(fmaxf(a, -1.f), 1.f);                      // allsteps_env.py:267-268
+    s.act[lane] = a;
+    s.tau[i] = gain * m.gear[lane] * a;                  // allsteps_env.py:273
+  }
+  for (int k = lane; k < 3 * T.num_steps; k += G) s.stones[k] = st.stones[k * n + e];
+  uint32_t mask[2] = {st.contact_mask[e], st.contact_mask[n + e]};
+  __syncthreads();
+  const bool do_physics = P.mode == kModeStep || P.mode == kModePhysics;
+  // ---- physics
+  if (do_physics) {
+    for (int sub = 0; sub < K.sim.substeps; ++sub) substep(K, sm, s, lane, mask);
+    // FK of the final pose for body_pos_w (articulation_data.py:439)
+    fk(K, s, lane);
+    if (lane == 0) {
+      uint32_t m0 = mask[0], m1 = mask[1];
+      s.mask[0] = m0;
+      s.mask[1] = m1;
+    }
+    __syncthreads();
+  }
+  if (lane == 0 && !do_physics) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
+  __syncthreads();
+  float bp[9];
+  if (do_physics) {
+    const int ls[3] = {m.torso_link, m.foot_link[0], m.foot_link[1]};
+    for (int b = 0; b < 3; ++b)
+      for (int k = 0; k < 3; ++k) bp[3 * b + k] = s.root_pos[k] + s.p[ls[b]][k];
+  } else {
+    for (int k = 0; k < 9; ++k) bp[k] = st.body_pos[k * n + e];
+  }
+  // ---- task epilogue (direct_rl_env.py:349-364)
+  int idx = st.idx[e], prev = st.prev[e], next = st.next[e], count = st.count[e], swing = st.swing[e];
+  int ep_len = st.ep_len[e];
+  float pot = st.pot[e], old_pot = st.old_pot[e];
+  float fc[2] = {st.foot_contact[e], st.foot_contact[n + e]};
+  uint32_t episode = st.episode[e];
+  bool done = false;
+  if (P.mode == kModeStep || P.mode == kModeTask) {
+    ep_len += 1;                                         // direct_rl_env.py:351
+    Useful u;
+    compute_useful(K, s.root_pos, s.root_quat, bp, s.stones, 1, s.mask[0], s.mask[1], idx, prev, next, count,
+                   swing, pot, old_pot, fc, true, u);    // allsteps_env.py:397 tick #1
+    // lane-parallel pieces of the reward: sum a^2, sum |qd a|, #(|q_scaled| > 0.99)
+    float a2 = 0.f, en = 0.f;
+    int atlim = 0;
+    if (lane < nh) {
+      int li = m.cfg_dof_link[lane];
+      float a = s.act[lane];
+      a2 = a * a;
+      en = fabsf(s.u[6 + li - 1] * a);
+      atlim = fabsf(scale_transform(s.qi[li - 1], m.lower[li], m.upper[li])) > 0.99f;
+    }
+    a2 = wave32_sum(a2);
+    en = wave32_sum(en);
+    uint64_t bl = __ballot(atlim != 0);
+    int nlim = __popcll(bl >> (32 * el) & 0xffffffffull);
+    const float* lv = s.u;
+    float speed = sqrtf(lv[0] * lv[0] + lv[1] * lv[1] + lv[2] * lv[2]);
+    bool time_out = ep_len >= T.max_episode_length - 1;  // allsteps_env.py:399
+    bool fell = u.h < T.term_curriculum[cur];            // :401
+    bool so_fast = speed > 5.0f;                         // :402
+    bool died = s.root_pos[2] < T.fall_abs;              // :403
+    bool terminated = fell || so_fast || died;
+    // allsteps_env.py:347-394
+    float progress = pot - old_pot;
+    bool roll_v = (u.roll > 0.4f) || (u.roll < -0.4f);
+    bool pitch_v = (u.pitch > 0.4f) || (u.pitch < -0.2f);
+    float roll_cost = roll_v ? fabsf(u.roll) : 0.f;
+    float pitch_cost = pitch_v ? fabsf(u.pitch) : 0.f;
+    float speed_cost = speed > 1.6f ? speed - 1.6f : 0.f;
+    float action_cost = T.action * sqrtf(a2);
+    float energy_cost = T.energy * en;
+    float limit_cost = (float)nlim * T.joint_limit;
+    bool cond = u.reached && count == 1 && idx < T.num_steps - 1;
+    float step_rew = cond ? 50.0f * expf(-u.dist_f[swing] / 0.25f) : 0.f;
+    bool bonus_c = idx == T.num_steps - 1 && u.body_dist < 0.15f;
+    float total = T.alive + progress;
+    total = total - roll_cost;
+    total = total - pitch_cost;
+    total = total - speed_cost;
+    total = total - energy_cost;
+    total = total - action_cost;
+    total = total - limit_cost;
+    total = total + step_rew;
+    total = total + (bonus_c ? 10.0f : 0.f);
+    float rew = terminated ? T.death : total;
+    done = terminated || time_out;
+    if (valid && lane == 0) {
+      P.reward[e] = rew;
+      P.terminated[e] = terminated ? 1 : 0;
+      P.truncated[e] = time_out ? 1 : 0;
+      atomicAdd(&P.counters[1], idx);                   // curriculum mean over tick-#1 indices
+      if (done) atomicOr(&P.counters[0], 1);
+    }
+  } else if (P.mode == kModeReset) {
+    done = true;
+    if (valid && lane == 0) {
+      atomicAdd(&P.counters[1], idx);
+      atomicOr(&P.counters[0], 1);
+    }
+  }
+  // ---- in-kernel reset (allsteps_env.py:481-565)
+  const bool any_done = __any(done);  // wave-uniform: both envs of the wave enter the FK together
+  if (P.mode != kModePhysics && any_done) {
+    if (done) {
+      float d[24];
+      if (P.reset_draws) {
+        for (int k = 0; k < 22; ++k) d[k] = P.reset_draws[(size_t)e * 22 + k];
+      } else {
+        for (int b = 0; b < 6; ++b)
+          philox_block(P.seed, (uint32_t)(P.env_offset + e), episode, (uint32_t)b, kResetTag, d + 4 * b);
+      }
+      ep_len = 0;
+      old_pot = 0.f; pot = 0.f; count = 0; swing = 0; idx = 1; prev = 0; next = 2;
+      const bool mirror = d[0] > 0.5f;
+      if (mirror) swing ^= 1;
+      if (lane < nh) {
+        // joint `lane` (cfg order): running-start pose, mirrored, noise, clip (allsteps_env.py:505-560)
+        int src = lane;
+        float sign = 1.f;
+        if (mirror) {
+          for (int t = 0; t < 9; ++t) {
+            if (T.right_idx[t] == lane) src = T.left_idx[t];
+            if (T.left_idx[t] == lane) src = T.right_idx[t];
+          }
+          if (T.neg_idx[0] == lane || T.neg_idx[1] == lane) sign = -1.f;
+        }
+        float jp = T.init_q[src] * sign;
+        float jv = 0.f * sign;
+        int li = m.cfg_dof_link[lane];
+        float x = jp + (d[1 + lane] * (T.noise_hi - T.noise_lo) + T.noise_lo);
+        float sc = fminf(fmaxf(scale_transform(x, m.lower[li], m.upper[li]), T.clip_lo), T.clip_hi);
+        s.qi[li - 1] = unscale_transform(sc, m.lower[li], m.upper[li]);
+        s.u[6 + li - 1] = jv;
+      }
+      if (lane < 3) {
+        s.root_pos[lane] = T.init_root[lane];
+        s.u[lane] = 0.f;
+        s.u[3 + lane] = 0.f;
+      }
+      if (lane == 0) {
+        float sg = mirror ? -1.f : 1.f;
+        s.root_quat[0] = 1.f;
+        s.root_quat[1] = 0.f * sg;
+        s.root_quat[2] = 0.f * sg;
+        s.root_quat[3] = 0.f * sg;
+      }
+      episode += 1u;
+    }
+    __syncthreads();
+    fk(K, s, lane);  // body_pos of the reset pose (write_joint_state_to_sim invalidates FK)
+    if (done) {
+      const int ls[3] = {m.torso_link, m.foot_link[0], m.foot_link[1]};
+      for (int b = 0; b < 3; ++b)
+        for (int k = 0; k < 3; ++k) bp[3 * b + k] = s.root_pos[k] + s.p[ls[b]][k];
+    }
+  }
+  __syncthreads();
+  // ---- store
+  if (!valid) return;
+  if (lane < 3) {
+    st.root_pos[lane * n + e] = s.root_pos[lane];
+    st.root_lin[lane * n + e] = s.u[lane];
+    st.root_ang[lane * n + e] = s.u[3 + lane];
+  }
+  if (lane < 4) st.root_quat[lane * n + e] = s.root_quat[lane];
+  if (lane < nh) {
+    int i = m.cfg_dof_link[lane] - 1;
+    st.q[lane * n + e] = s.qi[i];
+    st.qd[lane * n + e] = s.u[6 + i];
+  }
+  if (lane < 9) st.body_pos[lane * n + e] = bp[lane];
+  if (lane == 0) {
+    st.contact_mask[e] = s.mask[0];
+    st.contact_mask[n + e] = s.mask[1];
+    if (P.mode != kModePhysics) {
+      st.idx[e] = idx; st.prev[e] = prev; st.next[e] = next; st.count[e] = count; st.swing[e] = swing;
+      st.ep_len[e] = ep_len; st.pot[e] = pot; st.old_pot[e] = old_pot;
+      st.foot_contact[e] = fc[0]; st.foot_contact[n + e] = fc[1];
+      st.episode[e] = episode;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_obs(ObsArgs P) {
+  const as_task_t& T = P.consts->task;
+  const as_model_t& m = P.consts->model;
+  const int n = P.n;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int any_reset = P.counters[0];
+  if (any_reset && e == 0) {  // allsteps_env.py:471-479 (evaluated once, before the resets' tick #2)
+    int c = P.st.curriculum[0];
+    if ((float)P.counters[1] / (float)n > (float)T.curriculum_threshold) P.st.curriculum[0] = min(c + 1, T.max_curriculum);
+  }
+  if (e >= n) return;
+  const as_state_t& st = P.st;
+  float rp[3] = {st.root_pos[e], st.root_pos[n + e], st.root_pos[2 * n + e]};
+  float rq[4] = {st.root_quat[e], st.root_quat[n + e], st.root_quat[2 * n + e], st.root_quat[3 * n + e]};
+  float bp[9];
+  for (int k = 0; k < 9; ++k) bp[k] = st.body_pos[k * n + e];
+  int idx = st.idx[e], prev = st.prev[e], next = st.next[e], count = st.count[e], swing = st.swing[e];
+  float pot = st.pot[e], old_pot = st.old_pot[e];
+  float fc[2] = {st.foot_contact[e], st.foot_contact[n + e]};
+  Useful u;
+  compute_useful(*P.consts, rp, rq, bp, st.stones + e, n, st.contact_mask[e], st.contact_mask[n + e], idx, prev,
+                 next, count, swing, pot, old_pot, fc, any_reset != 0, u);
+  if (any_reset) {  // tick #2 results persist (allsteps_env.py:567)
+    st.idx[e] = idx; st.prev[e] = prev; st.next[e] = next; st.count[e] = count; st.swing[e] = swing;
+    st.pot[e] = pot; st.old_pot[e] = old_pot;
+    st.foot_contact[e] = fc[0]; st.foot_contact[n + e] = fc[1];
+  }
+  // allsteps_env.py:326-345 observation
+  float* o = P.obs + (size_t)e * AS_OBS_DIM;
+  o[0] = u.h;
+  o[1] = u.roll;
+  o[2] = u.pitch;
+  float lv[3] = {st.root_lin[e], st.root_lin[n + e], st.root_lin[2 * n + e]}, vb[3];
+  quat_rotate_inverse(rq, lv, vb);
+  o[3] = vb[0]; o[4] = vb[1]; o[5] = vb[2];
+  for (int k = 0; k < AS_ACT_DIM; ++k) {
+    int li = m.cfg_dof_link[k];
+    o[6 + k] = scale_transform(st.q[k * n + e], m.lower[li], m.upper[li]);
+    o[27 + k] = fminf(fmaxf(st.qd[k * n + e] * T.dof_vel_scale, -5.f), 5.f);
+  }
+  o[48] = fc[0];
+  o[49] = fc[1];
+  const int tix[3] = {prev, idx, next};
+  for (int t = 0; t < 3; ++t) {
+    float tw[3] = {st.stones[(tix[t] * 3 + 0) * n + e], st.stones[(tix[t] * 3 + 1) * n + e],
+                   st.stones[(tix[t] * 3 + 2) * n + e]};
+    subtract_frame_transforms(rp, rq, tw, o + 50 + 3 * t);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// allsteps_env.py:125-174 _generate_foot_steps_allsteps (+ env origin = 0)
+__device__ float lerp_t(float a, float b, float w) {  // torch.lerp (ATen Lerp.h)
+  return fabsf(w) < 0.5f ? a + w * (b - a) : b - (b - a) * (1.0f - w);
+}
+
+__global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
+  const as_task_t& T = P.consts->task;
+  const int n = P.n;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int N = T.num_steps, maxc = T.max_curriculum;
+  const int c = min(P.level, maxc);
+  const float ratio = (float)c / (float)maxc;
+  const float step = (0.9f - 0.75f) / (float)maxc;  // torch.linspace(0.75, 0.9, 10)[c]
+  const float dist_hi = c < (maxc + 1) / 2 ? 0.75f + step * (float)c : 0.9f - step * (float)(maxc - c);
+  const float d2r = 0.01745329251994329577f;
+  const float yaw_lo = (-20.0f * ratio) * d2r, yaw_hi = (20.0f * ratio) * d2r;
+  const float p_lo = (-30.0f * ratio) * d2r + 1.57079632679489661923f;
+  const float p_hi = (30.0f * ratio) * d2r + 1.57079632679489661923f;
+  float x = 0.f, y = 0.f, z = 0.f, phi = 0.f;
+  for (int k = 0; k < N; ++k) {
+    float w[3];
+    if (P.draws) {
+      for (int j = 0; j < 3; ++j) w[j] = P.draws[((size_t)j * n + e) * N + k];
+    } else {
+      float blk[4];
+      philox_block(P.seed, (uint32_t)(P.env_offset + e), 0u, (uint32_t)k, kStonesTag, blk);
+      w[0] = blk[0]; w[1] = blk[1]; w[2] = blk[2];
+    }
+    float dr = lerp_t(0.75f, dist_hi, w[0]);
+    float dph = lerp_t(yaw_lo, yaw_hi, w[1]);
+    float dth = lerp_t(p_lo, p_hi, w[2]);
+    if (k == 0) { dr = 0.f; dph = 0.f; dth = 1.57079632679489661923f; }
+    if (k == 1 || k == 2) { dr = 0.75f; dph = 0.f; dth = 1.57079632679489661923f; }
+    phi += dph;
+    float st_, ct_, sp, cp;
+    sincosf(dth, &st_, &ct_);
+    sincosf(phi, &sp, &cp);
+    x += dr * st_ * cp;
+    y += dr * st_ * sp;
+    z += dr * ct_;
+    P.stones[(k * 3 + 0) * n + e] = x;
+    P.stones[(k * 3 + 1) * n + e] = y;
+    P.stones[(k * 3 + 2) * n + e] = z;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+hipError_t launch_step(const StepArgs& a, hipStream_t stream) {
+  int blocks = (a.n + EPB - 1) / EPB;
+  hipLaunchKernelGGL(k_step, dim3(blocks), dim3(64), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_obs(const ObsArgs& a, hipStream_t stream) {
+  int blocks = (a.n + 255) / 256;
+  hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_stones(const StonesArgs& a, hipStream_t stream) {
+  int blocks = (a.n + 255) / 256;
+  hipLaunchKernelGGL(k_stones, dim3(blocks), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+size_t step_lds_bytes() { return sizeof(Smem) + sizeof(Consts); }
+
+}  // namespace as

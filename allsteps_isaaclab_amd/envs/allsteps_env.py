@@ -1,0 +1,309 @@
+"""``AllstepsEnv`` -- the Allsteps-v0 stepping-stone task on the MI355X-native step kernels.
+
+Drop-in for ``isaaclab_tasks/direct/allsteps/allsteps_env.py:34-567`` (``AllstepsEnv``): same
+constructor (``cfg, render_mode``), same ``step``/``reset`` results (policy obs (N, 59), reward,
+terminated, truncated, extras), same task buffers (``curr_target_index``, ``swing_leg``,
+``potentials`` ...), same mirror indices and symmetry functions.  Underneath, the whole
+``DirectRLEnv.step`` -- actuation, 4 physics substeps, contacts, foot-state machine, rewards,
+dones, resets, observations -- is two HIP kernels (``liballsteps_hip.so``) over a struct-of-arrays
+state that stays resident in HBM; there is no PhysX, no Python per-step logic and no host sync.
+"""
+
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from .. import _native
+from ..model import joint_limits_cfg, load_model
+from .allsteps_env_cfg import AllstepsEnvCfg
+from .direct_rl_env import DirectRLEnv
+
+RIGHT_FOOT = 0
+LEFT_FOOT = 1
+EPSILON = 1e-4
+
+_FLOAT_FIELDS = [(n, r) for n, r, t in _native.STATE_LAYOUT if t == "f"]
+_INT_FIELDS = [(n, r) for n, r, t in _native.STATE_LAYOUT if t == "i"]
+
+
+class _RobotData:
+    """The ``ArticulationData`` views the task reads (articulation_data.py:364-601), as zero-copy
+    (N, k) views of the SoA state (k-major storage, so rows are strided)."""
+
+    def __init__(self, env: "AllstepsEnv"):
+        self._env = env
+        s = env.state
+        n = env.num_envs
+        self.joint_names = list(env.model["dof_names"])
+        self.body_names = ["torso", "right_foot", "left_foot"]
+        lim = torch.as_tensor(joint_limits_cfg(env.model), device=env._device)
+        self.joint_pos_limits = lim.unsqueeze(0).expand(n, -1, -1)
+        self.default_joint_pos = torch.zeros(n, 21, device=env._device)
+        self.default_joint_vel = torch.zeros(n, 21, device=env._device)
+        self.default_root_state = torch.zeros(n, 13, device=env._device)
+        self.default_root_state[:, :3] = torch.tensor(env.cfg.init_root_pos, device=env._device)
+        self.default_root_state[:, 3] = 1.0
+        self._s = s
+
+    root_pos_w = property(lambda self: self._s["root_pos"].T)
+    root_quat_w = property(lambda self: self._s["root_quat"].T)
+    root_lin_vel_w = property(lambda self: self._s["root_lin"].T)
+    root_ang_vel_w = property(lambda self: self._s["root_ang"].T)
+    joint_pos = property(lambda self: self._s["q"].T)
+    joint_vel = property(lambda self: self._s["qd"].T)
+
+    @property
+    def root_state_w(self) -> torch.Tensor:
+        s = self._s
+        return torch.cat([s["root_pos"], s["root_quat"], s["root_lin"], s["root_ang"]], 0).T.contiguous()
+
+    @property
+    def body_pos_w(self) -> torch.Tensor:
+        """(N, 3, 3): torso, right_foot, left_foot link-frame positions (FK after the last substep)."""
+        return self._s["body_pos"].view(3, 3, -1).permute(2, 0, 1)
+
+
+class _RobotView:
+    """Minimal ``Articulation`` surface: ``data`` plus the state writers used on reset."""
+
+    def __init__(self, env: "AllstepsEnv"):
+        self._env = env
+        self.data = _RobotData(env)
+        self._ALL_INDICES = torch.arange(env.num_envs, dtype=torch.long, device=env._device)
+
+    def write_root_pose_to_sim(self, root_pose: torch.Tensor, env_ids=None):
+        ids = self._ALL_INDICES if env_ids is None else env_ids
+        s = self._env.state
+        s["root_pos"][:, ids] = root_pose[:, :3].T.to(s["root_pos"].dtype)
+        s["root_quat"][:, ids] = root_pose[:, 3:7].T.to(s["root_quat"].dtype)
+
+    def write_root_velocity_to_sim(self, root_velocity: torch.Tensor, env_ids=None):
+        ids = self._ALL_INDICES if env_ids is None else env_ids
+        s = self._env.state
+        s["root_lin"][:, ids] = root_velocity[:, :3].T.float()
+        s["root_ang"][:, ids] = root_velocity[:, 3:6].T.float()
+
+    def write_joint_state_to_sim(self, position, velocity, joint_ids=None, env_ids=None):
+        ids = self._ALL_INDICES if env_ids is None else env_ids
+        s = self._env.state
+        s["q"][:, ids] = position.T.float()
+        s["qd"][:, ids] = velocity.T.float()
+
+
+class AllstepsEnv(DirectRLEnv):
+    cfg: AllstepsEnvCfg
+
+    def __init__(self, cfg: AllstepsEnvCfg | None = None, render_mode: str | None = None, *,
+                 env_id_offset: int = 0, model: dict | None = None, **kwargs):
+        cfg = cfg if cfg is not None else AllstepsEnvCfg()
+        super().__init__(cfg, render_mode, **kwargs)
+        if self._device.type != "cuda":
+            raise _native.NativeError(
+                f"AllstepsEnv runs on the HIP backend only (device={self._device}); there is no CPU fallback")
+        self.model = model if model is not None else load_model()
+        n = self.num_envs
+        dev = self._device
+        # ---- SoA state, resident in HBM ([field][env])
+        nf = sum(r for _, r in _FLOAT_FIELDS)
+        ni = sum(r for _, r in _INT_FIELDS)
+        self._fbuf = torch.zeros((nf, n), dtype=torch.float32, device=dev)
+        self._ibuf = torch.zeros((ni, n), dtype=torch.int32, device=dev)
+        self.state: dict[str, torch.Tensor] = {}
+        o = 0
+        for name, r in _FLOAT_FIELDS:
+            self.state[name] = self._fbuf[o:o + r] if r > 1 else self._fbuf[o]
+            o += r
+        o = 0
+        for name, r in _INT_FIELDS:
+            self.state[name] = self._ibuf[o:o + r] if r > 1 else self._ibuf[o]
+            o += r
+        self.state["curriculum"] = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.state["root_quat"][0] = 1.0
+        self.state["idx"][:] = 1
+        self.state["next"][:] = 2
+        self.env_id_offset = int(env_id_offset)
+        self._seed_value = int(cfg.seed if cfg.seed is not None else 0)
+        with torch.cuda.device(dev):
+            self._native = _native.NativeEnv(n, self.model, cfg, self.state, self._seed_value,
+                                             dev.index if dev.index is not None else torch.cuda.current_device(),
+                                             self.env_id_offset)
+            # footsteps generated once at init (allsteps_env.py:71), curriculum level 0 by default
+            self._native.generate_stones(int(cfg.initial_stone_curriculum), stream=self._stream())
+        # ---- DirectRLEnv buffers (direct_rl_env.py:179-185)
+        self.reset_terminated = torch.zeros(n, dtype=torch.bool, device=dev)
+        self.reset_time_outs = torch.zeros(n, dtype=torch.bool, device=dev)
+        self.reward_buf = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.obs_buf = {"policy": torch.zeros(n, cfg.observation_space, device=dev)}
+        self._actions = torch.zeros(n, cfg.action_space, device=dev)
+        # ---- task constants / names (allsteps_env.py:41-92)
+        self.num_steps = cfg.num_steps
+        self.step_radius = cfg.step_radius
+        self.stop_frames = cfg.stop_frames
+        self.max_curriculum = torch.tensor(cfg.max_curriculum, dtype=torch.int64, device=dev)
+        self.termination_curriculum = torch.as_tensor(_native.linspace_f32(0.75, 0.45, cfg.max_curriculum + 1),
+                                                      device=dev)
+        self.applied_gain_curriculum = torch.as_tensor(_native.linspace_f32(1.2, 1.2, cfg.max_curriculum + 1),
+                                                       device=dev)
+        self.joint_gears = torch.tensor(cfg.joint_gears, dtype=torch.float32, device=dev)
+        self.robot = _RobotView(self)
+        jn = self.robot.data.joint_names
+        self.foot_names = list(cfg.foot_names)
+        self.foot_indices = [self.robot.data.body_names.index(x) for x in self.foot_names]
+        self.torso_index = self.robot.data.body_names.index(cfg.torso_name)
+        L = lambda names: torch.tensor([jn.index(x) for x in names], dtype=torch.int64, device=dev)  # noqa: E731
+        self.hip_y_index = L(cfg.hip_y_names)
+        self.right_body_indices = L(cfg.right_body_names)
+        self.left_body_indices = L(cfg.left_body_names)
+        self.negation_body_indices = L(cfg.negation_body_names)
+
+    # ------------------------------------------------------------------ task buffers (views)
+    episode_length_buf = property(lambda self: self.state["ep_len"])
+    curr_target_index = property(lambda self: self.state["idx"])
+    prev_target_index = property(lambda self: self.state["prev"])
+    next_target_index = property(lambda self: self.state["next"])
+    target_reach_count = property(lambda self: self.state["count"])
+    swing_leg = property(lambda self: self.state["swing"])
+    potentials = property(lambda self: self.state["pot"])
+    old_potentials = property(lambda self: self.state["old_pot"])
+    foot_contact = property(lambda self: self.state["foot_contact"].T)
+
+    @property
+    def curriculum(self) -> torch.Tensor:
+        """Per-env curriculum level (all envs share one level in the reference, allsteps_env.py:472)."""
+        return self.state["curriculum"].expand(self.num_envs)
+
+    @property
+    def steps_pos(self) -> torch.Tensor:
+        """(N, 20, 3) stepping-stone centres, env-local frame."""
+        return self.state["stones"].view(self.num_steps, 3, -1).permute(2, 0, 1)
+
+    @property
+    def actions(self) -> torch.Tensor:
+        return torch.clamp(self._actions, -1.0, 1.0)
+
+    @property
+    def reset_buf(self) -> torch.Tensor:
+        return self.reset_terminated | self.reset_time_outs
+
+    @property
+    def targets_w(self) -> torch.Tensor:
+        """(N, 3, 3) previous / current / next target stone (allsteps_env.py:459-467)."""
+        sp = self.steps_pos
+        ar = torch.arange(self.num_envs, device=self._device)
+        idx = [self.state[k].long() for k in ("prev", "idx", "next")]
+        return torch.stack([sp[ar, i] for i in idx], 1)
+
+    # ------------------------------------------------------------------ native backend
+    def _stream(self):
+        return torch.cuda.current_stream(self._device).cuda_stream
+
+    def _reseed(self, seed: int):
+        self._seed_value = int(seed)
+        self._native.set_seed(self._seed_value)
+
+    def _reset_impl(self, reset_draws: torch.Tensor | None = None):
+        obs = torch.empty(self.num_envs, self.cfg.observation_space, device=self._device)
+        self._native.reset_all(obs, reset_draws, stream=self._stream())
+        self.obs_buf = {"policy": obs}
+        return self.obs_buf
+
+    def _step_impl(self, action: torch.Tensor, reset_draws: torch.Tensor | None = None):
+        a = action if (action.dtype == torch.float32 and action.is_contiguous()) else action.float().contiguous()
+        if a.shape != (self.num_envs, self.cfg.action_space):
+            raise ValueError(f"actions must be ({self.num_envs}, {self.cfg.action_space}), got {tuple(a.shape)}")
+        obs = torch.empty(self.num_envs, self.cfg.observation_space, device=self._device)
+        rew = torch.empty(self.num_envs, device=self._device)
+        self._native.step(a, obs, rew, self.reset_terminated, self.reset_time_outs, reset_draws,
+                          stream=self._stream())
+        self._actions = a
+        self.obs_buf = {"policy": obs}
+        self.reward_buf = rew
+        return self.obs_buf, rew, self.reset_terminated, self.reset_time_outs, self.extras
+
+    def step_with_draws(self, action: torch.Tensor, reset_draws: torch.Tensor):
+        """``step`` with injected reset draws ((N, 22) U[0,1): mirror, 21 joint noise) -- parity tests."""
+        self._sim_step_counter += self.cfg.decimation
+        out = self._step_impl(action.to(self._device), reset_draws.to(self._device).float().contiguous())
+        self.common_step_counter += 1
+        return out
+
+    def reset_with_draws(self, reset_draws: torch.Tensor):
+        return self._reset_impl(reset_draws.to(self._device).float().contiguous()), self.extras
+
+    def task_step(self, action: torch.Tensor, reset_draws: torch.Tensor | None = None):
+        """Post-physics half of ``step`` on the current state (body_pos / contact_mask as written)."""
+        a = action.to(self._device).float().contiguous()
+        obs = torch.empty(self.num_envs, self.cfg.observation_space, device=self._device)
+        rew = torch.empty(self.num_envs, device=self._device)
+        d = None if reset_draws is None else reset_draws.to(self._device).float().contiguous()
+        self._native.task_step(a, obs, rew, self.reset_terminated, self.reset_time_outs, d, stream=self._stream())
+        return {"policy": obs}, rew, self.reset_terminated, self.reset_time_outs, self.extras
+
+    def physics_step(self, action: torch.Tensor):
+        """Physics only (4 substeps, no task logic) -- known-answer tests / profiling."""
+        a = action.to(self._device).float().contiguous()
+        self._native.physics_step(a, stream=self._stream())
+
+    def generate_foot_steps(self, level: int, draws: torch.Tensor | None = None):
+        """_generate_foot_steps_allsteps at `level` for every env (allsteps_env.py:106-174)."""
+        d = None if draws is None else draws.to(self._device).float().contiguous()
+        self._native.generate_stones(int(level), d, stream=self._stream())
+
+    def get_state(self) -> dict:
+        """Copy of the full SoA state (field -> (rows, N) tensor)."""
+        return {k: v.clone() for k, v in self.state.items()}
+
+    def set_state(self, state: dict):
+        for k, v in state.items():
+            self.state[k].copy_(torch.as_tensor(v).to(self.state[k].device, self.state[k].dtype).reshape(
+                self.state[k].shape))
+
+    def close(self):
+        if getattr(self, "_native", None) is not None:
+            self._native.close()
+            self._native = None
+        super().close()
+
+
+# ------------------------------------------------------------------------------------------------
+# mirror augmentation (allsteps_env.py:570-660)
+
+def _mirror_indices(env, obs_dim: int, act_dim: int, device):
+    uw = env.unwrapped
+    right, left, neg = uw.right_body_indices, uw.left_body_indices, uw.negation_body_indices
+    K = 2 if obs_dim == 56 else 3
+    steps_neg = torch.tensor([K * i + 1 for i in range(3)], dtype=torch.int64, device=device)
+    root_neg = torch.tensor([1, 4], dtype=torch.int64, device=device)
+    r_obs = torch.cat((right + 6, right + 6 + act_dim, torch.tensor([6 + act_dim * 2], device=device)))
+    l_obs = torch.cat((left + 6, left + 6 + act_dim, torch.tensor([6 + act_dim * 2 + 1], device=device)))
+    n_obs = torch.cat((root_neg, 6 + neg, 6 + act_dim + neg, 6 + act_dim * 2 + 2 + steps_neg))
+    return right, left, neg, r_obs, l_obs, n_obs
+
+
+def _mirror(x, right, left, neg):
+    y = x.clone()
+    y[:, right] = x[:, left]
+    y[:, left] = x[:, right]
+    y[:, neg] = -x[:, neg]
+    return y
+
+
+def get_symmetric_states_rsl_rl(obs, actions, env, is_critic: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    uw = env.unwrapped
+    dev = uw.right_body_indices.device
+    right, left, neg, r_obs, l_obs, n_obs = _mirror_indices(env, uw.observation_space.shape[1],
+                                                            uw.action_space.shape[1], dev)
+    ro = None if obs is None else torch.vstack((obs, _mirror(obs, r_obs, l_obs, n_obs)))
+    ra = None if actions is None else torch.vstack((actions, _mirror(actions, right, left, neg)))
+    return ro, ra
+
+
+def get_symmetric_states_rl_games(obs, actions, env, is_critic: bool, mus):
+    ro, ra = get_symmetric_states_rsl_rl(obs, actions, env, is_critic)
+    if mus is None:
+        return ro, ra, None
+    uw = env.unwrapped
+    rm = torch.vstack((mus, _mirror(mus, uw.right_body_indices, uw.left_body_indices, uw.negation_body_indices)))
+    return ro, ra, rm

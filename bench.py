@@ -1,0 +1,178 @@
+"""Allsteps-v0 step throughput on MI355X: env-steps/s (whole job), 4096 envs per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--num-envs 4096] [--level 0]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+Protocol (after scripts/benchmarks/benchmark_non_rl.py:155-179): W untimed warm-up
+steps, then K timed ``env.step`` calls bracketed by a barrier + device synchronize on both sides;
+fresh U(-1, 1) actions every step (pre-drawn on the device before the timed region); seed 42 + rank;
+episodes terminate and reset naturally inside the timed region.  Envs are sharded per rank (weak
+scaling, no collective in the step).  value = all ranks' env-steps / max-over-ranks wall time.
+
+Extra objects on the JSON line:
+  roofline     -- k_step (the dominant kernel): algorithmic bytes per launch / its average duration
+                  from HIP events recorded around every launch on its own stream, vs 8 TB/s HBM.
+  cpu_baseline -- rank 0, N = 1: the CPU oracle (oracle/, a port of the same step) timed on this
+                  host's cores on a bounded sample.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# Algorithmic bytes per env per launch: every state byte the kernel must read
+# or write once, from the SoA layout of include/allsteps.h.
+K_STEP_READ = 84 + 52 + 168 + 240 + 8 + 24 + 8 + 8 + 4    # actions, root, q/qd, stones, masks, ints, pots, contact, episode
+K_STEP_WRITE = 52 + 168 + 36 + 8 + 24 + 8 + 8 + 4 + 6     # root, q/qd, body_pos, masks, ints, pots, contact, episode, rew/term/trunc
+K_STEP_BYTES = K_STEP_READ + K_STEP_WRITE
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--num-envs", type=int, default=4096)
+    p.add_argument("--level", type=int, default=0, help="stone curriculum level (C3: 9)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    return p.parse_args()
+
+
+def cpu_baseline(num_envs: int, level: int, threads: int) -> dict:
+    """The oracle (CPU port of the same step) on the host cores, bounded sample (~10-30 s CPU)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    O.build()
+    orc = O.Oracle()
+    n = min(num_envs, 4096)
+    st = orc.state(n)
+    if level == 0:
+        for k in range(20):
+            st["stones"][3 * k + 0][:] = 0.75 * k
+            st["stones"][3 * k + 2][:] = np.float32(k * 0.75) * np.cos(np.float32(np.pi / 2), dtype=np.float32)
+    else:
+        rng = np.random.default_rng(0)
+        pos, _ = orc.footsteps(n, level, rng.uniform(0, 1, (5, n, 20)).astype(np.float32))
+        st["stones"][:] = pos.reshape(n, 60).T
+    orc.reset_all(st, seed=42)
+    rng = np.random.default_rng(42)
+    acts = [rng.uniform(-1, 1, (n, 21)).astype(np.float32) for _ in range(4)]
+    orc.env_step(st, acts[0], nthreads=threads)  # warm
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        orc.env_step(st, acts[steps % 4], nthreads=threads)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el * threads > 20.0 or steps >= 200:
+            break
+    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ C port, {n} envs x {steps} steps (level {level}, from reset, U(-1,1) actions), "
+                      f"OpenMP {threads} threads, {el:.2f} s wall"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    device = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(device)
+
+    from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv
+    from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
+
+    n = args.num_envs
+    cfg = AllstepsEnvCfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = str(device)
+    cfg.seed = 42 + rank
+    cfg.initial_stone_curriculum = args.level
+    env = AllstepsEnv(cfg, env_id_offset=rank * n)
+    gen = torch.Generator(device=device).manual_seed(1000 + rank)
+    K, W = args.steps, args.warmup
+    actions = torch.rand(K + W, n, 21, device=device, generator=gen) * 2.0 - 1.0
+    env.reset()
+    for t in range(W):
+        env.step(actions[K + t])
+    torch.cuda.synchronize(device)
+    env._native.profile(K)  # HIP events around every k_step / k_obs launch of the timed region
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    barrier()
+    t0 = time.perf_counter()
+    for t in range(K):
+        env.step(actions[t])
+    barrier()
+    el = time.perf_counter() - t0
+    k_ms, o_ms, launches = env._native.profile_read()
+    if world > 1:
+        tt = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    resets = int(env.reset_buf.sum().item())
+
+    if rank == 0:
+        value = n * world * K / el
+        avg_k = k_ms / max(launches, 1) / 1e3  # s per k_step launch
+        achieved = K_STEP_BYTES * n / avg_k / 1e9
+        line = {
+            "metric": "env-steps/sec (whole node), Allsteps-v0 at 4096 envs per GPU",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(el / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (U(-1,1) actions, reference reset distribution, natural resets)",
+            "config": {
+                "workload": f"Allsteps-v0 biped walker, {n} envs/GPU, stone curriculum level {args.level}, "
+                            f"decimation 4 x dt 1/240",
+                "num_envs_per_gpu": n,
+                "global_envs": n * world,
+                "parallelism": f"dp{world} (env shards, no collective in step)",
+            },
+            "kernels_ms": {"k_step_avg": round(k_ms / max(launches, 1), 5),
+                           "k_obs_avg": round(o_ms / max(launches, 1), 5)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                         "kernel": "k_step", "bytes_per_env": K_STEP_BYTES},
+            "cpu_baseline": None,
+            "resets_last_step": resets,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(n, args.level, args.cpu_threads)
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,191 @@
+/*
+ * allsteps.h -- C ABI of the MI355X-native Allsteps-v0 step (liballsteps_hip.so).
+ *
+ * The reference's hot path is DirectRLEnv.step (isaaclab/envs/direct_rl_env.py:296-383) over the
+ * Allsteps task (isaaclab_tasks/direct/allsteps/allsteps_env.py:257-567), whose physics half is
+ * the omni.physics.tensors / PhysX operator surface (SURVEY.md §8b "Ring 3"):
+ *   set_dof_actuation_forces      (articulation.py:195)          -> as_step (actions in, torque inside)
+ *   SimulationContext.step / simulate(dt) x decimation (simulation_context.py:453-478) -> as_step
+ *   get_root_transforms / get_root_velocities / get_dof_positions / get_dof_velocities
+ *       (articulation_data.py:374-376, 533, 542)                -> state views (as_state_t)
+ *   update_articulations_kinematic (articulation_data.py:439)   -> fused FK inside as_step
+ *   RigidContactView.get_contact_force_matrix (contact_sensor.py:341) -> contact_mask (as_state_t)
+ *   set_root_* / set_dof_* on reset (articulation.py:316-341, 400-420, 472-551) -> in-kernel reset
+ * and the task code around it (_apply_action, _get_dones, _get_rewards, _reset_idx,
+ * _get_observations), fused into two kernels per env step.
+ *
+ * Conventions: every buffer argument is a DEVICE pointer unless its name ends in _host; the caller
+ * owns all buffers (state included, see as_state_t) and keeps them alive for the handle's life;
+ * `stream` is a hipStream_t (NULL = default stream).  Calls on one handle are serialised by the
+ * caller.  No call synchronises the stream except as_get_curriculum_host.  Every function returns 0
+ * on success or a negative AS_ERR_* code; as_last_error() gives a message (thread-local).
+ */
+#ifndef ALLSTEPS_H
+#define ALLSTEPS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AS_ABI_VERSION 1
+#define AS_MAX_LINKS 32
+#define AS_MAX_GEOMS 32
+#define AS_NUM_STONES 20
+#define AS_MAX_CONTACTS 10
+#define AS_MAX_ROWS 40
+#define AS_OBS_DIM 59
+#define AS_ACT_DIM 21
+
+enum {
+  AS_OK = 0,
+  AS_ERR_INVALID = -1,   /* bad argument (null pointer, size out of range, model too large) */
+  AS_ERR_HIP = -2,       /* HIP runtime error (message has the hipError string) */
+  AS_ERR_NO_DEVICE = -3, /* no gfx950 device / code object for this device */
+};
+
+/* Robot model tables (allsteps_isaaclab_amd/model/walker3d.json; compiled from walker3d.xml). */
+typedef struct {
+  int32_t num_links;                  /* incl. floating root = link 0; link i >= 1 carries hinge i-1 */
+  int32_t num_hinges;                 /* num_links - 1 (== AS_ACT_DIM for the walker) */
+  int32_t parent[AS_MAX_LINKS];       /* topological: parent[i] < i */
+  float offset_pos[AS_MAX_LINKS][3];
+  float offset_quat[AS_MAX_LINKS][4]; /* (w, x, y, z) */
+  float axis[AS_MAX_LINKS][3];
+  float anchor[AS_MAX_LINKS][3];
+  float mass[AS_MAX_LINKS];
+  float com[AS_MAX_LINKS][3];
+  float inertia[AS_MAX_LINKS][6];     /* about COM, link frame: xx yy zz xy xz yz */
+  float armature[AS_MAX_LINKS];
+  float lower[AS_MAX_LINKS];
+  float upper[AS_MAX_LINKS];
+  int32_t cfg_dof_link[AS_MAX_LINKS]; /* PhysX/cfg dof k -> link */
+  float gear[AS_MAX_LINKS];           /* cfg order (allsteps_env_cfg.py:133-155) */
+  int32_t num_geoms;
+  int32_t geom_link[AS_MAX_GEOMS];
+  int32_t geom_type[AS_MAX_GEOMS];    /* 0 sphere, 1 capsule */
+  int32_t geom_foot[AS_MAX_GEOMS];    /* -1, 0 right foot, 1 left foot (contact sensors) */
+  float geom_radius[AS_MAX_GEOMS];
+  float geom_p0[AS_MAX_GEOMS][3];
+  float geom_p1[AS_MAX_GEOMS][3];
+  int32_t torso_link;
+  int32_t foot_link[2];
+} as_model_t;
+
+/* Physics constants (simulation_cfg.py; walker3d.py:21-46; allsteps_env_cfg.py:62). */
+typedef struct {
+  float dt;
+  int32_t substeps;
+  float gravity;
+  float friction;
+  float margin;
+  float baumgarte;
+  float slop;
+  float max_depen_vel;
+  int32_t pgs_iters;
+  float stone_half[3];
+  float max_joint_vel;
+} as_sim_t;
+
+/* Task constants (allsteps_env.py:29-60; allsteps_env_cfg.py:54-234). */
+typedef struct {
+  int32_t num_steps;
+  float step_radius;
+  int32_t stop_frames;
+  float eps;
+  float alive, energy, action, joint_limit, death, dof_vel_scale, fall_abs;
+  float step_dt;
+  int32_t max_episode_length;
+  int32_t max_curriculum;
+  int32_t curriculum_threshold;
+  float term_curriculum[10];
+  float gain_curriculum[10];
+  float init_root[3];
+  float init_q[21];
+  int32_t right_idx[9], left_idx[9], neg_idx[2];
+  float noise_lo, noise_hi, clip_lo, clip_hi;
+} as_task_t;
+
+/* Per-env state: structure of arrays, field-major / env-minor ([field][num_envs]), device memory,
+ * caller-owned.  These are the ArticulationData views of the reference:
+ *   root_pos/root_quat  = root_state_w[:, 0:7]  (root link frame, quat w,x,y,z)
+ *   root_lin/root_ang   = root_state_w[:, 7:13] (root link COM velocity, world)
+ *   q / qd              = joint_pos / joint_vel (cfg dof order)
+ *   body_pos            = body_pos_w[:, {torso, right_foot, left_foot}]
+ * and the AllstepsEnv task buffers (allsteps_env.py:66-96). */
+typedef struct {
+  float* root_pos;      /* [3][n] */
+  float* root_quat;     /* [4][n] */
+  float* root_lin;      /* [3][n] */
+  float* root_ang;      /* [3][n] */
+  float* q;             /* [21][n] */
+  float* qd;            /* [21][n] */
+  float* stones;        /* [20*3][n]  steps_pos, env-local frame (env origin = 0) */
+  float* pot;           /* [n] potentials */
+  float* old_pot;       /* [n] old_potentials */
+  float* foot_contact;  /* [2][n] */
+  float* body_pos;      /* [9][n] */
+  int32_t* idx;         /* [n] curr_target_index */
+  int32_t* prev;        /* [n] */
+  int32_t* next;        /* [n] */
+  int32_t* count;       /* [n] target_reach_count */
+  int32_t* swing;       /* [n] swing_leg */
+  int32_t* ep_len;      /* [n] episode_length_buf */
+  uint32_t* episode;    /* [n] reset counter: Philox stream of the reset draws */
+  uint32_t* contact_mask; /* [2][n] per-foot bitmask of stones with force > eps, last substep */
+  int32_t* curriculum;  /* [1] */
+} as_state_t;
+
+typedef struct as_env as_env_t;
+
+/* Create a handle for `num_envs` envs on HIP device `device`.  `env_id_offset` is this shard's
+ * first global env id (Philox stream = (seed, env_id_offset + e, episode)), so a sharded run is
+ * bit-identical to an unsharded one.  The state pointers are stored, not copied. */
+int as_create(int32_t num_envs, const as_model_t* model_host, const as_sim_t* sim_host,
+              const as_task_t* task_host, const as_state_t* state, uint64_t seed, int32_t device,
+              int64_t env_id_offset, as_env_t** out);
+int as_destroy(as_env_t* env);
+
+/* DirectRLEnv.reset (direct_rl_env.py:256-294): _reset_idx(all) -> FK -> observations. */
+int as_reset_all(as_env_t* env, float* obs, const float* reset_draws, void* stream);
+
+/* DirectRLEnv.step (direct_rl_env.py:296-383) for all envs: actions [n][21] (any range, clamped
+ * to [-1,1] inside) -> obs [n][59], reward [n], terminated [n], truncated [n] (uint8 0/1).
+ * reset_draws: NULL (Philox) or [n][22] U[0,1) draws (mirror, 21 joint-noise) for envs that reset
+ * this step -- the reference's torch.rand(K) / rand(K,21) (allsteps_env.py:518,542). */
+int as_step(as_env_t* env, const float* actions, float* obs, float* reward, uint8_t* terminated,
+            uint8_t* truncated, const float* reset_draws, void* stream);
+
+/* Task logic only (the post-physics half of as_step): body_pos / contact_mask are taken from the
+ * state as the caller wrote them -- the operator a task-logic golden replay drives. */
+int as_task_step(as_env_t* env, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                 uint8_t* truncated, const float* reset_draws, void* stream);
+
+/* Re-seed the Philox reset-draw stream (DirectRLEnv.seed / reset(seed=...)). */
+int as_set_seed(as_env_t* env, uint64_t seed);
+
+/* Physics only (decimation substeps, no task logic): for known-answer tests and profiling. */
+int as_physics_step(as_env_t* env, const float* actions, void* stream);
+
+/* _generate_foot_steps_allsteps (allsteps_env.py:125-174) on the device at curriculum `level`;
+ * draws: [5][n][20] U[0,1) (NULL = Philox stream (seed, env, 0xF007)). Writes state->stones. */
+int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* stream);
+
+/* Per-launch timing: record HIP events around the step kernel (k_step) and the observation
+ * kernel (k_obs) of the next `max_launches` calls on their own stream; as_profile_read
+ * synchronises on the last event and returns the summed durations (ms) and the launch count. */
+int as_profile(as_env_t* env, int32_t max_launches);
+int as_profile_read(as_env_t* env, double* step_kernel_ms, double* obs_kernel_ms, int32_t* launches);
+
+/* Device counters of the last step: [0] = any env reset, [1] = sum of curr_target_index. */
+int as_step_counters(as_env_t* env, const int32_t** counters_dev);
+int as_get_curriculum_host(as_env_t* env, int32_t* level_host); /* synchronises the stream */
+
+int as_abi_version(void);
+const char* as_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -266,6 +266,13 @@ class Oracle:
                            seed, fp(obs), fp(rew), u8p(term), u8p(trunc), ip(anyr), nthreads)
         return obs, rew, term.astype(bool), trunc.astype(bool), bool(anyr[0])
 
+    def physics_step(self, st: OracleState, actions: np.ndarray):
+        """Physics only (decimation substeps), no task logic: for known-answer tests."""
+        a = np.clip(np.ascontiguousarray(actions, np.float32), -1, 1)
+        for e in range(st.n):
+            row = np.ascontiguousarray(a[e])
+            self.L.or_physics_step(C.byref(self.model), C.byref(self.sim), C.byref(self.task), st.ptr, e, fp(row))
+
     def reset_all(self, st: OracleState, seed: int = 42, reset_draws=None):
         obs = np.zeros((st.n, 59), np.float32)
         rd = fp(np.ascontiguousarray(reset_draws, np.float32)) if reset_draws is not None else None

@@ -1,0 +1,106 @@
+"""C-ABI checks that need no GPU: the library loads, exports every entry point include/allsteps.h
+declares, the ctypes structs match the header's field lists, and errors surface as exceptions."""
+
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "allsteps.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(as_\w+)\(", src, re.M)))
+
+
+def test_header_declares_abi():
+    fns = _declared_functions()
+    assert "as_create" in fns and "as_step" in fns and len(fns) >= 12
+
+
+def test_library_exports_every_declared_symbol():
+    from allsteps_isaaclab_amd import _native
+
+    L = _native.load()
+    for fn in _declared_functions():
+        assert hasattr(L, fn), f"{fn} declared in allsteps.h but not exported"
+    assert set(_native.EXPORTED_SYMBOLS) == set(_declared_functions())
+    assert L.as_abi_version() == _native.ABI_VERSION
+
+
+def _struct_fields(name):
+    src = open(HEADER).read()
+    m = re.search(r"typedef struct \{([^{}]*)\}\s*" + name + ";", src, re.S)
+    body = re.sub(r"/\*.*?\*/", "", m.group(1), flags=re.S)
+    names = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        for part in decl.split(","):
+            nm = re.findall(r"\*?\s*(\w+)\s*(?:\[[^\]]*\])*\s*$", part.strip())
+            names.append(nm[0])
+    return names
+
+
+@pytest.mark.parametrize("cname,pyname", [("as_model_t", "AsModel"), ("as_sim_t", "AsSim"),
+                                          ("as_task_t", "AsTask"), ("as_state_t", "AsState")])
+def test_ctypes_structs_match_header(cname, pyname):
+    from allsteps_isaaclab_amd import _native
+
+    py = [f[0] for f in getattr(_native, pyname)._fields_]
+    assert py == _struct_fields(cname)
+
+
+def test_model_struct_size_matches_c():
+    """sizeof(as_model_t) etc. via a tiny C program compiled against the header."""
+    import subprocess
+    import tempfile
+
+    from allsteps_isaaclab_amd import _native
+
+    prog = r"""
+#include <stdio.h>
+#include "allsteps.h"
+int main(void){printf("%zu %zu %zu %zu\n", sizeof(as_model_t), sizeof(as_sim_t), sizeof(as_task_t), sizeof(as_state_t));return 0;}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "s.c")
+        open(c, "w").write(prog)
+        exe = os.path.join(d, "s")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    sizes = [C.sizeof(_native.AsModel), C.sizeof(_native.AsSim), C.sizeof(_native.AsTask), C.sizeof(_native.AsState)]
+    assert [int(x) for x in out] == sizes
+
+
+def test_create_without_device_fails_loudly():
+    """No silent CPU fallback: without a GPU the product path raises."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from allsteps_isaaclab_amd import _native
+    from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv
+    from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
+
+    cfg = AllstepsEnvCfg()
+    cfg.scene.num_envs = 4
+    cfg.sim.device = "cpu"
+    with pytest.raises(_native.NativeError):
+        AllstepsEnv(cfg)
+
+
+def test_null_arguments_return_error():
+    from allsteps_isaaclab_amd import _native
+
+    L = _native.load()
+    rc = L.as_step(None, None, None, None, None, None, None, None)
+    assert rc == -1
+    assert b"null" in L.as_last_error()
+    h = C.c_void_p()
+    assert L.as_create(0, None, None, None, None, 0, 0, 0, C.byref(h)) == -1
