@@ -22,7 +22,7 @@ ABI_VERSION = 1
 EXPORTED_SYMBOLS = [
     "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
-    "as_set_seed", "as_profile", "as_profile_read",
+    "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps",
 ]
 
 
@@ -108,6 +108,7 @@ def load() -> C.CDLL:
     L.as_task_step.argtypes = [V, V, V, V, V, V, V, V]
     L.as_set_seed.argtypes = [V, U64]
     L.as_profile.argtypes = [V, I32]
+    L.as_debug_stamps.argtypes = [V, V]
     L.as_profile_read.argtypes = [V, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(I32)]
     L.as_generate_stones.argtypes = [V, I32, V, V]
     L.as_step_counters.argtypes = [V, C.POINTER(V)]
@@ -279,6 +280,9 @@ class NativeEnv:
         a, b, k = C.c_double(), C.c_double(), C.c_int32()
         check(self.L.as_profile_read(self.h, C.byref(a), C.byref(b), C.byref(k)), "as_profile_read")
         return a.value, b.value, k.value
+
+    def debug_stamps(self, buf):
+        check(self.L.as_debug_stamps(self.h, None if buf is None else buf.data_ptr()), "as_debug_stamps")
 
     def counters_ptr(self) -> int:
         p = C.c_void_p()

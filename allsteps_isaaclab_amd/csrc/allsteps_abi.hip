@@ -35,8 +35,10 @@ struct as_env {
   as::Consts* consts_dev;
   int32_t* counters_dev;
   int32_t num_steps;
+  int32_t nv;
   // optional per-launch timing (as_profile): event triples around k_step / k_obs
   std::vector<hipEvent_t> ev;
+  unsigned long long* stamps = nullptr;  // diagnostic (as_debug_stamps)
   int32_t prof_cap = 0, prof_n = 0;
 };
 
@@ -96,6 +98,13 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
     int li = model->cfg_dof_link[k];
     if (li < 1 || li >= model->num_links) return fail(AS_ERR_INVALID, "as_create: cfg_dof_link");
   }
+  for (int l = 0; l < model->num_links; ++l) {
+    uint32_t mask = 0x3Fu;
+    for (int i = l; i > 0; i = model->parent[i]) mask |= 1u << (6 + i - 1);
+    h.ancmask[l] = mask;
+  }
+  if (!as::step_supported_nv(h.nv))
+    return fail(AS_ERR_INVALID, "as_create: no k_step instantiation for " + std::to_string(h.nv) + " dofs");
 
   as_env* env = new as_env();
   env->n = num_envs;
@@ -104,6 +113,7 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   env->env_offset = env_id_offset;
   env->st = *state;
   env->num_steps = task->num_steps;
+  env->nv = h.nv;
   if (hipMalloc(&env->consts_dev, sizeof(as::Consts)) != hipSuccess ||
       hipMalloc(&env->counters_dev, 4 * sizeof(int32_t)) != hipSuccess) {
     delete env;
@@ -142,9 +152,10 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   a.counters = env->counters_dev;
   a.seed = env->seed;
   a.env_offset = env->env_offset;
+  a.stamps = env->stamps;
   const bool prof = env->prof_n < env->prof_cap;
   if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n], s));
-  HIP_TRY(as::launch_step(a, s));
+  HIP_TRY(as::launch_step(a, env->nv, s));
   if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 1], s));
   if (mode == as::kModePhysics) {
     if (prof) {
@@ -164,6 +175,12 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
     HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 2], s));
     ++env->prof_n;
   }
+  return AS_OK;
+}
+
+int as_debug_stamps(as_env_t* env, uint64_t* stamps_dev) {
+  if (!env) return fail(AS_ERR_INVALID, "as_debug_stamps: null handle");
+  env->stamps = reinterpret_cast<unsigned long long*>(stamps_dev);
   return AS_OK;
 }
 

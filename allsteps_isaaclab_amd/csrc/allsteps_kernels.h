@@ -24,6 +24,7 @@ struct Consts {
   int32_t depth[kMaxLinks];
   int32_t nchild[kMaxLinks];
   int32_t child[kMaxLinks][kMaxChildren];  // descending link index
+  uint32_t ancmask[kMaxLinks];             // dofs on the path root..link (root dofs 0-5 always set)
 };
 
 struct StepArgs {
@@ -39,6 +40,13 @@ struct StepArgs {
   int32_t* counters;  // [0] any reset, [1] sum of curr_target_index (zeroed before the launch)
   uint64_t seed;
   int64_t env_offset;
+  unsigned long long* stamps;  // diagnostic phase timing (s_memtime deltas summed over waves) or null
+};
+
+// phase ids of the diagnostic stamps (as_debug_stamps)
+enum {
+  kStLoad = 0, kStFK, kStLinkQ, kStDyn, kStChol, kStSolve, kStCollide, kStRows, kStWsolve, kStPGS,
+  kStIntegrate, kStTask, kStReset, kStStore, kNumStamps
 };
 
 struct ObsArgs {
@@ -59,7 +67,8 @@ struct StonesArgs {
   int64_t env_offset;
 };
 
-hipError_t launch_step(const StepArgs& a, hipStream_t stream);
+bool step_supported_nv(int nv);
+hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream);
 hipError_t launch_obs(const ObsArgs& a, hipStream_t stream);
 hipError_t launch_stones(const StonesArgs& a, hipStream_t stream);
 size_t step_lds_bytes();

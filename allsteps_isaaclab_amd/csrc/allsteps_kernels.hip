@@ -1,20 +1,23 @@
 // allsteps_kernels.hip -- MI355X (gfx950) step kernels for Allsteps-v0.
 //
 // k_step (K1): one env per 32-lane group (two envs per 64-lane wave, one wave per workgroup).
-//   For each env: load the SoA state once, run `decimation` physics substeps
-//   (FK -> RNEA bias -> CRBA inertia -> Cholesky -> unconstrained velocity -> stone contacts +
-//   joint limits -> projected Gauss-Seidel -> semi-implicit integration), then the task epilogue of
-//   DirectRLEnv.step (direct_rl_env.py:349-364): episode counter, foot-state tick #1, targets,
-//   potentials, dones, rewards, and -- for envs that are done -- the in-kernel reset
-//   (allsteps_env.py:469-565) with Philox draws and an FK of the new pose.  All per-env scratch
-//   lives in LDS; the state is read and written exactly once per env step.
+//   For each env: load the SoA state once, run `decimation` physics substeps, then the task
+//   epilogue of DirectRLEnv.step (direct_rl_env.py:349-364): episode counter, foot-state tick #1,
+//   targets, potentials, dones, rewards and -- for envs that are done -- the in-kernel reset
+//   (allsteps_env.py:469-565) with Philox draws and an FK of the new pose.  The state is read and
+//   written exactly once per env step.
+//   One substep (oracle/physics.c is its serial restatement):
+//     FK (level-synchronous, lanes = links) -> link inertias / motion subspaces -> RNEA bias and
+//     composite inertias (lanes = links) -> joint-space inertia rows H_j (lane = dof j, from the
+//     ancestor bitmasks) -> H^-1 by in-register Gauss-Jordan (one row per lane, pivot row broadcast
+//     through LDS) -> u* = u + dt H^-1 (tau - C) -> stone contacts + joint-limit rows ->
+//     W = H^-1 J^T (lane = dof, J and W columns in VGPRs) -> projected Gauss-Seidel on the impulses
+//     with DPP cross-lane reductions -> semi-implicit integration.
 // k_obs (K2): one env per lane.  If any env reset this step (device counter written by K1), the
 //   second _compute_useful_values over ALL envs (allsteps_env.py:567: foot-state tick #2 with the
 //   stale last-substep contacts, targets, potentials) and the curriculum gate
 //   (allsteps_env.py:471-479); then the observation (allsteps_env.py:326-345).
 // k_stones: _generate_foot_steps_allsteps (allsteps_env.py:125-174), one env per lane.
-//
-// The algorithm is specified in DESIGN.md §Dynamics; oracle/physics.c is its serial restatement.
 #include <hip/hip_runtime.h>
 
 #include "../../include/allsteps.h"
@@ -23,11 +26,10 @@
 
 namespace as {
 
-constexpr int G = 32;              // lanes per env
-constexpr int EPB = 2;             // envs per 64-lane workgroup
-constexpr int LMAX = kMaxLinks;    // links (walker: 22)
-constexpr int NVMAX = 6 + LMAX - 1;// generalized velocities
-constexpr int LDH = 31;            // odd row stride: conflict-free column access
+constexpr int G = 32;               // lanes per env
+constexpr int EPB = 2;              // envs per 64-lane workgroup
+constexpr int LMAX = kMaxLinks;     // links (walker: 22)
+constexpr int NVMAX = 6 + LMAX - 1; // generalized velocities
 constexpr int MAXC = AS_MAX_CONTACTS;
 constexpr int MAXR = AS_MAX_ROWS;
 constexpr int NST = AS_NUM_STONES;
@@ -35,39 +37,58 @@ constexpr int GOLDEN_ITERS = 14;
 
 static_assert(NVMAX <= G, "one lane per generalized velocity");
 static_assert(LMAX <= G, "one lane per link");
+static_assert(MAXR <= G, "one row per lane in the row builders");
 
 // ------------------------------------------------------------------------------------------------
-// per-env LDS scratch
-struct EnvS {
-  float R[LMAX][9];
-  float p[LMAX][3];
+// per-env LDS scratch.  Occupancy at 4096 envs is set by LDS: two envs per 64-lane workgroup must
+// stay <= 20 KB so that 8 workgroups (2 waves/SIMD) fit a CU and 4096 envs run in one round.  The
+// phase-local arrays therefore share one union: FK (Rl) -> dynamics (c, Ib, Ic, Fh, V, A, F) ->
+// sweep (piv) -> constraint rows (Jm, Wm); each phase ends before the next one writes.
+constexpr int LDJ = 28;               // J / W row stride (>= NV = 27)
+struct DynScratch {
   float c[LMAX][3];
-  float Rl[LMAX][12];   // local joint transform (R 9, p 3)
   float Ib[LMAX][10];
   float Ic[LMAX][10];
-  float S[NVMAX][6];
+  float Fh[NVMAX][6];   // Ic_link(j) S_j (CRBA column forces)
   float V[LMAX][6];
   float A[LMAX][6];
   float F[LMAX][6];
-  float H[NVMAX * LDH];
-  float J[MAXR * LDH];
-  float W[MAXR * LDH];
-  float rtarget[MAXR], rAd[MAXR], rlam[MAXR];
-  int rtype[MAXR];
+};
+struct ConScratch {
+  float Jm[MAXR][LDJ];  // J rows (lane = dof column)
+  float Wm[MAXR][LDJ];  // W = H^-1 J^T rows (lane = dof column)
+};
+union PhaseScratch {
+  float Rl[LMAX][12];   // FK: local joint transforms (R 9, p 3)
+  DynScratch d;
+  float piv[2][32];     // sweep: pivot row (double-buffered)
+  ConScratch k;
+};
+
+struct EnvS {
+  float R[LMAX][9];
+  float p[LMAX][3];
+  float c0[3];          // root COM (relative), kept past the dynamics phase for integration
+  float S[NVMAX][6];
+  float b[32];          // tau - C
+  PhaseScratch x;
+  float rlam[MAXR];     // PGS impulses
+  alignas(16) float rmeta[MAXR][4]; // per row: 1/A_rr, target, type (0 normal, 1 tangent, 2 limit)
+  float rf6[MAXR][6];   // contact rows: spatial force direction [P x d; d]
+  int rlink[MAXR];      // contact link, or -1 - dof for a limit row
+  float rsign[MAXR];
+  float lamn[MAXC];     // normal impulses of the last PGS sweep (contact flags)
   float cpt[MAXC][3], cn[MAXC][3], csep[MAXC];
   int clink[MAXC], cstone[MAXC], cfoot[MAXC];
-  float u[NVMAX], b[NVMAX], acc[NVMAX];
+  float u[NVMAX];
   float qi[LMAX];       // hinge angles, link order (link i -> qi[i-1])
   float tau[LMAX];
   float act[AS_ACT_DIM];
   float stones[NST * 3];
   float root_pos[3], root_quat[4];
   int cand[NST];
-  int pair_ok[64];
-  int ncand, ncontact, nrow, npair;
+  int ncand, ncontact, nrow;
   uint32_t mask[2];
-  // task scratch
-  float red[4];
 };
 
 struct Smem {
@@ -75,12 +96,50 @@ struct Smem {
   int maxrow;
 };
 
+// ------------------------------------------------------------------------------------------------
+// cross-lane helpers
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+
+// Sum over the 32 lanes of this env's half-wave: DPP butterfly inside each 16-lane row
+// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the two row sums of each half
+// through SGPRs.  Every lane of a half gets the bit-identical value.
+__device__ __forceinline__ float half_sum(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0x140>(v);
+  float a = readlane_f(v, 0) + readlane_f(v, 16);
+  float b = readlane_f(v, 32) + readlane_f(v, 48);
+  return (threadIdx.x & 32) ? b : a;
+}
+
 __device__ __forceinline__ float wave32_sum(float v) {
-  // butterfly over the 32 lanes of this env group (xor < 32 stays inside the half-wave)
 #pragma unroll
   for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// diagnostic phase stamps: lane 0 of each wave adds s_memtime deltas (off when p == nullptr)
+struct Stamp {
+  unsigned long long* p;
+  unsigned long long t;
+  __device__ void start() {
+    if (p) t = __builtin_amdgcn_s_memtime();
+  }
+  __device__ void mark(int k) {
+    if (p) {
+      unsigned long long now = __builtin_amdgcn_s_memtime();
+      if ((threadIdx.x & 63) == 0) atomicAdd(p + k, now - t);
+      t = now;
+    }
+  }
+};
 
 // ------------------------------------------------------------------------------------------------
 // FK: local joint transforms (parallel), then level-synchronous composition.
@@ -95,11 +154,11 @@ __device__ void fk(const Consts& K, EnvS& s, int lane) {
       float Roff[9], Rj[9], Ro[3], t[3], tmp[3];
       quat_to_mat(m.offset_quat[i], Roff);
       axis_angle_mat(m.axis[i], s.qi[i - 1], Rj);
-      matmul3(Roff, Rj, s.Rl[i]);
+      matmul3(Roff, Rj, s.x.Rl[i]);
       matvec3(Rj, m.anchor[i], Ro);
       for (int k = 0; k < 3; ++k) t[k] = m.anchor[i][k] - Ro[k];
       matvec3(Roff, t, tmp);
-      for (int k = 0; k < 3; ++k) s.Rl[i][9 + k] = tmp[k] + m.offset_pos[i][k];
+      for (int k = 0; k < 3; ++k) s.x.Rl[i][9 + k] = tmp[k] + m.offset_pos[i][k];
     }
   }
   __syncthreads();
@@ -107,9 +166,9 @@ __device__ void fk(const Consts& K, EnvS& s, int lane) {
     for (int i = lane; i < nl; i += G) {
       if (K.depth[i] != d) continue;
       int pa = m.parent[i];
-      matmul3(s.R[pa], s.Rl[i], s.R[i]);
+      matmul3(s.R[pa], s.x.Rl[i], s.R[i]);
       float wp[3];
-      matvec3(s.R[pa], s.Rl[i] + 9, wp);
+      matvec3(s.R[pa], s.x.Rl[i] + 9, wp);
       for (int k = 0; k < 3; ++k) s.p[i][k] = s.p[pa][k] + wp[k];
     }
     __syncthreads();
@@ -125,7 +184,7 @@ __device__ void link_quantities(const Consts& K, EnvS& s, int lane) {
     float cw[3];
     matvec3(R, m.com[i], cw);
     float c[3] = {s.p[i][0] + cw[0], s.p[i][1] + cw[1], s.p[i][2] + cw[2]};
-    s.c[i][0] = c[0]; s.c[i][1] = c[1]; s.c[i][2] = c[2];
+    s.x.d.c[i][0] = c[0]; s.x.d.c[i][1] = c[1]; s.x.d.c[i][2] = c[2];
     const float* Il = m.inertia[i];
     float Im[9] = {Il[0], Il[3], Il[4], Il[3], Il[1], Il[5], Il[4], Il[5], Il[2]};
     float Rt[9] = {R[0], R[3], R[6], R[1], R[4], R[7], R[2], R[5], R[8]};
@@ -133,7 +192,7 @@ __device__ void link_quantities(const Consts& K, EnvS& s, int lane) {
     matmul3(R, Im, T);
     matmul3(T, Rt, Iw);
     float mass = m.mass[i], cc = dot3(c, c);
-    float* B = s.Ib[i];
+    float* B = s.x.d.Ib[i];
     B[0] = mass;
     B[1] = mass * c[0]; B[2] = mass * c[1]; B[3] = mass * c[2];
     B[4] = Iw[0] + mass * (cc - c[0] * c[0]);
@@ -142,7 +201,7 @@ __device__ void link_quantities(const Consts& K, EnvS& s, int lane) {
     B[7] = Iw[1] - mass * c[0] * c[1];
     B[8] = Iw[2] - mass * c[0] * c[2];
     B[9] = Iw[5] - mass * c[1] * c[2];
-    for (int k = 0; k < 10; ++k) s.Ic[i][k] = B[k];
+    for (int k = 0; k < 10; ++k) s.x.d.Ic[i][k] = B[k];
     if (i > 0) {
       float a[3], Ro[3], o[3];
       matvec3(R, m.axis[i], a);
@@ -154,6 +213,7 @@ __device__ void link_quantities(const Consts& K, EnvS& s, int lane) {
     }
   }
   __syncthreads();
+  if (lane < 3) s.c0[lane] = s.x.d.c[0][lane];
   if (lane < 6) {  // root columns need c0
     float* S = s.S[lane];
     for (int j = 0; j < 6; ++j) S[j] = 0.f;
@@ -164,27 +224,27 @@ __device__ void link_quantities(const Consts& K, EnvS& s, int lane) {
       float e[3] = {0.f, 0.f, 0.f};
       e[k] = 1.f;
       S[k] = 1.f;
-      cross3(s.c[0], e, S + 3);
+      cross3(s.x.d.c[0], e, S + 3);
     }
   }
   __syncthreads();
 }
 
-// Velocities, bias accelerations (qdd = 0), RNEA forces, composite inertias, C, H.
-__device__ void dynamics(const Consts& K, EnvS& s, int lane, float gravity) {
+// Velocities, bias accelerations (qdd = 0), RNEA forces and composite inertias (lanes = links);
+// then per dof j: C_j, b_j = tau_j - C_j (returned), Fh_j = Ic_link(j) S_j (LDS).
+__device__ float dynamics(const Consts& K, EnvS& s, int lane, float gravity) {
   const as_model_t& m = K.model;
   const int nl = m.num_links, nv = K.nv;
-  // level 0: root
   if (lane == 0) {
     const float* u = s.u;
     float wxc[3], vxw[3];
-    cross3(s.c[0], u + 3, wxc);
+    cross3(s.x.d.c[0], u + 3, wxc);
     cross3(u, u + 3, vxw);
     for (int k = 0; k < 3; ++k) {
-      s.V[0][k] = u[3 + k];
-      s.V[0][3 + k] = u[k] + wxc[k];
-      s.A[0][k] = 0.f;
-      s.A[0][3 + k] = vxw[k];
+      s.x.d.V[0][k] = u[3 + k];
+      s.x.d.V[0][3 + k] = u[k] + wxc[k];
+      s.x.d.A[0][k] = 0.f;
+      s.x.d.A[0][3 + k] = vxw[k];
     }
   }
   __syncthreads();
@@ -197,24 +257,24 @@ __device__ void dynamics(const Consts& K, EnvS& s, int lane, float gravity) {
       float Sq[6], cr[6];
       for (int k = 0; k < 6; ++k) {
         Sq[k] = S[k] * qd;
-        s.V[i][k] = s.V[pa][k] + Sq[k];
+        s.x.d.V[i][k] = s.x.d.V[pa][k] + Sq[k];
       }
-      crm(s.V[i], Sq, cr);
-      for (int k = 0; k < 6; ++k) s.A[i][k] = s.A[pa][k] + cr[k];
+      crm(s.x.d.V[i], Sq, cr);
+      for (int k = 0; k < 6; ++k) s.x.d.A[i][k] = s.x.d.A[pa][k] + cr[k];
     }
     __syncthreads();
   }
   for (int i = lane; i < nl; i += G) {
     float IA[6], IV[6], x[6];
-    inertia_mul(s.Ib[i], s.A[i], IA);
-    inertia_mul(s.Ib[i], s.V[i], IV);
-    crf(s.V[i], IV, x);
+    inertia_mul(s.x.d.Ib[i], s.x.d.A[i], IA);
+    inertia_mul(s.x.d.Ib[i], s.x.d.V[i], IV);
+    crf(s.x.d.V[i], IV, x);
     float mg[3] = {0.f, 0.f, m.mass[i] * gravity};
     float cxmg[3];
-    cross3(s.c[i], mg, cxmg);
+    cross3(s.x.d.c[i], mg, cxmg);
     for (int k = 0; k < 3; ++k) {
-      s.F[i][k] = IA[k] + x[k] - cxmg[k];
-      s.F[i][3 + k] = IA[3 + k] + x[3 + k] - mg[k];
+      s.x.d.F[i][k] = IA[k] + x[k] - cxmg[k];
+      s.x.d.F[i][3 + k] = IA[3 + k] + x[3 + k] - mg[k];
     }
   }
   __syncthreads();
@@ -224,93 +284,86 @@ __device__ void dynamics(const Consts& K, EnvS& s, int lane, float gravity) {
       if (K.depth[i] != d) continue;
       for (int t = 0; t < K.nchild[i]; ++t) {
         int ch = K.child[i][t];
-        for (int k = 0; k < 6; ++k) s.F[i][k] += s.F[ch][k];
-        for (int k = 0; k < 10; ++k) s.Ic[i][k] += s.Ic[ch][k];
+        for (int k = 0; k < 6; ++k) s.x.d.F[i][k] += s.x.d.F[ch][k];
+        for (int k = 0; k < 10; ++k) s.x.d.Ic[i][k] += s.x.d.Ic[ch][k];
       }
     }
     __syncthreads();
   }
-  // bias C, b = tau - C, and the joint-space inertia rows (lane = dof j)
+  float bj = 0.f;
   if (lane < nv) {
     const int j = lane;
     const int link = j < 6 ? 0 : j - 5;
-    float Cj = dot6(s.S[j], s.F[link]);
-    s.b[j] = (j < 6 ? 0.f : s.tau[j - 6]) - Cj;
-    float Fj[6];
-    inertia_mul(s.Ic[link], s.S[j], Fj);
-    float* Hrow = s.H + j * LDH;
-    for (int k = 0; k <= j; ++k) Hrow[k] = 0.f;
-    for (int l = link; l > 0; l = m.parent[l]) {
-      int k = 6 + l - 1;
-      if (k <= j) Hrow[k] = dot6(s.S[k], Fj);
-    }
-    for (int k = 0; k < 6; ++k)
-      if (k <= j) Hrow[k] = dot6(s.S[k], Fj);
-    if (j >= 6) Hrow[j] += m.armature[j - 5];
+    float Cj = dot6(s.S[j], s.x.d.F[link]);
+    bj = (j < 6 ? 0.f : s.tau[j - 6]) - Cj;
+    s.b[j] = bj;
+    inertia_mul(s.x.d.Ic[link], s.S[j], s.x.d.Fh[j]);
+  } else if (lane < 32) {
+    s.b[lane] = 0.f;
   }
   __syncthreads();
+  return bj;
 }
 
-// Left-looking Cholesky H = L L^T in place (lower triangle), lanes over rows.
-__device__ void cholesky(const Consts& K, EnvS& s, int lane) {
-  const int nv = K.nv;
-  float* H = s.H;
-  for (int j = 0; j < nv; ++j) {
-    if (lane == j) {
-      float acc = H[j * LDH + j];
-      for (int k = 0; k < j; ++k) acc -= H[j * LDH + k] * H[j * LDH + k];
-      H[j * LDH + j] = sqrtf(acc > 1e-12f ? acc : 1e-12f);
-    }
-    __syncthreads();
-    if (lane > j && lane < nv) {
-      const int i = lane;
-      float t = H[i * LDH + j];
-      for (int k = 0; k < j; ++k) t -= H[i * LDH + k] * H[j * LDH + k];
-      H[i * LDH + j] = t * (1.0f / H[j * LDH + j]);
-    }
-    __syncthreads();
-  }
-}
-
-// Solve H x = b for one RHS held in LDS (x may alias b), column-oriented, lanes over rows.
-__device__ void chol_solve_lds(const Consts& K, EnvS& s, int lane, float* b, float* x) {
-  const int nv = K.nv;
-  const float* L = s.H;
-  for (int j = 0; j < nv; ++j) {  // forward: y_j = b_j / L_jj ; b_i -= L_ij y_j
-    float yj = b[j] / L[j * LDH + j];
-    __syncthreads();
-    if (lane == j) b[j] = yj;
-    if (lane > j && lane < nv) b[lane] -= L[lane * LDH + j] * yj;
-    __syncthreads();
-  }
-  for (int j = nv - 1; j >= 0; --j) {  // backward: x_j = y_j / L_jj ; y_i -= L_ji x_j
-    float xj = b[j] / L[j * LDH + j];
-    __syncthreads();
-    if (lane == j) x[j] = xj;
-    if (lane < j) b[lane] -= L[j * LDH + lane] * xj;
-    __syncthreads();
-  }
-}
-
-// Per-lane serial solve of H w = J_r (row r), reading L (broadcast) and writing W_r.
-__device__ void chol_solve_row(int nv, const float* L, const float* Jr, float* Wr) {
-  float y[NVMAX];
+// Row j of the joint-space inertia H (lane j):
+//   H_jk = S_k . (Ic_link(j) S_j)  if dof k is on the path of link(j) (k ancestor-or-self),
+//        = S_j . (Ic_link(k) S_k)  if dof j is on the path of link(k),   else 0;  + armature.
+template <int NV>
+__device__ void h_row(const Consts& K, const EnvS& s, int lane, float (&Hr)[NV]) {
+  const int j = lane < NV ? lane : 0;
+  const int lj = j < 6 ? 0 : j - 5;
+  const uint32_t anc_j = K.ancmask[lj];
+  float Sj[6], Fj[6];
 #pragma unroll
-  for (int i = 0; i < NVMAX; ++i) {
-    if (i < nv) {
-      float acc = Jr[i];
-      for (int k = 0; k < i; ++k) acc -= L[i * LDH + k] * y[k];
-      y[i] = acc / L[i * LDH + i];
+  for (int a = 0; a < 6; ++a) { Sj[a] = s.S[j][a]; Fj[a] = s.x.d.Fh[j][a]; }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int lk = k < 6 ? 0 : k - 5;
+    const bool k_on_j = (anc_j >> k) & 1u;
+    const bool j_on_k = (K.ancmask[lk] >> j) & 1u;
+    float v1 = dot6(s.S[k], Fj);
+    float v2 = dot6(Sj, s.x.d.Fh[k]);
+    float h = k_on_j ? v1 : (j_on_k ? v2 : 0.f);
+    if (k == j && j >= 6) h += K.model.armature[j - 5];
+    Hr[k] = lane < NV ? h : 0.f;
+  }
+}
+
+// In-register Gauss-Jordan inverse: lane i holds row i; pivot row j is broadcast through LDS.
+// Same operation sequence as oracle/physics.c gj_inverse.
+// H^-1 by the symmetric sweep operator (same sequence as oracle/physics.c sweep_inverse).
+// Sweep on pivot k with the pre-sweep pivot row Q (d = Q_k, r = 1/d):
+//   row k:      a_kj <- r a_kj (j != k),        a_kk <- -r
+//   row i != k: a_ij <- a_ij - (r a_ik) Q_j,    a_ik <- r a_ik
+// Every intermediate matrix is symmetric, so lane i's pivot-column entry a_ik equals Q_i: it is read
+// from the broadcast row at the lane's own index and the register row is only ever indexed by
+// compile-time constants.  The pivot loop stays rolled (the whole step must fit the I-cache).
+// After all pivots the rows hold -H^-1; the sign is folded in at the end.
+template <int NV>
+__device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NV]) {
+#pragma unroll 1
+  for (int k = 0; k < NV; ++k) {
+    float* Q = s.x.piv[k & 1];
+    if (lane == k) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) Q[j] = Hr[j];
+    }
+    __syncthreads();
+    const float d = Q[k];
+    const float r = 1.0f / d;
+    const bool piv = lane == k;
+    const float g = piv ? 0.f : (lane < NV ? Q[lane] : 0.f) * r;
+    const float alpha = piv ? r : 1.f;
+    const float c = piv ? -r : g;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float t = alpha * Hr[j] - g * Q[j];
+      Hr[j] = (j == k) ? c : t;
     }
   }
 #pragma unroll
-  for (int i = NVMAX - 1; i >= 0; --i) {
-    if (i < nv) {
-      float acc = y[i];
-      for (int k = nv - 1; k > i; --k) acc -= L[k * LDH + i] * Wr[k];
-      Wr[i] = acc / L[i * LDH + i];
-    }
-  }
+  for (int j = 0; j < NV; ++j) Hr[j] = lane < NV ? -Hr[j] : 0.f;
+  __syncthreads();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -329,35 +382,28 @@ __device__ void collide(const Consts& K, EnvS& s, int lane) {
   const int nst = K.task.num_steps;
   // broadphase: stones within 1.8 m of the root link origin
   bool isc = false;
-  float rel[3] = {0.f, 0.f, 0.f};
   if (lane < nst) {
     float o = 0.f;
     for (int k = 0; k < 3; ++k) {
-      rel[k] = s.stones[3 * lane + k] - s.root_pos[k];
-      float d = fabsf(rel[k]) - h[k];
+      float d = fabsf(s.stones[3 * lane + k] - s.root_pos[k]) - h[k];
       if (d > 0.f) o += d * d;
     }
     isc = o < 1.8f * 1.8f;
   }
-  // compact candidates in stone order (ballot over this env's half-wave)
   uint64_t bal = __ballot(isc);
   const int half = (threadIdx.x >> 5) & 1;
   uint32_t mine = (uint32_t)(bal >> (32 * half));
-  if (isc) {
-    int pos = __popc(mine & ((1u << lane) - 1u));
-    s.cand[pos] = lane;
-  }
-  if (lane == 0) { s.ncand = __popc(mine); s.ncontact = 0; }
+  if (isc) s.cand[__popc(mine & ((1u << lane) - 1u))] = lane;
+  if (lane == 0) s.ncand = __popc(mine);
   __syncthreads();
   const int ncand = s.ncand, ng = m.num_geoms;
   const int npairs = ng * ncand;
-  // pass over pairs in (geom, stone) order, 32 at a time; each pair emits 0..3 contacts
   int base = 0;
   for (int p0 = 0; p0 < npairs; p0 += G) {
     int p = p0 + lane;
     int cnt = 0;
     int link = 0, stone = 0, foot = -1;
-    float P[3][3], N[3][3], SEP[3], rr = 0.f;
+    float P0[3], N0[3], P1[3], N1[3], P2[3], N2[3], SEP0 = 0.f, SEP1 = 0.f, SEP2 = 0.f, rr = 0.f;
     if (p < npairs) {
       int g = p / ncand, st = s.cand[p % ncand];
       link = m.geom_link[g]; stone = st; foot = m.geom_foot[g];
@@ -373,8 +419,8 @@ __device__ void collide(const Consts& K, EnvS& s, int lane) {
       if (m.geom_type[g] == 0) {
         float sd = sd_box(a, c, h, nr) - r;
         if (sd < K.sim.margin) {
-          for (int k = 0; k < 3; ++k) { P[0][k] = a[k]; N[0][k] = nr[k]; }
-          SEP[0] = sd;
+          for (int k = 0; k < 3; ++k) { P0[k] = a[k]; N0[k] = nr[k]; }
+          SEP0 = sd;
           cnt = 1;
         }
       } else {
@@ -388,40 +434,42 @@ __device__ void collide(const Consts& K, EnvS& s, int lane) {
           const float gr = 0.6180339887f;
           float lo = 0.f, hi = 1.f;
           float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
-          float P1[3], P2[3];
-          for (int k = 0; k < 3; ++k) { P1[k] = a[k] + x1 * (bb[k] - a[k]); P2[k] = a[k] + x2 * (bb[k] - a[k]); }
-          float f1 = sd_box(P1, c, h, tn), f2 = sd_box(P2, c, h, tn);
+          float Q1[3], Q2[3];
+          for (int k = 0; k < 3; ++k) { Q1[k] = a[k] + x1 * (bb[k] - a[k]); Q2[k] = a[k] + x2 * (bb[k] - a[k]); }
+          float f1 = sd_box(Q1, c, h, tn), f2 = sd_box(Q2, c, h, tn);
+#pragma unroll 1
           for (int it = 0; it < GOLDEN_ITERS; ++it) {
             if (f1 < f2) {
               hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
-              for (int k = 0; k < 3; ++k) P1[k] = a[k] + x1 * (bb[k] - a[k]);
-              f1 = sd_box(P1, c, h, tn);
+              for (int k = 0; k < 3; ++k) Q1[k] = a[k] + x1 * (bb[k] - a[k]);
+              f1 = sd_box(Q1, c, h, tn);
             } else {
               lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
-              for (int k = 0; k < 3; ++k) P2[k] = a[k] + x2 * (bb[k] - a[k]);
-              f2 = sd_box(P2, c, h, tn);
+              for (int k = 0; k < 3; ++k) Q2[k] = a[k] + x2 * (bb[k] - a[k]);
+              f2 = sd_box(Q2, c, h, tn);
             }
           }
           float ts = 0.5f * (lo + hi), Ps[3], ns[3];
           for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (bb[k] - a[k]);
           float ss = sd_box(Ps, c, h, ns) - r;
-          if (s0 < K.sim.margin) {
-            for (int k = 0; k < 3; ++k) { P[cnt][k] = a[k]; N[cnt][k] = n0[k]; }
-            SEP[cnt++] = s0;
+          bool e0 = s0 < K.sim.margin, e1 = s1 < K.sim.margin;
+          bool es = ss < K.sim.margin && ss < fminf(s0, s1) - 0.002f;
+          // pack the emitted contacts in (t=0, t=1, t*) order into slots 0..2
+          for (int k = 0; k < 3; ++k) { P0[k] = a[k]; N0[k] = n0[k]; }
+          SEP0 = s0;
+          if (e0) {
+            for (int k = 0; k < 3; ++k) { P1[k] = bb[k]; N1[k] = n1[k]; P2[k] = Ps[k]; N2[k] = ns[k]; }
+            SEP1 = s1; SEP2 = ss;
+            if (!e1) { for (int k = 0; k < 3; ++k) { P1[k] = Ps[k]; N1[k] = ns[k]; } SEP1 = ss; }
+          } else {
+            for (int k = 0; k < 3; ++k) { P0[k] = bb[k]; N0[k] = n1[k]; P1[k] = Ps[k]; N1[k] = ns[k]; }
+            SEP0 = s1; SEP1 = ss;
+            if (!e1) { for (int k = 0; k < 3; ++k) { P0[k] = Ps[k]; N0[k] = ns[k]; } SEP0 = ss; }
           }
-          if (s1 < K.sim.margin) {
-            for (int k = 0; k < 3; ++k) { P[cnt][k] = bb[k]; N[cnt][k] = n1[k]; }
-            SEP[cnt++] = s1;
-          }
-          float smin = fminf(s0, s1);
-          if (ss < K.sim.margin && ss < smin - 0.002f) {
-            for (int k = 0; k < 3; ++k) { P[cnt][k] = Ps[k]; N[cnt][k] = ns[k]; }
-            SEP[cnt++] = ss;
-          }
+          cnt = (int)e0 + (int)e1 + (int)es;
         }
       }
     }
-    // exclusive prefix sum of cnt over the 32 lanes of this env (in pair order)
     int incl = cnt;
 #pragma unroll
     for (int o = 1; o < 32; o <<= 1) {
@@ -430,24 +478,14 @@ __device__ void collide(const Consts& K, EnvS& s, int lane) {
     }
     int total = __shfl(incl, 31, 32);
     int slot = base + incl - cnt;
-    for (int t = 0; t < cnt; ++t) emit_contact(s, slot + t, link, stone, foot, P[t], N[t], SEP[t], rr);
+    if (cnt > 0) emit_contact(s, slot, link, stone, foot, P0, N0, SEP0, rr);
+    if (cnt > 1) emit_contact(s, slot + 1, link, stone, foot, P1, N1, SEP1, rr);
+    if (cnt > 2) emit_contact(s, slot + 2, link, stone, foot, P2, N2, SEP2, rr);
     base += total;
   }
   __syncthreads();
   if (lane == 0) s.ncontact = base < MAXC ? base : MAXC;
   __syncthreads();
-}
-
-// Jacobian row of direction d at point P on link `link` (lanes are rows; serial over dofs)
-__device__ void build_contact_row(const Consts& K, const EnvS& s, int link, const float* P, const float* d,
-                                  float* Jr) {
-  const as_model_t& m = K.model;
-  float f6[6];
-  cross3(P, d, f6);
-  f6[3] = d[0]; f6[4] = d[1]; f6[5] = d[2];
-  for (int j = 0; j < K.nv; ++j) Jr[j] = 0.f;
-  for (int l = link; l > 0; l = m.parent[l]) Jr[6 + l - 1] = dot6(s.S[6 + l - 1], f6);
-  for (int k = 0; k < 6; ++k) Jr[k] = dot6(s.S[k], f6);
 }
 
 __device__ void tangents(const float* n, float* t1, float* t2) {
@@ -460,36 +498,59 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
 }
 
 // ------------------------------------------------------------------------------------------------
-__device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* mask_out) {
+template <int NV>
+__device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* mask_out, Stamp& ts) {
   const as_model_t& m = K.model;
   const float dt = K.sim.dt;
-  const int nv = K.nv, nh = m.num_hinges;
+  const int nh = m.num_hinges;
   fk(K, s, lane);
+  ts.mark(kStFK);
   link_quantities(K, s, lane);
+  ts.mark(kStLinkQ);
   dynamics(K, s, lane, K.sim.gravity);
-  cholesky(K, s, lane);
-  chol_solve_lds(K, s, lane, s.b, s.acc);
-  if (lane < nv) s.u[lane] += dt * s.acc[lane];
+  float Hr[NV];
+  h_row<NV>(K, s, lane, Hr);
+  ts.mark(kStDyn);
+  sweep_inverse<NV>(s, lane, Hr);  // Hr <- row `lane` of H^-1
+  ts.mark(kStChol);
+  // u* = u + dt H^-1 b   (b broadcast from LDS)
+  float uj = 0.f;
+  {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc += Hr[k] * s.b[k];
+    if (lane < NV) {
+      uj = s.u[lane] + dt * acc;
+      s.u[lane] = uj;
+    }
+  }
   __syncthreads();
+  ts.mark(kStSolve);
   // ---- constraints
   collide(K, s, lane);
+  ts.mark(kStCollide);
   const int nc = s.ncontact;
-  // contact rows: lane c builds the three rows of contact c
-  if (lane < nc && 3 * lane + 3 <= MAXR) {
+  if (lane < nc) {  // contact rows 3c..3c+2: normal, tangent 1, tangent 2
     float t1[3], t2[3];
     tangents(s.cn[lane], t1, t2);
     const float* dirs[3] = {s.cn[lane], t1, t2};
+    const float* P = s.cpt[lane];
+    float sp = s.csep[lane];
     for (int d = 0; d < 3; ++d) {
       int r = 3 * lane + d;
-      s.rtype[r] = d == 0 ? 0 : 1;
-      build_contact_row(K, s, s.clink[lane], s.cpt[lane], dirs[d], s.J + r * LDH);
-      float sp = s.csep[lane];
-      s.rtarget[r] = d == 0 ? (sp < 0.f ? fminf(K.sim.baumgarte * fmaxf(-sp - K.sim.slop, 0.f) / dt, K.sim.max_depen_vel)
-                                        : -sp / dt)
-                            : 0.f;
+      float* f6 = s.rf6[r];
+      cross3(P, dirs[d], f6);
+      f6[3] = dirs[d][0]; f6[4] = dirs[d][1]; f6[5] = dirs[d][2];
+      s.rlink[r] = s.clink[lane];
+      s.rsign[r] = 0.f;
+      s.rmeta[r][1] = d == 0 ? (sp < 0.f ? fminf(K.sim.baumgarte * fmaxf(-sp - K.sim.slop, 0.f) / dt,
+                                                   K.sim.max_depen_vel)
+                                         : -sp / dt)
+                             : 0.f;
+      s.rmeta[r][2] = d == 0 ? 0.f : 1.f;
     }
   }
-  int crow = 3 * nc < MAXR ? 3 * nc : MAXR;
+  const int crow = 3 * nc;
   // joint-limit rows: lane h (hinge) emits lower then upper, in hinge order
   int lo_v = 0, hi_v = 0;
   float err_lo = 0.f, err_hi = 0.f;
@@ -514,59 +575,96 @@ __device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* 
     int viol = sd == 0 ? lo_v : hi_v;
     if (!viol) continue;
     if (slot < MAXR) {
-      float* Jr = s.J + slot * LDH;
-      for (int k = 0; k < nv; ++k) Jr[k] = 0.f;
-      Jr[6 + lane] = sd == 0 ? 1.f : -1.f;
       float err = sd == 0 ? err_lo : err_hi;
-      s.rtype[slot] = 2;
-      s.rtarget[slot] = err > 0.f ? fminf(K.sim.baumgarte * err / dt, K.sim.max_depen_vel) : err / dt;
+      s.rlink[slot] = -1 - (6 + lane);
+      s.rsign[slot] = sd == 0 ? 1.f : -1.f;
+      s.rmeta[slot][1] = err > 0.f ? fminf(K.sim.baumgarte * err / dt, K.sim.max_depen_vel) : err / dt;
+      s.rmeta[slot][2] = 2.f;
     }
     ++slot;
   }
   const int nrow = crow + total < MAXR ? crow + total : MAXR;
   if (lane == 0) s.nrow = nrow;
   __syncthreads();
-  // W_r = H^-1 J_r^T and the effective masses (lanes over rows)
-  for (int r = lane; r < nrow; r += G) {
-    const float* Jr = s.J + r * LDH;
-    float* Wr = s.W + r * LDH;
-    chol_solve_row(nv, s.H, Jr, Wr);
-    float a = 0.f;
-    for (int k = 0; k < nv; ++k) a += Jr[k] * Wr[k];
-    s.rAd[r] = 1.0f / (a + 1e-9f);
-    s.rlam[r] = 0.f;
-  }
   if (threadIdx.x == 0) sm.maxrow = max(sm.env[0].nrow, sm.env[1].nrow);
+  ts.mark(kStRows);
+  // ---- J and W = H^-1 J^T columns (lane = dof j), kept in LDS [row][dof]:
+  //      J_rj = S_j . f6_r on the contact link's path (ancestor bitmask), +-1 at a limited dof
+  float Sj[6];
+  const int jl = lane < NV ? lane : 0;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) Sj[a] = s.S[jl][a];
   __syncthreads();
-  // ---- projected Gauss-Seidel; lane j holds u_j
   const int maxrow = sm.maxrow;
-  float uj = lane < nv ? s.u[lane] : 0.f;
-  for (int it = 0; it < K.sim.pgs_iters; ++it) {
-    for (int r = 0; r < maxrow; ++r) {
-      bool act = r < nrow;
-      float Jrj = (act && lane < nv) ? s.J[r * LDH + lane] : 0.f;
-      float v = wave32_sum(Jrj * uj);
-      if (act) {
-        float l0 = s.rlam[r], l1;
-        if (s.rtype[r] == 1) {
-          int rn = r - (r % 3 == 1 ? 1 : 2);
-          float lim = K.sim.friction * s.rlam[rn];
-          l1 = fminf(fmaxf(l0 - v * s.rAd[r], -lim), lim);
-        } else {
-          l1 = fmaxf(l0 + (s.rtarget[r] - v) * s.rAd[r], 0.f);
-        }
-        float dl = l1 - l0;
-        if (lane < nv) uj += s.W[r * LDH + lane] * dl;
-        __syncthreads();  // every lane has read rlam before it changes
-        if (lane == 0) s.rlam[r] = l1;
-      } else {
-        __syncthreads();
+#pragma unroll 1
+  for (int r = 0; r < maxrow; ++r) {
+    float jv = 0.f;
+    if (r < nrow && lane < NV) {
+      int lk = s.rlink[r];
+      if (lk >= 0) {
+        if ((K.ancmask[lk] >> lane) & 1u) jv = dot6(Sj, s.rf6[r]);
+      } else if (-1 - lk == lane) {
+        jv = s.rsign[r];
       }
-      __syncthreads();
+    }
+    if (lane < LDJ) s.x.k.Jm[r][lane] = jv;
+  }
+  __syncthreads();
+  // lanes >= NV carry no dof: they read column 0 scaled by 0 (keeps every LDS address in bounds)
+  const int jc = lane < NV ? lane : 0;
+  const float jmask = lane < NV ? 1.f : 0.f;
+#pragma unroll 1
+  for (int r = 0; r < maxrow; ++r) {
+    float w = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) w += Hr[k] * s.x.k.Jm[r][k];
+    w = lane < NV ? w : 0.f;
+    if (lane < LDJ) s.x.k.Wm[r][lane] = w;
+    float a = half_sum(s.x.k.Jm[r][jc] * jmask * w);
+    if (lane == 0) {
+      s.rmeta[r][0] = r < nrow ? 1.0f / (a + 1e-9f) : 0.f;
+      if (r >= nrow) { s.rmeta[r][1] = 0.f; s.rmeta[r][2] = 0.f; }
+      s.rlam[r] = 0.f;
     }
   }
-  if (lane < nv) s.u[lane] = uj;
   __syncthreads();
+  ts.mark(kStWsolve);
+  // ---- projected Gauss-Seidel (lane j holds u_j; impulses uniform per env, kept in LDS).
+  // Rows in order: contacts as (normal, tangent, tangent) triplets, then joint limits; a tangent
+  // row's bound uses the impulse of the most recent normal row (ln).  One-row-ahead prefetch.
+  const float mu = K.sim.friction;
+#pragma unroll 1
+  for (int it = 0; it < K.sim.pgs_iters; ++it) {
+    float ln = 0.f;
+    float Jn = s.x.k.Jm[0][jc] * jmask, Wn = s.x.k.Wm[0][jc] * jmask;
+    float4 mn = *reinterpret_cast<const float4*>(s.rmeta[0]);
+    float lnext = s.rlam[0];
+#pragma unroll 1
+    for (int r = 0; r < maxrow; ++r) {
+      const float Jr = Jn, Wr = Wn, l0 = lnext;
+      const float4 mt = mn;
+      const int rn = r + 1 < maxrow ? r + 1 : r;
+      Jn = s.x.k.Jm[rn][jc] * jmask;
+      Wn = s.x.k.Wm[rn][jc] * jmask;
+      mn = *reinterpret_cast<const float4*>(s.rmeta[rn]);
+      lnext = s.rlam[rn];
+      const float v = half_sum(Jr * uj);
+      float l1;
+      if (mt.z == 1.f) {
+        const float lim = mu * ln;
+        l1 = fminf(fmaxf(l0 - v * mt.x, -lim), lim);
+      } else {
+        l1 = fmaxf(l0 + (mt.y - v) * mt.x, 0.f);
+        if (mt.z == 0.f) ln = l1;
+      }
+      uj += Wr * (l1 - l0);
+      if (lane == 0) s.rlam[r] = l1;
+    }
+  }
+  if (lane < NV) s.u[lane] = uj;
+  if (lane < MAXC) s.lamn[lane] = 3 * lane < nrow ? s.rlam[3 * lane] : 0.f;
+  __syncthreads();
+  ts.mark(kStPGS);
   // ---- contact-sensor flags of this substep (force_matrix_w = impulse / dt, > eps)
   if (lane == 0) {
     uint32_t mk[2] = {0u, 0u};
@@ -575,7 +673,7 @@ __device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* 
       float fx = 0.f, fy = 0.f, fz = 0.f;
       for (int c2 = 0; c2 < nc && 3 * c2 < nrow; ++c2) {
         if (s.cfoot[c2] != s.cfoot[c] || s.cstone[c2] != s.cstone[c]) continue;
-        float l = s.rlam[3 * c2];
+        float l = s.lamn[c2];
         fx += l * s.cn[c2][0]; fy += l * s.cn[c2][1]; fz += l * s.cn[c2][2];
       }
       if (sqrtf(fx * fx + fy * fy + fz * fz) / dt > 1e-4f) mk[s.cfoot[c]] |= 1u << s.cstone[c];
@@ -592,7 +690,7 @@ __device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* 
   if (lane == 0) {
     const float* u = s.u;
     float c0w[3];
-    for (int k = 0; k < 3; ++k) c0w[k] = s.root_pos[k] + s.c[0][k] + dt * u[k];
+    for (int k = 0; k < 3; ++k) c0w[k] = s.root_pos[k] + s.c0[k] + dt * u[k];
     const float* w = u + 3;
     float wn = sqrtf(dot3(w, w));
     float th = wn * dt, dq[4];
@@ -617,39 +715,41 @@ __device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* 
     for (int k = 0; k < 3; ++k) s.root_pos[k] = c0w[k] - cl[k];
   }
   __syncthreads();
+  ts.mark(kStIntegrate);
 }
 
 // ------------------------------------------------------------------------------------------------
 // task logic helpers (allsteps_env.py)
 
 struct Useful {
-  float h, roll, pitch, body_dist, dist_f[2];
+  float h, roll, pitch, body_dist, dist_s;  // dist_s: swing-foot xy distance to the target
   int reached;
 };
 
-// allsteps_env.py:418-457 foot-state tick + 459-467 targets + 407-416 potentials (one env, serial)
+// allsteps_env.py:418-457 foot-state tick + 459-467 targets + 407-416 potentials (one env, serial).
+// dist_s is the swing foot's distance with the swing leg AFTER the tick (allsteps_env.py:371).
 __device__ void compute_useful(const Consts& K, const float* root_pos, const float* root_quat, const float* bp,
-                               const float* stones_env /* [20][3] or strided via lambda */, int stride,
-                               uint32_t mask_r, uint32_t mask_l, int& idx, int& prev, int& next, int& count,
-                               int& swing, float& pot, float& old_pot, float* foot_contact, bool tick, Useful& u) {
+                               const float* stones_env, int stride, uint32_t mask_r, uint32_t mask_l, int& idx,
+                               int& prev, int& next, int& count, int& swing, float& pot, float& old_pot,
+                               float* foot_contact, bool tick, Useful& u) {
   const as_task_t& T = K.task;
   const int N = T.num_steps;
   float lower = fminf(bp[8], bp[5]);   // minimum(left_z, right_z)
   u.h = bp[2] - lower;
   euler_rp_from_quat(root_quat, &u.roll, &u.pitch);
   u.reached = 0;
+  u.dist_s = 0.f;
   if (tick) {
     float cf0 = ((mask_r >> idx) & 1u) ? 1.f : 0.f;
     float cf1 = ((mask_l >> idx) & 1u) ? 1.f : 0.f;
     foot_contact[0] = cf0;
     foot_contact[1] = cf1;
     float tx = stones_env[(idx * 3 + 0) * stride], ty = stones_env[(idx * 3 + 1) * stride];
-    for (int f = 0; f < 2; ++f) {
-      float dx = bp[3 + 3 * f] - tx, dy = bp[3 + 3 * f + 1] - ty;
-      u.dist_f[f] = sqrtf(dx * dx + dy * dy);
-    }
+    float dx0 = bp[3] - tx, dy0 = bp[4] - ty, dx1 = bp[6] - tx, dy1 = bp[7] - ty;
+    float d0 = sqrtf(dx0 * dx0 + dy0 * dy0), d1 = sqrtf(dx1 * dx1 + dy1 * dy1);
     float cfs = swing == 0 ? cf0 : cf1;
-    u.reached = (cfs > 0.f) && (u.dist_f[swing] < T.step_radius);
+    float ds = swing == 0 ? d0 : d1;
+    u.reached = (cfs > 0.f) && (ds < T.step_radius);
     if (u.reached) count += 1;
     if (count >= T.stop_frames) {
       swing ^= 1;
@@ -659,6 +759,7 @@ __device__ void compute_useful(const Consts& K, const float* root_pos, const flo
       next = min(max(ni + 1, 0), N - 1);
       count = 0;
     }
+    u.dist_s = swing == 0 ? d0 : d1;
   }
   float dx = stones_env[(next * 3 + 0) * stride] - root_pos[0];
   float dy = stones_env[(next * 3 + 1) * stride] - root_pos[1];
@@ -668,14 +769,12 @@ __device__ void compute_useful(const Consts& K, const float* root_pos, const flo
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_step(StepArgs P) {
+template <int NV>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_step(StepArgs P) {
   __shared__ Smem sm;
-  __shared__ Consts K;
-  {  // stage the constants in LDS
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(P.consts);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&K);
-    for (int i = threadIdx.x; i < (int)(sizeof(Consts) / 4); i += 64) dst[i] = src[i];
-  }
+  // model / plan constants stay in global memory (5.7 KB, L1/K$-resident): LDS is the occupancy
+  // budget, see EnvS
+  const Consts& K = *P.consts;
   const int el = threadIdx.x >> 5, lane = threadIdx.x & 31;
   const int n = P.n;
   const int e_raw = blockIdx.x * EPB + el;
@@ -683,6 +782,8 @@ __global__ __launch_bounds__(64) void k_step(StepArgs P) {
   const int e = valid ? e_raw : n - 1;
   EnvS& s = sm.env[el];
   const as_state_t& st = P.st;
+  Stamp ts{P.stamps, 0ull};
+  ts.start();
   __syncthreads();
   const as_model_t& m = K.model;
   const int nh = m.num_hinges;
@@ -709,18 +810,13 @@ __global__ __launch_bounds__(64) void k_step(StepArgs P) {
   for (int k = lane; k < 3 * T.num_steps; k += G) s.stones[k] = st.stones[k * n + e];
   uint32_t mask[2] = {st.contact_mask[e], st.contact_mask[n + e]};
   __syncthreads();
+  ts.mark(kStLoad);
   const bool do_physics = P.mode == kModeStep || P.mode == kModePhysics;
   // ---- physics
   if (do_physics) {
-    for (int sub = 0; sub < K.sim.substeps; ++sub) substep(K, sm, s, lane, mask);
-    // FK of the final pose for body_pos_w (articulation_data.py:439)
-    fk(K, s, lane);
-    if (lane == 0) {
-      uint32_t m0 = mask[0], m1 = mask[1];
-      s.mask[0] = m0;
-      s.mask[1] = m1;
-    }
-    __syncthreads();
+    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, mask, ts);
+    fk(K, s, lane);  // FK of the final pose for body_pos_w (articulation_data.py:439)
+    if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
   }
   if (lane == 0 && !do_physics) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
   __syncthreads();
@@ -754,8 +850,8 @@ __global__ __launch_bounds__(64) void k_step(StepArgs P) {
       en = fabsf(s.u[6 + li - 1] * a);
       atlim = fabsf(scale_transform(s.qi[li - 1], m.lower[li], m.upper[li])) > 0.99f;
     }
-    a2 = wave32_sum(a2);
-    en = wave32_sum(en);
+    a2 = half_sum(a2);
+    en = half_sum(en);
     uint64_t bl = __ballot(atlim != 0);
     int nlim = __popcll(bl >> (32 * el) & 0xffffffffull);
     const float* lv = s.u;
@@ -776,7 +872,7 @@ __global__ __launch_bounds__(64) void k_step(StepArgs P) {
     float energy_cost = T.energy * en;
     float limit_cost = (float)nlim * T.joint_limit;
     bool cond = u.reached && count == 1 && idx < T.num_steps - 1;
-    float step_rew = cond ? 50.0f * expf(-u.dist_f[swing] / 0.25f) : 0.f;
+    float step_rew = cond ? 50.0f * expf(-u.dist_s / 0.25f) : 0.f;
     bool bonus_c = idx == T.num_steps - 1 && u.body_dist < 0.15f;
     float total = T.alive + progress;
     total = total - roll_cost;
@@ -803,20 +899,29 @@ __global__ __launch_bounds__(64) void k_step(StepArgs P) {
       atomicOr(&P.counters[0], 1);
     }
   }
+  ts.mark(kStTask);
   // ---- in-kernel reset (allsteps_env.py:481-565)
   const bool any_done = __any(done);  // wave-uniform: both envs of the wave enter the FK together
   if (P.mode != kModePhysics && any_done) {
     if (done) {
-      float d[24];
+      float dm = 0.f, dn = 0.f;  // mirror draw, this lane's joint-noise draw
       if (P.reset_draws) {
-        for (int k = 0; k < 22; ++k) d[k] = P.reset_draws[(size_t)e * 22 + k];
+        dm = P.reset_draws[(size_t)e * 22];
+        if (lane < nh) dn = P.reset_draws[(size_t)e * 22 + 1 + lane];
       } else {
-        for (int b = 0; b < 6; ++b)
-          philox_block(P.seed, (uint32_t)(P.env_offset + e), episode, (uint32_t)b, kResetTag, d + 4 * b);
+        float blk[4];
+        philox_block(P.seed, (uint32_t)(P.env_offset + e), episode, 0u, kResetTag, blk);
+        dm = blk[0];
+        if (lane < nh) {  // draw k = 1 + lane lives in block (1 + lane) / 4, slot (1 + lane) % 4
+          const int k = 1 + lane;
+          philox_block(P.seed, (uint32_t)(P.env_offset + e), episode, (uint32_t)(k >> 2), kResetTag, blk);
+          const int sl = k & 3;
+          dn = sl == 0 ? blk[0] : (sl == 1 ? blk[1] : (sl == 2 ? blk[2] : blk[3]));
+        }
       }
       ep_len = 0;
       old_pot = 0.f; pot = 0.f; count = 0; swing = 0; idx = 1; prev = 0; next = 2;
-      const bool mirror = d[0] > 0.5f;
+      const bool mirror = dm > 0.5f;
       if (mirror) swing ^= 1;
       if (lane < nh) {
         // joint `lane` (cfg order): running-start pose, mirrored, noise, clip (allsteps_env.py:505-560)
@@ -832,7 +937,7 @@ __global__ __launch_bounds__(64) void k_step(StepArgs P) {
         float jp = T.init_q[src] * sign;
         float jv = 0.f * sign;
         int li = m.cfg_dof_link[lane];
-        float x = jp + (d[1 + lane] * (T.noise_hi - T.noise_lo) + T.noise_lo);
+        float x = jp + (dn * (T.noise_hi - T.noise_lo) + T.noise_lo);
         float sc = fminf(fmaxf(scale_transform(x, m.lower[li], m.upper[li]), T.clip_lo), T.clip_hi);
         s.qi[li - 1] = unscale_transform(sc, m.lower[li], m.upper[li]);
         s.u[6 + li - 1] = jv;
@@ -860,30 +965,38 @@ __global__ __launch_bounds__(64) void k_step(StepArgs P) {
     }
   }
   __syncthreads();
+  ts.mark(kStReset);
   // ---- store
-  if (!valid) return;
-  if (lane < 3) {
-    st.root_pos[lane * n + e] = s.root_pos[lane];
-    st.root_lin[lane * n + e] = s.u[lane];
-    st.root_ang[lane * n + e] = s.u[3 + lane];
-  }
-  if (lane < 4) st.root_quat[lane * n + e] = s.root_quat[lane];
-  if (lane < nh) {
-    int i = m.cfg_dof_link[lane] - 1;
-    st.q[lane * n + e] = s.qi[i];
-    st.qd[lane * n + e] = s.u[6 + i];
-  }
-  if (lane < 9) st.body_pos[lane * n + e] = bp[lane];
-  if (lane == 0) {
-    st.contact_mask[e] = s.mask[0];
-    st.contact_mask[n + e] = s.mask[1];
-    if (P.mode != kModePhysics) {
-      st.idx[e] = idx; st.prev[e] = prev; st.next[e] = next; st.count[e] = count; st.swing[e] = swing;
-      st.ep_len[e] = ep_len; st.pot[e] = pot; st.old_pot[e] = old_pot;
-      st.foot_contact[e] = fc[0]; st.foot_contact[n + e] = fc[1];
-      st.episode[e] = episode;
+  if (valid) {
+    if (lane < 3) {
+      st.root_pos[lane * n + e] = s.root_pos[lane];
+      st.root_lin[lane * n + e] = s.u[lane];
+      st.root_ang[lane * n + e] = s.u[3 + lane];
+    }
+    if (lane < 4) st.root_quat[lane * n + e] = s.root_quat[lane];
+    if (lane < nh) {
+      int i = m.cfg_dof_link[lane] - 1;
+      st.q[lane * n + e] = s.qi[i];
+      st.qd[lane * n + e] = s.u[6 + i];
+    }
+    if (lane < 9) {
+      float v = bp[0];
+#pragma unroll
+      for (int k = 1; k < 9; ++k) v = (lane == k) ? bp[k] : v;
+      st.body_pos[lane * n + e] = v;
+    }
+    if (lane == 0) {
+      st.contact_mask[e] = s.mask[0];
+      st.contact_mask[n + e] = s.mask[1];
+      if (P.mode != kModePhysics) {
+        st.idx[e] = idx; st.prev[e] = prev; st.next[e] = next; st.count[e] = count; st.swing[e] = swing;
+        st.ep_len[e] = ep_len; st.pot[e] = pot; st.old_pot[e] = old_pot;
+        st.foot_contact[e] = fc[0]; st.foot_contact[n + e] = fc[1];
+        st.episode[e] = episode;
+      }
     }
   }
+  ts.mark(kStStore);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -986,9 +1099,16 @@ __global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
 }
 
 // ------------------------------------------------------------------------------------------------
-hipError_t launch_step(const StepArgs& a, hipStream_t stream) {
+bool step_supported_nv(int nv) { return nv == 27 || nv == 6; }
+
+hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream) {
   int blocks = (a.n + EPB - 1) / EPB;
-  hipLaunchKernelGGL(k_step, dim3(blocks), dim3(64), 0, stream, a);
+  if (nv == 27)
+    hipLaunchKernelGGL(k_step<27>, dim3(blocks), dim3(64), 0, stream, a);
+  else if (nv == 6)
+    hipLaunchKernelGGL(k_step<6>, dim3(blocks), dim3(64), 0, stream, a);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -33,8 +33,8 @@ extern "C" {
 #define AS_MAX_LINKS 32
 #define AS_MAX_GEOMS 32
 #define AS_NUM_STONES 20
-#define AS_MAX_CONTACTS 10
-#define AS_MAX_ROWS 40
+#define AS_MAX_CONTACTS 8
+#define AS_MAX_ROWS 24
 #define AS_OBS_DIM 59
 #define AS_ACT_DIM 21
 
@@ -177,6 +177,11 @@ int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* s
  * synchronises on the last event and returns the summed durations (ms) and the launch count. */
 int as_profile(as_env_t* env, int32_t max_launches);
 int as_profile_read(as_env_t* env, double* step_kernel_ms, double* obs_kernel_ms, int32_t* launches);
+
+/* Diagnostic: when stamps_dev (device, >= 16 uint64) is non-null, every k_step wave adds the
+ * s_memtime cycles of each phase (load, fk, link, dynamics, cholesky, solve, collide, rows,
+ * W-solve, pgs, integrate, task, reset, store) to it.  Pass NULL to switch off. */
+int as_debug_stamps(as_env_t* env, uint64_t* stamps_dev);
 
 /* Device counters of the last step: [0] = any env reset, [1] = sum of curr_target_index. */
 int as_step_counters(as_env_t* env, const int32_t** counters_dev);

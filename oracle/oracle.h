@@ -30,8 +30,8 @@ extern "C" {
 #define OR_MAX_GEOMS 32
 #define OR_MAX_STONES 20
 #define OR_NDOF_ROOT 6
-#define OR_MAX_CONTACTS 10
-#define OR_MAX_ROWS 40
+#define OR_MAX_CONTACTS 8
+#define OR_MAX_ROWS 24
 
 /* Model tables compiled from walker3d.xml (allsteps_isaaclab_amd/model/walker3d.json). */
 typedef struct {

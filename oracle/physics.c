@@ -267,32 +267,36 @@ static void rnea_bias(const or_model_t* m, const kin_t* K, const float* u, float
   }
 }
 
-static void cholesky(float* H, int n) {
-  for (int j = 0; j < n; ++j) {
-    float s = H[j * n + j];
-    for (int k = 0; k < j; ++k) s -= H[j * n + k] * H[j * n + k];
-    float d = sqrtf(s > 1e-12f ? s : 1e-12f);
-    H[j * n + j] = d;
-    float inv = 1.0f / d;
-    for (int i = j + 1; i < n; ++i) {
-      float t = H[i * n + j];
-      for (int k = 0; k < j; ++k) t -= H[i * n + k] * H[j * n + k];
-      H[i * n + j] = t * inv;
+/* Inverse of the SPD joint-space inertia by the symmetric sweep operator (no pivoting needed for
+ * SPD).  Sweep on pivot k with the pre-sweep pivot row Q (d = Q_k, r = 1/d):
+ *   row k: a_kj <- r a_kj (j != k), a_kk <- -r;   row i != k: g = r a_ik, a_ij <- a_ij - g Q_j,
+ *   a_ik <- g.
+ * After all pivots a = -H^-1; the result is negated.  The HIP kernel runs the same sequence with
+ * one row per lane (a_ik = Q_i by symmetry). */
+static void sweep_inverse(float* a, int n) {
+  float Q[NV_MAX];
+  for (int k = 0; k < n; ++k) {
+    for (int j = 0; j < n; ++j) Q[j] = a[k * n + j];
+    const float d = Q[k], r = 1.0f / d;
+    for (int i = 0; i < n; ++i) {
+      float* row = a + i * n;
+      if (i == k) {
+        for (int j = 0; j < n; ++j) row[j] = (j == k) ? -r : r * row[j];
+      } else {
+        const float g = Q[i] * r;
+        for (int j = 0; j < n; ++j) row[j] = (j == k) ? g : row[j] - g * Q[j];
+      }
     }
   }
+  for (int i = 0; i < n * n; ++i) a[i] = -a[i];
 }
 
-static void chol_solve(const float* L, int n, const float* b, float* x) {
-  float y[NV_MAX];
+/* x = A b (row-major, sequential in k) */
+static void matvec_n(const float* A, int n, const float* b, float* x) {
   for (int i = 0; i < n; ++i) {
-    float s = b[i];
-    for (int k = 0; k < i; ++k) s -= L[i * n + k] * y[k];
-    y[i] = s / L[i * n + i];
-  }
-  for (int i = n - 1; i >= 0; --i) {
-    float s = y[i];
-    for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * x[k];
-    x[i] = s / L[i * n + i];
+    float s = 0.f;
+    for (int k = 0; k < n; ++k) s += A[i * n + k] * b[k];
+    x[i] = s;
   }
 }
 
@@ -446,8 +450,8 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
   crba(m, &K, H);
   rnea_bias(m, &K, u, sim->gravity, C);
   for (int j = 0; j < nv; ++j) b[j] = (j < OR_NDOF_ROOT ? 0.f : tau_int[j - OR_NDOF_ROOT]) - C[j];
-  cholesky(H, nv);
-  chol_solve(H, nv, b, acc);
+  sweep_inverse(H, nv); /* H <- H^-1 */
+  matvec_n(H, nv, b, acc);
   for (int j = 0; j < nv; ++j) u[j] += dt * acc[j];
 
   /* constraints */
@@ -492,7 +496,7 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
     }
   }
   for (int r = 0; r < R->nrow; ++r) {
-    chol_solve(H, nv, R->J[r], R->W[r]);
+    matvec_n(H, nv, R->J[r], R->W[r]); /* W_r = H^-1 J_r^T */
     float a = 0.f;
     for (int k = 0; k < nv; ++k) a += R->J[r][k] * R->W[r][k];
     R->Ad[r] = 1.0f / (a + 1e-9f);
