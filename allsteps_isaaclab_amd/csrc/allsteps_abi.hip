@@ -82,18 +82,17 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   h.sim = *sim;
   h.task = *task;
   h.nv = 6 + model->num_hinges;
-  h.max_depth = 0;
-  for (int i = 0; i < model->num_links; ++i) {
+  const int nl = model->num_links;
+  for (int i = 0; i < nl; ++i) {
     int pa = model->parent[i];
     if (i == 0 ? pa != -1 : (pa < 0 || pa >= i)) return fail(AS_ERR_INVALID, "as_create: parent not topological");
-    h.depth[i] = i == 0 ? 0 : h.depth[pa] + 1;
-    if (h.depth[i] > h.max_depth) h.max_depth = h.depth[i];
+    h.lpath[i] = (i == 0 ? 0u : h.lpath[pa]) | (1u << i);
+    if (i > 0 && pa == 0) h.root_kids |= 1u << i;
   }
-  for (int i = model->num_links - 1; i >= 1; --i) {
-    int pa = model->parent[i];
-    if (h.nchild[pa] >= as::kMaxChildren) return fail(AS_ERR_INVALID, "as_create: too many children per link");
-    h.child[pa][h.nchild[pa]++] = i;  // descending index order
-  }
+  for (int i = 0; i < nl; ++i)
+    for (int l = 0; l < nl; ++l)
+      if ((h.lpath[l] >> i) & 1u) h.lsub[i] |= 1u << l;
+  for (int j = 0; j < h.nv; ++j) h.dsub[j] = j < 6 ? h.lsub[0] : h.lsub[j - 5];
   for (int k = 0; k < model->num_hinges; ++k) {
     int li = model->cfg_dof_link[k];
     if (li < 1 || li >= model->num_links) return fail(AS_ERR_INVALID, "as_create: cfg_dof_link");

@@ -9,22 +9,24 @@
 namespace as {
 
 constexpr int kMaxLinks = 24;  // LDS sizing of the step kernel (walker: 22 links)
-constexpr int kMaxChildren = 4;
+constexpr int kMaxDofs = 6 + kMaxLinks - 1;
 
 enum { kModeStep = 0, kModeReset = 1, kModePhysics = 2, kModeTask = 3 };
 
 // Everything the kernels read that does not change per step: model tables + the tree plan
-// derived from them on the host (depth levels and child lists for the level-synchronous passes).
+// derived from them on the host.  The plan is bitmasks over links / dofs: every tree pass of the
+// step kernel is a walk over one lane's own ancestor path or subtree (no level barriers), and
+// each lane keeps its own masks in registers for the whole launch.
 struct Consts {
   as_model_t model;
   as_sim_t sim;
   as_task_t task;
   int32_t nv;
-  int32_t max_depth;
-  int32_t depth[kMaxLinks];
-  int32_t nchild[kMaxLinks];
-  int32_t child[kMaxLinks][kMaxChildren];  // descending link index
-  uint32_t ancmask[kMaxLinks];             // dofs on the path root..link (root dofs 0-5 always set)
+  uint32_t root_kids;              // links whose parent is the root
+  uint32_t lpath[kMaxLinks];       // links on the path root..link, both included
+  uint32_t lsub[kMaxLinks];        // links in the subtree of link, itself included
+  uint32_t ancmask[kMaxLinks];     // dofs on the path root..link (root dofs 0-5 always set)
+  uint32_t dsub[kMaxDofs];         // links moved by dof j (subtree of its link; root dofs: all)
 };
 
 struct StepArgs {

@@ -50,20 +50,55 @@ struct DynScratch {
   float Ib[LMAX][10];
   float Ic[LMAX][10];
   float Fh[NVMAX][6];   // Ic_link(j) S_j (CRBA column forces)
-  float V[LMAX][6];
-  float A[LMAX][6];
-  float F[LMAX][6];
+  float Sq[LMAX][6];    // S_i qd_i, later the subtree force sums F_i
+  union {
+    float Rl[LMAX][12]; // FK: local joint transforms (R 9, p 3); dead before cr / f are written
+    struct {
+      float cr[LMAX][6];  // V_i x_m S_i qd_i
+      float f[LMAX][6];   // body forces of the RNEA
+    } b;
+  };
 };
 struct ConScratch {
   float Jm[MAXR][LDJ];  // J rows (lane = dof column)
   float Wm[MAXR][LDJ];  // W = H^-1 J^T rows (lane = dof column)
 };
 union PhaseScratch {
-  float Rl[LMAX][12];   // FK: local joint transforms (R 9, p 3)
   DynScratch d;
-  float piv[2][32];     // sweep: pivot row (double-buffered)
+  struct {
+    float q[2][32];     // sweep: the two pivot rows of a round
+    float pb[4];        //        and the pivot block H_PP
+  } sw;                 // aliases d.c / d.Ib, dead by then
   ConScratch k;
 };
+
+// The constants block is read-only for the whole launch: address space 4 (constant) lets uniform
+// loads become scalar loads and keeps lane-varying ones global (not flat) loads.
+using CK = const __attribute__((address_space(4))) Consts;
+
+// Per-lane tree plan and joint constants, read once per launch and kept in registers
+// (lane = link for the l* fields, lane = dof for the d* fields, lane = hinge for lo / hi).
+struct Topo {
+  uint32_t lpath;  // links on the path root..link(lane)
+  uint32_t lsub;   // subtree of link(lane)
+  uint32_t dsub;   // links moved by dof lane
+  float lo, hi;    // limits of hinge lane (link lane + 1)
+};
+
+__device__ Topo load_topo(const Consts& K, int lane) {
+  const as_model_t& m = K.model;
+  const int nl = m.num_links, nv = K.nv;
+  Topo t;
+  const int l = lane < nl ? lane : 0;
+  const int j = lane < nv ? lane : 0;
+  const int hl = lane + 1 < nl ? lane + 1 : 0;
+  t.lpath = lane < nl ? K.lpath[l] : 0u;
+  t.lsub = lane < nl ? K.lsub[l] : 0u;
+  t.dsub = lane < nv ? K.dsub[j] : 0u;
+  t.lo = m.lower[hl];
+  t.hi = m.upper[hl];
+  return t;
+}
 
 struct EnvS {
   float R[LMAX][9];
@@ -93,6 +128,8 @@ struct EnvS {
 
 struct Smem {
   EnvS env[EPB];
+  Topo topo[G];  // per-lane tree plan (shared by both envs; registers cannot hold it)
+  unsigned long long stamp_acc[kNumStamps];
   int maxrow;
 };
 
@@ -125,179 +162,258 @@ __device__ __forceinline__ float wave32_sum(float v) {
   return v;
 }
 
-// diagnostic phase stamps: lane 0 of each wave adds s_memtime deltas (off when p == nullptr)
+// diagnostic phase stamps (off when p == nullptr): each wave accumulates its s_memtime deltas per
+// phase in LDS and adds them to the device counters once, at the end of the launch -- a global
+// atomic per phase boundary would put a contended memory round trip into the next phase.
 struct Stamp {
   unsigned long long* p;
+  unsigned long long* acc;  // LDS, kNumStamps
   unsigned long long t;
   __device__ void start() {
-    if (p) t = __builtin_amdgcn_s_memtime();
+    if (p) {
+      if (threadIdx.x < kNumStamps) acc[threadIdx.x] = 0ull;
+      t = __builtin_amdgcn_s_memtime();
+    }
   }
   __device__ void mark(int k) {
     if (p) {
       unsigned long long now = __builtin_amdgcn_s_memtime();
-      if ((threadIdx.x & 63) == 0) atomicAdd(p + k, now - t);
+      if (threadIdx.x == 0) acc[k] += now - t;
       t = now;
+    }
+  }
+  __device__ void flush() {
+    if (p) {
+      __syncthreads();
+      if (threadIdx.x < kNumStamps) atomicAdd(p + threadIdx.x, acc[threadIdx.x]);
     }
   }
 };
 
 // ------------------------------------------------------------------------------------------------
-// FK: local joint transforms (parallel), then level-synchronous composition.
-__device__ void fk(const Consts& K, EnvS& s, int lane) {
+// FK by ancestor-path walks.  Local joint transforms are formed in parallel (lane = link); then
+// lane i composes the transforms on its own path root -> i, which is the same sequence of products
+// a level-by-level pass would form (R_i = R_parent Rl_i, p_i = p_parent + R_parent t_i), with no
+// level barriers: the tree depth only sets the length of the longest lane's loop.
+// kDyn: also the link's spatial quantities for the dynamics (COM, spatial inertia at O, motion
+// subspace of its hinge, S_i qd_i) from the registers of the walk, and the six root columns.
+template <bool kDyn>
+__device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Topo& tp) {
   const as_model_t& m = K.model;
   const int nl = m.num_links;
-  for (int i = lane; i < nl; i += G) {
-    if (i == 0) {
-      quat_to_mat(s.root_quat, s.R[0]);
-      s.p[0][0] = s.p[0][1] = s.p[0][2] = 0.f;
-    } else {
-      float Roff[9], Rj[9], Ro[3], t[3], tmp[3];
-      quat_to_mat(m.offset_quat[i], Roff);
-      axis_angle_mat(m.axis[i], s.qi[i - 1], Rj);
-      matmul3(Roff, Rj, s.x.Rl[i]);
-      matvec3(Rj, m.anchor[i], Ro);
-      for (int k = 0; k < 3; ++k) t[k] = m.anchor[i][k] - Ro[k];
-      matvec3(Roff, t, tmp);
-      for (int k = 0; k < 3; ++k) s.x.Rl[i][9 + k] = tmp[k] + m.offset_pos[i][k];
+  DynScratch& d = s.x.d;
+  if (lane >= 1 && lane < nl) {
+    const int i = lane;
+    float Roff[9], Rj[9], Ro[3], t[3], tmp[3];
+    quat_to_mat(m.offset_quat[i], Roff);
+    axis_angle_mat(m.axis[i], s.qi[i - 1], Rj);
+    matmul3(Roff, Rj, d.Rl[i]);
+    matvec3(Rj, m.anchor[i], Ro);
+    for (int k = 0; k < 3; ++k) t[k] = m.anchor[i][k] - Ro[k];
+    matvec3(Roff, t, tmp);
+    for (int k = 0; k < 3; ++k) d.Rl[i][9 + k] = tmp[k] + m.offset_pos[i][k];
+  }
+  __syncthreads();
+  float R0[9];
+  quat_to_mat(s.root_quat, R0);
+  if (lane < nl) {
+    float R[9], p[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = R0[k];
+    uint32_t path = tp.lpath & ~1u;
+    while (path) {
+      const int l = __builtin_ctz(path);
+      path &= path - 1u;
+      const float* Rl = d.Rl[l];
+      float Rn[9], wp[3];
+      matmul3(R, Rl, Rn);
+      matvec3(R, Rl + 9, wp);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) p[k] += wp[k];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) R[k] = Rn[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s.R[lane][k] = R[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s.p[lane][k] = p[k];
+    if (kDyn) {
+      const int i = lane;
+      float cw[3];
+      matvec3(R, m.com[i], cw);
+      const float c[3] = {p[0] + cw[0], p[1] + cw[1], p[2] + cw[2]};
+      d.c[i][0] = c[0]; d.c[i][1] = c[1]; d.c[i][2] = c[2];
+      const float* Il = m.inertia[i];
+      const float Im[9] = {Il[0], Il[3], Il[4], Il[3], Il[1], Il[5], Il[4], Il[5], Il[2]};
+      const float Rt[9] = {R[0], R[3], R[6], R[1], R[4], R[7], R[2], R[5], R[8]};
+      float T[9], Iw[9];
+      matmul3(R, Im, T);
+      matmul3(T, Rt, Iw);
+      const float mass = m.mass[i], cc = dot3(c, c);
+      float* B = d.Ib[i];
+      B[0] = mass;
+      B[1] = mass * c[0]; B[2] = mass * c[1]; B[3] = mass * c[2];
+      B[4] = Iw[0] + mass * (cc - c[0] * c[0]);
+      B[5] = Iw[4] + mass * (cc - c[1] * c[1]);
+      B[6] = Iw[8] + mass * (cc - c[2] * c[2]);
+      B[7] = Iw[1] - mass * c[0] * c[1];
+      B[8] = Iw[2] - mass * c[0] * c[2];
+      B[9] = Iw[5] - mass * c[1] * c[2];
+      if (i > 0) {
+        float a[3], o[3];
+        matvec3(R, m.axis[i], a);
+        matvec3(R, m.anchor[i], o);
+        for (int k = 0; k < 3; ++k) o[k] += p[k];
+        float S[6] = {a[0], a[1], a[2], 0.f, 0.f, 0.f};
+        cross3(o, a, S + 3);
+        const float qd = s.u[6 + i - 1];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          s.S[6 + i - 1][k] = S[k];
+          d.Sq[i][k] = S[k] * qd;
+        }
+      }
+    }
+  }
+  if (kDyn) {
+    // root columns need the root COM c0 = R0 com_0 (p_0 = 0): every lane forms it itself
+    float c0[3];
+    matvec3(R0, m.com[0], c0);
+    if (lane < 3) s.c0[lane] = c0[lane];
+    if (lane < 6) {
+      float S[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const int k = lane % 3;
+      if (lane < 3) {
+        S[3 + k] = 1.f;
+      } else {
+        float e[3] = {0.f, 0.f, 0.f};
+        e[k] = 1.f;
+        S[k] = 1.f;
+        cross3(c0, e, S + 3);
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) s.S[lane][a] = S[a];
     }
   }
   __syncthreads();
-  for (int d = 1; d <= K.max_depth; ++d) {
-    for (int i = lane; i < nl; i += G) {
-      if (K.depth[i] != d) continue;
-      int pa = m.parent[i];
-      matmul3(s.R[pa], s.x.Rl[i], s.R[i]);
-      float wp[3];
-      matvec3(s.R[pa], s.x.Rl[i] + 9, wp);
-      for (int k = 0; k < 3; ++k) s.p[i][k] = s.p[pa][k] + wp[k];
-    }
-    __syncthreads();
-  }
 }
 
-// Per-link world quantities: COM, spatial inertia at O, motion subspace.
-__device__ void link_quantities(const Consts& K, EnvS& s, int lane) {
-  const as_model_t& m = K.model;
-  const int nl = m.num_links;
-  for (int i = lane; i < nl; i += G) {
-    const float* R = s.R[i];
-    float cw[3];
-    matvec3(R, m.com[i], cw);
-    float c[3] = {s.p[i][0] + cw[0], s.p[i][1] + cw[1], s.p[i][2] + cw[2]};
-    s.x.d.c[i][0] = c[0]; s.x.d.c[i][1] = c[1]; s.x.d.c[i][2] = c[2];
-    const float* Il = m.inertia[i];
-    float Im[9] = {Il[0], Il[3], Il[4], Il[3], Il[1], Il[5], Il[4], Il[5], Il[2]};
-    float Rt[9] = {R[0], R[3], R[6], R[1], R[4], R[7], R[2], R[5], R[8]};
-    float T[9], Iw[9];
-    matmul3(R, Im, T);
-    matmul3(T, Rt, Iw);
-    float mass = m.mass[i], cc = dot3(c, c);
-    float* B = s.x.d.Ib[i];
-    B[0] = mass;
-    B[1] = mass * c[0]; B[2] = mass * c[1]; B[3] = mass * c[2];
-    B[4] = Iw[0] + mass * (cc - c[0] * c[0]);
-    B[5] = Iw[4] + mass * (cc - c[1] * c[1]);
-    B[6] = Iw[8] + mass * (cc - c[2] * c[2]);
-    B[7] = Iw[1] - mass * c[0] * c[1];
-    B[8] = Iw[2] - mass * c[0] * c[2];
-    B[9] = Iw[5] - mass * c[1] * c[2];
-    for (int k = 0; k < 10; ++k) s.x.d.Ic[i][k] = B[k];
-    if (i > 0) {
-      float a[3], Ro[3], o[3];
-      matvec3(R, m.axis[i], a);
-      matvec3(R, m.anchor[i], Ro);
-      for (int k = 0; k < 3; ++k) o[k] = s.p[i][k] + Ro[k];
-      float* S = s.S[6 + i - 1];
-      S[0] = a[0]; S[1] = a[1]; S[2] = a[2];
-      cross3(o, a, S + 3);
-    }
-  }
-  __syncthreads();
-  if (lane < 3) s.c0[lane] = s.x.d.c[0][lane];
-  if (lane < 6) {  // root columns need c0
-    float* S = s.S[lane];
-    for (int j = 0; j < 6; ++j) S[j] = 0.f;
-    int k = lane % 3;
-    if (lane < 3) {
-      S[3 + k] = 1.f;
-    } else {
-      float e[3] = {0.f, 0.f, 0.f};
-      e[k] = 1.f;
-      S[k] = 1.f;
-      cross3(s.x.d.c[0], e, S + 3);
-    }
-  }
-  __syncthreads();
-}
-
-// Velocities, bias accelerations (qdd = 0), RNEA forces and composite inertias (lanes = links);
-// then per dof j: C_j, b_j = tau_j - C_j (returned), Fh_j = Ic_link(j) S_j (LDS).
-__device__ float dynamics(const Consts& K, EnvS& s, int lane, float gravity) {
+// RNEA bias forces (qdd = 0) and composite inertias by path / subtree walks (lanes = links):
+//   V_i  = V_0 + sum_{l on path, root->i} S_l qd_l            (= V_parent + S_i qd_i)
+//   A_i  = A_0 + sum_{l on path} V_l x_m S_l qd_l             (= A_parent + V_i x S_i qd_i)
+//   f_i  = I_i A_i + V_i x_f I_i V_i - gravity wrench
+//   F_i  = f_i + sum_{l in subtree(i), l > i, ascending} f_l  (non-root links), likewise Ic_i
+//   F_0  = f_0 + sum_{children c of the root, ascending} F_c, likewise Ic_0
+// (oracle/physics.c uses the same summation orders).  Then per dof j: C_j = S_j . F_link(j),
+// b_j = tau_j - C_j (returned, also in LDS), Fh_j = Ic_link(j) S_j.
+__device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, const Topo& tp, float gravity) {
   const as_model_t& m = K.model;
   const int nl = m.num_links, nv = K.nv;
-  if (lane == 0) {
+  DynScratch& d = s.x.d;
+  float V[6], A[6];
+  {
     const float* u = s.u;
     float wxc[3], vxw[3];
-    cross3(s.x.d.c[0], u + 3, wxc);
+    cross3(s.c0, u + 3, wxc);
     cross3(u, u + 3, vxw);
     for (int k = 0; k < 3; ++k) {
-      s.x.d.V[0][k] = u[3 + k];
-      s.x.d.V[0][3 + k] = u[k] + wxc[k];
-      s.x.d.A[0][k] = 0.f;
-      s.x.d.A[0][3 + k] = vxw[k];
+      V[k] = u[3 + k];
+      V[3 + k] = u[k] + wxc[k];
+      A[k] = 0.f;
+      A[3 + k] = vxw[k];
     }
   }
-  __syncthreads();
-  for (int d = 1; d <= K.max_depth; ++d) {
-    for (int i = lane; i < nl; i += G) {
-      if (K.depth[i] != d) continue;
-      int pa = m.parent[i];
-      float qd = s.u[6 + i - 1];
-      const float* S = s.S[6 + i - 1];
+  if (lane < nl) {
+    uint32_t path = tp.lpath & ~1u;
+    while (path) {
+      const int l = __builtin_ctz(path);
+      path &= path - 1u;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) V[k] += d.Sq[l][k];
+    }
+    if (lane > 0) {
       float Sq[6], cr[6];
-      for (int k = 0; k < 6; ++k) {
-        Sq[k] = S[k] * qd;
-        s.x.d.V[i][k] = s.x.d.V[pa][k] + Sq[k];
-      }
-      crm(s.x.d.V[i], Sq, cr);
-      for (int k = 0; k < 6; ++k) s.x.d.A[i][k] = s.x.d.A[pa][k] + cr[k];
-    }
-    __syncthreads();
-  }
-  for (int i = lane; i < nl; i += G) {
-    float IA[6], IV[6], x[6];
-    inertia_mul(s.x.d.Ib[i], s.x.d.A[i], IA);
-    inertia_mul(s.x.d.Ib[i], s.x.d.V[i], IV);
-    crf(s.x.d.V[i], IV, x);
-    float mg[3] = {0.f, 0.f, m.mass[i] * gravity};
-    float cxmg[3];
-    cross3(s.x.d.c[i], mg, cxmg);
-    for (int k = 0; k < 3; ++k) {
-      s.x.d.F[i][k] = IA[k] + x[k] - cxmg[k];
-      s.x.d.F[i][3 + k] = IA[3 + k] + x[3 + k] - mg[k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) Sq[k] = d.Sq[lane][k];
+      crm(V, Sq, cr);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) d.b.cr[lane][k] = cr[k];
     }
   }
   __syncthreads();
-  // inward accumulation: parents add their children (descending child index = oracle order)
-  for (int d = K.max_depth - 1; d >= 0; --d) {
-    for (int i = lane; i < nl; i += G) {
-      if (K.depth[i] != d) continue;
-      for (int t = 0; t < K.nchild[i]; ++t) {
-        int ch = K.child[i][t];
-        for (int k = 0; k < 6; ++k) s.x.d.F[i][k] += s.x.d.F[ch][k];
-        for (int k = 0; k < 10; ++k) s.x.d.Ic[i][k] += s.x.d.Ic[ch][k];
-      }
+  float f[6], Ib[10];
+  if (lane < nl) {
+    uint32_t path = tp.lpath & ~1u;
+    while (path) {
+      const int l = __builtin_ctz(path);
+      path &= path - 1u;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[k] += d.b.cr[l][k];
     }
-    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 10; ++k) Ib[k] = d.Ib[lane][k];
+    float IA[6], IV[6], x[6];
+    inertia_mul(Ib, A, IA);
+    inertia_mul(Ib, V, IV);
+    crf(V, IV, x);
+    const float mg[3] = {0.f, 0.f, Ib[0] * gravity};
+    float cxmg[3];
+    cross3(d.c[lane], mg, cxmg);
+    for (int k = 0; k < 3; ++k) {
+      f[k] = IA[k] + x[k] - cxmg[k];
+      f[3 + k] = IA[3 + k] + x[3 + k] - mg[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d.b.f[lane][k] = f[k];
   }
+  __syncthreads();
+  if (lane >= 1 && lane < nl) {
+    uint32_t sub = tp.lsub & ~(1u << lane);
+    while (sub) {
+      const int l = __builtin_ctz(sub);
+      sub &= sub - 1u;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) f[k] += d.b.f[l][k];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) Ib[k] += d.Ib[l][k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d.Sq[lane][k] = f[k];  // Sq is dead: F_i
+#pragma unroll
+    for (int k = 0; k < 10; ++k) d.Ic[lane][k] = Ib[k];
+  }
+  __syncthreads();
   float bj = 0.f;
   if (lane < nv) {
     const int j = lane;
     const int link = j < 6 ? 0 : j - 5;
-    float Cj = dot6(s.S[j], s.x.d.F[link]);
+    float F[6], Ic[10], S[6];
+    if (link == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) F[k] = d.b.f[0][k];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) Ic[k] = d.Ib[0][k];
+      uint32_t kids = K.root_kids;
+      while (kids) {
+        const int c = __builtin_ctz(kids);
+        kids &= kids - 1u;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) F[k] += d.Sq[c][k];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) Ic[k] += d.Ic[c][k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) F[k] = d.Sq[link][k];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) Ic[k] = d.Ic[link][k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) S[k] = s.S[j][k];
+    const float Cj = dot6(S, F);
     bj = (j < 6 ? 0.f : s.tau[j - 6]) - Cj;
     s.b[j] = bj;
-    inertia_mul(s.x.d.Ic[link], s.S[j], s.x.d.Fh[j]);
+    inertia_mul(Ic, S, d.Fh[j]);
   } else if (lane < 32) {
     s.b[lane] = 0.f;
   }
@@ -308,8 +424,10 @@ __device__ float dynamics(const Consts& K, EnvS& s, int lane, float gravity) {
 // Row j of the joint-space inertia H (lane j):
 //   H_jk = S_k . (Ic_link(j) S_j)  if dof k is on the path of link(j) (k ancestor-or-self),
 //        = S_j . (Ic_link(k) S_k)  if dof j is on the path of link(k),   else 0;  + armature.
+// The masks and the armature come from the constants (global / scalar loads): with the LDS copy in
+// Smem::topo the scheduler clusters all 12 NV LDS reads of S and Fh up front and spills.
 template <int NV>
-__device__ void h_row(const Consts& K, const EnvS& s, int lane, float (&Hr)[NV]) {
+__device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, float (&Hr)[NV]) {
   const int j = lane < NV ? lane : 0;
   const int lj = j < 6 ? 0 : j - 5;
   const uint32_t anc_j = K.ancmask[lj];
@@ -329,40 +447,52 @@ __device__ void h_row(const Consts& K, const EnvS& s, int lane, float (&Hr)[NV])
   }
 }
 
-// In-register Gauss-Jordan inverse: lane i holds row i; pivot row j is broadcast through LDS.
-// Same operation sequence as oracle/physics.c gj_inverse.
-// H^-1 by the symmetric sweep operator (same sequence as oracle/physics.c sweep_inverse).
-// Sweep on pivot k with the pre-sweep pivot row Q (d = Q_k, r = 1/d):
-//   row k:      a_kj <- r a_kj (j != k),        a_kk <- -r
-//   row i != k: a_ij <- a_ij - (r a_ik) Q_j,    a_ik <- r a_ik
-// Every intermediate matrix is symmetric, so lane i's pivot-column entry a_ik equals Q_i: it is read
-// from the broadcast row at the lane's own index and the register row is only ever indexed by
-// compile-time constants.  The pivot loop stays rolled (the whole step must fit the I-cache).
-// After all pivots the rows hold -H^-1; the sign is folded in at the end.
-template <int NV>
-__device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NV]) {
+// H^-1 by the block sweep operator on 2x2 pivot blocks, with column rotation (same arithmetic as
+// oracle/physics.c sweep_inverse).  H is padded to an even order NP with an identity row/column.
+// Lane i holds row i in Hr, rotated so that the current pivot columns are always Hr[0], Hr[1]: a
+// round shifts every row left by two and appends the two new pivot-column entries, so the register
+// row is only indexed by compile-time constants, no per-column select is needed and the pairs stay
+// aligned for packed FMAs.  Round on pivots P = {p, p+1} with D = (H_PP)^-1:
+//   the pivot lanes publish their rows with the pivot columns replaced by -I (Qh), and H_PP;
+//   row' = alpha row - (beta0 Qh_0 + beta1 Qh_1) with
+//     (alpha, beta) = (1, a_iP D)  for i not in P   (a_ij - a_iP D a_Pj;  a_iP <- a_iP D)
+//     (alpha, beta) = (0, -D_t)    for pivot lane t (D a_Pj;  a_PP <- -D).
+// After all rounds the rotation is back to the identity and the rows hold -H^-1.
+template <int NP>
+__device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
+  static_assert(NP % 2 == 0, "pairs");
 #pragma unroll 1
-  for (int k = 0; k < NV; ++k) {
-    float* Q = s.x.piv[k & 1];
-    if (lane == k) {
+  for (int p = 0; p < NP; p += 2) {
+    // one buffer: LDS operations of a wave complete in issue order, so the next round's writes
+    // cannot overtake this round's reads
+    float(&Q)[2][32] = s.x.sw.q;
+    float* Pb = s.x.sw.pb;
+    const int t = lane - p;
+    if (t == 0 || t == 1) {
+      Pb[2 * t] = Hr[0];
+      Pb[2 * t + 1] = Hr[1];
 #pragma unroll
-      for (int j = 0; j < NV; ++j) Q[j] = Hr[j];
+      for (int j = 2; j < NP; ++j) Q[t][j] = Hr[j];
     }
     __syncthreads();
-    const float d = Q[k];
-    const float r = 1.0f / d;
-    const bool piv = lane == k;
-    const float g = piv ? 0.f : (lane < NV ? Q[lane] : 0.f) * r;
-    const float alpha = piv ? r : 1.f;
-    const float c = piv ? -r : g;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const float t = alpha * Hr[j] - g * Q[j];
-      Hr[j] = (j == k) ? c : t;
+    const float P00 = Pb[0], P01 = Pb[1], P10 = Pb[2], P11 = Pb[3];
+    const float id = 1.0f / (P00 * P11 - P01 * P10);
+    const float D00 = P11 * id, D01 = -P01 * id, D10 = -P10 * id, D11 = P00 * id;
+    float alpha, b0, b1;
+    if (t == 0) {
+      alpha = 0.f; b0 = -D00; b1 = -D01;
+    } else if (t == 1) {
+      alpha = 0.f; b0 = -D10; b1 = -D11;
+    } else {
+      alpha = 1.f;
+      b0 = Hr[0] * D00 + Hr[1] * D10;
+      b1 = Hr[0] * D01 + Hr[1] * D11;
     }
-  }
 #pragma unroll
-  for (int j = 0; j < NV; ++j) Hr[j] = lane < NV ? -Hr[j] : 0.f;
+    for (int j = 2; j < NP; ++j) Hr[j - 2] = alpha * Hr[j] - (b0 * Q[0][j] + b1 * Q[1][j]);
+    Hr[NP - 2] = b0;
+    Hr[NP - 1] = b1;
+  }
   __syncthreads();
 }
 
@@ -376,11 +506,12 @@ __device__ void emit_contact(EnvS& s, int slot, int link, int stone, int foot, c
   for (int k = 0; k < 3; ++k) { s.cn[slot][k] = n[k]; s.cpt[slot][k] = P[k] - n[k] * r; }
 }
 
-__device__ void collide(const Consts& K, EnvS& s, int lane) {
+__device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   const as_model_t& m = K.model;
   const float* h = K.sim.stone_half;
-  const int nst = K.task.num_steps;
-  // broadphase: stones within 1.8 m of the root link origin
+  const float margin = K.sim.margin;
+  const int nst = K.task.num_steps, ng = m.num_geoms;
+  // broadphase (lane = stone): stones within 1.8 m of the root link origin
   bool isc = false;
   if (lane < nst) {
     float o = 0.f;
@@ -394,80 +525,80 @@ __device__ void collide(const Consts& K, EnvS& s, int lane) {
   const int half = (threadIdx.x >> 5) & 1;
   uint32_t mine = (uint32_t)(bal >> (32 * half));
   if (isc) s.cand[__popc(mine & ((1u << lane) - 1u))] = lane;
-  if (lane == 0) s.ncand = __popc(mine);
+  const int ncand = __popc(mine);
+  // geom segment in the O frame (lane = geom), formed once for all candidate stones
+  const bool gv = lane < ng;
+  const int g = gv ? lane : 0;
+  const int link = m.geom_link[g], gtype = m.geom_type[g], foot = m.geom_foot[g];
+  const float r = m.geom_radius[g];
+  float a[3], bb[3];
+  {
+    float t0[3], t1[3];
+    matvec3(s.R[link], m.geom_p0[g], t0);
+    matvec3(s.R[link], m.geom_p1[g], t1);
+    for (int k = 0; k < 3; ++k) { a[k] = s.p[link][k] + t0[k]; bb[k] = s.p[link][k] + t1[k]; }
+  }
+  const float L = sqrtf((bb[0] - a[0]) * (bb[0] - a[0]) + (bb[1] - a[1]) * (bb[1] - a[1]) +
+                        (bb[2] - a[2]) * (bb[2] - a[2]));
+  const float mid[3] = {0.5f * (a[0] + bb[0]), 0.5f * (a[1] + bb[1]), 0.5f * (a[2] + bb[2])};
   __syncthreads();
-  const int ncand = s.ncand, ng = m.num_geoms;
-  const int npairs = ng * ncand;
+  // narrowphase: candidate stones in ascending order, geoms in lane order within a stone
   int base = 0;
-  for (int p0 = 0; p0 < npairs; p0 += G) {
-    int p = p0 + lane;
+  for (int ci = 0; ci < ncand; ++ci) {
+    const int st = s.cand[ci];
     int cnt = 0;
-    int link = 0, stone = 0, foot = -1;
-    float P0[3], N0[3], P1[3], N1[3], P2[3], N2[3], SEP0 = 0.f, SEP1 = 0.f, SEP2 = 0.f, rr = 0.f;
-    if (p < npairs) {
-      int g = p / ncand, st = s.cand[p % ncand];
-      link = m.geom_link[g]; stone = st; foot = m.geom_foot[g];
-      float r = m.geom_radius[g];
-      rr = r;
-      float a[3], bb[3], t0[3], t1[3];
-      matvec3(s.R[link], m.geom_p0[g], t0);
-      matvec3(s.R[link], m.geom_p1[g], t1);
-      for (int k = 0; k < 3; ++k) { a[k] = s.p[link][k] + t0[k]; bb[k] = s.p[link][k] + t1[k]; }
+    float P0[3], N0[3], P1[3], N1[3], P2[3], N2[3], SEP0 = 0.f, SEP1 = 0.f, SEP2 = 0.f;
+    if (gv) {
       float c[3];
       for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * st + k] - s.root_pos[k];
       float nr[3];
-      if (m.geom_type[g] == 0) {
+      if (gtype == 0) {
         float sd = sd_box(a, c, h, nr) - r;
-        if (sd < K.sim.margin) {
+        if (sd < margin) {
           for (int k = 0; k < 3; ++k) { P0[k] = a[k]; N0[k] = nr[k]; }
           SEP0 = sd;
           cnt = 1;
         }
-      } else {
-        float L = sqrtf((bb[0] - a[0]) * (bb[0] - a[0]) + (bb[1] - a[1]) * (bb[1] - a[1]) +
-                        (bb[2] - a[2]) * (bb[2] - a[2]));
-        float mid[3] = {0.5f * (a[0] + bb[0]), 0.5f * (a[1] + bb[1]), 0.5f * (a[2] + bb[2])};
-        if (sd_box(mid, c, h, nr) <= 0.5f * L + r + K.sim.margin) {
-          float n0[3], n1[3], tn[3];
-          float s0 = sd_box(a, c, h, n0) - r;
-          float s1 = sd_box(bb, c, h, n1) - r;
-          const float gr = 0.6180339887f;
-          float lo = 0.f, hi = 1.f;
-          float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
-          float Q1[3], Q2[3];
-          for (int k = 0; k < 3; ++k) { Q1[k] = a[k] + x1 * (bb[k] - a[k]); Q2[k] = a[k] + x2 * (bb[k] - a[k]); }
-          float f1 = sd_box(Q1, c, h, tn), f2 = sd_box(Q2, c, h, tn);
+      } else if (sd_box(mid, c, h, nr) <= 0.5f * L + r + margin) {
+        float n0[3], n1[3], tn[3];
+        float s0 = sd_box(a, c, h, n0) - r;
+        float s1 = sd_box(bb, c, h, n1) - r;
+        const float gr = 0.6180339887f;
+        float lo = 0.f, hi = 1.f;
+        float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
+        float Q1[3], Q2[3];
+        for (int k = 0; k < 3; ++k) { Q1[k] = a[k] + x1 * (bb[k] - a[k]); Q2[k] = a[k] + x2 * (bb[k] - a[k]); }
+        float f1 = sd_box(Q1, c, h, tn), f2 = sd_box(Q2, c, h, tn);
 #pragma unroll 1
-          for (int it = 0; it < GOLDEN_ITERS; ++it) {
-            if (f1 < f2) {
-              hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
-              for (int k = 0; k < 3; ++k) Q1[k] = a[k] + x1 * (bb[k] - a[k]);
-              f1 = sd_box(Q1, c, h, tn);
-            } else {
-              lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
-              for (int k = 0; k < 3; ++k) Q2[k] = a[k] + x2 * (bb[k] - a[k]);
-              f2 = sd_box(Q2, c, h, tn);
-            }
-          }
-          float ts = 0.5f * (lo + hi), Ps[3], ns[3];
-          for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (bb[k] - a[k]);
-          float ss = sd_box(Ps, c, h, ns) - r;
-          bool e0 = s0 < K.sim.margin, e1 = s1 < K.sim.margin;
-          bool es = ss < K.sim.margin && ss < fminf(s0, s1) - 0.002f;
-          // pack the emitted contacts in (t=0, t=1, t*) order into slots 0..2
-          for (int k = 0; k < 3; ++k) { P0[k] = a[k]; N0[k] = n0[k]; }
-          SEP0 = s0;
-          if (e0) {
-            for (int k = 0; k < 3; ++k) { P1[k] = bb[k]; N1[k] = n1[k]; P2[k] = Ps[k]; N2[k] = ns[k]; }
-            SEP1 = s1; SEP2 = ss;
-            if (!e1) { for (int k = 0; k < 3; ++k) { P1[k] = Ps[k]; N1[k] = ns[k]; } SEP1 = ss; }
+        for (int it = 0; it < GOLDEN_ITERS; ++it) {
+          if (f1 < f2) {
+            hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
+            for (int k = 0; k < 3; ++k) Q1[k] = a[k] + x1 * (bb[k] - a[k]);
+            f1 = sd_box(Q1, c, h, tn);
           } else {
-            for (int k = 0; k < 3; ++k) { P0[k] = bb[k]; N0[k] = n1[k]; P1[k] = Ps[k]; N1[k] = ns[k]; }
-            SEP0 = s1; SEP1 = ss;
-            if (!e1) { for (int k = 0; k < 3; ++k) { P0[k] = Ps[k]; N0[k] = ns[k]; } SEP0 = ss; }
+            lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
+            for (int k = 0; k < 3; ++k) Q2[k] = a[k] + x2 * (bb[k] - a[k]);
+            f2 = sd_box(Q2, c, h, tn);
           }
-          cnt = (int)e0 + (int)e1 + (int)es;
         }
+        float ts = 0.5f * (lo + hi), Ps[3], ns[3];
+        for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (bb[k] - a[k]);
+        float ss = sd_box(Ps, c, h, ns) - r;
+        bool e0 = s0 < margin, e1 = s1 < margin;
+        bool es = ss < margin && ss < fminf(s0, s1) - 0.002f;
+        // pack the emitted contacts in (t=0, t=1, t*) order into slots 0..2
+        for (int k = 0; k < 3; ++k) { P0[k] = a[k]; N0[k] = n0[k]; }
+        SEP0 = s0;
+        if (e0) {
+          for (int k = 0; k < 3; ++k) { P1[k] = bb[k]; N1[k] = n1[k]; P2[k] = Ps[k]; N2[k] = ns[k]; }
+          SEP1 = s1; SEP2 = ss;
+          if (!e1) { for (int k = 0; k < 3; ++k) { P1[k] = Ps[k]; N1[k] = ns[k]; } SEP1 = ss; }
+        } else {
+          for (int k = 0; k < 3; ++k) { P0[k] = bb[k]; N0[k] = n1[k]; P1[k] = Ps[k]; N1[k] = ns[k]; }
+          SEP0 = s1; SEP1 = ss;
+          if (!e1) { for (int k = 0; k < 3; ++k) { P0[k] = Ps[k]; N0[k] = ns[k]; } SEP0 = ss; }
+        }
+        cnt = (int)e0 + (int)e1 + (int)es;
       }
     }
     int incl = cnt;
@@ -478,9 +609,9 @@ __device__ void collide(const Consts& K, EnvS& s, int lane) {
     }
     int total = __shfl(incl, 31, 32);
     int slot = base + incl - cnt;
-    if (cnt > 0) emit_contact(s, slot, link, stone, foot, P0, N0, SEP0, rr);
-    if (cnt > 1) emit_contact(s, slot + 1, link, stone, foot, P1, N1, SEP1, rr);
-    if (cnt > 2) emit_contact(s, slot + 2, link, stone, foot, P2, N2, SEP2, rr);
+    if (cnt > 0) emit_contact(s, slot, link, st, foot, P0, N0, SEP0, r);
+    if (cnt > 1) emit_contact(s, slot + 1, link, st, foot, P1, N1, SEP1, r);
+    if (cnt > 2) emit_contact(s, slot + 2, link, st, foot, P2, N2, SEP2, r);
     base += total;
   }
   __syncthreads();
@@ -499,19 +630,31 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
 
 // ------------------------------------------------------------------------------------------------
 template <int NV>
-__device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* mask_out, Stamp& ts) {
+__device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, uint32_t* mask_out,
+                        Stamp& ts) {
+  // Opaque copies of the constants pointer and the lane id: everything derived from them below
+  // (model-table loads, LDS addresses, lane masks) is loop-invariant, and without this the
+  // compiler hoists all of it out of the substep loop and spills it.
+  CK* kp = (CK*)(&K0);
+  int lane = lane0;
+  asm volatile("" : "+s"(kp), "+v"(lane));
+  const Consts& K = *(const Consts*)(kp);
+  const Topo& tp = tp0;  // LDS (Smem::topo)
   const as_model_t& m = K.model;
   const float dt = K.sim.dt;
   const int nh = m.num_hinges;
-  fk(K, s, lane);
+  fk<true>(K, s, lane, tp);
   ts.mark(kStFK);
-  link_quantities(K, s, lane);
+  dynamics(K, s, lane, tp, K.sim.gravity);
   ts.mark(kStLinkQ);
-  dynamics(K, s, lane, K.sim.gravity);
-  float Hr[NV];
-  h_row<NV>(K, s, lane, Hr);
+  constexpr int NP = NV + (NV & 1);  // sweep order, padded to pairs with an identity row/column
+  float Hr[NP];
+  h_row<NV>(K, s, lane, tp, *reinterpret_cast<float(*)[NV]>(Hr));
+  if (NP > NV) Hr[NP - 1] = lane == NV ? 1.f : 0.f;
   ts.mark(kStDyn);
-  sweep_inverse<NV>(s, lane, Hr);  // Hr <- row `lane` of H^-1
+  sweep_inverse<NP>(s, lane, Hr);  // Hr <- row `lane` of -H^-1
+#pragma unroll
+  for (int j = 0; j < NV; ++j) Hr[j] = lane < NV ? -Hr[j] : 0.f;
   ts.mark(kStChol);
   // u* = u + dt H^-1 b   (b broadcast from LDS)
   float uj = 0.f;
@@ -555,12 +698,11 @@ __device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* 
   int lo_v = 0, hi_v = 0;
   float err_lo = 0.f, err_hi = 0.f;
   if (lane < nh) {
-    int i = lane + 1;
     float qv = s.qi[lane], pred = qv + dt * s.u[6 + lane];
-    err_lo = m.lower[i] - qv;
-    err_hi = qv - m.upper[i];
-    lo_v = pred < m.lower[i];
-    hi_v = pred > m.upper[i];
+    err_lo = tp.lo - qv;
+    err_hi = qv - tp.hi;
+    lo_v = pred < tp.lo;
+    hi_v = pred > tp.hi;
   }
   int cnt = lo_v + hi_v;
   int incl = cnt;
@@ -602,7 +744,7 @@ __device__ void substep(const Consts& K, Smem& sm, EnvS& s, int lane, uint32_t* 
     if (r < nrow && lane < NV) {
       int lk = s.rlink[r];
       if (lk >= 0) {
-        if ((K.ancmask[lk] >> lane) & 1u) jv = dot6(Sj, s.rf6[r]);
+        if ((tp.dsub >> lk) & 1u) jv = dot6(Sj, s.rf6[r]);
       } else if (-1 - lk == lane) {
         jv = s.rsign[r];
       }
@@ -769,25 +911,37 @@ __device__ void compute_useful(const Consts& K, const float* root_pos, const flo
 }
 
 // ------------------------------------------------------------------------------------------------
+// XCD-aware env mapping.  Workgroup b is dispatched to XCD b % 8; a 128-B line of an SoA field
+// holds 32 consecutive envs = 16 workgroups, which with the identity mapping would be split over all
+// eight per-XCD L2s (each fetching and writing back the whole line for 16 useful bytes).  Give XCD x
+// a contiguous range of env pairs instead (a bijection for any grid size; placement only affects
+// speed, never results).
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7, slot = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
+}
+
 template <int NV>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_step(StepArgs P) {
   __shared__ Smem sm;
   // model / plan constants stay in global memory (5.7 KB, L1/K$-resident): LDS is the occupancy
   // budget, see EnvS
-  const Consts& K = *P.consts;
+  const Consts& K = *(const Consts*)(CK*)P.consts;
   const int el = threadIdx.x >> 5, lane = threadIdx.x & 31;
   const int n = P.n;
-  const int e_raw = blockIdx.x * EPB + el;
+  const int e_raw = xcd_block(blockIdx.x, gridDim.x) * EPB + el;
   const bool valid = e_raw < n;
   const int e = valid ? e_raw : n - 1;
   EnvS& s = sm.env[el];
   const as_state_t& st = P.st;
-  Stamp ts{P.stamps, 0ull};
+  Stamp ts{P.stamps, sm.stamp_acc, 0ull};
   ts.start();
   __syncthreads();
   const as_model_t& m = K.model;
   const int nh = m.num_hinges;
   const as_task_t& T = K.task;
+  if (el == 0) sm.topo[lane] = load_topo(K, lane);
+  const Topo& tp = sm.topo[lane];
   // ---- load
   if (lane < 3) {
     s.root_pos[lane] = st.root_pos[lane * n + e];
@@ -814,8 +968,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const bool do_physics = P.mode == kModeStep || P.mode == kModePhysics;
   // ---- physics
   if (do_physics) {
-    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, mask, ts);
-    fk(K, s, lane);  // FK of the final pose for body_pos_w (articulation_data.py:439)
+    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, mask, ts);
+    fk<false>(K, s, lane, tp);  // FK of the final pose for body_pos_w (articulation_data.py:439)
     if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
   }
   if (lane == 0 && !do_physics) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
@@ -957,7 +1111,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       episode += 1u;
     }
     __syncthreads();
-    fk(K, s, lane);  // body_pos of the reset pose (write_joint_state_to_sim invalidates FK)
+    fk<false>(K, s, lane, tp);  // body_pos of the reset pose (write_joint_state_to_sim invalidates FK)
     if (done) {
       const int ls[3] = {m.torso_link, m.foot_link[0], m.foot_link[1]};
       for (int b = 0; b < 3; ++b)
@@ -997,12 +1151,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
   }
   ts.mark(kStStore);
+  ts.flush();
 }
 
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_obs(ObsArgs P) {
-  const as_task_t& T = P.consts->task;
-  const as_model_t& m = P.consts->model;
+  const Consts& K = *(const Consts*)(CK*)P.consts;
+  const as_task_t& T = K.task;
+  const as_model_t& m = K.model;
   const int n = P.n;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int any_reset = P.counters[0];
@@ -1020,7 +1176,7 @@ __global__ __launch_bounds__(256) void k_obs(ObsArgs P) {
   float pot = st.pot[e], old_pot = st.old_pot[e];
   float fc[2] = {st.foot_contact[e], st.foot_contact[n + e]};
   Useful u;
-  compute_useful(*P.consts, rp, rq, bp, st.stones + e, n, st.contact_mask[e], st.contact_mask[n + e], idx, prev,
+  compute_useful(K, rp, rq, bp, st.stones + e, n, st.contact_mask[e], st.contact_mask[n + e], idx, prev,
                  next, count, swing, pot, old_pot, fc, any_reset != 0, u);
   if (any_reset) {  // tick #2 results persist (allsteps_env.py:567)
     st.idx[e] = idx; st.prev[e] = prev; st.next[e] = next; st.count[e] = count; st.swing[e] = swing;
@@ -1057,7 +1213,7 @@ __device__ float lerp_t(float a, float b, float w) {  // torch.lerp (ATen Lerp.h
 }
 
 __global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
-  const as_task_t& T = P.consts->task;
+  const as_task_t& T = ((const Consts*)(CK*)P.consts)->task;
   const int n = P.n;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;

@@ -12,7 +12,8 @@
  *   1. FK of all links, spatial quantities in a world-aligned frame with origin at the root link
  *      origin (O).  Generalised velocity u = [v_com0 (3), w0 (3), qd hinges (nh)].
  *   2. RNEA with qdd = 0 -> bias C(q, u) (Coriolis, centrifugal, gyroscopic, gravity).
- *   3. CRBA -> joint-space inertia H (+ armature on the hinge diagonal), Cholesky H = L L^T.
+ *   3. CRBA -> joint-space inertia H (+ armature on the hinge diagonal); H^-1 by the symmetric
+ *      sweep operator.  Subtree sums (composite inertias, RNEA forces) in the kernel's order.
  *   4. u* = u + dt H^-1 (tau - C).
  *   5. Contacts (robot spheres/capsules vs the 20 axis-aligned stone boxes, speculative margin)
  *      and joint-limit rows; projected Gauss-Seidel on impulses (normal >= 0, box friction,
@@ -113,6 +114,27 @@ static void crf(const float V[6], const float Fv[6], float o[6]) {
   for (int k = 0; k < 3; ++k) { o[k] = a[k] + b[k]; o[3 + k] = c[k]; }
 }
 
+static int is_ancestor(const or_model_t* m, int a, int l) {
+  while (l > a) l = m->parent[l];
+  return l == a;
+}
+
+/* Subtree sums in the order of the HIP kernel (dynamics() in csrc/allsteps_kernels.hip, one lane per
+ * link): a non-root link adds the values of its proper descendants, in ascending link index, to its
+ * own value; the root adds the totals of its children, in ascending index, to its own. */
+static void subtree_sums(const or_model_t* m, int nl, int w, const float* own, float* tot) {
+  for (int i = 1; i < nl; ++i) {
+    for (int k = 0; k < w; ++k) tot[i * w + k] = own[i * w + k];
+    for (int l = i + 1; l < nl; ++l)
+      if (is_ancestor(m, i, l))
+        for (int k = 0; k < w; ++k) tot[i * w + k] += own[l * w + k];
+  }
+  for (int k = 0; k < w; ++k) tot[k] = own[k];
+  for (int c = 1; c < nl; ++c)
+    if (m->parent[c] == 0)
+      for (int k = 0; k < w; ++k) tot[k] += tot[c * w + k];
+}
+
 /* FK + motion subspace + spatial inertias. q_int: hinge angles in link order (link i -> q_int[i-1]). */
 static void kinematics(const or_model_t* m, const float root_quat[4], const float* q_int, kin_t* K) {
   const int nl = m->num_links;
@@ -183,9 +205,7 @@ static void kinematics(const or_model_t* m, const float root_quat[4], const floa
     cross(o, a, S + 3);
   }
   /* composite inertias (world frame: plain sums over the subtree) */
-  for (int i = 0; i < nl; ++i) memcpy(K->Ic[i], K->Ib[i], sizeof(float) * 10);
-  for (int i = nl - 1; i >= 1; --i)
-    for (int k = 0; k < 10; ++k) K->Ic[m->parent[i]][k] += K->Ic[i][k];
+  subtree_sums(m, nl, 10, &K->Ib[0][0], &K->Ic[0][0]);
 }
 
 /* dofs influencing link i: hinge dofs on the path to the root (deepest first), then root dofs */
@@ -232,7 +252,7 @@ static void link_velocities(const or_model_t* m, const kin_t* K, const float* u,
 }
 
 static void rnea_bias(const or_model_t* m, const kin_t* K, const float* u, float gravity, float* C) {
-  float V[OR_MAX_LINKS][6], A[OR_MAX_LINKS][6], Fl[OR_MAX_LINKS][6];
+  float V[OR_MAX_LINKS][6], A[OR_MAX_LINKS][6], fb[OR_MAX_LINKS][6], Fl[OR_MAX_LINKS][6];
   link_velocities(m, K, u, V);
   /* A_0 = [0; v_c0 x w] */
   float vxw[3];
@@ -255,40 +275,54 @@ static void rnea_bias(const or_model_t* m, const kin_t* K, const float* u, float
     float cxmg[3];
     cross(K->c[i], mg, cxmg);
     for (int k = 0; k < 3; ++k) {
-      Fl[i][k] = IA[k] + x[k] - cxmg[k];
-      Fl[i][3 + k] = IA[3 + k] + x[3 + k] - mg[k];
+      fb[i][k] = IA[k] + x[k] - cxmg[k];
+      fb[i][3 + k] = IA[3 + k] + x[3 + k] - mg[k];
     }
   }
-  for (int i = K->nl - 1; i >= 1; --i)
-    for (int k = 0; k < 6; ++k) Fl[m->parent[i]][k] += Fl[i][k];
+  subtree_sums(m, K->nl, 6, &fb[0][0], &Fl[0][0]);
   for (int j = 0; j < K->nv; ++j) {
     int link = j < OR_NDOF_ROOT ? 0 : j - OR_NDOF_ROOT + 1;
     C[j] = dot6(K->S[j], Fl[link]);
   }
 }
 
-/* Inverse of the SPD joint-space inertia by the symmetric sweep operator (no pivoting needed for
- * SPD).  Sweep on pivot k with the pre-sweep pivot row Q (d = Q_k, r = 1/d):
- *   row k: a_kj <- r a_kj (j != k), a_kk <- -r;   row i != k: g = r a_ik, a_ij <- a_ij - g Q_j,
- *   a_ik <- g.
- * After all pivots a = -H^-1; the result is negated.  The HIP kernel runs the same sequence with
- * one row per lane (a_ik = Q_i by symmetry). */
-static void sweep_inverse(float* a, int n) {
-  float Q[NV_MAX];
-  for (int k = 0; k < n; ++k) {
-    for (int j = 0; j < n; ++j) Q[j] = a[k * n + j];
-    const float d = Q[k], r = 1.0f / d;
-    for (int i = 0; i < n; ++i) {
-      float* row = a + i * n;
-      if (i == k) {
-        for (int j = 0; j < n; ++j) row[j] = (j == k) ? -r : r * row[j];
+/* Inverse of the SPD joint-space inertia by the block sweep operator on 2x2 pivot blocks (no
+ * pivoting needed for SPD), in the arithmetic of the HIP kernel (sweep_inverse in
+ * csrc/allsteps_kernels.hip).  The matrix is padded to even order with an identity row/column.
+ * Round on P = {p, p+1}, D = (a_PP)^-1 via the 2x2 adjugate; Qh_t = row p+t of a with the pivot
+ * columns replaced by -I;  row' = alpha row_base - (beta0 Qh_0 + beta1 Qh_1), where row_base has its
+ * pivot-column entries zeroed and (alpha, beta) = (1, a_iP D) for i not in P, (0, -D_t) for the
+ * pivot rows.  After all rounds a = -H^-1; the result is negated. */
+static void sweep_inverse(float* h, int n) {
+  const int np = n + (n & 1);
+  float a[NV_MAX + 1][NV_MAX + 1], Q[2][NV_MAX + 1];
+  for (int i = 0; i < np; ++i)
+    for (int j = 0; j < np; ++j) a[i][j] = (i < n && j < n) ? h[i * n + j] : (i == j ? 1.f : 0.f);
+  for (int p = 0; p < np; p += 2) {
+    const float P00 = a[p][p], P01 = a[p][p + 1], P10 = a[p + 1][p], P11 = a[p + 1][p + 1];
+    const float id = 1.0f / (P00 * P11 - P01 * P10);
+    const float D00 = P11 * id, D01 = -P01 * id, D10 = -P10 * id, D11 = P00 * id;
+    for (int t = 0; t < 2; ++t)
+      for (int j = 0; j < np; ++j) Q[t][j] = (j == p) ? (t == 0 ? -1.f : 0.f) : (j == p + 1 ? (t == 1 ? -1.f : 0.f) : a[p + t][j]);
+    for (int i = 0; i < np; ++i) {
+      float alpha, b0, b1;
+      if (i == p) {
+        alpha = 0.f; b0 = -D00; b1 = -D01;
+      } else if (i == p + 1) {
+        alpha = 0.f; b0 = -D10; b1 = -D11;
       } else {
-        const float g = Q[i] * r;
-        for (int j = 0; j < n; ++j) row[j] = (j == k) ? g : row[j] - g * Q[j];
+        alpha = 1.f;
+        b0 = a[i][p] * D00 + a[i][p + 1] * D10;
+        b1 = a[i][p] * D01 + a[i][p + 1] * D11;
+      }
+      for (int j = 0; j < np; ++j) {
+        const float base = (j == p || j == p + 1) ? 0.f : a[i][j];
+        a[i][j] = alpha * base - (b0 * Q[0][j] + b1 * Q[1][j]);
       }
     }
   }
-  for (int i = 0; i < n * n; ++i) a[i] = -a[i];
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) h[i * n + j] = -a[i][j];
 }
 
 /* x = A b (row-major, sequential in k) */
@@ -356,17 +390,29 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
     }
     if (o < 1.8f * 1.8f) cand[nc++] = s;
   }
+  /* geom segments in the O frame */
+  float ga[OR_MAX_GEOMS][3], gb[OR_MAX_GEOMS][3], gL[OR_MAX_GEOMS];
   for (int g = 0; g < m->num_geoms; ++g) {
     int l = m->geom_link[g];
-    float r = m->geom_radius[g];
-    float a[3], b[3], t0[3], t1[3];
+    float t0[3], t1[3];
     matvec3(K->R[l], m->geom_p0[g], t0);
     matvec3(K->R[l], m->geom_p1[g], t1);
-    for (int k = 0; k < 3; ++k) { a[k] = K->p[l][k] + t0[k]; b[k] = K->p[l][k] + t1[k]; }
-    float L = sqrtf((b[0] - a[0]) * (b[0] - a[0]) + (b[1] - a[1]) * (b[1] - a[1]) + (b[2] - a[2]) * (b[2] - a[2]));
-    for (int ci = 0; ci < nc; ++ci) {
-      int s = cand[ci];
-      const float* c = stones_rel + 3 * s;
+    for (int k = 0; k < 3; ++k) { ga[g][k] = K->p[l][k] + t0[k]; gb[g][k] = K->p[l][k] + t1[k]; }
+    const float* a = ga[g];
+    const float* b = gb[g];
+    gL[g] = sqrtf((b[0] - a[0]) * (b[0] - a[0]) + (b[1] - a[1]) * (b[1] - a[1]) + (b[2] - a[2]) * (b[2] - a[2]));
+  }
+  /* narrowphase: candidate stones in ascending order, geoms in index order within a stone (the HIP
+   * kernel runs one geom per lane and loops over the candidates) */
+  for (int ci = 0; ci < nc; ++ci) {
+    int s = cand[ci];
+    const float* c = stones_rel + 3 * s;
+    for (int g = 0; g < m->num_geoms; ++g) {
+      int l = m->geom_link[g];
+      float r = m->geom_radius[g];
+      const float* a = ga[g];
+      const float* b = gb[g];
+      float L = gL[g];
       float nr[3];
       if (m->geom_type[g] == 0) {
         float sd = sd_box(a, c, h, nr) - r;

@@ -423,7 +423,7 @@ void or_task_reset_all(const or_model_t* model, const or_task_t* task, or_state_
   /* DRL:256-294 reset(): _reset_idx(all envs) -> write_data_to_sim/forward -> _get_observations */
   const int n = st->n;
   useful_t* u = (useful_t*)malloc(sizeof(useful_t) * (size_t)n);
-  uint8_t* done = (uint8_t*)malloc((size_t)n);
+  uint8_t* done = (uint8_t*)calloc((size_t)n + 1, 1);
   long long idx_sum = 0;
   for (int e = 0; e < n; ++e) { done[e] = 1; idx_sum += st->idx[e]; }
   reset_and_tick2(model, task, st, done, idx_sum, reset_draws, seed, NULL, NULL, NULL, NULL, u);
@@ -438,7 +438,7 @@ void or_task_post_physics(const or_model_t* model, const or_task_t* task, or_sta
                           uint8_t* trunc, int32_t* any_reset) {
   const int n = st->n;
   useful_t* u = (useful_t*)malloc(sizeof(useful_t) * (size_t)n);
-  uint8_t* done = (uint8_t*)malloc((size_t)n);
+  uint8_t* done = (uint8_t*)calloc((size_t)n + 1, 1);
   float a[21];
   int nreset = 0;
   long long idx_sum = 0;

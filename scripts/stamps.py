@@ -12,7 +12,7 @@ import torch  # noqa: E402
 from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv  # noqa: E402
 from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg  # noqa: E402
 
-PHASES = ["load", "fk", "linkq", "dyn", "chol", "solve", "collide", "rows", "wsolve", "pgs", "integrate", "task",
+PHASES = ["load", "fk", "rnea", "hrow", "sweep", "solve", "collide", "rows", "wsolve", "pgs", "integrate", "task",
           "reset", "store"]
 
 
