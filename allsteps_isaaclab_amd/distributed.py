@@ -1,0 +1,134 @@
+"""Multi-GPU plumbing for the Allsteps step: one process per GPU, envs sharded, no data-path
+collective inside ``env.step``.
+
+* Env sharding.  Rank r of W owns global env ids ``[r N, (r+1) N)``: its ``AllstepsEnv`` is built with
+  ``env_id_offset = r N`` so the in-kernel Philox reset draws are keyed by (seed, global env id): with
+  one seed on every rank a sharded run is bit-identical to one GPU stepping all ``W N`` envs
+  (tests/test_gpu_parity.py::test_shards_match_unsharded).  ``make_sharded_env`` follows train.py:100
+  instead (``seed + rank``), which the reference does for its per-rank envs.
+* The curriculum mean stays per process (allsteps_env.py:471 reads the process's own envs, which is
+  what the reference does under ``--distributed``); ``global_curriculum_mean`` is the optional
+  4-byte all-reduce variant.
+* The only exchange is at the PPO update boundary: ``RolloutGather`` all-gathers a horizon of rollout
+  tensors from every rank in ONE collective per dtype over RCCL (xGMI ring; the payload is packed
+  into a single flat buffer so the ring runs at message sizes where the per-link bandwidth, not
+  latency, is the bound).  With the gloo backend (CPU tests) the same code path runs.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ShardInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+
+    def env_offset(self, envs_per_rank: int) -> int:
+        return self.rank * envs_per_rank
+
+    def seed(self, base_seed: int) -> int:
+        return base_seed + self.rank
+
+
+def shard_info() -> ShardInfo:
+    """Rank / world / local rank from torch.distributed (or the launcher's environment)."""
+    if dist.is_available() and dist.is_initialized():
+        return ShardInfo(dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", dist.get_rank())))
+    return ShardInfo(int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+                     int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def init_process_group(backend: str | None = None) -> ShardInfo:
+    """torch.distributed.run rendezvous (MASTER_ADDR defaults to 127.0.0.1); nccl = RCCL on ROCm."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    info = shard_info()
+    if info.world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(info.local_rank)
+            kw["device_id"] = torch.device(f"cuda:{info.local_rank}")
+        dist.init_process_group(backend, **kw)
+        info = shard_info()
+    return info
+
+
+def make_sharded_env(cfg, info: ShardInfo | None = None, **kwargs):
+    """AllstepsEnv for this rank's env shard (device cuda:local_rank, offset ids, seed + rank)."""
+    from .envs.allsteps_env import AllstepsEnv
+
+    info = info or shard_info()
+    cfg.sim.device = f"cuda:{info.local_rank}"
+    if cfg.seed is not None:
+        cfg.seed = info.seed(cfg.seed)
+    return AllstepsEnv(cfg, env_id_offset=info.env_offset(int(cfg.scene.num_envs)), **kwargs)
+
+
+def global_curriculum_mean(env, group=None) -> float:
+    """Mean curr_target_index over ALL ranks' envs (one 8-byte all-reduce) -- an opt-in variant of
+    the per-process gate of allsteps_env.py:471."""
+    idx = env.curr_target_index
+    t = torch.stack([idx.sum().to(torch.float64), torch.tensor(float(idx.numel()), dtype=torch.float64,
+                                                               device=idx.device)])
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, group=group)
+    return float(t[0] / t[1])
+
+
+class RolloutGather:
+    """All-gather of a PPO horizon of rollout tensors across ranks.
+
+    ``gather({"obs": [H, N, 59], "actions": [H, N, 21], "rewards": [H, N], "dones": [H, N] (bool), ...})``
+    returns the same keys with the env axis (axis 1) concatenated over ranks in rank order
+    ([H, W N, ...]), i.e. global env id order.  Tensors are packed per dtype into one flat send
+    buffer; receive buffers are cached across calls (same shapes every horizon).
+    """
+
+    def __init__(self, group=None, env_axis: int = 1):
+        self.group = group
+        self.env_axis = env_axis
+        self._recv: dict = {}
+
+    def _world(self) -> int:
+        return dist.get_world_size(self.group) if dist.is_initialized() else 1
+
+    def gather(self, tensors: dict[str, torch.Tensor]) -> dict[str, torch.Tensor]:
+        world = self._world()
+        if world == 1:
+            return dict(tensors)
+        out: dict[str, torch.Tensor] = {}
+        by_dtype: dict[torch.dtype, list[str]] = {}
+        for k, t in tensors.items():
+            by_dtype.setdefault(t.dtype, []).append(k)
+        for dtype, keys in by_dtype.items():
+            flat = torch.cat([tensors[k].contiguous().reshape(-1) for k in keys])
+            wire = flat.view(torch.uint8) if dtype == torch.bool else flat
+            key = (dtype, wire.numel(), wire.device)
+            recv = self._recv.get(key)
+            if recv is None:
+                recv = torch.empty(world * wire.numel(), dtype=wire.dtype, device=wire.device)
+                self._recv[key] = recv
+            backend = dist.get_backend(self.group)
+            if backend == "nccl":
+                dist.all_gather_into_tensor(recv, wire, group=self.group)
+            else:
+                dist.all_gather(list(recv.chunk(world)), wire, group=self.group)
+            parts = recv.chunk(world)
+            if dtype == torch.bool:
+                parts = [p.view(torch.bool) for p in parts]
+            off = 0
+            for k in keys:
+                t = tensors[k]
+                n = t.numel()
+                pieces = [p[off:off + n].view(t.shape) for p in parts]
+                out[k] = torch.cat(pieces, dim=self.env_axis)
+                off += n
+        return out

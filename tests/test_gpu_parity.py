@@ -253,3 +253,67 @@ def test_determinism_and_long_rollout():
         env.close()
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+def _env_off(n, offset, seed=42):
+    from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv
+    from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
+
+    cfg = AllstepsEnvCfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    cfg.seed = seed
+    return AllstepsEnv(cfg, env_id_offset=offset)
+
+
+def test_shards_match_unsharded():
+    """Weak-scaling layout: two shards (global env ids [0, n/2), [n/2, n)) stepped side by side give
+    bitwise the same trajectories as one env of n (Philox reset draws keyed by global env id)."""
+    n, h, steps = 1024, 512, 120
+    full = _env_off(n, 0)
+    parts = [_env_off(h, 0), _env_off(h, h)]
+    full.reset()
+    for p in parts:
+        p.reset()
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    resets = 0
+    for _ in range(steps):
+        a = torch.rand(n, 21, device="cuda", generator=gen) * 2 - 1
+        of, rf, tf, uf, _ = full.step(a)
+        outs = [p.step(a[i * h:(i + 1) * h]) for i, p in enumerate(parts)]
+        torch.testing.assert_close(torch.cat([o[0]["policy"] for o in outs]), of["policy"], rtol=0, atol=0)
+        torch.testing.assert_close(torch.cat([o[1] for o in outs]), rf, rtol=0, atol=0)
+        assert torch.equal(torch.cat([o[2] for o in outs]), tf) and torch.equal(torch.cat([o[3] for o in outs]), uf)
+        resets += int((tf | uf).sum())
+    assert resets > 0, "no env reset: the test did not exercise the Philox reset path"
+    sf = full.get_state()
+    for k in ("q", "qd", "root_pos", "idx", "episode"):
+        cat = torch.cat([p.get_state()[k].reshape(-1, h) for p in parts], dim=1)
+        assert torch.equal(cat.reshape(sf[k].shape), sf[k]), k
+    for e in [full] + parts:
+        e.close()
+
+
+def test_c3_large_config_invariants():
+    """C3 (32768 envs, stone curriculum level 9): size-independent invariants of the task state
+    after 60 steps of random actions (allsteps_env.py semantics): finite outputs, stones never
+    regenerated, target indices consistent, done envs restarted, episode counters bounded."""
+    n = 32768
+    env = _env(n, level=9)
+    stones0 = env.state["stones"].clone()
+    env.reset()
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    for _ in range(60):
+        a = torch.rand(n, 21, device="cuda", generator=gen) * 2 - 1
+        obs, rew, term, trunc, _ = env.step(a)
+        done = term | trunc
+        assert torch.isfinite(obs["policy"]).all() and torch.isfinite(rew).all()
+        ep = env.episode_length_buf
+        assert bool((ep[done] == 0).all()) and int(ep.max()) <= 899
+    assert torch.equal(env.state["stones"], stones0)
+    idx, prev, nxt = (env.state[k] for k in ("idx", "prev", "next"))
+    assert int(idx.min()) >= 1 and int(idx.max()) <= 19
+    assert torch.equal(prev, idx - 1) and torch.equal(nxt, torch.clamp(idx + 1, max=19))
+    assert 0 <= int(env.state["curriculum"][0]) <= 9
+    assert bool(((env.state["swing"] == 0) | (env.state["swing"] == 1)).all())
+    env.close()
