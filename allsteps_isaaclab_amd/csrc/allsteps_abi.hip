@@ -1,6 +1,7 @@
 // allsteps_abi.hip -- extern "C" implementation of include/allsteps.h.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -93,6 +94,10 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
     for (int l = 0; l < nl; ++l)
       if ((h.lpath[l] >> i) & 1u) h.lsub[i] |= 1u << l;
   for (int j = 0; j < h.nv; ++j) h.dsub[j] = j < 6 ? h.lsub[0] : h.lsub[j - 5];
+  for (int i = 0; i < nl; ++i) {
+    h.max_path = std::max(h.max_path, __builtin_popcount(h.lpath[i]) - 1);
+    if (i > 0) h.max_sub = std::max(h.max_sub, __builtin_popcount(h.lsub[i]) - 1);
+  }
   for (int k = 0; k < model->num_hinges; ++k) {
     int li = model->cfg_dof_link[k];
     if (li < 1 || li >= model->num_links) return fail(AS_ERR_INVALID, "as_create: cfg_dof_link");

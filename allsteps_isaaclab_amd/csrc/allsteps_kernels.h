@@ -22,6 +22,8 @@ struct Consts {
   as_sim_t sim;
   as_task_t task;
   int32_t nv;
+  int32_t max_path;                // longest root->link path, root excluded (links)
+  int32_t max_sub;                 // largest subtree of a non-root link, itself excluded
   uint32_t root_kids;              // links whose parent is the root
   uint32_t lpath[kMaxLinks];       // links on the path root..link, both included
   uint32_t lsub[kMaxLinks];        // links in the subtree of link, itself included

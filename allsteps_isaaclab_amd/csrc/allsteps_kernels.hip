@@ -34,6 +34,7 @@ constexpr int MAXC = AS_MAX_CONTACTS;
 constexpr int MAXR = AS_MAX_ROWS;
 constexpr int NST = AS_NUM_STONES;
 constexpr int GOLDEN_ITERS = 14;
+constexpr int kSweepB = 4;        // pivot block of the H^-1 sweep
 
 static_assert(NVMAX <= G, "one lane per generalized velocity");
 static_assert(LMAX <= G, "one lane per link");
@@ -66,8 +67,8 @@ struct ConScratch {
 union PhaseScratch {
   DynScratch d;
   struct {
-    float q[2][32];     // sweep: the two pivot rows of a round
-    float pb[4];        //        and the pivot block H_PP
+    float q[kSweepB][32];       // sweep: the pivot rows of a round (without the pivot columns)
+    float pb[kSweepB][kSweepB]; //        and the pivot block H_PP
   } sw;                 // aliases d.c / d.Ib, dead by then
   ConScratch k;
 };
@@ -191,6 +192,37 @@ struct Stamp {
 };
 
 // ------------------------------------------------------------------------------------------------
+// Mask walks.  take_bit pops the lowest set bit (0 and !valid once the mask is empty); the walks run
+// a wave-uniform number of iterations (the model's longest path / largest subtree) with several
+// rows loaded per iteration, and add an invalid row as +0 (no-op), so the LDS loads of one
+// iteration are independent of each other and of the running sum.
+__device__ __forceinline__ int take_bit(uint32_t& m, bool& valid) {
+  valid = m != 0u;
+  const int l = valid ? __builtin_ctz(m) : 0;
+  m &= m - 1u;
+  return l;
+}
+
+// acc += sum of rows[l] over the set bits l of `mask`, ascending, U rows per iteration.
+template <int W, int U>
+__device__ __forceinline__ void path_sum(uint32_t mask, int n_max, float (&acc)[W], const float (*rows)[W]) {
+  for (int it = 0; it < n_max; it += U) {
+    bool v[U];
+    int l[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) l[u] = take_bit(mask, v[u]);
+    float x[U][W];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < W; ++k) x[u][k] = rows[l[u]][k];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < W; ++k) acc[k] += v[u] ? x[u][k] : 0.f;
+  }
+}
+
 // FK by ancestor-path walks.  Local joint transforms are formed in parallel (lane = link); then
 // lane i composes the transforms on its own path root -> i, which is the same sequence of products
 // a level-by-level pass would form (R_i = R_parent Rl_i, p_i = p_parent + R_parent t_i), with no
@@ -220,18 +252,28 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
     float R[9], p[3] = {0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 9; ++k) R[k] = R0[k];
+    // two path links per iteration: both local transforms are loaded before the products
     uint32_t path = tp.lpath & ~1u;
-    while (path) {
-      const int l = __builtin_ctz(path);
-      path &= path - 1u;
-      const float* Rl = d.Rl[l];
-      float Rn[9], wp[3];
-      matmul3(R, Rl, Rn);
-      matvec3(R, Rl + 9, wp);
+    for (int it = 0; it < K.max_path; it += 2) {
+      bool v[2];
+      int l[2];
+      l[0] = take_bit(path, v[0]);
+      l[1] = take_bit(path, v[1]);
+      float Tl[2][12];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) p[k] += wp[k];
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int k = 0; k < 9; ++k) R[k] = Rn[k];
+        for (int k = 0; k < 12; ++k) Tl[u][k] = d.Rl[l[u]][k];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float Rn[9], wp[3];
+        matmul3(R, Tl[u], Rn);
+        matvec3(R, Tl[u] + 9, wp);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p[k] = v[u] ? p[k] + wp[k] : p[k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[k] = v[u] ? Rn[k] : R[k];
+      }
     }
 #pragma unroll
     for (int k = 0; k < 9; ++k) s.R[lane][k] = R[k];
@@ -324,13 +366,7 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
     }
   }
   if (lane < nl) {
-    uint32_t path = tp.lpath & ~1u;
-    while (path) {
-      const int l = __builtin_ctz(path);
-      path &= path - 1u;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) V[k] += d.Sq[l][k];
-    }
+    path_sum<6, 4>(tp.lpath & ~1u, K.max_path, V, d.Sq);
     if (lane > 0) {
       float Sq[6], cr[6];
 #pragma unroll
@@ -343,13 +379,7 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
   __syncthreads();
   float f[6], Ib[10];
   if (lane < nl) {
-    uint32_t path = tp.lpath & ~1u;
-    while (path) {
-      const int l = __builtin_ctz(path);
-      path &= path - 1u;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) A[k] += d.b.cr[l][k];
-    }
+    path_sum<6, 4>(tp.lpath & ~1u, K.max_path, A, d.b.cr);
 #pragma unroll
     for (int k = 0; k < 10; ++k) Ib[k] = d.Ib[lane][k];
     float IA[6], IV[6], x[6];
@@ -369,13 +399,26 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
   __syncthreads();
   if (lane >= 1 && lane < nl) {
     uint32_t sub = tp.lsub & ~(1u << lane);
-    while (sub) {
-      const int l = __builtin_ctz(sub);
-      sub &= sub - 1u;
+    for (int it = 0; it < K.max_sub; it += 2) {  // two subtree links per iteration
+      bool v[2];
+      int l[2];
+      l[0] = take_bit(sub, v[0]);
+      l[1] = take_bit(sub, v[1]);
+      float fl[2][6], Il[2][10];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) f[k] += d.b.f[l][k];
+      for (int u = 0; u < 2; ++u) {
 #pragma unroll
-      for (int k = 0; k < 10; ++k) Ib[k] += d.Ib[l][k];
+        for (int k = 0; k < 6; ++k) fl[u][k] = d.b.f[l[u]][k];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) Il[u][k] = d.Ib[l[u]][k];
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) f[k] += v[u] ? fl[u][k] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) Ib[k] += v[u] ? Il[u][k] : 0.f;
+      }
     }
 #pragma unroll
     for (int k = 0; k < 6; ++k) d.Sq[lane][k] = f[k];  // Sq is dead: F_i
@@ -447,51 +490,87 @@ __device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, 
   }
 }
 
-// H^-1 by the block sweep operator on 2x2 pivot blocks, with column rotation (same arithmetic as
-// oracle/physics.c sweep_inverse).  H is padded to an even order NP with an identity row/column.
-// Lane i holds row i in Hr, rotated so that the current pivot columns are always Hr[0], Hr[1]: a
-// round shifts every row left by two and appends the two new pivot-column entries, so the register
-// row is only indexed by compile-time constants, no per-column select is needed and the pairs stay
-// aligned for packed FMAs.  Round on pivots P = {p, p+1} with D = (H_PP)^-1:
-//   the pivot lanes publish their rows with the pivot columns replaced by -I (Qh), and H_PP;
-//   row' = alpha row - (beta0 Qh_0 + beta1 Qh_1) with
+// H^-1 by the block sweep operator on BxB pivot blocks, with column rotation (same arithmetic as
+// oracle/physics.c sweep_inverse).  H is padded to an order NP (a multiple of B) with identity rows
+// and columns.  Lane i holds row i in Hr, rotated so that the current pivot columns are always
+// Hr[0..B-1]: a round shifts every row left by B and appends the B new pivot-column entries, so the
+// register row is only indexed by compile-time constants, no per-column select is needed and (B
+// even) pairs stay aligned for packed FMAs.  Round on pivots P = {p..p+B-1}, D = (H_PP)^-1:
+//   the pivot lanes publish their rows without the pivot columns (Q) and H_PP (Pb);
+//   every lane forms D (in-register sweep of the uniform BxB block);
+//   row'_j = alpha row_j - sum_c beta_c Q_cj, new pivot-column entries = beta, with
 //     (alpha, beta) = (1, a_iP D)  for i not in P   (a_ij - a_iP D a_Pj;  a_iP <- a_iP D)
 //     (alpha, beta) = (0, -D_t)    for pivot lane t (D a_Pj;  a_PP <- -D).
 // After all rounds the rotation is back to the identity and the rows hold -H^-1.
-template <int NP>
+template <int B>
+__device__ __forceinline__ void block_inverse(float (&M)[B][B]) {  // M <- M^-1 (SPD), sweep order
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const float r = 1.0f / M[k][k];
+    float col[B], row[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) { col[i] = M[i][k]; row[i] = M[k][i]; }
+#pragma unroll
+    for (int i = 0; i < B; ++i)
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        if (i == k && j == k) M[i][j] = -r;
+        else if (i == k) M[i][j] = r * row[j];
+        else if (j == k) M[i][j] = r * col[i];
+        else M[i][j] = M[i][j] - col[i] * (r * row[j]);
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < B; ++i)
+#pragma unroll
+    for (int j = 0; j < B; ++j) M[i][j] = -M[i][j];
+}
+
+template <int NP, int B>
 __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
-  static_assert(NP % 2 == 0, "pairs");
+  static_assert(NP % B == 0, "padded order");
 #pragma unroll 1
-  for (int p = 0; p < NP; p += 2) {
+  for (int p = 0; p < NP; p += B) {
     // one buffer: LDS operations of a wave complete in issue order, so the next round's writes
     // cannot overtake this round's reads
-    float(&Q)[2][32] = s.x.sw.q;
-    float* Pb = s.x.sw.pb;
+    float(&Q)[kSweepB][32] = s.x.sw.q;
+    float(&Pb)[kSweepB][kSweepB] = s.x.sw.pb;
     const int t = lane - p;
-    if (t == 0 || t == 1) {
-      Pb[2 * t] = Hr[0];
-      Pb[2 * t + 1] = Hr[1];
+    const bool piv = (unsigned)t < (unsigned)B;
+    if (piv) {
 #pragma unroll
-      for (int j = 2; j < NP; ++j) Q[t][j] = Hr[j];
+      for (int c = 0; c < B; ++c) Pb[t][c] = Hr[c];
+#pragma unroll
+      for (int j = B; j < NP; ++j) Q[t][j] = Hr[j];
     }
     __syncthreads();
-    const float P00 = Pb[0], P01 = Pb[1], P10 = Pb[2], P11 = Pb[3];
-    const float id = 1.0f / (P00 * P11 - P01 * P10);
-    const float D00 = P11 * id, D01 = -P01 * id, D10 = -P10 * id, D11 = P00 * id;
-    float alpha, b0, b1;
-    if (t == 0) {
-      alpha = 0.f; b0 = -D00; b1 = -D01;
-    } else if (t == 1) {
-      alpha = 0.f; b0 = -D10; b1 = -D11;
-    } else {
-      alpha = 1.f;
-      b0 = Hr[0] * D00 + Hr[1] * D10;
-      b1 = Hr[0] * D01 + Hr[1] * D11;
+    float D[B][B];
+#pragma unroll
+    for (int a = 0; a < B; ++a)
+#pragma unroll
+      for (int c = 0; c < B; ++c) D[a][c] = Pb[a][c];
+    block_inverse<B>(D);
+    float alpha = 1.f, beta[B];
+#pragma unroll
+    for (int c = 0; c < B; ++c) {
+      float v = 0.f;
+#pragma unroll
+      for (int e = 0; e < B; ++e) v += Hr[e] * D[e][c];
+      float pv = -D[0][c];
+#pragma unroll
+      for (int e = 1; e < B; ++e) pv = t == e ? -D[e][c] : pv;
+      beta[c] = piv ? pv : v;
+    }
+    if (piv) alpha = 0.f;
+#pragma unroll
+    for (int j = B; j < NP; ++j) {
+      float v = alpha * Hr[j];
+#pragma unroll
+      for (int c = 0; c < B; ++c) v -= beta[c] * Q[c][j];
+      Hr[j - B] = v;
     }
 #pragma unroll
-    for (int j = 2; j < NP; ++j) Hr[j - 2] = alpha * Hr[j] - (b0 * Q[0][j] + b1 * Q[1][j]);
-    Hr[NP - 2] = b0;
-    Hr[NP - 1] = b1;
+    for (int c = 0; c < B; ++c) Hr[NP - B + c] = beta[c];
   }
   __syncthreads();
 }
@@ -647,12 +726,13 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   ts.mark(kStFK);
   dynamics(K, s, lane, tp, K.sim.gravity);
   ts.mark(kStLinkQ);
-  constexpr int NP = NV + (NV & 1);  // sweep order, padded to pairs with an identity row/column
+  constexpr int NP = (NV + kSweepB - 1) / kSweepB * kSweepB;  // sweep order, padded with identity
   float Hr[NP];
   h_row<NV>(K, s, lane, tp, *reinterpret_cast<float(*)[NV]>(Hr));
-  if (NP > NV) Hr[NP - 1] = lane == NV ? 1.f : 0.f;
+#pragma unroll
+  for (int j = NV; j < NP; ++j) Hr[j] = lane == j ? 1.f : 0.f;
   ts.mark(kStDyn);
-  sweep_inverse<NP>(s, lane, Hr);  // Hr <- row `lane` of -H^-1
+  sweep_inverse<NP, kSweepB>(s, lane, Hr);  // Hr <- row `lane` of -H^-1
 #pragma unroll
   for (int j = 0; j < NV; ++j) Hr[j] = lane < NV ? -Hr[j] : 0.f;
   ts.mark(kStChol);

@@ -286,39 +286,63 @@ static void rnea_bias(const or_model_t* m, const kin_t* K, const float* u, float
   }
 }
 
-/* Inverse of the SPD joint-space inertia by the block sweep operator on 2x2 pivot blocks (no
- * pivoting needed for SPD), in the arithmetic of the HIP kernel (sweep_inverse in
- * csrc/allsteps_kernels.hip).  The matrix is padded to even order with an identity row/column.
- * Round on P = {p, p+1}, D = (a_PP)^-1 via the 2x2 adjugate; Qh_t = row p+t of a with the pivot
- * columns replaced by -I;  row' = alpha row_base - (beta0 Qh_0 + beta1 Qh_1), where row_base has its
- * pivot-column entries zeroed and (alpha, beta) = (1, a_iP D) for i not in P, (0, -D_t) for the
- * pivot rows.  After all rounds a = -H^-1; the result is negated. */
+/* Inverse of the SPD joint-space inertia by the block sweep operator on SWEEP_B x SWEEP_B pivot
+ * blocks (no pivoting needed for SPD), in the arithmetic of the HIP kernel (sweep_inverse /
+ * block_inverse in csrc/allsteps_kernels.hip).  The matrix is padded to a multiple of SWEEP_B with
+ * identity rows/columns.  Round on P = {p..p+B-1}: D = (a_PP)^-1 by an in-block scalar sweep;
+ * row'_j = alpha a_ij - sum_c beta_c a_Pc,j for j not in P, row'_P = beta, where
+ * (alpha, beta) = (1, a_iP D) for i not in P and (0, -D_t) for pivot row t.  After all rounds
+ * a = -H^-1; the result is negated. */
+#define SWEEP_B 4
+static void block_inverse(float M[SWEEP_B][SWEEP_B]) {
+  for (int k = 0; k < SWEEP_B; ++k) {
+    const float r = 1.0f / M[k][k];
+    float col[SWEEP_B], row[SWEEP_B];
+    for (int i = 0; i < SWEEP_B; ++i) { col[i] = M[i][k]; row[i] = M[k][i]; }
+    for (int i = 0; i < SWEEP_B; ++i)
+      for (int j = 0; j < SWEEP_B; ++j) {
+        if (i == k && j == k) M[i][j] = -r;
+        else if (i == k) M[i][j] = r * row[j];
+        else if (j == k) M[i][j] = r * col[i];
+        else M[i][j] = M[i][j] - col[i] * (r * row[j]);
+      }
+  }
+  for (int i = 0; i < SWEEP_B; ++i)
+    for (int j = 0; j < SWEEP_B; ++j) M[i][j] = -M[i][j];
+}
+
 static void sweep_inverse(float* h, int n) {
-  const int np = n + (n & 1);
-  float a[NV_MAX + 1][NV_MAX + 1], Q[2][NV_MAX + 1];
+  const int np = (n + SWEEP_B - 1) / SWEEP_B * SWEEP_B;
+  float a[NV_MAX + SWEEP_B][NV_MAX + SWEEP_B];
+  float out[NV_MAX + SWEEP_B];
   for (int i = 0; i < np; ++i)
     for (int j = 0; j < np; ++j) a[i][j] = (i < n && j < n) ? h[i * n + j] : (i == j ? 1.f : 0.f);
-  for (int p = 0; p < np; p += 2) {
-    const float P00 = a[p][p], P01 = a[p][p + 1], P10 = a[p + 1][p], P11 = a[p + 1][p + 1];
-    const float id = 1.0f / (P00 * P11 - P01 * P10);
-    const float D00 = P11 * id, D01 = -P01 * id, D10 = -P10 * id, D11 = P00 * id;
-    for (int t = 0; t < 2; ++t)
-      for (int j = 0; j < np; ++j) Q[t][j] = (j == p) ? (t == 0 ? -1.f : 0.f) : (j == p + 1 ? (t == 1 ? -1.f : 0.f) : a[p + t][j]);
+  for (int p = 0; p < np; p += SWEEP_B) {
+    float D[SWEEP_B][SWEEP_B], Q[SWEEP_B][NV_MAX + SWEEP_B];
+    for (int x = 0; x < SWEEP_B; ++x)
+      for (int c = 0; c < SWEEP_B; ++c) D[x][c] = a[p + x][p + c];
+    block_inverse(D);
+    for (int x = 0; x < SWEEP_B; ++x)
+      for (int j = 0; j < np; ++j) Q[x][j] = a[p + x][j];
     for (int i = 0; i < np; ++i) {
-      float alpha, b0, b1;
-      if (i == p) {
-        alpha = 0.f; b0 = -D00; b1 = -D01;
-      } else if (i == p + 1) {
-        alpha = 0.f; b0 = -D10; b1 = -D11;
-      } else {
-        alpha = 1.f;
-        b0 = a[i][p] * D00 + a[i][p + 1] * D10;
-        b1 = a[i][p] * D01 + a[i][p + 1] * D11;
+      const int t = i - p;
+      const int piv = t >= 0 && t < SWEEP_B;
+      float alpha = piv ? 0.f : 1.f, beta[SWEEP_B];
+      for (int c = 0; c < SWEEP_B; ++c) {
+        float v = 0.f;
+        for (int e = 0; e < SWEEP_B; ++e) v += a[i][p + e] * D[e][c];
+        beta[c] = piv ? -D[t][c] : v;
       }
       for (int j = 0; j < np; ++j) {
-        const float base = (j == p || j == p + 1) ? 0.f : a[i][j];
-        a[i][j] = alpha * base - (b0 * Q[0][j] + b1 * Q[1][j]);
+        if (j >= p && j < p + SWEEP_B) {
+          out[j] = beta[j - p];
+        } else {
+          float v = alpha * a[i][j];
+          for (int c = 0; c < SWEEP_B; ++c) v -= beta[c] * Q[c][j];
+          out[j] = v;
+        }
       }
+      for (int j = 0; j < np; ++j) a[i][j] = out[j];
     }
   }
   for (int i = 0; i < n; ++i)
