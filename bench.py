@@ -51,6 +51,17 @@ def parse():
     return p.parse_args()
 
 
+def pmc_traffic(num_envs: int):
+    """HBM bytes per k_step launch from the committed rocprofv3 PMC passes (scripts/profile.sh writes
+    profiles/traffic_k_step.json: FETCH_SIZE x 2 + WRITE_SIZE); None when absent or for another size."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic_k_step.json")) as f:
+            t = json.load(f)
+        return t["traffic_bytes_per_launch"] if int(t["num_envs"]) == num_envs else None
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(num_envs: int, level: int, threads: int) -> dict:
     """The oracle (CPU port of the same step) on the host cores, bounded sample (~10-30 s CPU)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -161,7 +172,8 @@ def main():
             "kernels_ms": {"k_step_avg": round(k_ms / max(launches, 1), 5),
                            "k_obs_avg": round(o_ms / max(launches, 1), 5)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(n),
+                         "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/traffic_k_step.json)",
                          "kernel": "k_step", "bytes_per_env": K_STEP_BYTES},
             "cpu_baseline": None,
             "resets_last_step": resets,

@@ -19,3 +19,22 @@ for P in "FETCH_SIZE" "WRITE_SIZE" \
 done
 echo "== ablation"; date
 timeout -k 10 300 python3 $R/scripts/ablate.py > $OUT/ablate.log 2>&1; cat $OUT/ablate.log
+# per-launch HBM traffic of k_step from the FETCH_SIZE / WRITE_SIZE passes (bench.py's roofline.traffic)
+python3 - "$OUT" "${NUM_ENVS:-4096}" > $OUT/traffic_k_step.json <<'PY'
+import csv, glob, json, sys
+out, n = sys.argv[1], int(sys.argv[2])
+vals = {}
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    rows = [r for r in csv.DictReader(open(glob.glob(f"{out}/pmc_{c}/run_counter_collection.csv")[0]))
+            if r["Kernel_Name"].startswith("void as::k_step<27>")]
+    per = {}
+    for r in rows:
+        per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    vals[c] = sum(per.values()) / max(len(per), 1)
+traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+print(json.dumps({"kernel": "k_step<27>", "num_envs": n, "fetch_kb": round(vals["FETCH_SIZE"], 1),
+                  "write_kb": round(vals["WRITE_SIZE"], 1), "traffic_bytes_per_launch": round(traffic),
+                  "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE doubled "
+                            "(MI355X_MICROARCH.md gfx950 correction), WRITE_SIZE as reported"}))
+PY
+cat $OUT/traffic_k_step.json
