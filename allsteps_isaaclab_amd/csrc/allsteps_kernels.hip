@@ -846,43 +846,47 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     if (lane == 0) {
       s.rmeta[r][0] = r < nrow ? 1.0f / (a + 1e-9f) : 0.f;
       if (r >= nrow) { s.rmeta[r][1] = 0.f; s.rmeta[r][2] = 0.f; }
-      s.rlam[r] = 0.f;
     }
   }
   __syncthreads();
   ts.mark(kStWsolve);
-  // ---- projected Gauss-Seidel (lane j holds u_j; impulses uniform per env, kept in LDS).
+  // ---- projected Gauss-Seidel (lane j holds u_j; lane r holds the impulse lambda_r of its env).
   // Rows in order: contacts as (normal, tangent, tangent) triplets, then joint limits; a tangent
-  // row's bound uses the impulse of the most recent normal row (ln).  One-row-ahead prefetch.
-  const float mu = K.sim.friction;
+  // row's bound uses the impulse of the most recent normal row (ln).  Lane j's J / W columns of
+  // every row sit in registers (loaded once, up front); the row's old impulse comes from lane r by
+  // readlane and the projection is branch-free, so the only LDS access in the loop is the row
+  // metadata.
+  float mu = K.sim.friction;
+  asm volatile("" : "+v"(mu));
+  const bool hi = threadIdx.x & 32;
+  float lam = 0.f;
+  const int iters = K.sim.pgs_iters;
+  float Jc[MAXR], Wc[MAXR];
+#pragma unroll
+  for (int r = 0; r < MAXR; ++r) {
+    Jc[r] = s.x.k.Jm[r][jc] * jmask;
+    Wc[r] = s.x.k.Wm[r][jc] * jmask;
+  }
 #pragma unroll 1
-  for (int it = 0; it < K.sim.pgs_iters; ++it) {
+  for (int it = 0; it < iters; ++it) {
     float ln = 0.f;
-    float Jn = s.x.k.Jm[0][jc] * jmask, Wn = s.x.k.Wm[0][jc] * jmask;
-    float4 mn = *reinterpret_cast<const float4*>(s.rmeta[0]);
-    float lnext = s.rlam[0];
 #pragma unroll 1
-    for (int r = 0; r < maxrow; ++r) {
-      const float Jr = Jn, Wr = Wn, l0 = lnext;
-      const float4 mt = mn;
-      const int rn = r + 1 < maxrow ? r + 1 : r;
-      Jn = s.x.k.Jm[rn][jc] * jmask;
-      Wn = s.x.k.Wm[rn][jc] * jmask;
-      mn = *reinterpret_cast<const float4*>(s.rmeta[rn]);
-      lnext = s.rlam[rn];
-      const float v = half_sum(Jr * uj);
-      float l1;
-      if (mt.z == 1.f) {
-        const float lim = mu * ln;
-        l1 = fminf(fmaxf(l0 - v * mt.x, -lim), lim);
-      } else {
-        l1 = fmaxf(l0 + (mt.y - v) * mt.x, 0.f);
-        if (mt.z == 0.f) ln = l1;
-      }
-      uj += Wr * (l1 - l0);
-      if (lane == 0) s.rlam[r] = l1;
+    for (int r = 0; r < maxrow; ++r) {  // Jc[r] / Wc[r]: indexed register reads (s_set_gpr_idx)
+      const float4 mt = *reinterpret_cast<const float4*>(s.rmeta[r]);
+      const float v = half_sum(Jc[r] * uj);
+      const float l00 = readlane_f(lam, r), l01 = readlane_f(lam, r + 32);
+      const float l0 = hi ? l01 : l00;
+      const float lim = mu * ln;
+      const float lt = fminf(fmaxf(l0 - v * mt.x, -lim), lim);
+      const float lnrm = fmaxf(l0 + (mt.y - v) * mt.x, 0.f);
+      const float l1 = mt.z == 1.f ? lt : lnrm;
+      ln = mt.z == 0.f ? l1 : ln;
+      uj += Wc[r] * (l1 - l0);
+      lam = lane == r ? l1 : lam;
     }
   }
+  if (lane < MAXR) s.rlam[lane] = lane < maxrow ? lam : 0.f;
+  __syncthreads();
   if (lane < NV) s.u[lane] = uj;
   if (lane < MAXC) s.lamn[lane] = 3 * lane < nrow ? s.rlam[3 * lane] : 0.f;
   __syncthreads();
