@@ -157,6 +157,26 @@ __device__ __forceinline__ float half_sum(float v) {
   return (threadIdx.x & 32) ? b : a;
 }
 
+__device__ __forceinline__ float half_min(float v) {
+  v = fminf(v, dpp<0xB1>(v));
+  v = fminf(v, dpp<0x4E>(v));
+  v = fminf(v, dpp<0x141>(v));
+  v = fminf(v, dpp<0x140>(v));
+  float a = fminf(readlane_f(v, 0), readlane_f(v, 16));
+  float b = fminf(readlane_f(v, 32), readlane_f(v, 48));
+  return (threadIdx.x & 32) ? b : a;
+}
+
+__device__ __forceinline__ float half_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0x140>(v));
+  float a = fmaxf(readlane_f(v, 0), readlane_f(v, 16));
+  float b = fmaxf(readlane_f(v, 32), readlane_f(v, 48));
+  return (threadIdx.x & 32) ? b : a;
+}
+
 __device__ __forceinline__ float wave32_sum(float v) {
 #pragma unroll
   for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -590,21 +610,6 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   const float* h = K.sim.stone_half;
   const float margin = K.sim.margin;
   const int nst = K.task.num_steps, ng = m.num_geoms;
-  // broadphase (lane = stone): stones within 1.8 m of the root link origin
-  bool isc = false;
-  if (lane < nst) {
-    float o = 0.f;
-    for (int k = 0; k < 3; ++k) {
-      float d = fabsf(s.stones[3 * lane + k] - s.root_pos[k]) - h[k];
-      if (d > 0.f) o += d * d;
-    }
-    isc = o < 1.8f * 1.8f;
-  }
-  uint64_t bal = __ballot(isc);
-  const int half = (threadIdx.x >> 5) & 1;
-  uint32_t mine = (uint32_t)(bal >> (32 * half));
-  if (isc) s.cand[__popc(mine & ((1u << lane) - 1u))] = lane;
-  const int ncand = __popc(mine);
   // geom segment in the O frame (lane = geom), formed once for all candidate stones
   const bool gv = lane < ng;
   const int g = gv ? lane : 0;
@@ -620,6 +625,31 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   const float L = sqrtf((bb[0] - a[0]) * (bb[0] - a[0]) + (bb[1] - a[1]) * (bb[1] - a[1]) +
                         (bb[2] - a[2]) * (bb[2] - a[2]));
   const float mid[3] = {0.5f * (a[0] + bb[0]), 0.5f * (a[1] + bb[1]), 0.5f * (a[2] + bb[2])};
+  // broadphase (lane = stone): stone boxes that come within the contact margin of the robot's
+  // bounding box (union of the geoms' boxes).  Conservative: every pair the narrowphase would
+  // turn into a contact survives, so the contact set and order match the oracle's broadphase.
+  float blo[3], bhi[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float e = gtype == 0 ? a[k] : fminf(a[k], bb[k]);
+    const float f = gtype == 0 ? a[k] : fmaxf(a[k], bb[k]);
+    blo[k] = half_min(gv ? e - r : 1e30f) - margin;
+    bhi[k] = half_max(gv ? f + r : -1e30f) + margin;
+  }
+  bool isc = false;
+  if (lane < nst) {
+    isc = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float c = s.stones[3 * lane + k] - s.root_pos[k];
+      isc = isc && (c - h[k] <= bhi[k]) && (c + h[k] >= blo[k]);
+    }
+  }
+  uint64_t bal = __ballot(isc);
+  const int half = (threadIdx.x >> 5) & 1;
+  uint32_t mine = (uint32_t)(bal >> (32 * half));
+  if (isc) s.cand[__popc(mine & ((1u << lane) - 1u))] = lane;
+  const int ncand = __popc(mine);
   __syncthreads();
   // narrowphase: candidate stones in ascending order, geoms in lane order within a stone
   int base = 0;
