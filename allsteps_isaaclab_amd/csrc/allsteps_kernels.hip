@@ -157,6 +157,21 @@ __device__ __forceinline__ float half_sum(float v) {
   return (threadIdx.x & 32) ? b : a;
 }
 
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ uint32_t half_or(uint32_t v) {
+  v |= dpp_u<0xB1>(v);
+  v |= dpp_u<0x4E>(v);
+  v |= dpp_u<0x141>(v);
+  v |= dpp_u<0x140>(v);
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0) | (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return (threadIdx.x & 32) ? b : a;
+}
+
 __device__ __forceinline__ float half_min(float v) {
   v = fminf(v, dpp<0xB1>(v));
   v = fminf(v, dpp<0x4E>(v));
@@ -206,7 +221,15 @@ struct Stamp {
   __device__ void flush() {
     if (p) {
       __syncthreads();
-      if (threadIdx.x < kNumStamps) atomicAdd(p + threadIdx.x, acc[threadIdx.x]);
+      if (threadIdx.x < kNumStamps) {
+        atomicAdd(p + threadIdx.x, acc[threadIdx.x]);
+        atomicMax(p + 16 + threadIdx.x, acc[threadIdx.x]);  // slots 16..: per-phase maximum
+      }
+      if (threadIdx.x == 0) {  // slot kNumStamps: the slowest wave's total (the launch's tail)
+        unsigned long long tot = 0;
+        for (int k = 0; k < kNumStamps; ++k) tot += acc[k];
+        atomicMax(p + kNumStamps, tot);
+      }
     }
   }
 };
@@ -848,34 +871,47 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   for (int a = 0; a < 6; ++a) Sj[a] = s.S[jl][a];
   __syncthreads();
   const int maxrow = sm.maxrow;
+  // four rows per iteration: the rows are independent, so their LDS reads and FMA chains overlap
+  // (MAXR is a multiple of 4; rows in [maxrow, r0 + 4) are written as zero / ignored)
+  static_assert(MAXR % 4 == 0, "row blocks");
 #pragma unroll 1
-  for (int r = 0; r < maxrow; ++r) {
-    float jv = 0.f;
-    if (r < nrow && lane < NV) {
-      int lk = s.rlink[r];
-      if (lk >= 0) {
-        if ((tp.dsub >> lk) & 1u) jv = dot6(Sj, s.rf6[r]);
-      } else if (-1 - lk == lane) {
-        jv = s.rsign[r];
+  for (int r0 = 0; r0 < maxrow; r0 += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + u;
+      float jv = 0.f;
+      if (r < nrow && lane < NV) {
+        int lk = s.rlink[r];
+        if (lk >= 0) {
+          if ((tp.dsub >> lk) & 1u) jv = dot6(Sj, s.rf6[r]);
+        } else if (-1 - lk == lane) {
+          jv = s.rsign[r];
+        }
       }
+      if (lane < LDJ) s.x.k.Jm[r][lane] = jv;
     }
-    if (lane < LDJ) s.x.k.Jm[r][lane] = jv;
   }
   __syncthreads();
   // lanes >= NV carry no dof: they read column 0 scaled by 0 (keeps every LDS address in bounds)
   const int jc = lane < NV ? lane : 0;
   const float jmask = lane < NV ? 1.f : 0.f;
 #pragma unroll 1
-  for (int r = 0; r < maxrow; ++r) {
-    float w = 0.f;
+  for (int r0 = 0; r0 < maxrow; r0 += 4) {
+    float w[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < NV; ++k) w += Hr[k] * s.x.k.Jm[r][k];
-    w = lane < NV ? w : 0.f;
-    if (lane < LDJ) s.x.k.Wm[r][lane] = w;
-    float a = half_sum(s.x.k.Jm[r][jc] * jmask * w);
-    if (lane == 0) {
-      s.rmeta[r][0] = r < nrow ? 1.0f / (a + 1e-9f) : 0.f;
-      if (r >= nrow) { s.rmeta[r][1] = 0.f; s.rmeta[r][2] = 0.f; }
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] += Hr[k] * s.x.k.Jm[r0 + u][k];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + u;
+      w[u] = lane < NV ? w[u] : 0.f;
+      if (lane < LDJ) s.x.k.Wm[r][lane] = w[u];
+      const float a = half_sum(s.x.k.Jm[r][jc] * jmask * w[u]);
+      if (lane == 0) {
+        s.rmeta[r][0] = r < nrow ? 1.0f / (a + 1e-9f) : 0.f;
+        if (r >= nrow) { s.rmeta[r][1] = 0.f; s.rmeta[r][2] = 0.f; }
+      }
     }
   }
   __syncthreads();
@@ -921,21 +957,29 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   if (lane < MAXC) s.lamn[lane] = 3 * lane < nrow ? s.rlam[3 * lane] : 0.f;
   __syncthreads();
   ts.mark(kStPGS);
-  // ---- contact-sensor flags of this substep (force_matrix_w = impulse / dt, > eps)
-  if (lane == 0) {
-    uint32_t mk[2] = {0u, 0u};
-    for (int c = 0; c < nc; ++c) {
-      if (s.cfoot[c] < 0 || 3 * c >= nrow) continue;
-      float fx = 0.f, fy = 0.f, fz = 0.f;
-      for (int c2 = 0; c2 < nc && 3 * c2 < nrow; ++c2) {
-        if (s.cfoot[c2] != s.cfoot[c] || s.cstone[c2] != s.cstone[c]) continue;
-        float l = s.lamn[c2];
-        fx += l * s.cn[c2][0]; fy += l * s.cn[c2][1]; fz += l * s.cn[c2][2];
+  // ---- contact-sensor flags of this substep (force_matrix_w = impulse / dt, > eps): lane c sums
+  //      lambda_n n over the contacts with its (foot, stone) pair in ascending order, and the
+  //      per-foot stone bits are OR-reduced over the half-wave
+  {
+    uint32_t b0 = 0u, b1 = 0u;
+    if (lane < nc && 3 * lane < nrow) {
+      const int f = s.cfoot[lane], st = s.cstone[lane];
+      if (f >= 0) {
+        float fx = 0.f, fy = 0.f, fz = 0.f;
+        for (int c2 = 0; c2 < nc && 3 * c2 < nrow; ++c2) {
+          const bool same = s.cfoot[c2] == f && s.cstone[c2] == st;
+          const float l = s.lamn[c2];
+          fx += same ? l * s.cn[c2][0] : 0.f;
+          fy += same ? l * s.cn[c2][1] : 0.f;
+          fz += same ? l * s.cn[c2][2] : 0.f;
+        }
+        if (sqrtf(fx * fx + fy * fy + fz * fz) / dt > 1e-4f) {
+          if (f == 0) b0 = 1u << st; else b1 = 1u << st;
+        }
       }
-      if (sqrtf(fx * fx + fy * fy + fz * fz) / dt > 1e-4f) mk[s.cfoot[c]] |= 1u << s.cstone[c];
     }
-    mask_out[0] = mk[0];
-    mask_out[1] = mk[1];
+    mask_out[0] = half_or(b0);
+    mask_out[1] = half_or(b1);
   }
   // ---- integrate
   if (lane < nh) {

@@ -178,9 +178,11 @@ int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* s
 int as_profile(as_env_t* env, int32_t max_launches);
 int as_profile_read(as_env_t* env, double* step_kernel_ms, double* obs_kernel_ms, int32_t* launches);
 
-/* Diagnostic: when stamps_dev (device, >= 16 uint64) is non-null, every k_step wave adds the
+/* Diagnostic: when stamps_dev (device, >= 32 uint64) is non-null, every k_step wave adds the
  * s_memtime cycles of each phase (load, fk, link, dynamics, cholesky, solve, collide, rows,
- * W-solve, pgs, integrate, task, reset, store) to it.  Pass NULL to switch off. */
+ * W-solve, pgs, integrate, task, reset, store) to it, and slot 14 keeps the largest single-wave
+ * total of any launch and slots 16.. the largest single-wave cycles of each phase (atomicMax).
+ * Pass NULL to switch off. */
 int as_debug_stamps(as_env_t* env, uint64_t* stamps_dev);
 
 /* Device counters of the last step: [0] = any env reset, [1] = sum of curr_target_index. */

@@ -26,7 +26,7 @@ def main(n=4096, steps=50):
     acts = torch.rand(steps + 10, n, 21, device="cuda", generator=gen) * 2 - 1
     for t in range(10):
         env.step(acts[t])
-    buf = torch.zeros(16, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(32, dtype=torch.int64, device="cuda")
     env._native.debug_stamps(buf)
     for t in range(steps):
         env.step(acts[10 + t])
@@ -36,7 +36,9 @@ def main(n=4096, steps=50):
     tot = buf.cpu().tolist()
     per = {PHASES[i]: round(tot[i] / waves) for i in range(len(PHASES))}
     s = sum(per.values())
-    print(json.dumps({"n": n, "cycles_per_wave_step": s, "per_phase": per,
+    mx = {PHASES[i]: tot[16 + i] for i in range(len(PHASES))}
+    print(json.dumps({"n": n, "cycles_per_wave_step": s, "max_wave_step_total": tot[len(PHASES)], "per_phase_max": mx,
+                      "per_phase": per,
                       "share": {k: round(v / s, 3) for k, v in per.items()}}))
     env.close()
 
