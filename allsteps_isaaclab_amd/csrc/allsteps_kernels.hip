@@ -67,6 +67,10 @@ struct ConScratch {
 union PhaseScratch {
   DynScratch d;
   struct {
+    float g[32][8];     // collide: geom segment endpoints, radius, packed type/foot/link
+    int pl[64];         //          pending (stone << 8 | geom) pairs, stone-major
+  } col;
+  struct {
     float q[kSweepB][32];       // sweep: the pivot rows of a round (without the pivot columns)
     float pb[kSweepB][kSweepB]; //        and the pivot block H_PP
   } sw;                 // aliases d.c / d.Ib, dead by then
@@ -674,59 +678,83 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   if (isc) s.cand[__popc(mine & ((1u << lane) - 1u))] = lane;
   const int ncand = __popc(mine);
   __syncthreads();
-  // narrowphase: candidate stones in ascending order, geoms in lane order within a stone
-  int base = 0;
-  for (int ci = 0; ci < ncand; ++ci) {
-    const int st = s.cand[ci];
-    int cnt = 0;
-    float P0[3], N0[3], P1[3], N1[3], P2[3], N2[3], SEP0 = 0.f, SEP1 = 0.f, SEP2 = 0.f;
+  // narrowphase in two passes.  (A) lane = geom, loop over the candidate stones: the cheap
+  // bounding test (spheres: the exact separation) appends the surviving (stone, geom) pairs to a
+  // list in LDS, stone-major and geom-minor -- the oracle's emission order.  (B) lane = pair, in
+  // chunks of 32: the exact test (capsules: golden-section search) and the contacts, emitted in
+  // list order by a prefix sum.  A chunk is flushed as soon as 32 pairs are pending, so the list
+  // never exceeds 32 + 22 entries, and the search stops once this env has MAXC contacts.
+  {
+    float* gs = s.x.col.g[lane];  // staging of this lane's geom for pass B
     if (gv) {
+      gs[0] = a[0]; gs[1] = a[1]; gs[2] = a[2];
+      gs[3] = bb[0]; gs[4] = bb[1]; gs[5] = bb[2];
+      gs[6] = r;
+      gs[7] = __int_as_float(gtype | ((foot + 1) << 4) | (link << 8));
+    }
+  }
+  int* pl = s.x.col.pl;
+  int pend = 0, base = 0;
+  auto flush = [&](int npairs) {  // pass B over pl[0, npairs) (npairs <= 32), then shift the rest
+    int cnt = 0, plink = 0, pst = 0, pfoot = -1;
+    float P0[3], N0[3], P1[3], N1[3], P2[3], N2[3], SEP0 = 0.f, SEP1 = 0.f, SEP2 = 0.f, pr = 0.f;
+    if (lane < npairs) {
+      const int e = pl[lane];
+      const int gi = e & 0xff;
+      pst = e >> 8;
+      const float* q = s.x.col.g[gi];
+      const float A[3] = {q[0], q[1], q[2]}, Bb[3] = {q[3], q[4], q[5]};
+      pr = q[6];
+      const int meta = __float_as_int(q[7]);
+      const int pty = meta & 15;
+      pfoot = ((meta >> 4) & 15) - 1;
+      plink = meta >> 8;
       float c[3];
-      for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * st + k] - s.root_pos[k];
+      for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * pst + k] - s.root_pos[k];
       float nr[3];
-      if (gtype == 0) {
-        float sd = sd_box(a, c, h, nr) - r;
+      if (pty == 0) {
+        float sd = sd_box(A, c, h, nr) - pr;
         if (sd < margin) {
-          for (int k = 0; k < 3; ++k) { P0[k] = a[k]; N0[k] = nr[k]; }
+          for (int k = 0; k < 3; ++k) { P0[k] = A[k]; N0[k] = nr[k]; }
           SEP0 = sd;
           cnt = 1;
         }
-      } else if (sd_box(mid, c, h, nr) <= 0.5f * L + r + margin) {
+      } else {
         float n0[3], n1[3], tn[3];
-        float s0 = sd_box(a, c, h, n0) - r;
-        float s1 = sd_box(bb, c, h, n1) - r;
+        float s0 = sd_box(A, c, h, n0) - pr;
+        float s1 = sd_box(Bb, c, h, n1) - pr;
         const float gr = 0.6180339887f;
         float lo = 0.f, hi = 1.f;
         float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
         float Q1[3], Q2[3];
-        for (int k = 0; k < 3; ++k) { Q1[k] = a[k] + x1 * (bb[k] - a[k]); Q2[k] = a[k] + x2 * (bb[k] - a[k]); }
+        for (int k = 0; k < 3; ++k) { Q1[k] = A[k] + x1 * (Bb[k] - A[k]); Q2[k] = A[k] + x2 * (Bb[k] - A[k]); }
         float f1 = sd_box(Q1, c, h, tn), f2 = sd_box(Q2, c, h, tn);
 #pragma unroll 1
         for (int it = 0; it < GOLDEN_ITERS; ++it) {
           if (f1 < f2) {
             hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
-            for (int k = 0; k < 3; ++k) Q1[k] = a[k] + x1 * (bb[k] - a[k]);
+            for (int k = 0; k < 3; ++k) Q1[k] = A[k] + x1 * (Bb[k] - A[k]);
             f1 = sd_box(Q1, c, h, tn);
           } else {
             lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
-            for (int k = 0; k < 3; ++k) Q2[k] = a[k] + x2 * (bb[k] - a[k]);
+            for (int k = 0; k < 3; ++k) Q2[k] = A[k] + x2 * (Bb[k] - A[k]);
             f2 = sd_box(Q2, c, h, tn);
           }
         }
         float ts = 0.5f * (lo + hi), Ps[3], ns[3];
-        for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (bb[k] - a[k]);
-        float ss = sd_box(Ps, c, h, ns) - r;
+        for (int k = 0; k < 3; ++k) Ps[k] = A[k] + ts * (Bb[k] - A[k]);
+        float ss = sd_box(Ps, c, h, ns) - pr;
         bool e0 = s0 < margin, e1 = s1 < margin;
         bool es = ss < margin && ss < fminf(s0, s1) - 0.002f;
         // pack the emitted contacts in (t=0, t=1, t*) order into slots 0..2
-        for (int k = 0; k < 3; ++k) { P0[k] = a[k]; N0[k] = n0[k]; }
+        for (int k = 0; k < 3; ++k) { P0[k] = A[k]; N0[k] = n0[k]; }
         SEP0 = s0;
         if (e0) {
-          for (int k = 0; k < 3; ++k) { P1[k] = bb[k]; N1[k] = n1[k]; P2[k] = Ps[k]; N2[k] = ns[k]; }
+          for (int k = 0; k < 3; ++k) { P1[k] = Bb[k]; N1[k] = n1[k]; P2[k] = Ps[k]; N2[k] = ns[k]; }
           SEP1 = s1; SEP2 = ss;
           if (!e1) { for (int k = 0; k < 3; ++k) { P1[k] = Ps[k]; N1[k] = ns[k]; } SEP1 = ss; }
         } else {
-          for (int k = 0; k < 3; ++k) { P0[k] = bb[k]; N0[k] = n1[k]; P1[k] = Ps[k]; N1[k] = ns[k]; }
+          for (int k = 0; k < 3; ++k) { P0[k] = Bb[k]; N0[k] = n1[k]; P1[k] = Ps[k]; N1[k] = ns[k]; }
           SEP0 = s1; SEP1 = ss;
           if (!e1) { for (int k = 0; k < 3; ++k) { P0[k] = Ps[k]; N0[k] = ns[k]; } SEP0 = ss; }
         }
@@ -739,13 +767,37 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
       int v = __shfl_up(incl, o, 32);
       if (lane >= o) incl += v;
     }
-    int total = __shfl(incl, 31, 32);
-    int slot = base + incl - cnt;
-    if (cnt > 0) emit_contact(s, slot, link, st, foot, P0, N0, SEP0, r);
-    if (cnt > 1) emit_contact(s, slot + 1, link, st, foot, P1, N1, SEP1, r);
-    if (cnt > 2) emit_contact(s, slot + 2, link, st, foot, P2, N2, SEP2, r);
+    const int total = __shfl(incl, 31, 32);
+    const int slot = base + incl - cnt;
+    if (cnt > 0) emit_contact(s, slot, plink, pst, pfoot, P0, N0, SEP0, pr);
+    if (cnt > 1) emit_contact(s, slot + 1, plink, pst, pfoot, P1, N1, SEP1, pr);
+    if (cnt > 2) emit_contact(s, slot + 2, plink, pst, pfoot, P2, N2, SEP2, pr);
     base += total;
+    // shift the unprocessed tail (< 32 entries) to the front
+    const int rest = pend - npairs;
+    const int tail = lane < rest ? pl[npairs + lane] : 0;
+    __syncthreads();
+    if (lane < rest) pl[lane] = tail;
+    pend = rest;
+    __syncthreads();
+  };
+  __syncthreads();
+  for (int ci = 0; ci < ncand; ++ci) {
+    if (base >= MAXC) break;  // later contacts would be dropped anyway
+    const int st = s.cand[ci];
+    float c[3], nr[3];
+    for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * st + k] - s.root_pos[k];
+    bool need = false;
+    if (gv) {
+      need = gtype == 0 ? sd_box(a, c, h, nr) - r < margin : sd_box(mid, c, h, nr) <= 0.5f * L + r + margin;
+    }
+    const uint32_t bl = (uint32_t)(__ballot(need) >> (32 * half));
+    if (need) pl[pend + __popc(bl & ((1u << lane) - 1u))] = (st << 8) | lane;
+    pend += __popc(bl);
+    __syncthreads();
+    if (pend >= 32) flush(32);
   }
+  if (pend > 0 && base < MAXC) flush(pend);
   __syncthreads();
   if (lane == 0) s.ncontact = base < MAXC ? base : MAXC;
   __syncthreads();
