@@ -149,16 +149,20 @@ __device__ __forceinline__ float dpp(float v) {
 __device__ __forceinline__ float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
 
 // Sum over the 32 lanes of this env's half-wave: DPP butterfly inside each 16-lane row
-// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the two row sums of each half
-// through SGPRs.  Every lane of a half gets the bit-identical value.
+// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then v_permlane16_swap exchanges the
+// two rows of each half so that every lane adds (row 0 + row 1) of its half -- no SGPR round trip.
+// Every lane of a half gets the bit-identical value.
+__device__ __forceinline__ float row_pair_sum(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(p[0]) + __int_as_float(p[1]);
+}
+
 __device__ __forceinline__ float half_sum(float v) {
   v += dpp<0xB1>(v);
   v += dpp<0x4E>(v);
   v += dpp<0x141>(v);
   v += dpp<0x140>(v);
-  float a = readlane_f(v, 0) + readlane_f(v, 16);
-  float b = readlane_f(v, 32) + readlane_f(v, 48);
-  return (threadIdx.x & 32) ? b : a;
+  return row_pair_sum(v);
 }
 
 template <int CTRL>
@@ -171,9 +175,8 @@ __device__ __forceinline__ uint32_t half_or(uint32_t v) {
   v |= dpp_u<0x4E>(v);
   v |= dpp_u<0x141>(v);
   v |= dpp_u<0x140>(v);
-  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0) | (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
-  const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
-  return (threadIdx.x & 32) ? b : a;
+  const auto p = __builtin_amdgcn_permlane16_swap((int)v, (int)v, false, false);
+  return (uint32_t)p[0] | (uint32_t)p[1];
 }
 
 __device__ __forceinline__ float half_min(float v) {
@@ -181,9 +184,8 @@ __device__ __forceinline__ float half_min(float v) {
   v = fminf(v, dpp<0x4E>(v));
   v = fminf(v, dpp<0x141>(v));
   v = fminf(v, dpp<0x140>(v));
-  float a = fminf(readlane_f(v, 0), readlane_f(v, 16));
-  float b = fminf(readlane_f(v, 32), readlane_f(v, 48));
-  return (threadIdx.x & 32) ? b : a;
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fminf(__int_as_float(p[0]), __int_as_float(p[1]));
 }
 
 __device__ __forceinline__ float half_max(float v) {
@@ -191,15 +193,8 @@ __device__ __forceinline__ float half_max(float v) {
   v = fmaxf(v, dpp<0x4E>(v));
   v = fmaxf(v, dpp<0x141>(v));
   v = fmaxf(v, dpp<0x140>(v));
-  float a = fmaxf(readlane_f(v, 0), readlane_f(v, 16));
-  float b = fmaxf(readlane_f(v, 32), readlane_f(v, 48));
-  return (threadIdx.x & 32) ? b : a;
-}
-
-__device__ __forceinline__ float wave32_sum(float v) {
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
 }
 
 // diagnostic phase stamps (off when p == nullptr): each wave accumulates its s_memtime deltas per
@@ -988,9 +983,11 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
     float ln = 0.f;
+    float4 mn = *reinterpret_cast<const float4*>(s.rmeta[0]);
 #pragma unroll 1
     for (int r = 0; r < maxrow; ++r) {  // Jc[r] / Wc[r]: indexed register reads (s_set_gpr_idx)
-      const float4 mt = *reinterpret_cast<const float4*>(s.rmeta[r]);
+      const float4 mt = mn;
+      mn = *reinterpret_cast<const float4*>(s.rmeta[r + 1 < maxrow ? r + 1 : r]);  // one row ahead
       const float v = half_sum(Jc[r] * uj);
       const float l00 = readlane_f(lam, r), l01 = readlane_f(lam, r + 32);
       const float l0 = hi ? l01 : l00;
