@@ -60,11 +60,11 @@ struct DynScratch {
     } b;
   };
 };
-struct ConScratch {
+struct alignas(16) ConScratch {
   float Jm[MAXR][LDJ];  // J rows (lane = dof column)
   float Wm[MAXR][LDJ];  // W = H^-1 J^T rows (lane = dof column)
 };
-union PhaseScratch {
+union alignas(16) PhaseScratch {
   DynScratch d;
   struct {
     float g[32][8];     // collide: geom segment endpoints, radius, packed type/foot/link
@@ -918,6 +918,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   for (int a = 0; a < 6; ++a) Sj[a] = s.S[jl][a];
   __syncthreads();
   const int maxrow = sm.maxrow;
+  const uint32_t dsub = tp.dsub;
   // four rows per iteration: the rows are independent, so their LDS reads and FMA chains overlap
   // (MAXR is a multiple of 4; rows in [maxrow, r0 + 4) are written as zero / ignored)
   static_assert(MAXR % 4 == 0, "row blocks");
@@ -926,15 +927,16 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int r = r0 + u;
-      float jv = 0.f;
-      if (r < nrow && lane < NV) {
-        int lk = s.rlink[r];
-        if (lk >= 0) {
-          if ((tp.dsub >> lk) & 1u) jv = dot6(Sj, s.rf6[r]);
-        } else if (-1 - lk == lane) {
-          jv = s.rsign[r];
-        }
-      }
+      // branch-free: contact row -> S_j . f6 on the link's path; limit row -> +-1 at its dof
+      const int lk = s.rlink[r];
+      float f6[6];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) f6[a] = s.rf6[r][a];
+      const float sg = s.rsign[r];
+      const bool onpath = lk >= 0 && ((dsub >> (lk & 31)) & 1u);
+      const float jcon = dot6(Sj, f6);
+      float jv = onpath ? jcon : (-1 - lk == lane ? sg : 0.f);
+      jv = (r < nrow && lane < NV) ? jv : 0.f;
       if (lane < LDJ) s.x.k.Jm[r][lane] = jv;
     }
   }
@@ -946,9 +948,17 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   for (int r0 = 0; r0 < maxrow; r0 += 4) {
     float w[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < NV; ++k)
+    for (int u = 0; u < 4; ++u) {
+      const float4* jr = reinterpret_cast<const float4*>(s.x.k.Jm[r0 + u]);  // 16-B aligned rows
+      float jrow[LDJ];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) w[u] += Hr[k] * s.x.k.Jm[r0 + u][k];
+      for (int q = 0; q < LDJ / 4; ++q) {
+        const float4 t = jr[q];
+        jrow[4 * q] = t.x; jrow[4 * q + 1] = t.y; jrow[4 * q + 2] = t.z; jrow[4 * q + 3] = t.w;
+      }
+#pragma unroll
+      for (int k = 0; k < NV; ++k) w[u] += Hr[k] * jrow[k];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int r = r0 + u;
