@@ -39,6 +39,7 @@ constexpr int kSweepB = 4;        // pivot block of the H^-1 sweep
 static_assert(NVMAX <= G, "one lane per generalized velocity");
 static_assert(LMAX <= G, "one lane per link");
 static_assert(MAXR <= G, "one row per lane in the row builders");
+static_assert(MAXR <= 3 * MAXC, "a row index / 3 is a valid contact slot");
 
 // ------------------------------------------------------------------------------------------------
 // per-env LDS scratch.  Occupancy at 4096 envs is set by LDS: two envs per 64-lane workgroup must
@@ -50,7 +51,7 @@ struct DynScratch {
   float c[LMAX][3];
   float Ib[LMAX][10];
   float Ic[LMAX][10];
-  float Fh[NVMAX][6];   // Ic_link(j) S_j (CRBA column forces)
+  alignas(16) float Fh[NVMAX][8];  // Ic_link(j) S_j (CRBA column forces), rows padded to 32 B
   float Sq[LMAX][6];    // S_i qd_i, later the subtree force sums F_i
   union {
     float Rl[LMAX][12]; // FK: local joint transforms (R 9, p 3); dead before cr / f are written
@@ -109,12 +110,12 @@ struct EnvS {
   float R[LMAX][9];
   float p[LMAX][3];
   float c0[3];          // root COM (relative), kept past the dynamics phase for integration
-  float S[NVMAX][6];
+  alignas(16) float S[NVMAX][8];  // motion subspace [w; v_O] per dof, rows padded to 32 B (b128 reads)
   float b[32];          // tau - C
   PhaseScratch x;
   float rlam[MAXR];     // PGS impulses
   alignas(16) float rmeta[MAXR][4]; // per row: 1/A_rr, target, type (0 normal, 1 tangent, 2 limit)
-  float rf6[MAXR][6];   // contact rows: spatial force direction [P x d; d]
+  float cdir[MAXC][3][3];  // contact frame: normal, tangent 1, tangent 2
   int rlink[MAXR];      // contact link, or -1 - dof for a limit row
   float rsign[MAXR];
   float lamn[MAXC];     // normal impulses of the last PGS sweep (contact flags)
@@ -857,13 +858,10 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     float t1[3], t2[3];
     tangents(s.cn[lane], t1, t2);
     const float* dirs[3] = {s.cn[lane], t1, t2};
-    const float* P = s.cpt[lane];
     float sp = s.csep[lane];
     for (int d = 0; d < 3; ++d) {
       int r = 3 * lane + d;
-      float* f6 = s.rf6[r];
-      cross3(P, dirs[d], f6);
-      f6[3] = dirs[d][0]; f6[4] = dirs[d][1]; f6[5] = dirs[d][2];
+      for (int k = 0; k < 3; ++k) s.cdir[lane][d][k] = dirs[d][k];
       s.rlink[r] = s.clink[lane];
       s.rsign[r] = 0.f;
       s.rmeta[r][1] = d == 0 ? (sp < 0.f ? fminf(K.sim.baumgarte * fmaxf(-sp - K.sim.slop, 0.f) / dt,
@@ -929,9 +927,12 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       const int r = r0 + u;
       // branch-free: contact row -> S_j . f6 on the link's path; limit row -> +-1 at its dof
       const int lk = s.rlink[r];
-      float f6[6];
-#pragma unroll
-      for (int a = 0; a < 6; ++a) f6[a] = s.rf6[r][a];
+      const int c = r / 3;  // contact of a contact row (r < 3 MAXC = MAXR)
+      const float* P = s.cpt[c];
+      const float* dir = s.cdir[c][r - 3 * c];
+      float f6[6];  // spatial force direction [P x d; d]
+      cross3(P, dir, f6);
+      f6[3] = dir[0]; f6[4] = dir[1]; f6[5] = dir[2];
       const float sg = s.rsign[r];
       const bool onpath = lk >= 0 && ((dsub >> (lk & 31)) & 1u);
       const float jcon = dot6(Sj, f6);
