@@ -545,28 +545,49 @@ __device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, 
 //     (alpha, beta) = (1, a_iP D)  for i not in P   (a_ij - a_iP D a_Pj;  a_iP <- a_iP D)
 //     (alpha, beta) = (0, -D_t)    for pivot lane t (D a_Pj;  a_PP <- -D).
 // After all rounds the rotation is back to the identity and the rows hold -H^-1.
+// 4x4 SPD inverse by 2x2 blocks (Schur complement): two 2x2 determinant inverses instead of four
+// sequential pivots, so the chain on each sweep round's critical path is two divisions deep.
+//   M = [A B; C D]:  Ai = A^-1, X = Ai B, Y = C Ai, S = D - C X, Si = S^-1,
+//   M^-1 = [Ai + (X Si) Y, -(X Si); -(Si Y), Si]       (oracle/physics.c block_inverse: same order)
+__device__ __forceinline__ void inv2(float a, float b, float c, float d, float (&o)[2][2]) {
+  const float id = 1.0f / (a * d - b * c);
+  o[0][0] = d * id; o[0][1] = -b * id; o[1][0] = -c * id; o[1][1] = a * id;
+}
+__device__ __forceinline__ void mul2(const float (&x)[2][2], const float (&y)[2][2], float (&o)[2][2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) o[i][j] = x[i][0] * y[0][j] + x[i][1] * y[1][j];
+}
 template <int B>
-__device__ __forceinline__ void block_inverse(float (&M)[B][B]) {  // M <- M^-1 (SPD), sweep order
+__device__ __forceinline__ void block_inverse(float (&M)[B][B]) {  // M <- M^-1 (SPD)
+  static_assert(B == 4, "2x2-block Schur inverse");
+  const float A[2][2] = {{M[0][0], M[0][1]}, {M[1][0], M[1][1]}};
+  const float Bm[2][2] = {{M[0][2], M[0][3]}, {M[1][2], M[1][3]}};
+  const float C[2][2] = {{M[2][0], M[2][1]}, {M[3][0], M[3][1]}};
+  const float D[2][2] = {{M[2][2], M[2][3]}, {M[3][2], M[3][3]}};
+  float Ai[2][2], X[2][2], Y[2][2], CX[2][2], S[2][2], Si[2][2], XS[2][2], XSY[2][2], SY[2][2];
+  inv2(A[0][0], A[0][1], A[1][0], A[1][1], Ai);
+  mul2(Ai, Bm, X);
+  mul2(C, Ai, Y);
+  mul2(C, X, CX);
 #pragma unroll
-  for (int k = 0; k < B; ++k) {
-    const float r = 1.0f / M[k][k];
-    float col[B], row[B];
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int i = 0; i < B; ++i) { col[i] = M[i][k]; row[i] = M[k][i]; }
+    for (int j = 0; j < 2; ++j) S[i][j] = D[i][j] - CX[i][j];
+  inv2(S[0][0], S[0][1], S[1][0], S[1][1], Si);
+  mul2(X, Si, XS);
+  mul2(XS, Y, XSY);
+  mul2(Si, Y, SY);
 #pragma unroll
-    for (int i = 0; i < B; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < B; ++j) {
-        if (i == k && j == k) M[i][j] = -r;
-        else if (i == k) M[i][j] = r * row[j];
-        else if (j == k) M[i][j] = r * col[i];
-        else M[i][j] = M[i][j] - col[i] * (r * row[j]);
-      }
-  }
-#pragma unroll
-  for (int i = 0; i < B; ++i)
-#pragma unroll
-    for (int j = 0; j < B; ++j) M[i][j] = -M[i][j];
+    for (int j = 0; j < 2; ++j) {
+      M[i][j] = Ai[i][j] + XSY[i][j];
+      M[i][2 + j] = -XS[i][j];
+      M[2 + i][j] = -SY[i][j];
+      M[2 + i][2 + j] = Si[i][j];
+    }
 }
 
 template <int NP, int B>

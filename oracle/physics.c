@@ -289,26 +289,45 @@ static void rnea_bias(const or_model_t* m, const kin_t* K, const float* u, float
 /* Inverse of the SPD joint-space inertia by the block sweep operator on SWEEP_B x SWEEP_B pivot
  * blocks (no pivoting needed for SPD), in the arithmetic of the HIP kernel (sweep_inverse /
  * block_inverse in csrc/allsteps_kernels.hip).  The matrix is padded to a multiple of SWEEP_B with
- * identity rows/columns.  Round on P = {p..p+B-1}: D = (a_PP)^-1 by an in-block scalar sweep;
+ * identity rows/columns.  Round on P = {p..p+B-1}: D = (a_PP)^-1 by 2x2-block Schur complement;
  * row'_j = alpha a_ij - sum_c beta_c a_Pc,j for j not in P, row'_P = beta, where
  * (alpha, beta) = (1, a_iP D) for i not in P and (0, -D_t) for pivot row t.  After all rounds
  * a = -H^-1; the result is negated. */
 #define SWEEP_B 4
+/* 4x4 SPD inverse by 2x2 blocks (Schur complement), the kernel's block_inverse:
+ *   M = [A B; C D]: Ai = A^-1, X = Ai B, Y = C Ai, S = D - C X, Si = S^-1,
+ *   M^-1 = [Ai + (X Si) Y, -(X Si); -(Si Y), Si]. */
+static void inv2(float a, float b, float c, float d, float o[2][2]) {
+  const float id = 1.0f / (a * d - b * c);
+  o[0][0] = d * id; o[0][1] = -b * id; o[1][0] = -c * id; o[1][1] = a * id;
+}
+static void mul2(const float x[2][2], const float y[2][2], float o[2][2]) {
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) o[i][j] = x[i][0] * y[0][j] + x[i][1] * y[1][j];
+}
 static void block_inverse(float M[SWEEP_B][SWEEP_B]) {
-  for (int k = 0; k < SWEEP_B; ++k) {
-    const float r = 1.0f / M[k][k];
-    float col[SWEEP_B], row[SWEEP_B];
-    for (int i = 0; i < SWEEP_B; ++i) { col[i] = M[i][k]; row[i] = M[k][i]; }
-    for (int i = 0; i < SWEEP_B; ++i)
-      for (int j = 0; j < SWEEP_B; ++j) {
-        if (i == k && j == k) M[i][j] = -r;
-        else if (i == k) M[i][j] = r * row[j];
-        else if (j == k) M[i][j] = r * col[i];
-        else M[i][j] = M[i][j] - col[i] * (r * row[j]);
-      }
-  }
-  for (int i = 0; i < SWEEP_B; ++i)
-    for (int j = 0; j < SWEEP_B; ++j) M[i][j] = -M[i][j];
+  float A[2][2] = {{M[0][0], M[0][1]}, {M[1][0], M[1][1]}};
+  float Bm[2][2] = {{M[0][2], M[0][3]}, {M[1][2], M[1][3]}};
+  float C[2][2] = {{M[2][0], M[2][1]}, {M[3][0], M[3][1]}};
+  float D[2][2] = {{M[2][2], M[2][3]}, {M[3][2], M[3][3]}};
+  float Ai[2][2], X[2][2], Y[2][2], CX[2][2], S[2][2], Si[2][2], XS[2][2], XSY[2][2], SY[2][2];
+  inv2(A[0][0], A[0][1], A[1][0], A[1][1], Ai);
+  mul2(Ai, Bm, X);
+  mul2(C, Ai, Y);
+  mul2(C, X, CX);
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) S[i][j] = D[i][j] - CX[i][j];
+  inv2(S[0][0], S[0][1], S[1][0], S[1][1], Si);
+  mul2(X, Si, XS);
+  mul2(XS, Y, XSY);
+  mul2(Si, Y, SY);
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) {
+      M[i][j] = Ai[i][j] + XSY[i][j];
+      M[i][2 + j] = -XS[i][j];
+      M[2 + i][j] = -SY[i][j];
+      M[2 + i][2 + j] = Si[i][j];
+    }
 }
 
 static void sweep_inverse(float* h, int n) {
