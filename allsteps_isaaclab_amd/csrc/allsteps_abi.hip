@@ -107,6 +107,11 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
     for (int i = l; i > 0; i = model->parent[i]) mask |= 1u << (6 + i - 1);
     h.ancmask[l] = mask;
   }
+  for (int j = 0; j < h.nv; ++j)
+    for (int k = 0; k < h.nv; ++k) {
+      const int lk = k < 6 ? 0 : k - 5;
+      if ((h.ancmask[lk] >> j) & 1u) h.ddesc[j] |= 1u << k;
+    }
   if (!as::step_supported_nv(h.nv))
     return fail(AS_ERR_INVALID, "as_create: no k_step instantiation for " + std::to_string(h.nv) + " dofs");
 

@@ -29,6 +29,7 @@ struct Consts {
   uint32_t lsub[kMaxLinks];        // links in the subtree of link, itself included
   uint32_t ancmask[kMaxLinks];     // dofs on the path root..link (root dofs 0-5 always set)
   uint32_t dsub[kMaxDofs];         // links moved by dof j (subtree of its link; root dofs: all)
+  uint32_t ddesc[kMaxDofs];        // dofs k whose link path contains dof j (bit k)
 };
 
 struct StepArgs {

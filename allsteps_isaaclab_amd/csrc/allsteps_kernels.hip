@@ -517,17 +517,19 @@ __device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, 
   const int j = lane < NV ? lane : 0;
   const int lj = j < 6 ? 0 : j - 5;
   const uint32_t anc_j = K.ancmask[lj];
+  const uint32_t jon = K.ddesc[j];
   float Sj[6], Fj[6];
 #pragma unroll
   for (int a = 0; a < 6; ++a) { Sj[a] = s.S[j][a]; Fj[a] = s.x.d.Fh[j][a]; }
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    const int lk = k < 6 ? 0 : k - 5;
     const bool k_on_j = (anc_j >> k) & 1u;
-    const bool j_on_k = (K.ancmask[lk] >> j) & 1u;
+    const bool j_on_k = (jon >> k) & 1u;
     float v1 = dot6(s.S[k], Fj);
     float v2 = dot6(Sj, s.x.d.Fh[k]);
     float h = k_on_j ? v1 : (j_on_k ? v2 : 0.f);
+    // (the armature load stays under the k == j branch: hoisting it lets the scheduler issue all
+    // 12 NV loads of this loop up front, which spills)
     if (k == j && j >= 6) h += K.model.armature[j - 5];
     Hr[k] = lane < NV ? h : 0.f;
   }
