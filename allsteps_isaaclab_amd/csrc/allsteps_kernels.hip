@@ -1400,7 +1400,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_obs(ObsArgs P) {
+__global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
   const Consts& K = *(const Consts*)(CK*)P.consts;
   const as_task_t& T = K.task;
   const as_model_t& m = K.model;
@@ -1514,8 +1514,10 @@ hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream) {
 }
 
 hipError_t launch_obs(const ObsArgs& a, hipStream_t stream) {
-  int blocks = (a.n + 255) / 256;
-  hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(256), 0, stream, a);
+  // 64-thread workgroups: one wave per CU spreads the (latency-bound, one env per lane) work over
+  // 4x as many CUs and their L1 / address paths
+  int blocks = (a.n + 63) / 64;
+  hipLaunchKernelGGL(k_obs, dim3(blocks), dim3(64), 0, stream, a);
   return hipGetLastError();
 }
 
