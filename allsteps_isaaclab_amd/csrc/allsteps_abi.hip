@@ -35,6 +35,7 @@ struct as_env {
   as_state_t st;
   as::Consts* consts_dev;
   int32_t* counters_dev;
+  uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_fix
   int32_t num_steps;
   int32_t nv;
   // optional per-launch timing (as_profile): event triples around k_step / k_obs
@@ -124,7 +125,10 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   env->num_steps = task->num_steps;
   env->nv = h.nv;
   if (hipMalloc(&env->consts_dev, sizeof(as::Consts)) != hipSuccess ||
-      hipMalloc(&env->counters_dev, 4 * sizeof(int32_t)) != hipSuccess) {
+      hipMalloc(&env->counters_dev, 4 * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&env->side_dev, (size_t)as::kSideWords * num_envs * sizeof(uint32_t)) != hipSuccess) {
+    (void)hipFree(env->consts_dev);
+    (void)hipFree(env->counters_dev);
     delete env;
     return fail(AS_ERR_HIP, "as_create: hipMalloc failed");
   }
@@ -140,6 +144,7 @@ int as_destroy(as_env_t* env) {
   for (hipEvent_t e : env->ev) (void)hipEventDestroy(e);
   (void)hipFree(env->consts_dev);
   (void)hipFree(env->counters_dev);
+  (void)hipFree(env->side_dev);
   delete env;
   return AS_OK;
 }
@@ -162,6 +167,8 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   a.seed = env->seed;
   a.env_offset = env->env_offset;
   a.stamps = env->stamps;
+  a.obs = mode == as::kModePhysics ? nullptr : obs;
+  a.side = env->side_dev;
   const bool prof = env->prof_n < env->prof_cap;
   if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n], s));
   HIP_TRY(as::launch_step(a, env->nv, s));
@@ -179,6 +186,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   o.n = env->n;
   o.counters = env->counters_dev;
   o.obs = obs;
+  o.side = env->side_dev;
   HIP_TRY(as::launch_obs(o, s));
   if (prof) {
     HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 2], s));

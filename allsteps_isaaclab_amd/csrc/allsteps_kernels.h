@@ -39,6 +39,8 @@ struct StepArgs {
   int32_t mode;
   const float* actions;
   float* reward;
+  float* obs;                  // [n][59] observation rows (speculative second tick, see k_step)
+  uint32_t* side;              // [kSideWords][n]: tick-#1 state and observation entries for k_fix
   uint8_t* terminated;
   uint8_t* truncated;
   const float* reset_draws;
@@ -54,12 +56,19 @@ enum {
   kStIntegrate, kStTask, kStReset, kStStore, kNumStamps
 };
 
+// side buffer of k_step -> k_fix: idx, prev, next, count, swing, pot, old_pot, foot_contact[2]
+// (tick-#1 state) and foot_contact[2], targets[9] (tick-#1 observation entries 48..58)
+constexpr int kSideState = 9;
+constexpr int kSideObs = 11;
+constexpr int kSideWords = kSideState + kSideObs;
+
 struct ObsArgs {
   const Consts* consts;
   as_state_t st;
   int32_t n;
   const int32_t* counters;
   float* obs;
+  const uint32_t* side;
 };
 
 struct StonesArgs {

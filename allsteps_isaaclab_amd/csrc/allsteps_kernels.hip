@@ -67,6 +67,7 @@ struct alignas(16) ConScratch {
 };
 union alignas(16) PhaseScratch {
   DynScratch d;
+  float obs[64];        // epilogue: observation row staging
   struct {
     float g[32][8];     // collide: geom segment endpoints, radius, packed type/foot/link
     int pl[64];         //          pending (stone << 8 | geom) pairs, stone-major
@@ -1364,6 +1365,62 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
   }
   __syncthreads();
+  // ---- observation with a speculative second tick (allsteps_env.py:326-345, 567).  The reference
+  //      re-runs _compute_useful_values for ALL envs when ANY env reset this step -- a launch-wide
+  //      condition.  The tick is applied here as if some env reset (true at any realistic env
+  //      count); the tick-#1 state and the tick-dependent observation entries (foot contact,
+  //      targets) go to a side buffer, and k_fix restores them in a launch where no env reset.
+  if (P.obs) {
+    int i2 = idx, p2 = prev, n2 = next, c2 = count, w2 = swing;
+    float pot2 = pot, op2 = old_pot, fc2[2] = {fc[0], fc[1]};
+    Useful u2;
+    compute_useful(K, s.root_pos, s.root_quat, bp, s.stones, 1, s.mask[0], s.mask[1], i2, p2, n2, c2, w2, pot2,
+                   op2, fc2, true, u2);
+    float* ob = s.x.obs;
+    uint32_t* side = P.side;
+    if (lane == 0) {
+      ob[0] = u2.h;
+      ob[1] = u2.roll;
+      ob[2] = u2.pitch;
+      float vb[3];
+      quat_rotate_inverse(s.root_quat, s.u, vb);
+      ob[3] = vb[0]; ob[4] = vb[1]; ob[5] = vb[2];
+      ob[48] = fc2[0];
+      ob[49] = fc2[1];
+    }
+    if (lane < nh) {
+      const int li = m.cfg_dof_link[lane];
+      ob[6 + lane] = scale_transform(s.qi[li - 1], m.lower[li], m.upper[li]);
+      ob[27 + lane] = fminf(fmaxf(s.u[6 + li - 1] * T.dof_vel_scale, -5.f), 5.f);
+    }
+    if (lane < 6) {  // lanes 0-2: targets after the second tick, lanes 3-5: after the first
+      const int t = lane < 3 ? lane : lane - 3;
+      const int ti = lane < 3 ? (t == 0 ? p2 : (t == 1 ? i2 : n2)) : (t == 0 ? prev : (t == 1 ? idx : next));
+      const float tw[3] = {s.stones[3 * ti], s.stones[3 * ti + 1], s.stones[3 * ti + 2]};
+      float o3[3];
+      subtract_frame_transforms(s.root_pos, s.root_quat, tw, o3);
+      if (lane < 3) {
+        for (int k = 0; k < 3; ++k) ob[50 + 3 * t + k] = o3[k];
+      } else if (valid) {
+        for (int k = 0; k < 3; ++k) side[(kSideState + 2 + 3 * t + k) * n + e] = __float_as_uint(o3[k]);
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      float* orow = P.obs + (size_t)e * AS_OBS_DIM;
+      orow[lane] = ob[lane];
+      if (lane < AS_OBS_DIM - 32) orow[32 + lane] = ob[32 + lane];
+      if (lane == 0) {
+        const uint32_t sv[kSideState + 2] = {(uint32_t)idx, (uint32_t)prev, (uint32_t)next, (uint32_t)count,
+                                             (uint32_t)swing, __float_as_uint(pot), __float_as_uint(old_pot),
+                                             __float_as_uint(fc[0]), __float_as_uint(fc[1]),
+                                             __float_as_uint(fc[0]), __float_as_uint(fc[1])};
+        for (int k = 0; k < kSideState + 2; ++k) side[k * n + e] = sv[k];
+      }
+    }
+    idx = i2; prev = p2; next = n2; count = c2; swing = w2;
+    pot = pot2; old_pot = op2; fc[0] = fc2[0]; fc[1] = fc2[1];
+  }
   ts.mark(kStReset);
   // ---- store
   if (valid) {
@@ -1400,55 +1457,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 }
 
 // ------------------------------------------------------------------------------------------------
+// K2: the launch-wide part of the observation step.  If any env reset this step (device counter
+// written by k_step): the curriculum gate (allsteps_env.py:471-479, evaluated on the tick-#1 target
+// indices) -- k_step has already applied the second tick.  If none did: restore the tick-#1 state
+// and observation entries k_step saved in the side buffer.
 __global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
   const Consts& K = *(const Consts*)(CK*)P.consts;
   const as_task_t& T = K.task;
-  const as_model_t& m = K.model;
   const int n = P.n;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int any_reset = P.counters[0];
-  if (any_reset && e == 0) {  // allsteps_env.py:471-479 (evaluated once, before the resets' tick #2)
-    int c = P.st.curriculum[0];
-    if ((float)P.counters[1] / (float)n > (float)T.curriculum_threshold) P.st.curriculum[0] = min(c + 1, T.max_curriculum);
+  if (any_reset) {
+    if (e == 0) {
+      int c = P.st.curriculum[0];
+      if ((float)P.counters[1] / (float)n > (float)T.curriculum_threshold) P.st.curriculum[0] = min(c + 1, T.max_curriculum);
+    }
+    return;
   }
   if (e >= n) return;
   const as_state_t& st = P.st;
-  float rp[3] = {st.root_pos[e], st.root_pos[n + e], st.root_pos[2 * n + e]};
-  float rq[4] = {st.root_quat[e], st.root_quat[n + e], st.root_quat[2 * n + e], st.root_quat[3 * n + e]};
-  float bp[9];
-  for (int k = 0; k < 9; ++k) bp[k] = st.body_pos[k * n + e];
-  int idx = st.idx[e], prev = st.prev[e], next = st.next[e], count = st.count[e], swing = st.swing[e];
-  float pot = st.pot[e], old_pot = st.old_pot[e];
-  float fc[2] = {st.foot_contact[e], st.foot_contact[n + e]};
-  Useful u;
-  compute_useful(K, rp, rq, bp, st.stones + e, n, st.contact_mask[e], st.contact_mask[n + e], idx, prev,
-                 next, count, swing, pot, old_pot, fc, any_reset != 0, u);
-  if (any_reset) {  // tick #2 results persist (allsteps_env.py:567)
-    st.idx[e] = idx; st.prev[e] = prev; st.next[e] = next; st.count[e] = count; st.swing[e] = swing;
-    st.pot[e] = pot; st.old_pot[e] = old_pot;
-    st.foot_contact[e] = fc[0]; st.foot_contact[n + e] = fc[1];
-  }
-  // allsteps_env.py:326-345 observation
+  const uint32_t* sd = P.side;
+  st.idx[e] = (int)sd[e];
+  st.prev[e] = (int)sd[n + e];
+  st.next[e] = (int)sd[2 * n + e];
+  st.count[e] = (int)sd[3 * n + e];
+  st.swing[e] = (int)sd[4 * n + e];
+  st.pot[e] = __uint_as_float(sd[5 * n + e]);
+  st.old_pot[e] = __uint_as_float(sd[6 * n + e]);
+  st.foot_contact[e] = __uint_as_float(sd[7 * n + e]);
+  st.foot_contact[n + e] = __uint_as_float(sd[8 * n + e]);
   float* o = P.obs + (size_t)e * AS_OBS_DIM;
-  o[0] = u.h;
-  o[1] = u.roll;
-  o[2] = u.pitch;
-  float lv[3] = {st.root_lin[e], st.root_lin[n + e], st.root_lin[2 * n + e]}, vb[3];
-  quat_rotate_inverse(rq, lv, vb);
-  o[3] = vb[0]; o[4] = vb[1]; o[5] = vb[2];
-  for (int k = 0; k < AS_ACT_DIM; ++k) {
-    int li = m.cfg_dof_link[k];
-    o[6 + k] = scale_transform(st.q[k * n + e], m.lower[li], m.upper[li]);
-    o[27 + k] = fminf(fmaxf(st.qd[k * n + e] * T.dof_vel_scale, -5.f), 5.f);
-  }
-  o[48] = fc[0];
-  o[49] = fc[1];
-  const int tix[3] = {prev, idx, next};
-  for (int t = 0; t < 3; ++t) {
-    float tw[3] = {st.stones[(tix[t] * 3 + 0) * n + e], st.stones[(tix[t] * 3 + 1) * n + e],
-                   st.stones[(tix[t] * 3 + 2) * n + e]};
-    subtract_frame_transforms(rp, rq, tw, o + 50 + 3 * t);
-  }
+  for (int k = 0; k < kSideObs; ++k) o[48 + k] = __uint_as_float(sd[(kSideState + k) * n + e]);
 }
 
 // ------------------------------------------------------------------------------------------------
