@@ -34,7 +34,8 @@ struct as_env {
   int64_t env_offset;
   as_state_t st;
   as::Consts* consts_dev;
-  int32_t* counters_dev;
+  int32_t* counters_dev;  // two banks of 4: step t uses bank t % 2, k_obs clears the other
+  int32_t bank = 0, last_bank = 0;
   uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_fix
   int32_t num_steps;
   int32_t nv;
@@ -125,7 +126,7 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   env->num_steps = task->num_steps;
   env->nv = h.nv;
   if (hipMalloc(&env->consts_dev, sizeof(as::Consts)) != hipSuccess ||
-      hipMalloc(&env->counters_dev, 4 * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&env->counters_dev, 8 * sizeof(int32_t)) != hipSuccess ||
       hipMalloc(&env->side_dev, (size_t)as::kSideWords * num_envs * sizeof(uint32_t)) != hipSuccess) {
     (void)hipFree(env->consts_dev);
     (void)hipFree(env->counters_dev);
@@ -133,7 +134,7 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
     return fail(AS_ERR_HIP, "as_create: hipMalloc failed");
   }
   HIP_TRY(hipMemcpy(env->consts_dev, &h, sizeof(as::Consts), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(env->counters_dev, 0, 4 * sizeof(int32_t)));
+  HIP_TRY(hipMemset(env->counters_dev, 0, 8 * sizeof(int32_t)));
   *out = env;
   return AS_OK;
 }
@@ -152,7 +153,9 @@ int as_destroy(as_env_t* env) {
 static int run(as_env_t* env, int mode, const float* actions, float* obs, float* reward, uint8_t* term,
                uint8_t* trunc, const float* reset_draws, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  HIP_TRY(hipMemsetAsync(env->counters_dev, 0, 4 * sizeof(int32_t), s));
+  // no memset per step: this launch's counter bank was cleared by the previous launch's k_obs
+  // (physics-only launches do not touch the counters and keep the bank)
+  int32_t* cnt = env->counters_dev + 4 * env->bank;
   as::StepArgs a{};
   a.consts = env->consts_dev;
   a.st = env->st;
@@ -163,7 +166,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   a.terminated = term;
   a.truncated = trunc;
   a.reset_draws = reset_draws;
-  a.counters = env->counters_dev;
+  a.counters = cnt;
   a.seed = env->seed;
   a.env_offset = env->env_offset;
   a.stamps = env->stamps;
@@ -184,7 +187,10 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   o.consts = env->consts_dev;
   o.st = env->st;
   o.n = env->n;
-  o.counters = env->counters_dev;
+  o.counters = cnt;
+  o.next_counters = env->counters_dev + 4 * (env->bank ^ 1);
+  env->last_bank = env->bank;
+  env->bank ^= 1;
   o.obs = obs;
   o.side = env->side_dev;
   HIP_TRY(as::launch_obs(o, s));
@@ -277,7 +283,7 @@ int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* s
 
 int as_step_counters(as_env_t* env, const int32_t** counters_dev) {
   if (!env || !counters_dev) return fail(AS_ERR_INVALID, "as_step_counters: null argument");
-  *counters_dev = env->counters_dev;
+  *counters_dev = env->counters_dev + 4 * env->last_bank;
   return AS_OK;
 }
 

@@ -44,7 +44,7 @@ struct StepArgs {
   uint8_t* terminated;
   uint8_t* truncated;
   const float* reset_draws;
-  int32_t* counters;  // [0] any reset, [1] sum of curr_target_index (zeroed before the launch)
+  int32_t* counters;  // [0] any reset, [1] sum of curr_target_index (zero at launch: see k_obs)
   uint64_t seed;
   int64_t env_offset;
   unsigned long long* stamps;  // diagnostic phase timing (s_memtime deltas summed over waves) or null
@@ -67,6 +67,7 @@ struct ObsArgs {
   as_state_t st;
   int32_t n;
   const int32_t* counters;
+  int32_t* next_counters;  // the other bank, cleared here for the next launch
   float* obs;
   const uint32_t* side;
 };

@@ -1467,6 +1467,7 @@ __global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
   const int n = P.n;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int any_reset = P.counters[0];
+  if (e < 4) P.next_counters[e] = 0;  // the next launch's bank (this launch reads the other one)
   if (any_reset) {
     if (e == 0) {
       int c = P.st.curriculum[0];
