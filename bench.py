@@ -31,6 +31,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# BASELINE.json "metric" (the driver compares the line against it)
+BASELINE_METRIC = "env-steps/sec (whole node), Allsteps-v0 at 4096 envs, 1/2/4/8 MI355X"
 
 # Algorithmic bytes per env per launch: every state byte the kernel must read
 # or write once, from the SoA layout of include/allsteps.h.
@@ -150,7 +152,7 @@ def main():
         avg_k = k_ms / max(launches, 1) / 1e3  # s per k_step launch
         achieved = K_STEP_BYTES * n / avg_k / 1e9
         line = {
-            "metric": "env-steps/sec (whole node), Allsteps-v0 at 4096 envs per GPU",
+            "metric": BASELINE_METRIC,
             "value": round(value, 1),
             "unit": "env-steps/s",
             "n_gpus": world,
