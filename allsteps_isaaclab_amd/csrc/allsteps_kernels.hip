@@ -33,7 +33,9 @@ constexpr int NVMAX = 6 + LMAX - 1; // generalized velocities
 constexpr int MAXC = AS_MAX_CONTACTS;
 constexpr int MAXR = AS_MAX_ROWS;
 constexpr int NST = AS_NUM_STONES;
-constexpr int GOLDEN_ITERS = 14;
+constexpr int kSectionLanes = 4;    // lanes per (stone, capsule) pair in the section search
+constexpr int kSectionIters = 8;    // interval shrinks by 2/5 per round: 0.4^8 = 6.6e-4
+constexpr int kPairsPerChunk = G / kSectionLanes;
 constexpr int kSweepB = 4;        // pivot block of the H^-1 sweep
 
 static_assert(NVMAX <= G, "one lane per generalized velocity");
@@ -701,9 +703,10 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   // narrowphase in two passes.  (A) lane = geom, loop over the candidate stones: the cheap
   // bounding test (spheres: the exact separation) appends the surviving (stone, geom) pairs to a
   // list in LDS, stone-major and geom-minor -- the oracle's emission order.  (B) lane = pair, in
-  // chunks of 32: the exact test (capsules: golden-section search) and the contacts, emitted in
-  // list order by a prefix sum.  A chunk is flushed as soon as 32 pairs are pending, so the list
-  // never exceeds 32 + 22 entries, and the search stops once this env has MAXC contacts.
+  // chunks of kPairsPerChunk (4 lanes per pair): the exact test (capsules: a 4-point section
+  // search) and the contacts, emitted in list order by a prefix sum.  A chunk is flushed as soon as
+  // kPairsPerChunk pairs are pending, so the list never exceeds 8 + 22 entries, and the search stops
+  // once this env has MAXC contacts.
   {
     float* gs = s.x.col.g[lane];  // staging of this lane's geom for pass B
     if (gv) {
@@ -715,22 +718,54 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   }
   int* pl = s.x.col.pl;
   int pend = 0, base = 0;
-  auto flush = [&](int npairs) {  // pass B over pl[0, npairs) (npairs <= 32), then shift the rest
+  auto flush = [&](int npairs) {  // pass B over pl[0, npairs) (npairs <= kPairsPerChunk), shift the rest
+    // kSectionLanes lanes per pair: lane q of a group evaluates one of the section points
+    const int pi = lane / kSectionLanes, q = lane % kSectionLanes;
     int cnt = 0, plink = 0, pst = 0, pfoot = -1;
     float P0[3], N0[3], P1[3], N1[3], P2[3], N2[3], SEP0 = 0.f, SEP1 = 0.f, SEP2 = 0.f, pr = 0.f;
-    if (lane < npairs) {
-      const int e = pl[lane];
-      const int gi = e & 0xff;
-      pst = e >> 8;
-      const float* q = s.x.col.g[gi];
-      const float A[3] = {q[0], q[1], q[2]}, Bb[3] = {q[3], q[4], q[5]};
-      pr = q[6];
-      const int meta = __float_as_int(q[7]);
-      const int pty = meta & 15;
-      pfoot = ((meta >> 4) & 15) - 1;
-      plink = meta >> 8;
-      float c[3];
-      for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * pst + k] - s.root_pos[k];
+    const bool act = pi < npairs;
+    const int e = pl[act ? pi : 0];
+    const int gi = e & 0xff;
+    pst = e >> 8;
+    const float* gq = s.x.col.g[gi];
+    const float A[3] = {gq[0], gq[1], gq[2]}, Bb[3] = {gq[3], gq[4], gq[5]};
+    pr = gq[6];
+    const int meta = __float_as_int(gq[7]);
+    const int pty = meta & 15;
+    pfoot = ((meta >> 4) & 15) - 1;
+    plink = meta >> 8;
+    float c[3];
+    for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * pst + k] - s.root_pos[k];
+    // capsule: section search for the minimum of the (convex) signed distance along the segment.
+    // Each round the kSectionLanes lanes of the pair evaluate the interior points
+    // lo + (q+1)(hi-lo)/(kSectionLanes+1); the interval shrinks to the two sub-intervals around
+    // the smallest value (ties to the lowest q).  Runs for every group (the result is only used
+    // by capsule pairs) so the DPP exchanges see all four lanes.
+    float lo = 0.f, hi = 1.f;
+#pragma unroll 1
+    for (int it = 0; it < kSectionIters; ++it) {
+      const float w = (hi - lo) * (1.0f / (kSectionLanes + 1));
+      const float t = lo + (float)(q + 1) * w;
+      float Q[3], tn[3];
+      for (int k = 0; k < 3; ++k) Q[k] = A[k] + t * (Bb[k] - A[k]);
+      float f = sd_box(Q, c, h, tn);
+      int qi = q;
+      // argmin over the 4 lanes of the group: quad_perm [1,0,3,2] then [2,3,0,1]
+      {
+        const float f1 = dpp<0xB1>(f);
+        const int q1 = __builtin_amdgcn_update_dpp(0, qi, 0xB1, 0xF, 0xF, false);
+        const bool tk = f1 < f || (f1 == f && q1 < qi);
+        f = tk ? f1 : f; qi = tk ? q1 : qi;
+        const float f2 = dpp<0x4E>(f);
+        const int q2 = __builtin_amdgcn_update_dpp(0, qi, 0x4E, 0xF, 0xF, false);
+        const bool tk2 = f2 < f || (f2 == f && q2 < qi);
+        f = tk2 ? f2 : f; qi = tk2 ? q2 : qi;
+      }
+      const float nlo = lo + (float)qi * w;
+      hi = lo + (float)(qi + 2) * w;
+      lo = nlo;
+    }
+    if (act && q == 0) {
       float nr[3];
       if (pty == 0) {
         float sd = sd_box(A, c, h, nr) - pr;
@@ -740,27 +775,9 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
           cnt = 1;
         }
       } else {
-        float n0[3], n1[3], tn[3];
+        float n0[3], n1[3];
         float s0 = sd_box(A, c, h, n0) - pr;
         float s1 = sd_box(Bb, c, h, n1) - pr;
-        const float gr = 0.6180339887f;
-        float lo = 0.f, hi = 1.f;
-        float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
-        float Q1[3], Q2[3];
-        for (int k = 0; k < 3; ++k) { Q1[k] = A[k] + x1 * (Bb[k] - A[k]); Q2[k] = A[k] + x2 * (Bb[k] - A[k]); }
-        float f1 = sd_box(Q1, c, h, tn), f2 = sd_box(Q2, c, h, tn);
-#pragma unroll 1
-        for (int it = 0; it < GOLDEN_ITERS; ++it) {
-          if (f1 < f2) {
-            hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
-            for (int k = 0; k < 3; ++k) Q1[k] = A[k] + x1 * (Bb[k] - A[k]);
-            f1 = sd_box(Q1, c, h, tn);
-          } else {
-            lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
-            for (int k = 0; k < 3; ++k) Q2[k] = A[k] + x2 * (Bb[k] - A[k]);
-            f2 = sd_box(Q2, c, h, tn);
-          }
-        }
         float ts = 0.5f * (lo + hi), Ps[3], ns[3];
         for (int k = 0; k < 3; ++k) Ps[k] = A[k] + ts * (Bb[k] - A[k]);
         float ss = sd_box(Ps, c, h, ns) - pr;
@@ -815,7 +832,7 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
     if (need) pl[pend + __popc(bl & ((1u << lane) - 1u))] = (st << 8) | lane;
     pend += __popc(bl);
     __syncthreads();
-    if (pend >= 32) flush(32);
+    if (pend >= kPairsPerChunk) flush(kPairsPerChunk);
   }
   if (pend > 0 && base < MAXC) flush(pend);
   __syncthreads();

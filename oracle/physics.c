@@ -416,7 +416,8 @@ static void add_contact(contacts_t* C, int link, int stone, int foot, const floa
   for (int k = 0; k < 3; ++k) { C->nrm[c][k] = nrm[k]; C->pt[c][k] = P[k] - nrm[k] * r; }
 }
 
-#define GOLDEN_ITERS 14
+#define SECTION_LANES 4
+#define SECTION_ITERS 8
 
 static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, const float* stones_rel, int nst,
                     contacts_t* C) {
@@ -468,23 +469,24 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
       float n0[3], n1[3];
       float s0 = sd_box(a, c, h, n0) - r;
       float s1 = sd_box(b, c, h, n1) - r;
-      /* golden-section minimisation of the (convex) sd along the segment */
-      const float gr = 0.6180339887f;
-      float lo = 0.f, hi = 1.f;
-      float x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
-      float P1[3], P2[3], tn[3];
-      for (int k = 0; k < 3; ++k) { P1[k] = a[k] + x1 * (b[k] - a[k]); P2[k] = a[k] + x2 * (b[k] - a[k]); }
-      float f1 = sd_box(P1, c, h, tn), f2 = sd_box(P2, c, h, tn);
-      for (int it = 0; it < GOLDEN_ITERS; ++it) {
-        if (f1 < f2) {
-          hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
-          for (int k = 0; k < 3; ++k) P1[k] = a[k] + x1 * (b[k] - a[k]);
-          f1 = sd_box(P1, c, h, tn);
-        } else {
-          lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
-          for (int k = 0; k < 3; ++k) P2[k] = a[k] + x2 * (b[k] - a[k]);
-          f2 = sd_box(P2, c, h, tn);
+      /* section search for the minimum of the (convex) sd along the segment, the HIP kernel's
+       * 4-lane form: each round evaluates lo + (q+1)(hi-lo)/5, q = 0..3, and keeps the two
+       * sub-intervals around the smallest value (ties to the lowest q) */
+      float lo = 0.f, hi = 1.f, tn[3];
+      for (int it = 0; it < SECTION_ITERS; ++it) {
+        const float w = (hi - lo) * (1.0f / (SECTION_LANES + 1));
+        float fb = 0.f;
+        int qb = 0;
+        for (int q = 0; q < SECTION_LANES; ++q) {
+          const float t = lo + (float)(q + 1) * w;
+          float Q[3];
+          for (int k = 0; k < 3; ++k) Q[k] = a[k] + t * (b[k] - a[k]);
+          const float f = sd_box(Q, c, h, tn);
+          if (q == 0 || f < fb) { fb = f; qb = q; }
         }
+        const float nlo = lo + (float)qb * w;
+        hi = lo + (float)(qb + 2) * w;
+        lo = nlo;
       }
       float ts = 0.5f * (lo + hi), Ps[3], ns[3];
       for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (b[k] - a[k]);
