@@ -1035,25 +1035,26 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
     float ln = 0.f;
-    // lambda of row r only changes at row r, so its old value is read from the sweep's starting
-    // vector: the readlanes do not wait on the running updates
-    const float lam_prev = lam;
-    // the row loop is unrolled (registers indexed by constants) with an exit per 4-row block
+    // The row loop is unrolled (registers indexed by constants) with an exit per 4-row block; rows
+    // in [maxrow, block end) have zero J / W / metadata and leave everything unchanged.  Per-row
+    // lane masks would be hoisted out of the sweep loop (and spilled), so lane r is found with a
+    // counter that reaches 0 at row r instead.
+    int dr = lane;
 #pragma unroll
     for (int r = 0; r < MAXR; ++r) {
       if ((r & 3) == 0 && r >= maxrow) break;
-      const bool live = r < maxrow;
       const float4 mt = *reinterpret_cast<const float4*>(s.rmeta[r]);
       const float v = half_sum(Jc[r] * uj);
-      const float l00 = readlane_f(lam_prev, r), l01 = readlane_f(lam_prev, r + 32);
+      const float l00 = readlane_f(lam, r), l01 = readlane_f(lam, r + 32);
       const float l0 = hi ? l01 : l00;
       const float lim = mu * ln;
       const float lt = fminf(fmaxf(l0 - v * mt.x, -lim), lim);
       const float lnrm = fmaxf(l0 + (mt.y - v) * mt.x, 0.f);
       const float l1 = mt.z == 1.f ? lt : lnrm;
       ln = mt.z == 0.f ? l1 : ln;
-      uj += live ? Wc[r] * (l1 - l0) : 0.f;
-      lam = live && lane == r ? l1 : lam;
+      uj += Wc[r] * (l1 - l0);
+      lam = dr == 0 ? l1 : lam;
+      --dr;
     }
   }
   if (lane < MAXR) s.rlam[lane] = lane < maxrow ? lam : 0.f;
