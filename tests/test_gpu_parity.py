@@ -136,12 +136,18 @@ def test_task_logic_golden_replay(orc, oracle_mod):
     env.close()
 
 
-def _random_states(orc, n, steps, seed):
-    """Reference-distribution states: oracle reset then `steps` random-action env steps."""
+def _random_states(orc, n, steps, seed, level=0):
+    """Reference-distribution states: oracle reset then `steps` random-action env steps, on the
+    level-0 straight line or on stones generated at curriculum `level`."""
     st = orc.state(n)
-    for k in range(20):
-        st["stones"][3 * k + 0][:] = 0.75 * k
-        st["stones"][3 * k + 2][:] = np.float32(k * 0.75) * np.cos(np.float32(np.pi / 2), dtype=np.float32)
+    if level == 0:
+        for k in range(20):
+            st["stones"][3 * k + 0][:] = 0.75 * k
+            st["stones"][3 * k + 2][:] = np.float32(k * 0.75) * np.cos(np.float32(np.pi / 2), dtype=np.float32)
+    else:
+        rng = np.random.default_rng(seed + 1000)
+        pos, _ = orc.footsteps(n, level, rng.uniform(0, 1, (5, n, 20)).astype(np.float32))
+        st["stones"][:] = pos.reshape(n, 60).T
     orc.reset_all(st, seed=seed)
     rng = np.random.default_rng(seed)
     for _ in range(steps):
@@ -149,10 +155,10 @@ def _random_states(orc, n, steps, seed):
     return st
 
 
-@pytest.mark.parametrize("warm", [0, 10, 40])
-def test_env_step_parity(orc, warm):
+@pytest.mark.parametrize("warm,level", [(0, 0), (10, 0), (40, 0), (10, 9), (40, 9)])
+def test_env_step_parity(orc, warm, level):
     n = 256
-    st = _random_states(orc, n, warm, seed=7 + warm)
+    st = _random_states(orc, n, warm, seed=7 + warm, level=level)
     env = _env(n)
     _from_oracle(env, st)
     rng = np.random.default_rng(100 + warm)
