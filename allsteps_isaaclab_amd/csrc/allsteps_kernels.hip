@@ -963,32 +963,50 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   static_assert(MAXR % 4 == 0, "row blocks");
 #pragma unroll 1
   for (int r0 = 0; r0 < maxrow; r0 += 4) {
+    // all four rows' inputs are read before any row is stored, so the reads of the block overlap
+    int lk[4];
+    float P[4][3], dir[4][3], sg[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + u;
+      const int c = r / 3;  // contact of a contact row (r < 3 MAXC = MAXR)
+      lk[u] = s.rlink[r];
+      sg[u] = s.rsign[r];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        P[u][k] = s.cpt[c][k];
+        dir[u][k] = s.cdir[c][r - 3 * c][k];
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int r = r0 + u;
       // branch-free: contact row -> S_j . f6 on the link's path; limit row -> +-1 at its dof
-      const int lk = s.rlink[r];
-      const int c = r / 3;  // contact of a contact row (r < 3 MAXC = MAXR)
-      const float* P = s.cpt[c];
-      const float* dir = s.cdir[c][r - 3 * c];
       float f6[6];  // spatial force direction [P x d; d]
-      cross3(P, dir, f6);
-      f6[3] = dir[0]; f6[4] = dir[1]; f6[5] = dir[2];
-      const float sg = s.rsign[r];
-      const bool onpath = lk >= 0 && ((dsub >> (lk & 31)) & 1u);
+      cross3(P[u], dir[u], f6);
+      f6[3] = dir[u][0]; f6[4] = dir[u][1]; f6[5] = dir[u][2];
+      const bool onpath = lk[u] >= 0 && ((dsub >> (lk[u] & 31)) & 1u);
       const float jcon = dot6(Sj, f6);
-      float jv = onpath ? jcon : (-1 - lk == lane ? sg : 0.f);
+      float jv = onpath ? jcon : (-1 - lk[u] == lane ? sg[u] : 0.f);
       jv = (r < nrow && lane < NV) ? jv : 0.f;
       if (lane < LDJ) s.x.k.Jm[r][lane] = jv;
     }
   }
   __syncthreads();
-  // lanes >= NV carry no dof: they read column 0 scaled by 0 (keeps every LDS address in bounds)
+  // W rows, four per iteration; each row's dot product runs as two interleaved partial sums, so
+  // the block is eight independent FMA chains.  Hr is zero on lanes >= NV, so their W entries are
+  // zero; they read J column 0 (keeps every LDS address in bounds).  A_rr = J_r . W_r is reduced
+  // across the half-wave for the four rows together and kept by lane r; the reciprocals of all
+  // rows are then formed at once, one row per lane.
   const int jc = lane < NV ? lane : 0;
   const float jmask = lane < NV ? 1.f : 0.f;
+  float arr = 0.f;
 #pragma unroll 1
   for (int r0 = 0; r0 < maxrow; r0 += 4) {
-    float w[4] = {0.f, 0.f, 0.f, 0.f};
+    float w[4][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+    float jown[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) jown[u] = s.x.k.Jm[r0 + u][jc];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const float4* jr = reinterpret_cast<const float4*>(s.x.k.Jm[r0 + u]);  // 16-B aligned rows
@@ -999,19 +1017,23 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
         jrow[4 * q] = t.x; jrow[4 * q + 1] = t.y; jrow[4 * q + 2] = t.z; jrow[4 * q + 3] = t.w;
       }
 #pragma unroll
-      for (int k = 0; k < NV; ++k) w[u] += Hr[k] * jrow[k];
+      for (int k = 0; k < NV; ++k) w[u][k & 1] += Hr[k] * jrow[k];
     }
+    float a[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int r = r0 + u;
-      w[u] = lane < NV ? w[u] : 0.f;
-      if (lane < LDJ) s.x.k.Wm[r][lane] = w[u];
-      const float a = half_sum(s.x.k.Jm[r][jc] * jmask * w[u]);
-      if (lane == 0) {
-        s.rmeta[r][0] = r < nrow ? 1.0f / (a + 1e-9f) : 0.f;
-        if (r >= nrow) { s.rmeta[r][1] = 0.f; s.rmeta[r][2] = 0.f; }
-      }
+      const float wu = w[u][0] + w[u][1];
+      if (lane < LDJ) s.x.k.Wm[r0 + u][lane] = wu;
+      a[u] = jown[u] * wu;
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] = half_sum(a[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) arr = lane == r0 + u ? a[u] : arr;
+  }
+  if (lane < MAXR && lane < ((maxrow + 3) & ~3)) {
+    s.rmeta[lane][0] = lane < nrow ? 1.0f / (arr + 1e-9f) : 0.f;
+    if (lane >= nrow) { s.rmeta[lane][1] = 0.f; s.rmeta[lane][2] = 0.f; }
   }
   __syncthreads();
   ts.mark(kStWsolve);
