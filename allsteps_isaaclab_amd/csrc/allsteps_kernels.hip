@@ -48,6 +48,7 @@ static_assert(MAXR <= 3 * MAXC, "a row index / 3 is a valid contact slot");
 // stay <= 20 KB so that 8 workgroups (2 waves/SIMD) fit a CU and 4096 envs run in one round.  The
 // phase-local arrays therefore share one union: FK (Rl) -> dynamics (c, Ib, Ic, Fh, V, A, F) ->
 // sweep (piv) -> constraint rows (Jm, Wm); each phase ends before the next one writes.
+constexpr int kRowGroup = 3;          // constraint rows per J / W / PGS group (a contact triplet)
 constexpr int LDJ = 28;               // J / W row stride (>= NV = 27)
 struct DynScratch {
   float c[LMAX][3];
@@ -167,6 +168,22 @@ __device__ __forceinline__ float half_sum(float v) {
   v += dpp<0x141>(v);
   v += dpp<0x140>(v);
   return row_pair_sum(v);
+}
+
+// half_sum of N independent values, step by step, so the N butterflies interleave (the DPP
+// results of one value fill the other values' hazard slots).  Same arithmetic as half_sum.
+template <int N>
+__device__ __forceinline__ void half_sum_n(float (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0xB1>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x4E>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x141>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x140>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = row_pair_sum(v[i]);
 }
 
 template <int CTRL>
@@ -850,6 +867,20 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// One projected Gauss-Seidel row from its velocity v = J_r . u and metadata {1/A_rr, target, type,
+// coupling}: normal and limit rows clamp at 0, tangent rows at +-mu * (latest normal impulse ln).
+// Updates the row's impulse (and ln on a normal row) and returns the impulse change.
+__device__ __forceinline__ float pgs_row(const float4& mt, float v, float mu, float& lam, float& ln) {
+  const float l0 = lam;
+  const float lim = mu * ln;
+  const float lt = fminf(fmaxf(l0 - v * mt.x, -lim), lim);
+  const float lnrm = fmaxf(l0 + (mt.y - v) * mt.x, 0.f);
+  const float l1 = mt.z == 1.f ? lt : lnrm;
+  ln = mt.z == 0.f ? l1 : ln;
+  lam = l1;
+  return l1 - l0;
+}
+
 template <int NV>
 __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, uint32_t* mask_out,
                         Stamp& ts) {
@@ -958,32 +989,31 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   __syncthreads();
   const int maxrow = sm.maxrow;
   const uint32_t dsub = tp.dsub;
-  // four rows per iteration: the rows are independent, so their LDS reads and FMA chains overlap
-  // (MAXR is a multiple of 4; rows in [maxrow, r0 + 4) are written as zero / ignored)
-  static_assert(MAXR % 4 == 0, "row blocks");
+  // Rows are handled in groups of three (a contact's normal / tangent / tangent triplet, or three
+  // consecutive limit rows; MAXR is a multiple of 3).  Rows of the last group at or past maxrow are
+  // written as zero / ignored.
+  static_assert(MAXR % kRowGroup == 0, "row groups");
 #pragma unroll 1
-  for (int r0 = 0; r0 < maxrow; r0 += 4) {
-    // all four rows' inputs are read before any row is stored, so the reads of the block overlap
-    int lk[4];
-    float P[4][3], dir[4][3], sg[4];
+  for (int r0 = 0; r0 < maxrow; r0 += kRowGroup) {
+    // all inputs of the group are read before any row is stored, so the group's reads overlap
+    const int c = r0 / 3;  // contact of the triplet (r0 < 3 MAXC = MAXR)
+    float P[3], dir[kRowGroup][3], sg[kRowGroup];
+    int lk[kRowGroup];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int r = r0 + u;
-      const int c = r / 3;  // contact of a contact row (r < 3 MAXC = MAXR)
-      lk[u] = s.rlink[r];
-      sg[u] = s.rsign[r];
+    for (int k = 0; k < 3; ++k) P[k] = s.cpt[c][k];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        P[u][k] = s.cpt[c][k];
-        dir[u][k] = s.cdir[c][r - 3 * c][k];
-      }
+    for (int u = 0; u < kRowGroup; ++u) {
+      lk[u] = s.rlink[r0 + u];
+      sg[u] = s.rsign[r0 + u];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dir[u][k] = s.cdir[c][u][k];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kRowGroup; ++u) {
       const int r = r0 + u;
       // branch-free: contact row -> S_j . f6 on the link's path; limit row -> +-1 at its dof
       float f6[6];  // spatial force direction [P x d; d]
-      cross3(P[u], dir[u], f6);
+      cross3(P, dir[u], f6);
       f6[3] = dir[u][0]; f6[4] = dir[u][1]; f6[5] = dir[u][2];
       const bool onpath = lk[u] >= 0 && ((dsub >> (lk[u] & 31)) & 1u);
       const float jcon = dot6(Sj, f6);
@@ -993,22 +1023,25 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     }
   }
   __syncthreads();
-  // W rows, four per iteration; each row's dot product runs as two interleaved partial sums, so
-  // the block is eight independent FMA chains.  Hr is zero on lanes >= NV, so their W entries are
-  // zero; they read J column 0 (keeps every LDS address in bounds).  A_rr = J_r . W_r is reduced
-  // across the half-wave for the four rows together and kept by lane r; the reciprocals of all
-  // rows are then formed at once, one row per lane.
+  // W rows, one group per iteration; each row's dot product runs as two interleaved partial sums.
+  // Hr is zero on lanes >= NV, so their W entries are zero; they read J column 0 (keeps every LDS
+  // address in bounds).  Per group, the half-wave reduces A_rr = J_r . W_r of its rows and the
+  // in-group couplings A_10, A_20, A_21 (A_sr = J_s . W_r) that the PGS sweep uses; lane r keeps
+  // the values of row r, and the reciprocals are formed at once, one row per lane.
   const int jc = lane < NV ? lane : 0;
   const float jmask = lane < NV ? 1.f : 0.f;
-  float arr = 0.f;
+  float arr = 0.f, acp = 0.f;
 #pragma unroll 1
-  for (int r0 = 0; r0 < maxrow; r0 += 4) {
-    float w[4][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-    float jown[4];
+  for (int r0 = 0; r0 < maxrow; r0 += kRowGroup) {
+    float w[kRowGroup][2];
+    float jown[kRowGroup];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) jown[u] = s.x.k.Jm[r0 + u][jc];
+    for (int u = 0; u < kRowGroup; ++u) {
+      jown[u] = s.x.k.Jm[r0 + u][jc];
+      w[u][0] = w[u][1] = 0.f;
+    }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kRowGroup; ++u) {
       const float4* jr = reinterpret_cast<const float4*>(s.x.k.Jm[r0 + u]);  // 16-B aligned rows
       float jrow[LDJ];
 #pragma unroll
@@ -1019,66 +1052,75 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
 #pragma unroll
       for (int k = 0; k < NV; ++k) w[u][k & 1] += Hr[k] * jrow[k];
     }
-    float a[4];
+    float wu[kRowGroup], a[2 * kRowGroup];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float wu = w[u][0] + w[u][1];
-      if (lane < LDJ) s.x.k.Wm[r0 + u][lane] = wu;
-      a[u] = jown[u] * wu;
+    for (int u = 0; u < kRowGroup; ++u) {
+      wu[u] = w[u][0] + w[u][1];
+      if (lane < LDJ) s.x.k.Wm[r0 + u][lane] = wu[u];
+      a[u] = jown[u] * wu[u];
     }
+    a[3] = jown[1] * wu[0];  // A_10, kept by row r0
+    a[4] = jown[2] * wu[0];  // A_20, kept by row r0 + 1
+    a[5] = jown[2] * wu[1];  // A_21, kept by row r0 + 2
+    half_sum_n(a);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] = half_sum(a[u]);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) arr = lane == r0 + u ? a[u] : arr;
+    for (int u = 0; u < kRowGroup; ++u) {
+      arr = lane == r0 + u ? a[u] : arr;
+      acp = lane == r0 + u ? a[kRowGroup + u] : acp;
+    }
   }
-  if (lane < MAXR && lane < ((maxrow + 3) & ~3)) {
+  if (lane < MAXR && lane < (maxrow + kRowGroup - 1) / kRowGroup * kRowGroup) {
     s.rmeta[lane][0] = lane < nrow ? 1.0f / (arr + 1e-9f) : 0.f;
+    s.rmeta[lane][3] = acp;
     if (lane >= nrow) { s.rmeta[lane][1] = 0.f; s.rmeta[lane][2] = 0.f; }
   }
   __syncthreads();
   ts.mark(kStWsolve);
-  // ---- projected Gauss-Seidel (lane j holds u_j; lane r holds the impulse lambda_r of its env).
+  // ---- projected Gauss-Seidel (lane j holds u_j; every lane of an env holds all its impulses).
   // Rows in order: contacts as (normal, tangent, tangent) triplets, then joint limits; a tangent
   // row's bound uses the impulse of the most recent normal row (ln).  Lane j's J / W columns of
-  // every row sit in registers (loaded once, up front); the row's old impulse comes from lane r by
-  // readlane and the projection is branch-free, so the only LDS access in the loop is the row
-  // metadata.
+  // every row sit in registers (loaded once, up front).  A group of three rows takes the three
+  // velocities J_r . u from the u at its start (three independent reductions) and adds the
+  // in-group coupling A_sr dlambda_r of the rows before it, which is the Gauss-Seidel sweep row by
+  // row (J_s . (u + W_r dl_r) = J_s . u + A_sr dl_r) with one reduction latency per group instead
+  // of one per row.  The row loop is unrolled with an exit per group; rows in [maxrow, group end)
+  // have zero J / W / metadata and leave everything unchanged.
   float mu = K.sim.friction;
   asm volatile("" : "+v"(mu));
-  const bool hi = threadIdx.x & 32;
-  float lam = 0.f;
   const int iters = K.sim.pgs_iters;
-  float Jc[MAXR], Wc[MAXR];
+  float Jc[MAXR], Wc[MAXR], lamr[MAXR];
 #pragma unroll
   for (int r = 0; r < MAXR; ++r) {
     Jc[r] = s.x.k.Jm[r][jc] * jmask;
     Wc[r] = s.x.k.Wm[r][jc] * jmask;
+    lamr[r] = 0.f;
   }
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
     float ln = 0.f;
-    // The row loop is unrolled (registers indexed by constants) with an exit per 4-row block; rows
-    // in [maxrow, block end) have zero J / W / metadata and leave everything unchanged.  Per-row
-    // lane masks would be hoisted out of the sweep loop (and spilled), so lane r is found with a
-    // counter that reaches 0 at row r instead.
-    int dr = lane;
 #pragma unroll
-    for (int r = 0; r < MAXR; ++r) {
-      if ((r & 3) == 0 && r >= maxrow) break;
-      const float4 mt = *reinterpret_cast<const float4*>(s.rmeta[r]);
-      const float v = half_sum(Jc[r] * uj);
-      const float l00 = readlane_f(lam, r), l01 = readlane_f(lam, r + 32);
-      const float l0 = hi ? l01 : l00;
-      const float lim = mu * ln;
-      const float lt = fminf(fmaxf(l0 - v * mt.x, -lim), lim);
-      const float lnrm = fmaxf(l0 + (mt.y - v) * mt.x, 0.f);
-      const float l1 = mt.z == 1.f ? lt : lnrm;
-      ln = mt.z == 0.f ? l1 : ln;
-      uj += Wc[r] * (l1 - l0);
-      lam = dr == 0 ? l1 : lam;
-      --dr;
+    for (int r = 0; r < MAXR; r += kRowGroup) {
+      if (r >= maxrow) break;
+      const float4 m0 = *reinterpret_cast<const float4*>(s.rmeta[r]);
+      const float4 m1 = *reinterpret_cast<const float4*>(s.rmeta[r + 1]);
+      const float4 m2 = *reinterpret_cast<const float4*>(s.rmeta[r + 2]);
+      float vg[3] = {Jc[r] * uj, Jc[r + 1] * uj, Jc[r + 2] * uj};
+      half_sum_n(vg);
+      float v0 = vg[0], v1 = vg[1], v2 = vg[2];
+      const float d0 = pgs_row(m0, v0, mu, lamr[r], ln);
+      v1 += m0.w * d0;
+      v2 += m1.w * d0;
+      uj += Wc[r] * d0;
+      const float d1 = pgs_row(m1, v1, mu, lamr[r + 1], ln);
+      v2 += m2.w * d1;
+      uj += Wc[r + 1] * d1;
+      const float d2 = pgs_row(m2, v2, mu, lamr[r + 2], ln);
+      uj += Wc[r + 2] * d2;
     }
   }
+  float lam = 0.f;
+#pragma unroll
+  for (int r = 0; r < MAXR; ++r) lam = lane == r ? lamr[r] : lam;
   if (lane < MAXR) s.rlam[lane] = lane < maxrow ? lam : 0.f;
   __syncthreads();
   if (lane < NV) s.u[lane] = uj;
