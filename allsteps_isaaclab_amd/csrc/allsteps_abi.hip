@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -34,7 +35,7 @@ struct as_env {
   int64_t env_offset;
   as_state_t st;
   as::Consts* consts_dev;
-  int32_t* counters_dev;  // two banks of 4: step t uses bank t % 2, k_obs clears the other
+  int32_t* counters_dev;  // two banks of kCntBank: step t uses bank t % 2, k_obs clears the other
   int32_t bank = 0, last_bank = 0;
   uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_fix
   int32_t num_steps;
@@ -43,6 +44,7 @@ struct as_env {
   std::vector<hipEvent_t> ev;
   unsigned long long* stamps = nullptr;  // diagnostic (as_debug_stamps)
   int32_t prof_cap = 0, prof_n = 0;
+  int32_t tune = 0;  // AS_TUNE (diagnostic scheduling experiments; 0 = default)
 };
 
 extern "C" {
@@ -119,6 +121,7 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
 
   as_env* env = new as_env();
   env->n = num_envs;
+  if (const char* t = getenv("AS_TUNE")) env->tune = atoi(t);
   env->device = device;
   env->seed = seed;
   env->env_offset = env_id_offset;
@@ -126,7 +129,7 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   env->num_steps = task->num_steps;
   env->nv = h.nv;
   if (hipMalloc(&env->consts_dev, sizeof(as::Consts)) != hipSuccess ||
-      hipMalloc(&env->counters_dev, 8 * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&env->counters_dev, 2 * as::kCntBank * sizeof(int32_t)) != hipSuccess ||
       hipMalloc(&env->side_dev, (size_t)as::kSideWords * num_envs * sizeof(uint32_t)) != hipSuccess) {
     (void)hipFree(env->consts_dev);
     (void)hipFree(env->counters_dev);
@@ -134,7 +137,7 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
     return fail(AS_ERR_HIP, "as_create: hipMalloc failed");
   }
   HIP_TRY(hipMemcpy(env->consts_dev, &h, sizeof(as::Consts), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(env->counters_dev, 0, 8 * sizeof(int32_t)));
+  HIP_TRY(hipMemset(env->counters_dev, 0, 2 * as::kCntBank * sizeof(int32_t)));
   *out = env;
   return AS_OK;
 }
@@ -155,7 +158,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // no memset per step: this launch's counter bank was cleared by the previous launch's k_obs
   // (physics-only launches do not touch the counters and keep the bank)
-  int32_t* cnt = env->counters_dev + 4 * env->bank;
+  int32_t* cnt = env->counters_dev + as::kCntBank * env->bank;
   as::StepArgs a{};
   a.consts = env->consts_dev;
   a.st = env->st;
@@ -170,6 +173,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   a.seed = env->seed;
   a.env_offset = env->env_offset;
   a.stamps = env->stamps;
+  a.tune = env->tune;
   a.obs = mode == as::kModePhysics ? nullptr : obs;
   a.side = env->side_dev;
   const bool prof = env->prof_n < env->prof_cap;
@@ -188,7 +192,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   o.st = env->st;
   o.n = env->n;
   o.counters = cnt;
-  o.next_counters = env->counters_dev + 4 * (env->bank ^ 1);
+  o.next_counters = env->counters_dev + as::kCntBank * (env->bank ^ 1);
   env->last_bank = env->bank;
   env->bank ^= 1;
   o.obs = obs;
@@ -283,7 +287,7 @@ int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* s
 
 int as_step_counters(as_env_t* env, const int32_t** counters_dev) {
   if (!env || !counters_dev) return fail(AS_ERR_INVALID, "as_step_counters: null argument");
-  *counters_dev = env->counters_dev + 4 * env->last_bank;
+  *counters_dev = env->counters_dev + as::kCntBank * env->last_bank;
   return AS_OK;
 }
 

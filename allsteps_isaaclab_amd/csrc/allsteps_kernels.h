@@ -44,17 +44,27 @@ struct StepArgs {
   uint8_t* terminated;
   uint8_t* truncated;
   const float* reset_draws;
-  int32_t* counters;  // [0] any reset, [1] sum of curr_target_index (zero at launch: see k_obs)
+  int32_t* counters;  // one bank (kCntBank ints, zero at launch: see k_obs), layout below
   uint64_t seed;
   int64_t env_offset;
   unsigned long long* stamps;  // diagnostic phase timing (s_memtime deltas summed over waves) or null
+  int32_t tune;                // scheduling experiments (env AS_TUNE, diagnostic): 0 default, 1 no s_setprio
 };
 
 // phase ids of the diagnostic stamps (as_debug_stamps)
 enum {
   kStLoad = 0, kStFK, kStLinkQ, kStDyn, kStChol, kStSolve, kStCollide, kStRows, kStWsolve, kStPGS,
-  kStIntegrate, kStTask, kStReset, kStStore, kNumStamps
+  kStIntegrate, kStFKFinal, kStTask, kStReset, kStStore, kNumStamps
 };
+
+// Step counters, one bank per launch (two banks alternate; k_obs clears the next one):
+//   [0]  any env reset (plain store of 1)
+//   [1]  sum of curr_target_index over all envs, published by k_obs from the partial sums
+//   [kCntStride * (1 + i)], i < kCntSlots: partial sums, one atomic per wave into slot block % kCntSlots
+//        (one 64-B line each: 4096 same-address atomics serialise at the memory side)
+constexpr int kCntSlots = 16;
+constexpr int kCntStride = 16;
+constexpr int kCntBank = kCntStride * (1 + kCntSlots);
 
 // side buffer of k_step -> k_fix: idx, prev, next, count, swing, pot, old_pot, foot_contact[2]
 // (tick-#1 state) and foot_contact[2], targets[9] (tick-#1 observation entries 48..58)
@@ -66,7 +76,7 @@ struct ObsArgs {
   const Consts* consts;
   as_state_t st;
   int32_t n;
-  const int32_t* counters;
+  int32_t* counters;       // this launch's bank (k_obs publishes the sum into [1])
   int32_t* next_counters;  // the other bank, cleared here for the next launch
   float* obs;
   const uint32_t* side;

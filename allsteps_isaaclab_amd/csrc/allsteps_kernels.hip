@@ -48,6 +48,7 @@ static_assert(MAXR <= 3 * MAXC, "a row index / 3 is a valid contact slot");
 // stay <= 20 KB so that 8 workgroups (2 waves/SIMD) fit a CU and 4096 envs run in one round.  The
 // phase-local arrays therefore share one union: FK (Rl) -> dynamics (c, Ib, Ic, Fh, V, A, F) ->
 // sweep (piv) -> constraint rows (Jm, Wm); each phase ends before the next one writes.
+constexpr int kPrioRows = 6;          // constraint rows per issue-priority level (see substep)
 constexpr int kRowGroup = 3;          // constraint rows per J / W / PGS group (a contact triplet)
 constexpr int LDJ = 28;               // J / W row stride (>= NV = 27)
 struct DynScratch {
@@ -93,6 +94,7 @@ struct Topo {
   uint32_t lsub;   // subtree of link(lane)
   uint32_t dsub;   // links moved by dof lane
   float lo, hi;    // limits of hinge lane (link lane + 1)
+  float arm;       // armature of dof lane (0 on the root dofs)
 };
 
 __device__ Topo load_topo(const Consts& K, int lane) {
@@ -107,6 +109,7 @@ __device__ Topo load_topo(const Consts& K, int lane) {
   t.dsub = lane < nv ? K.dsub[j] : 0u;
   t.lo = m.lower[hl];
   t.hi = m.upper[hl];
+  t.arm = lane >= 6 && lane < nv ? m.armature[lane - 5] : 0.f;
   return t;
 }
 
@@ -221,14 +224,27 @@ __device__ __forceinline__ float half_max(float v) {
 // diagnostic phase stamps (off when p == nullptr): each wave accumulates its s_memtime deltas per
 // phase in LDS and adds them to the device counters once, at the end of the launch -- a global
 // atomic per phase boundary would put a contended memory round trip into the next phase.
+// With p[kWaveRecFlag] != 0 each wave also writes a record of its own (the last launch's waves:
+// phase cycles, total, start / end time, HW_ID / XCC_ID, rows and contacts summed over substeps per
+// env) at p + kWaveRecBase + block * kWaveRecWords, for tail analysis (scripts/stamps.py).
+constexpr int kWaveRecFlag = 31, kWaveRecBase = 64, kWaveRecWords = 24;
+static_assert(16 + kNumStamps <= kWaveRecFlag && kNumStamps + 9 <= kWaveRecWords, "stamp slots");
 struct Stamp {
   unsigned long long* p;
   unsigned long long* acc;  // LDS, kNumStamps
   unsigned long long t;
+  unsigned long long t0 = 0ull;
+  unsigned rows = 0u, cons = 0u;
   __device__ void start() {
     if (p) {
       if (threadIdx.x < kNumStamps) acc[threadIdx.x] = 0ull;
-      t = __builtin_amdgcn_s_memtime();
+      t = t0 = __builtin_amdgcn_s_memtime();
+    }
+  }
+  __device__ void count(int nrow, int nc) {
+    if (p) {
+      rows += (unsigned)nrow;
+      cons += (unsigned)nc;
     }
   }
   __device__ void mark(int k) {
@@ -241,14 +257,29 @@ struct Stamp {
   __device__ void flush() {
     if (p) {
       __syncthreads();
-      if (threadIdx.x < kNumStamps) {
-        atomicAdd(p + threadIdx.x, acc[threadIdx.x]);
-        atomicMax(p + 16 + threadIdx.x, acc[threadIdx.x]);  // slots 16..: per-phase maximum
-      }
-      if (threadIdx.x == 0) {  // slot kNumStamps: the slowest wave's total (the launch's tail)
-        unsigned long long tot = 0;
-        for (int k = 0; k < kNumStamps; ++k) tot += acc[k];
-        atomicMax(p + kNumStamps, tot);
+      unsigned long long tot = 0;
+      for (int k = 0; k < kNumStamps; ++k) tot += acc[k];
+      if (p[kWaveRecFlag]) {
+        // per-wave records, plain stores only: the atomics of the aggregate mode would queue in
+        // front of the late waves' own memory traffic and distort exactly the tail being measured
+        unsigned long long* rec = p + kWaveRecBase + (size_t)blockIdx.x * kWaveRecWords;
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        const int k = threadIdx.x;
+        if (k < kNumStamps) rec[k] = acc[k];
+        if (k == 0) {
+          rec[kNumStamps] = tot; rec[kNumStamps + 1] = t0; rec[kNumStamps + 2] = now;
+          rec[kNumStamps + 3] = hw; rec[kNumStamps + 4] = xcc;
+          rec[kNumStamps + 5] = rows; rec[kNumStamps + 7] = cons;
+        }
+        if (k == 32) { rec[kNumStamps + 6] = rows; rec[kNumStamps + 8] = cons; }
+      } else {
+        if (threadIdx.x < kNumStamps) {
+          atomicAdd(p + threadIdx.x, acc[threadIdx.x]);
+          atomicMax(p + 16 + threadIdx.x, acc[threadIdx.x]);  // slots 16..: per-phase maximum
+        }
+        if (threadIdx.x == 0) atomicMax(p + kNumStamps, tot);  // slot kNumStamps: the slowest wave's total
       }
     }
   }
@@ -530,7 +561,7 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
 // Row j of the joint-space inertia H (lane j):
 //   H_jk = S_k . (Ic_link(j) S_j)  if dof k is on the path of link(j) (k ancestor-or-self),
 //        = S_j . (Ic_link(k) S_k)  if dof j is on the path of link(k),   else 0;  + armature.
-// The masks and the armature come from the constants (global / scalar loads): with the LDS copy in
+// The masks come from the constants (one global load each per lane): with an LDS copy in
 // Smem::topo the scheduler clusters all 12 NV LDS reads of S and Fh up front and spills.
 template <int NV>
 __device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, float (&Hr)[NV]) {
@@ -541,16 +572,21 @@ __device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, 
   float Sj[6], Fj[6];
 #pragma unroll
   for (int a = 0; a < 6; ++a) { Sj[a] = s.S[j][a]; Fj[a] = s.x.d.Fh[j][a]; }
+  const float arm = tp.arm;
+  // Column k's row index passes through an empty asm that also takes column k - kAhead's result, so
+  // its LDS reads cannot be issued before that column is done: at most kAhead columns of reads are
+  // in flight (left alone, the scheduler issues all 12 NV reads of the loop up front and spills).
+  constexpr int kAhead = 3;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
+    int kk = k;
+    if (k >= kAhead) asm volatile("" : "+v"(kk) : "v"(Hr[k - kAhead]));
     const bool k_on_j = (anc_j >> k) & 1u;
     const bool j_on_k = (jon >> k) & 1u;
-    float v1 = dot6(s.S[k], Fj);
-    float v2 = dot6(Sj, s.x.d.Fh[k]);
+    float v1 = dot6(s.S[kk], Fj);
+    float v2 = dot6(Sj, s.x.d.Fh[kk]);
     float h = k_on_j ? v1 : (j_on_k ? v2 : 0.f);
-    // (the armature load stays under the k == j branch: hoisting it lets the scheduler issue all
-    // 12 NV loads of this loop up front, which spills)
-    if (k == j && j >= 6) h += K.model.armature[j - 5];
+    h += k == j ? arm : 0.f;
     Hr[k] = lane < NV ? h : 0.f;
   }
 }
@@ -883,7 +919,7 @@ __device__ __forceinline__ float pgs_row(const float4& mt, float v, float mu, fl
 
 template <int NV>
 __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, uint32_t* mask_out,
-                        Stamp& ts) {
+                        Stamp& ts, int tune) {
   // Opaque copies of the constants pointer and the lane id: everything derived from them below
   // (model-table loads, LDS addresses, lane masks) is loop-invariant, and without this the
   // compiler hoists all of it out of the substep loop and spills it.
@@ -977,6 +1013,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   }
   const int nrow = crow + total < MAXR ? crow + total : MAXR;
   if (lane == 0) s.nrow = nrow;
+  ts.count(nrow, nc);
   __syncthreads();
   if (threadIdx.x == 0) sm.maxrow = max(sm.env[0].nrow, sm.env[1].nrow);
   ts.mark(kStRows);
@@ -988,6 +1025,18 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   for (int a = 0; a < 6; ++a) Sj[a] = s.S[jl][a];
   __syncthreads();
   const int maxrow = sm.maxrow;
+  // Issue priority by constraint load: the two waves of a SIMD are arbitrated by priority, then
+  // age, so a contact-heavy wave that happens to be the younger one would get only the leftover
+  // issue slots and set the launch's tail.  The heavier wave of the pair takes precedence for the
+  // rest of this substep and the fixed-cost phases of the next (scalar branch: s_setprio is not
+  // masked by EXEC, so exactly one of them may execute).
+  if (tune != 1) {
+    const int lvl = __builtin_amdgcn_readfirstlane(maxrow) / kPrioRows;
+    if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+    else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  }
   const uint32_t dsub = tp.dsub;
   // Rows are handled in groups of three (a contact's normal / tangent / tangent triplet, or three
   // consecutive limit rows; MAXR is a multiple of 3).  Rows of the last group at or past maxrow are
@@ -1296,10 +1345,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const bool do_physics = P.mode == kModeStep || P.mode == kModePhysics;
   // ---- physics
   if (do_physics) {
-    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, mask, ts);
+    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, mask, ts, P.tune);
     fk<false>(K, s, lane, tp);  // FK of the final pose for body_pos_w (articulation_data.py:439)
     if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
   }
+  ts.mark(kStFKFinal);
   if (lane == 0 && !do_physics) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
   __syncthreads();
   float bp[9];
@@ -1371,14 +1421,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       P.reward[e] = rew;
       P.terminated[e] = terminated ? 1 : 0;
       P.truncated[e] = time_out ? 1 : 0;
-      atomicAdd(&P.counters[1], idx);                   // curriculum mean over tick-#1 indices
-      if (done) atomicOr(&P.counters[0], 1);
     }
   } else if (P.mode == kModeReset) {
     done = true;
-    if (valid && lane == 0) {
-      atomicAdd(&P.counters[1], idx);
-      atomicOr(&P.counters[0], 1);
+  }
+  if (P.mode != kModePhysics) {
+    // curriculum mean over the tick-#1 indices and the any-reset flag: one atomic per wave into a
+    // striped partial sum, the flag by plain store
+    const int cidx = valid ? idx : 0;
+    const bool vdone = valid && done;
+    const int wsum = __builtin_amdgcn_readlane(cidx, 0) + __builtin_amdgcn_readlane(cidx, 32);
+    const bool wdone = __any(vdone);
+    if (threadIdx.x == 0) {
+      atomicAdd(&P.counters[kCntStride * (1 + (int)(blockIdx.x % kCntSlots))], wsum);
+      if (wdone) P.counters[0] = 1;
     }
   }
   ts.mark(kStTask);
@@ -1549,14 +1605,18 @@ __global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
   const int n = P.n;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int any_reset = P.counters[0];
-  if (e < 4) P.next_counters[e] = 0;  // the next launch's bank (this launch reads the other one)
-  if (any_reset) {
-    if (e == 0) {
-      int c = P.st.curriculum[0];
-      if ((float)P.counters[1] / (float)n > (float)T.curriculum_threshold) P.st.curriculum[0] = min(c + 1, T.max_curriculum);
+  // the next launch's bank (this launch reads the other one)
+  for (int k = e; k < kCntBank; k += gridDim.x * blockDim.x) P.next_counters[k] = 0;
+  if (e == 0) {
+    int sum = 0;
+    for (int i = 0; i < kCntSlots; ++i) sum += P.counters[kCntStride * (1 + i)];
+    P.counters[1] = sum;
+    if (any_reset) {
+      const int c = P.st.curriculum[0];
+      if ((float)sum / (float)n > (float)T.curriculum_threshold) P.st.curriculum[0] = min(c + 1, T.max_curriculum);
     }
-    return;
   }
+  if (any_reset) return;
   if (e >= n) return;
   const as_state_t& st = P.st;
   const uint32_t* sd = P.side;

@@ -179,10 +179,13 @@ int as_profile(as_env_t* env, int32_t max_launches);
 int as_profile_read(as_env_t* env, double* step_kernel_ms, double* obs_kernel_ms, int32_t* launches);
 
 /* Diagnostic: when stamps_dev (device, >= 32 uint64) is non-null, every k_step wave adds the
- * s_memtime cycles of each phase (load, fk, link, dynamics, cholesky, solve, collide, rows,
- * W-solve, pgs, integrate, task, reset, store) to it, and slot 14 keeps the largest single-wave
- * total of any launch and slots 16.. the largest single-wave cycles of each phase (atomicMax).
- * Pass NULL to switch off. */
+ * s_memtime cycles of each of its 15 phases (load, fk, rnea, H rows, H^-1 sweep, solve, collide,
+ * rows, W, pgs, integrate, final fk, task, reset, store) to slots 0..14; slot 15 keeps the largest
+ * single-wave total of any launch and slots 16..30 the largest single-wave cycles of each phase
+ * (atomicMax).  If slot 31 is non-zero on entry, the buffer must hold 64 + 24 * ceil(num_envs / 2)
+ * words and each wave instead stores (no atomics) a 24-word record of its own at 64 + 24 * block
+ * (phases, total, start / end s_memtime, HW_ID, XCC_ID, rows and contacts per env), overwritten
+ * by every launch (scripts/stamps.py).  Pass NULL to switch off. */
 int as_debug_stamps(as_env_t* env, uint64_t* stamps_dev);
 
 /* Device counters of the last step: [0] = any env reset, [1] = sum of curr_target_index. */

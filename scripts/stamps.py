@@ -1,4 +1,11 @@
-"""Diagnostic: per-phase cycles of k_step from in-kernel s_memtime stamps (as_debug_stamps)."""
+"""Diagnostic: per-phase cycles of k_step from in-kernel s_memtime stamps (as_debug_stamps).
+
+Runs in the per-wave record mode (slot 31 set): every wave of a launch stores its own record with
+plain stores (no atomics, which would queue in front of the late waves' memory traffic and distort
+the tail).  The records of each of the last `steps` launches are read back after the launch and
+aggregated here: mean / max cycles per phase over all waves, the distribution of per-wave totals,
+and the slowest waves of the slowest launch with their SIMD partner (same HW_ID / XCC_ID key).
+"""
 
 import json
 import os
@@ -7,39 +14,75 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv  # noqa: E402
 from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg  # noqa: E402
 
-PHASES = ["load", "fk", "rnea", "hrow", "sweep", "solve", "collide", "rows", "wsolve", "pgs", "integrate", "task",
-          "reset", "store"]
+PHASES = ["load", "fk", "rnea", "hrow", "sweep", "solve", "collide", "rows", "wsolve", "pgs", "integrate", "fkfinal",
+          "task", "reset", "store"]
+NP = len(PHASES)
+BASE, WORDS = 64, 24
 
 
-def main(n=4096, steps=50):
+def simd_key(r):
+    hw = r[:, NP + 3]
+    simd, cu, sh, se = (hw >> 4) & 3, (hw >> 8) & 15, (hw >> 12) & 1, (hw >> 13) & 7
+    xcc = r[:, NP + 4] & 15
+    return ((xcc * 8 + se) * 2 + sh) * 16 * 4 + cu * 4 + simd
+
+
+def launch_summary(r, top=6):
+    tot = r[:, NP]
+    key = simd_key(r)
+    rows = np.maximum(r[:, NP + 5], r[:, NP + 6])
+    out = []
+    for i in np.argsort(-tot)[:top]:
+        mates = np.where((key == key[i]) & (np.arange(len(r)) != i))[0]
+        out.append({"blk": int(i), "tot": int(tot[i]), "rows": [int(r[i, NP + 5]), int(r[i, NP + 6])],
+                    "cons": [int(r[i, NP + 7]), int(r[i, NP + 8])],
+                    "mates": [[int(tot[j]), int(rows[j]), int(r[j, NP + 1]) - int(r[i, NP + 1])] for j in mates],
+                    "phases": {PHASES[k]: int(r[i, k]) for k in range(NP)}})
+    return out
+
+
+def main(n=4096, steps=30, warm=10):
     cfg = AllstepsEnvCfg()
     cfg.scene.num_envs = n
     cfg.sim.device = "cuda:0"
     env = AllstepsEnv(cfg)
     env.reset()
     gen = torch.Generator(device="cuda").manual_seed(0)
-    acts = torch.rand(steps + 10, n, 21, device="cuda", generator=gen) * 2 - 1
-    for t in range(10):
+    acts = torch.rand(steps + warm, n, 21, device="cuda", generator=gen) * 2 - 1
+    for t in range(warm):
         env.step(acts[t])
-    buf = torch.zeros(32, dtype=torch.int64, device="cuda")
+    nblk = (n + 1) // 2
+    buf = torch.zeros(BASE + nblk * WORDS, dtype=torch.int64, device="cuda")
+    buf[31] = 1
     env._native.debug_stamps(buf)
+    recs = []
     for t in range(steps):
-        env.step(acts[10 + t])
-    torch.cuda.synchronize()
+        env.step(acts[warm + t])
+        torch.cuda.synchronize()
+        recs.append(buf[BASE:].view(nblk, WORDS).cpu().numpy().astype(np.int64).copy())
     env._native.debug_stamps(None)
-    waves = (n + 1) // 2 * steps
-    tot = buf.cpu().tolist()
-    per = {PHASES[i]: round(tot[i] / waves) for i in range(len(PHASES))}
-    s = sum(per.values())
-    mx = {PHASES[i]: tot[16 + i] for i in range(len(PHASES))}
-    print(json.dumps({"n": n, "cycles_per_wave_step": s, "max_wave_step_total": tot[len(PHASES)], "per_phase_max": mx,
-                      "per_phase": per,
-                      "share": {k: round(v / s, 3) for k, v in per.items()}}))
+    R = np.stack(recs)  # [steps, waves, words]
+    ph = R[:, :, :NP]
+    tot = R[:, :, NP]
+    rows = np.maximum(R[:, :, NP + 5], R[:, :, NP + 6]).ravel()
+    worst = int(np.argmax(tot.max(axis=1)))
+    per = {PHASES[k]: int(ph[:, :, k].mean()) for k in range(NP)}
+    s = max(sum(per.values()), 1)
+    print(json.dumps({
+        "n": n, "launches": steps, "cycles_per_wave_step": s,
+        "max_wave_step_total_mean": int(tot.max(axis=1).mean()), "max_wave_step_total": int(tot.max()),
+        "total_pct": {q: int(np.percentile(tot, q)) for q in (10, 50, 90, 99)},
+        "corr_total_rows": round(float(np.corrcoef(tot.ravel(), rows)[0, 1]), 3),
+        "per_phase": per, "share": {k: round(v / s, 3) for k, v in per.items()},
+        "per_phase_max": {PHASES[k]: int(ph[:, :, k].max()) for k in range(NP)},
+        "per_phase_p99": {PHASES[k]: int(np.percentile(ph[:, :, k], 99)) for k in range(NP)},
+        "worst_launch_top": launch_summary(R[worst])}))
     env.close()
 
 
