@@ -189,6 +189,17 @@ __device__ __forceinline__ void half_sum_n(float (&v)[N]) {
   for (int i = 0; i < N; ++i) v[i] = row_pair_sum(v[i]);
 }
 
+// Exclusive prefix sum over this env's half-wave of a count c in [0, 3], and the half's total:
+// two ballots (bit 0 and bit 1 of c) and popcounts, no cross-lane data movement.
+__device__ __forceinline__ int half_scan3(int c, int& total) {
+  const int sh = threadIdx.x & 32;
+  const uint32_t m0 = (uint32_t)(__ballot((c & 1) != 0) >> sh);
+  const uint32_t m1 = (uint32_t)(__ballot((c & 2) != 0) >> sh);
+  const uint32_t lt = (1u << (threadIdx.x & 31)) - 1u;
+  total = __popc(m0) + 2 * __popc(m1);
+  return __popc(m0 & lt) + 2 * __popc(m1 & lt);
+}
+
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
@@ -851,14 +862,8 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
         cnt = (int)e0 + (int)e1 + (int)es;
       }
     }
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      int v = __shfl_up(incl, o, 32);
-      if (lane >= o) incl += v;
-    }
-    const int total = __shfl(incl, 31, 32);
-    const int slot = base + incl - cnt;
+    int total;
+    const int slot = base + half_scan3(cnt, total);
     if (cnt > 0) emit_contact(s, slot, plink, pst, pfoot, P0, N0, SEP0, pr);
     if (cnt > 1) emit_contact(s, slot + 1, plink, pst, pfoot, P1, N1, SEP1, pr);
     if (cnt > 2) emit_contact(s, slot + 2, plink, pst, pfoot, P2, N2, SEP2, pr);
@@ -990,15 +995,8 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     lo_v = pred < tp.lo;
     hi_v = pred > tp.hi;
   }
-  int cnt = lo_v + hi_v;
-  int incl = cnt;
-#pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
-    int v = __shfl_up(incl, o, 32);
-    if (lane >= o) incl += v;
-  }
-  int total = __shfl(incl, 31, 32);
-  int slot = crow + incl - cnt;
+  int total;
+  int slot = crow + half_scan3(lo_v + hi_v, total);
   for (int sd = 0; sd < 2; ++sd) {
     int viol = sd == 0 ? lo_v : hi_v;
     if (!viol) continue;
