@@ -151,7 +151,9 @@ struct Smem {
 
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  // bound_ctrl: the quad permutes and row mirrors used here never read outside the row, so the
+  // "old" operand is dead and the move folds into the consuming v_add_f32_dpp
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
 __device__ __forceinline__ float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
@@ -202,7 +204,7 @@ __device__ __forceinline__ int half_scan3(int c, int& total) {
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
 }
 
 __device__ __forceinline__ uint32_t half_or(uint32_t v) {
@@ -817,11 +819,11 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
       // argmin over the 4 lanes of the group: quad_perm [1,0,3,2] then [2,3,0,1]
       {
         const float f1 = dpp<0xB1>(f);
-        const int q1 = __builtin_amdgcn_update_dpp(0, qi, 0xB1, 0xF, 0xF, false);
+        const int q1 = __builtin_amdgcn_update_dpp(0, qi, 0xB1, 0xF, 0xF, true);
         const bool tk = f1 < f || (f1 == f && q1 < qi);
         f = tk ? f1 : f; qi = tk ? q1 : qi;
         const float f2 = dpp<0x4E>(f);
-        const int q2 = __builtin_amdgcn_update_dpp(0, qi, 0x4E, 0xF, 0xF, false);
+        const int q2 = __builtin_amdgcn_update_dpp(0, qi, 0x4E, 0xF, 0xF, true);
         const bool tk2 = f2 < f || (f2 == f && q2 < qi);
         f = tk2 ? f2 : f; qi = tk2 ? q2 : qi;
       }
@@ -914,7 +916,7 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
 __device__ __forceinline__ float pgs_row(const float4& mt, float v, float mu, float& lam, float& ln) {
   const float l0 = lam;
   const float lim = mu * ln;
-  const float lt = fminf(fmaxf(l0 - v * mt.x, -lim), lim);
+  const float lt = __builtin_amdgcn_fmed3f(l0 - v * mt.x, -lim, lim);  // = min(max(., -lim), lim), lim >= 0
   const float lnrm = fmaxf(l0 + (mt.y - v) * mt.x, 0.f);
   const float l1 = mt.z == 1.f ? lt : lnrm;
   ln = mt.z == 0.f ? l1 : ln;
