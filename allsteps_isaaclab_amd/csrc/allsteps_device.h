@@ -92,6 +92,18 @@ AS_DEV void crf(const float* V, const float* Fv, float* o) {
 }
 
 // signed distance from p to an axis-aligned box (center c, half extents h); outward normal
+// Monotone key of sd_box(p) for comparisons only (the capsule section search): the squared
+// outside distance, or minus the squared depth inside -- no square root (oracle sd_box_key).
+AS_DEV float sd_box_key(const float* p, const float* c, const float* h) {
+  float d[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) d[k] = fabsf(p[k] - c[k]) - h[k];
+  const float o0 = fmaxf(d[0], 0.f), o1 = fmaxf(d[1], 0.f), o2 = fmaxf(d[2], 0.f);
+  const float out2 = o0 * o0 + o1 * o1 + o2 * o2;
+  const float m = fmaxf(d[0], fmaxf(d[1], d[2]));
+  return out2 > 0.f ? out2 : -(m * m);
+}
+
 AS_DEV float sd_box(const float* p, const float* c, const float* h, float* nrm) {
   float d[3], s[3];
 #pragma unroll

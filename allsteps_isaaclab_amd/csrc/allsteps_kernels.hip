@@ -802,7 +802,8 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
     plink = meta >> 8;
     float c[3];
     for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * pst + k] - s.root_pos[k];
-    // capsule: section search for the minimum of the (convex) signed distance along the segment.
+    // capsule: section search for the minimum of the (convex) signed distance along the segment
+    // (compared through sd_box_key, a monotone function of it without the square root).
     // Each round the kSectionLanes lanes of the pair evaluate the interior points
     // lo + (q+1)(hi-lo)/(kSectionLanes+1); the interval shrinks to the two sub-intervals around
     // the smallest value (ties to the lowest q).  Runs for every group (the result is only used
@@ -812,9 +813,9 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
     for (int it = 0; it < kSectionIters; ++it) {
       const float w = (hi - lo) * (1.0f / (kSectionLanes + 1));
       const float t = lo + (float)(q + 1) * w;
-      float Q[3], tn[3];
+      float Q[3];
       for (int k = 0; k < 3; ++k) Q[k] = A[k] + t * (Bb[k] - A[k]);
-      float f = sd_box(Q, c, h, tn);
+      float f = sd_box_key(Q, c, h);
       int qi = q;
       // argmin over the 4 lanes of the group: quad_perm [1,0,3,2] then [2,3,0,1]
       {

@@ -380,6 +380,18 @@ static void matvec_n(const float* A, int n, const float* b, float* x) {
 /* ---------------------------------------------------------------- collision (boxes, spheres, capsules) */
 
 /* signed distance from p to an axis-aligned box (center c, half extents h); normal out of box */
+/* Monotone key of sd_box for comparisons (capsule section search): squared outside distance, or
+ * minus the squared depth inside; the same ordering as sd_box without its square root. */
+static float sd_box_key(const float p[3], const float c[3], const float h[3]) {
+  float d[3];
+  for (int k = 0; k < 3; ++k) d[k] = fabsf(p[k] - c[k]) - h[k];
+  float o0 = d[0] > 0.f ? d[0] : 0.f, o1 = d[1] > 0.f ? d[1] : 0.f, o2 = d[2] > 0.f ? d[2] : 0.f;
+  float out2 = o0 * o0 + o1 * o1 + o2 * o2;
+  float m = d[0] > d[1] ? d[0] : d[1];
+  m = m > d[2] ? m : d[2];
+  return out2 > 0.f ? out2 : -(m * m);
+}
+
 static float sd_box(const float p[3], const float c[3], const float h[3], float nrm[3]) {
   float d[3], s[3];
   for (int k = 0; k < 3; ++k) {
@@ -472,7 +484,7 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
       /* section search for the minimum of the (convex) sd along the segment, the HIP kernel's
        * 4-lane form: each round evaluates lo + (q+1)(hi-lo)/5, q = 0..3, and keeps the two
        * sub-intervals around the smallest value (ties to the lowest q) */
-      float lo = 0.f, hi = 1.f, tn[3];
+      float lo = 0.f, hi = 1.f;
       for (int it = 0; it < SECTION_ITERS; ++it) {
         const float w = (hi - lo) * (1.0f / (SECTION_LANES + 1));
         float fb = 0.f;
@@ -481,7 +493,7 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
           const float t = lo + (float)(q + 1) * w;
           float Q[3];
           for (int k = 0; k < 3; ++k) Q[k] = a[k] + t * (b[k] - a[k]);
-          const float f = sd_box(Q, c, h, tn);
+          const float f = sd_box_key(Q, c, h);
           if (q == 0 || f < fb) { fb = f; qb = q; }
         }
         const float nlo = lo + (float)qb * w;
