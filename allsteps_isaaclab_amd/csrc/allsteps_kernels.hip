@@ -33,9 +33,9 @@ constexpr int NVMAX = 6 + LMAX - 1; // generalized velocities
 constexpr int MAXC = AS_MAX_CONTACTS;
 constexpr int MAXR = AS_MAX_ROWS;
 constexpr int NST = AS_NUM_STONES;
-constexpr int kSectionLanes = 4;    // lanes per (stone, capsule) pair in the section search
-constexpr int kSectionIters = 8;    // interval shrinks by 2/5 per round: 0.4^8 = 6.6e-4
-constexpr int kPairsPerChunk = G / kSectionLanes;
+constexpr int kBisectIters = 12;    // capsule minimum: slope-sign bisection, interval 2^-12 = 2.4e-4
+constexpr int kPairsPerChunk = G;   // one lane per (stone, geom) pair in the exact test
+static_assert(kPairsPerChunk - 1 + G <= 64, "pending pair list (PhaseScratch::col.pl)");
 constexpr int kSweepB = 4;        // pivot block of the H^-1 sweep
 
 static_assert(NVMAX <= G, "one lane per generalized velocity");
@@ -74,7 +74,7 @@ union alignas(16) PhaseScratch {
   float obs[64];        // epilogue: observation row staging
   struct {
     float g[32][8];     // collide: geom segment endpoints, radius, packed type/foot/link
-    int pl[64];         //          pending (stone << 8 | geom) pairs, stone-major
+    int pl[64];         //          pending (stone << 8 | geom) pairs, stone-major (< 32 + G)
   } col;
   struct {
     float q[kSweepB][32];       // sweep: the pivot rows of a round (without the pivot columns)
@@ -769,10 +769,10 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   // narrowphase in two passes.  (A) lane = geom, loop over the candidate stones: the cheap
   // bounding test (spheres: the exact separation) appends the surviving (stone, geom) pairs to a
   // list in LDS, stone-major and geom-minor -- the oracle's emission order.  (B) lane = pair, in
-  // chunks of kPairsPerChunk (4 lanes per pair): the exact test (capsules: a 4-point section
-  // search) and the contacts, emitted in list order by a prefix sum.  A chunk is flushed as soon as
-  // kPairsPerChunk pairs are pending, so the list never exceeds 8 + 22 entries, and the search stops
-  // once this env has MAXC contacts.
+  // chunks of kPairsPerChunk: the exact test (capsules: slope bisection for the segment's closest
+  // point) and the contacts, emitted in list order by a prefix sum.  A chunk is flushed as soon as
+  // kPairsPerChunk pairs are pending, so the list never exceeds 32 + 22 entries, and the search
+  // stops once this env has MAXC contacts.
   {
     float* gs = s.x.col.g[lane];  // staging of this lane's geom for pass B
     if (gv) {
@@ -785,12 +785,10 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   int* pl = s.x.col.pl;
   int pend = 0, base = 0;
   auto flush = [&](int npairs) {  // pass B over pl[0, npairs) (npairs <= kPairsPerChunk), shift the rest
-    // kSectionLanes lanes per pair: lane q of a group evaluates one of the section points
-    const int pi = lane / kSectionLanes, q = lane % kSectionLanes;
     int cnt = 0, plink = 0, pst = 0, pfoot = -1;
     float P0[3], N0[3], P1[3], N1[3], P2[3], N2[3], SEP0 = 0.f, SEP1 = 0.f, SEP2 = 0.f, pr = 0.f;
-    const bool act = pi < npairs;
-    const int e = pl[act ? pi : 0];
+    const bool act = lane < npairs;
+    const int e = pl[act ? lane : 0];
     const int gi = e & 0xff;
     pst = e >> 8;
     const float* gq = s.x.col.g[gi];
@@ -802,37 +800,17 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
     plink = meta >> 8;
     float c[3];
     for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * pst + k] - s.root_pos[k];
-    // capsule: section search for the minimum of the (convex) signed distance along the segment
-    // (compared through sd_box_key, a monotone function of it without the square root).
-    // Each round the kSectionLanes lanes of the pair evaluate the interior points
-    // lo + (q+1)(hi-lo)/(kSectionLanes+1); the interval shrinks to the two sub-intervals around
-    // the smallest value (ties to the lowest q).  Runs for every group (the result is only used
-    // by capsule pairs) so the DPP exchanges see all four lanes.
+    // capsule: minimum of the (convex) signed distance along the segment by bisection on the sign
+    // of its slope.  Runs for every lane (the result is only used by capsule pairs).
     float lo = 0.f, hi = 1.f;
-#pragma unroll 1
-    for (int it = 0; it < kSectionIters; ++it) {
-      const float w = (hi - lo) * (1.0f / (kSectionLanes + 1));
-      const float t = lo + (float)(q + 1) * w;
-      float Q[3];
-      for (int k = 0; k < 3; ++k) Q[k] = A[k] + t * (Bb[k] - A[k]);
-      float f = sd_box_key(Q, c, h);
-      int qi = q;
-      // argmin over the 4 lanes of the group: quad_perm [1,0,3,2] then [2,3,0,1]
-      {
-        const float f1 = dpp<0xB1>(f);
-        const int q1 = __builtin_amdgcn_update_dpp(0, qi, 0xB1, 0xF, 0xF, true);
-        const bool tk = f1 < f || (f1 == f && q1 < qi);
-        f = tk ? f1 : f; qi = tk ? q1 : qi;
-        const float f2 = dpp<0x4E>(f);
-        const int q2 = __builtin_amdgcn_update_dpp(0, qi, 0x4E, 0xF, 0xF, true);
-        const bool tk2 = f2 < f || (f2 == f && q2 < qi);
-        f = tk2 ? f2 : f; qi = tk2 ? q2 : qi;
-      }
-      const float nlo = lo + (float)qi * w;
-      hi = lo + (float)(qi + 2) * w;
-      lo = nlo;
+#pragma unroll 2
+    for (int it = 0; it < kBisectIters; ++it) {
+      const float t = 0.5f * (lo + hi);
+      const bool up = sd_box_slope(A, Bb, t, c, h) > 0.f;
+      hi = up ? t : hi;
+      lo = up ? lo : t;
     }
-    if (act && q == 0) {
+    if (act) {
       float nr[3];
       if (pty == 0) {
         float sd = sd_box(A, c, h, nr) - pr;

@@ -380,16 +380,24 @@ static void matvec_n(const float* A, int n, const float* b, float* x) {
 /* ---------------------------------------------------------------- collision (boxes, spheres, capsules) */
 
 /* signed distance from p to an axis-aligned box (center c, half extents h); normal out of box */
-/* Monotone key of sd_box for comparisons (capsule section search): squared outside distance, or
- * minus the squared depth inside; the same ordering as sd_box without its square root. */
-static float sd_box_key(const float p[3], const float c[3], const float h[3]) {
-  float d[3];
-  for (int k = 0; k < 3; ++k) d[k] = fabsf(p[k] - c[k]) - h[k];
+/* Slope sign carrier of t -> sd_box(a + t (b - a)), convex in t: outside the box sum_k o_k s_k D_k
+ * (half the derivative of the squared distance), inside s_ax D_ax of the deepest slab (ties to the
+ * lowest axis).  Only its sign is used. */
+static float sd_box_slope(const float a[3], const float b[3], float t, const float c[3], const float h[3]) {
+  float d[3], sD[3];
+  for (int k = 0; k < 3; ++k) {
+    const float D = b[k] - a[k];
+    const float r = a[k] + t * D - c[k];
+    sD[k] = r >= 0.f ? D : -D;
+    d[k] = fabsf(r) - h[k];
+  }
   float o0 = d[0] > 0.f ? d[0] : 0.f, o1 = d[1] > 0.f ? d[1] : 0.f, o2 = d[2] > 0.f ? d[2] : 0.f;
   float out2 = o0 * o0 + o1 * o1 + o2 * o2;
-  float m = d[0] > d[1] ? d[0] : d[1];
-  m = m > d[2] ? m : d[2];
-  return out2 > 0.f ? out2 : -(m * m);
+  if (out2 > 0.f) return o0 * sD[0] + o1 * sD[1] + o2 * sD[2];
+  int ax = 0;
+  if (d[1] > d[ax]) ax = 1;
+  if (d[2] > d[ax]) ax = 2;
+  return sD[ax];
 }
 
 static float sd_box(const float p[3], const float c[3], const float h[3], float nrm[3]) {
@@ -428,8 +436,7 @@ static void add_contact(contacts_t* C, int link, int stone, int foot, const floa
   for (int k = 0; k < 3; ++k) { C->nrm[c][k] = nrm[k]; C->pt[c][k] = P[k] - nrm[k] * r; }
 }
 
-#define SECTION_LANES 4
-#define SECTION_ITERS 8
+#define BISECT_ITERS 12
 
 static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, const float* stones_rel, int nst,
                     contacts_t* C) {
@@ -481,24 +488,12 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
       float n0[3], n1[3];
       float s0 = sd_box(a, c, h, n0) - r;
       float s1 = sd_box(b, c, h, n1) - r;
-      /* section search for the minimum of the (convex) sd along the segment, the HIP kernel's
-       * 4-lane form: each round evaluates lo + (q+1)(hi-lo)/5, q = 0..3, and keeps the two
-       * sub-intervals around the smallest value (ties to the lowest q) */
+      /* minimum of the (convex) sd along the segment: bisection on the sign of its slope
+       * (sd_box_slope), BISECT_ITERS rounds, the HIP kernel's form */
       float lo = 0.f, hi = 1.f;
-      for (int it = 0; it < SECTION_ITERS; ++it) {
-        const float w = (hi - lo) * (1.0f / (SECTION_LANES + 1));
-        float fb = 0.f;
-        int qb = 0;
-        for (int q = 0; q < SECTION_LANES; ++q) {
-          const float t = lo + (float)(q + 1) * w;
-          float Q[3];
-          for (int k = 0; k < 3; ++k) Q[k] = a[k] + t * (b[k] - a[k]);
-          const float f = sd_box_key(Q, c, h);
-          if (q == 0 || f < fb) { fb = f; qb = q; }
-        }
-        const float nlo = lo + (float)qb * w;
-        hi = lo + (float)(qb + 2) * w;
-        lo = nlo;
+      for (int it = 0; it < BISECT_ITERS; ++it) {
+        const float t = 0.5f * (lo + hi);
+        if (sd_box_slope(a, b, t, c, h) > 0.f) hi = t; else lo = t;
       }
       float ts = 0.5f * (lo + hi), Ps[3], ns[3];
       for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (b[k] - a[k]);
