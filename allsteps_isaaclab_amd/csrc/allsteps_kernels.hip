@@ -889,18 +889,20 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// One projected Gauss-Seidel row from its velocity v = J_r . u and metadata {1/A_rr, target, type,
-// coupling}: normal and limit rows clamp at 0, tangent rows at +-mu * (latest normal impulse ln).
-// Updates the row's impulse (and ln on a normal row) and returns the impulse change.
-__device__ __forceinline__ float pgs_row(const float4& mt, float v, float mu, float& lam, float& ln) {
-  const float l0 = lam;
-  const float lim = mu * ln;
-  const float lt = __builtin_amdgcn_fmed3f(l0 - v * mt.x, -lim, lim);  // = min(max(., -lim), lim), lim >= 0
-  const float lnrm = fmaxf(l0 + (mt.y - v) * mt.x, 0.f);
-  const float l1 = mt.z == 1.f ? lt : lnrm;
+// One projected Gauss-Seidel row: t = lambda_old + (target - J_r . u) / A_rr is formed by the
+// caller; normal and limit rows clamp it to [0, inf), tangent rows to +-mu * (latest normal
+// impulse ln) -- one v_med3 for both (a tangent row's target is 0).  Updates the row's impulse
+// (and ln on a normal row) and returns the impulse change.
+__device__ __forceinline__ float pgs_clamp(const float4& mt, float t, float mu, float& lam, float& ln) {
+  // bounds as one FMA each from ln (tangent: mu_r = mu, off = 0; otherwise mu_r = 0, off = inf;
+  // 0 * ln + 0 keeps the normal rows' lower bound +0)
+  const bool tangent = mt.z == 1.f;
+  const float mu_r = tangent ? mu : 0.f, off = tangent ? 0.f : __builtin_inff();
+  const float l1 = __builtin_amdgcn_fmed3f(t, fmaf(-mu_r, ln, 0.f), fmaf(mu_r, ln, off));
   ln = mt.z == 0.f ? l1 : ln;
+  const float d = l1 - lam;
   lam = l1;
-  return l1 - l0;
+  return d;
 }
 
 template <int NV>
@@ -1134,16 +1136,21 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       const float4 m2 = *reinterpret_cast<const float4*>(s.rmeta[r + 2]);
       float vg[3] = {Jc[r] * uj, Jc[r + 1] * uj, Jc[r + 2] * uj};
       half_sum_n(vg);
-      float v0 = vg[0], v1 = vg[1], v2 = vg[2];
-      const float d0 = pgs_row(m0, v0, mu, lamr[r], ln);
-      v1 += m0.w * d0;
-      v2 += m1.w * d0;
-      uj += Wc[r] * d0;
-      const float d1 = pgs_row(m1, v1, mu, lamr[r + 1], ln);
-      v2 += m2.w * d1;
-      uj += Wc[r + 1] * d1;
-      const float d2 = pgs_row(m2, v2, mu, lamr[r + 2], ln);
-      uj += Wc[r + 2] * d2;
+      // t_s = lambda_s + (target_s - v_s - sum_{r<s} A_sr dl_r) x_s, with the parts that do not
+      // depend on this sweep's impulse changes formed first: the chain from one row's dl to the
+      // next row's clamp is a single FMA
+      const float k10 = m1.x * m0.w, k20 = m2.x * m1.w, k21 = m2.x * m2.w;  // x_s A_sr
+      float t1 = fmaf(-vg[1], m1.x, fmaf(m1.y, m1.x, lamr[r + 1]));
+      float t2 = fmaf(-vg[2], m2.x, fmaf(m2.y, m2.x, lamr[r + 2]));
+      const float d0 = pgs_clamp(m0, fmaf(-vg[0], m0.x, fmaf(m0.y, m0.x, lamr[r])), mu, lamr[r], ln);
+      t1 = fmaf(-k10, d0, t1);
+      t2 = fmaf(-k20, d0, t2);
+      uj = fmaf(Wc[r], d0, uj);
+      const float d1 = pgs_clamp(m1, t1, mu, lamr[r + 1], ln);
+      t2 = fmaf(-k21, d1, t2);
+      uj = fmaf(Wc[r + 1], d1, uj);
+      const float d2 = pgs_clamp(m2, t2, mu, lamr[r + 2], ln);
+      uj = fmaf(Wc[r + 2], d2, uj);
     }
   }
   float lam = 0.f;
