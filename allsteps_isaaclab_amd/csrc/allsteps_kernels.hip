@@ -359,20 +359,21 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
     float R[9], p[3] = {0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 9; ++k) R[k] = R0[k];
-    // two path links per iteration: both local transforms are loaded before the products
+    // kPathU path links per iteration: their local transforms are loaded before the products
+    constexpr int kPathU = 4;
     uint32_t path = tp.lpath & ~1u;
-    for (int it = 0; it < K.max_path; it += 2) {
-      bool v[2];
-      int l[2];
-      l[0] = take_bit(path, v[0]);
-      l[1] = take_bit(path, v[1]);
-      float Tl[2][12];
+    for (int it = 0; it < K.max_path; it += kPathU) {
+      bool v[kPathU];
+      int l[kPathU];
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < kPathU; ++u) l[u] = take_bit(path, v[u]);
+      float Tl[kPathU][12];
+#pragma unroll
+      for (int u = 0; u < kPathU; ++u)
 #pragma unroll
         for (int k = 0; k < 12; ++k) Tl[u][k] = d.Rl[l[u]][k];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < kPathU; ++u) {
         float Rn[9], wp[3];
         matmul3(R, Tl[u], Rn);
         matvec3(R, Tl[u] + 9, wp);
@@ -506,21 +507,22 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
   __syncthreads();
   if (lane >= 1 && lane < nl) {
     uint32_t sub = tp.lsub & ~(1u << lane);
-    for (int it = 0; it < K.max_sub; it += 2) {  // two subtree links per iteration
-      bool v[2];
-      int l[2];
-      l[0] = take_bit(sub, v[0]);
-      l[1] = take_bit(sub, v[1]);
-      float fl[2][6], Il[2][10];
+    constexpr int kSubU = 4;
+    for (int it = 0; it < K.max_sub; it += kSubU) {  // kSubU subtree links per iteration
+      bool v[kSubU];
+      int l[kSubU];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < kSubU; ++u) l[u] = take_bit(sub, v[u]);
+      float fl[kSubU][6], Il[kSubU][10];
+#pragma unroll
+      for (int u = 0; u < kSubU; ++u) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) fl[u][k] = d.b.f[l[u]][k];
 #pragma unroll
         for (int k = 0; k < 10; ++k) Il[u][k] = d.Ib[l[u]][k];
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < kSubU; ++u) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) f[k] += v[u] ? fl[u][k] : 0.f;
 #pragma unroll
