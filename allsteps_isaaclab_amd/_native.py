@@ -22,7 +22,7 @@ ABI_VERSION = 1
 EXPORTED_SYMBOLS = [
     "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
-    "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps",
+    "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask",
 ]
 
 
@@ -103,6 +103,7 @@ def load() -> C.CDLL:
     L.as_create.argtypes = [I32, V, V, V, V, U64, I32, I64, C.POINTER(V)]
     L.as_destroy.argtypes = [V]
     L.as_reset_all.argtypes = [V, V, V, V]
+    L.as_reset_mask.argtypes = [V, V, V, V, V]
     L.as_step.argtypes = [V, V, V, V, V, V, V, V]
     L.as_physics_step.argtypes = [V, V, V]
     L.as_task_step.argtypes = [V, V, V, V, V, V, V, V]
@@ -265,6 +266,11 @@ class NativeEnv:
         check(self.L.as_reset_all(self.h, obs.data_ptr(),
                                   reset_draws.data_ptr() if reset_draws is not None else None, stream),
               "as_reset_all")
+
+    def reset_mask(self, mask, obs, reset_draws=None, stream=None):
+        check(self.L.as_reset_mask(self.h, mask.data_ptr(), obs.data_ptr(),
+                                   reset_draws.data_ptr() if reset_draws is not None else None, stream),
+              "as_reset_mask")
 
     def physics_step(self, actions, stream=None):
         check(self.L.as_physics_step(self.h, actions.data_ptr(), stream), "as_physics_step")

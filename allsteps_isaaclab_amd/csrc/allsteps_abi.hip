@@ -154,7 +154,7 @@ int as_destroy(as_env_t* env) {
 }
 
 static int run(as_env_t* env, int mode, const float* actions, float* obs, float* reward, uint8_t* term,
-               uint8_t* trunc, const float* reset_draws, void* stream) {
+               uint8_t* trunc, const float* reset_draws, void* stream, const uint8_t* reset_mask = nullptr) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // no memset per step: this launch's counter bank was cleared by the previous launch's k_obs
   // (physics-only launches do not touch the counters and keep the bank)
@@ -169,6 +169,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   a.terminated = term;
   a.truncated = trunc;
   a.reset_draws = reset_draws;
+  a.reset_mask = reset_mask;
   a.counters = cnt;
   a.seed = env->seed;
   a.env_offset = env->env_offset;
@@ -263,6 +264,11 @@ int as_set_seed(as_env_t* env, uint64_t seed) {
 int as_reset_all(as_env_t* env, float* obs, const float* reset_draws, void* stream) {
   if (!env || !obs) return fail(AS_ERR_INVALID, "as_reset_all: null argument");
   return run(env, as::kModeReset, nullptr, obs, nullptr, nullptr, nullptr, reset_draws, stream);
+}
+
+int as_reset_mask(as_env_t* env, const uint8_t* mask, float* obs, const float* reset_draws, void* stream) {
+  if (!env || !mask || !obs) return fail(AS_ERR_INVALID, "as_reset_mask: null argument");
+  return run(env, as::kModeReset, nullptr, obs, nullptr, nullptr, nullptr, reset_draws, stream, mask);
 }
 
 int as_physics_step(as_env_t* env, const float* actions, void* stream) {

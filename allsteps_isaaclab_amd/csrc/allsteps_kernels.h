@@ -44,6 +44,7 @@ struct StepArgs {
   uint8_t* terminated;
   uint8_t* truncated;
   const float* reset_draws;
+  const uint8_t* reset_mask;   // kModeReset: envs to reset (null: all)
   int32_t* counters;  // one bank (kCntBank ints, zero at launch: see k_obs), layout below
   uint64_t seed;
   int64_t env_offset;

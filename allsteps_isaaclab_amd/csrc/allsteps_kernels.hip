@@ -1411,7 +1411,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       P.truncated[e] = time_out ? 1 : 0;
     }
   } else if (P.mode == kModeReset) {
-    done = true;
+    done = P.reset_mask == nullptr || P.reset_mask[e] != 0;
   }
   if (P.mode != kModePhysics) {
     // curriculum mean over the tick-#1 indices and the any-reset flag: one atomic per wave into a

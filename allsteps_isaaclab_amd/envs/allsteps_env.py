@@ -209,6 +209,29 @@ class AllstepsEnv(DirectRLEnv):
         self.obs_buf = {"policy": obs}
         return self.obs_buf
 
+    def _reset_idx(self, env_ids, reset_draws: torch.Tensor | None = None):
+        """AllstepsEnv._reset_idx(env_ids) (allsteps_env.py:469-567): reset the given envs (curriculum
+        gate and second foot-state tick for all envs, as the reference does), then refresh the
+        observation buffer.  ``env_ids``: indices, a bool mask, or None (all envs)."""
+        if env_ids is None:
+            return self._reset_impl(reset_draws)
+        ids = torch.as_tensor(env_ids, device=self._device)
+        if ids.dtype == torch.bool:
+            if ids.shape != (self.num_envs,):
+                raise ValueError(f"env_ids mask must be ({self.num_envs},), got {tuple(ids.shape)}")
+            mask = ids.to(torch.uint8).contiguous()
+        else:
+            ids = ids.long().reshape(-1)
+            if ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= self.num_envs):
+                raise IndexError(f"env_ids out of range [0, {self.num_envs})")
+            mask = torch.zeros(self.num_envs, dtype=torch.uint8, device=self._device)
+            mask[ids] = 1
+        obs = torch.empty(self.num_envs, self.cfg.observation_space, device=self._device)
+        d = None if reset_draws is None else reset_draws.to(self._device).float().contiguous()
+        self._native.reset_mask(mask, obs, d, stream=self._stream())
+        self.obs_buf = {"policy": obs}
+        return self.obs_buf
+
     def _step_impl(self, action: torch.Tensor, reset_draws: torch.Tensor | None = None):
         a = action if (action.dtype == torch.float32 and action.is_contiguous()) else action.float().contiguous()
         if a.shape != (self.num_envs, self.cfg.action_space):

@@ -150,6 +150,13 @@ int as_destroy(as_env_t* env);
 /* DirectRLEnv.reset (direct_rl_env.py:256-294): _reset_idx(all) -> FK -> observations. */
 int as_reset_all(as_env_t* env, float* obs, const float* reset_draws, void* stream);
 
+/* AllstepsEnv._reset_idx(env_ids) (allsteps_env.py:469-567, direct_rl_env.py:563-584) on the envs
+ * with mask[e] != 0 (device, [n] uint8), then _get_observations for all envs into obs [n][59].
+ * Like the reference's _reset_idx it applies the curriculum gate (mean target index over all envs)
+ * and the second foot-state tick to every env; an all-zero mask changes nothing (the reference
+ * never calls _reset_idx with no ids).  reset_draws as in as_step. */
+int as_reset_mask(as_env_t* env, const uint8_t* mask, float* obs, const float* reset_draws, void* stream);
+
 /* DirectRLEnv.step (direct_rl_env.py:296-383) for all envs: actions [n][21] (any range, clamped
  * to [-1,1] inside) -> obs [n][59], reward [n], terminated [n], truncated [n] (uint8 0/1).
  * reset_draws: NULL (Philox) or [n][22] U[0,1) draws (mirror, 21 joint-noise) for envs that reset

@@ -137,6 +137,10 @@ void or_task_post_physics(const or_model_t* model, const or_task_t* task, or_sta
 
 void or_task_reset_all(const or_model_t* model, const or_task_t* task, or_state_t* st, const float* reset_draws,
                        uint64_t seed, float* obs);
+/* ENV:469-567 _reset_idx on the envs with mask[e] != 0 (curriculum gate and second tick for all
+ * envs), then _get_observations; an all-zero mask leaves the state unchanged. */
+void or_task_reset_mask(const or_model_t* model, const or_task_t* task, or_state_t* st, const uint8_t* mask,
+                        const float* reset_draws, uint64_t seed, float* obs);
 
 /* ---- physics ---- */
 void or_fk_bodies(const or_model_t* m, const float root_pos[3], const float root_quat[4], const float* q_cfg,

@@ -88,6 +88,7 @@ def lib() -> C.CDLL:
         L.or_task_post_physics.argtypes = [V, V, V, FP, FP, FP, FP, C.c_uint64, V, V, FP, FP,
                                            C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), IP]
         L.or_task_reset_all.argtypes = [V, V, V, FP, C.c_uint64, FP]
+        L.or_task_reset_mask.argtypes = [V, V, V, C.POINTER(C.c_uint8), FP, C.c_uint64, FP]
         L.or_env_step.argtypes = [V, V, V, V, FP, FP, C.c_uint64, FP, FP, C.POINTER(C.c_uint8),
                                   C.POINTER(C.c_uint8), IP, C.c_int]
         L.or_env_reset_all.argtypes = [V, V, V, V, FP, C.c_uint64, FP]
@@ -278,6 +279,14 @@ class Oracle:
         rd = fp(np.ascontiguousarray(reset_draws, np.float32)) if reset_draws is not None else None
         self.L.or_env_reset_all(C.byref(self.model), C.byref(self.sim), C.byref(self.task), st.ptr, rd, seed,
                                 fp(obs))
+        return obs
+
+    def reset_mask(self, st: OracleState, mask, seed: int = 42, reset_draws=None):
+        """_reset_idx on the envs with mask != 0, then the observations (or_task_reset_mask)."""
+        obs = np.zeros((st.n, 59), np.float32)
+        m = np.ascontiguousarray(np.asarray(mask) != 0, np.uint8)
+        rd = fp(np.ascontiguousarray(reset_draws, np.float32)) if reset_draws is not None else None
+        self.L.or_task_reset_mask(C.byref(self.model), C.byref(self.task), st.ptr, u8p(m), rd, seed, fp(obs))
         return obs
 
     def footsteps(self, n: int, level: int, draws: np.ndarray):

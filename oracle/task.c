@@ -245,8 +245,8 @@ static void foot_state(const or_task_t* task, or_state_t* st, int e, const float
 }
 
 /* ENV:276-324 _compute_useful_values for one env (incl. foot-state tick, targets, potentials). */
-static void compute_useful(const or_model_t* model, const or_task_t* task, or_state_t* st, int e,
-                           const float* fm_r, const float* fm_l, useful_t* u) {
+static void useful_values(const or_model_t* model, const or_task_t* task, or_state_t* st, int e,
+                          const float* fm_r, const float* fm_l, useful_t* u, int tick) {
   const int n = st->n;
   float rz = F(st->body_pos, 3 + 2, n, e), lz = F(st->body_pos, 6 + 2, n, e);
   float lower = lz < rz ? lz : rz;                                      /* ENV:281 minimum(left, right) */
@@ -261,7 +261,7 @@ static void compute_useful(const or_model_t* model, const or_task_t* task, or_st
   }
   float v[3] = {F(st->root_lin, 0, n, e), F(st->root_lin, 1, n, e), F(st->root_lin, 2, n, e)};
   or_quat_rotate_inverse(q, v, u->vb);                                  /* ENV:293 */
-  foot_state(task, st, e, fm_r, fm_l, u);                               /* ENV:298 */
+  if (tick) foot_state(task, st, e, fm_r, fm_l, u);                     /* ENV:298 */
   const int N = task->num_steps;
   int tix[3] = {st->prev[e], st->idx[e], st->next[e]};                  /* ENV:459-467 */
   float rp[3] = {F(st->root_pos, 0, n, e), F(st->root_pos, 1, n, e), F(st->root_pos, 2, n, e)};
@@ -273,8 +273,21 @@ static void compute_useful(const or_model_t* model, const or_task_t* task, or_st
   (void)N;
   float dx = tw[2][0] - rp[0], dy = tw[2][1] - rp[1];                   /* ENV:407-416 */
   u->body_dist_xy = sqrtf(dx * dx + dy * dy);
+  if (!tick) return;
   st->old_pot[e] = st->pot[e];
   st->pot[e] = -(u->body_dist_xy) / task->step_dt;
+}
+
+/* ENV:276-324 _compute_useful_values (foot-state tick and potentials included). */
+static void compute_useful(const or_model_t* model, const or_task_t* task, or_state_t* st, int e,
+                           const float* fm_r, const float* fm_l, useful_t* u) {
+  useful_values(model, task, st, e, fm_r, fm_l, u, 1);
+}
+
+/* The observation inputs of the current state without a foot-state tick (no _compute_useful_values
+ * call: an empty reset set). */
+static void useful_no_tick(const or_model_t* model, const or_task_t* task, or_state_t* st, int e, useful_t* u) {
+  useful_values(model, task, st, e, NULL, NULL, u, 0);
 }
 
 /* ENV:326-345 _get_observations for one env. */
@@ -430,6 +443,25 @@ void or_task_reset_all(const or_model_t* model, const or_task_t* task, or_state_
   for (int e = 0; e < n; ++e) write_obs(task, st, e, &u[e], obs + (size_t)e * 59);
   free(u);
   free(done);
+}
+
+void or_task_reset_mask(const or_model_t* model, const or_task_t* task, or_state_t* st, const uint8_t* mask,
+                        const float* reset_draws, uint64_t seed, float* obs) {
+  /* ENV:469-567 _reset_idx(env_ids) then ENV:326-345 _get_observations; an empty id set is a no-op
+   * (DRL:361 only calls _reset_idx when some env is done) */
+  const int n = st->n;
+  int any = 0;
+  long long idx_sum = 0;
+  for (int e = 0; e < n; ++e) { any |= mask[e] != 0; idx_sum += st->idx[e]; }
+  useful_t* u = (useful_t*)malloc(sizeof(useful_t) * (size_t)n);
+  if (any) {
+    reset_and_tick2(model, task, st, mask, idx_sum, reset_draws, seed, NULL, NULL, NULL, NULL, u);
+  } else {
+    /* no reset: the observation of the current state, no foot-state tick */
+    for (int e = 0; e < n; ++e) useful_no_tick(model, task, st, e, &u[e]);
+  }
+  for (int e = 0; e < n; ++e) write_obs(task, st, e, &u[e], obs + (size_t)e * 59);
+  free(u);
 }
 
 void or_task_post_physics(const or_model_t* model, const or_task_t* task, or_state_t* st, const float* actions,

@@ -212,6 +212,40 @@ def test_reset_all_parity(orc):
     env.close()
 
 
+@pytest.mark.parametrize("kind", ["partial", "none", "all"])
+def test_reset_mask_parity(orc, kind):
+    """_reset_idx(env_ids) on a subset (as_reset_mask) vs the oracle's masked reset, from states
+    reached by random stepping (non-trivial foot state for the second tick)."""
+    n = 128
+    st = _random_states(orc, n, 12, seed=31)
+    env = _env(n)
+    _from_oracle(env, st)
+    rng = np.random.default_rng(5)
+    mask = {"partial": rng.uniform(size=n) < 0.3, "none": np.zeros(n, bool), "all": np.ones(n, bool)}[kind]
+    draws = rng.uniform(0, 1, (n, 22)).astype(np.float32)
+    before = _gpu_state(env)
+    o_g = env._reset_idx(torch.from_numpy(mask), reset_draws=torch.from_numpy(draws))
+    torch.cuda.synchronize()
+    o_c = orc.reset_mask(st, mask, reset_draws=draws)
+    gs = _gpu_state(env)
+    for k in ("idx", "prev", "next", "count", "swing", "ep_len", "episode", "curriculum"):
+        np.testing.assert_array_equal(gs[k], st[k], k)
+    for k in ("q", "qd", "root_pos", "root_quat", "root_lin", "root_ang"):
+        np.testing.assert_allclose(gs[k], st[k], atol=1e-5, err_msg=k)
+        # envs outside the mask keep their physical state bit for bit
+        np.testing.assert_array_equal(gs[k][..., ~mask], before[k][..., ~mask], k)
+    np.testing.assert_allclose(gs["body_pos"], st["body_pos"], atol=1e-5)
+    np.testing.assert_allclose(gs["pot"], st["pot"], rtol=1e-5, atol=1e-4)
+    og = o_g["policy"].cpu().numpy()
+    d = np.abs(og - o_c)
+    d[:, 1:3] = np.minimum(d[:, 1:3], np.abs(d[:, 1:3] - 2 * np.pi))
+    assert d.max() < 1e-4, d.max()
+    if kind == "none":
+        for k in before:
+            np.testing.assert_array_equal(gs[k], before[k], k)
+    env.close()
+
+
 def test_philox_reset_draws_match_oracle(orc):
     """Without injected draws both sides use Philox(seed, env, episode): resets agree."""
     n = 64

@@ -155,3 +155,42 @@ def test_philox_uniform_range(orc):
     np.testing.assert_array_equal(a, orc.philox(42, 3, 1))
     assert not np.array_equal(a, orc.philox(42, 3, 2))
     assert not np.array_equal(a, orc.philox(43, 3, 1))
+
+
+def _stepped_state(orc, n, steps, seed):
+    st = orc.state(n)
+    rng = np.random.default_rng(seed)
+    orc.reset_all(st, reset_draws=rng.uniform(0, 1, (n, 22)).astype(np.float32))
+    for _ in range(steps):
+        orc.env_step(st, rng.uniform(-1, 1, (n, 21)).astype(np.float32),
+                     reset_draws=rng.uniform(0, 1, (n, 22)).astype(np.float32))
+    return st
+
+
+def test_reset_mask_matches_reset_all_and_noop(orc):
+    """_reset_idx(all ids) == reset(); _reset_idx(no ids) changes nothing; a subset resets exactly
+    the masked envs (the foot-state tick and the curriculum gate apply to all, as in the reference)."""
+    n = 24
+    draws = np.random.default_rng(1).uniform(0, 1, (n, 22)).astype(np.float32)
+    a, b = _stepped_state(orc, n, 6, 9), _stepped_state(orc, n, 6, 9)
+    oa = orc.reset_all(a, reset_draws=draws)
+    ob = orc.reset_mask(b, np.ones(n, bool), reset_draws=draws)
+    for k in ("q", "qd", "root_pos", "root_quat", "idx", "prev", "next", "count", "swing", "pot", "old_pot",
+              "episode", "ep_len", "curriculum", "body_pos", "foot_contact"):
+        np.testing.assert_array_equal(a[k], b[k], k)
+    np.testing.assert_array_equal(oa, ob)
+    c = _stepped_state(orc, n, 6, 9)
+    before = {k: np.array(c[k]) for k in ("q", "qd", "root_pos", "idx", "count", "swing", "pot", "old_pot",
+                                          "ep_len", "episode", "foot_contact")}
+    oc = orc.reset_mask(c, np.zeros(n, bool), reset_draws=draws)
+    for k, v in before.items():
+        np.testing.assert_array_equal(c[k], v, k)
+    assert np.isfinite(oc).all()
+    # partial: masked envs get the reset pose of the full reset, the others keep their joints
+    d = _stepped_state(orc, n, 6, 9)
+    q0 = np.array(d["q"])
+    m = np.arange(n) % 3 == 0
+    orc.reset_mask(d, m, reset_draws=draws)
+    np.testing.assert_array_equal(d["q"][:, m], a["q"][:, m])
+    np.testing.assert_array_equal(d["q"][:, ~m], q0[:, ~m])
+    np.testing.assert_array_equal(d["ep_len"][m], 0)
