@@ -13,6 +13,7 @@ import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "liballsteps_hip.so")
+PPO_LIB_PATH = os.path.join(PKG, "libppo_hip.so")
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 
@@ -131,13 +132,19 @@ def check(rc: int, what: str) -> None:
 
 
 def build_native(verbose: bool = False) -> str:
-    """Compile liballsteps_hip.so for gfx950 in-tree (hipcc)."""
+    """Compile liballsteps_hip.so and libppo_hip.so for gfx950 in-tree (hipcc)."""
     import subprocess
 
     srcs = [os.path.join(CSRC, f) for f in ("allsteps_kernels.hip", "allsteps_abi.hip")]
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
            "-I", INCLUDE, "-o", LIB_PATH] + srcs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    # PPO-update kernels (include/ppo.h) -> libppo_hip.so
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+           "-I", INCLUDE, "-o", PPO_LIB_PATH, os.path.join(CSRC, "ppo_kernels.hip")]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

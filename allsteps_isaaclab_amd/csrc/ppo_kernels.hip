@@ -1,0 +1,488 @@
+// ppo_kernels.hip -- the non-GEMM half of one PPO minibatch step (include/ppo.h), gfx950.
+//
+// Restates rl_games 1.6.1 (absent offline): a2c_continuous.py calc_gradients
+// (actor_loss / critic_loss / bound_loss / entropy, policy_kl, update_mu_sigma), running_mean_std.py
+// (train-mode update + normalise), torch clip_grad_norm_ + torch.optim.Adam, schedulers.py
+// AdaptiveScheduler.  Gradients are the analytic derivatives of those losses (the autograd graph of
+// the reference reduces to them); tests/test_gpu_learning.py checks them against torch autograd.
+//
+// Everything is deterministic (fixed-order block partials, no float atomics), so ranks that replay
+// the same update on the same data stay bit-identical (multi_gpu_mode allgather).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "ppo.h"
+
+namespace {
+
+thread_local char g_err[256] = "";
+
+int fail(int code, const char* what) {
+    snprintf(g_err, sizeof(g_err), "%s", what);
+    return code;
+}
+
+int launched(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+        return -2;
+    }
+    return 0;
+}
+
+constexpr int kWave = 64;
+constexpr float kLog2Pi = 1.8378770664093453f;
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {  // round to nearest even
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7f800000u) == 0x7f800000u) return uint16_t((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return uint16_t(u >> 16);
+}
+
+__device__ __forceinline__ float load_as_f32(const void* p, int64_t i, int dtype) {
+    return dtype ? bf16_to_f32(static_cast<const uint16_t*>(p)[i]) : static_cast<const float*>(p)[i];
+}
+
+__device__ __forceinline__ void store_from_f32(void* p, int64_t i, int dtype, float x) {
+    if (dtype)
+        static_cast<uint16_t*>(p)[i] = f32_to_bf16(x);
+    else
+        static_cast<float*>(p)[i] = x;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, kWave);
+    return x;
+}
+
+// ------------------------------------------------------------------------------ obs normaliser
+
+constexpr int kStatRows = 256;
+
+__global__ void __launch_bounds__(64) k_obs_stats(const float* __restrict__ x, const int32_t* __restrict__ mb_idx,
+                                                  int mb_rows, int cols, double* __restrict__ partials) {
+    const int c = threadIdx.x;
+    const int64_t base = int64_t(*mb_idx) * mb_rows;
+    const int r0 = blockIdx.x * kStatRows;
+    const int r1 = min(r0 + kStatRows, mb_rows);
+    double s = 0.0, ss = 0.0;
+    if (c < cols) {
+        for (int r = r0; r < r1; ++r) {
+            const double v = x[(base + r) * cols + c];
+            s += v;
+            ss += v * v;
+        }
+    }
+    partials[(blockIdx.x * 2 + 0) * 64 + c] = s;
+    partials[(blockIdx.x * 2 + 1) * 64 + c] = ss;
+}
+
+__global__ void __launch_bounds__(64) k_obs_stats_update(const double* __restrict__ partials, int nblk, int cols,
+                                                         int mb_rows, double* __restrict__ mean,
+                                                         double* __restrict__ var, double* __restrict__ count) {
+    const int c = threadIdx.x;
+    const double cnt = *count;  // every lane reads before lane 0 writes (single wave, in-order)
+    if (c < cols) {
+        double s = 0.0, ss = 0.0;
+        for (int b = 0; b < nblk; ++b) {
+            s += partials[(b * 2 + 0) * 64 + c];
+            ss += partials[(b * 2 + 1) * 64 + c];
+        }
+        const double n = double(mb_rows);
+        const double bm = s / n;
+        const double bv = fmax(ss - n * bm * bm, 0.0) / (n - 1.0);  // torch.var: unbiased
+        const double d = bm - mean[c];
+        const double tot = cnt + n;
+        const double m2 = var[c] * cnt + bv * n + d * d * cnt * n / tot;
+        mean[c] = mean[c] + d * n / tot;
+        var[c] = m2 / tot;
+    }
+    __syncthreads();
+    if (c == 0) *count = cnt + double(mb_rows);
+}
+
+__global__ void k_obs_normalize(const float* __restrict__ x, const int32_t* __restrict__ mb_idx, int mb_rows, int cols,
+                                const double* __restrict__ mean, const double* __restrict__ var, float eps,
+                                void* __restrict__ out, int out_stride, int out_bf16) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= int64_t(mb_rows) * out_stride) return;
+    const int r = int(i / out_stride), c = int(i % out_stride);
+    float y = 0.f;
+    if (c < cols) {
+        const float v = x[(int64_t(*mb_idx) * mb_rows + r) * cols + c];
+        // rl_games: (x - mean.float()) / sqrt(var.float() + eps), then clamp
+        y = (v - float(mean[c])) / sqrtf(float(var[c]) + eps);
+        y = fminf(fmaxf(y, -5.f), 5.f);
+    }
+    store_from_f32(out, i, out_bf16, y);
+}
+
+// ------------------------------------------------------------------------------ PPO losses
+
+constexpr int kLossThreads = 256;
+
+// gradient of max(u1, u2) (torch.maximum: ties split the gradient in half)
+__device__ __forceinline__ float max_grad(float u1, float u2, float g1, float g2) {
+    return u1 > u2 ? g1 : (u2 > u1 ? g2 : 0.5f * (g1 + g2));
+}
+
+template <int A>
+__global__ void __launch_bounds__(kLossThreads) k_loss_grad(
+    const float* __restrict__ head, const float* __restrict__ logstd, int mb_rows, const int32_t* __restrict__ mb_idx,
+    const float* __restrict__ actions, float* __restrict__ ds_mu, float* __restrict__ ds_sigma,
+    const float* __restrict__ old_nlp, const float* __restrict__ adv_, const float* __restrict__ old_v,
+    const float* __restrict__ ret_, ppo_loss_cfg_t cfg, float* __restrict__ dhead, float* __restrict__ partials) {
+    constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
+    __shared__ float red[kLossThreads / kWave][NV];
+    const int r = blockIdx.x * kLossThreads + threadIdx.x;
+    const bool live = r < mb_rows;
+    const float inv_b = 1.f / float(mb_rows);
+    float vals[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) vals[k] = 0.f;
+    if (live) {
+        const int64_t row = int64_t(*mb_idx) * mb_rows + r;
+        const float* h = head + int64_t(r) * (A + 1);
+        float mu[A], d[A], sig[A];
+        float sum_ls = 0.f, q = 0.f, kl = 0.f;
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            const float ls = logstd[j];
+            sig[j] = expf(ls);
+            mu[j] = h[j];
+            d[j] = (actions[row * A + j] - mu[j]) / sig[j];
+            q += d[j] * d[j];
+            sum_ls += ls;
+            // policy_kl(p0 = current, p1 = dataset): log(s1/s0 + 1e-5) + (s0^2 + (m1-m0)^2) / (2 (s1^2 + 1e-5)) - 1/2
+            const float m1 = ds_mu[row * A + j], s1 = ds_sigma[row * A + j];
+            const float dm = m1 - mu[j];
+            kl += logf(s1 / sig[j] + 1e-5f) + (sig[j] * sig[j] + dm * dm) / (2.f * (s1 * s1 + 1e-5f)) - 0.5f;
+        }
+        const float nlp = 0.5f * q + 0.5f * kLog2Pi * float(A) + sum_ls;
+        const float adv = adv_[row];
+        // actor
+        float a_loss, g_nlp;
+        if (cfg.ppo) {
+            const float ratio = expf(old_nlp[row] - nlp);
+            const float rc = fminf(fmaxf(ratio, 1.f - cfg.e_clip), 1.f + cfg.e_clip);
+            const float u1 = -adv * ratio, u2 = -adv * rc;
+            const bool inside = ratio >= 1.f - cfg.e_clip && ratio <= 1.f + cfg.e_clip;
+            // d(-adv * ratio)/d nlp = adv * ratio (d ratio / d nlp = -ratio)
+            g_nlp = max_grad(u1, u2, adv * ratio, inside ? adv * ratio : 0.f);
+            a_loss = fmaxf(u1, u2);
+        } else {
+            a_loss = nlp * adv;
+            g_nlp = adv;
+        }
+        g_nlp *= inv_b;
+        // critic
+        const float v = h[A], vp = old_v[row], R = ret_[row];
+        float c_loss, g_v;
+        if (cfg.clip_value) {
+            const float dv = v - vp;
+            const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
+            const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
+            const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
+            g_v = max_grad(l1, l2, 2.f * (v - R), inside ? 2.f * (vc - R) : 0.f);
+            c_loss = fmaxf(l1, l2);
+        } else {
+            c_loss = (R - v) * (R - v);
+            g_v = 2.f * (v - R);
+        }
+        g_v *= 0.5f * cfg.critic_coef * inv_b;
+        // bound loss + head gradients
+        float b_loss = 0.f;
+        const float gb = cfg.bounds_coef * inv_b;
+        float* dh = dhead + int64_t(r) * (A + 1);
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            float db = 0.f;
+            if (cfg.bound_loss == 1) {
+                const float lo = fminf(mu[j] + cfg.soft_bound, 0.f), hi = fmaxf(mu[j] - cfg.soft_bound, 0.f);
+                b_loss += lo * lo + hi * hi;
+                db = 2.f * (lo + hi);
+            } else if (cfg.bound_loss == 2) {
+                b_loss += mu[j] * mu[j];
+                db = 2.f * mu[j];
+            }
+            // d nlp / d mu = -(a - mu) / sigma^2 = -d / sigma ; d nlp / d logstd = 1 - d^2
+            const float gmu = -g_nlp * d[j] / sig[j] + gb * db;
+            dh[j] = gmu;
+            vals[j] = gmu;
+            vals[A + 1 + j] = g_nlp * (1.f - d[j] * d[j]);
+            ds_mu[row * A + j] = mu[j];  // dataset.update_mu_sigma
+            ds_sigma[row * A + j] = sig[j];
+        }
+        dh[A] = g_v;
+        vals[A] = g_v;
+        const float entropy = float(A) * (0.5f + 0.5f * kLog2Pi) + sum_ls;
+        vals[2 * A + 1 + 0] = a_loss;
+        vals[2 * A + 1 + 1] = c_loss;
+        vals[2 * A + 1 + 2] = b_loss;
+        vals[2 * A + 1 + 3] = entropy;
+        vals[2 * A + 1 + 4] = kl;
+    }
+    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const float s = wave_sum(vals[k]);
+        if (lane == 0) red[w][k] = s;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < NV; k += kLossThreads) {
+        float s = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < kLossThreads / kWave; ++ww) s += red[ww][k];
+        partials[int64_t(blockIdx.x) * NV + k] = s;
+    }
+}
+
+__global__ void k_loss_finalize(const float* __restrict__ partials, int nblk, int A, int mb_rows, float entropy_coef,
+                                float* __restrict__ g_hb, float* __restrict__ g_ls, float* __restrict__ stats,
+                                const int32_t* __restrict__ stat_idx, float* __restrict__ kl_out) {
+    const int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
+    const int k = threadIdx.x;
+    if (k >= NV) return;
+    float s = 0.f;
+    for (int b = 0; b < nblk; ++b) s += partials[int64_t(b) * NV + k];
+    if (k <= A) {
+        g_hb[k] = s;
+    } else if (k <= 2 * A) {
+        g_ls[k - A - 1] = s - entropy_coef;  // - entropy_coef * mean(entropy): d/d logstd_j = -entropy_coef
+    } else {
+        const int st = k - 2 * A - 1;
+        const float mean = s / float(mb_rows);
+        stats[int64_t(*stat_idx) * PPO_LOSS_NSTAT + st] = mean;
+        if (st == 4) *kl_out = mean;
+    }
+}
+
+// ------------------------------------------------------------------------------ ELU backward
+
+constexpr int kEluRows = 64;
+
+__global__ void __launch_bounds__(256) k_elu_bwd(const void* __restrict__ dh, int dh_t, const void* __restrict__ h,
+                                                 int h_t, void* __restrict__ dz, int dz_t, int rows, int cols,
+                                                 float* __restrict__ partials) {
+    const int r0 = blockIdx.x * kEluRows;
+    const int r1 = min(r0 + kEluRows, rows);
+    for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+        float s = 0.f;
+        for (int r = r0; r < r1; ++r) {
+            const int64_t i = int64_t(r) * cols + c;
+            const float hv = load_as_f32(h, i, h_t);
+            const float g = load_as_f32(dh, i, dh_t);
+            const float z = hv > 0.f ? g : g * (hv + 1.f);
+            store_from_f32(dz, i, dz_t, z);
+            s += dz_t ? bf16_to_f32(f32_to_bf16(z)) : z;  // bias grad from the stored (GEMM-visible) dz
+        }
+        partials[int64_t(blockIdx.x) * cols + c] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------ clip + Adam
+
+constexpr int kNormBlocks = 256;
+constexpr int kAdamThreads = 256;
+
+__global__ void __launch_bounds__(256) k_sqnorm(const float* __restrict__ g, int64_t n, float* __restrict__ partials) {
+    __shared__ float red[256 / kWave];
+    float s = 0.f;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+        s += g[i] * g[i];
+    s = wave_sum(s);
+    if (threadIdx.x % kWave == 0) red[threadIdx.x / kWave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int w = 0; w < 256 / kWave; ++w) t += red[w];
+        partials[blockIdx.x] = t;
+    }
+}
+
+struct SegTable {
+    ppo_seg_t s[PPO_MAX_SEG];
+    int n;
+};
+
+__global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                       const float* __restrict__ np, int nnp, float max_norm,
+                                                       const double* __restrict__ lr_p, const double* __restrict__ step_p,
+                                                       float b1, float b2, float eps, SegTable segs,
+                                                       uint16_t* __restrict__ mirror) {
+    __shared__ float red[kAdamThreads / kWave];
+    __shared__ float coef_s;
+    float s = 0.f;
+    for (int k = threadIdx.x; k < nnp; k += kAdamThreads) s += np[k];
+    s = wave_sum(s);
+    if (threadIdx.x % kWave == 0) red[threadIdx.x / kWave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int w = 0; w < kAdamThreads / kWave; ++w) t += red[w];
+        // torch.nn.utils.clip_grad_norm_: coef = max_norm / (total_norm + 1e-6), clamped to 1
+        coef_s = max_norm > 0.f ? fminf(max_norm / (sqrtf(t) + 1e-6f), 1.f) : 1.f;
+    }
+    __syncthreads();
+    const float coef = coef_s;
+    const double t = *step_p + 1.0;
+    const double bc1 = 1.0 - pow(double(b1), t);
+    const double bc2 = 1.0 - pow(double(b2), t);
+    const float step_size = float(*lr_p / bc1);
+    const float bc2_sqrt = float(sqrt(bc2));
+    const int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x;
+    if (i >= n) return;
+    const float gi = g[i] * coef;
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    const float pi = p[i] - step_size * (mi / denom);
+    p[i] = pi;
+    if (mirror) {
+        for (int k = 0; k < segs.n; ++k) {
+            const ppo_seg_t& sg = segs.s[k];
+            if (i >= sg.off && i < sg.off + sg.len) {
+                const int64_t j = i - sg.off;
+                mirror[sg.moff + (j / sg.cols) * sg.mstride + (j % sg.cols)] = f32_to_bf16(pi);
+            }
+        }
+    }
+}
+
+__global__ void k_tail(double* lr, const float* kl, float thr, double min_lr, double max_lr, double* step,
+                       int32_t* mb_idx, int nmb, int32_t* stat_idx) {
+    if (threadIdx.x != 0) return;
+    if (thr > 0.f) {
+        const double k = double(*kl);
+        double cur = *lr, nxt = cur;
+        if (k > 2.0 * double(thr)) nxt = fmax(cur / 1.5, min_lr);
+        if (k < 0.5 * double(thr)) nxt = fmin(cur * 1.5, max_lr);
+        *lr = nxt;
+    }
+    *step += 1.0;
+    *mb_idx = (*mb_idx + 1) % nmb;
+    *stat_idx += 1;
+}
+
+inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+
+}  // namespace
+
+extern "C" {
+
+int ppo_abi_version(void) { return PPO_ABI_VERSION; }
+const char* ppo_last_error(void) { return g_err; }
+
+int ppo_obs_stats_blocks(int32_t mb_rows) { return (mb_rows + kStatRows - 1) / kStatRows; }
+
+int ppo_obs_stats(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_t cols, double* partials,
+                  void* stream) {
+    if (cols <= 0 || cols > 64 || mb_rows < 2) return fail(-1, "ppo_obs_stats: need 1 <= cols <= 64, mb_rows >= 2");
+    hipLaunchKernelGGL(k_obs_stats, dim3(ppo_obs_stats_blocks(mb_rows)), dim3(64), 0, S(stream), x, mb_idx, mb_rows,
+                       cols, partials);
+    return launched("k_obs_stats");
+}
+
+int ppo_obs_stats_update(const double* partials, int32_t nblk, int32_t cols, int32_t mb_rows, double* running_mean,
+                         double* running_var, double* count, void* stream) {
+    if (cols <= 0 || cols > 64) return fail(-1, "ppo_obs_stats_update: cols must be in [1, 64]");
+    hipLaunchKernelGGL(k_obs_stats_update, dim3(1), dim3(64), 0, S(stream), partials, nblk, cols, mb_rows, running_mean,
+                       running_var, count);
+    return launched("k_obs_stats_update");
+}
+
+int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_t cols, const double* running_mean,
+                      const double* running_var, float eps, void* out, int32_t out_stride, int32_t out_bf16,
+                      void* stream) {
+    if (out_stride < cols) return fail(-1, "ppo_obs_normalize: out_stride < cols");
+    const int64_t n = int64_t(mb_rows) * out_stride;
+    hipLaunchKernelGGL(k_obs_normalize, dim3(unsigned((n + 255) / 256)), dim3(256), 0, S(stream), x, mb_idx, mb_rows,
+                       cols, running_mean, running_var, eps, out, out_stride, out_bf16);
+    return launched("k_obs_normalize");
+}
+
+int ppo_loss_blocks(int32_t mb_rows) { return (mb_rows + kLossThreads - 1) / kLossThreads; }
+
+int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
+                  const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
+                  const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
+                  float* dhead, float* partials, void* stream) {
+    const dim3 grid(ppo_loss_blocks(mb_rows)), block(kLossThreads);
+#define PPO_LOSS_CASE(AA)                                                                                        \
+    case AA:                                                                                                     \
+        hipLaunchKernelGGL(k_loss_grad<AA>, grid, block, 0, S(stream), head, logstd, mb_rows, mb_idx, actions, \
+                           ds_mu, ds_sigma, old_neglogp, advantages, old_values, returns, cfg, dhead, partials); \
+        break;
+    switch (A) {
+        PPO_LOSS_CASE(2)
+        PPO_LOSS_CASE(12)
+        PPO_LOSS_CASE(21)
+        default:
+            return fail(-1, "ppo_loss_grad: action dims 2, 12 and 21 are instantiated");
+    }
+#undef PPO_LOSS_CASE
+    return launched("k_loss_grad");
+}
+
+int ppo_loss_finalize(const float* partials, int32_t nblk, int32_t A, int32_t mb_rows, float entropy_coef,
+                      float* grad_head_bias, float* grad_logstd, float* stats, const int32_t* stat_idx, float* kl_out,
+                      void* stream) {
+    if (A <= 0 || A > PPO_MAX_ACT) return fail(-1, "ppo_loss_finalize: bad action dim");
+    hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(128), 0, S(stream), partials, nblk, A, mb_rows, entropy_coef,
+                       grad_head_bias, grad_logstd, stats, stat_idx, kl_out);
+    return launched("k_loss_finalize");
+}
+
+int ppo_elu_bwd_blocks(int32_t rows) { return (rows + kEluRows - 1) / kEluRows; }
+
+int ppo_elu_bwd(const void* dh, int32_t dh_dtype, const void* h, int32_t h_dtype, void* dz, int32_t dz_dtype,
+                int32_t rows, int32_t cols, float* partials, void* stream) {
+    if (cols % 64) return fail(-1, "ppo_elu_bwd: cols must be a multiple of 64");
+    hipLaunchKernelGGL(k_elu_bwd, dim3(ppo_elu_bwd_blocks(rows)), dim3(cols < 256 ? cols : 256), 0, S(stream), dh,
+                       dh_dtype, h, h_dtype, dz, dz_dtype, rows, cols, partials);
+    return launched("k_elu_bwd");
+}
+
+int ppo_sqnorm_blocks(void) { return kNormBlocks; }
+
+int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream) {
+    hipLaunchKernelGGL(k_sqnorm, dim3(kNormBlocks), dim3(256), 0, S(stream), g, n, partials);
+    return launched("k_sqnorm");
+}
+
+int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials, int32_t nblk_norm,
+             float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,
+             const ppo_seg_t* segs_host, int32_t nseg, void* mirror_bf16, void* stream) {
+    if (nseg < 0 || nseg > PPO_MAX_SEG) return fail(-1, "ppo_adam: too many mirror segments");
+    SegTable t{};
+    t.n = mirror_bf16 ? nseg : 0;
+    for (int k = 0; k < t.n; ++k) {
+        t.s[k] = segs_host[k];
+        if (t.s[k].cols <= 0 || t.s[k].mstride < t.s[k].cols) return fail(-1, "ppo_adam: bad segment");
+    }
+    hipLaunchKernelGGL(k_adam, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0, S(stream),
+                       p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
+                       static_cast<uint16_t*>(mirror_bf16));
+    return launched("k_adam");
+}
+
+int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,
+             int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, void* stream) {
+    if (n_minibatches <= 0) return fail(-1, "ppo_tail: n_minibatches must be positive");
+    hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, S(stream), lr, kl, kl_threshold, min_lr, max_lr, step, mb_idx,
+                       n_minibatches, stat_idx);
+    return launched("k_tail");
+}
+
+}  // extern "C"

@@ -1,0 +1,331 @@
+"""The PPO minibatch step as two HIP graphs (MI355X-first replacement of rl_games' autograd step).
+
+rl_games 1.6.1 (``a2c_continuous.py::calc_gradients`` + ``trancate_gradients_and_step`` +
+``a2c_common.py::train_epoch``) runs, per minibatch, an autograd forward/backward of
+``ModelA2CContinuousLogStd`` under autocast, the PPO losses, ``clip_grad_norm_``, Adam, then the
+adaptive LR from the KL -- ~300 kernel launches and several host round trips per minibatch.  Here
+the same maths is an explicit forward / backward:
+
+* trunk (59 -> 256 x 5, ELU) in bf16 on hipBLASLt: ``addmm`` forward, ``dz @ W`` for the input
+  gradients, and the weight gradients as a **split-K** batched GEMM (``bmm`` over S row chunks,
+  fp32 out, summed) -- the library's single ``dz^T h`` with K = 32768 and a 256 x 256 output runs on 16
+  workgroups (measured 113 us vs 29 us split, scripts/mlp_microbench.py);
+* heads (mu | value, 22 x 256) and everything after them in fp32;
+* ``libppo_hip.so`` (include/ppo.h) for the rest: obs normaliser update + normalise, the fused
+  loss / KL / head-gradient kernel, ELU backward with bias-gradient partials, clip + Adam over the flat
+  buffer (writing the bf16 trunk mirror), adaptive LR and the device minibatch counter;
+* graph A = forward + losses + backward (gradients and the KL land in the flat [grads | kl] bucket),
+  graph B = clip + Adam + LR; in multi-GPU ``allreduce`` mode the RCCL all-reduce of the bucket runs
+  between them.  Minibatch rows are addressed through a device counter, so one graph serves every
+  minibatch; two variants of A exist (obs normaliser updating: first mini-epoch; frozen: the rest).
+
+``compute_dtype=torch.float32`` runs the same schedule in fp32 (tests compare it with autograd).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+import torch.nn.functional as F
+
+from .._native import PPO_LIB_PATH, NativeError
+
+_LIB = None
+PPO_ABI_VERSION = 1
+PPO_LOSS_NSTAT = 5
+
+
+class PpoLossCfg(C.Structure):
+    _fields_ = [("e_clip", C.c_float), ("critic_coef", C.c_float), ("entropy_coef", C.c_float),
+                ("bounds_coef", C.c_float), ("soft_bound", C.c_float), ("ppo", C.c_int32),
+                ("clip_value", C.c_int32), ("bound_loss", C.c_int32)]
+
+
+class PpoSeg(C.Structure):
+    _fields_ = [("off", C.c_int64), ("len", C.c_int64), ("moff", C.c_int64), ("cols", C.c_int32),
+                ("mstride", C.c_int32)]
+
+
+EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks", "ppo_obs_stats",
+                    "ppo_obs_stats_update", "ppo_obs_normalize", "ppo_loss_blocks", "ppo_loss_grad",
+                    "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
+                    "ppo_adam", "ppo_tail"]
+
+
+def load() -> C.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = os.environ.get("PPO_HIP_LIB", PPO_LIB_PATH)
+    if not os.path.exists(path):
+        raise NativeError(f"{path} not found: the PPO HIP kernels are not built "
+                          f"(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    L = C.CDLL(path)
+    V, I32, I64, F32, F64 = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double
+    L.ppo_obs_stats.argtypes = [V, V, I32, I32, V, V]
+    L.ppo_obs_stats_update.argtypes = [V, I32, I32, I32, V, V, V, V]
+    L.ppo_obs_normalize.argtypes = [V, V, I32, I32, V, V, F32, V, I32, I32, V]
+    L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V]
+    L.ppo_loss_finalize.argtypes = [V, I32, I32, I32, F32, V, V, V, V, V, V]
+    L.ppo_elu_bwd.argtypes = [V, I32, V, I32, V, I32, I32, I32, V, V]
+    L.ppo_sqnorm.argtypes = [V, I64, V, V]
+    L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, V]
+    L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V]
+    for f in ("ppo_obs_stats_blocks", "ppo_loss_blocks", "ppo_elu_bwd_blocks"):
+        getattr(L, f).argtypes = [I32]
+    L.ppo_last_error.restype = C.c_char_p
+    if L.ppo_abi_version() != PPO_ABI_VERSION:
+        raise NativeError(f"libppo_hip ABI {L.ppo_abi_version()} != {PPO_ABI_VERSION}")
+    _LIB = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise NativeError(f"{what} failed ({rc}): {load().ppo_last_error().decode(errors='replace')}")
+
+
+def _p(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _split(rows: int) -> int:
+    """Split-K factor for the weight-gradient GEMMs: row chunks of >= 512, at most 32 chunks."""
+    s = 1
+    while s < 32 and rows % (2 * s) == 0 and rows // (2 * s) >= 512:
+        s *= 2
+    return s
+
+
+class FusedPPOUpdate:
+    """Owns the static buffers and the two graphs of one agent's minibatch step."""
+
+    def __init__(self, agent, compute_dtype: torch.dtype = torch.bfloat16, use_graphs: bool = True):
+        self.L = load()
+        self.agent = agent
+        self.dev = agent.device
+        if self.dev.type != "cuda":
+            raise NativeError("the fused PPO update runs on the HIP device only")
+        model = agent.model
+        net = model.a2c_network
+        self.linears = [m for m in net.actor_mlp if isinstance(m, torch.nn.Linear)]
+        if not all(isinstance(m, (torch.nn.Linear, torch.nn.ELU)) for m in net.actor_mlp):
+            raise NotImplementedError("the fused update implements the ELU trunk of the Allsteps agent")
+        self.net, self.model = net, model
+        self.A = agent.actions_num
+        self.obs_dim = agent.obs_shape[0]
+        self.mb = agent.dataset.minibatch_size
+        self.n_mb = len(agent.dataset)
+        self.dt = compute_dtype
+        self.bf16 = compute_dtype == torch.bfloat16
+        self.k0 = (self.obs_dim + 7) // 8 * 8 if self.bf16 else self.obs_dim  # 16-B aligned bf16 rows
+        self.use_graphs = use_graphs
+        flat = agent.flat
+        self.flat = flat
+        B, dev, dt = self.mb, self.dev, self.dt
+        widths = [self.k0] + [m.out_features for m in self.linears]
+        self.h = [torch.zeros(B, w, device=dev, dtype=dt) for w in widths]
+        self.h_last_f = torch.empty(B, widths[-1], device=dev) if self.bf16 else self.h[-1]
+        self.head = torch.empty(B, self.A + 1, device=dev)
+        self.dhead = torch.empty(B, self.A + 1, device=dev)
+        wmax = max(widths[1:])
+        self.dz = torch.empty(B, wmax, device=dev, dtype=dt)
+        self.dh = torch.empty(B, wmax, device=dev, dtype=dt)
+        self.dh_last = torch.empty(B, widths[-1], device=dev)  # fp32 from the heads
+        self.S = _split(B)
+        L = self.L
+        self.loss_partials = torch.empty(L.ppo_loss_blocks(B), 2 * self.A + 1 + PPO_LOSS_NSTAT, device=dev)
+        self.elu_partials = torch.empty(L.ppo_elu_bwd_blocks(B), wmax, device=dev)
+        self.stat_partials = torch.empty(L.ppo_obs_stats_blocks(B) * 2 * 64, device=dev, dtype=torch.float64)
+        self.norm_partials = torch.empty(L.ppo_sqnorm_blocks(), device=dev)
+        self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.stat_idx = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.stats = torch.zeros(agent.mini_epochs_num * self.n_mb + 1, PPO_LOSS_NSTAT, device=dev)
+        # grads of the trunk / heads as views of the flat bucket
+        g = flat.grads
+        self.gW, self.gb = [], []
+        for m in self.linears:
+            o = flat.offset(m.weight)
+            self.gW.append(g[o:o + m.weight.numel()].view_as(m.weight))
+            o = flat.offset(m.bias)
+            self.gb.append(g[o:o + m.bias.numel()])
+        o = flat.offset(net.mu.weight)
+        self.Wh = flat.params[o:o + (self.A + 1) * widths[-1]].view(self.A + 1, widths[-1])  # [mu.w | value.w]
+        self.gWh = g[o:o + (self.A + 1) * widths[-1]].view(self.A + 1, widths[-1])
+        o = flat.offset(net.mu.bias)
+        self.bh = flat.params[o:o + self.A + 1]
+        self.gbh = g[o:o + self.A + 1]
+        o = flat.offset(net.sigma)
+        self.logstd = flat.params[o:o + self.A]
+        self.gls = g[o:o + self.A]
+        if net.value.weight.data_ptr() != self.Wh[self.A].data_ptr() or \
+                net.value.bias.data_ptr() != self.bh[self.A:].data_ptr():
+            raise RuntimeError("flat layout: value head must follow the mu head (fused_param_order)")
+        # bf16 trunk mirror (row-padded first layer), written by the Adam kernel
+        segs, moff = [], 0
+        self.W_lp, self.b_lp = [], []
+        if self.bf16:
+            sizes = [m.out_features * (self.k0 if i == 0 else m.in_features) + m.out_features
+                     for i, m in enumerate(self.linears)]
+            self.mirror = torch.zeros(sum(sizes), device=dev, dtype=torch.bfloat16)
+            for i, m in enumerate(self.linears):
+                kin = self.k0 if i == 0 else m.in_features
+                segs.append(PpoSeg(flat.offset(m.weight), m.weight.numel(), moff, m.in_features, kin))
+                self.W_lp.append(self.mirror[moff:moff + m.out_features * kin].view(m.out_features, kin))
+                moff += m.out_features * kin
+                segs.append(PpoSeg(flat.offset(m.bias), m.out_features, moff, m.out_features, m.out_features))
+                self.b_lp.append(self.mirror[moff:moff + m.out_features])
+                moff += m.out_features
+            self.refresh_mirror()
+        else:
+            self.mirror = None
+            self.W_lp = [m.weight.detach() for m in self.linears]
+            self.b_lp = [m.bias.detach() for m in self.linears]
+        self.segs = (PpoSeg * max(len(segs), 1))(*segs)
+        self.nseg = len(segs)
+        c = agent.config
+        blt = agent.bound_loss_type if agent.bounds_loss_coef is not None else None
+        self.loss_cfg = PpoLossCfg(agent.e_clip, agent.critic_coef, agent.entropy_coef,
+                                   float(agent.bounds_loss_coef or 0.0), 1.1, int(agent.ppo), int(agent.clip_value),
+                                   {"bound": 1, "regularisation": 2}.get(blt, 0))
+        sch = agent.scheduler
+        self.kl_thr = float(getattr(sch, "kl_threshold", 0.0))
+        self.min_lr, self.max_lr = float(getattr(sch, "min_lr", 1e-6)), float(getattr(sch, "max_lr", 1e-2))
+        self.legacy = agent.schedule_type == "legacy"
+        self.rms = model.running_mean_std
+        if self.rms is None:
+            raise NotImplementedError("the fused update expects normalize_input")
+        self.graphs: dict = {}
+        self.ds: dict | None = None
+        del c
+
+    # ------------------------------------------------------------------ helpers
+    def refresh_mirror(self) -> None:
+        """Rewrite the bf16 trunk mirror from the fp32 parameters (after restore / broadcast)."""
+        if self.mirror is None:
+            return
+        with torch.no_grad():
+            for i, m in enumerate(self.linears):
+                self.W_lp[i][:, :m.in_features].copy_(m.weight)
+                self.b_lp[i].copy_(m.bias)
+
+    def set_dataset(self, ds: dict) -> None:
+        """Bind the (static) dataset tensors; graphs are (re)captured when the pointers change."""
+        need = ("obs", "actions", "mu", "sigma", "old_logp_actions", "advantages", "old_values", "returns")
+        for k in need:
+            if not ds[k].is_contiguous():
+                raise ValueError(f"dataset tensor {k} must be contiguous")
+        key = tuple(ds[k].data_ptr() for k in need)
+        if self.ds is None or key != self._ds_key:
+            self.graphs.clear()
+        self.ds, self._ds_key = ds, key
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    # ------------------------------------------------------------------ the two halves
+    @torch.no_grad()
+    def _forward_backward(self, rms_train: bool) -> None:
+        L, s, ds, B, A = self.L, self._stream(), self.ds, self.mb, self.A
+        rms = self.rms
+        if rms_train:
+            _check(L.ppo_obs_stats(_p(ds["obs"]), _p(self.mb_idx), B, self.obs_dim, _p(self.stat_partials), s),
+                   "ppo_obs_stats")
+            _check(L.ppo_obs_stats_update(_p(self.stat_partials), L.ppo_obs_stats_blocks(B), self.obs_dim, B,
+                                          _p(rms.running_mean), _p(rms.running_var), _p(rms.count), s),
+                   "ppo_obs_stats_update")
+        _check(L.ppo_obs_normalize(_p(ds["obs"]), _p(self.mb_idx), B, self.obs_dim, _p(rms.running_mean),
+                                   _p(rms.running_var), rms.epsilon, _p(self.h[0]), self.k0, int(self.bf16), s),
+               "ppo_obs_normalize")
+        nl = len(self.linears)
+        for i in range(nl):  # z = h W^T + b ; h' = elu(z)
+            out = self.h[i + 1]
+            torch.addmm(self.b_lp[i], self.h[i], self.W_lp[i].t(), out=out)
+            F.elu(out, inplace=True)
+        if self.bf16:
+            self.h_last_f.copy_(self.h[-1])
+        torch.addmm(self.bh, self.h_last_f, self.Wh.t(), out=self.head)
+        self.flat.zero_grad()
+        _check(L.ppo_loss_grad(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
+                               _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
+                               _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.dhead),
+                               _p(self.loss_partials), s), "ppo_loss_grad")
+        _check(L.ppo_loss_finalize(_p(self.loss_partials), self.loss_partials.shape[0], A, B,
+                                   self.loss_cfg.entropy_coef, _p(self.gbh), _p(self.gls), _p(self.stats),
+                                   _p(self.stat_idx), _p(self.flat.extra), s), "ppo_loss_finalize")
+        S = self.S
+        hl = self.h_last_f
+        # heads: dWh = dhead^T h (split-K), dh_last = dhead Wh
+        torch.sum(torch.bmm(self.dhead.view(S, B // S, A + 1).transpose(1, 2), hl.view(S, B // S, hl.shape[1])),
+                  0, out=self.gWh)
+        torch.mm(self.dhead, self.Wh, out=self.dh_last)
+        dh, dh_t = self.dh_last, 0
+        dt_code = int(self.bf16)
+        for i in reversed(range(nl)):
+            m = self.linears[i]
+            n_out = m.out_features
+            dz = self.dz[:, :n_out]
+            # dz_i = elu'(h_{i+1}) * dh_{i+1}; bias grad from the per-block column sums
+            _check(L.ppo_elu_bwd(_p(dh), dh_t, _p(self.h[i + 1]), dt_code, _p(dz), dt_code, B, n_out,
+                                 _p(self.elu_partials), s), "ppo_elu_bwd")
+            torch.sum(self.elu_partials[:, :n_out], 0, out=self.gb[i])
+            hin = self.h[i]
+            kin = hin.shape[1]
+            gw = torch.bmm(dz.view(S, B // S, n_out).transpose(1, 2), hin.view(S, B // S, kin),
+                           out_dtype=torch.float32) if self.bf16 else \
+                torch.bmm(dz.view(S, B // S, n_out).transpose(1, 2), hin.view(S, B // S, kin))
+            if kin == m.in_features:
+                torch.sum(gw, 0, out=self.gW[i])
+            else:
+                self.gW[i].copy_(gw.sum(0)[:, :m.in_features])
+            if i > 0:
+                dhi = self.dh[:, :kin]
+                torch.mm(dz, self.W_lp[i], out=dhi)
+                dh, dh_t = dhi, dt_code
+
+    @torch.no_grad()
+    def _optimizer_step(self) -> None:
+        L, s, ag, fl = self.L, self._stream(), self.agent, self.flat
+        n = fl.numel
+        _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.norm_partials), s), "ppo_sqnorm")
+        opt = ag.optimizer
+        _check(L.ppo_adam(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
+                          _p(self.norm_partials), self.norm_partials.numel(),
+                          ag.grad_norm if ag.truncate_grads else 0.0, _p(ag.lr), _p(opt.step_t), opt.beta1, opt.beta2,
+                          opt.eps, self.segs, self.nseg, _p(self.mirror), s), "ppo_adam")
+        _check(L.ppo_tail(_p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr, self.max_lr,
+                          _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), s), "ppo_tail")
+
+    # ------------------------------------------------------------------ graphs
+    def _run(self, key, fn) -> None:
+        """First call of a variant: run eagerly (real work; warms up hipBLASLt handles / workspaces and
+        the allocator).  Second call: capture the graph (capture does not execute), then replay."""
+        g = self.graphs.get(key)
+        if g is None:
+            fn()
+            self.graphs[key] = "warm"
+            return
+        if g == "warm":
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            self.graphs[key] = g
+        g.replay()
+
+    def begin_epoch(self) -> None:
+        self.mb_idx.zero_()
+        self.stat_idx.zero_()
+
+    def step_a(self, rms_train: bool) -> None:
+        if self.use_graphs:
+            self._run(("a", rms_train), lambda: self._forward_backward(rms_train))
+        else:
+            self._forward_backward(rms_train)
+
+    def step_b(self) -> None:
+        if self.use_graphs:
+            self._run(("b",), self._optimizer_step)
+        else:
+            self._optimizer_step()

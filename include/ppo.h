@@ -1,0 +1,110 @@
+/*
+ * ppo.h -- C ABI of the MI355X PPO-update kernels (libppo_hip.so) used by the rl_games-semantics
+ * trainer (allsteps_isaaclab_amd/learning/fused.py).
+ *
+ * The reference trains with rl_games 1.6.1 (third-party, absent offline): every minibatch it runs
+ * autograd over ModelA2CContinuousLogStd + the PPO losses (a2c_continuous.py calc_gradients), clips
+ * the gradient norm and steps torch.optim.Adam, then adapts the learning rate from the KL
+ * (a2c_common.py train_epoch, schedule_type 'legacy').  These kernels are the non-GEMM half of that
+ * minibatch step, written for a HIP-graph replay with NO host round trip:
+ *   ppo_obs_stats / ppo_obs_stats_update  RunningMeanStd train-mode update (running_mean_std.py)
+ *   ppo_obs_normalize                     (x - mean) / sqrt(var + eps), clamp +-5 -> trunk input
+ *   ppo_loss_grad / ppo_loss_finalize     actor (clipped ratio) + critic (clipped value) + bound +
+ *                                         entropy losses, KL(policy_kl), and their analytic
+ *                                         gradients w.r.t. the heads (mu, value) and log-sigma;
+ *                                         writes mu / sigma back into the dataset (update_mu_sigma)
+ *   ppo_elu_bwd                           ELU backward (output form) + per-block bias-grad partials
+ *   ppo_sqnorm / ppo_adam                 clip_grad_norm_ + Adam over the flat parameter buffer, and
+ *                                         the bf16 mirror of the trunk weights for the next forward
+ *   ppo_tail                              adaptive LR from the (rank-averaged) KL; minibatch counter
+ * The trunk GEMMs stay on hipBLASLt (torch.mm / addmm / split-K bmm).
+ *
+ * Minibatch rows are selected on the device: row r of minibatch i is dataset row i*mb_rows + r with i
+ * read from `mb_idx` (int32, device), so one captured graph serves every minibatch.
+ * All pointers are DEVICE pointers; `stream` is a hipStream_t.  Every function returns 0 or a
+ * negative error code (ppo_last_error()).
+ */
+#ifndef PPO_H
+#define PPO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPO_ABI_VERSION 1
+#define PPO_MAX_ACT 32
+#define PPO_MAX_SEG 16
+#define PPO_LOSS_NSTAT 5 /* a_loss, c_loss, b_loss, entropy, kl */
+
+typedef struct {
+    float e_clip, critic_coef, entropy_coef, bounds_coef, soft_bound;
+    int32_t ppo, clip_value, bound_loss; /* bound_loss: 0 none, 1 'bound', 2 'regularisation' */
+} ppo_loss_cfg_t;
+
+/* one contiguous run of the flat parameter buffer that has a low-precision mirror (trunk layers):
+ * flat[off + r*cols + c] -> mirror[moff + r*mstride + c]  (mstride >= cols; the pad stays zero) */
+typedef struct {
+    int64_t off, len, moff;
+    int32_t cols, mstride;
+} ppo_seg_t;
+
+int ppo_abi_version(void);
+const char* ppo_last_error(void);
+
+/* column sum / sum of squares (fp64) of rows [i*mb_rows, (i+1)*mb_rows) of x (row stride `cols`),
+ * one partial per block into partials[nblk][2][64]; nblk = ppo_obs_stats_blocks(mb_rows). */
+int ppo_obs_stats_blocks(int32_t mb_rows);
+int ppo_obs_stats(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_t cols, double* partials,
+                  void* stream);
+/* fold the partials into running_mean / running_var / count (fp64, rl_games formula, unbiased batch var) */
+int ppo_obs_stats_update(const double* partials, int32_t nblk, int32_t cols, int32_t mb_rows, double* running_mean,
+                         double* running_var, double* count, void* stream);
+/* out[r][c] = clamp((x[row][c] - mean[c]) / sqrt(var[c] + eps), -5, 5) for c < cols, 0 for cols <= c < out_stride;
+ * out_bf16 selects bf16 (else fp32) output */
+int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_t cols, const double* running_mean,
+                      const double* running_var, float eps, void* out, int32_t out_stride, int32_t out_bf16,
+                      void* stream);
+
+/* Per-row PPO losses and head gradients.  head = [mu(0..A-1) | value(A)] (mb_rows x (A+1), fp32);
+ * logstd (A); dataset rows (selected by mb_idx): actions / mu / sigma (A each), old_neglogp,
+ * advantages, old_values, returns (1 each).  Writes dhead (mb_rows x (A+1)) = d loss / d head,
+ * new mu / sigma into the dataset rows, and per-block partials[nblk][2A+1+PPO_LOSS_NSTAT]
+ * (sum over rows of dhead columns, d loss / d logstd, the five statistics); nblk = ppo_loss_blocks(). */
+int ppo_loss_blocks(int32_t mb_rows);
+int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
+                  const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
+                  const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
+                  float* dhead, float* partials, void* stream);
+/* sum the partials: bias grads of the heads -> grad_head_bias (A+1), logstd grads (+ -entropy_coef) ->
+ * grad_logstd (A); the statistics (means) -> stats[stat_idx][PPO_LOSS_NSTAT] (stat_idx from device);
+ * the KL also -> kl_out (the slot that rides in the gradient all-reduce) */
+int ppo_loss_finalize(const float* partials, int32_t nblk, int32_t A, int32_t mb_rows, float entropy_coef,
+                      float* grad_head_bias, float* grad_logstd, float* stats, const int32_t* stat_idx, float* kl_out,
+                      void* stream);
+
+/* dz = dh * (h > 0 ? 1 : h + 1) (ELU alpha 1, output form), rows x cols (cols multiple of 64);
+ * dtype of dh / h / dz: 0 fp32, 1 bf16 (dh_dtype, h_dtype, dz_dtype); per-block column partial sums
+ * of dz into partials[nblk][cols] (nblk = ppo_elu_bwd_blocks(rows)) */
+int ppo_elu_bwd_blocks(int32_t rows);
+int ppo_elu_bwd(const void* dh, int32_t dh_dtype, const void* h, int32_t h_dtype, void* dz, int32_t dz_dtype,
+                int32_t rows, int32_t cols, float* partials, void* stream);
+
+/* ||g||^2 partials (fp32, nblk = ppo_sqnorm_blocks()) */
+int ppo_sqnorm_blocks(void);
+int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream);
+/* clip (max_norm > 0: g *= min(1, max_norm / (||g|| + 1e-6))) + Adam (torch.optim.Adam, amsgrad off,
+ * weight_decay 0) with device lr / step (fp64); writes the bf16 mirror of the listed segments */
+int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials, int32_t nblk_norm,
+             float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,
+             const ppo_seg_t* segs_host, int32_t nseg, void* mirror_bf16, void* stream);
+/* adaptive LR (rl_games AdaptiveScheduler; kl_threshold <= 0: identity) from kl (device fp32), then
+ * step += 1 (Adam's count; ppo_adam used step + 1), mb_idx = (mb_idx + 1) % n_minibatches, stat_idx += 1 */
+int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,
+             int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

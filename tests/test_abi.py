@@ -104,3 +104,38 @@ def test_null_arguments_return_error():
     assert b"null" in L.as_last_error()
     h = C.c_void_p()
     assert L.as_create(0, None, None, None, None, 0, 0, 0, C.byref(h)) == -1
+
+
+# ---------------------------------------------------------------- libppo_hip.so (include/ppo.h)
+
+PPO_HEADER = os.path.join(ROOT, "include", "ppo.h")
+
+
+def test_ppo_library_exports_every_declared_symbol():
+    from allsteps_isaaclab_amd.learning import fused
+
+    src = open(PPO_HEADER).read()
+    declared = sorted(set(re.findall(r"^(?:int|const char\*)\s+(ppo_\w+)\(", src, re.M)))
+    assert len(declared) >= 14
+    L = fused.load()
+    for fn in declared:
+        assert hasattr(L, fn), f"{fn} declared in ppo.h but not exported"
+    assert set(fused.EXPORTED_SYMBOLS) == set(declared)
+    assert L.ppo_abi_version() == fused.PPO_ABI_VERSION
+    # block-count helpers are pure host functions
+    assert L.ppo_loss_blocks(32768) == 128 and L.ppo_elu_bwd_blocks(32768) == 512
+
+
+@pytest.mark.parametrize("cname,pyname", [("ppo_loss_cfg_t", "PpoLossCfg"), ("ppo_seg_t", "PpoSeg")])
+def test_ppo_structs_match_header(cname, pyname):
+    from allsteps_isaaclab_amd.learning import fused
+
+    src = open(PPO_HEADER).read()
+    m = re.search(r"typedef struct \{([^{}]*)\}\s*" + cname + ";", src, re.S)
+    body = re.sub(r"/\*.*?\*/", "", m.group(1), flags=re.S)
+    names = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if decl:
+            names += [p.strip().split()[-1] for p in decl.split(",")]
+    assert [f[0] for f in getattr(fused, pyname)._fields_] == names

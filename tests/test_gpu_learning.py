@@ -1,0 +1,198 @@
+"""PPO trainer on the HIP env: the reference's train.py flow end to end on
+cuda:0 -- registry -> AllstepsEnv (native) -> RlGamesVecEnvWrapper -> Runner -> A2CAgentSymmetry."""
+
+import math
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_train_script_runs_on_allsteps(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "scripts", "reinforcement_learning", "rl_games"))
+    import train
+
+    runner, _ = train.main(["--task", "Allsteps-v0", "--headless", "--num_envs", "1024", "--max_iterations", "3",
+                            "--seed", "3", "--log_root", str(tmp_path)])
+    agent = runner.agent
+    st = agent.last_stats
+    assert agent.epoch_num == 3 and agent.frame == 3 * 1024 * 32
+    for k in ("a_loss", "c_loss", "kl", "entropy", "lr"):
+        assert math.isfinite(st[k]), (k, st)
+    assert torch.isfinite(agent.flat.params).all()
+    # the native env really ran: the step counters advanced and observations are not all zero
+    assert agent.tensor_dict["obses"].abs().sum() > 0
+    nn_dir = os.path.join(agent.experiment_dir, "nn")
+    assert any(f.endswith(".pth") for f in os.listdir(nn_dir))
+
+
+@pytest.mark.gpu
+def test_symmetry_agent_doubles_batch(tmp_path):
+    from allsteps_isaaclab_amd import registry
+    from allsteps_isaaclab_amd.learning.a2c_ppo_mirroring import A2CAgentSymmetry
+    from allsteps_isaaclab_amd.rl_games import RlGamesGpuEnv, RlGamesVecEnvWrapper, env_configurations, vecenv
+
+    cfg = registry.load_cfg_from_registry("Allsteps-v0", "env_cfg_entry_point")
+    cfg.scene.num_envs = 256
+    env = RlGamesVecEnvWrapper(registry.make("Allsteps-v0", cfg=cfg), "cuda:0", math.inf, 1.0)
+    vecenv.register("IsaacRlgWrapper", lambda n, a, **kw: RlGamesGpuEnv(n, a, **kw))
+    env_configurations.register("rlgpu", {"vecenv_type": "IsaacRlgWrapper", "env_creator": lambda **kw: env})
+    params = registry.load_cfg_from_registry("Allsteps-v0", "rl_games_cfg_entry_point")["params"]
+    params["config"].update(num_actors=256, symmetry=True, minibatch_size=4096, max_epochs=1,
+                            train_dir=str(tmp_path), print_stats=False)
+    agent = A2CAgentSymmetry("run", params)
+    agent.init_tensors()
+    agent.obs = agent.env_reset()
+    batch = agent.play_steps()
+    assert batch["obses"].shape == (2 * 256 * 32, 59) and batch["actions"].shape == (2 * 256 * 32, 21)
+    h = 256 * 32
+    # mirrored half: left/right joint columns swapped
+    uw = env.unwrapped
+    r, l = uw.right_body_indices, uw.left_body_indices
+    assert torch.equal(batch["actions"][h:, r], batch["actions"][:h, l])
+    agent.model.train()
+    agent.prepare_dataset({k: v for k, v in batch.items() if k not in ("played_frames", "step_time")})
+    assert len(agent.dataset) == 2 * h // 4096
+    env.close()
+
+
+class _SpacesOnlyEnv:
+    """VecEnv stand-in with the Allsteps spaces (59 obs, 21 actions) for update-only tests."""
+
+    def __init__(self, n):
+        from allsteps_isaaclab_amd.envs.spaces import Box
+
+        self.n = n
+        self._info = {"observation_space": Box(-math.inf, math.inf, (59,)), "action_space": Box(-1.0, 1.0, (21,)),
+                      "state_space": None}
+
+    def get_env_info(self):
+        return self._info
+
+
+def _agents_and_batch(n_envs, mixed, tmp):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _toy_env import agent_params
+    from allsteps_isaaclab_amd.learning.a2c_continuous import A2CAgent
+
+    def make(fused):
+        p = agent_params(n_envs, device="cuda:0", mixed_precision=mixed, fused_update=fused, train_dir=str(tmp),
+                         minibatch_size=n_envs * 8, horizon_length=16)
+        p["network"]["mlp"]["units"] = [256, 256, 256, 256, 256]
+        p["config"]["vec_env"] = _SpacesOnlyEnv(n_envs)
+        torch.manual_seed(11)
+        a = A2CAgent("run", p)
+        a.init_tensors()
+        return a
+
+    ref, fus = make(False), make(True)
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    B = n_envs * 16
+    r = lambda *s: torch.randn(*s, device="cuda:0", generator=g)  # noqa: E731
+    batch = {"obses": r(B, 59) * 2 + 0.5, "actions": r(B, 21), "neglogpacs": r(B).abs() * 5 + 20,
+             "values": r(B, 1), "returns": r(B, 1) * 2, "mus": r(B, 21) * 0.3,
+             "sigmas": torch.exp(r(B, 21) * 0.1), "dones": torch.zeros(B, dtype=torch.uint8, device="cuda:0")}
+    for a in (ref, fus):
+        a.model.train()
+        a.prepare_dataset({k: v.clone() for k, v in batch.items()})
+    return ref, fus
+
+
+def _grads(agent):
+    return {n: p.grad.detach().clone() for n, p in agent.model.named_parameters()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fused_minibatch_step_matches_autograd_fp32(tmp_path, graphs):
+    ref, fus = _agents_and_batch(256, mixed=False, tmp=tmp_path)
+    fus.fused.use_graphs = graphs
+    ref.truncate_grads = False  # compare raw gradients (the fused clip happens inside the Adam kernel)
+    saved = ref.optimizer.step
+    ref.optimizer.step = lambda: None
+    out = ref.calc_gradients(ref.dataset[0])
+    ref.optimizer.step = saved
+    fus.fused.begin_epoch()
+    if graphs:  # first call runs eagerly (warm-up); undo its side effects, then capture + replay
+        rms = fus.model.running_mean_std
+        keep = [t.clone() for t in (rms.running_mean, rms.running_var, rms.count, fus.fused.ds["mu"],
+                                    fus.fused.ds["sigma"])]
+        fus.fused.step_a(True)
+        for t, v in zip((rms.running_mean, rms.running_var, rms.count, fus.fused.ds["mu"], fus.fused.ds["sigma"]),
+                        keep):
+            t.copy_(v)
+        fus.flat.grads.zero_()
+    fus.fused.step_a(True)
+    torch.cuda.synchronize()
+    if graphs:
+        assert isinstance(fus.fused.graphs[("a", True)], torch.cuda.CUDAGraph)
+    gr, gf = _grads(ref), _grads(fus)
+    for k in gr:
+        err = (gr[k] - gf[k]).abs().max().item()
+        scale = gr[k].abs().max().item() + 1e-8
+        assert err <= 2e-4 * scale + 1e-7, (k, err, scale)
+    # obs normaliser (train-mode update of the first mini-epoch), KL and statistics
+    for b in ("running_mean", "running_var", "count"):
+        torch.testing.assert_close(getattr(fus.model.running_mean_std, b), getattr(ref.model.running_mean_std, b),
+                                   rtol=1e-6, atol=1e-9)
+    a_loss, c_loss, entropy, kl = out[0], out[1], out[2], out[3]
+    st = fus.fused.stats[0]
+    torch.testing.assert_close(st[0], a_loss, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(st[1], c_loss, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(st[3], entropy, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(st[4], kl.reshape(()), rtol=1e-3, atol=1e-6)
+    # update_mu_sigma: the dataset rows of minibatch 0 now hold the current policy
+    torch.testing.assert_close(fus.dataset.values_dict["mu"][:fus.minibatch_size], out[4], rtol=1e-5, atol=1e-5)
+    # optimizer half: same gradients in -> same clipped Adam step out
+    for (n, pf), (_, pr) in zip(fus.model.named_parameters(), ref.model.named_parameters()):
+        pf.grad.copy_(pr.grad)
+    ref.truncate_grads = True
+    g = ref.flat.grads
+    coef = torch.clamp(ref.grad_norm / (torch.linalg.vector_norm(g) + 1e-6), max=1.0)
+    g.mul_(coef)
+    ref.optimizer.step()
+    fus.fused.step_b()
+    torch.cuda.synchronize()
+    for (n, pf), (_, pr) in zip(fus.model.named_parameters(), ref.model.named_parameters()):
+        torch.testing.assert_close(pf, pr, rtol=1e-5, atol=2e-7, msg=n)
+    assert int(fus.fused.mb_idx) == 1 % len(fus.dataset)
+
+
+@pytest.mark.gpu
+def test_fused_bf16_step_close_to_fp32_autograd(tmp_path):
+    ref, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path)
+    ref.mixed_precision = False
+    ref.truncate_grads = False
+    saved = ref.optimizer.step
+    ref.optimizer.step = lambda: None
+    ref.calc_gradients(ref.dataset[0])
+    ref.optimizer.step = saved
+    fus.fused.begin_epoch()
+    fus.fused.step_a(True)
+    torch.cuda.synchronize()
+    gr, gf = _grads(ref), _grads(fus)
+    for k in gr:
+        rel = (gr[k] - gf[k]).norm().item() / (gr[k].norm().item() + 1e-12)
+        assert rel < 3e-2, (k, rel)
+
+
+@pytest.mark.gpu
+def test_fused_train_epoch_runs_graph_replays(tmp_path):
+    ref, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path)
+    fus.obs = None
+    p0 = fus.flat.params.clone()
+    fus.model.train()
+    # one full fused epoch over the prepared dataset (mini_epochs x minibatches replays)
+    out = fus._train_epoch_fused(0.0, 0.0, 0.0)
+    stats = out[4]
+    assert all(math.isfinite(float(v)) for v in stats.values()), stats
+    assert not torch.equal(p0, fus.flat.params)
+    n = fus.mini_epochs_num * len(fus.dataset)
+    assert int(fus.fused.stat_idx) == n and int(fus.fused.mb_idx) == 0
+    assert float(fus.optimizer.step_t) == n
+    assert len(fus.fused.graphs) == 3  # A (normaliser updating), A (frozen), B
+    assert all(isinstance(g, torch.cuda.CUDAGraph) for g in fus.fused.graphs.values())
