@@ -66,23 +66,32 @@ __device__ __forceinline__ T wave_sum(T x) {
 // ------------------------------------------------------------------------------ obs normaliser
 
 constexpr int kStatRows = 256;
+constexpr int kStatPhases = 4;
 
-__global__ void __launch_bounds__(64) k_obs_stats(const float* __restrict__ x, const int32_t* __restrict__ mb_idx,
-                                                  int mb_rows, int cols, double* __restrict__ partials) {
-    const int c = threadIdx.x;
+__global__ void __launch_bounds__(64 * kStatPhases) k_obs_stats(const float* __restrict__ x,
+                                                                const int32_t* __restrict__ mb_idx, int mb_rows,
+                                                                int cols, double* __restrict__ partials) {
+    __shared__ double red[2][kStatPhases][64];
+    const int c = threadIdx.x % 64, ph = threadIdx.x / 64;
     const int64_t base = int64_t(*mb_idx) * mb_rows;
     const int r0 = blockIdx.x * kStatRows;
     const int r1 = min(r0 + kStatRows, mb_rows);
     double s = 0.0, ss = 0.0;
     if (c < cols) {
-        for (int r = r0; r < r1; ++r) {
+        for (int r = r0 + ph; r < r1; r += kStatPhases) {
             const double v = x[(base + r) * cols + c];
             s += v;
             ss += v * v;
         }
     }
-    partials[(blockIdx.x * 2 + 0) * 64 + c] = s;
-    partials[(blockIdx.x * 2 + 1) * 64 + c] = ss;
+    red[0][ph][c] = s;
+    red[1][ph][c] = ss;
+    __syncthreads();
+    if (ph < 2) {
+        double t = 0.0;
+        for (int q = 0; q < kStatPhases; ++q) t += red[ph][q][c];
+        partials[(blockIdx.x * 2 + ph) * 64 + c] = t;
+    }
 }
 
 __global__ void __launch_bounds__(64) k_obs_stats_update(const double* __restrict__ partials, int nblk, int cols,
@@ -245,14 +254,16 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
     }
 }
 
-__global__ void k_loss_finalize(const float* __restrict__ partials, int nblk, int A, int mb_rows, float entropy_coef,
-                                float* __restrict__ g_hb, float* __restrict__ g_ls, float* __restrict__ stats,
-                                const int32_t* __restrict__ stat_idx, float* __restrict__ kl_out) {
+__global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ partials, int nblk, int A, int mb_rows,
+                                                      float entropy_coef, float* __restrict__ g_hb,
+                                                      float* __restrict__ g_ls, float* __restrict__ stats,
+                                                      const int32_t* __restrict__ stat_idx, float* __restrict__ kl_out) {
     const int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
-    const int k = threadIdx.x;
-    if (k >= NV) return;
+    const int k = blockIdx.x;  // one wave per value, lanes stride over the block partials (fixed order)
     float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += partials[int64_t(b) * NV + k];
+    for (int b = threadIdx.x; b < nblk; b += kWave) s += partials[int64_t(b) * NV + k];
+    s = wave_sum(s);
+    if (threadIdx.x != 0) return;
     if (k <= A) {
         g_hb[k] = s;
     } else if (k <= 2 * A) {
@@ -267,25 +278,88 @@ __global__ void k_loss_finalize(const float* __restrict__ partials, int nblk, in
 
 // ------------------------------------------------------------------------------ ELU backward
 
-constexpr int kEluRows = 64;
+constexpr int kEluRows = 256;
+constexpr int kEluThreads = 1024;
 
-__global__ void __launch_bounds__(256) k_elu_bwd(const void* __restrict__ dh, int dh_t, const void* __restrict__ h,
-                                                 int h_t, void* __restrict__ dz, int dz_t, int rows, int cols,
-                                                 float* __restrict__ partials) {
+// two adjacent columns per thread (4-B bf16 pair / 8-B float pair loads), row phases across the block
+template <int DH_T, int H_T, int DZ_T>
+__global__ void __launch_bounds__(kEluThreads) k_elu_bwd(const void* __restrict__ dh, const void* __restrict__ h,
+                                                         void* __restrict__ dz, int rows, int cols,
+                                                         float* __restrict__ partials) {
+    __shared__ float red[kEluThreads * 2];
+    const int pairs = cols / 2;
+    const int nph = kEluThreads / pairs;
+    const int cp = threadIdx.x % pairs, ph = threadIdx.x / pairs;
     const int r0 = blockIdx.x * kEluRows;
     const int r1 = min(r0 + kEluRows, rows);
-    for (int c = threadIdx.x; c < cols; c += blockDim.x) {
-        float s = 0.f;
-        for (int r = r0; r < r1; ++r) {
-            const int64_t i = int64_t(r) * cols + c;
-            const float hv = load_as_f32(h, i, h_t);
-            const float g = load_as_f32(dh, i, dh_t);
-            const float z = hv > 0.f ? g : g * (hv + 1.f);
-            store_from_f32(dz, i, dz_t, z);
-            s += dz_t ? bf16_to_f32(f32_to_bf16(z)) : z;  // bias grad from the stored (GEMM-visible) dz
+    float s0 = 0.f, s1 = 0.f;
+    if (ph < nph) {
+#pragma unroll 4
+        for (int r = r0 + ph; r < r1; r += nph) {
+            const int64_t i = int64_t(r) * cols + 2 * cp;
+            float g0, g1, h0, h1;
+            if (DH_T) {
+                const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(dh) + i);
+                g0 = bf16_to_f32(uint16_t(u & 0xffffu));
+                g1 = bf16_to_f32(uint16_t(u >> 16));
+            } else {
+                const float2 u = *reinterpret_cast<const float2*>(static_cast<const float*>(dh) + i);
+                g0 = u.x;
+                g1 = u.y;
+            }
+            if (H_T) {
+                const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(h) + i);
+                h0 = bf16_to_f32(uint16_t(u & 0xffffu));
+                h1 = bf16_to_f32(uint16_t(u >> 16));
+            } else {
+                const float2 u = *reinterpret_cast<const float2*>(static_cast<const float*>(h) + i);
+                h0 = u.x;
+                h1 = u.y;
+            }
+            float z0 = h0 > 0.f ? g0 : g0 * (h0 + 1.f);
+            float z1 = h1 > 0.f ? g1 : g1 * (h1 + 1.f);
+            if (DZ_T) {
+                const uint16_t b0 = f32_to_bf16(z0), b1 = f32_to_bf16(z1);
+                *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(dz) + i) = uint32_t(b0) | (uint32_t(b1) << 16);
+                z0 = bf16_to_f32(b0);  // bias grad from the stored (GEMM-visible) dz
+                z1 = bf16_to_f32(b1);
+            } else {
+                *reinterpret_cast<float2*>(static_cast<float*>(dz) + i) = make_float2(z0, z1);
+            }
+            s0 += z0;
+            s1 += z1;
         }
-        partials[int64_t(blockIdx.x) * cols + c] = s;
     }
+    red[2 * threadIdx.x] = s0;
+    red[2 * threadIdx.x + 1] = s1;
+    __syncthreads();
+    for (int c = threadIdx.x; c < cols; c += kEluThreads) {
+        float t = 0.f;
+        for (int q = 0; q < nph; ++q) t += red[2 * (q * pairs) + c];
+        partials[int64_t(blockIdx.x) * cols + c] = t;
+    }
+}
+
+// ------------------------------------------------------------------------------ partial-row reductions
+
+struct JobTable {
+    ppo_reduce_job_t j[PPO_MAX_JOBS];
+    int64_t start[PPO_MAX_JOBS + 1];
+    int n;
+};
+
+__global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
+    const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= t.start[t.n]) return;
+    int k = 0;
+    while (e >= t.start[k + 1]) ++k;
+    const ppo_reduce_job_t& jb = t.j[k];
+    const int64_t o = e - t.start[k];
+    const int r = int(o / jb.dst_cols), c = int(o % jb.dst_cols);
+    const float* src = jb.src + int64_t(r) * jb.src_cols + c;
+    float s = 0.f;
+    for (int q = 0; q < jb.S; ++q) s += src[int64_t(q) * jb.src_n];
+    jb.dst[int64_t(r) * jb.dst_stride + c] = s;
 }
 
 // ------------------------------------------------------------------------------ clip + Adam
@@ -389,7 +463,8 @@ int ppo_obs_stats_blocks(int32_t mb_rows) { return (mb_rows + kStatRows - 1) / k
 int ppo_obs_stats(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_t cols, double* partials,
                   void* stream) {
     if (cols <= 0 || cols > 64 || mb_rows < 2) return fail(-1, "ppo_obs_stats: need 1 <= cols <= 64, mb_rows >= 2");
-    hipLaunchKernelGGL(k_obs_stats, dim3(ppo_obs_stats_blocks(mb_rows)), dim3(64), 0, S(stream), x, mb_idx, mb_rows,
+    hipLaunchKernelGGL(k_obs_stats, dim3(ppo_obs_stats_blocks(mb_rows)), dim3(64 * kStatPhases), 0, S(stream), x,
+                       mb_idx, mb_rows,
                        cols, partials);
     return launched("k_obs_stats");
 }
@@ -439,7 +514,8 @@ int ppo_loss_finalize(const float* partials, int32_t nblk, int32_t A, int32_t mb
                       float* grad_head_bias, float* grad_logstd, float* stats, const int32_t* stat_idx, float* kl_out,
                       void* stream) {
     if (A <= 0 || A > PPO_MAX_ACT) return fail(-1, "ppo_loss_finalize: bad action dim");
-    hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(128), 0, S(stream), partials, nblk, A, mb_rows, entropy_coef,
+    hipLaunchKernelGGL(k_loss_finalize, dim3(2 * A + 1 + PPO_LOSS_NSTAT), dim3(kWave), 0, S(stream), partials, nblk, A,
+                       mb_rows, entropy_coef,
                        grad_head_bias, grad_logstd, stats, stat_idx, kl_out);
     return launched("k_loss_finalize");
 }
@@ -448,10 +524,33 @@ int ppo_elu_bwd_blocks(int32_t rows) { return (rows + kEluRows - 1) / kEluRows; 
 
 int ppo_elu_bwd(const void* dh, int32_t dh_dtype, const void* h, int32_t h_dtype, void* dz, int32_t dz_dtype,
                 int32_t rows, int32_t cols, float* partials, void* stream) {
-    if (cols % 64) return fail(-1, "ppo_elu_bwd: cols must be a multiple of 64");
-    hipLaunchKernelGGL(k_elu_bwd, dim3(ppo_elu_bwd_blocks(rows)), dim3(cols < 256 ? cols : 256), 0, S(stream), dh,
-                       dh_dtype, h, h_dtype, dz, dz_dtype, rows, cols, partials);
+    if (cols % 64 || cols > 2 * kEluThreads) return fail(-1, "ppo_elu_bwd: cols must be a multiple of 64, <= 2048");
+    const dim3 grid(ppo_elu_bwd_blocks(rows)), block(kEluThreads);
+    const int code = dh_dtype * 4 + h_dtype * 2 + dz_dtype;
+    switch (code) {
+        case 0: hipLaunchKernelGGL((k_elu_bwd<0, 0, 0>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
+        case 3: hipLaunchKernelGGL((k_elu_bwd<0, 1, 1>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
+        case 7: hipLaunchKernelGGL((k_elu_bwd<1, 1, 1>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
+        default: return fail(-1, "ppo_elu_bwd: dtype combination (dh, h, dz) must be (f32,f32,f32), (f32,bf16,bf16) or (bf16,bf16,bf16)");
+    }
     return launched("k_elu_bwd");
+}
+
+int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stream) {
+    if (njobs <= 0 || njobs > PPO_MAX_JOBS) return fail(-1, "ppo_reduce_rows: 1..16 jobs");
+    JobTable t{};
+    t.n = njobs;
+    t.start[0] = 0;
+    for (int k = 0; k < njobs; ++k) {
+        const ppo_reduce_job_t& j = jobs_host[k];
+        if (j.S <= 0 || j.dst_cols <= 0 || j.src_cols < j.dst_cols || j.dst_stride < j.dst_cols || !j.src || !j.dst)
+            return fail(-1, "ppo_reduce_rows: bad job");
+        t.j[k] = j;
+        t.start[k + 1] = t.start[k] + int64_t(j.out_rows) * j.dst_cols;
+    }
+    const int64_t n = t.start[njobs];
+    hipLaunchKernelGGL(k_reduce_rows, dim3(unsigned((n + 255) / 256)), dim3(256), 0, S(stream), t);
+    return launched("k_reduce_rows");
 }
 
 int ppo_sqnorm_blocks(void) { return kNormBlocks; }

@@ -43,6 +43,11 @@ class PpoLossCfg(C.Structure):
                 ("clip_value", C.c_int32), ("bound_loss", C.c_int32)]
 
 
+class PpoReduceJob(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("S", C.c_int32), ("out_rows", C.c_int32),
+                ("src_cols", C.c_int32), ("dst_cols", C.c_int32), ("dst_stride", C.c_int32), ("src_n", C.c_int64)]
+
+
 class PpoSeg(C.Structure):
     _fields_ = [("off", C.c_int64), ("len", C.c_int64), ("moff", C.c_int64), ("cols", C.c_int32),
                 ("mstride", C.c_int32)]
@@ -51,7 +56,7 @@ class PpoSeg(C.Structure):
 EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks", "ppo_obs_stats",
                     "ppo_obs_stats_update", "ppo_obs_normalize", "ppo_loss_blocks", "ppo_loss_grad",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
-                    "ppo_adam", "ppo_tail"]
+                    "ppo_adam", "ppo_tail", "ppo_reduce_rows"]
 
 
 def load() -> C.CDLL:
@@ -73,6 +78,7 @@ def load() -> C.CDLL:
     L.ppo_sqnorm.argtypes = [V, I64, V, V]
     L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, V]
     L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V]
+    L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
     for f in ("ppo_obs_stats_blocks", "ppo_loss_blocks", "ppo_elu_bwd_blocks"):
         getattr(L, f).argtypes = [I32]
     L.ppo_last_error.restype = C.c_char_p
@@ -131,13 +137,15 @@ class FusedPPOUpdate:
         self.head = torch.empty(B, self.A + 1, device=dev)
         self.dhead = torch.empty(B, self.A + 1, device=dev)
         wmax = max(widths[1:])
+        if any(w != wmax for w in widths[1:]):
+            raise NotImplementedError("the fused update expects equal hidden widths (the agent's [256] x 5)")
         self.dz = torch.empty(B, wmax, device=dev, dtype=dt)
         self.dh = torch.empty(B, wmax, device=dev, dtype=dt)
         self.dh_last = torch.empty(B, widths[-1], device=dev)  # fp32 from the heads
         self.S = _split(B)
         L = self.L
         self.loss_partials = torch.empty(L.ppo_loss_blocks(B), 2 * self.A + 1 + PPO_LOSS_NSTAT, device=dev)
-        self.elu_partials = torch.empty(L.ppo_elu_bwd_blocks(B), wmax, device=dev)
+        self.elu_partials = torch.empty(len(self.linears), L.ppo_elu_bwd_blocks(B), wmax, device=dev)
         self.stat_partials = torch.empty(L.ppo_obs_stats_blocks(B) * 2 * 64, device=dev, dtype=torch.float64)
         self.norm_partials = torch.empty(L.ppo_sqnorm_blocks(), device=dev)
         self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -257,33 +265,43 @@ class FusedPPOUpdate:
                                    _p(self.stat_idx), _p(self.flat.extra), s), "ppo_loss_finalize")
         S = self.S
         hl = self.h_last_f
-        # heads: dWh = dhead^T h (split-K), dh_last = dhead Wh
-        torch.sum(torch.bmm(self.dhead.view(S, B // S, A + 1).transpose(1, 2), hl.view(S, B // S, hl.shape[1])),
-                  0, out=self.gWh)
+        jobs, keep = [], []
+
+        def job(src: torch.Tensor, dst: torch.Tensor, n_s: int, out_rows: int, src_cols: int, dst_cols: int,
+                dst_stride: int) -> None:
+            keep.append(src)
+            jobs.append(PpoReduceJob(src.data_ptr(), dst.data_ptr(), n_s, out_rows, src_cols, dst_cols, dst_stride,
+                                     src.numel() // n_s))
+
+        # heads: dWh = dhead^T h (split-K partials), dh_last = dhead Wh
+        pw = torch.bmm(self.dhead.view(S, B // S, A + 1).transpose(1, 2), hl.view(S, B // S, hl.shape[1]))
+        job(pw, self.gWh, S, A + 1, hl.shape[1], hl.shape[1], hl.shape[1])
         torch.mm(self.dhead, self.Wh, out=self.dh_last)
         dh, dh_t = self.dh_last, 0
         dt_code = int(self.bf16)
+        nblk = self.elu_partials.shape[1]
         for i in reversed(range(nl)):
             m = self.linears[i]
             n_out = m.out_features
             dz = self.dz[:, :n_out]
             # dz_i = elu'(h_{i+1}) * dh_{i+1}; bias grad from the per-block column sums
             _check(L.ppo_elu_bwd(_p(dh), dh_t, _p(self.h[i + 1]), dt_code, _p(dz), dt_code, B, n_out,
-                                 _p(self.elu_partials), s), "ppo_elu_bwd")
-            torch.sum(self.elu_partials[:, :n_out], 0, out=self.gb[i])
+                                 _p(self.elu_partials[i]), s),
+                   "ppo_elu_bwd")
+            job(self.elu_partials[i], self.gb[i], nblk, 1, n_out, n_out, n_out)
             hin = self.h[i]
             kin = hin.shape[1]
             gw = torch.bmm(dz.view(S, B // S, n_out).transpose(1, 2), hin.view(S, B // S, kin),
                            out_dtype=torch.float32) if self.bf16 else \
                 torch.bmm(dz.view(S, B // S, n_out).transpose(1, 2), hin.view(S, B // S, kin))
-            if kin == m.in_features:
-                torch.sum(gw, 0, out=self.gW[i])
-            else:
-                self.gW[i].copy_(gw.sum(0)[:, :m.in_features])
+            job(gw, self.gW[i], S, n_out, kin, m.in_features, m.in_features)
             if i > 0:
                 dhi = self.dh[:, :kin]
                 torch.mm(dz, self.W_lp[i], out=dhi)
                 dh, dh_t = dhi, dt_code
+        arr = (PpoReduceJob * len(jobs))(*jobs)
+        _check(L.ppo_reduce_rows(arr, len(jobs), s), "ppo_reduce_rows")
+        del keep
 
     @torch.no_grad()
     def _optimizer_step(self) -> None:

@@ -91,6 +91,18 @@ int ppo_elu_bwd_blocks(int32_t rows);
 int ppo_elu_bwd(const void* dh, int32_t dh_dtype, const void* h, int32_t h_dtype, void* dz, int32_t dz_dtype,
                 int32_t rows, int32_t cols, float* partials, void* stream);
 
+/* Sum S partial rows into the flat gradient, several independent jobs in ONE launch (split-K GEMM
+ * partials, ELU bias partials): dst[r*dst_stride + c] = sum_s src[s*src_n + r*src_cols + c] for
+ * r < out_rows, c < dst_cols (fixed summation order). */
+typedef struct {
+    const float* src;
+    float* dst;
+    int32_t S, out_rows, src_cols, dst_cols, dst_stride;
+    int64_t src_n;
+} ppo_reduce_job_t;
+#define PPO_MAX_JOBS 16
+int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stream);
+
 /* ||g||^2 partials (fp32, nblk = ppo_sqnorm_blocks()) */
 int ppo_sqnorm_blocks(void);
 int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream);

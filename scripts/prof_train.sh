@@ -1,7 +1,11 @@
+#!/bin/bash
+# rocprofv3 kernel trace of scripts/bench_train.py (1 warm-up + 1 timed epoch); summary to stdout.
 set -o pipefail
-mkdir -p gpurun_out
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-O=$GRAFT_REPO_ROOT/gpurun_out/prof_train
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o run -- python3 $GRAFT_REPO_ROOT/scripts/bench_train.py --num_envs 32768 --epochs 1 --warmup 1 > $GRAFT_REPO_ROOT/gpurun_out/prof_train.log 2>&1 || exit $?
+O=$R/gpurun_out/prof_train${TAG}
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o run -- python3 $R/scripts/bench_train.py --num_envs ${NUM_ENVS:-32768} --epochs 1 --warmup 1 > $R/gpurun_out/prof_train${TAG}.log 2>&1 || exit $?
 rm -f $O/run_kernel_trace.csv
-head -40 $O/run_kernel_stats.csv
+tail -1 $R/gpurun_out/prof_train${TAG}.log
+python3 $R/scripts/kstats.py $O/run_kernel_stats.csv 30
