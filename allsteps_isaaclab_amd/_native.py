@@ -23,7 +23,7 @@ ABI_VERSION = 1
 EXPORTED_SYMBOLS = [
     "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
-    "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask",
+    "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask", "as_set_graph_safe",
 ]
 
 
@@ -109,6 +109,7 @@ def load() -> C.CDLL:
     L.as_physics_step.argtypes = [V, V, V]
     L.as_task_step.argtypes = [V, V, V, V, V, V, V, V]
     L.as_set_seed.argtypes = [V, U64]
+    L.as_set_graph_safe.argtypes = [V, I32]
     L.as_profile.argtypes = [V, I32]
     L.as_debug_stamps.argtypes = [V, V]
     L.as_profile_read.argtypes = [V, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(I32)]
@@ -268,6 +269,9 @@ class NativeEnv:
 
     def set_seed(self, seed: int):
         check(self.L.as_set_seed(self.h, seed & 0xFFFFFFFFFFFFFFFF), "as_set_seed")
+
+    def set_graph_safe(self, on: bool):
+        check(self.L.as_set_graph_safe(self.h, int(bool(on))), "as_set_graph_safe")
 
     def reset_all(self, obs, reset_draws=None, stream=None):
         check(self.L.as_reset_all(self.h, obs.data_ptr(),

@@ -37,6 +37,7 @@ struct as_env {
   as::Consts* consts_dev;
   int32_t* counters_dev;  // two banks of kCntBank: step t uses bank t % 2, k_obs clears the other
   int32_t bank = 0, last_bank = 0;
+  int32_t graph_safe = 0;  // as_set_graph_safe: fixed bank 0 + memset per call
   uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_fix
   int32_t num_steps;
   int32_t nv;
@@ -158,6 +159,10 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // no memset per step: this launch's counter bank was cleared by the previous launch's k_obs
   // (physics-only launches do not touch the counters and keep the bank)
+  if (env->graph_safe && mode != as::kModePhysics) {
+    env->bank = 0;
+    HIP_TRY(hipMemsetAsync(env->counters_dev, 0, sizeof(int32_t) * as::kCntBank, s));
+  }
   int32_t* cnt = env->counters_dev + as::kCntBank * env->bank;
   as::StepArgs a{};
   a.consts = env->consts_dev;
@@ -195,7 +200,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   o.counters = cnt;
   o.next_counters = env->counters_dev + as::kCntBank * (env->bank ^ 1);
   env->last_bank = env->bank;
-  env->bank ^= 1;
+  if (!env->graph_safe) env->bank ^= 1;
   o.obs = obs;
   o.side = env->side_dev;
   HIP_TRY(as::launch_obs(o, s));
@@ -288,6 +293,12 @@ int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* s
   a.seed = env->seed;
   a.env_offset = env->env_offset;
   HIP_TRY(as::launch_stones(a, reinterpret_cast<hipStream_t>(stream)));
+  return AS_OK;
+}
+
+int as_set_graph_safe(as_env_t* env, int32_t on) {
+  if (!env) return fail(AS_ERR_INVALID, "as_set_graph_safe: null handle");
+  env->graph_safe = on != 0;
   return AS_OK;
 }
 

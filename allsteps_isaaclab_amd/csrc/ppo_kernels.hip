@@ -340,6 +340,72 @@ __global__ void __launch_bounds__(kEluThreads) k_elu_bwd(const void* __restrict_
     }
 }
 
+// ------------------------------------------------------------------------------ rollout policy head
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t u) { return float(u >> 8) * 5.9604644775390625e-8f + 2.98023223876953125e-8f; }
+
+template <int A>
+__global__ void __launch_bounds__(256) k_policy_sample(const float* __restrict__ head, const float* __restrict__ logstd,
+                                                       int rows, uint64_t seed, const int64_t* __restrict__ step_ctr,
+                                                       const double* __restrict__ vm, const double* __restrict__ vv,
+                                                       float veps, float* __restrict__ act, float* __restrict__ nlp,
+                                                       float* __restrict__ val, float* __restrict__ mus,
+                                                       float* __restrict__ sigmas) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const uint64_t sc = uint64_t(*step_ctr);
+    const uint2 key = make_uint2(uint32_t(seed), uint32_t(seed >> 32));
+    const float* h = head + int64_t(r) * (A + 1);
+    float q = 0.f, sum_ls = 0.f;
+    float z[(A + 3) / 4 * 4];
+#pragma unroll
+    for (int c = 0; c < (A + 3) / 4; ++c) {
+        const uint4 b = philox4x32_10(make_uint4(uint32_t(r), uint32_t(c), uint32_t(sc), uint32_t(sc >> 32)), key);
+        // Box-Muller, two normals per uniform pair
+        float s0, c0, s1, c1;
+        __sincosf(6.283185307179586f * u01(b.y), &s0, &c0);
+        __sincosf(6.283185307179586f * u01(b.w), &s1, &c1);
+        const float r0 = sqrtf(-2.f * __logf(u01(b.x))), r1 = sqrtf(-2.f * __logf(u01(b.z)));
+        z[4 * c + 0] = r0 * c0;
+        z[4 * c + 1] = r0 * s0;
+        z[4 * c + 2] = r1 * c1;
+        z[4 * c + 3] = r1 * s1;
+    }
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+        const float ls = logstd[j];
+        const float sg = expf(ls);
+        const float mu = h[j];
+        const float a = mu + sg * z[j];
+        const float d = (a - mu) / sg;
+        q += d * d;
+        sum_ls += ls;
+        act[int64_t(r) * A + j] = a;
+        mus[int64_t(r) * A + j] = mu;
+        sigmas[int64_t(r) * A + j] = sg;
+    }
+    nlp[r] = 0.5f * q + 0.5f * kLog2Pi * float(A) + sum_ls;
+    float v = h[A];
+    if (vm) v = sqrtf(float(vv[0]) + veps) * fminf(fmaxf(v, -5.f), 5.f) + float(vm[0]);
+    val[r] = v;
+}
+
+__global__ void k_counter_add(int64_t* ctr, int64_t inc) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *ctr += inc;
+}
+
 // ------------------------------------------------------------------------------ partial-row reductions
 
 struct JobTable {
@@ -551,6 +617,31 @@ int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stre
     const int64_t n = t.start[njobs];
     hipLaunchKernelGGL(k_reduce_rows, dim3(unsigned((n + 255) / 256)), dim3(256), 0, S(stream), t);
     return launched("k_reduce_rows");
+}
+
+int ppo_policy_sample(const float* head, const float* logstd, int32_t A, int32_t rows, uint64_t seed,
+                      const int64_t* step_ctr, const double* vms_mean, const double* vms_var, float vms_eps,
+                      float* actions, float* neglogp, float* values, float* mus, float* sigmas, void* stream) {
+    const dim3 grid((rows + 255) / 256), block(256);
+#define PPO_SAMPLE_CASE(AA)                                                                                          \
+    case AA:                                                                                                         \
+        hipLaunchKernelGGL(k_policy_sample<AA>, grid, block, 0, S(stream), head, logstd, rows, seed, step_ctr,     \
+                           vms_mean, vms_var, vms_eps, actions, neglogp, values, mus, sigmas);                      \
+        break;
+    switch (A) {
+        PPO_SAMPLE_CASE(2)
+        PPO_SAMPLE_CASE(12)
+        PPO_SAMPLE_CASE(21)
+        default:
+            return fail(-1, "ppo_policy_sample: action dims 2, 12 and 21 are instantiated");
+    }
+#undef PPO_SAMPLE_CASE
+    return launched("k_policy_sample");
+}
+
+int ppo_counter_add(int64_t* ctr, int64_t inc, void* stream) {
+    hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(64), 0, S(stream), ctr, inc);
+    return launched("k_counter_add");
 }
 
 int ppo_sqnorm_blocks(void) { return kNormBlocks; }

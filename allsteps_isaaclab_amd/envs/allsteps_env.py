@@ -245,6 +245,20 @@ class AllstepsEnv(DirectRLEnv):
         self.reward_buf = rew
         return self.obs_buf, rew, self.reset_terminated, self.reset_time_outs, self.extras
 
+    # ---- HIP-graph capture of step() (trainer rollout graphs)
+    graph_safe_step = True  # step() launches only stream-ordered work with no host synchronisation
+
+    def set_graph_capture(self, on: bool = True) -> None:
+        """Make ``step`` replayable from a captured HIP graph (as_set_graph_safe: fixed counter bank,
+        cleared by a memset node per call)."""
+        self._native.set_graph_safe(on)
+
+    def account_steps(self, k: int = 1) -> None:
+        """Advance the host-side step counters for ``k`` steps replayed from a graph (the replay runs
+        the device work of ``step`` but not its Python bookkeeping)."""
+        self._sim_step_counter += self.cfg.decimation * k
+        self.common_step_counter += k
+
     def step_with_draws(self, action: torch.Tensor, reset_draws: torch.Tensor):
         """``step`` with injected reset draws ((N, 22) U[0,1): mirror, 21 joint noise) -- parity tests."""
         self._sim_step_counter += self.cfg.decimation

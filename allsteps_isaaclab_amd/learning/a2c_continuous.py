@@ -380,6 +380,15 @@ class A2CAgent:
         self.game_lengths = AverageMeter(1, self.games_to_track, dev)
         world_mb = self.world_size if (self.multi_gpu and self.multi_gpu_mode == "allgather") else 1
         self.dataset = PPODataset(self.batch_size * world_mb, self.minibatch_size * world_mb)
+        self._play_graphs = None
+        uw = getattr(getattr(self.vec_env, "env", None), "unwrapped", None)
+        if self.fused_update and self.config.get("rollout_graphs", True) and getattr(uw, "graph_safe_step", False):
+            # one HIP graph per rollout step index: policy forward + sampling + env step + bookkeeping
+            uw.set_graph_capture(True)
+            self._uw = uw
+            self._play_graphs = {}
+            self._obs_buf = torch.zeros((N,) + self.obs_shape, device=dev)
+            self._dones_buf = torch.ones(N, dtype=torch.uint8, device=dev)
         self.fused = None
         if self.fused_update:
             from .fused import FusedPPOUpdate
@@ -387,6 +396,8 @@ class A2CAgent:
             self.fused = FusedPPOUpdate(self, compute_dtype=torch.bfloat16 if self.mixed_precision else torch.float32,
                                         use_graphs=bool(self.config.get("hip_graphs", True)))
             self._ds_static: dict = {}
+            if self._play_graphs is not None:
+                self.fused.init_rollout(N, int(self.params.get("seed", 0)) * 7919 + self.rank)
 
     # ------------------------------------------------------------------ env / policy
     def obs_to_tensors(self, obs):
@@ -437,10 +448,66 @@ class A2CAgent:
             mb_advs[t] = lastgaelam = delta + self.gamma * self.tau * nextnonterminal * lastgaelam
         return mb_advs
 
+    def _play_step_body(self, n: int) -> None:
+        """Rollout step n on static buffers (the captured form of one play_steps iteration)."""
+        td = self.tensor_dict
+        obs = self._obs_buf
+        res = {k: td[k][n] for k in ("actions", "neglogpacs", "values", "mus", "sigmas")}
+        self.fused.policy_act(obs, res)  # trunk + heads + Philox sampling straight into the buffers
+        td["obses"][n].copy_(obs)
+        td["dones"][n].copy_(self._dones_buf)
+        obs2, rewards, dones, infos = self.env_step(res["actions"])
+        shaped = self.rewards_shaper(rewards)
+        if self.value_bootstrap and "time_outs" in infos:
+            shaped = shaped + self.gamma * res["values"] * infos["time_outs"].unsqueeze(1).float()
+        td["rewards"][n].copy_(shaped)
+        self.current_rewards += rewards
+        self.current_shaped_rewards += shaped
+        self.current_lengths += 1
+        done = dones.bool()
+        self.game_rewards.update(self.current_rewards, done)
+        self.game_shaped_rewards.update(self.current_shaped_rewards, done)
+        self.game_lengths.update(self.current_lengths.unsqueeze(1), done)
+        not_dones = 1.0 - dones.float()
+        self.current_rewards *= not_dones.unsqueeze(1)
+        self.current_shaped_rewards *= not_dones.unsqueeze(1)
+        self.current_lengths *= not_dones
+        self._obs_buf.copy_(obs2["obs"])
+        self._dones_buf.copy_(dones)
+
+    def _play_step_graph(self, n: int) -> None:
+        """First call: eager (warm-up, real step).  Second: capture (no execution) + replay.  Later:
+        replay, then advance the env's host-side counters the replay did not touch."""
+        g = self._play_graphs.get(n)
+        if g is None:
+            self._play_step_body(n)
+            self._play_graphs[n] = "warm"
+            return
+        if g == "warm":
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._play_step_body(n)  # the env's Python counters advance here, once
+            self._play_graphs[n] = g
+            g.replay()
+            return
+        g.replay()
+        self._uw.account_steps(1)
+
     @torch.no_grad()
     def play_steps(self) -> dict:
         td = self.tensor_dict
         step_time = 0.0
+        if self._play_graphs is not None:
+            self.model.eval()
+            if self.obs["obs"].data_ptr() != self._obs_buf.data_ptr():
+                self._obs_buf.copy_(self.obs["obs"])
+            if self.dones.data_ptr() != self._dones_buf.data_ptr():
+                self._dones_buf.copy_(self.dones)
+            for n in range(self.horizon_length):
+                self._play_step_graph(n)
+            self.obs = {"obs": self._obs_buf}
+            self.dones = self._dones_buf
+            return self._finish_rollout(step_time)
         for n in range(self.horizon_length):
             res = self.get_action_values(self.obs)
             td["obses"][n] = self.obs["obs"]
@@ -466,7 +533,14 @@ class A2CAgent:
             self.current_rewards *= not_dones.unsqueeze(1)
             self.current_shaped_rewards *= not_dones.unsqueeze(1)
             self.current_lengths *= not_dones
-        last_values = self.get_values(self.obs)
+        return self._finish_rollout(step_time)
+
+    def _finish_rollout(self, step_time: float) -> dict:
+        td = self.tensor_dict
+        if self._play_graphs is not None:
+            last_values = self.fused.policy_values(self.obs["obs"])
+        else:
+            last_values = self.get_values(self.obs)
         mb_advs = self.discount_values(self.dones.float(), last_values, td["dones"].float(), td["values"],
                                        td["rewards"])
         mb_returns = mb_advs + td["values"]
@@ -562,6 +636,8 @@ class A2CAgent:
         self.model.eval()
         t_play = time.perf_counter()
         batch = self.play_steps()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)  # play / update split of the epoch time (once per epoch)
         if self.multi_gpu and self.multi_gpu_mode == "allgather" and self.world_size > 1:
             batch = self.gather_batch(batch)
         t_update = time.perf_counter()

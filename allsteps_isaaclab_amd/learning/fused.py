@@ -56,7 +56,7 @@ class PpoSeg(C.Structure):
 EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks", "ppo_obs_stats",
                     "ppo_obs_stats_update", "ppo_obs_normalize", "ppo_loss_blocks", "ppo_loss_grad",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
-                    "ppo_adam", "ppo_tail", "ppo_reduce_rows"]
+                    "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add"]
 
 
 def load() -> C.CDLL:
@@ -79,6 +79,8 @@ def load() -> C.CDLL:
     L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, V]
     L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V]
     L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
+    L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
+    L.ppo_counter_add.argtypes = [V, I64, V]
     for f in ("ppo_obs_stats_blocks", "ppo_loss_blocks", "ppo_elu_bwd_blocks"):
         getattr(L, f).argtypes = [I32]
     L.ppo_last_error.restype = C.c_char_p
@@ -234,6 +236,57 @@ class FusedPPOUpdate:
         return torch.cuda.current_stream(self.dev).cuda_stream
 
     # ------------------------------------------------------------------ the two halves
+    def _trunk(self, x, idx, rows, h, h_last_f, head) -> None:
+        """Normalise rows [idx*rows, (idx+1)*rows) of x, run the trunk (bf16 mirror or fp32 weights) and
+        the fp32 heads into head = [mu | value]."""
+        L, s, rms = self.L, self._stream(), self.rms
+        _check(L.ppo_obs_normalize(_p(x), _p(idx), rows, self.obs_dim, _p(rms.running_mean), _p(rms.running_var),
+                                   rms.epsilon, _p(h[0]), self.k0, int(self.bf16), s), "ppo_obs_normalize")
+        for i in range(len(self.linears)):  # z = h W^T + b ; h' = elu(z)
+            out = h[i + 1]
+            torch.addmm(self.b_lp[i], h[i], self.W_lp[i].t(), out=out)
+            F.elu(out, inplace=True)
+        if h_last_f is not h[-1]:
+            h_last_f.copy_(h[-1])
+        torch.addmm(self.bh, h_last_f, self.Wh.t(), out=head)
+
+    # ------------------------------------------------------------------ rollout policy (graph-safe)
+    def init_rollout(self, n_envs: int, seed: int) -> None:
+        dev, dt = self.dev, self.dt
+        widths = [self.k0] + [m.out_features for m in self.linears]
+        self.N = n_envs
+        self.hr = [torch.zeros(n_envs, w, device=dev, dtype=dt) for w in widths]
+        self.hr_last_f = torch.empty(n_envs, widths[-1], device=dev) if self.bf16 else self.hr[-1]
+        self.head_r = torch.empty(n_envs, self.A + 1, device=dev)
+        self.zero_idx = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.step_ctr = torch.zeros(1, device=dev, dtype=torch.int64)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+
+    @torch.no_grad()
+    def policy_act(self, obs: torch.Tensor, out: dict) -> None:
+        """ModelA2CContinuousLogStd eval forward + sample for the rollout, written into
+        out['actions' | 'neglogpacs' | 'values' | 'mus' | 'sigmas'] (contiguous, rows = n_envs).
+        Same trunk precision as the training forward (bf16 mirror when mixed_precision)."""
+        if not obs.is_contiguous() or obs.shape[0] != self.N:
+            raise ValueError("policy_act: obs must be contiguous (n_envs, obs_dim)")
+        self._trunk(obs, self.zero_idx, self.N, self.hr, self.hr_last_f, self.head_r)
+        vms = self.model.value_mean_std
+        s = self._stream()
+        _check(self.L.ppo_policy_sample(_p(self.head_r), _p(self.logstd), self.A, self.N, self.seed,
+                                        _p(self.step_ctr), _p(vms.running_mean) if vms is not None else None,
+                                        _p(vms.running_var) if vms is not None else None,
+                                        vms.epsilon if vms is not None else 0.0, _p(out["actions"]),
+                                        _p(out["neglogpacs"]), _p(out["values"]), _p(out["mus"]), _p(out["sigmas"]),
+                                        s), "ppo_policy_sample")
+        _check(self.L.ppo_counter_add(_p(self.step_ctr), 1, s), "ppo_counter_add")
+
+    @torch.no_grad()
+    def policy_values(self, obs: torch.Tensor) -> torch.Tensor:
+        """Denormalised values (n_envs, 1) of the rollout policy (get_values)."""
+        self._trunk(obs.contiguous(), self.zero_idx, self.N, self.hr, self.hr_last_f, self.head_r)
+        v = self.head_r[:, self.A:].clone()
+        return self.model.denorm_value(v)
+
     @torch.no_grad()
     def _forward_backward(self, rms_train: bool) -> None:
         L, s, ds, B, A = self.L, self._stream(), self.ds, self.mb, self.A
@@ -244,17 +297,8 @@ class FusedPPOUpdate:
             _check(L.ppo_obs_stats_update(_p(self.stat_partials), L.ppo_obs_stats_blocks(B), self.obs_dim, B,
                                           _p(rms.running_mean), _p(rms.running_var), _p(rms.count), s),
                    "ppo_obs_stats_update")
-        _check(L.ppo_obs_normalize(_p(ds["obs"]), _p(self.mb_idx), B, self.obs_dim, _p(rms.running_mean),
-                                   _p(rms.running_var), rms.epsilon, _p(self.h[0]), self.k0, int(self.bf16), s),
-               "ppo_obs_normalize")
+        self._trunk(ds["obs"], self.mb_idx, B, self.h, self.h_last_f, self.head)
         nl = len(self.linears)
-        for i in range(nl):  # z = h W^T + b ; h' = elu(z)
-            out = self.h[i + 1]
-            torch.addmm(self.b_lp[i], self.h[i], self.W_lp[i].t(), out=out)
-            F.elu(out, inplace=True)
-        if self.bf16:
-            self.h_last_f.copy_(self.h[-1])
-        torch.addmm(self.bh, self.h_last_f, self.Wh.t(), out=self.head)
         self.flat.zero_grad()
         _check(L.ppo_loss_grad(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
                                _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),

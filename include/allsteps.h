@@ -195,6 +195,12 @@ int as_profile_read(as_env_t* env, double* step_kernel_ms, double* obs_kernel_ms
  * by every launch (scripts/stamps.py).  Pass NULL to switch off. */
 int as_debug_stamps(as_env_t* env, uint64_t* stamps_dev);
 
+/* Graph-safe stepping (on != 0): every as_step / as_task_step / as_reset_* uses the SAME counter bank,
+ * cleared by a memset node at the start of the call, instead of alternating two banks from host
+ * state -- so a call captured once in a HIP graph (hipStreamBeginCapture) can be replayed any number
+ * of times.  Off (default): two banks, no memset (lowest eager launch count). */
+int as_set_graph_safe(as_env_t* env, int32_t on);
+
 /* Device counters of the last step: [0] = any env reset, [1] = sum of curr_target_index. */
 int as_step_counters(as_env_t* env, const int32_t** counters_dev);
 int as_get_curriculum_host(as_env_t* env, int32_t* level_host); /* synchronises the stream */

@@ -103,6 +103,18 @@ typedef struct {
 #define PPO_MAX_JOBS 16
 int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stream);
 
+/* Rollout policy head (graph-safe sampling): head = [mu | value] (rows x (A+1), fp32), logstd (A).
+ * actions = mu + exp(logstd) * N(0, 1) with the normals from Philox4x32-10 keyed by `seed` and
+ * countered by (row, chunk, *step_ctr) -- the same draw for the same (seed, step, row) on any replay;
+ * neglogp as ModelA2CContinuousLogStd.neglogp; values denormalised by the value normaliser
+ * (sqrt(var + eps) * clamp(v, -5, 5) + mean) when vms_mean != NULL.  Outputs are row-major
+ * (rows x A for actions / mus / sigmas, rows for neglogp / values). */
+int ppo_policy_sample(const float* head, const float* logstd, int32_t A, int32_t rows, uint64_t seed,
+                      const int64_t* step_ctr, const double* vms_mean, const double* vms_var, float vms_eps,
+                      float* actions, float* neglogp, float* values, float* mus, float* sigmas, void* stream);
+/* *ctr += inc (one thread; orders after the kernels that read it) */
+int ppo_counter_add(int64_t* ctr, int64_t inc, void* stream);
+
 /* ||g||^2 partials (fp32, nblk = ppo_sqnorm_blocks()) */
 int ppo_sqnorm_blocks(void);
 int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream);

@@ -21,6 +21,9 @@ def test_train_script_runs_on_allsteps(tmp_path):
     agent = runner.agent
     st = agent.last_stats
     assert agent.epoch_num == 3 and agent.frame == 3 * 1024 * 32
+    # rollout graphs: epoch 1 eager, epoch 2 captured, epoch 3 replayed; host counters still advance
+    assert all(isinstance(g, torch.cuda.CUDAGraph) for g in agent._play_graphs.values())
+    assert agent._uw.common_step_counter == 3 * 32
     for k in ("a_loss", "c_loss", "kl", "entropy", "lr"):
         assert math.isfinite(st[k]), (k, st)
     assert torch.isfinite(agent.flat.params).all()
@@ -196,3 +199,82 @@ def test_fused_train_epoch_runs_graph_replays(tmp_path):
     assert float(fus.optimizer.step_t) == n
     assert len(fus.fused.graphs) == 3  # A (normaliser updating), A (frozen), B
     assert all(isinstance(g, torch.cuda.CUDAGraph) for g in fus.fused.graphs.values())
+
+
+@pytest.mark.gpu
+def test_env_step_replayed_from_graph_matches_eager():
+    """AllstepsEnv.step captured once in a HIP graph (graph-safe counters) and replayed with fresh
+    actions gives bit-identical obs / rewards / dones to eager stepping, resets included."""
+    from allsteps_isaaclab_amd import registry
+
+    envs = []
+    for graph in (False, True):
+        cfg = registry.load_cfg_from_registry("Allsteps-v0", "env_cfg_entry_point")
+        cfg.scene.num_envs = 512
+        e = registry.make("Allsteps-v0", cfg=cfg)
+        e.set_graph_capture(graph)
+        e.reset()
+        envs.append(e)
+    eager, ge = envs
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    acts = [torch.rand(512, 21, device="cuda:0", generator=g) * 2 - 1 for _ in range(150)]
+    static = torch.zeros(512, 21, device="cuda:0")
+    static.copy_(acts[0])
+    ge.step(static)  # warm-up (eager) step 0
+    graph = torch.cuda.CUDAGraph()
+    static.copy_(acts[1])
+    with torch.cuda.graph(graph):
+        out = ge.step(static)
+    resets = 0
+    for k in range(150):
+        o1, r1, t1, tr1, _ = eager.step(acts[k])
+        if k == 0:
+            continue
+        static.copy_(acts[k])
+        graph.replay()
+        torch.cuda.synchronize()
+        o2, r2, t2, tr2 = out[0]["policy"], out[1], out[2], out[3]
+        assert torch.equal(o1["policy"], o2) and torch.equal(r1, r2), k
+        assert torch.equal(t1, t2) and torch.equal(tr1, tr2), k
+        resets += int((t1 | tr1).sum())
+    assert resets > 0  # the in-kernel reset path ran inside the replays
+    for e in envs:
+        e.close()
+
+
+@pytest.mark.gpu
+def test_rollout_policy_sampling_kernel(tmp_path):
+    """ppo_policy_sample: N(mu, sigma) draws (moments), neglogp / denormalised value formulas, and the
+    same draw for the same step counter (graph replays are reproducible)."""
+    ref, fus = _agents_and_batch(256, mixed=False, tmp=tmp_path)
+    f = fus.fused
+    n = 4096
+    f.init_rollout(n, seed=123)
+    with torch.no_grad():
+        fus.model.a2c_network.sigma.fill_(-0.7)
+        fus.model.value_mean_std.running_mean.fill_(0.3)
+        fus.model.value_mean_std.running_var.fill_(4.0)
+    obs = torch.randn(n, 59, device="cuda:0")
+    out = {k: torch.empty(n, 21, device="cuda:0") for k in ("actions", "mus", "sigmas")}
+    out["neglogpacs"] = torch.empty(n, device="cuda:0")
+    out["values"] = torch.empty(n, 1, device="cuda:0")
+    f.policy_act(obs, out)
+    first = out["actions"].clone()
+    fus.model.eval()
+    ref_out = fus.model({"is_train": False, "prev_actions": None, "obs": obs})  # fp32 torch forward
+    torch.testing.assert_close(out["mus"], ref_out["mus"], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(out["values"], ref_out["values"], rtol=1e-4, atol=1e-4)
+    sig = math.exp(-0.7)
+    assert torch.allclose(out["sigmas"], torch.full_like(out["sigmas"], sig))
+    z = (out["actions"] - out["mus"]) / sig
+    assert abs(z.mean().item()) < 0.01 and abs(z.std().item() - 1.0) < 0.01
+    from allsteps_isaaclab_amd.learning.models import neglogp
+
+    ls = torch.full_like(out["mus"], -0.7)
+    torch.testing.assert_close(out["neglogpacs"], neglogp(out["actions"], out["mus"], out["sigmas"], ls),
+                               rtol=1e-5, atol=1e-4)
+    f.policy_act(obs, out)
+    assert not torch.equal(first, out["actions"])  # counter advanced: fresh draws
+    f.step_ctr.fill_(0)
+    f.policy_act(obs, out)
+    assert torch.equal(first, out["actions"])  # same counter, same draws
