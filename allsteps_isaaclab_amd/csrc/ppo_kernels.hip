@@ -143,48 +143,72 @@ __device__ __forceinline__ float max_grad(float u1, float u2, float g1, float g2
     return u1 > u2 ? g1 : (u2 > u1 ? g2 : 0.5f * (g1 + g2));
 }
 
+// One row per 32-lane group: lane j < A owns action j, lane A owns the value; row sums by xor
+// shuffles inside the group.  Loads of a row's A floats are contiguous across lanes (coalesced).
+// Each lane keeps running sums for its own column over the rows its group visits.
+constexpr int kLossRowsPerGroup = 16;
+
 template <int A>
 __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
     const float* __restrict__ head, const float* __restrict__ logstd, int mb_rows, const int32_t* __restrict__ mb_idx,
     const float* __restrict__ actions, float* __restrict__ ds_mu, float* __restrict__ ds_sigma,
     const float* __restrict__ old_nlp, const float* __restrict__ adv_, const float* __restrict__ old_v,
     const float* __restrict__ ret_, ppo_loss_cfg_t cfg, float* __restrict__ dhead, float* __restrict__ partials) {
+    static_assert(A + 1 <= 32, "one 32-lane group per row");
     constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
-    __shared__ float red[kLossThreads / kWave][NV];
-    const int r = blockIdx.x * kLossThreads + threadIdx.x;
-    const bool live = r < mb_rows;
+    constexpr int G = kLossThreads / 32;
+    __shared__ float red[G][NV];
+    const int j = threadIdx.x % 32, grp = threadIdx.x / 32;
     const float inv_b = 1.f / float(mb_rows);
-    float vals[NV];
+    const int64_t base = int64_t(*mb_idx) * mb_rows;
+    const bool act_lane = j < A;
+    const float ls = act_lane ? logstd[j] : 0.f;
+    const float sg = expf(ls);
+    float sum_ls = ls;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) vals[k] = 0.f;
-    if (live) {
-        const int64_t row = int64_t(*mb_idx) * mb_rows + r;
+    for (int o = 16; o > 0; o >>= 1) sum_ls += __shfl_xor(sum_ls, o, 32);
+    const float entropy = float(A) * (0.5f + 0.5f * kLog2Pi) + sum_ls;
+    float acc_mu = 0.f, acc_ls = 0.f, acc_v = 0.f;
+    float st_a = 0.f, st_c = 0.f, st_b = 0.f, st_e = 0.f, st_k = 0.f;
+    const int r_begin = (blockIdx.x * G + grp) * kLossRowsPerGroup;
+    for (int rr = 0; rr < kLossRowsPerGroup; ++rr) {
+        const int r = r_begin + rr;
+        if (r >= mb_rows) break;  // uniform across the group
+        const int64_t row = base + r;
         const float* h = head + int64_t(r) * (A + 1);
-        float mu[A], d[A], sig[A];
-        float sum_ls = 0.f, q = 0.f, kl = 0.f;
-#pragma unroll
-        for (int j = 0; j < A; ++j) {
-            const float ls = logstd[j];
-            sig[j] = expf(ls);
-            mu[j] = h[j];
-            d[j] = (actions[row * A + j] - mu[j]) / sig[j];
-            q += d[j] * d[j];
-            sum_ls += ls;
-            // policy_kl(p0 = current, p1 = dataset): log(s1/s0 + 1e-5) + (s0^2 + (m1-m0)^2) / (2 (s1^2 + 1e-5)) - 1/2
+        const float hj = j <= A ? h[j] : 0.f;  // mu_j, or the value on lane A
+        float d = 0.f, klj = 0.f, blj = 0.f, dbj = 0.f;
+        if (act_lane) {
+            d = (actions[row * A + j] - hj) / sg;
             const float m1 = ds_mu[row * A + j], s1 = ds_sigma[row * A + j];
-            const float dm = m1 - mu[j];
-            kl += logf(s1 / sig[j] + 1e-5f) + (sig[j] * sig[j] + dm * dm) / (2.f * (s1 * s1 + 1e-5f)) - 0.5f;
+            const float dm = m1 - hj;
+            // policy_kl(p0 = current, p1 = dataset)
+            klj = logf(s1 / sg + 1e-5f) + (sg * sg + dm * dm) / (2.f * (s1 * s1 + 1e-5f)) - 0.5f;
+            if (cfg.bound_loss == 1) {
+                const float lo = fminf(hj + cfg.soft_bound, 0.f), hi = fmaxf(hj - cfg.soft_bound, 0.f);
+                blj = lo * lo + hi * hi;
+                dbj = 2.f * (lo + hi);
+            } else if (cfg.bound_loss == 2) {
+                blj = hj * hj;
+                dbj = 2.f * hj;
+            }
+        }
+        float q = d * d, kl = klj, bl = blj;
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) {
+            q += __shfl_xor(q, o, 32);
+            kl += __shfl_xor(kl, o, 32);
+            bl += __shfl_xor(bl, o, 32);
         }
         const float nlp = 0.5f * q + 0.5f * kLog2Pi * float(A) + sum_ls;
         const float adv = adv_[row];
-        // actor
         float a_loss, g_nlp;
         if (cfg.ppo) {
             const float ratio = expf(old_nlp[row] - nlp);
             const float rc = fminf(fmaxf(ratio, 1.f - cfg.e_clip), 1.f + cfg.e_clip);
             const float u1 = -adv * ratio, u2 = -adv * rc;
             const bool inside = ratio >= 1.f - cfg.e_clip && ratio <= 1.f + cfg.e_clip;
-            // d(-adv * ratio)/d nlp = adv * ratio (d ratio / d nlp = -ratio)
+            // d(-adv * ratio)/d nlp = adv * ratio (d ratio / d nlp = -ratio); torch.maximum ties split
             g_nlp = max_grad(u1, u2, adv * ratio, inside ? adv * ratio : 0.f);
             a_loss = fmaxf(u1, u2);
         } else {
@@ -192,65 +216,63 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
             g_nlp = adv;
         }
         g_nlp *= inv_b;
-        // critic
-        const float v = h[A], vp = old_v[row], R = ret_[row];
-        float c_loss, g_v;
-        if (cfg.clip_value) {
-            const float dv = v - vp;
-            const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
-            const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
-            const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
-            g_v = max_grad(l1, l2, 2.f * (v - R), inside ? 2.f * (vc - R) : 0.f);
-            c_loss = fmaxf(l1, l2);
-        } else {
-            c_loss = (R - v) * (R - v);
-            g_v = 2.f * (v - R);
-        }
-        g_v *= 0.5f * cfg.critic_coef * inv_b;
-        // bound loss + head gradients
-        float b_loss = 0.f;
-        const float gb = cfg.bounds_coef * inv_b;
         float* dh = dhead + int64_t(r) * (A + 1);
-#pragma unroll
-        for (int j = 0; j < A; ++j) {
-            float db = 0.f;
-            if (cfg.bound_loss == 1) {
-                const float lo = fminf(mu[j] + cfg.soft_bound, 0.f), hi = fmaxf(mu[j] - cfg.soft_bound, 0.f);
-                b_loss += lo * lo + hi * hi;
-                db = 2.f * (lo + hi);
-            } else if (cfg.bound_loss == 2) {
-                b_loss += mu[j] * mu[j];
-                db = 2.f * mu[j];
-            }
-            // d nlp / d mu = -(a - mu) / sigma^2 = -d / sigma ; d nlp / d logstd = 1 - d^2
-            const float gmu = -g_nlp * d[j] / sig[j] + gb * db;
+        if (act_lane) {
+            // d nlp / d mu = -d / sigma ; d nlp / d logstd = 1 - d^2
+            const float gmu = -g_nlp * d / sg + cfg.bounds_coef * inv_b * dbj;
             dh[j] = gmu;
-            vals[j] = gmu;
-            vals[A + 1 + j] = g_nlp * (1.f - d[j] * d[j]);
-            ds_mu[row * A + j] = mu[j];  // dataset.update_mu_sigma
-            ds_sigma[row * A + j] = sig[j];
+            acc_mu += gmu;
+            acc_ls += g_nlp * (1.f - d * d);
+            ds_mu[row * A + j] = hj;  // dataset.update_mu_sigma
+            ds_sigma[row * A + j] = sg;
+        } else if (j == A) {
+            const float v = hj, vp = old_v[row], R = ret_[row];
+            float c_loss, g_v;
+            if (cfg.clip_value) {
+                const float dv = v - vp;
+                const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
+                const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
+                const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
+                g_v = max_grad(l1, l2, 2.f * (v - R), inside ? 2.f * (vc - R) : 0.f);
+                c_loss = fmaxf(l1, l2);
+            } else {
+                c_loss = (R - v) * (R - v);
+                g_v = 2.f * (v - R);
+            }
+            g_v *= 0.5f * cfg.critic_coef * inv_b;
+            dh[A] = g_v;
+            acc_v += g_v;
+            st_c += c_loss;
         }
-        dh[A] = g_v;
-        vals[A] = g_v;
-        const float entropy = float(A) * (0.5f + 0.5f * kLog2Pi) + sum_ls;
-        vals[2 * A + 1 + 0] = a_loss;
-        vals[2 * A + 1 + 1] = c_loss;
-        vals[2 * A + 1 + 2] = b_loss;
-        vals[2 * A + 1 + 3] = entropy;
-        vals[2 * A + 1 + 4] = kl;
+        if (j == 0) {
+            st_a += a_loss;
+            st_b += bl;
+            st_e += entropy;
+            st_k += kl;
+        }
     }
-    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        const float s = wave_sum(vals[k]);
-        if (lane == 0) red[w][k] = s;
+    // block partials: column sums owned by lanes, statistics from lanes 0 / A
+    float* rg = red[grp];
+    if (act_lane) {
+        rg[j] = acc_mu;
+        rg[A + 1 + j] = acc_ls;
+    }
+    if (j == A) {
+        rg[A] = acc_v;
+        rg[2 * A + 1 + 1] = st_c;
+    }
+    if (j == 0) {
+        rg[2 * A + 1 + 0] = st_a;
+        rg[2 * A + 1 + 2] = st_b;
+        rg[2 * A + 1 + 3] = st_e;
+        rg[2 * A + 1 + 4] = st_k;
     }
     __syncthreads();
     for (int k = threadIdx.x; k < NV; k += kLossThreads) {
-        float s = 0.f;
+        float t = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < kLossThreads / kWave; ++ww) s += red[ww][k];
-        partials[int64_t(blockIdx.x) * NV + k] = s;
+        for (int g = 0; g < G; ++g) t += red[g][k];
+        partials[int64_t(blockIdx.x) * NV + k] = t;
     }
 }
 
@@ -278,64 +300,69 @@ __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ 
 
 // ------------------------------------------------------------------------------ ELU backward
 
-constexpr int kEluRows = 256;
+constexpr int kEluRows = 128;
 constexpr int kEluThreads = 1024;
 
-// two adjacent columns per thread (4-B bf16 pair / 8-B float pair loads), row phases across the block
+template <int T>
+__device__ __forceinline__ void load4(const void* p, int64_t i, float (&x)[4]) {
+    if (T) {
+        const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p) + i);
+        x[0] = bf16_to_f32(uint16_t(u.x & 0xffffu));
+        x[1] = bf16_to_f32(uint16_t(u.x >> 16));
+        x[2] = bf16_to_f32(uint16_t(u.y & 0xffffu));
+        x[3] = bf16_to_f32(uint16_t(u.y >> 16));
+    } else {
+        const float4 u = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+        x[0] = u.x;
+        x[1] = u.y;
+        x[2] = u.z;
+        x[3] = u.w;
+    }
+}
+
+// four adjacent columns per thread (8-B bf16 / 16-B fp32 loads), row phases across the block
 template <int DH_T, int H_T, int DZ_T>
 __global__ void __launch_bounds__(kEluThreads) k_elu_bwd(const void* __restrict__ dh, const void* __restrict__ h,
                                                          void* __restrict__ dz, int rows, int cols,
                                                          float* __restrict__ partials) {
-    __shared__ float red[kEluThreads * 2];
-    const int pairs = cols / 2;
-    const int nph = kEluThreads / pairs;
-    const int cp = threadIdx.x % pairs, ph = threadIdx.x / pairs;
+    __shared__ float red[kEluThreads * 4];
+    const int quads = cols / 4;
+    const int nph = kEluThreads / quads;
+    const int cq = threadIdx.x % quads, ph = threadIdx.x / quads;
     const int r0 = blockIdx.x * kEluRows;
     const int r1 = min(r0 + kEluRows, rows);
-    float s0 = 0.f, s1 = 0.f;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
     if (ph < nph) {
-#pragma unroll 4
+#pragma unroll 2
         for (int r = r0 + ph; r < r1; r += nph) {
-            const int64_t i = int64_t(r) * cols + 2 * cp;
-            float g0, g1, h0, h1;
-            if (DH_T) {
-                const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(dh) + i);
-                g0 = bf16_to_f32(uint16_t(u & 0xffffu));
-                g1 = bf16_to_f32(uint16_t(u >> 16));
-            } else {
-                const float2 u = *reinterpret_cast<const float2*>(static_cast<const float*>(dh) + i);
-                g0 = u.x;
-                g1 = u.y;
-            }
-            if (H_T) {
-                const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(h) + i);
-                h0 = bf16_to_f32(uint16_t(u & 0xffffu));
-                h1 = bf16_to_f32(uint16_t(u >> 16));
-            } else {
-                const float2 u = *reinterpret_cast<const float2*>(static_cast<const float*>(h) + i);
-                h0 = u.x;
-                h1 = u.y;
-            }
-            float z0 = h0 > 0.f ? g0 : g0 * (h0 + 1.f);
-            float z1 = h1 > 0.f ? g1 : g1 * (h1 + 1.f);
+            const int64_t i = int64_t(r) * cols + 4 * cq;
+            float g[4], hv[4], z[4];
+            load4<DH_T>(dh, i, g);
+            load4<H_T>(h, i, hv);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z[k] = hv[k] > 0.f ? g[k] : g[k] * (hv[k] + 1.f);
             if (DZ_T) {
-                const uint16_t b0 = f32_to_bf16(z0), b1 = f32_to_bf16(z1);
-                *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(dz) + i) = uint32_t(b0) | (uint32_t(b1) << 16);
-                z0 = bf16_to_f32(b0);  // bias grad from the stored (GEMM-visible) dz
-                z1 = bf16_to_f32(b1);
+                uint16_t b[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    b[k] = f32_to_bf16(z[k]);
+                    z[k] = bf16_to_f32(b[k]);  // bias grad from the stored (GEMM-visible) dz
+                }
+                *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dz) + i) =
+                    make_uint2(uint32_t(b[0]) | (uint32_t(b[1]) << 16), uint32_t(b[2]) | (uint32_t(b[3]) << 16));
             } else {
-                *reinterpret_cast<float2*>(static_cast<float*>(dz) + i) = make_float2(z0, z1);
+                *reinterpret_cast<float4*>(static_cast<float*>(dz) + i) = make_float4(z[0], z[1], z[2], z[3]);
             }
-            s0 += z0;
-            s1 += z1;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] += z[k];
         }
     }
-    red[2 * threadIdx.x] = s0;
-    red[2 * threadIdx.x + 1] = s1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[4 * threadIdx.x + k] = acc[k];
     __syncthreads();
     for (int c = threadIdx.x; c < cols; c += kEluThreads) {
         float t = 0.f;
-        for (int q = 0; q < nph; ++q) t += red[2 * (q * pairs) + c];
+        for (int q = 0; q < nph; ++q) t += red[4 * (q * quads) + c];
         partials[int64_t(blockIdx.x) * cols + c] = t;
     }
 }
@@ -424,7 +451,15 @@ __global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
     const int r = int(o / jb.dst_cols), c = int(o % jb.dst_cols);
     const float* src = jb.src + int64_t(r) * jb.src_cols + c;
     float s = 0.f;
-    for (int q = 0; q < jb.S; ++q) s += src[int64_t(q) * jb.src_n];
+    int q = 0;
+    for (; q + 8 <= jb.S; q += 8) {  // eight loads in flight, added in order (fixed summation order)
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[int64_t(q + u) * jb.src_n];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; q < jb.S; ++q) s += src[int64_t(q) * jb.src_n];
     jb.dst[int64_t(r) * jb.dst_stride + c] = s;
 }
 
@@ -553,7 +588,10 @@ int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, in
     return launched("k_obs_normalize");
 }
 
-int ppo_loss_blocks(int32_t mb_rows) { return (mb_rows + kLossThreads - 1) / kLossThreads; }
+int ppo_loss_blocks(int32_t mb_rows) {
+    const int rows_per_block = (kLossThreads / 32) * kLossRowsPerGroup;
+    return (mb_rows + rows_per_block - 1) / rows_per_block;
+}
 
 int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
                   const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
@@ -590,7 +628,7 @@ int ppo_elu_bwd_blocks(int32_t rows) { return (rows + kEluRows - 1) / kEluRows; 
 
 int ppo_elu_bwd(const void* dh, int32_t dh_dtype, const void* h, int32_t h_dtype, void* dz, int32_t dz_dtype,
                 int32_t rows, int32_t cols, float* partials, void* stream) {
-    if (cols % 64 || cols > 2 * kEluThreads) return fail(-1, "ppo_elu_bwd: cols must be a multiple of 64, <= 2048");
+    if (cols % 64 || cols > 4 * kEluThreads) return fail(-1, "ppo_elu_bwd: cols must be a multiple of 64, <= 4096");
     const dim3 grid(ppo_elu_bwd_blocks(rows)), block(kEluThreads);
     const int code = dh_dtype * 4 + h_dtype * 2 + dz_dtype;
     switch (code) {
