@@ -724,6 +724,8 @@ class A2CAgent:
             curr_frames = self.curr_frames * (self.world_size if self.multi_gpu else 1)
             self.frame += curr_frames
             should_exit = False
+            if step_time <= 0.0:  # graph replays: env steps are not separately timed
+                step_time = play_time
             self.last_stats = {"epoch": epoch_num, "frames": self.frame, "play_time": play_time,
                                "update_time": update_time, "step_time": step_time,
                                "fps_step": curr_frames / max(step_time, 1e-9),

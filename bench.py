@@ -14,6 +14,9 @@ Extra objects on the JSON line:
                   from HIP events recorded around every launch on its own stream, vs 8 TB/s HBM.
   cpu_baseline -- rank 0, N = 1: the CPU oracle (oracle/, a port of the same step) timed on this
                   host's cores on a bounded sample.
+  train        -- rank 0, N = 1 (BASELINE C4 per GPU, SURVEY §8d "env+PPO separately"): env-steps/s
+                  of the PPO trainer (scripts/bench_train.py: reference agent config, 32768 envs,
+                  horizon 32, 10 mini-epochs) -- reported beside `value`, never as `value`.
 """
 
 from __future__ import annotations
@@ -50,6 +53,8 @@ def parse():
     p.add_argument("--level", type=int, default=0, help="stone curriculum level (C3: 9)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-train", action="store_true", help="skip the env+PPO trainer measurement")
+    p.add_argument("--train-envs", type=int, default=32768)
     return p.parse_args()
 
 
@@ -182,8 +187,17 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(n, args.level, args.cpu_threads)
-        print(json.dumps(line), flush=True)
     env.close()
+    if rank == 0:
+        if world == 1 and not args.no_train:
+            sys.path.insert(0, os.path.join(ROOT, "scripts"))
+            import bench_train
+
+            try:
+                line["train"] = bench_train.measure(args.train_envs, epochs=2, warmup=2, verbose=False)
+            except Exception as e:  # reported, never fatal for the env metric
+                line["train"] = {"error": f"{type(e).__name__}: {e}"}
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

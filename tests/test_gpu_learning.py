@@ -278,3 +278,17 @@ def test_rollout_policy_sampling_kernel(tmp_path):
     f.step_ctr.fill_(0)
     f.policy_act(obs, out)
     assert torch.equal(first, out["actions"])  # same counter, same draws
+
+
+@pytest.mark.gpu
+def test_play_script_restores_trained_checkpoint(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "scripts", "reinforcement_learning", "rl_games"))
+    import play
+    import train
+
+    runner, _ = train.main(["--task", "Allsteps-v0", "--num_envs", "1024", "--max_iterations", "1", "--seed", "4",
+                            "--log_root", str(tmp_path)])
+    nn_dir = os.path.join(runner.agent.experiment_dir, "nn")
+    ckpt = os.path.join(nn_dir, sorted(os.listdir(nn_dir))[0])
+    out = play.main(["--task", "Allsteps-v0", "--num_envs", "256", "--checkpoint", ckpt, "--steps", "200"])
+    assert out["steps"] == 200 and out["episodes"] > 0 and math.isfinite(out["mean_reward"])
