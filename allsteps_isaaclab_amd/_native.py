@@ -145,7 +145,7 @@ def build_native(verbose: bool = False) -> str:
     subprocess.run(cmd, check=True)
     # PPO-update kernels (include/ppo.h) -> libppo_hip.so
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-I", INCLUDE, "-o", PPO_LIB_PATH, os.path.join(CSRC, "ppo_kernels.hip")]
+           "-I", INCLUDE, "-o", PPO_LIB_PATH, os.path.join(CSRC, "ppo_kernels.hip"), os.path.join(CSRC, "ppo_mlp.hip")]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

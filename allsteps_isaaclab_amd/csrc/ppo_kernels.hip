@@ -633,9 +633,10 @@ int ppo_elu_bwd(const void* dh, int32_t dh_dtype, const void* h, int32_t h_dtype
     const int code = dh_dtype * 4 + h_dtype * 2 + dz_dtype;
     switch (code) {
         case 0: hipLaunchKernelGGL((k_elu_bwd<0, 0, 0>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
+        case 1: hipLaunchKernelGGL((k_elu_bwd<0, 0, 1>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
         case 3: hipLaunchKernelGGL((k_elu_bwd<0, 1, 1>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
         case 7: hipLaunchKernelGGL((k_elu_bwd<1, 1, 1>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
-        default: return fail(-1, "ppo_elu_bwd: dtype combination (dh, h, dz) must be (f32,f32,f32), (f32,bf16,bf16) or (bf16,bf16,bf16)");
+        default: return fail(-1, "ppo_elu_bwd: dtype combination (dh, h, dz) must be (f32,f32,f32), (f32,f32,bf16), (f32,bf16,bf16) or (bf16,bf16,bf16)");
     }
     return launched("k_elu_bwd");
 }

@@ -48,6 +48,12 @@ class PpoReduceJob(C.Structure):
                 ("src_cols", C.c_int32), ("dst_cols", C.c_int32), ("dst_stride", C.c_int32), ("src_n", C.c_int64)]
 
 
+class PpoMlpFwd(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("w", C.c_void_p * 5), ("b", C.c_void_p * 5), ("wh", C.c_void_p),
+                ("bh", C.c_void_p), ("h", C.c_void_p * 4), ("h5", C.c_void_p), ("head", C.c_void_p),
+                ("rows", C.c_int32), ("nh", C.c_int32)]
+
+
 class PpoSeg(C.Structure):
     _fields_ = [("off", C.c_int64), ("len", C.c_int64), ("moff", C.c_int64), ("cols", C.c_int32),
                 ("mstride", C.c_int32)]
@@ -56,7 +62,8 @@ class PpoSeg(C.Structure):
 EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks", "ppo_obs_stats",
                     "ppo_obs_stats_update", "ppo_obs_normalize", "ppo_loss_blocks", "ppo_loss_grad",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
-                    "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add"]
+                    "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
+                    "ppo_mlp_forward"]
 
 
 def load() -> C.CDLL:
@@ -81,6 +88,7 @@ def load() -> C.CDLL:
     L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
     L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
     L.ppo_counter_add.argtypes = [V, I64, V]
+    L.ppo_mlp_forward.argtypes = [C.POINTER(PpoMlpFwd), V]
     for f in ("ppo_obs_stats_blocks", "ppo_loss_blocks", "ppo_elu_bwd_blocks"):
         getattr(L, f).argtypes = [I32]
     L.ppo_last_error.restype = C.c_char_p
@@ -193,6 +201,17 @@ class FusedPPOUpdate:
             self.mirror = None
             self.W_lp = [m.weight.detach() for m in self.linears]
             self.b_lp = [m.bias.detach() for m in self.linears]
+        # fused MFMA trunk (csrc/ppo_mlp.hip): bf16 mirror, 59 -> 256 x 5 ELU, heads <= 32
+        self.mfma_trunk = bool(self.bf16 and len(self.linears) == 5 and widths[1:] == [256] * 5 and self.k0 == 64
+                               and self.A + 1 <= 32 and getattr(agent, "config", {}).get("mfma_trunk", True))
+        if self.mfma_trunk:
+            a = PpoMlpFwd()
+            for i in range(5):
+                a.w[i] = self.W_lp[i].data_ptr()
+                o = flat.offset(self.linears[i].bias)
+                a.b[i] = flat.params[o:o + 256].data_ptr()
+            a.wh, a.bh, a.nh = self.Wh.data_ptr(), self.bh.data_ptr(), self.A + 1
+            self._mlp_args = a
         self.segs = (PpoSeg * max(len(segs), 1))(*segs)
         self.nseg = len(segs)
         c = agent.config
@@ -242,6 +261,17 @@ class FusedPPOUpdate:
         L, s, rms = self.L, self._stream(), self.rms
         _check(L.ppo_obs_normalize(_p(x), _p(idx), rows, self.obs_dim, _p(rms.running_mean), _p(rms.running_var),
                                    rms.epsilon, _p(h[0]), self.k0, int(self.bf16), s), "ppo_obs_normalize")
+        if self.mfma_trunk:
+            # one launch: 5 x (MFMA + bias + ELU) with the activations chained in registers, fp32 heads;
+            # stores layers 1..4 (bf16) and layer 5 (fp32) only when h has room for them (training)
+            a = self._mlp_args
+            a.x = h[0].data_ptr()
+            for i in range(4):
+                a.h[i] = h[i + 1].data_ptr() if len(h) > 1 else None
+            a.h5 = h_last_f.data_ptr() if h_last_f is not None else None
+            a.head, a.rows = head.data_ptr(), rows
+            _check(L.ppo_mlp_forward(C.byref(a), s), "ppo_mlp_forward")
+            return
         for i in range(len(self.linears)):  # z = h W^T + b ; h' = elu(z)
             out = h[i + 1]
             torch.addmm(self.b_lp[i], h[i], self.W_lp[i].t(), out=out)
@@ -255,8 +285,12 @@ class FusedPPOUpdate:
         dev, dt = self.dev, self.dt
         widths = [self.k0] + [m.out_features for m in self.linears]
         self.N = n_envs
-        self.hr = [torch.zeros(n_envs, w, device=dev, dtype=dt) for w in widths]
-        self.hr_last_f = torch.empty(n_envs, widths[-1], device=dev) if self.bf16 else self.hr[-1]
+        if self.mfma_trunk:  # activations stay in registers: only the input row block is materialised
+            self.hr = [torch.zeros(n_envs, widths[0], device=dev, dtype=dt)]
+            self.hr_last_f = None
+        else:
+            self.hr = [torch.zeros(n_envs, w, device=dev, dtype=dt) for w in widths]
+            self.hr_last_f = torch.empty(n_envs, widths[-1], device=dev) if self.bf16 else self.hr[-1]
         self.head_r = torch.empty(n_envs, self.A + 1, device=dev)
         self.zero_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.step_ctr = torch.zeros(1, device=dev, dtype=torch.int64)
@@ -329,7 +363,9 @@ class FusedPPOUpdate:
             n_out = m.out_features
             dz = self.dz[:, :n_out]
             # dz_i = elu'(h_{i+1}) * dh_{i+1}; bias grad from the per-block column sums
-            _check(L.ppo_elu_bwd(_p(dh), dh_t, _p(self.h[i + 1]), dt_code, _p(dz), dt_code, B, n_out,
+            last = i == nl - 1 and self.mfma_trunk  # layer 5 is kept in fp32 by the MFMA trunk
+            h_act, h_t = (self.h_last_f, 0) if last else (self.h[i + 1], dt_code)
+            _check(L.ppo_elu_bwd(_p(dh), dh_t, _p(h_act), h_t, _p(dz), dt_code, B, n_out,
                                  _p(self.elu_partials[i]), s),
                    "ppo_elu_bwd")
             job(self.elu_partials[i], self.gb[i], nblk, 1, n_out, n_out, n_out)

@@ -115,6 +115,26 @@ int ppo_policy_sample(const float* head, const float* logstd, int32_t A, int32_t
 /* *ctr += inc (one thread; orders after the kernels that read it) */
 int ppo_counter_add(int64_t* ctr, int64_t inc, void* stream);
 
+/* Fused actor-critic trunk forward on MFMA (bf16 in, fp32 accumulate): 5 layers x 256, ELU, then the
+ * fp32 heads.  x: rows x 64 bf16 (normalised obs, zero-padded 59 -> 64); w[0]: 256 x 64 bf16,
+ * w[1..4]: 256 x 256 bf16 (the trunk mirror); b[l]: 256 fp32; wh: nh x 256 fp32 ([mu.w | value.w]),
+ * bh: nh fp32 (nh <= 32).  Outputs (row-major, NULL = skip): h[0..3] = layers 1..4 (bf16 rows x 256),
+ * h5 = layer 5 in fp32 (rows x 256), head = rows x nh fp32.  Each wave keeps its 32 rows' activations
+ * in registers between layers (an MFMA accumulator tile is the next layer's B operand); each layer's
+ * weights are staged once per workgroup in LDS. */
+typedef struct {
+    const uint16_t* x;
+    const uint16_t* w[5];
+    const float* b[5];
+    const float* wh;
+    const float* bh;
+    uint16_t* h[4];
+    float* h5;
+    float* head;
+    int32_t rows, nh;
+} ppo_mlp_fwd_t;
+int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream);
+
 /* ||g||^2 partials (fp32, nblk = ppo_sqnorm_blocks()) */
 int ppo_sqnorm_blocks(void);
 int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream);

@@ -292,3 +292,57 @@ def test_play_script_restores_trained_checkpoint(tmp_path):
     ckpt = os.path.join(nn_dir, sorted(os.listdir(nn_dir))[0])
     out = play.main(["--task", "Allsteps-v0", "--num_envs", "256", "--checkpoint", ckpt, "--steps", "200"])
     assert out["steps"] == 200 and out["episodes"] > 0 and math.isfinite(out["mean_reward"])
+
+
+def _bf16_round(t):
+    return t.to(torch.bfloat16).float()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [32768, 1000])
+def test_fused_mlp_forward_kernel(rows):
+    """ppo_mlp_forward (MFMA, activations chained in registers) vs an fp32 torch statement of the same
+    rounding points: each hidden layer rounded to bf16 once, layer 5 and the heads in fp32."""
+    import ctypes as C
+
+    from allsteps_isaaclab_amd.learning import fused as FU
+
+    L = FU.load()
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    dev = "cuda:0"
+    x = torch.zeros(rows, 64, device=dev)
+    x[:, :59] = torch.randn(rows, 59, device=dev, generator=g).clamp(-5, 5)
+    xb = x.to(torch.bfloat16)
+    ws = [(torch.randn(256, 64 if i == 0 else 256, device=dev, generator=g) / (8 if i == 0 else 16)).to(torch.bfloat16)
+          for i in range(5)]
+    ws[0][:, 59:] = 0
+    bs = [torch.randn(256, device=dev, generator=g) * 0.1 for _ in range(5)]
+    wh = torch.randn(22, 256, device=dev, generator=g) / 16
+    bh = torch.randn(22, device=dev, generator=g) * 0.1
+    hs = [torch.empty(rows, 256, device=dev, dtype=torch.bfloat16) for _ in range(4)]
+    h5 = torch.empty(rows, 256, device=dev)
+    head = torch.empty(rows, 22, device=dev)
+    a = FU.PpoMlpFwd()
+    a.x = xb.data_ptr()
+    for i in range(5):
+        a.w[i] = ws[i].data_ptr()
+        a.b[i] = bs[i].data_ptr()
+    for i in range(4):
+        a.h[i] = hs[i].data_ptr()
+    a.wh, a.bh, a.h5, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), h5.data_ptr(), head.data_ptr(), rows, 22
+    FU._check(L.ppo_mlp_forward(C.byref(a), torch.cuda.current_stream().cuda_stream), "ppo_mlp_forward")
+    torch.cuda.synchronize()
+    hin = xb.float()
+    for i in range(5):
+        z = hin @ ws[i].float().t() + bs[i]
+        y = torch.nn.functional.elu(z)
+        if i < 4:
+            got = hs[i].float()
+            assert (got - _bf16_round(y)).abs().max().item() < 0.05, i
+            frac = ((got - _bf16_round(y)).abs() > 1e-6).float().mean().item()
+            assert frac < 0.02, (i, frac)  # only bf16 rounding-boundary flips
+            hin = got  # chain on the kernel's own rounding, as the kernel does
+        else:
+            torch.testing.assert_close(h5, y, rtol=2e-3, atol=2e-3)
+            ref_head = h5 @ wh.t() + bh
+            torch.testing.assert_close(head, ref_head, rtol=1e-4, atol=1e-4)
