@@ -433,6 +433,73 @@ __global__ void k_counter_add(int64_t* ctr, int64_t inc) {
     if (threadIdx.x == 0 && blockIdx.x == 0) *ctr += inc;
 }
 
+// ------------------------------------------------------------------------------ rollout bookkeeping
+
+constexpr int kPostThreads = 256;
+
+__global__ void __launch_bounds__(kPostThreads) k_rollout_post(const float* __restrict__ rew,
+                                                               const uint8_t* __restrict__ done,
+                                                               const uint8_t* __restrict__ tout,
+                                                               const float* __restrict__ val, int n, float scale,
+                                                               float shift, float gamma, int boot,
+                                                               float* __restrict__ shaped_out, float* __restrict__ cr,
+                                                               float* __restrict__ cs, float* __restrict__ cl,
+                                                               float* __restrict__ partials) {
+    __shared__ float red[kPostThreads / kWave][4];
+    const int i = blockIdx.x * kPostThreads + threadIdx.x;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (i < n) {
+        const float r = rew[i];
+        float sh = (r + shift) * scale;  // DefaultRewardsShaper
+        if (boot && tout[i]) sh = sh + gamma * val[i] * 1.f;  // value_bootstrap on time-outs
+        shaped_out[i] = sh;
+        const float r1 = cr[i] + r, s1 = cs[i] + sh, l1 = cl[i] + 1.f;
+        const bool d = done[i] != 0;
+        if (d) {
+            v[0] = r1;
+            v[1] = s1;
+            v[2] = l1;
+            v[3] = 1.f;
+        }
+        cr[i] = d ? 0.f : r1;  // current_* *= not_dones
+        cs[i] = d ? 0.f : s1;
+        cl[i] = d ? 0.f : l1;
+    }
+    const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float t = wave_sum(v[k]);
+        if (lane == 0) red[w][k] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        float t = 0.f;
+        for (int q = 0; q < kPostThreads / kWave; ++q) t += red[q][threadIdx.x];
+        partials[blockIdx.x * 4 + threadIdx.x] = t;
+    }
+}
+
+__global__ void __launch_bounds__(64) k_meter_update(const float* __restrict__ partials, int nblk, float max_size,
+                                                     float* __restrict__ mean3, float* __restrict__ size3) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int b = threadIdx.x; b < nblk; b += kWave) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] += partials[b * 4 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] = wave_sum(s[k]);
+    if (threadIdx.x != 0 || s[3] <= 0.f) return;  // no finished episode: meters unchanged
+    // torch_ext.AverageMeter.update: size = min(count, max_size), old = min(max_size - size, current)
+    const float size = fminf(s[3], max_size);
+    for (int k = 0; k < 3; ++k) {
+        const float new_mean = s[k] / s[3];
+        const float old = fminf(max_size - size, size3[k]);
+        const float tot = old + size;
+        mean3[k] = (mean3[k] * old + new_mean * size) / tot;
+        size3[k] = tot;
+    }
+}
+
 // ------------------------------------------------------------------------------ partial-row reductions
 
 struct JobTable {
@@ -681,6 +748,23 @@ int ppo_policy_sample(const float* head, const float* logstd, int32_t A, int32_t
 int ppo_counter_add(int64_t* ctr, int64_t inc, void* stream) {
     hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(64), 0, S(stream), ctr, inc);
     return launched("k_counter_add");
+}
+
+int ppo_rollout_post_blocks(int32_t n) { return (n + kPostThreads - 1) / kPostThreads; }
+
+int ppo_rollout_post(const float* reward, const uint8_t* done, const uint8_t* time_out, const float* value,
+                     int32_t n, float scale, float shift, float gamma, int32_t bootstrap, float* shaped_out,
+                     float* cur_r, float* cur_s, float* cur_l, float* partials, void* stream) {
+    if (n <= 0 || (bootstrap && (!time_out || !value))) return fail(-1, "ppo_rollout_post: bad arguments");
+    hipLaunchKernelGGL(k_rollout_post, dim3(ppo_rollout_post_blocks(n)), dim3(kPostThreads), 0, S(stream), reward,
+                       done, time_out, value, n, scale, shift, gamma, bootstrap, shaped_out, cur_r, cur_s, cur_l,
+                       partials);
+    return launched("k_rollout_post");
+}
+
+int ppo_meter_update(const float* partials, int32_t nblk, float max_size, float* mean3, float* size3, void* stream) {
+    hipLaunchKernelGGL(k_meter_update, dim3(1), dim3(kWave), 0, S(stream), partials, nblk, max_size, mean3, size3);
+    return launched("k_meter_update");
 }
 
 int ppo_sqnorm_blocks(void) { return kNormBlocks; }

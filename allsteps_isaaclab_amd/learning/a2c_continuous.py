@@ -285,6 +285,7 @@ class A2CAgent:
         self.actions_low = torch.as_tensor(action_space.low, dtype=torch.float32, device=self.device)
         self.actions_high = torch.as_tensor(action_space.high, dtype=torch.float32, device=self.device)
         self.clip_actions = bool(config.get("clip_actions", True))
+        self._unit_box = bool(torch.all(self.actions_low == -1.0) and torch.all(self.actions_high == 1.0))
         self.num_agents = int(self.env_info.get("agents", 1))
         self.value_size = int(self.env_info.get("value_size", 1))
 
@@ -398,6 +399,7 @@ class A2CAgent:
             self._ds_static: dict = {}
             if self._play_graphs is not None:
                 self.fused.init_rollout(N, int(self.params.get("seed", 0)) * 7919 + self.rank)
+                self.fused.init_bookkeeping(self)
 
     # ------------------------------------------------------------------ env / policy
     def obs_to_tensors(self, obs):
@@ -412,6 +414,8 @@ class A2CAgent:
         if not self.clip_actions:
             return actions
         a = torch.clamp(actions, -1.0, 1.0)
+        if self._unit_box:  # rescale_actions to [-1, 1] is the identity
+            return a
         d = (self.actions_high - self.actions_low) / 2.0
         m = (self.actions_high + self.actions_low) / 2.0
         return a * d + m
@@ -457,21 +461,9 @@ class A2CAgent:
         td["obses"][n].copy_(obs)
         td["dones"][n].copy_(self._dones_buf)
         obs2, rewards, dones, infos = self.env_step(res["actions"])
-        shaped = self.rewards_shaper(rewards)
-        if self.value_bootstrap and "time_outs" in infos:
-            shaped = shaped + self.gamma * res["values"] * infos["time_outs"].unsqueeze(1).float()
-        td["rewards"][n].copy_(shaped)
-        self.current_rewards += rewards
-        self.current_shaped_rewards += shaped
-        self.current_lengths += 1
-        done = dones.bool()
-        self.game_rewards.update(self.current_rewards, done)
-        self.game_shaped_rewards.update(self.current_shaped_rewards, done)
-        self.game_lengths.update(self.current_lengths.unsqueeze(1), done)
-        not_dones = 1.0 - dones.float()
-        self.current_rewards *= not_dones.unsqueeze(1)
-        self.current_shaped_rewards *= not_dones.unsqueeze(1)
-        self.current_lengths *= not_dones
+        # shaping + value bootstrap + episode sums + AverageMeters: two launches (fused.rollout_post)
+        self.fused.rollout_post(self, rewards.reshape(-1), dones, infos.get("time_outs"), res["values"].reshape(-1),
+                                td["rewards"][n].reshape(-1))
         self._obs_buf.copy_(obs2["obs"])
         self._dones_buf.copy_(dones)
 

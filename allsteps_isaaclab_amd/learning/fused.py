@@ -63,7 +63,7 @@ EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks",
                     "ppo_obs_stats_update", "ppo_obs_normalize", "ppo_loss_blocks", "ppo_loss_grad",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
-                    "ppo_mlp_forward"]
+                    "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update"]
 
 
 def load() -> C.CDLL:
@@ -89,6 +89,9 @@ def load() -> C.CDLL:
     L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
     L.ppo_counter_add.argtypes = [V, I64, V]
     L.ppo_mlp_forward.argtypes = [C.POINTER(PpoMlpFwd), V]
+    L.ppo_rollout_post_blocks.argtypes = [I32]
+    L.ppo_rollout_post.argtypes = [V, V, V, V, I32, F32, F32, F32, I32, V, V, V, V, V, V]
+    L.ppo_meter_update.argtypes = [V, I32, F32, V, V, V]
     for f in ("ppo_obs_stats_blocks", "ppo_loss_blocks", "ppo_elu_bwd_blocks"):
         getattr(L, f).argtypes = [I32]
     L.ppo_last_error.restype = C.c_char_p
@@ -313,6 +316,37 @@ class FusedPPOUpdate:
                                         _p(out["neglogpacs"]), _p(out["values"]), _p(out["mus"]), _p(out["sigmas"]),
                                         s), "ppo_policy_sample")
         _check(self.L.ppo_counter_add(_p(self.step_ctr), 1, s), "ppo_counter_add")
+
+    def init_bookkeeping(self, agent) -> None:
+        """Bind the rollout bookkeeping kernel to the agent's episode buffers; the three AverageMeters
+        are re-homed into one (2, 3) device block [means | sizes] the meter kernel updates."""
+        n = agent.num_actors * agent.num_agents
+        blk = torch.zeros(2, 3, device=self.dev)
+        for k, m in enumerate((agent.game_rewards, agent.game_shaped_rewards, agent.game_lengths)):
+            blk[0, k] = m.mean.reshape(-1)[0]
+            blk[1, k] = m.current_size
+            m.mean = blk[0, k:k + 1]
+            m.current_size = blk[1, k]
+        self.meters = blk
+        self.post_partials = torch.zeros(self.L.ppo_rollout_post_blocks(n), 4, device=self.dev)
+        self.max_games = float(agent.games_to_track)
+
+    def rollout_post(self, agent, rewards, dones, time_outs, values, shaped_out) -> None:
+        """play_steps' per-step bookkeeping in two launches (shaping, bootstrap, episode sums, meters)."""
+        L, s = self.L, self._stream()
+        sh = agent.rewards_shaper
+        if sh.min_val != -float("inf") or sh.max_val != float("inf"):
+            raise NotImplementedError("reward clipping in the fused rollout bookkeeping")
+        n = rewards.shape[0]
+        boot = int(agent.value_bootstrap and time_outs is not None)
+        d = dones if dones.dtype == torch.uint8 else dones.view(torch.uint8)
+        t = None if time_outs is None else (time_outs if time_outs.dtype == torch.uint8 else time_outs.view(torch.uint8))
+        _check(L.ppo_rollout_post(_p(rewards), _p(d), _p(t), _p(values), n, float(sh.scale_value),
+                                  float(sh.shift_value), float(agent.gamma), boot, _p(shaped_out),
+                                  _p(agent.current_rewards), _p(agent.current_shaped_rewards),
+                                  _p(agent.current_lengths), _p(self.post_partials), s), "ppo_rollout_post")
+        _check(L.ppo_meter_update(_p(self.post_partials), self.post_partials.shape[0], self.max_games,
+                                  _p(self.meters[0]), _p(self.meters[1]), s), "ppo_meter_update")
 
     @torch.no_grad()
     def policy_values(self, obs: torch.Tensor) -> torch.Tensor:

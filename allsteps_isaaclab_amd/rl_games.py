@@ -130,7 +130,8 @@ class RlGamesVecEnvWrapper(IVecEnv):
         return self._process_obs(obs_dict)
 
     def step(self, actions: torch.Tensor):
-        a = torch.clamp(actions.detach().clone().to(device=self._sim_device), -self._clip_actions, self._clip_actions)
+        # clamp returns a new tensor (the reference's detach().clone() + clamp in one op)
+        a = torch.clamp(actions.detach().to(device=self._sim_device), -self._clip_actions, self._clip_actions)
         obs_dict, rew, terminated, truncated, extras = self.env.step(a)
         if not self.unwrapped.cfg.is_finite_horizon:
             extras["time_outs"] = truncated.to(device=self._rl_device)
@@ -149,7 +150,10 @@ class RlGamesVecEnvWrapper(IVecEnv):
         return self.env.close()
 
     def _process_obs(self, obs_dict):
-        obs = torch.clamp(obs_dict["policy"], -self._clip_obs, self._clip_obs).to(device=self._rl_device).clone()
+        o = obs_dict["policy"]
+        # clamp to +-inf is the identity (NaN stays NaN): then only the reference's defensive clone
+        obs = (o.clone() if self._clip_obs == float("inf") else torch.clamp(o, -self._clip_obs, self._clip_obs)
+               ).to(device=self._rl_device)
         if self.rlg_num_states == 0:
             return obs
         if "critic" not in obs_dict:

@@ -135,6 +135,19 @@ typedef struct {
 } ppo_mlp_fwd_t;
 int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream);
 
+/* Rollout bookkeeping of one step (a2c_common.play_steps after env_step), per env:
+ *   shaped = (reward + shift) * scale [+ gamma * value * time_out]  -> shaped_out (td rewards[n])
+ *   cur_r += reward; cur_s += shaped; cur_l += 1
+ *   for done envs: block partials of (cur_r, cur_s, cur_l, 1) -> partials[nblk][4], then cur_* = 0
+ * then ppo_meter_update folds the finished episodes into the three AverageMeters (rl_games
+ * torch_ext.AverageMeter: mean of the last max_size games) -- no host round trip, no nonzero(). */
+int ppo_rollout_post_blocks(int32_t n);
+int ppo_rollout_post(const float* reward, const uint8_t* done, const uint8_t* time_out, const float* value,
+                     int32_t n, float scale, float shift, float gamma, int32_t bootstrap, float* shaped_out,
+                     float* cur_r, float* cur_s, float* cur_l, float* partials, void* stream);
+/* meters: mean[3] (reward, shaped reward, length), size[3] (current_size) */
+int ppo_meter_update(const float* partials, int32_t nblk, float max_size, float* mean3, float* size3, void* stream);
+
 /* ||g||^2 partials (fp32, nblk = ppo_sqnorm_blocks()) */
 int ppo_sqnorm_blocks(void);
 int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream);

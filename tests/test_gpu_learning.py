@@ -346,3 +346,49 @@ def test_fused_mlp_forward_kernel(rows):
             torch.testing.assert_close(h5, y, rtol=2e-3, atol=2e-3)
             ref_head = h5 @ wh.t() + bh
             torch.testing.assert_close(head, ref_head, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_rollout_bookkeeping_kernel_matches_reference_ops(tmp_path):
+    """ppo_rollout_post + ppo_meter_update == the play_steps tensor ops (shaping, value bootstrap,
+    episode sums, AverageMeter updates, reset of the sums) over several steps."""
+    from allsteps_isaaclab_amd.learning import a2c_continuous as A
+
+    ref, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path)
+    f = fus.fused
+    n = 256
+    fus.current_rewards = torch.zeros(n, 1, device="cuda:0")
+    fus.current_shaped_rewards = torch.zeros(n, 1, device="cuda:0")
+    fus.current_lengths = torch.zeros(n, device="cuda:0")
+    fus.game_rewards = A.AverageMeter(1, 100, "cuda:0")
+    fus.game_shaped_rewards = A.AverageMeter(1, 100, "cuda:0")
+    fus.game_lengths = A.AverageMeter(1, 100, "cuda:0")
+    f.init_bookkeeping(fus)
+    cr, cs, cl = (torch.zeros(n, 1, device="cuda:0"), torch.zeros(n, 1, device="cuda:0"), torch.zeros(n, device="cuda:0"))
+    meters = [A.AverageMeter(1, 100, "cuda:0") for _ in range(3)]
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+    for step in range(40):
+        rew = torch.randn(n, device="cuda:0", generator=g)
+        done = torch.rand(n, device="cuda:0", generator=g) < (0.02 if step < 20 else 0.3)
+        tout = done & (torch.rand(n, device="cuda:0", generator=g) < 0.5)
+        val = torch.randn(n, 1, device="cuda:0", generator=g)
+        out = torch.empty(n, device="cuda:0")
+        f.rollout_post(fus, rew, done, tout, val.reshape(-1), out)
+        shaped = fus.rewards_shaper(rew.unsqueeze(1)) + fus.gamma * val * tout.unsqueeze(1).float()
+        torch.testing.assert_close(out, shaped.reshape(-1))
+        cr += rew.unsqueeze(1)
+        cs += shaped
+        cl += 1
+        meters[0].update(cr, done)
+        meters[1].update(cs, done)
+        meters[2].update(cl.unsqueeze(1), done)
+        nd = 1.0 - done.float()
+        cr *= nd.unsqueeze(1)
+        cs *= nd.unsqueeze(1)
+        cl *= nd
+        torch.testing.assert_close(fus.current_rewards, cr)
+        torch.testing.assert_close(fus.current_shaped_rewards, cs, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(fus.current_lengths, cl)
+        for m, mm in zip(meters, (fus.game_rewards, fus.game_shaped_rewards, fus.game_lengths)):
+            torch.testing.assert_close(mm.mean.reshape(-1), m.mean.reshape(-1), rtol=1e-5, atol=1e-5)
+            assert float(mm.current_size) == float(m.current_size)
