@@ -24,6 +24,14 @@ int fail(int code, const char* what) {
     return code;
 }
 
+}  // namespace
+
+namespace ppo_detail {
+void set_error(const char* msg) { snprintf(g_err, sizeof(g_err), "%s", msg); }
+}  // namespace ppo_detail
+
+namespace {
+
 int launched(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -120,10 +128,11 @@ __global__ void __launch_bounds__(64) k_obs_stats_update(const double* __restric
 
 __global__ void k_obs_normalize(const float* __restrict__ x, const int32_t* __restrict__ mb_idx, int mb_rows, int cols,
                                 const double* __restrict__ mean, const double* __restrict__ var, float eps,
-                                void* __restrict__ out, int out_stride, int out_bf16) {
-    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= int64_t(mb_rows) * out_stride) return;
-    const int r = int(i / out_stride), c = int(i % out_stride);
+                                void* __restrict__ out, int out_cols, int out_stride, int out_bf16) {
+    const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= int64_t(mb_rows) * out_cols) return;
+    const int r = int(e / out_cols), c = int(e % out_cols);
+    const int64_t i = int64_t(r) * out_stride + c;
     float y = 0.f;
     if (c < cols) {
         const float v = x[(int64_t(*mb_idx) * mb_rows + r) * cols + c];
@@ -146,7 +155,7 @@ __device__ __forceinline__ float max_grad(float u1, float u2, float g1, float g2
 // One row per 32-lane group: lane j < A owns action j, lane A owns the value; row sums by xor
 // shuffles inside the group.  Loads of a row's A floats are contiguous across lanes (coalesced).
 // Each lane keeps running sums for its own column over the rows its group visits.
-constexpr int kLossRowsPerGroup = 16;
+constexpr int kLossRowsPerGroup = 4;
 
 template <int A>
 __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
@@ -596,7 +605,8 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
             const ppo_seg_t& sg = segs.s[k];
             if (i >= sg.off && i < sg.off + sg.len) {
                 const int64_t j = i - sg.off;
-                mirror[sg.moff + (j / sg.cols) * sg.mstride + (j % sg.cols)] = f32_to_bf16(pi);
+                const int64_t r = j / sg.cols, c = j % sg.cols;
+                mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] = f32_to_bf16(pi);
             }
         }
     }
@@ -646,12 +656,12 @@ int ppo_obs_stats_update(const double* partials, int32_t nblk, int32_t cols, int
 }
 
 int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_t cols, const double* running_mean,
-                      const double* running_var, float eps, void* out, int32_t out_stride, int32_t out_bf16,
-                      void* stream) {
-    if (out_stride < cols) return fail(-1, "ppo_obs_normalize: out_stride < cols");
-    const int64_t n = int64_t(mb_rows) * out_stride;
+                      const double* running_var, float eps, void* out, int32_t out_cols, int32_t out_stride,
+                      int32_t out_bf16, void* stream) {
+    if (out_cols < cols || out_stride < out_cols) return fail(-1, "ppo_obs_normalize: need cols <= out_cols <= out_stride");
+    const int64_t n = int64_t(mb_rows) * out_cols;
     hipLaunchKernelGGL(k_obs_normalize, dim3(unsigned((n + 255) / 256)), dim3(256), 0, S(stream), x, mb_idx, mb_rows,
-                       cols, running_mean, running_var, eps, out, out_stride, out_bf16);
+                       cols, running_mean, running_var, eps, out, out_cols, out_stride, out_bf16);
     return launched("k_obs_normalize");
 }
 
@@ -782,7 +792,9 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
     t.n = mirror_bf16 ? nseg : 0;
     for (int k = 0; k < t.n; ++k) {
         t.s[k] = segs_host[k];
-        if (t.s[k].cols <= 0 || t.s[k].mstride < t.s[k].cols) return fail(-1, "ppo_adam: bad segment");
+        const int64_t rows = t.s[k].cols > 0 ? t.s[k].len / t.s[k].cols : 0;
+        if (t.s[k].cols <= 0 || t.s[k].mstride < (t.s[k].trans ? rows : t.s[k].cols))
+            return fail(-1, "ppo_adam: bad segment");
     }
     hipLaunchKernelGGL(k_adam, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0, S(stream),
                        p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,

@@ -15,6 +15,10 @@
 
 #include "ppo.h"
 
+namespace ppo_detail {
+void set_error(const char* msg);
+}
+
 #ifndef PPO_MLP_DBG
 #define PPO_MLP_DBG 0
 #endif
@@ -33,7 +37,7 @@ constexpr int kPad = 8;              // bf16 elements of padding per LDS row (16
 constexpr int kWBytes = kHid * (kHid + kPad) * 2;  // 135168 B: one 256 x 256 layer
 constexpr int kLdsBytes = kWBytes + 5 * kHid * 4;   // + the five bias vectors (fp32)
 
-thread_local char g_err[256] = "";
+char g_err[256];  // formatted here, published through ppo_last_error() (ppo_kernels.hip)
 
 union Frag {
     bf16x8 v;
@@ -123,7 +127,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
             f.q[0] = make_uint2(0, 0);
             f.q[1] = make_uint2(0, 0);
             if (kt < kK0 / 32 && live) {
-                const uint16_t* p = a.x + int64_t(row) * kK0 + kt * 32 + 16 * s + 4 * h;
+                const uint16_t* p = a.x + int64_t(row) * a.x_stride + kt * 32 + 16 * s + 4 * h;
                 f.q[0] = *reinterpret_cast<const uint2*>(p);
                 f.q[1] = *reinterpret_cast<const uint2*>(p + 8);
             }
@@ -175,7 +179,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int c = ot * 32 + 8 * g + 4 * h;
-                    if (hout) *reinterpret_cast<uint2*>(hout + int64_t(row) * kHid + c) = f[g >> 1].q[g & 1];
+                    if (hout) *reinterpret_cast<uint2*>(hout + int64_t(row) * a.h_stride + c) = f[g >> 1].q[g & 1];
                     if (l == 4 && a.h5)
                         *reinterpret_cast<float4*>(a.h5 + int64_t(row) * kHid + c) =
                             make_float4(acc[ot][4 * g], acc[ot][4 * g + 1], acc[ot][4 * g + 2], acc[ot][4 * g + 3]);
@@ -223,11 +227,133 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
     }
 }
 
+// ------------------------------------------------------------------------------ backward chain
+
+__global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const int j = lane & 31, h = lane >> 5, i = lane & 31;
+    const int row = blockIdx.x * kRowsPerBlock + wave * 32 + j;
+    const bool live = row < a.rows;
+    constexpr int kHs = kHid + 4;
+    // dh5 = Wh^T dhead: A[feature i][k] = wh[k][feature], B[k][batch j] = dhead[j][k]; k = 2t + h
+    float* wl = reinterpret_cast<float*>(lds);
+    {
+        constexpr int per = 32 * kHid / 4 / (64 * kWaves);
+        float4 v[per];
+#pragma unroll
+        for (int u = 0; u < per; ++u) {
+            const int c = u * (64 * kWaves) + threadIdx.x;
+            const int o = c / (kHid / 4), col = (c % (kHid / 4)) * 4;
+            v[u] = o < a.nh ? *reinterpret_cast<const float4*>(a.wh + o * kHid + col) : make_float4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < per; ++u) {
+            const int c = u * (64 * kWaves) + threadIdx.x;
+            *reinterpret_cast<float4*>(wl + (c / (kHid / 4)) * kHs + (c % (kHid / 4)) * 4) = v[u];
+        }
+    }
+    float bq[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const int k = 2 * t + h;
+        bq[t] = (live && k < a.nh) ? a.dhead[int64_t(row) * a.nh + k] : 0.f;
+    }
+    __syncthreads();
+    f32x16 acc[kTiles];
+#pragma unroll
+    for (int ot = 0; ot < kTiles; ++ot) acc[ot] = f32x16{};
+    const int nsteps = (a.nh + 1) / 2;
+    for (int t = 0; t < nsteps; ++t) {
+        const int k = 2 * t + h;
+#pragma unroll
+        for (int ot = 0; ot < kTiles; ++ot)
+            acc[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[k * kHs + ot * 32 + i], bq[t], acc[ot], 0, 0, 0);
+    }
+    bf16x8 xb[kTiles][2];
+    for (int l = 4; l >= 0; --l) {
+        // dz_l = dh * elu'(y_l), y_l = layer-l activations (layer 5 in fp32, the others bf16)
+        uint16_t* __restrict__ dzo = a.dz[l];
+#pragma unroll
+        for (int ot = 0; ot < kTiles; ++ot) {
+            float y[16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int c = ot * 32 + 8 * g + 4 * h;
+                if (!live) {
+                    y[4 * g] = y[4 * g + 1] = y[4 * g + 2] = y[4 * g + 3] = 0.f;
+                } else if (l == 4) {
+                    const float4 q = *reinterpret_cast<const float4*>(a.h5 + int64_t(row) * kHid + c);
+                    y[4 * g] = q.x;
+                    y[4 * g + 1] = q.y;
+                    y[4 * g + 2] = q.z;
+                    y[4 * g + 3] = q.w;
+                } else {
+                    Frag ff;
+                    ff.q[0] = *reinterpret_cast<const uint2*>(a.h[l] + int64_t(row) * a.h_stride + c);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) y[4 * g + e] = float(ff.v[e]);
+                }
+            }
+            Frag f[2];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float dz = y[r] > 0.f ? acc[ot][r] : acc[ot][r] * (y[r] + 1.f);
+                f[r >> 3].v[r & 7] = (__bf16)dz;
+            }
+            xb[ot][0] = f[0].v;
+            xb[ot][1] = f[1].v;
+            if (live) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    *reinterpret_cast<uint2*>(dzo + int64_t(row) * kHid + ot * 32 + 8 * g + 4 * h) = f[g >> 1].q[g & 1];
+            }
+        }
+        if (l == 0) break;
+        // dh of layer l's input = W_l^T dz_l
+        __syncthreads();
+        stage_w<kHid>(lds, a.wt[l - 1]);
+        __syncthreads();
+        layer_mma<kHid>(lds, xb, acc, lane);
+    }
+}
+
 }  // namespace
 
+extern "C" int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream) {
+    if (!args_host || !args_host->dhead || args_host->nh <= 0 || args_host->nh > 32 || args_host->rows <= 0 ||
+        args_host->h_stride < kHid) {
+        snprintf(g_err, sizeof(g_err), "ppo_mlp_backward: bad arguments");
+        ppo_detail::set_error(g_err);
+        return -1;
+    }
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_mlp_bwd), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kWBytes) != hipSuccess) {
+            snprintf(g_err, sizeof(g_err), "ppo_mlp_backward: cannot reserve %d B of LDS", kWBytes);
+        ppo_detail::set_error(g_err);
+            return -2;
+        }
+        attr = true;
+    }
+    const int blocks = (args_host->rows + kRowsPerBlock - 1) / kRowsPerBlock;
+    hipLaunchKernelGGL(k_mlp_bwd, dim3(blocks), dim3(64 * kWaves), kWBytes, static_cast<hipStream_t>(stream),
+                       *args_host);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "k_mlp_bwd: %s", hipGetErrorString(e));
+        ppo_detail::set_error(g_err);
+        return -2;
+    }
+    return 0;
+}
+
 extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
-    if (!args_host || !args_host->x || args_host->nh <= 0 || args_host->nh > 32 || args_host->rows <= 0) {
+    if (!args_host || !args_host->x || args_host->nh <= 0 || args_host->nh > 32 || args_host->rows <= 0 ||
+        args_host->x_stride < kK0 || args_host->h_stride < kHid || (args_host->x_stride % 4) || (args_host->h_stride % 4)) {
         snprintf(g_err, sizeof(g_err), "ppo_mlp_forward: bad arguments");
+        ppo_detail::set_error(g_err);
         return -1;
     }
     static bool attr = false;
@@ -235,6 +361,7 @@ extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_mlp_fwd), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kLdsBytes) != hipSuccess) {
             snprintf(g_err, sizeof(g_err), "ppo_mlp_forward: cannot reserve %d B of LDS", kLdsBytes);
+        ppo_detail::set_error(g_err);
             return -2;
         }
         attr = true;
@@ -245,6 +372,7 @@ extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         snprintf(g_err, sizeof(g_err), "k_mlp_fwd: %s", hipGetErrorString(e));
+        ppo_detail::set_error(g_err);
         return -2;
     }
     return 0;

@@ -51,19 +51,26 @@ class PpoReduceJob(C.Structure):
 class PpoMlpFwd(C.Structure):
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p * 5), ("b", C.c_void_p * 5), ("wh", C.c_void_p),
                 ("bh", C.c_void_p), ("h", C.c_void_p * 4), ("h5", C.c_void_p), ("head", C.c_void_p),
-                ("rows", C.c_int32), ("nh", C.c_int32)]
+                ("rows", C.c_int32), ("nh", C.c_int32), ("x_stride", C.c_int32), ("h_stride", C.c_int32)]
+
+
+class PpoMlpBwd(C.Structure):
+    _fields_ = [("dhead", C.c_void_p), ("wh", C.c_void_p), ("wt", C.c_void_p * 4), ("h5", C.c_void_p),
+                ("h", C.c_void_p * 4), ("dz", C.c_void_p * 5), ("rows", C.c_int32), ("nh", C.c_int32),
+                ("h_stride", C.c_int32)]
 
 
 class PpoSeg(C.Structure):
     _fields_ = [("off", C.c_int64), ("len", C.c_int64), ("moff", C.c_int64), ("cols", C.c_int32),
-                ("mstride", C.c_int32)]
+                ("mstride", C.c_int32), ("trans", C.c_int32)]
 
 
 EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks", "ppo_obs_stats",
                     "ppo_obs_stats_update", "ppo_obs_normalize", "ppo_loss_blocks", "ppo_loss_grad",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
-                    "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update"]
+                    "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update",
+                    "ppo_mlp_backward"]
 
 
 def load() -> C.CDLL:
@@ -78,7 +85,7 @@ def load() -> C.CDLL:
     V, I32, I64, F32, F64 = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double
     L.ppo_obs_stats.argtypes = [V, V, I32, I32, V, V]
     L.ppo_obs_stats_update.argtypes = [V, I32, I32, I32, V, V, V, V]
-    L.ppo_obs_normalize.argtypes = [V, V, I32, I32, V, V, F32, V, I32, I32, V]
+    L.ppo_obs_normalize.argtypes = [V, V, I32, I32, V, V, F32, V, I32, I32, I32, V]
     L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V]
     L.ppo_loss_finalize.argtypes = [V, I32, I32, I32, F32, V, V, V, V, V, V]
     L.ppo_elu_bwd.argtypes = [V, I32, V, I32, V, I32, I32, I32, V, V]
@@ -89,6 +96,7 @@ def load() -> C.CDLL:
     L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
     L.ppo_counter_add.argtypes = [V, I64, V]
     L.ppo_mlp_forward.argtypes = [C.POINTER(PpoMlpFwd), V]
+    L.ppo_mlp_backward.argtypes = [C.POINTER(PpoMlpBwd), V]
     L.ppo_rollout_post_blocks.argtypes = [I32]
     L.ppo_rollout_post.argtypes = [V, V, V, V, I32, F32, F32, F32, I32, V, V, V, V, V, V]
     L.ppo_meter_update.argtypes = [V, I32, F32, V, V, V]
@@ -145,20 +153,34 @@ class FusedPPOUpdate:
         self.flat = flat
         B, dev, dt = self.mb, self.dev, self.dt
         widths = [self.k0] + [m.out_features for m in self.linears]
-        self.h = [torch.zeros(B, w, device=dev, dtype=dt) for w in widths]
-        self.h_last_f = torch.empty(B, widths[-1], device=dev) if self.bf16 else self.h[-1]
-        self.head = torch.empty(B, self.A + 1, device=dev)
-        self.dhead = torch.empty(B, self.A + 1, device=dev)
         wmax = max(widths[1:])
         if any(w != wmax for w in widths[1:]):
             raise NotImplementedError("the fused update expects equal hidden widths (the agent's [256] x 5)")
-        self.dz = torch.empty(B, wmax, device=dev, dtype=dt)
-        self.dh = torch.empty(B, wmax, device=dev, dtype=dt)
-        self.dh_last = torch.empty(B, widths[-1], device=dev)  # fp32 from the heads
-        self.S = _split(B)
+        # fused MFMA trunk (csrc/ppo_mlp.hip): bf16 mirror, 59 -> 256 x 5 ELU, heads <= 32
+        self.mfma_trunk = bool(self.bf16 and len(self.linears) == 5 and widths[1:] == [256] * 5 and self.k0 == 64
+                               and self.A + 1 <= 32 and getattr(agent, "config", {}).get("mfma_trunk", True))
         L = self.L
+        if self.mfma_trunk:
+            # layer inputs carry a constant ones column (x: col 64 of 72, hidden: col 256 of 264), so the
+            # split-K weight-gradient GEMM also yields the bias gradient (its column `in`)
+            self.h = [torch.zeros(B, 72, device=dev, dtype=dt)] + [torch.zeros(B, 264, device=dev, dtype=dt)
+                                                                     for _ in range(4)]
+            self.h[0][:, 64] = 1.0
+            for t in self.h[1:]:
+                t[:, 256] = 1.0
+            self.h_last_f = torch.empty(B, 256, device=dev)
+            self.dzs = [torch.empty(B, 256, device=dev, dtype=dt) for _ in range(5)]
+        else:
+            self.h = [torch.zeros(B, w, device=dev, dtype=dt) for w in widths]
+            self.h_last_f = torch.empty(B, widths[-1], device=dev) if self.bf16 else self.h[-1]
+            self.dz = torch.empty(B, wmax, device=dev, dtype=dt)
+            self.dh = torch.empty(B, wmax, device=dev, dtype=dt)
+            self.dh_last = torch.empty(B, widths[-1], device=dev)  # fp32 from the heads
+            self.elu_partials = torch.empty(len(self.linears), L.ppo_elu_bwd_blocks(B), wmax, device=dev)
+        self.head = torch.empty(B, self.A + 1, device=dev)
+        self.dhead = torch.empty(B, self.A + 1, device=dev)
+        self.S = _split(B)
         self.loss_partials = torch.empty(L.ppo_loss_blocks(B), 2 * self.A + 1 + PPO_LOSS_NSTAT, device=dev)
-        self.elu_partials = torch.empty(len(self.linears), L.ppo_elu_bwd_blocks(B), wmax, device=dev)
         self.stat_partials = torch.empty(L.ppo_obs_stats_blocks(B) * 2 * 64, device=dev, dtype=torch.float64)
         self.norm_partials = torch.empty(L.ppo_sqnorm_blocks(), device=dev)
         self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -190,23 +212,28 @@ class FusedPPOUpdate:
         if self.bf16:
             sizes = [m.out_features * (self.k0 if i == 0 else m.in_features) + m.out_features
                      for i, m in enumerate(self.linears)]
+            if self.mfma_trunk:  # + W^T of layers 1..4 for the backward chain
+                sizes += [m.weight.numel() for m in self.linears[1:]]
             self.mirror = torch.zeros(sum(sizes), device=dev, dtype=torch.bfloat16)
             for i, m in enumerate(self.linears):
                 kin = self.k0 if i == 0 else m.in_features
-                segs.append(PpoSeg(flat.offset(m.weight), m.weight.numel(), moff, m.in_features, kin))
+                segs.append(PpoSeg(flat.offset(m.weight), m.weight.numel(), moff, m.in_features, kin, 0))
                 self.W_lp.append(self.mirror[moff:moff + m.out_features * kin].view(m.out_features, kin))
                 moff += m.out_features * kin
-                segs.append(PpoSeg(flat.offset(m.bias), m.out_features, moff, m.out_features, m.out_features))
+                segs.append(PpoSeg(flat.offset(m.bias), m.out_features, moff, m.out_features, m.out_features, 0))
                 self.b_lp.append(self.mirror[moff:moff + m.out_features])
                 moff += m.out_features
+            self.WT_lp = []
+            if self.mfma_trunk:
+                for m in self.linears[1:]:
+                    segs.append(PpoSeg(flat.offset(m.weight), m.weight.numel(), moff, m.in_features, m.out_features, 1))
+                    self.WT_lp.append(self.mirror[moff:moff + m.weight.numel()].view(m.in_features, m.out_features))
+                    moff += m.weight.numel()
             self.refresh_mirror()
         else:
             self.mirror = None
             self.W_lp = [m.weight.detach() for m in self.linears]
             self.b_lp = [m.bias.detach() for m in self.linears]
-        # fused MFMA trunk (csrc/ppo_mlp.hip): bf16 mirror, 59 -> 256 x 5 ELU, heads <= 32
-        self.mfma_trunk = bool(self.bf16 and len(self.linears) == 5 and widths[1:] == [256] * 5 and self.k0 == 64
-                               and self.A + 1 <= 32 and getattr(agent, "config", {}).get("mfma_trunk", True))
         if self.mfma_trunk:
             a = PpoMlpFwd()
             for i in range(5):
@@ -215,6 +242,15 @@ class FusedPPOUpdate:
                 a.b[i] = flat.params[o:o + 256].data_ptr()
             a.wh, a.bh, a.nh = self.Wh.data_ptr(), self.bh.data_ptr(), self.A + 1
             self._mlp_args = a
+            bw = PpoMlpBwd()
+            bw.dhead, bw.wh, bw.nh = self.dhead.data_ptr(), self.Wh.data_ptr(), self.A + 1
+            for k in range(4):
+                bw.wt[k] = self.WT_lp[k].data_ptr()
+                bw.h[k] = self.h[k + 1].data_ptr()
+            for k in range(5):
+                bw.dz[k] = self.dzs[k].data_ptr()
+            bw.h5, bw.rows, bw.h_stride = self.h_last_f.data_ptr(), B, self.h[1].stride(0)
+            self._mlp_bwd_args = bw
         self.segs = (PpoSeg * max(len(segs), 1))(*segs)
         self.nseg = len(segs)
         c = agent.config
@@ -242,6 +278,8 @@ class FusedPPOUpdate:
             for i, m in enumerate(self.linears):
                 self.W_lp[i][:, :m.in_features].copy_(m.weight)
                 self.b_lp[i].copy_(m.bias)
+            for k, m in enumerate(self.linears[1:len(self.WT_lp) + 1]):
+                self.WT_lp[k].copy_(m.weight.t())
 
     def set_dataset(self, ds: dict) -> None:
         """Bind the (static) dataset tensors; graphs are (re)captured when the pointers change."""
@@ -263,12 +301,14 @@ class FusedPPOUpdate:
         the fp32 heads into head = [mu | value]."""
         L, s, rms = self.L, self._stream(), self.rms
         _check(L.ppo_obs_normalize(_p(x), _p(idx), rows, self.obs_dim, _p(rms.running_mean), _p(rms.running_var),
-                                   rms.epsilon, _p(h[0]), self.k0, int(self.bf16), s), "ppo_obs_normalize")
+                                   rms.epsilon, _p(h[0]), self.k0, h[0].stride(0), int(self.bf16), s),
+               "ppo_obs_normalize")
         if self.mfma_trunk:
             # one launch: 5 x (MFMA + bias + ELU) with the activations chained in registers, fp32 heads;
             # stores layers 1..4 (bf16) and layer 5 (fp32) only when h has room for them (training)
             a = self._mlp_args
-            a.x = h[0].data_ptr()
+            a.x, a.x_stride = h[0].data_ptr(), h[0].stride(0)
+            a.h_stride = h[1].stride(0) if len(h) > 1 else 256
             for i in range(4):
                 a.h[i] = h[i + 1].data_ptr() if len(h) > 1 else None
             a.h5 = h_last_f.data_ptr() if h_last_f is not None else None
@@ -378,6 +418,9 @@ class FusedPPOUpdate:
         S = self.S
         hl = self.h_last_f
         jobs, keep = [], []
+        if self.mfma_trunk:
+            self._backward_mfma()
+            return
 
         def job(src: torch.Tensor, dst: torch.Tensor, n_s: int, out_rows: int, src_cols: int, dst_cols: int,
                 dst_stride: int) -> None:
@@ -413,6 +456,30 @@ class FusedPPOUpdate:
                 dhi = self.dh[:, :kin]
                 torch.mm(dz, self.W_lp[i], out=dhi)
                 dh, dh_t = dhi, dt_code
+        arr = (PpoReduceJob * len(jobs))(*jobs)
+        _check(L.ppo_reduce_rows(arr, len(jobs), s), "ppo_reduce_rows")
+        del keep
+
+    def _backward_mfma(self) -> None:
+        """dz of all five layers from one MFMA launch (ppo_mlp_backward), then the weight and bias
+        gradients as split-K GEMMs against the ones-augmented layer inputs, summed by ONE reduce launch."""
+        L, s, B, A, S = self.L, self._stream(), self.mb, self.A, self.S
+        hl = self.h_last_f
+        jobs, keep = [], []
+        pw = torch.bmm(self.dhead.view(S, B // S, A + 1).transpose(1, 2), hl.view(S, B // S, 256))
+        keep.append(pw)
+        jobs.append(PpoReduceJob(pw.data_ptr(), self.gWh.data_ptr(), S, A + 1, 256, 256, 256, pw.numel() // S))
+        _check(L.ppo_mlp_backward(C.byref(self._mlp_bwd_args), s), "ppo_mlp_backward")
+        for i, m in enumerate(self.linears):
+            hin = self.h[i]
+            w = hin.shape[1]                     # 72 or 264: [features | 1 | 0 ...]
+            ones = 64 if i == 0 else 256
+            gw = torch.bmm(self.dzs[i].view(S, B // S, 256).transpose(1, 2), hin.view(S, B // S, w),
+                           out_dtype=torch.float32)  # (S, 256, w)
+            keep.append(gw)
+            n_s = gw.numel() // S
+            jobs.append(PpoReduceJob(gw.data_ptr(), self.gW[i].data_ptr(), S, 256, w, m.in_features, m.in_features, n_s))
+            jobs.append(PpoReduceJob(gw.data_ptr() + 4 * ones, self.gb[i].data_ptr(), S, 256, w, 1, 1, n_s))
         arr = (PpoReduceJob * len(jobs))(*jobs)
         _check(L.ppo_reduce_rows(arr, len(jobs), s), "ppo_reduce_rows")
         del keep

@@ -44,10 +44,11 @@ typedef struct {
 } ppo_loss_cfg_t;
 
 /* one contiguous run of the flat parameter buffer that has a low-precision mirror (trunk layers):
- * flat[off + r*cols + c] -> mirror[moff + r*mstride + c]  (mstride >= cols; the pad stays zero) */
+ * flat[off + r*cols + c] -> mirror[moff + r*mstride + c]  (mstride >= cols; the pad stays zero), or
+ * with trans != 0 the transpose: mirror[moff + c*mstride + r] (mstride >= rows = len / cols) */
 typedef struct {
     int64_t off, len, moff;
-    int32_t cols, mstride;
+    int32_t cols, mstride, trans;
 } ppo_seg_t;
 
 int ppo_abi_version(void);
@@ -61,11 +62,12 @@ int ppo_obs_stats(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_
 /* fold the partials into running_mean / running_var / count (fp64, rl_games formula, unbiased batch var) */
 int ppo_obs_stats_update(const double* partials, int32_t nblk, int32_t cols, int32_t mb_rows, double* running_mean,
                          double* running_var, double* count, void* stream);
-/* out[r][c] = clamp((x[row][c] - mean[c]) / sqrt(var[c] + eps), -5, 5) for c < cols, 0 for cols <= c < out_stride;
+/* out[r*out_stride + c] = clamp((x[row][c] - mean[c]) / sqrt(var[c] + eps), -5, 5) for c < cols, 0 for
+ * cols <= c < out_cols (columns out_cols .. out_stride-1 are left untouched, e.g. a constant ones column);
  * out_bf16 selects bf16 (else fp32) output */
 int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_t cols, const double* running_mean,
-                      const double* running_var, float eps, void* out, int32_t out_stride, int32_t out_bf16,
-                      void* stream);
+                      const double* running_var, float eps, void* out, int32_t out_cols, int32_t out_stride,
+                      int32_t out_bf16, void* stream);
 
 /* Per-row PPO losses and head gradients.  head = [mu(0..A-1) | value(A)] (mb_rows x (A+1), fp32);
  * logstd (A); dataset rows (selected by mb_idx): actions / mu / sigma (A each), old_neglogp,
@@ -116,9 +118,10 @@ int ppo_policy_sample(const float* head, const float* logstd, int32_t A, int32_t
 int ppo_counter_add(int64_t* ctr, int64_t inc, void* stream);
 
 /* Fused actor-critic trunk forward on MFMA (bf16 in, fp32 accumulate): 5 layers x 256, ELU, then the
- * fp32 heads.  x: rows x 64 bf16 (normalised obs, zero-padded 59 -> 64); w[0]: 256 x 64 bf16,
- * w[1..4]: 256 x 256 bf16 (the trunk mirror); b[l]: 256 fp32; wh: nh x 256 fp32 ([mu.w | value.w]),
- * bh: nh fp32 (nh <= 32).  Outputs (row-major, NULL = skip): h[0..3] = layers 1..4 (bf16 rows x 256),
+ * fp32 heads.  x: rows x 64 bf16 (normalised obs, zero-padded 59 -> 64; row stride x_stride >= 64);
+ * w[0]: 256 x 64 bf16, w[1..4]: 256 x 256 bf16 (the trunk mirror); b[l]: 256 fp32; wh: nh x 256 fp32
+ * ([mu.w | value.w]), bh: nh fp32 (nh <= 32).  Outputs (row-major, NULL = skip): h[0..3] = layers
+ * 1..4 (bf16, columns 0..255 of rows with stride h_stride >= 256; columns beyond are not touched),
  * h5 = layer 5 in fp32 (rows x 256), head = rows x nh fp32.  Each wave keeps its 32 rows' activations
  * in registers between layers (an MFMA accumulator tile is the next layer's B operand); each layer's
  * weights are staged once per workgroup in LDS. */
@@ -131,9 +134,26 @@ typedef struct {
     uint16_t* h[4];
     float* h5;
     float* head;
-    int32_t rows, nh;
+    int32_t rows, nh, x_stride, h_stride;
 } ppo_mlp_fwd_t;
 int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream);
+
+/* Fused backward of the trunk's input-gradient chain (the weight gradients stay split-K GEMMs):
+ *   dh5 = Wh^T dhead (exact f32 MFMA), dz4 = dh5 * elu'(h5),
+ *   for l = 4..1: dz_{l-1} = (W_l^T dz_l) * elu'(h_l)   (bf16 MFMA, W_l^T from wt[l-1])
+ * with elu'(y) = 1 if y > 0 else y + 1 (output form).  dhead: rows x nh fp32; wh: nh x 256 fp32;
+ * wt[k]: W_{k+1}^T (256 x 256 bf16, row = input feature); h5: rows x 256 fp32; h[k]: layer k+1
+ * activations (bf16, row stride h_stride); outputs dz[l] (l = 0..4): rows x 256 bf16. */
+typedef struct {
+    const float* dhead;
+    const float* wh;
+    const uint16_t* wt[4];
+    const float* h5;
+    const uint16_t* h[4];
+    uint16_t* dz[5];
+    int32_t rows, nh, h_stride;
+} ppo_mlp_bwd_t;
+int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream);
 
 /* Rollout bookkeeping of one step (a2c_common.play_steps after env_step), per env:
  *   shaped = (reward + shift) * scale [+ gamma * value * time_out]  -> shaped_out (td rewards[n])

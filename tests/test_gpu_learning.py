@@ -330,6 +330,7 @@ def test_fused_mlp_forward_kernel(rows):
     for i in range(4):
         a.h[i] = hs[i].data_ptr()
     a.wh, a.bh, a.h5, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), h5.data_ptr(), head.data_ptr(), rows, 22
+    a.x_stride, a.h_stride = 64, 256
     FU._check(L.ppo_mlp_forward(C.byref(a), torch.cuda.current_stream().cuda_stream), "ppo_mlp_forward")
     torch.cuda.synchronize()
     hin = xb.float()
