@@ -161,7 +161,9 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   // (physics-only launches do not touch the counters and keep the bank)
   if (env->graph_safe && mode != as::kModePhysics) {
     env->bank = 0;
-    HIP_TRY(hipMemsetAsync(env->counters_dev, 0, sizeof(int32_t) * as::kCntBank, s));
+    // a kernel node, not hipMemsetAsync: replaying a captured memset node next to other graphs was
+    // observed to leave the bank holding pointer-sized garbage on this ROCm build
+    HIP_TRY(as::launch_zero(env->counters_dev, as::kCntBank, s));
   }
   int32_t* cnt = env->counters_dev + as::kCntBank * env->bank;
   as::StepArgs a{};

@@ -97,6 +97,8 @@ bool step_supported_nv(int nv);
 hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream);
 hipError_t launch_obs(const ObsArgs& a, hipStream_t stream);
 hipError_t launch_stones(const StonesArgs& a, hipStream_t stream);
+// zero n int32 words with a kernel (graph-safe stepping: a kernel node instead of a memset node)
+hipError_t launch_zero(int32_t* p, int n, hipStream_t stream);
 size_t step_lds_bytes();
 
 }  // namespace as

@@ -1691,6 +1691,15 @@ hipError_t launch_obs(const ObsArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void k_zero(int32_t* p, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0;
+}
+
+hipError_t launch_zero(int32_t* p, int n, hipStream_t stream) {
+  hipLaunchKernelGGL(k_zero, dim3(1), dim3(256), 0, stream, p, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_stones(const StonesArgs& a, hipStream_t stream) {
   int blocks = (a.n + 255) / 256;
   hipLaunchKernelGGL(k_stones, dim3(blocks), dim3(256), 0, stream, a);

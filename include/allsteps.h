@@ -196,7 +196,7 @@ int as_profile_read(as_env_t* env, double* step_kernel_ms, double* obs_kernel_ms
 int as_debug_stamps(as_env_t* env, uint64_t* stamps_dev);
 
 /* Graph-safe stepping (on != 0): every as_step / as_task_step / as_reset_* uses the SAME counter bank,
- * cleared by a memset node at the start of the call, instead of alternating two banks from host
+ * cleared by a one-block kernel at the start of the call, instead of alternating two banks from host
  * state -- so a call captured once in a HIP graph (hipStreamBeginCapture) can be replayed any number
  * of times.  Off (default): two banks, no memset (lowest eager launch count). */
 int as_set_graph_safe(as_env_t* env, int32_t on);

@@ -24,6 +24,11 @@ def test_train_script_runs_on_allsteps(tmp_path):
     # rollout graphs: epoch 1 eager, epoch 2 captured, epoch 3 replayed; host counters still advance
     assert all(isinstance(g, torch.cuda.CUDAGraph) for g in agent._play_graphs.values())
     assert agent._uw.common_step_counter == 3 * 32
+    # replayed env graphs keep the device step counters sane: no spurious curriculum bump (the gate
+    # needs mean target index > 12; a random policy stays near 1) -- regression for a captured
+    # hipMemsetAsync node that left garbage in the counter bank
+    assert int(agent._uw.state["curriculum"][0]) == 0
+    assert float(agent._uw.curr_target_index.float().mean()) < 3.0
     for k in ("a_loss", "c_loss", "kl", "entropy", "lr"):
         assert math.isfinite(st[k]), (k, st)
     assert torch.isfinite(agent.flat.params).all()
