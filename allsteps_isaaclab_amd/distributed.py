@@ -50,8 +50,8 @@ def init_process_group(backend: str | None = None) -> ShardInfo:
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     info = shard_info()
     if info.world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:  # ALLSTEPS_DIST_BACKEND overrides (e.g. gloo for ranks sharing one GPU in tests)
+            backend = os.environ.get("ALLSTEPS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         kw = {}
         if backend == "nccl":
             torch.cuda.set_device(info.local_rank)

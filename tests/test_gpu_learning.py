@@ -398,3 +398,55 @@ def test_rollout_bookkeeping_kernel_matches_reference_ops(tmp_path):
         for m, mm in zip(meters, (fus.game_rewards, fus.game_shaped_rewards, fus.game_lengths)):
             torch.testing.assert_close(mm.mean.reshape(-1), m.mean.reshape(-1), rtol=1e-5, atol=1e-5)
             assert float(mm.current_size) == float(m.current_size)
+
+
+def _dist_train_worker(rank, port, mode, tmp, q):
+    import socket  # noqa: F401
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK="0", ALLSTEPS_DIST_BACKEND="gloo")
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "scripts", "reinforcement_learning", "rl_games"))
+    import torch.distributed as dist
+
+    import train
+
+    try:
+        runner, _ = train.main(["--task", "Allsteps-v0", "--num_envs", "1024", "--max_iterations", "3", "--seed", "7",
+                                "--distributed", "--multi_gpu_mode", mode, "--log_root", f"{tmp}/r{rank}"])
+        ag = runner.agent
+        q.put((rank, ag.flat.params.cpu(), float(ag.lr), ag.frame, ag.dataset.minibatch_size,
+               int(ag._uw.env_id_offset), bool(ag.fused is not None and ag._play_graphs is not None)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["allreduce", "allgather"])
+def test_distributed_fused_trainer_two_ranks_one_gpu(tmp_path, mode):
+    """The --distributed train.py path with the fused HIP-graph update and rollout graphs, two ranks
+    (gloo, both on cuda:0): the gradient / rollout exchange keeps the ranks' parameters identical,
+    env shards are offset, frames count both ranks."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_train_worker, args=(r, port, mode, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=200) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, p0, lr0, f0, mb0, off0, fused0), (_, p1, lr1, f1, mb1, off1, _) = res
+    assert fused0, "the fused update / rollout graphs must be the path under test"
+    assert torch.equal(p0, p1), f"{mode}: ranks diverged"
+    assert lr0 == lr1 and f0 == f1 == 3 * 2 * 1024 * 32
+    assert (off0, off1) == (0, 1024)
+    assert mb0 == (2 * 32768 if mode == "allgather" else 32768)
