@@ -62,7 +62,7 @@ class AsTask(C.Structure):
         ("term_curriculum", C.c_float * 10), ("gain_curriculum", C.c_float * 10), ("init_root", C.c_float * 3),
         ("init_q", C.c_float * 21), ("right_idx", C.c_int32 * 9), ("left_idx", C.c_int32 * 9),
         ("neg_idx", C.c_int32 * 2), ("noise_lo", C.c_float), ("noise_hi", C.c_float), ("clip_lo", C.c_float),
-        ("clip_hi", C.c_float),
+        ("clip_hi", C.c_float), ("regen_footsteps", C.c_int32),
     ]
 
 
@@ -205,6 +205,7 @@ def make_task(cfg, dof_names: list) -> AsTask:
     T.neg_idx[:] = [J(x) for x in cfg.negation_body_names]
     T.noise_lo, T.noise_hi = cfg.initial_joint_angle_range
     T.clip_lo, T.clip_hi = cfg.initial_joint_angle_clip_range
+    T.regen_footsteps = int(bool(getattr(cfg, "regenerate_footsteps", False)))
     return T
 
 

@@ -205,6 +205,8 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   if (!env->graph_safe) env->bank ^= 1;
   o.obs = obs;
   o.side = env->side_dev;
+  o.seed = env->seed;
+  o.env_offset = env->env_offset;
   HIP_TRY(as::launch_obs(o, s));
   if (prof) {
     HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 2], s));

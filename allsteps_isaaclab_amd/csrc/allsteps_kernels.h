@@ -71,7 +71,9 @@ constexpr int kCntBank = kCntStride * (1 + kCntSlots);
 // (tick-#1 state) and foot_contact[2], targets[9] (tick-#1 observation entries 48..58)
 constexpr int kSideState = 9;
 constexpr int kSideObs = 11;
-constexpr int kSideWords = kSideState + kSideObs;
+constexpr int kSideRegen = kSideState + kSideObs;  // 1 = reset env due new stones (regen_footsteps)
+constexpr int kSideWords = kSideRegen + 1;
+constexpr int kCntLevel = 2;  // counter-bank word: the curriculum level k_step saw (k_obs regen level)
 
 struct ObsArgs {
   const Consts* consts;
@@ -81,6 +83,8 @@ struct ObsArgs {
   int32_t* next_counters;  // the other bank, cleared here for the next launch
   float* obs;
   const uint32_t* side;
+  uint64_t seed;
+  int64_t env_offset;
 };
 
 struct StonesArgs {

@@ -1423,11 +1423,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (threadIdx.x == 0) {
       atomicAdd(&P.counters[kCntStride * (1 + (int)(blockIdx.x % kCntSlots))], wsum);
       if (wdone) P.counters[0] = 1;
+      if (T.regen_footsteps) P.counters[kCntLevel] = P.st.curriculum[0];  // same value from every wave
     }
   }
   ts.mark(kStTask);
   // ---- in-kernel reset (allsteps_env.py:481-565)
   const bool any_done = __any(done);  // wave-uniform: both envs of the wave enter the FK together
+  // regen_footsteps: the over-half test on the PRE-reset target index (allsteps_env.py:497-500 as
+  // intended); k_obs draws the new course once the launch-wide curriculum gate is known
+  const bool regen = T.regen_footsteps && P.mode != kModePhysics && done && idx > T.num_steps / 2;
   if (P.mode != kModePhysics && any_done) {
     if (done) {
       float dm = 0.f, dn = 0.f;  // mirror draw, this lane's joint-noise draw
@@ -1542,6 +1546,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                                              __float_as_uint(fc[0]), __float_as_uint(fc[1]),
                                              __float_as_uint(fc[0]), __float_as_uint(fc[1])};
         for (int k = 0; k < kSideState + 2; ++k) side[k * n + e] = sv[k];
+        side[kSideRegen * n + e] = regen ? 1u : 0u;
       }
     }
     idx = i2; prev = p2; next = n2; count = c2; swing = w2;
@@ -1587,6 +1592,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 // written by k_step): the curriculum gate (allsteps_env.py:471-479, evaluated on the tick-#1 target
 // indices) -- k_step has already applied the second tick.  If none did: restore the tick-#1 state
 // and observation entries k_step saved in the side buffer.
+__device__ void gen_stones(const as_task_t& T, int level, uint64_t seed, uint32_t env, uint32_t episode,
+                           const float* draws, float* stones, int n, int e);
+
 __global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
   const Consts& K = *(const Consts*)(CK*)P.consts;
   const as_task_t& T = K.task;
@@ -1599,10 +1607,17 @@ __global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
     int sum = 0;
     for (int i = 0; i < kCntSlots; ++i) sum += P.counters[kCntStride * (1 + i)];
     P.counters[1] = sum;
-    if (any_reset) {
+    if (any_reset) {  // (regen below recomputes this gate per thread from the bank, race-free)
       const int c = P.st.curriculum[0];
       if ((float)sum / (float)n > (float)T.curriculum_threshold) P.st.curriculum[0] = min(c + 1, T.max_curriculum);
     }
+  }
+  if (any_reset && T.regen_footsteps && e < n && P.side[kSideRegen * n + e]) {
+    int sum = 0;
+    for (int i = 0; i < kCntSlots; ++i) sum += P.counters[kCntStride * (1 + i)];
+    const int c0 = P.counters[kCntLevel];
+    const int level = (float)sum / (float)n > (float)T.curriculum_threshold ? min(c0 + 1, T.max_curriculum) : c0;
+    gen_stones(T, level, P.seed, (uint32_t)(P.env_offset + e), P.st.episode[e], nullptr, P.st.stones, n, e);
   }
   if (any_reset) return;
   if (e >= n) return;
@@ -1627,13 +1642,11 @@ __device__ float lerp_t(float a, float b, float w) {  // torch.lerp (ATen Lerp.h
   return fabsf(w) < 0.5f ? a + w * (b - a) : b - (b - a) * (1.0f - w);
 }
 
-__global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
-  const as_task_t& T = ((const Consts*)(CK*)P.consts)->task;
-  const int n = P.n;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
+// one env's course at `level`: draws[3][n][N] if given, else Philox (seed, env, episode, k, "Ston")
+__device__ void gen_stones(const as_task_t& T, int level, uint64_t seed, uint32_t env, uint32_t episode,
+                           const float* draws, float* stones, int n, int e) {
   const int N = T.num_steps, maxc = T.max_curriculum;
-  const int c = min(P.level, maxc);
+  const int c = min(level, maxc);
   const float ratio = (float)c / (float)maxc;
   const float step = (0.9f - 0.75f) / (float)maxc;  // torch.linspace(0.75, 0.9, 10)[c]
   const float dist_hi = c < (maxc + 1) / 2 ? 0.75f + step * (float)c : 0.9f - step * (float)(maxc - c);
@@ -1644,11 +1657,11 @@ __global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
   float x = 0.f, y = 0.f, z = 0.f, phi = 0.f;
   for (int k = 0; k < N; ++k) {
     float w[3];
-    if (P.draws) {
-      for (int j = 0; j < 3; ++j) w[j] = P.draws[((size_t)j * n + e) * N + k];
+    if (draws) {
+      for (int j = 0; j < 3; ++j) w[j] = draws[((size_t)j * n + e) * N + k];
     } else {
       float blk[4];
-      philox_block(P.seed, (uint32_t)(P.env_offset + e), 0u, (uint32_t)k, kStonesTag, blk);
+      philox_block(seed, env, episode, (uint32_t)k, kStonesTag, blk);
       w[0] = blk[0]; w[1] = blk[1]; w[2] = blk[2];
     }
     float dr = lerp_t(0.75f, dist_hi, w[0]);
@@ -1663,10 +1676,17 @@ __global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
     x += dr * st_ * cp;
     y += dr * st_ * sp;
     z += dr * ct_;
-    P.stones[(k * 3 + 0) * n + e] = x;
-    P.stones[(k * 3 + 1) * n + e] = y;
-    P.stones[(k * 3 + 2) * n + e] = z;
+    stones[(k * 3 + 0) * n + e] = x;
+    stones[(k * 3 + 1) * n + e] = y;
+    stones[(k * 3 + 2) * n + e] = z;
   }
+}
+
+__global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
+  const as_task_t& T = ((const Consts*)(CK*)P.consts)->task;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.n) return;
+  gen_stones(T, P.level, P.seed, (uint32_t)(P.env_offset + e), 0u, P.draws, P.stones, P.n, e);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -64,6 +64,10 @@ class AllstepsEnvCfg:
     # Curriculum level the stones are generated at.  The reference generates them once at level 0
     # (allsteps_env.py:71) and never regenerates; C3 uses 9 as an init knob.
     initial_stone_curriculum: int = 0
+    # The reference never regenerates stones (its _reset_idx resets curr_target_index before testing
+    # it, allsteps_env.py:492-500).  True = the intended behaviour: a reset env
+    # whose target index was past half the stones gets a new course at the current curriculum level.
+    regenerate_footsteps: bool = False
 
     # joint gears, cfg/PhysX dof order (allsteps_env_cfg.py:133-155)
     joint_gears: list = field(default_factory=lambda: [

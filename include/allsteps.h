@@ -105,6 +105,10 @@ typedef struct {
   float init_q[21];
   int32_t right_idx[9], left_idx[9], neg_idx[2];
   float noise_lo, noise_hi, clip_lo, clip_hi;
+  /* 0 = reference behaviour (stones never regenerate: _reset_idx resets curr_target_index before its
+   * over-half test, allsteps_env.py:492-500); 1 = the intended behaviour: a reset
+   * env whose target index was > num_steps / 2 gets new stones at the (post-gate) curriculum level */
+  int32_t regen_footsteps;
 } as_task_t;
 
 /* Per-env state: structure of arrays, field-major / env-minor ([field][num_envs]), device memory,

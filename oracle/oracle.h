@@ -93,6 +93,7 @@ typedef struct {
   float init_q[21];             /* running-start pose, cfg order */
   int32_t right_idx[9], left_idx[9], neg_idx[2];
   float noise_lo, noise_hi, clip_lo, clip_hi;
+  int32_t regen_footsteps; /* as_task_t.regen_footsteps: fix of allsteps_env.py:492-500 behind a flag */
 } or_task_t;
 
 /* Per-env state, structure of arrays: field-major, env-minor ([field][num_envs]). */
@@ -161,6 +162,8 @@ void or_mass_matrix(const or_model_t* m, const float root_pos[3], const float ro
 void or_bias_forces(const or_model_t* m, const float root_pos[3], const float root_quat[4], const float* q_int,
                     const float* u /* nv */, float gravity, float* C /* nv */);
 void or_philox_uniform(uint64_t seed, uint32_t env, uint32_t episode, int k, float* out);
+/* every env's course at `level` from the Philox "Ston" stream of (seed, env, episode[e] or 0) */
+void or_stones_philox(const or_task_t* task, int n, int level, uint64_t seed, const uint32_t* episode, float* stones);
 
 #ifdef __cplusplus
 }

@@ -194,6 +194,43 @@ void or_philox_uniform(uint64_t seed, uint32_t env, uint32_t episode, int k, flo
   }
 }
 
+/* One env's course at `level` from Philox draws keyed (seed, env, episode, block k, "Ston"): the
+ * kernel's k_stones / k_obs regeneration stream (ENV:125-174 formulas, as or_footsteps). */
+static void stones_philox(const or_task_t* task, int n, int e, int level, uint64_t seed, uint32_t env,
+                          uint32_t episode, float* stones /* [60][n] */) {
+  const int N = task->num_steps, maxc = task->max_curriculum;
+  const int c = level < maxc ? level : maxc;
+  const float ratio = (float)c / (float)maxc;
+  const float dist_hi = linspace_at(0.75f, 0.9f, maxc + 1, c);
+  const float d2r = (float)(3.14159265358979323846 / 180.0);
+  const float yaw_lo = (-20.0f * ratio) * d2r, yaw_hi = (20.0f * ratio) * d2r;
+  const float half_pi = (float)(3.14159265358979323846 / 2.0);
+  const float p_lo = (-30.0f * ratio) * d2r + half_pi, p_hi = (30.0f * ratio) * d2r + half_pi;
+  const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  float x = 0.f, y = 0.f, z = 0.f, phi = 0.f;
+  for (int k = 0; k < N; ++k) {
+    uint32_t ctr[4] = {env, episode, (uint32_t)k, 0x53746f6eu /* "Ston" */};
+    philox4x32_10(ctr, key);
+    float w[3];
+    for (int j = 0; j < 3; ++j) w[j] = (float)(ctr[j] >> 8) * (1.0f / 16777216.0f);
+    float dr = lerpf_t(0.75f, dist_hi, w[0]), dph = lerpf_t(yaw_lo, yaw_hi, w[1]), dth = lerpf_t(p_lo, p_hi, w[2]);
+    if (k == 0) { dr = 0.f; dph = 0.f; dth = half_pi; }
+    if (k == 1 || k == 2) { dr = 0.75f; dph = 0.f; dth = half_pi; }
+    phi += dph;
+    x += dr * sinf(dth) * cosf(phi);
+    y += dr * sinf(dth) * sinf(phi);
+    z += dr * cosf(dth);
+    stones[(size_t)(3 * k + 0) * n + e] = x;
+    stones[(size_t)(3 * k + 1) * n + e] = y;
+    stones[(size_t)(3 * k + 2) * n + e] = z;
+  }
+}
+
+void or_stones_philox(const or_task_t* task, int n, int level, uint64_t seed, const uint32_t* episode,
+                      float* stones) {
+  for (int e = 0; e < n; ++e) stones_philox(task, n, e, level, seed, (uint32_t)e, episode ? episode[e] : 0u, stones);
+}
+
 /* ------------------------------------------------------------------ task logic */
 
 #define F(arr, f, n, e) (arr)[(size_t)(f) * (n) + (e)]
@@ -414,7 +451,12 @@ static void reset_and_tick2(const or_model_t* model, const or_task_t* task, or_s
       memcpy(d, reset_draws + (size_t)e * 22, sizeof d);
     else
       or_philox_uniform(seed, (uint32_t)e, st->episode[e], 22, d);
+    /* ENV:497-500 as intended (flag): the over-half test on the PRE-reset target index */
+    const int regen = task->regen_footsteps && st->idx[e] > task->num_steps / 2;
     reset_env(model, task, st, e, d);
+    /* stones 0..2 are the same for every course, so the reset observation / potentials (targets
+     * 0..2 after a reset) do not change; the new course is keyed by the new episode */
+    if (regen) stones_philox(task, n, e, st->curriculum[0], seed, (uint32_t)e, st->episode[e], st->stones);
     float bp[9];
     if (post_fk) {
       post_fk(ctx, e, bp);

@@ -1,0 +1,109 @@
+"""regenerate_footsteps: the intended behaviour of allsteps_env.py:492-500 behind a flag (SURVEY
+Appendix C.4; off by default = reference behaviour, stones never regenerate).  A reset env whose
+pre-reset target index was > num_steps // 2 gets a new course at the post-gate curriculum level,
+drawn from the Philox "Ston" stream keyed by (seed, env, new episode).  CPU: oracle semantics;
+GPU: kernel vs oracle (reset_mask and in-step resets)."""
+
+import numpy as np
+import pytest
+import torch
+
+
+def _orc(flag):
+    import oracle as O
+
+    from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
+
+    cfg = AllstepsEnvCfg()
+    cfg.regenerate_footsteps = flag
+    return O.Oracle(cfg)
+
+
+def _level0_state(orc, n):
+    st = orc.state(n)
+    pos, _ = orc.footsteps(n, 0, np.zeros((5, n, 20), np.float32))
+    st["stones"][:] = pos.reshape(n, 60).T
+    st["root_quat"][0][:] = 1.0
+    st["idx"][:] = 1
+    st["next"][:] = 2
+    return st
+
+
+@pytest.mark.parametrize("flag", [False, True])
+def test_oracle_regen_on_reset_mask(oracle_mod, flag):
+    orc = _orc(flag)
+    n = 16
+    st = _level0_state(orc, n)
+    st["idx"][:8] = 12  # past half the course
+    st["prev"][:8], st["next"][:8] = 11, 13
+    st["curriculum"][0] = 5
+    before = st["stones"].copy()
+    mask = np.ones(n, bool)
+    orc.reset_mask(st, mask, seed=7, reset_draws=np.full((n, 22), 0.3, np.float32))
+    after = st["stones"]
+    # stones 0..2 are the same for every course
+    np.testing.assert_allclose(after[:9], before[:9], atol=1e-6)
+    # envs that were not past half keep their course
+    np.testing.assert_array_equal(after[:, 8:], before[:, 8:])
+    if not flag:
+        np.testing.assert_array_equal(after, before)
+        return
+    assert np.abs(after[9:, :8] - before[9:, :8]).max() > 0.01
+    # the new course is level 5 (mean target index 6.5 < 12: no curriculum bump) keyed by the new episode
+    ref = np.zeros_like(after)
+    import ctypes as C
+
+    from oracle import fp
+
+    ep = np.ascontiguousarray(st["episode"]).astype(np.uint32)
+    orc.L.or_stones_philox.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_void_p, C.c_void_p]
+    orc.L.or_stones_philox(C.byref(orc.task), n, 5, 7, ep.ctypes.data, fp(ref))
+    np.testing.assert_array_equal(after[:, :8], ref[:, :8])
+    # yaw / pitch ranges of level 5 are non-zero: the course leaves the straight line
+    assert np.abs(after[3 * 19 + 1, :8]).max() > 0.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("how", ["reset_mask", "step"])
+def test_gpu_regen_matches_oracle(oracle_mod, how):
+    from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv
+    from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
+
+    orc = _orc(True)
+    n = 128
+    st = _level0_state(orc, n)
+    rng = np.random.default_rng(3)
+    past = rng.uniform(size=n) < 0.5
+    st["idx"][past] = 12
+    st["prev"][past], st["next"][past] = 11, 13
+    st["curriculum"][0] = 6
+    cfg = AllstepsEnvCfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    cfg.seed = 7
+    cfg.regenerate_footsteps = True
+    env = AllstepsEnv(cfg)
+    st["root_pos"][2][:] = 1.5
+    if how == "step":
+        st["root_pos"][2][past] = 0.2  # below the fall height: terminated -> in-step reset
+    env.set_state({k: torch.from_numpy(np.ascontiguousarray(st[k]).view(np.int32) if st[k].dtype == np.uint32
+                                       else np.ascontiguousarray(st[k])) for k in env.state})
+    draws = rng.uniform(0, 1, (n, 22)).astype(np.float32)
+    if how == "reset_mask":
+        env._reset_idx(torch.from_numpy(past), reset_draws=torch.from_numpy(draws))
+        orc.reset_mask(st, past, seed=7, reset_draws=draws)
+    else:
+        acts = np.zeros((n, 21), np.float32)
+        _, _, term, _, _ = env.step_with_draws(torch.from_numpy(acts).cuda(), torch.from_numpy(draws))
+        _, _, term_c, _, _ = orc.env_step(st, acts, seed=7, reset_draws=draws)
+        assert np.array_equal(term.cpu().numpy(), term_c)
+        assert term_c[past].all()
+    torch.cuda.synchronize()
+    gs = env.get_state()
+    assert int(gs["curriculum"][0]) == int(st["curriculum"][0])
+    np.testing.assert_array_equal(gs["episode"].cpu().numpy().view(np.uint32), st["episode"])
+    g = gs["stones"].cpu().numpy()
+    np.testing.assert_allclose(g, st["stones"], atol=2e-5)
+    assert np.abs(g[3 * 19 + 1, past]).max() > 0.05  # regenerated (level 6 courses bend)
+    assert np.abs(g[3 * 19 + 1, ~past]).max() < 1e-5  # untouched level-0 courses
+    env.close()
