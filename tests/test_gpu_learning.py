@@ -450,3 +450,21 @@ def test_distributed_fused_trainer_two_ranks_one_gpu(tmp_path, mode):
     assert lr0 == lr1 and f0 == f1 == 3 * 2 * 1024 * 32
     assert (off0, off1) == (0, 1024)
     assert mb0 == (2 * 32768 if mode == "allgather" else 32768)
+
+
+@pytest.mark.gpu
+def test_training_is_deterministic(tmp_path):
+    """Same seed, same config -> bit-identical parameters after 3 epochs (env Philox resets, Philox
+    policy sampling, deterministic kernels and graph replays; cf. the reference's
+    test_environment_determinism.py for the env)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts", "reinforcement_learning", "rl_games"))
+    import train
+
+    out = []
+    for k in range(2):
+        runner, _ = train.main(["--task", "Allsteps-v0", "--num_envs", "1024", "--max_iterations", "3", "--seed", "11",
+                                "--log_root", str(tmp_path / f"run{k}")])
+        out.append((runner.agent.flat.params.clone(), runner.agent._uw.get_state()))
+    assert torch.equal(out[0][0], out[1][0])
+    for key in ("q", "qd", "root_pos", "idx", "episode"):
+        assert torch.equal(out[0][1][key], out[1][1][key]), key
