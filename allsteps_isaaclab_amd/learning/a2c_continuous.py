@@ -743,6 +743,7 @@ class A2CAgent:
                         if self.last_mean_rewards > self.score_to_win:
                             self.save(os.path.join(self.nn_dir, name))
                             should_exit = True
+                self._log_metrics()
                 if self.max_epochs != -1 and epoch_num >= self.max_epochs:
                     mean = self.game_rewards.get_mean()[0] if float(self.game_rewards.current_size) > 0 else -math.inf
                     self.save(os.path.join(self.nn_dir, f"last_{self.name}_ep_{epoch_num}_rew_{mean}"))
@@ -753,6 +754,19 @@ class A2CAgent:
                 should_exit = bool(t.item())
             if should_exit:
                 return self.last_mean_rewards, epoch_num
+
+    def _log_metrics(self) -> None:
+        """rl_games writes its per-epoch scalars to TensorBoard (absent here): one JSON line per epoch
+        in <train_dir>/<experiment>/summaries/metrics.jsonl (losses, lr, kl, fps, episode stats)."""
+        if not self.config.get("write_metrics", True):
+            return
+        import json
+
+        d = os.path.join(self.experiment_dir, "summaries")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "metrics.jsonl"), "a") as f:
+            f.write(json.dumps({k: (round(v, 6) if isinstance(v, float) else v) for k, v in self.last_stats.items()})
+                    + "\n")
 
     # ------------------------------------------------------------------ checkpoints (rl_games layout)
     def get_weights(self) -> dict:

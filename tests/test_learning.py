@@ -207,6 +207,8 @@ def test_runner_train_loop(tmp_path):
     assert agent.epoch_num == 2
     saved = [f for f in os.listdir(os.path.join(tmp_path, agent.experiment_name, "nn"))]
     assert saved and all(f.endswith(".pth") for f in saved)
+    lines = open(os.path.join(tmp_path, agent.experiment_name, "summaries", "metrics.jsonl")).read().splitlines()
+    assert len(lines) == 2 and '"a_loss"' in lines[0] and '"lr"' in lines[1]
     player = runner.create_player()
     player.restore(os.path.join(tmp_path, agent.experiment_name, "nn", saved[0]))
     res = player.run(max_steps=50)
