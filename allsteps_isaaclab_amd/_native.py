@@ -24,6 +24,7 @@ EXPORTED_SYMBOLS = [
     "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
     "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask", "as_set_graph_safe",
+    "as_profile_sampled",
 ]
 
 
@@ -111,6 +112,7 @@ def load() -> C.CDLL:
     L.as_set_seed.argtypes = [V, U64]
     L.as_set_graph_safe.argtypes = [V, I32]
     L.as_profile.argtypes = [V, I32]
+    L.as_profile_sampled.argtypes = [V, I32, I32]
     L.as_debug_stamps.argtypes = [V, V]
     L.as_profile_read.argtypes = [V, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(I32)]
     L.as_generate_stones.argtypes = [V, I32, V, V]
@@ -290,6 +292,9 @@ class NativeEnv:
     def generate_stones(self, level: int, draws=None, stream=None):
         check(self.L.as_generate_stones(self.h, level, draws.data_ptr() if draws is not None else None, stream),
               "as_generate_stones")
+
+    def profile_sampled(self, max_records: int, stride: int):
+        check(self.L.as_profile_sampled(self.h, max_records, stride), "as_profile_sampled")
 
     def profile(self, max_launches: int):
         check(self.L.as_profile(self.h, max_launches), "as_profile")

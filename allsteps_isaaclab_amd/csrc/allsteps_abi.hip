@@ -44,7 +44,7 @@ struct as_env {
   // optional per-launch timing (as_profile): event triples around k_step / k_obs
   std::vector<hipEvent_t> ev;
   unsigned long long* stamps = nullptr;  // diagnostic (as_debug_stamps)
-  int32_t prof_cap = 0, prof_n = 0;
+  int32_t prof_cap = 0, prof_n = 0, prof_stride = 1, prof_calls = 0;
   int32_t tune = 0;  // AS_TUNE (diagnostic scheduling experiments; 0 = default)
 };
 
@@ -184,7 +184,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   a.tune = env->tune;
   a.obs = mode == as::kModePhysics ? nullptr : obs;
   a.side = env->side_dev;
-  const bool prof = env->prof_n < env->prof_cap;
+  const bool prof = env->prof_n < env->prof_cap && (env->prof_calls++ % env->prof_stride) == 0;
   if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n], s));
   HIP_TRY(as::launch_step(a, env->nv, s));
   if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 1], s));
@@ -229,6 +229,16 @@ int as_profile(as_env_t* env, int32_t max_launches) {
   for (auto& e : env->ev) HIP_TRY(hipEventCreate(&e));
   env->prof_cap = max_launches;
   env->prof_n = 0;
+  env->prof_stride = 1;
+  env->prof_calls = 0;
+  return AS_OK;
+}
+
+int as_profile_sampled(as_env_t* env, int32_t max_records, int32_t stride) {
+  if (!env || stride < 1) return fail(AS_ERR_INVALID, "as_profile_sampled: bad argument");
+  const int rc = as_profile(env, max_records);
+  if (rc != AS_OK) return rc;
+  env->prof_stride = stride;
   return AS_OK;
 }
 

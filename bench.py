@@ -11,7 +11,8 @@ scaling, no collective in the step).  value = all ranks' env-steps / max-over-ra
 
 Extra objects on the JSON line:
   roofline     -- k_step (the dominant kernel): algorithmic bytes per launch / its average duration
-                  from HIP events recorded around every launch on its own stream, vs 8 TB/s HBM.
+                  from HIP events recorded around every 10th launch of the timed region on its own
+                  stream (events on every launch would add their own launch gaps), vs 8 TB/s HBM.
   cpu_baseline -- rank 0, N = 1: the CPU oracle (oracle/, a port of the same step) timed on this
                   host's cores on a bounded sample.
   train        -- rank 0, N = 1 (BASELINE C4 per GPU, SURVEY §8d "env+PPO separately"): env-steps/s
@@ -132,7 +133,9 @@ def main():
     for t in range(W):
         env.step(actions[K + t])
     torch.cuda.synchronize(device)
-    env._native.profile(K)  # HIP events around every k_step / k_obs launch of the timed region
+    # HIP events around every 10th k_step / k_obs launch of the timed region: per-launch events add a
+    # launch gap (~10 us at 4096 envs), so timing every launch would slow the loop it measures
+    env._native.profile_sampled(max(K // 10, 1), 10)
 
     def barrier():
         if world > 1:

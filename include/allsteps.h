@@ -187,6 +187,9 @@ int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* s
  * kernel (k_obs) of the next `max_launches` calls on their own stream; as_profile_read
  * synchronises on the last event and returns the summed durations (ms) and the launch count. */
 int as_profile(as_env_t* env, int32_t max_launches);
+/* Sampled form: time every `stride`-th call only (up to `max_records` of them), so the events'
+ * launch gaps touch 1 / stride of the calls of a timed loop. */
+int as_profile_sampled(as_env_t* env, int32_t max_records, int32_t stride);
 int as_profile_read(as_env_t* env, double* step_kernel_ms, double* obs_kernel_ms, int32_t* launches);
 
 /* Diagnostic: when stamps_dev (device, >= 32 uint64) is non-null, every k_step wave adds the
