@@ -571,7 +571,7 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
                                                        float b1, float b2, float eps, SegTable segs,
                                                        uint16_t* __restrict__ mirror) {
     __shared__ float red[kAdamThreads / kWave];
-    __shared__ float coef_s;
+    __shared__ float coef_s, step_size_s, bc2_sqrt_s;
     float s = 0.f;
     for (int k = threadIdx.x; k < nnp; k += kAdamThreads) s += np[k];
     s = wave_sum(s);
@@ -582,14 +582,15 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
         for (int w = 0; w < kAdamThreads / kWave; ++w) t += red[w];
         // torch.nn.utils.clip_grad_norm_: coef = max_norm / (total_norm + 1e-6), clamped to 1
         coef_s = max_norm > 0.f ? fminf(max_norm / (sqrtf(t) + 1e-6f), 1.f) : 1.f;
+        // bias corrections once per block (fp64 pow / sqrt are long instruction sequences)
+        const double ts = *step_p + 1.0;
+        step_size_s = float(*lr_p / (1.0 - pow(double(b1), ts)));
+        bc2_sqrt_s = float(sqrt(1.0 - pow(double(b2), ts)));
     }
     __syncthreads();
     const float coef = coef_s;
-    const double t = *step_p + 1.0;
-    const double bc1 = 1.0 - pow(double(b1), t);
-    const double bc2 = 1.0 - pow(double(b2), t);
-    const float step_size = float(*lr_p / bc1);
-    const float bc2_sqrt = float(sqrt(bc2));
+    const float step_size = step_size_s;
+    const float bc2_sqrt = bc2_sqrt_s;
     const int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x;
     if (i >= n) return;
     const float gi = g[i] * coef;

@@ -407,7 +407,8 @@ class FusedPPOUpdate:
                    "ppo_obs_stats_update")
         self._trunk(ds["obs"], self.mb_idx, B, self.h, self.h_last_f, self.head)
         nl = len(self.linears)
-        self.flat.zero_grad()
+        # no zero_grad: every entry of the [grads | kl] bucket is written below (loss finalize: head
+        # biases, log-sigma, kl; the reduce jobs: every weight and bias gradient)
         _check(L.ppo_loss_grad(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
                                _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
                                _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.dhead),
