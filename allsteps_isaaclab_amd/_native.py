@@ -147,7 +147,8 @@ def build_native(verbose: bool = False) -> str:
     subprocess.run(cmd, check=True)
     # PPO-update kernels (include/ppo.h) -> libppo_hip.so
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-I", INCLUDE, "-o", PPO_LIB_PATH, os.path.join(CSRC, "ppo_kernels.hip"), os.path.join(CSRC, "ppo_mlp.hip")]
+           "-I", INCLUDE, "-o", PPO_LIB_PATH, os.path.join(CSRC, "ppo_kernels.hip"), os.path.join(CSRC, "ppo_mlp.hip"),
+           os.path.join(CSRC, "ppo_wgrad.hip")]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -513,30 +513,41 @@ __global__ void __launch_bounds__(64) k_meter_update(const float* __restrict__ p
 
 struct JobTable {
     ppo_reduce_job_t j[PPO_MAX_JOBS];
-    int64_t start[PPO_MAX_JOBS + 1];
+    int64_t start[PPO_MAX_JOBS + 1];  // first thread of each job
+    int vec[PPO_MAX_JOBS];            // columns per thread: 4 (float4 path) or 1
     int n;
 };
 
+template <int V>
+__device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int64_t o) {
+    typedef float fv __attribute__((ext_vector_type(V)));
+    const int cols = jb.dst_cols / V;
+    const int r = int(o / cols), c = int(o % cols) * V;
+    const float* src = jb.src + int64_t(r) * jb.src_cols + c;
+    fv s = {};
+    int q = 0;
+    for (; q + 8 <= jb.S; q += 8) {  // eight loads in flight, added in order (fixed summation order)
+        fv v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; q < jb.S; ++q) s += *reinterpret_cast<const fv*>(src + int64_t(q) * jb.src_n);
+    *reinterpret_cast<fv*>(jb.dst + int64_t(r) * jb.dst_stride + c) = s;
+}
+
+// dst[r][c] = sum_q src[q][r][c] in q order; one thread per output element, or per 4 consecutive
+// elements when the job's strides and pointers allow 16-B accesses (the same per-element sums)
 __global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
     const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= t.start[t.n]) return;
     int k = 0;
     while (e >= t.start[k + 1]) ++k;
-    const ppo_reduce_job_t& jb = t.j[k];
-    const int64_t o = e - t.start[k];
-    const int r = int(o / jb.dst_cols), c = int(o % jb.dst_cols);
-    const float* src = jb.src + int64_t(r) * jb.src_cols + c;
-    float s = 0.f;
-    int q = 0;
-    for (; q + 8 <= jb.S; q += 8) {  // eight loads in flight, added in order (fixed summation order)
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = src[int64_t(q + u) * jb.src_n];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; q < jb.S; ++q) s += src[int64_t(q) * jb.src_n];
-    jb.dst[int64_t(r) * jb.dst_stride + c] = s;
+    if (t.vec[k] == 4)
+        reduce_cols<4>(t.j[k], e - t.start[k]);
+    else
+        reduce_cols<1>(t.j[k], e - t.start[k]);
 }
 
 // ------------------------------------------------------------------------------ clip + Adam
@@ -729,7 +740,10 @@ int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stre
         if (j.S <= 0 || j.dst_cols <= 0 || j.src_cols < j.dst_cols || j.dst_stride < j.dst_cols || !j.src || !j.dst)
             return fail(-1, "ppo_reduce_rows: bad job");
         t.j[k] = j;
-        t.start[k + 1] = t.start[k] + int64_t(j.out_rows) * j.dst_cols;
+        const bool v4 = j.dst_cols % 4 == 0 && j.src_cols % 4 == 0 && j.dst_stride % 4 == 0 && j.src_n % 4 == 0 &&
+                        (reinterpret_cast<uintptr_t>(j.src) | reinterpret_cast<uintptr_t>(j.dst)) % 16 == 0;
+        t.vec[k] = v4 ? 4 : 1;
+        t.start[k + 1] = t.start[k] + int64_t(j.out_rows) * j.dst_cols / t.vec[k];
     }
     const int64_t n = t.start[njobs];
     hipLaunchKernelGGL(k_reduce_rows, dim3(unsigned((n + 255) / 256)), dim3(256), 0, S(stream), t);

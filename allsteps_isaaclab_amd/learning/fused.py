@@ -60,6 +60,11 @@ class PpoMlpBwd(C.Structure):
                 ("h_stride", C.c_int32)]
 
 
+class PpoWgrad(C.Structure):
+    _fields_ = [("dz", C.c_void_p * 5), ("hin", C.c_void_p * 5), ("part", C.c_void_p * 5), ("kin", C.c_int32 * 5),
+                ("hin_stride", C.c_int32 * 5), ("rows", C.c_int32), ("splits", C.c_int32), ("layers", C.c_int32)]
+
+
 class PpoSeg(C.Structure):
     _fields_ = [("off", C.c_int64), ("len", C.c_int64), ("moff", C.c_int64), ("cols", C.c_int32),
                 ("mstride", C.c_int32), ("trans", C.c_int32)]
@@ -70,7 +75,7 @@ EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
                     "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update",
-                    "ppo_mlp_backward"]
+                    "ppo_mlp_backward", "ppo_weight_grads"]
 
 
 def load() -> C.CDLL:
@@ -97,6 +102,7 @@ def load() -> C.CDLL:
     L.ppo_counter_add.argtypes = [V, I64, V]
     L.ppo_mlp_forward.argtypes = [C.POINTER(PpoMlpFwd), V]
     L.ppo_mlp_backward.argtypes = [C.POINTER(PpoMlpBwd), V]
+    L.ppo_weight_grads.argtypes = [C.POINTER(PpoWgrad), V]
     L.ppo_rollout_post_blocks.argtypes = [I32]
     L.ppo_rollout_post.argtypes = [V, V, V, V, I32, F32, F32, F32, I32, V, V, V, V, V, V]
     L.ppo_meter_update.argtypes = [V, I32, F32, V, V, V]
@@ -251,6 +257,15 @@ class FusedPPOUpdate:
                 bw.dz[k] = self.dzs[k].data_ptr()
             bw.h5, bw.rows, bw.h_stride = self.h_last_f.data_ptr(), B, self.h[1].stride(0)
             self._mlp_bwd_args = bw
+            # split-K partials of the weight / bias gradients, (S, 256, 72 | 264) fp32 per layer
+            self.mfma_wgrad = bool(getattr(agent, "config", {}).get("mfma_wgrad", True))
+            self.wg_part = [torch.empty(self.S, 256, t.shape[1], device=dev) for t in self.h]
+            wg = PpoWgrad()
+            for k in range(5):
+                wg.dz[k], wg.hin[k], wg.part[k] = self.dzs[k].data_ptr(), self.h[k].data_ptr(), self.wg_part[k].data_ptr()
+                wg.kin[k], wg.hin_stride[k] = 64 if k == 0 else 256, self.h[k].shape[1]
+            wg.rows, wg.splits, wg.layers = B, self.S, 5
+            self._wgrad_args = wg
         self.segs = (PpoSeg * max(len(segs), 1))(*segs)
         self.nseg = len(segs)
         c = agent.config
@@ -471,12 +486,17 @@ class FusedPPOUpdate:
         keep.append(pw)
         jobs.append(PpoReduceJob(pw.data_ptr(), self.gWh.data_ptr(), S, A + 1, 256, 256, 256, pw.numel() // S))
         _check(L.ppo_mlp_backward(C.byref(self._mlp_bwd_args), s), "ppo_mlp_backward")
+        if self.mfma_wgrad:
+            _check(L.ppo_weight_grads(C.byref(self._wgrad_args), s), "ppo_weight_grads")
         for i, m in enumerate(self.linears):
             hin = self.h[i]
             w = hin.shape[1]                     # 72 or 264: [features | 1 | 0 ...]
             ones = 64 if i == 0 else 256
-            gw = torch.bmm(self.dzs[i].view(S, B // S, 256).transpose(1, 2), hin.view(S, B // S, w),
-                           out_dtype=torch.float32)  # (S, 256, w)
+            if self.mfma_wgrad:
+                gw = self.wg_part[i]             # (S, 256, w), bias sums in column `ones`
+            else:
+                gw = torch.bmm(self.dzs[i].view(S, B // S, 256).transpose(1, 2), hin.view(S, B // S, w),
+                               out_dtype=torch.float32)  # (S, 256, w)
             keep.append(gw)
             n_s = gw.numel() // S
             jobs.append(PpoReduceJob(gw.data_ptr(), self.gW[i].data_ptr(), S, 256, w, m.in_features, m.in_features, n_s))

@@ -17,7 +17,9 @@
  *   ppo_sqnorm / ppo_adam                 clip_grad_norm_ + Adam over the flat parameter buffer, and
  *                                         the bf16 mirror of the trunk weights for the next forward
  *   ppo_tail                              adaptive LR from the (rank-averaged) KL; minibatch counter
- * The trunk GEMMs stay on hipBLASLt (torch.mm / addmm / split-K bmm).
+ *   ppo_mlp_forward / ppo_mlp_backward    the whole trunk forward / input-gradient chain (MFMA)
+ *   ppo_weight_grads                      split-K weight + bias gradients of all trunk layers (MFMA)
+ * The head weight gradient (fp32) stays a hipBLASLt split-K bmm.
  *
  * Minibatch rows are selected on the device: row r of minibatch i is dataset row i*mb_rows + r with i
  * read from `mb_idx` (int32, device), so one captured graph serves every minibatch.
@@ -154,6 +156,24 @@ typedef struct {
     int32_t rows, nh, h_stride;
 } ppo_mlp_bwd_t;
 int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream);
+
+/* Split-K weight + bias gradients of the trunk layers, all layers in one launch (the Linear weight /
+ * bias gradients of loss.backward() in a2c_continuous.py calc_gradients; replaces five per-layer
+ * split-K `torch.bmm(dz^T, [h | 1])` calls):
+ *   part[l][s][o][c]   = sum_{b in split s} dz[l][b][o] * hin[l][b][c]   (o < 256, c < kin[l])
+ *   part[l][s][o][kin] = sum_{b in split s} dz[l][b][o]                   (bias column)
+ * dz[l]: rows x 256 bf16; hin[l]: rows x hin_stride[l] bf16 (kin[l] = 64 or 256 features); part[l]:
+ * splits x 256 x hin_stride[l] fp32 (columns past kin[l] untouched).  Split s covers rows
+ * [rows*s/splits, rows*(s+1)/splits); the partials are summed by ppo_reduce_rows. */
+typedef struct {
+    const uint16_t* dz[5];
+    const uint16_t* hin[5];
+    float* part[5];
+    int32_t kin[5];
+    int32_t hin_stride[5];
+    int32_t rows, splits, layers;
+} ppo_wgrad_t;
+int ppo_weight_grads(const ppo_wgrad_t* args_host, void* stream);
 
 /* Rollout bookkeeping of one step (a2c_common.play_steps after env_step), per env:
  *   shaped = (reward + shift) * scale [+ gamma * value * time_out]  -> shaped_out (td rewards[n])

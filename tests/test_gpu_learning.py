@@ -355,6 +355,54 @@ def test_fused_mlp_forward_kernel(rows):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rows,splits", [(32768, 32), (1000, 3), (64, 1)])
+def test_weight_grads_kernel(rows, splits):
+    """ppo_weight_grads (MFMA, transposed LDS reads) vs fp32 torch on the same bf16 inputs: per split
+    s, part[s] = dz[rows of s]^T [hin | 1] over columns 0..kin (the products of two bf16 values are
+    exact in fp32; only the summation order differs).  Columns past the bias column stay untouched;
+    ragged splits (rows not a multiple of splits or of the 64-row stage) are covered."""
+    import ctypes as C
+
+    from allsteps_isaaclab_amd.learning import fused as FU
+
+    L = FU.load()
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(5)
+    widths = [72] + [264] * 4
+    dz = [torch.randn(rows, 256, device=dev, generator=g).to(torch.bfloat16) for _ in range(5)]
+    hin = [torch.randn(rows, w, device=dev, generator=g).to(torch.bfloat16) for w in widths]
+    part = [torch.full((splits, 256, w), float("nan"), device=dev) for w in widths]
+    a = FU.PpoWgrad()
+    for k in range(5):
+        a.dz[k], a.hin[k], a.part[k] = dz[k].data_ptr(), hin[k].data_ptr(), part[k].data_ptr()
+        a.kin[k], a.hin_stride[k] = 64 if k == 0 else 256, widths[k]
+    a.rows, a.splits, a.layers = rows, splits, 5
+    FU._check(L.ppo_weight_grads(C.byref(a), torch.cuda.current_stream().cuda_stream), "ppo_weight_grads")
+    torch.cuda.synchronize()
+    for k in range(5):
+        kin = 64 if k == 0 else 256
+        for s in range(splits):
+            r0, r1 = rows * s // splits, rows * (s + 1) // splits
+            d, h = dz[k][r0:r1].double(), hin[k][r0:r1].double()
+            ref = torch.cat([d.t() @ h[:, :kin], d.sum(0)[:, None]], 1).float()
+            got = part[k][s, :, :kin + 1]
+            torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5 * (r1 - r0) ** 0.5, msg=f"layer {k} split {s}")
+        assert torch.isnan(part[k][:, :, kin + 1:]).all(), k
+
+
+def test_weight_grads_rejects_bad_arguments():
+    import ctypes as C
+
+    from allsteps_isaaclab_amd.learning import fused as FU
+
+    L = FU.load()
+    a = FU.PpoWgrad()
+    a.rows, a.splits, a.layers = 128, 1, 1
+    assert L.ppo_weight_grads(C.byref(a), None) == -1  # null pointers: refused before any launch
+    assert b"bad arguments" in L.ppo_last_error()
+
+
+@pytest.mark.gpu
 def test_rollout_bookkeeping_kernel_matches_reference_ops(tmp_path):
     """ppo_rollout_post + ppo_meter_update == the play_steps tensor ops (shaping, value bootstrap,
     episode sums, AverageMeter updates, reset of the sums) over several steps."""
