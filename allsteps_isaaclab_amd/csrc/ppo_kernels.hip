@@ -526,12 +526,12 @@ __device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int64_t 
     const float* src = jb.src + int64_t(r) * jb.src_cols + c;
     fv s = {};
     int q = 0;
-    for (; q + 8 <= jb.S; q += 8) {  // eight loads in flight, added in order (fixed summation order)
-        fv v[8];
+    for (; q + 16 <= jb.S; q += 16) {  // sixteen loads in flight, added in order (fixed summation order)
+        fv v[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n);
+        for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
+        for (int u = 0; u < 16; ++u) s += v[u];
     }
     for (; q < jb.S; ++q) s += *reinterpret_cast<const fv*>(src + int64_t(q) * jb.src_n);
     *reinterpret_cast<fv*>(jb.dst + int64_t(r) * jb.dst_stride + c) = s;

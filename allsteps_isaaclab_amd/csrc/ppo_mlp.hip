@@ -45,57 +45,73 @@ union Frag {
     uint16_t s[8];
 };
 
-// A fragment of k-step s of input tile kt for output row `row` (lane half h): two 4-element runs
+// LDS image of a layer's weights: row o = output feature, row stride K + kPad; inside every 16-element
+// block of a row the four 4-element quads are stored in the order [0-3, 8-11, 4-7, 12-15], so the A
+// fragment of either lane half (quads {0, 2} for h = 0, {1, 3} for h = 1 of the k-step's block, the
+// permuted k order above) is ONE 16-B read: ds_read_b128, conflict-free (row stride 132 dwords puts
+// the 16 rows of a lane group on distinct 4-bank slots).
 __device__ __forceinline__ bf16x8 load_a(const uint16_t* lds, int stride, int row, int kt, int s, int h) {
-    Frag f;
-    const uint16_t* p = lds + row * stride + kt * 32 + 16 * s + 4 * h;
-    f.q[0] = *reinterpret_cast<const uint2*>(p);
-    f.q[1] = *reinterpret_cast<const uint2*>(p + 8);
-    return f.v;
+    return *reinterpret_cast<const bf16x8*>(lds + row * stride + kt * 32 + 16 * s + 8 * h);
 }
 
-// stage a rows x K bf16 matrix (row stride K) into LDS (row stride K + kPad); eight 16-B loads in
-// flight per thread so the copy runs at L2 bandwidth rather than one load latency per chunk
+// stage a 256 x K bf16 matrix (row stride K) into the LDS image above.  A thread copies whole 16-element
+// blocks (two 16-B loads, quads re-paired in registers, two 16-B stores); addresses are one per-thread
+// base plus compile-time offsets, so the PPO_STAGE_DEPTH blocks of a round are all in flight at once.
+#ifndef PPO_STAGE_DEPTH
+#define PPO_STAGE_DEPTH 4
+#endif
 template <int K>
 __device__ __forceinline__ void stage_w(uint16_t* lds, const uint16_t* __restrict__ w) {
-    constexpr int chunks = kHid * K / 8;
-    constexpr int per = chunks / (64 * kWaves);
-    static_assert(per % 8 == 0, "staging unroll");
+    constexpr int kBlk = K / 16;                           // blocks per row
+    constexpr int kRowsPerU = 64 * kWaves / kBlk;          // rows advanced per block of a thread
+    constexpr int per = kHid / kRowsPerU;                  // blocks per thread
+    constexpr int D = per < PPO_STAGE_DEPTH ? per : PPO_STAGE_DEPTH;
+    static_assert(64 * kWaves % kBlk == 0 && per % D == 0, "staging split");
+    const int t = threadIdx.x;
+    const uint16_t* __restrict__ src = w + (t / kBlk) * K + (t % kBlk) * 16;
+    uint16_t* dst = lds + (t / kBlk) * (K + kPad) + (t % kBlk) * 16;
 #pragma unroll
-    for (int c0 = 0; c0 < per; c0 += 8) {
-        uint4 v[8];
+    for (int u0 = 0; u0 < per; u0 += D) {
+        uint4 lo[D], hi[D];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int c = (c0 + u) * (64 * kWaves) + threadIdx.x;
-            v[u] = *reinterpret_cast<const uint4*>(w + (c / (K / 8)) * K + (c % (K / 8)) * 8);
+        for (int u = 0; u < D; ++u) {
+            lo[u] = *reinterpret_cast<const uint4*>(src + (u0 + u) * kRowsPerU * K);
+            hi[u] = *reinterpret_cast<const uint4*>(src + (u0 + u) * kRowsPerU * K + 8);
         }
+        __builtin_amdgcn_sched_barrier(0);  // keep the round's loads together (the scheduler sinks them)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int c = (c0 + u) * (64 * kWaves) + threadIdx.x;
-            *reinterpret_cast<uint4*>(lds + (c / (K / 8)) * (K + kPad) + (c % (K / 8)) * 8) = v[u];
+        for (int u = 0; u < D; ++u) {
+            uint16_t* d = dst + (u0 + u) * kRowsPerU * (K + kPad);
+            *reinterpret_cast<uint4*>(d) = make_uint4(lo[u].x, lo[u].y, hi[u].x, hi[u].y);      // e0-3, e8-11
+            *reinterpret_cast<uint4*>(d + 8) = make_uint4(lo[u].z, lo[u].w, hi[u].z, hi[u].w);  // e4-7, e12-15
         }
     }
 }
 
 // acc[ot] = W (256 x K, in LDS) . X (K x 32); xb[kt][s] are the B fragments of X.  k-steps outer,
-// output tiles inner: eight independent accumulator chains keep the MFMA pipe full.
+// output tiles inner: eight independent accumulator chains; the A fragments of k-step n + 1 are read
+// while the MFMAs of k-step n run (two fragment sets).
 template <int K>
 __device__ __forceinline__ void layer_mma(const uint16_t* lds, const bf16x8 (&xb)[kTiles][2], f32x16 (&acc)[kTiles],
                                           int lane) {
+    constexpr int NS = K / 16;
     const int i = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int ot = 0; ot < kTiles; ++ot) acc[ot] = f32x16{};
+    bf16x8 af[2][kTiles];
 #pragma unroll
-    for (int kt = 0; kt < K / 32; ++kt) {
+    for (int ot = 0; ot < kTiles; ++ot) af[0][ot] = load_a(lds, K + kPad, ot * 32 + i, 0, 0, h);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            bf16x8 af[kTiles];
-#pragma unroll
-            for (int ot = 0; ot < kTiles; ++ot) af[ot] = load_a(lds, K + kPad, ot * 32 + i, kt, s, h);
+    for (int n = 0; n < NS; ++n) {
+        if (n + 1 < NS) {
 #pragma unroll
             for (int ot = 0; ot < kTiles; ++ot)
-                acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ot], xb[kt][s], acc[ot], 0, 0, 0);
+                af[(n + 1) & 1][ot] = load_a(lds, K + kPad, ot * 32 + i, (n + 1) >> 1, (n + 1) & 1, h);
         }
+        __builtin_amdgcn_sched_barrier(0);  // next k-step's reads stay ahead of this k-step's MFMAs
+#pragma unroll
+        for (int ot = 0; ot < kTiles; ++ot)
+            acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[n & 1][ot], xb[n >> 1][n & 1], acc[ot], 0, 0, 0);
     }
 }
 
@@ -152,7 +168,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
         }
         // epilogue: bias + ELU in fp32, store, and the next layer's B fragments
         const float* bias = lbias + l * kHid;
-        uint16_t* __restrict__ hout = l < 4 ? a.h[l] : nullptr;
+        // per-lane row bases: every store below is base + a compile-time offset (no per-store address)
+        uint16_t* __restrict__ hrow = l < 4 && a.h[l] ? a.h[l] + int64_t(row) * a.h_stride + 4 * h : nullptr;
+        float* __restrict__ h5row = l == 4 && a.h5 ? a.h5 + int64_t(row) * kHid + 4 * h : nullptr;
 #pragma unroll
         for (int ot = 0; ot < kTiles; ++ot) {
             Frag f[2];
@@ -178,10 +196,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
             if (live) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const int c = ot * 32 + 8 * g + 4 * h;
-                    if (hout) *reinterpret_cast<uint2*>(hout + int64_t(row) * a.h_stride + c) = f[g >> 1].q[g & 1];
-                    if (l == 4 && a.h5)
-                        *reinterpret_cast<float4*>(a.h5 + int64_t(row) * kHid + c) =
+                    if (hrow) *reinterpret_cast<uint2*>(hrow + ot * 32 + 8 * g) = f[g >> 1].q[g & 1];
+                    if (h5row)
+                        *reinterpret_cast<float4*>(h5row + ot * 32 + 8 * g) =
                             make_float4(acc[ot][4 * g], acc[ot][4 * g + 1], acc[ot][4 * g + 2], acc[ot][4 * g + 3]);
                 }
             }

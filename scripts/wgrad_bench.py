@@ -47,9 +47,25 @@ def t(fn, n=50):
     return e0.elapsed_time(e1) / n * 1000
 
 
-tk, tl = t(kernel), t(library)
+jobs, keep = [], []
+for k in range(5):
+    w, kin = widths[k], 64 if k == 0 else 256
+    n_s = 256 * w
+    gw = torch.empty(256, kin, device=dev)
+    gb = torch.empty(256, device=dev)
+    jobs += [FU.PpoReduceJob(part[k].data_ptr(), gw.data_ptr(), S, 256, w, kin, kin, n_s),
+             FU.PpoReduceJob(part[k].data_ptr() + 4 * kin, gb.data_ptr(), S, 256, w, 1, 1, n_s)]
+    keep += [gw, gb]
+arr = (FU.PpoReduceJob * len(jobs))(*jobs)
+
+
+def reduce():
+    FU._check(L.ppo_reduce_rows(arr, len(jobs), torch.cuda.current_stream().cuda_stream), "reduce")
+
+
+tk, tl, tr = t(kernel), (t(library) if B % S == 0 else float('nan')), t(reduce)
 flops = 2 * B * 256 * (65 + 4 * 257)
 in_bytes = sum(d.numel() * 2 for d in dz) + B * 2 * (64 + 4 * 256)
 out_bytes = S * 256 * 4 * (65 + 4 * 257)
-print(json.dumps({"rows": B, "splits": S, "kernel_us": round(tk, 1), "bmm_us": round(tl, 1),
+print(json.dumps({"rows": B, "splits": S, "kernel_us": round(tk, 1), "bmm_us": round(tl, 1), "reduce_us": round(tr, 1),
                   "kernel_tflops": round(flops / tk / 1e6, 1), "kernel_gbs": round((in_bytes + out_bytes) / tk / 1e3, 1)}))
