@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = [
     "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
     "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask", "as_set_graph_safe",
-    "as_profile_sampled",
+    "as_profile_sampled", "as_hbm_copy",
 ]
 
 
@@ -118,6 +118,7 @@ def load() -> C.CDLL:
     L.as_generate_stones.argtypes = [V, I32, V, V]
     L.as_step_counters.argtypes = [V, C.POINTER(V)]
     L.as_get_curriculum_host.argtypes = [V, C.POINTER(I32)]
+    L.as_hbm_copy.argtypes = [V, V, I64, V]
     L.as_last_error.restype = C.c_char_p
     for name in EXPORTED_SYMBOLS:
         if name != "as_last_error":
@@ -132,6 +133,33 @@ def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = load().as_last_error().decode(errors="replace")
         raise NativeError(f"{what} failed ({rc}): {msg}")
+
+
+def hbm_copy_bandwidth(device, nbytes: int = 2 << 30, iters: int = 20) -> float:
+    """Achievable HBM bandwidth (GB/s, read + write bytes) of the in-tree STREAM-copy kernel
+    (as_hbm_copy) between two `nbytes` device buffers, timed with HIP events on the current stream."""
+    import torch
+
+    L = load()
+    n16 = nbytes // 16
+    src = torch.empty(n16 * 4, dtype=torch.float32, device=device).uniform_()
+    dst = torch.empty_like(src)
+    stream = torch.cuda.current_stream(device)
+    sp = C.c_void_p(stream.cuda_stream)
+    for _ in range(3):
+        check(L.as_hbm_copy(C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), n16, sp), "as_hbm_copy")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        check(L.as_hbm_copy(C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), n16, sp), "as_hbm_copy")
+    e1.record(stream)
+    e1.synchronize()
+    ok = bool(torch.equal(src, dst))
+    ms = e0.elapsed_time(e1) / iters
+    del src, dst
+    if not ok:
+        raise NativeError("as_hbm_copy: destination differs from source")
+    return 2.0 * n16 * 16 / (ms * 1e-3) / 1e9
 
 
 def build_native(verbose: bool = False) -> str:

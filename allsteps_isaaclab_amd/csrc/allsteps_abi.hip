@@ -26,6 +26,23 @@ int fail(int code, const std::string& msg) {
     if (_e != hipSuccess) return fail(AS_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
   } while (0)
 
+// STREAM-style copy: each thread moves 4 x 16 B per iteration (loads issued before stores), grid
+// stride over the whole buffer, non-temporal so the copy does not thrash the MALL it measures past.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_hbm_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
+                                                   int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * 256 * 4;
+  for (int64_t base = (int64_t)blockIdx.x * 256 * 4 + threadIdx.x; base < n; base += stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * 256 < n) v[u] = __builtin_nontemporal_load(src + base + u * 256);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * 256 < n) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+  }
+}
+
 }  // namespace
 
 struct as_env {
@@ -51,6 +68,18 @@ struct as_env {
 extern "C" {
 
 int as_abi_version(void) { return AS_ABI_VERSION; }
+
+int as_hbm_copy(void* dst, const void* src, int64_t n16, void* stream) {
+  if (!dst || !src || n16 < 0) return fail(AS_ERR_INVALID, "as_hbm_copy: null pointer or negative size");
+  if (((uintptr_t)dst | (uintptr_t)src) & 15) return fail(AS_ERR_INVALID, "as_hbm_copy: pointers must be 16-B aligned");
+  if (n16 == 0) return AS_OK;
+  const int64_t per_block = 256 * 4;
+  const int64_t blocks = std::min<int64_t>((n16 + per_block - 1) / per_block, 256 * 32);
+  hipLaunchKernelGGL(k_hbm_copy, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (u32x4*)dst,
+                     (const u32x4*)src, n16);
+  HIP_TRY(hipGetLastError());
+  return AS_OK;
+}
 
 const char* as_last_error(void) { return g_err.c_str(); }
 

@@ -59,14 +59,26 @@ def parse():
     return p.parse_args()
 
 
-def pmc_traffic(num_envs: int):
-    """HBM bytes per k_step launch from the committed rocprofv3 PMC passes (scripts/profile.sh writes
-    profiles/traffic_k_step.json: FETCH_SIZE x 2 + WRITE_SIZE); None when absent or for another size."""
+def pmc_record(num_envs: int) -> dict:
+    """The committed rocprofv3 PMC figures of k_step (scripts/profile.sh writes
+    profiles/traffic_k_step.json): HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE) and the VALU
+    issue fraction (SQ_INSTS_VALU vs the SIMDs' cycles); empty when absent or for another size."""
     try:
         with open(os.path.join(ROOT, "profiles", "traffic_k_step.json")) as f:
             t = json.load(f)
-        return t["traffic_bytes_per_launch"] if int(t["num_envs"]) == num_envs else None
+        return t if int(t["num_envs"]) == num_envs else {}
     except (OSError, KeyError, ValueError):
+        return {}
+
+
+def measured_hbm_peak(device) -> float | None:
+    """Achievable HBM GB/s of the in-tree STREAM-copy kernel (as_hbm_copy, 2 x 2 GiB buffers)."""
+    from allsteps_isaaclab_amd import _native
+
+    try:
+        return round(_native.hbm_copy_bandwidth(device), 1)
+    except Exception as e:  # reported, never fatal for the env metric
+        print(f"bench: as_hbm_copy probe failed: {e}", file=sys.stderr)
         return None
 
 
@@ -78,7 +90,7 @@ def cpu_baseline(num_envs: int, level: int, threads: int) -> dict:
 
     O.build()
     orc = O.Oracle()
-    n = min(num_envs, 4096)
+    n = num_envs  # the sample is bounded by time (~20 CPU-s), not by size
     st = orc.state(n)
     if level == 0:
         for k in range(20):
@@ -159,6 +171,7 @@ def main():
         value = n * world * K / el
         avg_k = k_ms / max(launches, 1) / 1e3  # s per k_step launch
         achieved = K_STEP_BYTES * n / avg_k / 1e9
+        pmc = pmc_record(n)
         line = {
             "metric": BASELINE_METRIC,
             "value": round(value, 1),
@@ -182,9 +195,12 @@ def main():
             "kernels_ms": {"k_step_avg": round(k_ms / max(launches, 1), 5),
                            "k_obs_avg": round(o_ms / max(launches, 1), 5)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(n),
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc.get("traffic_bytes_per_launch"),
                          "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/traffic_k_step.json)",
-                         "kernel": "k_step", "bytes_per_env": K_STEP_BYTES},
+                         "kernel": "k_step", "bytes_per_env": K_STEP_BYTES,
+                         "peak_measured": measured_hbm_peak(device),
+                         "peak_measured_method": "in-tree STREAM copy (as_hbm_copy), read + write GB/s",
+                         "valu_issue_frac": pmc.get("valu_issue_frac")},
             "cpu_baseline": None,
             "resets_last_step": resets,
         }

@@ -212,6 +212,12 @@ int as_set_graph_safe(as_env_t* env, int32_t on);
 int as_step_counters(as_env_t* env, const int32_t** counters_dev);
 int as_get_curriculum_host(as_env_t* env, int32_t* level_host); /* synchronises the stream */
 
+/* Diagnostic (SURVEY §8d "confirm with an in-repo STREAM-copy kernel"): dst[i] = src[i] for
+ * n16 16-byte elements (both device pointers 16-B aligned, non-overlapping), a grid-stride copy
+ * with non-temporal loads/stores sized to fill all 256 CUs.  bench.py times it with HIP events to
+ * report the achievable HBM bandwidth beside the 8 TB/s spec peak. */
+int as_hbm_copy(void* dst, const void* src, int64_t n16, void* stream);
+
 int as_abi_version(void);
 const char* as_last_error(void);
 

@@ -57,6 +57,25 @@ def test_library_exports_and_loads():
     assert L.as_abi_version() == _native.ABI_VERSION
 
 
+@pytest.mark.parametrize("n16", [1, 1023, 1024 * 256 * 40 + 7])
+def test_hbm_copy_probe(n16):
+    """as_hbm_copy (bench.py's measured HBM peak) copies every 16-B element, ragged tails included,
+    and rejects misaligned pointers."""
+    import ctypes as C
+
+    from allsteps_isaaclab_amd import _native
+
+    L = _native.load()
+    src = torch.randint(-2**31, 2**31 - 1, (n16 * 4 + 4,), dtype=torch.int32, device="cuda:0")
+    dst = torch.zeros_like(src)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _native.check(L.as_hbm_copy(C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), n16, s), "as_hbm_copy")
+    torch.cuda.synchronize()
+    assert torch.equal(dst[: n16 * 4], src[: n16 * 4])
+    assert not dst[n16 * 4:].any(), "copy wrote past n16 elements"
+    assert L.as_hbm_copy(C.c_void_p(dst.data_ptr() + 4), C.c_void_p(src.data_ptr()), 1, s) != 0
+
+
 @pytest.mark.parametrize("level", [0, 3, 9])
 def test_stones_vs_golden(level):
     g = golden("footsteps")
