@@ -121,12 +121,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; ALLSTEPS_DIST_BACKEND=gloo lets ranks share one GPU (the rehearsal in
+    # tests/test_gpu_parity.py::test_bench_two_ranks_one_gpu), the default is RCCL ("nccl")
+    backend = os.environ.get("ALLSTEPS_DIST_BACKEND", "nccl")
+    device = torch.device(f"cuda:{local % max(torch.cuda.device_count(), 1) if backend == 'gloo' else local}")
+    torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    device = torch.device(f"cuda:{local}")
-    torch.cuda.set_device(device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv
     from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
@@ -162,7 +167,7 @@ def main():
     el = time.perf_counter() - t0
     k_ms, o_ms, launches = env._native.profile_read()
     if world > 1:
-        tt = torch.tensor([el], device=device, dtype=torch.float64)
+        tt = torch.tensor([el], device=device if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     resets = int(env.reset_buf.sum().item())

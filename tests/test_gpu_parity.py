@@ -404,3 +404,30 @@ def test_c3_large_config_invariants():
     assert 0 <= int(env.state["curriculum"][0]) <= 9
     assert bool(((env.state["swing"] == 0) | (env.state["swing"] == 1)).all())
     env.close()
+
+
+def test_bench_two_ranks_one_gpu():
+    """Rehearsal of the driver's multi-GPU bench launch (torch.distributed.run, one process per rank,
+    barrier + max-over-ranks timing) with two ranks sharing cuda:0 over gloo: rank 0 prints ONE JSON
+    line whose value counts both ranks' envs."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, ALLSTEPS_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20",
+           "--warmup", "3", "--num-envs", "256", "--no-cpu-baseline", "--no-train"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["config"]["global_envs"] == 512 and line["scaling"] == "weak"
+    assert abs(line["value"] - 512 * 20 / (line["ms_per_step"] * 20 / 1e3)) / line["value"] < 1e-2
