@@ -288,6 +288,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
             acc[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[k * kHs + ot * 32 + i], bq[t], acc[ot], 0, 0, 0);
     }
     bf16x8 xb[kTiles][2];
+    uint2 yb[kTiles][4];  // bf16 activations of layer l - 1, loaded while layer l's MFMAs run
     for (int l = 4; l >= 0; --l) {
         // dz_l = dh * elu'(y_l), y_l = layer-l activations (layer 5 in fp32, the others bf16)
         uint16_t* __restrict__ dzo = a.dz[l];
@@ -307,7 +308,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
                     y[4 * g + 3] = q.w;
                 } else {
                     Frag ff;
-                    ff.q[0] = *reinterpret_cast<const uint2*>(a.h[l] + int64_t(row) * a.h_stride + c);
+                    ff.q[0] = yb[ot][g];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) y[4 * g + e] = float(ff.v[e]);
                 }
@@ -331,6 +332,14 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
         __syncthreads();
         stage_w<kHid>(lds, a.wt[l - 1]);
         __syncthreads();
+        // issued after the staging loads have been waited for, so only the MFMAs below cover them
+        if (live) {
+            const uint16_t* __restrict__ yrow = a.h[l - 1] + int64_t(row) * a.h_stride + 4 * h;
+#pragma unroll
+            for (int ot = 0; ot < kTiles; ++ot)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) yb[ot][g] = *reinterpret_cast<const uint2*>(yrow + ot * 32 + 8 * g);
+        }
         layer_mma<kHid>(lds, xb, acc, lane);
     }
 }
