@@ -115,6 +115,16 @@ __device__ __forceinline__ void layer_mma(const uint16_t* lds, const bf16x8 (&xb
     }
 }
 
+// Row stores of a tile's bf16 chunks.  Lane (j, h) holds chunk g = features 8g + 4h + 0..3 of row j;
+// one v_permlane32_swap per dword gives the lower lanes features 8g + 0..7 and the upper lanes
+// 8(g + 1) + 0..7, so a lane writes 16 contiguous bytes at feature 8(g + h) (32-B runs per row per
+// store instead of 16-B ones).  Every lane must execute it (cross-lane), live or not.
+__device__ __forceinline__ uint4 pair_chunks(uint2 ga, uint2 gb) {
+    const auto x = __builtin_amdgcn_permlane32_swap(ga.x, gb.x, false, false);
+    const auto y = __builtin_amdgcn_permlane32_swap(ga.y, gb.y, false, false);
+    return make_uint4(x[0], y[0], x[1], y[1]);
+}
+
 // feature of register r of a tile for lane half h
 __device__ __forceinline__ int feat(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -169,7 +179,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
         // epilogue: bias + ELU in fp32, store, and the next layer's B fragments
         const float* bias = lbias + l * kHid;
         // per-lane row bases: every store below is base + a compile-time offset (no per-store address)
-        uint16_t* __restrict__ hrow = l < 4 && a.h[l] ? a.h[l] + int64_t(row) * a.h_stride + 4 * h : nullptr;
+        uint16_t* __restrict__ hrow = l < 4 && a.h[l] ? a.h[l] + int64_t(row) * a.h_stride + 8 * h : nullptr;
         float* __restrict__ h5row = l == 4 && a.h5 ? a.h5 + int64_t(row) * kHid + 4 * h : nullptr;
 #pragma unroll
         for (int ot = 0; ot < kTiles; ++ot) {
@@ -193,10 +203,16 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
             }
             xb[ot][0] = f[0].v;
             xb[ot][1] = f[1].v;
+            if (hrow) {
+                const uint4 c01 = pair_chunks(f[0].q[0], f[0].q[1]), c23 = pair_chunks(f[1].q[0], f[1].q[1]);
+                if (live) {
+                    *reinterpret_cast<uint4*>(hrow + ot * 32) = c01;
+                    *reinterpret_cast<uint4*>(hrow + ot * 32 + 16) = c23;
+                }
+            }
             if (live) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    if (hrow) *reinterpret_cast<uint2*>(hrow + ot * 32 + 8 * g) = f[g >> 1].q[g & 1];
                     if (h5row)
                         *reinterpret_cast<float4*>(h5row + ot * 32 + 8 * g) =
                             make_float4(acc[ot][4 * g], acc[ot][4 * g + 1], acc[ot][4 * g + 2], acc[ot][4 * g + 3]);
@@ -321,10 +337,11 @@ __global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
             }
             xb[ot][0] = f[0].v;
             xb[ot][1] = f[1].v;
+            const uint4 c01 = pair_chunks(f[0].q[0], f[0].q[1]), c23 = pair_chunks(f[1].q[0], f[1].q[1]);
             if (live) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    *reinterpret_cast<uint2*>(dzo + int64_t(row) * kHid + ot * 32 + 8 * g + 4 * h) = f[g >> 1].q[g & 1];
+                uint16_t* d = dzo + int64_t(row) * kHid + ot * 32 + 8 * h;
+                *reinterpret_cast<uint4*>(d) = c01;
+                *reinterpret_cast<uint4*>(d + 16) = c23;
             }
         }
         if (l == 0) break;
@@ -377,7 +394,7 @@ extern "C" int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream) {
 
 extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
     if (!args_host || !args_host->x || args_host->nh <= 0 || args_host->nh > 32 || args_host->rows <= 0 ||
-        args_host->x_stride < kK0 || args_host->h_stride < kHid || (args_host->x_stride % 4) || (args_host->h_stride % 4)) {
+        args_host->x_stride < kK0 || args_host->h_stride < kHid || (args_host->x_stride % 4) || (args_host->h_stride % 8)) {
         snprintf(g_err, sizeof(g_err), "ppo_mlp_forward: bad arguments");
         ppo_detail::set_error(g_err);
         return -1;

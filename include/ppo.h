@@ -123,7 +123,8 @@ int ppo_counter_add(int64_t* ctr, int64_t inc, void* stream);
  * fp32 heads.  x: rows x 64 bf16 (normalised obs, zero-padded 59 -> 64; row stride x_stride >= 64);
  * w[0]: 256 x 64 bf16, w[1..4]: 256 x 256 bf16 (the trunk mirror); b[l]: 256 fp32; wh: nh x 256 fp32
  * ([mu.w | value.w]), bh: nh fp32 (nh <= 32).  Outputs (row-major, NULL = skip): h[0..3] = layers
- * 1..4 (bf16, columns 0..255 of rows with stride h_stride >= 256; columns beyond are not touched),
+ * 1..4 (bf16, columns 0..255 of rows with stride h_stride >= 256, a multiple of 8; columns beyond are
+ * not touched),
  * h5 = layer 5 in fp32 (rows x 256), head = rows x nh fp32.  Each wave keeps its 32 rows' activations
  * in registers between layers (an MFMA accumulator tile is the next layer's B operand); each layer's
  * weights are staged once per workgroup in LDS. */
