@@ -230,10 +230,13 @@ def make_task(cfg, dof_names: list) -> AsTask:
     T.gain_curriculum[:] = [float(x) for x in linspace_f32(1.2, 1.2, cfg.max_curriculum + 1)]
     T.init_root[:] = list(cfg.init_root_pos)
     T.init_q[:] = [float(np.float32(x)) for x in running_start_pose()]
-    J = dof_names.index
-    T.right_idx[:] = [J(x) for x in cfg.right_body_names]
-    T.left_idx[:] = [J(x) for x in cfg.left_body_names]
-    T.neg_idx[:] = [J(x) for x in cfg.negation_body_names]
+    if all(x in dof_names for x in (*cfg.right_body_names, *cfg.left_body_names, *cfg.negation_body_names)):
+        J = dof_names.index
+        T.right_idx[:] = [J(x) for x in cfg.right_body_names]
+        T.left_idx[:] = [J(x) for x in cfg.left_body_names]
+        T.neg_idx[:] = [J(x) for x in cfg.negation_body_names]
+    # else: a model without the walker's joints (the C5 quadruped) is stepped physics-only
+    # (as_physics_step), which never reads the reset mirror tables
     T.noise_lo, T.noise_hi = cfg.initial_joint_angle_range
     T.clip_lo, T.clip_hi = cfg.initial_joint_angle_clip_range
     T.regen_footsteps = int(bool(getattr(cfg, "regenerate_footsteps", False)))

@@ -1690,14 +1690,16 @@ __global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
 }
 
 // ------------------------------------------------------------------------------------------------
-bool step_supported_nv(int nv) { return nv == 27 || nv == 6; }
+// NV = 27: the Allsteps walker (6 + 21 hinges); NV = 18: the quadruped of BASELINE C5
+// (model/anymal_c.xml, 6 + 12 hinges), stepped through as_physics_step.
+bool step_supported_nv(int nv) { return nv == 27 || nv == 18; }
 
 hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream) {
   int blocks = (a.n + EPB - 1) / EPB;
   if (nv == 27)
     hipLaunchKernelGGL(k_step<27>, dim3(blocks), dim3(64), 0, stream, a);
-  else if (nv == 6)
-    hipLaunchKernelGGL(k_step<6>, dim3(blocks), dim3(64), 0, stream, a);
+  else if (nv == 18)
+    hipLaunchKernelGGL(k_step<18>, dim3(blocks), dim3(64), 0, stream, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -17,6 +17,7 @@ MAX_LINKS = 32
 MAX_GEOMS = 32
 HERE = os.path.dirname(os.path.abspath(__file__))
 WALKER_JSON = os.path.join(HERE, "walker3d.json")
+ANYMAL_C_JSON = os.path.join(HERE, "anymal_c.json")  # BASELINE C5 quadruped (authored approximation)
 
 
 def load_json(path: str = WALKER_JSON) -> dict:
@@ -68,15 +69,18 @@ def load_model(path: str = WALKER_JSON) -> dict:
     m["cfg_dof_link"][: nl - 1] = j["cfg_dof_link"]
     m["gear"][: nl - 1] = j["gears"]
 
-    # geoms: feet first (right then left), then every other geom in link order
+    # geoms: feet first (the walker: right then left; the quadruped: its four feet), then every other
+    # geom in link order; the two sensor feet get geom_foot 0 / 1 (contact-sensor bitmasks)
     bl = j["body_link"]
-    foot_link = [bl["right_foot"], bl["left_foot"]]
+    foot_link = [bl[b] for b in j.get("sensor_feet", ["right_foot", "left_foot"])]
+    first = [bl[b] for b in j.get("contact_first", ["right_foot", "left_foot"])]
     geoms = []
     for i, L in enumerate(links):
         for g in L["geoms"]:
             foot = foot_link.index(i) if i in foot_link else -1
-            geoms.append((0 if foot >= 0 else 1, foot, i, g))
+            geoms.append((0 if i in first else 1, first.index(i) if i in first else 0, i, foot, g))
     geoms.sort(key=lambda t: (t[0], t[1], t[2]))
+    geoms = [(t[0], t[3], t[2], t[4]) for t in geoms]
     if len(geoms) > MAX_GEOMS:
         raise ValueError("too many geoms")
     m["num_geoms"] = len(geoms)
@@ -95,7 +99,7 @@ def load_model(path: str = WALKER_JSON) -> dict:
         m["geom_p0"][k] = g["p0"]
         m["geom_p1"][k] = g["p1"]
         m["geom_name"].append(g["name"])
-    m["torso_link"] = bl["torso"]
+    m["torso_link"] = bl[j.get("torso", "torso")]
     m["foot_link"] = np.array(foot_link, np.int32)
     m["link_names"] = [L["name"] for L in links]
     m["dof_names"] = list(j["cfg_dof_order"])

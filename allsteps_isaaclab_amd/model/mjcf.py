@@ -14,7 +14,9 @@ step kernel and the CPU oracle consume:
 * the DOF permutation to the PhysX/cfg DOF order of ``allsteps_env_cfg.py:133-155``.
 
 Run ``python -m allsteps_isaaclab_amd.model.mjcf <walker3d.xml> <out.json>`` to regenerate
-``walker3d.json`` (committed; the GPU box has no ``/root/reference``).
+``walker3d.json`` (committed; the GPU box has no ``/root/reference``), and
+``python -m allsteps_isaaclab_amd.model.mjcf anymal_c.xml anymal_c.json anymal_c`` for the BASELINE C5
+quadruped (an authored approximation, ``anymal_c.xml``).
 """
 
 from __future__ import annotations
@@ -41,6 +43,19 @@ CFG_DOF_ORDER = [
 ]
 # allsteps_env_cfg.py:133-155
 CFG_GEARS = [60, 80, 60, 50, 60, 60, 50, 60, 60, 60, 60, 80, 100, 60, 80, 100, 60, 90, 90, 60, 60]
+
+# Per-model compile options: DOF order, gears, the torso body and the two contact-sensor feet
+# (geom_foot 0 / 1), and the bodies whose geoms are ordered first under the contact cap.
+WALKER = {"source": "isaaclab_assets/data/mjcf/walker3d.xml", "dof_order": CFG_DOF_ORDER, "gears": CFG_GEARS,
+          "torso": "torso", "sensor_feet": ["right_foot", "left_foot"], "contact_first": ["right_foot", "left_foot"]}
+# BASELINE C5 quadruped (model/anymal_c.xml, an authored approximation): IsaacLab's ANYmal joint order
+# (PhysX breadth-first: all HAA, then HFE, then KFE, legs LF, LH, RF, RH); gear 66.67 so that the
+# Allsteps actuation 1.2 * gear * a reaches 80 N m; the front feet carry the two contact sensors.
+_LEGS = ["LF", "LH", "RF", "RH"]
+ANYMAL_C = {"source": "allsteps_isaaclab_amd/model/anymal_c.xml (authored; the vendor USD is Nucleus-only)",
+            "dof_order": [f"{leg}_{j}" for j in ("HAA", "HFE", "KFE") for leg in _LEGS],
+            "gears": [80.0 / 1.2] * 12, "torso": "base", "sensor_feet": ["RF_SHANK", "LF_SHANK"],
+            "contact_first": [f"{leg}_SHANK" for leg in _LEGS]}
 
 
 def _floats(s: str | None, n: int | None = None) -> list[float]:
@@ -127,7 +142,8 @@ class _Defaults:
         return self.joint.get(key, fallback)
 
 
-def compile_mjcf(path: str) -> dict:
+def compile_mjcf(path: str, opts: dict | None = None) -> dict:
+    opts = opts or WALKER
     root = ET.parse(path).getroot()
     comp = root.find("compiler")
     deg = comp is None or comp.get("angle", "degree") == "degree"
@@ -241,24 +257,27 @@ def compile_mjcf(path: str) -> dict:
 
     # DOF permutation: link i (i>=1) carries internal hinge dof i-1
     jname_to_link = {L["joint"]["name"]: i for i, L in enumerate(links) if L["joint"] is not None}
-    cfg_to_link = [jname_to_link[n] for n in CFG_DOF_ORDER]
+    cfg_to_link = [jname_to_link[n] for n in opts["dof_order"]]
 
-    return {
-        "source": "isaaclab_assets/data/mjcf/walker3d.xml",
+    out = {
+        "source": opts["source"],
         "density": DENSITY,
         "links": links,
         "body_link": body_link,
-        "cfg_dof_order": CFG_DOF_ORDER,
+        "cfg_dof_order": list(opts["dof_order"]),
         "cfg_dof_link": cfg_to_link,
-        "gears": CFG_GEARS,
+        "gears": list(opts["gears"]),
         "mjcf_base_pos": pos.tolist(),
         "total_mass": float(sum(L["mass"] for L in links)),
     }
+    if opts is not WALKER:  # the walker's json predates these keys; load_model defaults to them
+        out.update(torso=opts["torso"], sensor_feet=opts["sensor_feet"], contact_first=opts["contact_first"])
+    return out
 
 
 def main(argv: list[str]) -> None:
     src, dst = argv[1], argv[2]
-    model = compile_mjcf(src)
+    model = compile_mjcf(src, ANYMAL_C if len(argv) > 3 and argv[3] == "anymal_c" else WALKER)
     with open(dst, "w") as f:
         json.dump(model, f, indent=1)
     print(f"wrote {dst}: {len(model['links'])} links, total mass {model['total_mass']:.3f} kg")

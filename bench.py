@@ -18,6 +18,8 @@ Extra objects on the JSON line:
   train        -- rank 0, N = 1 (BASELINE C4 per GPU, SURVEY §8d "env+PPO separately"): env-steps/s
                   of the PPO trainer (scripts/bench_train.py: reference agent config, 32768 envs,
                   horizon 32, 10 mini-epochs) -- reported beside `value`, never as `value`.
+  c5           -- rank 0, N = 1 (BASELINE C5): the quadruped (model/anymal_c.xml) on the stones,
+                  physics only, 16384 envs (scripts/bench_quadruped.py) -- beside `value`.
 """
 
 from __future__ import annotations
@@ -56,6 +58,7 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-train", action="store_true", help="skip the env+PPO trainer measurement")
     p.add_argument("--train-envs", type=int, default=32768)
+    p.add_argument("--no-c5", action="store_true", help="skip the quadruped (BASELINE C5) physics measurement")
     return p.parse_args()
 
 
@@ -221,6 +224,14 @@ def main():
                 line["train"] = bench_train.measure(args.train_envs, epochs=2, warmup=2, verbose=False)
             except Exception as e:  # reported, never fatal for the env metric
                 line["train"] = {"error": f"{type(e).__name__}: {e}"}
+        if world == 1 and not args.no_c5:
+            sys.path.insert(0, os.path.join(ROOT, "scripts"))
+            import bench_quadruped
+
+            try:
+                line["c5"] = bench_quadruped.measure(16384, steps=300, warmup=20, device=str(device))
+            except Exception as e:  # reported, never fatal for the env metric
+                line["c5"] = {"error": f"{type(e).__name__}: {e}"}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

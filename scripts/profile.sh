@@ -5,7 +5,7 @@ TAG=${TAG:-r01}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu-baseline --no-train ${BENCH_ARGS}"
+B="python3 $R/bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu-baseline --no-train --no-c5 ${BENCH_ARGS}"
 set -o pipefail
 echo "== kernel trace"; date
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 || exit $?

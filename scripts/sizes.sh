@@ -8,7 +8,7 @@ OUT=gpurun_out/sizes_${TAG:-r01}.jsonl
 for cfg in "2 0" "4096 0" "32768 9"; do
   set -- $cfg
   echo "== N=$1 level=$2"; date
-  timeout -k 10 300 python bench.py --num-envs $1 --level $2 --no-train --steps ${STEPS:-1000} \
+  timeout -k 10 300 python bench.py --num-envs $1 --level $2 --no-train --no-c5 --steps ${STEPS:-1000} \
     > gpurun_out/sizes_$1.log 2>&1 || { rc=$?; tail -5 gpurun_out/sizes_$1.log; exit $rc; }
   grep '^{' gpurun_out/sizes_$1.log >> $OUT
 done
