@@ -74,7 +74,7 @@ int as_hbm_copy(void* dst, const void* src, int64_t n16, void* stream) {
   if (((uintptr_t)dst | (uintptr_t)src) & 15) return fail(AS_ERR_INVALID, "as_hbm_copy: pointers must be 16-B aligned");
   if (n16 == 0) return AS_OK;
   const int64_t per_block = 256 * 4;
-  const int64_t blocks = std::min<int64_t>((n16 + per_block - 1) / per_block, 256 * 32);
+  const int64_t blocks = std::min<int64_t>((n16 + per_block - 1) / per_block, 1 << 20);
   hipLaunchKernelGGL(k_hbm_copy, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (u32x4*)dst,
                      (const u32x4*)src, n16);
   HIP_TRY(hipGetLastError());
