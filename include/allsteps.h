@@ -145,7 +145,9 @@ typedef struct as_env as_env_t;
 
 /* Create a handle for `num_envs` envs on HIP device `device`.  `env_id_offset` is this shard's
  * first global env id (Philox stream = (seed, env_id_offset + e, episode)), so a sharded run is
- * bit-identical to an unsharded one.  The state pointers are stored, not copied. */
+ * bit-identical to an unsharded one.  The state pointers are stored, not copied.  The model's
+ * 6 + num_hinges must have a compiled step kernel: 27 (the Allsteps walker, as_step / as_task_step /
+ * as_physics_step) or 18 (the BASELINE C5 quadruped, as_physics_step); otherwise AS_ERR_INVALID. */
 int as_create(int32_t num_envs, const as_model_t* model_host, const as_sim_t* sim_host,
               const as_task_t* task_host, const as_state_t* state, uint64_t seed, int32_t device,
               int64_t env_id_offset, as_env_t** out);
