@@ -66,6 +66,37 @@ def test_quadruped_free_fall(qorc, qmodel):
     assert st["contact_mask"].max() == 0
 
 
+def test_quadruped_zero_gravity_conservation(oracle_mod, qmodel):
+    """No gravity, no contacts, no torque: linear momentum H[:3] u and kinetic energy u^T H u / 2 are
+    conserved (ties the CRBA H to the RNEA bias C on this model, as for the walker)."""
+    orc = oracle_mod.Oracle(model=qmodel)
+    orc.sim.gravity = 0.0
+    st = _stand_state(orc, qmodel, 1)
+    st["root_pos"][2] = 50.0
+    rng = np.random.default_rng(3)
+    st["qd"][:12, 0] = rng.uniform(-1.0, 1.0, 12)
+    st["root_lin"][:, 0] = rng.uniform(-0.3, 0.3, 3)
+    st["root_ang"][:, 0] = rng.uniform(-0.5, 0.5, 3)
+
+    def momentum_energy():
+        q = np.zeros(12, np.float32)
+        u = np.zeros(18, np.float32)
+        u[:3], u[3:6] = st["root_lin"][:, 0], st["root_ang"][:, 0]
+        for k in range(12):
+            li = qmodel["cfg_dof_link"][k]
+            q[li - 1] = st["q"][k, 0]
+            u[6 + li - 1] = st["qd"][k, 0]
+        H, _ = orc.mass_matrix(st["root_quat"][:, 0], q)
+        return H[:3] @ u, 0.5 * u @ H @ u
+
+    p0, e0 = momentum_energy()
+    for _ in range(10):  # 40 substeps, inside the joint limits
+        orc.physics_step(st, np.zeros((1, 12), np.float32))
+    p1, e1 = momentum_energy()
+    assert np.abs(p1 - p0).max() < 2e-2 * (np.abs(p0).max() + 1.0)
+    assert abs(e1 - e0) < 3e-2 * e0
+
+
 def test_quadruped_stance_rests_on_two_stones(qorc, qmodel):
     st = _stand_state(qorc, qmodel, 2)
     q0 = stand_pose(qmodel["dof_names"])
