@@ -43,7 +43,7 @@ BASELINE_METRIC = "env-steps/sec (whole node), Allsteps-v0 at 4096 envs, 1/2/4/8
 # Algorithmic bytes per env per launch: every state byte the kernel must read
 # or write once, from the SoA layout of include/allsteps.h.
 K_STEP_READ = 84 + 52 + 168 + 240 + 8 + 24 + 8 + 8 + 4    # actions, root, q/qd, stones, masks, ints, pots, contact, episode
-K_STEP_WRITE = 52 + 168 + 36 + 8 + 24 + 8 + 8 + 4 + 6     # root, q/qd, body_pos, masks, ints, pots, contact, episode, rew/term/trunc
+K_STEP_WRITE = 52 + 168 + 36 + 8 + 24 + 8 + 8 + 4 + 6 + 236  # root, q/qd, body_pos, masks, ints, pots, contact, episode, rew/term/trunc, obs row
 K_STEP_BYTES = K_STEP_READ + K_STEP_WRITE
 
 
