@@ -84,14 +84,30 @@ __global__ void __launch_bounds__(64 * kStatPhases) k_obs_stats(const float* __r
     const int64_t base = int64_t(*mb_idx) * mb_rows;
     const int r0 = blockIdx.x * kStatRows;
     const int r1 = min(r0 + kStatRows, mb_rows);
-    double s = 0.0, ss = 0.0;
+    // four independent chains per thread (rows r, r + 4, r + 8, r + 12 of a 16-row step), so four
+    // loads are in flight and the fp64 adds do not serialise on one accumulator; combined in a fixed
+    // order (deterministic)
+    double sa[4] = {0.0, 0.0, 0.0, 0.0}, qa[4] = {0.0, 0.0, 0.0, 0.0};
     if (c < cols) {
-        for (int r = r0 + ph; r < r1; r += kStatPhases) {
+        int r = r0 + ph;
+        for (; r + 3 * kStatPhases < r1; r += 4 * kStatPhases) {
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = x[(base + r + u * kStatPhases) * cols + c];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                sa[u] += v[u];
+                qa[u] += v[u] * v[u];
+            }
+        }
+        for (; r < r1; r += kStatPhases) {
             const double v = x[(base + r) * cols + c];
-            s += v;
-            ss += v * v;
+            sa[0] += v;
+            qa[0] += v * v;
         }
     }
+    const double s = (sa[0] + sa[1]) + (sa[2] + sa[3]);
+    const double ss = (qa[0] + qa[1]) + (qa[2] + qa[3]);
     red[0][ph][c] = s;
     red[1][ph][c] = ss;
     __syncthreads();
@@ -102,17 +118,44 @@ __global__ void __launch_bounds__(64 * kStatPhases) k_obs_stats(const float* __r
     }
 }
 
-__global__ void __launch_bounds__(64) k_obs_stats_update(const double* __restrict__ partials, int nblk, int cols,
-                                                         int mb_rows, double* __restrict__ mean,
-                                                         double* __restrict__ var, double* __restrict__ count) {
-    const int c = threadIdx.x;
+// 4 waves: wave w sums the partial blocks b = w, w + 4, ... (eight loads in flight per lane), the four
+// sums are combined in a fixed order, then wave 0 applies the running-moment update
+__global__ void __launch_bounds__(256) k_obs_stats_update(const double* __restrict__ partials, int nblk, int cols,
+                                                          int mb_rows, double* __restrict__ mean,
+                                                          double* __restrict__ var, double* __restrict__ count) {
+    __shared__ double red[2][4][64];
+    const int c = threadIdx.x % 64, w = threadIdx.x / 64;
+    {
+        double s = 0.0, ss = 0.0;
+        if (c < cols) {
+            int b = w;
+            for (; b + 12 < nblk; b += 16) {
+                double v[4], q[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    v[u] = partials[((b + 4 * u) * 2 + 0) * 64 + c];
+                    q[u] = partials[((b + 4 * u) * 2 + 1) * 64 + c];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    s += v[u];
+                    ss += q[u];
+                }
+            }
+            for (; b < nblk; b += 4) {
+                s += partials[(b * 2 + 0) * 64 + c];
+                ss += partials[(b * 2 + 1) * 64 + c];
+            }
+        }
+        red[0][w][c] = s;
+        red[1][w][c] = ss;
+    }
+    __syncthreads();
+    if (w != 0) return;
     const double cnt = *count;  // every lane reads before lane 0 writes (single wave, in-order)
     if (c < cols) {
-        double s = 0.0, ss = 0.0;
-        for (int b = 0; b < nblk; ++b) {
-            s += partials[(b * 2 + 0) * 64 + c];
-            ss += partials[(b * 2 + 1) * 64 + c];
-        }
+        const double s = (red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c]);
+        const double ss = (red[1][0][c] + red[1][1][c]) + (red[1][2][c] + red[1][3][c]);
         const double n = double(mb_rows);
         const double bm = s / n;
         const double bv = fmax(ss - n * bm * bm, 0.0) / (n - 1.0);  // torch.var: unbiased
@@ -122,7 +165,7 @@ __global__ void __launch_bounds__(64) k_obs_stats_update(const double* __restric
         mean[c] = mean[c] + d * n / tot;
         var[c] = m2 / tot;
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
     if (c == 0) *count = cnt + double(mb_rows);
 }
 
@@ -662,7 +705,7 @@ int ppo_obs_stats(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_
 int ppo_obs_stats_update(const double* partials, int32_t nblk, int32_t cols, int32_t mb_rows, double* running_mean,
                          double* running_var, double* count, void* stream) {
     if (cols <= 0 || cols > 64) return fail(-1, "ppo_obs_stats_update: cols must be in [1, 64]");
-    hipLaunchKernelGGL(k_obs_stats_update, dim3(1), dim3(64), 0, S(stream), partials, nblk, cols, mb_rows, running_mean,
+    hipLaunchKernelGGL(k_obs_stats_update, dim3(1), dim3(256), 0, S(stream), partials, nblk, cols, mb_rows, running_mean,
                        running_var, count);
     return launched("k_obs_stats_update");
 }
