@@ -334,8 +334,18 @@ __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ 
                                                       const int32_t* __restrict__ stat_idx, float* __restrict__ kl_out) {
     const int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
     const int k = blockIdx.x;  // one wave per value, lanes stride over the block partials (fixed order)
-    float s = 0.f;
-    for (int b = threadIdx.x; b < nblk; b += kWave) s += partials[int64_t(b) * NV + k];
+    // four independent chains per lane (four loads in flight), combined in a fixed order
+    float sa[4] = {0.f, 0.f, 0.f, 0.f};
+    int b = threadIdx.x;
+    for (; b + 3 * kWave < nblk; b += 4 * kWave) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = partials[int64_t(b + u * kWave) * NV + k];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sa[u] += v[u];
+    }
+    for (; b < nblk; b += kWave) sa[0] += partials[int64_t(b) * NV + k];
+    float s = (sa[0] + sa[1]) + (sa[2] + sa[3]);
     s = wave_sum(s);
     if (threadIdx.x != 0) return;
     if (k <= A) {
