@@ -168,8 +168,11 @@ def build_native(verbose: bool = False) -> str:
 
     srcs = [os.path.join(CSRC, f) for f in ("allsteps_kernels.hip", "allsteps_abi.hip")]
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    # -ffp-contract=off: no implicit FMA contraction -- every FMA of the physics path is an explicit
+    # fmaf() in the order include/as_detmath.h fixes, so the oracle (built the same way) rounds
+    # identically and HIP <-> oracle parity is bit-exact
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-I", INCLUDE, "-o", LIB_PATH] + srcs
+           "-ffp-contract=off", "-I", INCLUDE, "-o", LIB_PATH] + srcs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -8,87 +8,31 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/as_detmath.h"
+
 namespace as {
 
 #define AS_DEV __device__ __forceinline__
 
-AS_DEV void cross3(const float* a, const float* b, float* o) {
+// Physics-path primitives: the fmaf-ordered arithmetic of include/as_detmath.h, shared with the
+// oracle (oracle/physics.c) so both sides round identically (the library is built with
+// -ffp-contract=off, so nothing else is contracted).
+AS_DEV void cross3(const float* a, const float* b, float* o) { as_cross3(a, b, o); }
+AS_DEV float dot3(const float* a, const float* b) { return as_dot3(a, b); }
+AS_DEV float dot6(const float* a, const float* b) { return as_dot6(a, b); }
+AS_DEV void quat_to_mat(const float* q, float* R) { as_quat_to_mat(q, R); }
+AS_DEV void axis_angle_mat(const float* a, float ang, float* R) { as_axis_angle_mat(a, ang, R); }
+AS_DEV void matmul3(const float* A, const float* B, float* C) { as_matmul3(A, B, C); }
+AS_DEV void matvec3(const float* A, const float* v, float* o) { as_matvec3(A, v, o); }
+AS_DEV void inertia_mul(const float* I, const float* V, float* out) { as_inertia_mul(I, V, out); }
+AS_DEV void crm(const float* V, const float* M, float* o) { as_crm(V, M, o); }
+AS_DEV void crf(const float* V, const float* Fv, float* o) { as_crf(V, Fv, o); }
+
+// Task-path cross product (isaaclab.utils.math uses torch.cross: plain products and a difference,
+// oracle/task.c cross3)
+AS_DEV void task_cross3(const float* a, const float* b, float* o) {
   float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
   o[0] = x; o[1] = y; o[2] = z;
-}
-AS_DEV float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-AS_DEV float dot6(const float* a, const float* b) {
-  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
-}
-
-AS_DEV void quat_to_mat(const float* q, float* R) {
-  float w = q[0], x = q[1], y = q[2], z = q[3];
-  R[0] = 1.f - 2.f * (y * y + z * z); R[1] = 2.f * (x * y - w * z);       R[2] = 2.f * (x * z + w * y);
-  R[3] = 2.f * (x * y + w * z);       R[4] = 1.f - 2.f * (x * x + z * z); R[5] = 2.f * (y * z - w * x);
-  R[6] = 2.f * (x * z - w * y);       R[7] = 2.f * (y * z + w * x);       R[8] = 1.f - 2.f * (x * x + y * y);
-}
-
-AS_DEV void axis_angle_mat(const float* a, float ang, float* R) {
-  float s, c;
-  sincosf(ang, &s, &c);
-  float t = 1.f - c;
-  R[0] = c + t * a[0] * a[0];        R[1] = t * a[0] * a[1] - s * a[2]; R[2] = t * a[0] * a[2] + s * a[1];
-  R[3] = t * a[0] * a[1] + s * a[2]; R[4] = c + t * a[1] * a[1];        R[5] = t * a[1] * a[2] - s * a[0];
-  R[6] = t * a[0] * a[2] - s * a[1]; R[7] = t * a[1] * a[2] + s * a[0]; R[8] = c + t * a[2] * a[2];
-}
-
-AS_DEV void matmul3(const float* A, const float* B, float* C) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
-}
-
-AS_DEV void matvec3(const float* A, const float* v, float* o) {
-  float x = A[0] * v[0] + A[1] * v[1] + A[2] * v[2];
-  float y = A[3] * v[0] + A[4] * v[1] + A[5] * v[2];
-  float z = A[6] * v[0] + A[7] * v[1] + A[8] * v[2];
-  o[0] = x; o[1] = y; o[2] = z;
-}
-
-// symmetric (xx yy zz xy xz yz) times vector
-AS_DEV void sym_mul(const float* I, const float* w, float* o) {
-  o[0] = I[0] * w[0] + I[3] * w[1] + I[4] * w[2];
-  o[1] = I[3] * w[0] + I[1] * w[1] + I[5] * w[2];
-  o[2] = I[4] * w[0] + I[5] * w[1] + I[2] * w[2];
-}
-
-// spatial inertia (m, h, Io) x motion [w; v] = [Io w + h x v; m v - h x w]
-AS_DEV void inertia_mul(const float* I, const float* V, float* out) {
-  float Iw[3], hv[3], hw[3];
-  sym_mul(I + 4, V, Iw);
-  cross3(I + 1, V + 3, hv);
-  cross3(I + 1, V, hw);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    out[k] = Iw[k] + hv[k];
-    out[3 + k] = I[0] * V[3 + k] - hw[k];
-  }
-}
-
-// [w;v] x_m [w2;v2] = [w x w2; w x v2 + v x w2]
-AS_DEV void crm(const float* V, const float* M, float* o) {
-  float a[3], b[3], c[3];
-  cross3(V, M, a);
-  cross3(V, M + 3, b);
-  cross3(V + 3, M, c);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) { o[k] = a[k]; o[3 + k] = b[k] + c[k]; }
-}
-
-// [w;v] x_f [n;f] = [w x n + v x f; w x f]
-AS_DEV void crf(const float* V, const float* Fv, float* o) {
-  float a[3], b[3], c[3];
-  cross3(V, Fv, a);
-  cross3(V + 3, Fv + 3, b);
-  cross3(V, Fv + 3, c);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) { o[k] = a[k] + b[k]; o[3 + k] = c[k]; }
 }
 
 // signed distance from p to an axis-aligned box (center c, half extents h); outward normal
@@ -166,7 +110,7 @@ AS_DEV void quat_rotate_inverse(const float* q, const float* v, float* out) {
   const float* qv = q + 1;
   float s = 2.0f * (w * w) - 1.0f;
   float cr[3];
-  cross3(qv, v, cr);
+  task_cross3(qv, v, cr);
   float d = qv[0] * v[0] + qv[1] * v[1] + qv[2] * v[2];
 #pragma unroll
   for (int i = 0; i < 3; ++i) out[i] = v[i] * s - cr[i] * w * 2.0f + qv[i] * d * 2.0f;
@@ -179,9 +123,9 @@ AS_DEV void subtract_frame_transforms(const float* t01, const float* q01, const 
   float q10[4] = {c0 / nrm, c1 / nrm, c2 / nrm, c3 / nrm};
   float v[3] = {t02[0] - t01[0], t02[1] - t01[1], t02[2] - t01[2]};
   float t[3], t2[3];
-  cross3(q10 + 1, v, t);
+  task_cross3(q10 + 1, v, t);
   t[0] *= 2.0f; t[1] *= 2.0f; t[2] *= 2.0f;
-  cross3(q10 + 1, t, t2);
+  task_cross3(q10 + 1, t, t2);
 #pragma unroll
   for (int i = 0; i < 3; ++i) out[i] = v[i] + q10[0] * t[i] + t2[i];
 }

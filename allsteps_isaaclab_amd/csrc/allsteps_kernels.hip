@@ -623,14 +623,14 @@ __device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, 
 //   M = [A B; C D]:  Ai = A^-1, X = Ai B, Y = C Ai, S = D - C X, Si = S^-1,
 //   M^-1 = [Ai + (X Si) Y, -(X Si); -(Si Y), Si]       (oracle/physics.c block_inverse: same order)
 __device__ __forceinline__ void inv2(float a, float b, float c, float d, float (&o)[2][2]) {
-  const float id = 1.0f / (a * d - b * c);
+  const float id = 1.0f / fmaf(a, d, -(b * c));
   o[0][0] = d * id; o[0][1] = -b * id; o[1][0] = -c * id; o[1][1] = a * id;
 }
 __device__ __forceinline__ void mul2(const float (&x)[2][2], const float (&y)[2][2], float (&o)[2][2]) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) o[i][j] = x[i][0] * y[0][j] + x[i][1] * y[1][j];
+    for (int j = 0; j < 2; ++j) o[i][j] = fmaf(x[i][1], y[1][j], x[i][0] * y[0][j]);
 }
 template <int B>
 __device__ __forceinline__ void block_inverse(float (&M)[B][B]) {  // M <- M^-1 (SPD)
@@ -692,7 +692,7 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
     for (int c = 0; c < B; ++c) {
       float v = 0.f;
 #pragma unroll
-      for (int e = 0; e < B; ++e) v += Hr[e] * D[e][c];
+      for (int e = 0; e < B; ++e) v = fmaf(Hr[e], D[e][c], v);
       float pv = -D[0][c];
 #pragma unroll
       for (int e = 1; e < B; ++e) pv = t == e ? -D[e][c] : pv;
@@ -703,7 +703,7 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
     for (int j = B; j < NP; ++j) {
       float v = alpha * Hr[j];
 #pragma unroll
-      for (int c = 0; c < B; ++c) v -= beta[c] * Q[c][j];
+      for (int c = 0; c < B; ++c) v = fmaf(-beta[c], Q[c][j], v);
       Hr[j - B] = v;
     }
 #pragma unroll
@@ -940,9 +940,9 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   {
     float acc = 0.f;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc += Hr[k] * s.b[k];
+    for (int k = 0; k < NV; ++k) acc = fmaf(Hr[k], s.b[k], acc);
     if (lane < NV) {
-      uj = s.u[lane] + dt * acc;
+      uj = fmaf(dt, acc, s.u[lane]);
       s.u[lane] = uj;
     }
   }
@@ -1082,7 +1082,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
         jrow[4 * q] = t.x; jrow[4 * q + 1] = t.y; jrow[4 * q + 2] = t.z; jrow[4 * q + 3] = t.w;
       }
 #pragma unroll
-      for (int k = 0; k < NV; ++k) w[u][k & 1] += Hr[k] * jrow[k];
+      for (int k = 0; k < NV; ++k) w[u][k & 1] = fmaf(Hr[k], jrow[k], w[u][k & 1]);
     }
     float wu[kRowGroup], a[2 * kRowGroup];
 #pragma unroll
@@ -1192,18 +1192,18 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   if (lane < nh) {
     float v = fminf(fmaxf(s.u[6 + lane], -K.sim.max_joint_vel), K.sim.max_joint_vel);
     s.u[6 + lane] = v;
-    s.qi[lane] += dt * v;
+    s.qi[lane] = fmaf(dt, v, s.qi[lane]);
   }
   if (lane == 0) {
     const float* u = s.u;
     float c0w[3];
-    for (int k = 0; k < 3; ++k) c0w[k] = s.root_pos[k] + s.c0[k] + dt * u[k];
+    for (int k = 0; k < 3; ++k) c0w[k] = fmaf(dt, u[k], s.root_pos[k] + s.c0[k]);
     const float* w = u + 3;
     float wn = sqrtf(dot3(w, w));
     float th = wn * dt, dq[4];
     if (th > 1e-12f) {
       float sn, cs;
-      sincosf(0.5f * th, &sn, &cs);
+      as_sincosf(0.5f * th, &sn, &cs);
       float sc = sn / wn;
       dq[0] = cs; dq[1] = w[0] * sc; dq[2] = w[1] * sc; dq[3] = w[2] * sc;
     } else {
@@ -1671,8 +1671,8 @@ __device__ void gen_stones(const as_task_t& T, int level, uint64_t seed, uint32_
     if (k == 1 || k == 2) { dr = 0.75f; dph = 0.f; dth = 1.57079632679489661923f; }
     phi += dph;
     float st_, ct_, sp, cp;
-    sincosf(dth, &st_, &ct_);
-    sincosf(phi, &sp, &cp);
+    as_sincosf(dth, &st_, &ct_);
+    as_sincosf(phi, &sp, &cp);
     x += dr * st_ * cp;
     y += dr * st_ * sp;
     z += dr * ct_;

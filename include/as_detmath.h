@@ -1,0 +1,142 @@
+/*
+ * as_detmath.h -- the float32 arithmetic specification shared by the HIP step kernels
+ * (allsteps_isaaclab_amd/csrc) and the CPU oracle (oracle/physics.c).
+ *
+ * Bit-exact HIP <-> oracle parity needs every float operation
+ * on the physics path to be the same correctly rounded IEEE-754 operation in the same order on both
+ * sides.  Both sides are compiled with -ffp-contract=off, so a * b + c is a multiply and an add
+ * everywhere; where an FMA is wanted it is written as fmaf() (v_fma_f32 on gfx950, the correctly
+ * rounded fmaf of C99 on the host), in the order fixed here.  Division and sqrtf are correctly
+ * rounded on both sides (HIP's default -fhip-fp32-correctly-rounded-divide-sqrt; IEEE on x86-64).
+ *
+ * Library transcendentals differ between the device math library and the host libm by an ulp, so
+ * the physics path uses as_sincosf below instead: Cody-Waite reduction by pi/2 and minimax
+ * polynomials on [-pi/4, pi/4], built only from rintf / multiply / fmaf (max error ~2 ulp for
+ * |x| < 1e4; the path's arguments are joint angles, half rotation angles and stone bearings).
+ *
+ * Plain C99 + HIP: every function is usable from gcc (oracle) and hipcc (device and host).
+ */
+#ifndef AS_DETMATH_H
+#define AS_DETMATH_H
+
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define AS_HD __host__ __device__ __forceinline__
+#else
+#define AS_HD static inline
+#endif
+
+/* dot products: fmaf chain from the first product, ascending index */
+AS_HD float as_dot3(const float* a, const float* b) { return fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0])); }
+
+AS_HD float as_dot6(const float* a, const float* b) {
+  float s = a[0] * b[0];
+  s = fmaf(a[1], b[1], s);
+  s = fmaf(a[2], b[2], s);
+  s = fmaf(a[3], b[3], s);
+  s = fmaf(a[4], b[4], s);
+  return fmaf(a[5], b[5], s);
+}
+
+/* a x b, each component as fmaf(p, q, -(r s)) */
+AS_HD void as_cross3(const float* a, const float* b, float* o) {
+  const float x = fmaf(a[1], b[2], -(a[2] * b[1]));
+  const float y = fmaf(a[2], b[0], -(a[0] * b[2]));
+  const float z = fmaf(a[0], b[1], -(a[1] * b[0]));
+  o[0] = x; o[1] = y; o[2] = z;
+}
+
+/* row-major 3x3 */
+AS_HD void as_matvec3(const float* A, const float* v, float* o) {
+  const float x = as_dot3(A, v), y = as_dot3(A + 3, v), z = as_dot3(A + 6, v);
+  o[0] = x; o[1] = y; o[2] = z;
+}
+
+AS_HD void as_matmul3(const float* A, const float* B, float* C) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      C[3 * i + j] = fmaf(A[3 * i + 2], B[6 + j], fmaf(A[3 * i + 1], B[3 + j], A[3 * i] * B[j]));
+}
+
+/* symmetric (xx yy zz xy xz yz) times vector */
+AS_HD void as_sym_mul(const float* I, const float* w, float* o) {
+  const float x = fmaf(I[4], w[2], fmaf(I[3], w[1], I[0] * w[0]));
+  const float y = fmaf(I[5], w[2], fmaf(I[1], w[1], I[3] * w[0]));
+  const float z = fmaf(I[2], w[2], fmaf(I[5], w[1], I[4] * w[0]));
+  o[0] = x; o[1] = y; o[2] = z;
+}
+
+/* spatial inertia (m, h, Io) x motion [w; v] = [Io w + h x v; m v - h x w] */
+AS_HD void as_inertia_mul(const float* I, const float* V, float* out) {
+  float Iw[3], hv[3], hw[3];
+  as_sym_mul(I + 4, V, Iw);
+  as_cross3(I + 1, V + 3, hv);
+  as_cross3(I + 1, V, hw);
+  for (int k = 0; k < 3; ++k) {
+    out[k] = Iw[k] + hv[k];
+    out[3 + k] = fmaf(I[0], V[3 + k], -hw[k]);
+  }
+}
+
+/* [w;v] x_m [w2;v2] = [w x w2; w x v2 + v x w2] */
+AS_HD void as_crm(const float* V, const float* M, float* o) {
+  float a[3], b[3], c[3];
+  as_cross3(V, M, a);
+  as_cross3(V, M + 3, b);
+  as_cross3(V + 3, M, c);
+  for (int k = 0; k < 3; ++k) { o[k] = a[k]; o[3 + k] = b[k] + c[k]; }
+}
+
+/* [w;v] x_f [n;f] = [w x n + v x f; w x f] */
+AS_HD void as_crf(const float* V, const float* Fv, float* o) {
+  float a[3], b[3], c[3];
+  as_cross3(V, Fv, a);
+  as_cross3(V + 3, Fv + 3, b);
+  as_cross3(V, Fv + 3, c);
+  for (int k = 0; k < 3; ++k) { o[k] = a[k] + b[k]; o[3 + k] = c[k]; }
+}
+
+/* unit quaternion (w, x, y, z) -> row-major rotation matrix */
+AS_HD void as_quat_to_mat(const float* q, float* R) {
+  const float w = q[0], x = q[1], y = q[2], z = q[3];
+  const float xx = x * x, yy = y * y, zz = z * z;
+  const float xy = x * y, xz = x * z, yz = y * z, wx = w * x, wy = w * y, wz = w * z;
+  R[0] = 1.f - 2.f * (yy + zz); R[1] = 2.f * (xy - wz);       R[2] = 2.f * (xz + wy);
+  R[3] = 2.f * (xy + wz);       R[4] = 1.f - 2.f * (xx + zz); R[5] = 2.f * (yz - wx);
+  R[6] = 2.f * (xz - wy);       R[7] = 2.f * (yz + wx);       R[8] = 1.f - 2.f * (xx + yy);
+}
+
+/* sin and cos of x: k = rint(x 2/pi), r = x - k pi/2 in three fmaf steps (Cody-Waite), minimax
+ * polynomials in r^2 on [-pi/4, pi/4], quadrant select by k mod 4. */
+AS_HD void as_sincosf(float x, float* sn, float* cs) {
+  const float k = rintf(x * 0.636619772f);
+  float r = fmaf(-k, 1.57079625e+00f, x);
+  r = fmaf(-k, 7.54978942e-08f, r);
+  r = fmaf(-k, 5.39030253e-15f, r);
+  const float z = r * r;
+  float ps = fmaf(-1.9515296e-04f, z, 8.3321608e-03f);
+  ps = fmaf(ps, z, -1.6666655e-01f);
+  const float s = fmaf(ps * z, r, r);
+  float pc = fmaf(2.4433157e-05f, z, -1.3887316e-03f);
+  pc = fmaf(pc, z, 4.1666646e-02f);
+  const float c = fmaf(pc * z, z, fmaf(-0.5f, z, 1.0f));
+  const int q = ((int)k) & 3;
+  const float s1 = (q & 1) ? c : s;
+  const float c1 = (q & 1) ? s : c;
+  *sn = (q & 2) ? -s1 : s1;
+  *cs = ((q + 1) & 2) ? -c1 : c1;
+}
+
+/* Rodrigues rotation about the unit axis a by ang (as_sincosf) */
+AS_HD void as_axis_angle_mat(const float* a, float ang, float* R) {
+  float s, c;
+  as_sincosf(ang, &s, &c);
+  const float t = 1.f - c;
+  const float tx = t * a[0], ty = t * a[1], tz = t * a[2];
+  R[0] = fmaf(tx, a[0], c);           R[1] = fmaf(tx, a[1], -(s * a[2])); R[2] = fmaf(tx, a[2], s * a[1]);
+  R[3] = fmaf(tx, a[1], s * a[2]);    R[4] = fmaf(ty, a[1], c);          R[5] = fmaf(ty, a[2], -(s * a[0]));
+  R[6] = fmaf(tx, a[2], -(s * a[1])); R[7] = fmaf(ty, a[2], s * a[0]);   R[8] = fmaf(tz, a[2], c);
+}
+
+#endif /* AS_DETMATH_H */

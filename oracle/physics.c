@@ -28,6 +28,7 @@
 #include <string.h>
 
 #include "oracle.h"
+#include "../include/as_detmath.h"
 
 #define NV_MAX (OR_NDOF_ROOT + OR_MAX_LINKS)
 #define F(arr, f, n, e) (arr)[(size_t)(f) * (n) + (e)]
@@ -42,76 +43,29 @@ typedef struct {
   float Ib[OR_MAX_LINKS][10];/* single-body spatial inertia at O */
 } kin_t;
 
-static void quat_to_mat(const float q[4], float R[9]) {
-  float w = q[0], x = q[1], y = q[2], z = q[3];
-  R[0] = 1.f - 2.f * (y * y + z * z); R[1] = 2.f * (x * y - w * z);       R[2] = 2.f * (x * z + w * y);
-  R[3] = 2.f * (x * y + w * z);       R[4] = 1.f - 2.f * (x * x + z * z); R[5] = 2.f * (y * z - w * x);
-  R[6] = 2.f * (x * z - w * y);       R[7] = 2.f * (y * z + w * x);       R[8] = 1.f - 2.f * (x * x + y * y);
-}
+/* The primitives of the shared float32 arithmetic specification (include/as_detmath.h): explicit
+ * fmaf in a fixed order, everything else uncontracted (-ffp-contract=off), identical to the HIP
+ * kernel's rounding. */
+#define quat_to_mat as_quat_to_mat
+#define axis_angle_mat as_axis_angle_mat
+#define matmul3 as_matmul3
+#define matvec3 as_matvec3
+#define cross as_cross3
+#define dot3 as_dot3
+#define dot6 as_dot6
+#define inertia_mul as_inertia_mul
+#define crm as_crm
+#define crf as_crf
 
-static void axis_angle_mat(const float a[3], float ang, float R[9]) {
-  float c = cosf(ang), s = sinf(ang), t = 1.f - c;
-  R[0] = c + t * a[0] * a[0];        R[1] = t * a[0] * a[1] - s * a[2]; R[2] = t * a[0] * a[2] + s * a[1];
-  R[3] = t * a[0] * a[1] + s * a[2]; R[4] = c + t * a[1] * a[1];        R[5] = t * a[1] * a[2] - s * a[0];
-  R[6] = t * a[0] * a[2] - s * a[1]; R[7] = t * a[1] * a[2] + s * a[0]; R[8] = c + t * a[2] * a[2];
-}
-
-static void matmul3(const float A[9], const float B[9], float C[9]) {
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
-}
-
-static void matvec3(const float A[9], const float v[3], float o[3]) {
-  o[0] = A[0] * v[0] + A[1] * v[1] + A[2] * v[2];
-  o[1] = A[3] * v[0] + A[4] * v[1] + A[5] * v[2];
-  o[2] = A[6] * v[0] + A[7] * v[1] + A[8] * v[2];
-}
-
-static void cross(const float a[3], const float b[3], float o[3]) {
-  float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
-  o[0] = x; o[1] = y; o[2] = z;
-}
-
-static float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-static float dot6(const float a[6], const float b[6]) {
-  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
-}
-
-/* Io w for symmetric (xx yy zz xy xz yz) */
-static void sym_mul(const float I[6], const float w[3], float o[3]) {
-  o[0] = I[0] * w[0] + I[3] * w[1] + I[4] * w[2];
-  o[1] = I[3] * w[0] + I[1] * w[1] + I[5] * w[2];
-  o[2] = I[4] * w[0] + I[5] * w[1] + I[2] * w[2];
-}
-
-/* spatial inertia (m, h, Io) times motion [w; v] -> force [Io w + h x v; m v - h x w] */
-static void inertia_mul(const float I[10], const float V[6], float out[6]) {
-  float Iw[3], hv[3], hw[3];
-  sym_mul(I + 4, V, Iw);
-  cross(I + 1, V + 3, hv);
-  cross(I + 1, V, hw);
-  for (int k = 0; k < 3; ++k) {
-    out[k] = Iw[k] + hv[k];
-    out[3 + k] = I[0] * V[3 + k] - hw[k];
-  }
-}
-
-/* [w;v] x_m [w2;v2] = [w x w2; w x v2 + v x w2] */
-static void crm(const float V[6], const float M[6], float o[6]) {
-  float a[3], b[3], c[3];
-  cross(V, M, a);
-  cross(V, M + 3, b);
-  cross(V + 3, M, c);
-  for (int k = 0; k < 3; ++k) { o[k] = a[k]; o[3 + k] = b[k] + c[k]; }
-}
-
-/* [w;v] x_f [n;f] = [w x n + v x f; w x f] */
-static void crf(const float V[6], const float Fv[6], float o[6]) {
-  float a[3], b[3], c[3];
-  cross(V, Fv, a);
-  cross(V + 3, Fv + 3, b);
-  cross(V, Fv + 3, c);
-  for (int k = 0; k < 3; ++k) { o[k] = a[k] + b[k]; o[3 + k] = c[k]; }
+/* Sum of 32 lane values as the kernel's half-wave reduction forms it (half_sum: DPP butterflies
+ * over lane pairs, quads, 8-lane halves, 16-lane rows, then the two rows): a balanced binary tree
+ * over lanes 0..31 in index order.  Lanes past the row's width carry 0. */
+static float tree32(const float* v) {
+  float a[32];
+  for (int i = 0; i < 32; ++i) a[i] = v[i];
+  for (int w = 1; w < 32; w *= 2)
+    for (int i = 0; i < 32; i += 2 * w) a[i] = a[i] + a[i + w];
+  return a[0];
 }
 
 static int is_ancestor(const or_model_t* m, int a, int l) {
@@ -233,6 +187,13 @@ static void crba(const or_model_t* m, const kin_t* K, float* H) {
       H[k * nv + j] = h;
     }
   }
+  /* root block: the kernel's row j (lane j) forms every root column k from its own column force,
+   * H_jk = S_k . (Ic_0 S_j), so its upper triangle is not the mirror of the lower one */
+  for (int j = 0; j < OR_NDOF_ROOT; ++j) {
+    float Fj[6];
+    inertia_mul(K->Ic[0], K->S[j], Fj);
+    for (int k = j + 1; k < OR_NDOF_ROOT; ++k) H[j * nv + k] = dot6(K->S[k], Fj);
+  }
   for (int i = 1; i < m->num_links; ++i) {
     int j = OR_NDOF_ROOT + i - 1;
     H[j * nv + j] += m->armature[i];
@@ -298,12 +259,12 @@ static void rnea_bias(const or_model_t* m, const kin_t* K, const float* u, float
  *   M = [A B; C D]: Ai = A^-1, X = Ai B, Y = C Ai, S = D - C X, Si = S^-1,
  *   M^-1 = [Ai + (X Si) Y, -(X Si); -(Si Y), Si]. */
 static void inv2(float a, float b, float c, float d, float o[2][2]) {
-  const float id = 1.0f / (a * d - b * c);
+  const float id = 1.0f / fmaf(a, d, -(b * c));
   o[0][0] = d * id; o[0][1] = -b * id; o[1][0] = -c * id; o[1][1] = a * id;
 }
 static void mul2(const float x[2][2], const float y[2][2], float o[2][2]) {
   for (int i = 0; i < 2; ++i)
-    for (int j = 0; j < 2; ++j) o[i][j] = x[i][0] * y[0][j] + x[i][1] * y[1][j];
+    for (int j = 0; j < 2; ++j) o[i][j] = fmaf(x[i][1], y[1][j], x[i][0] * y[0][j]);
 }
 static void block_inverse(float M[SWEEP_B][SWEEP_B]) {
   float A[2][2] = {{M[0][0], M[0][1]}, {M[1][0], M[1][1]}};
@@ -349,7 +310,7 @@ static void sweep_inverse(float* h, int n) {
       float alpha = piv ? 0.f : 1.f, beta[SWEEP_B];
       for (int c = 0; c < SWEEP_B; ++c) {
         float v = 0.f;
-        for (int e = 0; e < SWEEP_B; ++e) v += a[i][p + e] * D[e][c];
+        for (int e = 0; e < SWEEP_B; ++e) v = fmaf(a[i][p + e], D[e][c], v);
         beta[c] = piv ? -D[t][c] : v;
       }
       for (int j = 0; j < np; ++j) {
@@ -357,7 +318,7 @@ static void sweep_inverse(float* h, int n) {
           out[j] = beta[j - p];
         } else {
           float v = alpha * a[i][j];
-          for (int c = 0; c < SWEEP_B; ++c) v -= beta[c] * Q[c][j];
+          for (int c = 0; c < SWEEP_B; ++c) v = fmaf(-beta[c], Q[c][j], v);
           out[j] = v;
         }
       }
@@ -368,11 +329,11 @@ static void sweep_inverse(float* h, int n) {
     for (int j = 0; j < n; ++j) h[i * n + j] = -a[i][j];
 }
 
-/* x = A b (row-major, sequential in k) */
+/* x = A b (row-major, fmaf chain ascending in k) */
 static void matvec_n(const float* A, int n, const float* b, float* x) {
   for (int i = 0; i < n; ++i) {
     float s = 0.f;
-    for (int k = 0; k < n; ++k) s += A[i * n + k] * b[k];
+    for (int k = 0; k < n; ++k) s = fmaf(A[i * n + k], b[k], s);
     x[i] = s;
   }
 }
@@ -550,7 +511,7 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
   for (int j = 0; j < nv; ++j) b[j] = (j < OR_NDOF_ROOT ? 0.f : tau_int[j - OR_NDOF_ROOT]) - C[j];
   sweep_inverse(H, nv); /* H <- H^-1 */
   matvec_n(H, nv, b, acc);
-  for (int j = 0; j < nv; ++j) u[j] += dt * acc[j];
+  for (int j = 0; j < nv; ++j) u[j] = fmaf(dt, acc[j], u[j]);
 
   /* constraints */
   float stones_rel[OR_MAX_STONES * 3];
@@ -593,31 +554,74 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
       R->target[r] = err > 0.f ? fminf(sim->baumgarte * err / dt, sim->max_depen_vel) : err / dt;
     }
   }
-  for (int r = 0; r < R->nrow; ++r) {
-    matvec_n(H, nv, R->J[r], R->W[r]); /* W_r = H^-1 J_r^T */
-    float a = 0.f;
-    for (int k = 0; k < nv; ++k) a += R->J[r][k] * R->W[r][k];
-    R->Ad[r] = 1.0f / (a + 1e-9f);
+  /* W_r = H^-1 J_r^T: per entry two interleaved partial sums (even / odd k, fmaf chains), added at
+   * the end; the projections A_rr = J_r . W_r and the in-triplet couplings A_sr = J_s . W_r
+   * (s > r in the same row triplet) as 32-lane trees (the kernel's W loop, substep()). */
+  const int ngrp = (R->nrow + 2) / 3, nr3 = 3 * ngrp;
+  for (int r = R->nrow; r < nr3; ++r) {
+    for (int k = 0; k < NV_MAX; ++k) R->J[r][k] = 0.f;
+    R->type[r] = 0;
+    R->target[r] = 0.f;
+  }
+  float cpl[OR_MAX_ROWS + 3];
+  for (int r = 0; r < nr3; ++r) {
+    for (int i = 0; i < nv; ++i) {
+      float w0 = 0.f, w1 = 0.f;
+      for (int k = 0; k < nv; ++k) {
+        if (k & 1) w1 = fmaf(H[i * nv + k], R->J[r][k], w1);
+        else w0 = fmaf(H[i * nv + k], R->J[r][k], w0);
+      }
+      R->W[r][i] = w0 + w1;
+    }
+    float pr[32] = {0.f};
+    for (int k = 0; k < nv; ++k) pr[k] = R->J[r][k] * R->W[r][k];
+    R->Ad[r] = r < R->nrow ? 1.0f / (tree32(pr) + 1e-9f) : 0.f;
     R->lam[r] = 0.f;
   }
+  for (int g = 0; g < ngrp; ++g) {
+    const int r0 = 3 * g;
+    const int ps[3][2] = {{1, 0}, {2, 0}, {2, 1}}; /* (s, r): A_10, A_20, A_21 */
+    for (int c = 0; c < 3; ++c) {
+      float pr[32] = {0.f};
+      for (int k = 0; k < nv; ++k) pr[k] = R->J[r0 + ps[c][0]][k] * R->W[r0 + ps[c][1]][k];
+      cpl[r0 + c] = tree32(pr);
+    }
+  }
+  /* projected Gauss-Seidel, row triplets (the kernel's PGS loop): the three velocities J_r . u of a
+   * triplet come from the u at its start, rows 2 and 3 add the in-triplet couplings of this sweep's
+   * impulse changes; t = lambda + (target - v) / A_rr as fmaf chains; normal and limit rows clamp to
+   * [0, inf), tangent rows to +-mu * (the latest normal impulse). */
   for (int it = 0; it < sim->pgs_iters; ++it) {
-    for (int r = 0; r < R->nrow; ++r) {
-      float v = 0.f;
-      for (int k = 0; k < nv; ++k) v += R->J[r][k] * u[k];
-      float l0 = R->lam[r];
-      float l1;
-      if (R->type[r] == 1) {
-        int rn = r - (r % 3 == 1 ? 1 : 2); /* normal row of this contact */
-        float lim = sim->friction * R->lam[rn];
-        l1 = l0 - v * R->Ad[r];
-        l1 = l1 < -lim ? -lim : (l1 > lim ? lim : l1);
-      } else {
-        l1 = l0 + (R->target[r] - v) * R->Ad[r];
-        l1 = l1 > 0.f ? l1 : 0.f;
+    float ln = 0.f;
+    for (int g = 0; g < ngrp; ++g) {
+      const int r0 = 3 * g;
+      float vg[3];
+      for (int c = 0; c < 3; ++c) {
+        float pr[32] = {0.f};
+        for (int k = 0; k < nv; ++k) pr[k] = R->J[r0 + c][k] * u[k];
+        vg[c] = tree32(pr);
       }
-      float dl = l1 - l0;
-      R->lam[r] = l1;
-      for (int k = 0; k < nv; ++k) u[k] += R->W[r][k] * dl;
+      const float* x = R->Ad + r0;
+      const float* y = R->target + r0;
+      const float k10 = x[1] * cpl[r0], k20 = x[2] * cpl[r0 + 1], k21 = x[2] * cpl[r0 + 2];
+      float t[3];
+      for (int c = 0; c < 3; ++c) t[c] = fmaf(-vg[c], x[c], fmaf(y[c], x[c], R->lam[r0 + c]));
+      for (int c = 0; c < 3; ++c) {
+        const int r = r0 + c;
+        float l1;
+        if (R->type[r] == 1) {
+          const float lo = fmaf(-sim->friction, ln, 0.f), hi = fmaf(sim->friction, ln, 0.f);
+          l1 = t[c] < lo ? lo : (t[c] > hi ? hi : t[c]);
+        } else {
+          l1 = t[c] > 0.f ? t[c] : 0.f;
+        }
+        if (R->type[r] == 0) ln = l1;
+        const float dl = l1 - R->lam[r];
+        R->lam[r] = l1;
+        if (c == 0) { t[1] = fmaf(-k10, dl, t[1]); t[2] = fmaf(-k20, dl, t[2]); }
+        if (c == 1) t[2] = fmaf(-k21, dl, t[2]);
+        for (int k = 0; k < nv; ++k) u[k] = fmaf(R->W[r][k], dl, u[k]);
+      }
     }
   }
   /* contact sensor flags of this substep: |sum_n lambda_n n| / dt > eps per (foot, stone) */
@@ -639,16 +643,18 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
     float* v = &u[OR_NDOF_ROOT + i];
     if (*v > sim->max_joint_vel) *v = sim->max_joint_vel;
     if (*v < -sim->max_joint_vel) *v = -sim->max_joint_vel;
-    q_int[i] += dt * *v;
+    q_int[i] = fmaf(dt, *v, q_int[i]);
   }
   float c0w[3];
-  for (int k = 0; k < 3; ++k) c0w[k] = root_pos[k] + K.c[0][k] + dt * u[k];
+  for (int k = 0; k < 3; ++k) c0w[k] = fmaf(dt, u[k], root_pos[k] + K.c[0][k]);
   const float* w = u + 3;
   float wn = sqrtf(dot3(w, w));
   float th = wn * dt, dq[4];
   if (th > 1e-12f) {
-    float s = sinf(0.5f * th) / wn;
-    dq[0] = cosf(0.5f * th); dq[1] = w[0] * s; dq[2] = w[1] * s; dq[3] = w[2] * s;
+    float sn, cs;
+    as_sincosf(0.5f * th, &sn, &cs);
+    float s = sn / wn;
+    dq[0] = cs; dq[1] = w[0] * s; dq[2] = w[1] * s; dq[3] = w[2] * s;
   } else {
     dq[0] = 1.f; dq[1] = 0.5f * dt * w[0]; dq[2] = 0.5f * dt * w[1]; dq[3] = 0.5f * dt * w[2];
   }

@@ -142,13 +142,12 @@ def test_quadruped_gpu_matches_oracle(qorc, qmodel, warm):
     torch.cuda.synchronize()
     qorc.physics_step(st, act.cpu().numpy())
     g = {k: v.cpu().numpy() for k, v in env.state.items()}
-    mask_eq = (g["contact_mask"] == st["contact_mask"]).all(axis=0)
-    assert mask_eq.mean() >= 0.99, f"contact bits differ on {np.count_nonzero(~mask_eq)} envs"
-    ok = mask_eq
-    for k, tol in (("root_pos", 2e-3), ("root_quat", 2e-3), ("q", 2e-3)):
-        np.testing.assert_allclose(g[k][..., ok], st[k][..., ok], atol=tol, rtol=tol, err_msg=k)
-    for k in ("root_lin", "root_ang", "qd"):
-        np.testing.assert_allclose(g[k][..., ok], st[k][..., ok], atol=1e-2, rtol=1e-2, err_msg=k)
+    mask_eq = (g["contact_mask"].view(np.uint32) == st["contact_mask"]).all(axis=0)
+    print(f"quadruped parity warm={warm}: contact bits differ on {np.count_nonzero(~mask_eq)} of {n} envs")
+    assert mask_eq.all(), f"contact bits differ on {np.count_nonzero(~mask_eq)} envs"
+    # the same float32 operations in the same order on both sides (include/as_detmath.h): bit-exact
+    for k in ("root_pos", "root_quat", "q", "root_lin", "root_ang", "qd", "body_pos"):
+        assert np.array_equal(g[k], st[k]), (k, np.abs(g[k] - st[k]).max())
     env.close()
 
 
