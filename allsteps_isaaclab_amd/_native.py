@@ -17,8 +17,8 @@ PPO_LIB_PATH = os.path.join(PKG, "libppo_hip.so")
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 
-MAXL, MAXG = 32, 32
-ABI_VERSION = 1
+MAXL, MAXG, MAXSP = 32, 32, 256
+ABI_VERSION = 2
 
 EXPORTED_SYMBOLS = [
     "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
@@ -42,7 +42,8 @@ class AsModel(C.Structure):
         ("gear", C.c_float * MAXL), ("num_geoms", C.c_int32), ("geom_link", C.c_int32 * MAXG),
         ("geom_type", C.c_int32 * MAXG), ("geom_foot", C.c_int32 * MAXG), ("geom_radius", C.c_float * MAXG),
         ("geom_p0", (C.c_float * 3) * MAXG), ("geom_p1", (C.c_float * 3) * MAXG), ("torso_link", C.c_int32),
-        ("foot_link", C.c_int32 * 2),
+        ("foot_link", C.c_int32 * 2), ("num_priority_geoms", C.c_int32), ("num_self_pairs", C.c_int32),
+        ("self_pair", C.c_int32 * MAXSP),
     ]
 
 
@@ -201,6 +202,9 @@ def make_model(m: dict) -> AsModel:
         for i, row in enumerate(m[name]):
             arr[i][:] = [float(x) for x in row]
     M.num_geoms = m["num_geoms"]
+    M.num_priority_geoms = int(m["num_priority_geoms"])
+    M.num_self_pairs = int(m["num_self_pairs"])
+    M.self_pair[:] = [int(x) for x in m["self_pair"]]
     M.torso_link = int(m["torso_link"])
     M.foot_link[:] = [int(x) for x in m["foot_link"]]
     return M

@@ -62,7 +62,6 @@ struct as_env {
   std::vector<hipEvent_t> ev;
   unsigned long long* stamps = nullptr;  // diagnostic (as_debug_stamps)
   int32_t prof_cap = 0, prof_n = 0, prof_stride = 1, prof_calls = 0;
-  int32_t tune = 0;  // AS_TUNE (diagnostic scheduling experiments; 0 = default)
 };
 
 extern "C" {
@@ -151,7 +150,6 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
 
   as_env* env = new as_env();
   env->n = num_envs;
-  if (const char* t = getenv("AS_TUNE")) env->tune = atoi(t);
   env->device = device;
   env->seed = seed;
   env->env_offset = env_id_offset;
@@ -210,7 +208,6 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   a.seed = env->seed;
   a.env_offset = env->env_offset;
   a.stamps = env->stamps;
-  a.tune = env->tune;
   a.obs = mode == as::kModePhysics ? nullptr : obs;
   a.side = env->side_dev;
   const bool prof = env->prof_n < env->prof_cap && (env->prof_calls++ % env->prof_stride) == 0;

@@ -49,7 +49,6 @@ struct StepArgs {
   uint64_t seed;
   int64_t env_offset;
   unsigned long long* stamps;  // diagnostic phase timing (s_memtime deltas summed over waves) or null
-  int32_t tune;                // scheduling experiments (env AS_TUNE, diagnostic): 0 default, 1 no s_setprio
 };
 
 // phase ids of the diagnostic stamps (as_debug_stamps)

@@ -37,6 +37,7 @@ constexpr int kBisectIters = 12;    // capsule minimum: slope-sign bisection, in
 constexpr int kPairsPerChunk = G;   // one lane per (stone, geom) pair in the exact test
 static_assert(kPairsPerChunk - 1 + G <= 64, "pending pair list (PhaseScratch::col.pl)");
 constexpr int kSweepB = 4;        // pivot block of the H^-1 sweep
+typedef float v4f __attribute__((ext_vector_type(4)));  // native 16-B vector (LDS b128 accesses)
 
 static_assert(NVMAX <= G, "one lane per generalized velocity");
 static_assert(LMAX <= G, "one lane per link");
@@ -66,17 +67,18 @@ struct DynScratch {
   };
 };
 struct alignas(16) ConScratch {
-  float Jm[MAXR][LDJ];  // J rows (lane = dof column)
-  float Wm[MAXR][LDJ];  // W = H^-1 J^T rows (lane = dof column)
+  float Jm[MAXR][LDJ];  // J rows (lane = dof column); W = H^-1 J^T stays in registers (lane = dof)
 };
 union alignas(16) PhaseScratch {
   DynScratch d;
   float obs[64];        // epilogue: observation row staging
   struct {
     float g[32][8];     // collide: geom segment endpoints, radius, packed type/foot/link
-    int pl[64];         //          pending (stone << 8 | geom) pairs, stone-major (< 32 + G)
+    alignas(16) float bs[32][4];  //  bounding sphere (segment midpoint, half length + radius)
+    int pl[64];         //          pending (stone << 8 | geom) pairs (< 32 + G), then self pairs
+    uint32_t need[NST]; //          per candidate stone: geoms past the bounding test
   } col;
-  struct {
+  struct alignas(16) {
     float q[kSweepB][32];       // sweep: the pivot rows of a round (without the pivot columns)
     float pb[kSweepB][kSweepB]; //        and the pivot block H_PP
   } sw;                 // aliases d.c / d.Ib, dead by then
@@ -123,11 +125,11 @@ struct EnvS {
   float rlam[MAXR];     // PGS impulses
   alignas(16) float rmeta[MAXR][4]; // per row: 1/A_rr, target, type (0 normal, 1 tangent, 2 limit)
   float cdir[MAXC][3][3];  // contact frame: normal, tangent 1, tangent 2
-  int rlink[MAXR];      // contact link, or -1 - dof for a limit row
+  int rlink[MAXR];      // contact rows: link | (link2 + 1) << 8 (link2 = -1: stone); limit rows: -1 - dof
   float rsign[MAXR];
   float lamn[MAXC];     // normal impulses of the last PGS sweep (contact flags)
   float cpt[MAXC][3], cn[MAXC][3], csep[MAXC];
-  int clink[MAXC], cstone[MAXC], cfoot[MAXC];
+  int clink[MAXC], clink2[MAXC], cstone[MAXC], cfoot[MAXC];  // clink2 / cstone: -1 unless self / stone
   float u[NVMAX];
   float qi[LMAX];       // hinge angles, link order (link i -> qi[i-1])
   float tau[LMAX];
@@ -674,18 +676,22 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
     float(&Pb)[kSweepB][kSweepB] = s.x.sw.pb;
     const int t = lane - p;
     const bool piv = (unsigned)t < (unsigned)B;
+    // explicit 16-B LDS accesses on a native 4-vector type (float4 is a struct whose copies SROA
+    // splits; the stores then come out as b96 + b32 pairs whenever the rotated row does not sit in
+    // aligned register quads)
+    static_assert(B == 4, "16-B pivot rows");
     if (piv) {
+      *reinterpret_cast<v4f*>(Pb[t]) = v4f{Hr[0], Hr[1], Hr[2], Hr[3]};
 #pragma unroll
-      for (int c = 0; c < B; ++c) Pb[t][c] = Hr[c];
-#pragma unroll
-      for (int j = B; j < NP; ++j) Q[t][j] = Hr[j];
+      for (int j = B; j < NP; j += 4) *reinterpret_cast<v4f*>(&Q[t][j]) = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
     }
     __syncthreads();
     float D[B][B];
 #pragma unroll
-    for (int a = 0; a < B; ++a)
-#pragma unroll
-      for (int c = 0; c < B; ++c) D[a][c] = Pb[a][c];
+    for (int a = 0; a < B; ++a) {
+      const v4f d = *reinterpret_cast<const v4f*>(Pb[a]);
+      D[a][0] = d.x; D[a][1] = d.y; D[a][2] = d.z; D[a][3] = d.w;
+    }
     block_inverse<B>(D);
     float alpha = 1.f, beta[B];
 #pragma unroll
@@ -700,11 +706,20 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
     }
     if (piv) alpha = 0.f;
 #pragma unroll
-    for (int j = B; j < NP; ++j) {
-      float v = alpha * Hr[j];
+    for (int j = B; j < NP; j += 4) {
+      float q[B][4];
 #pragma unroll
-      for (int c = 0; c < B; ++c) v = fmaf(-beta[c], Q[c][j], v);
-      Hr[j - B] = v;
+      for (int c = 0; c < B; ++c) {
+        const v4f x = *reinterpret_cast<const v4f*>(&Q[c][j]);
+        q[c][0] = x.x; q[c][1] = x.y; q[c][2] = x.z; q[c][3] = x.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = alpha * Hr[j + i];
+#pragma unroll
+        for (int c = 0; c < B; ++c) v = fmaf(-beta[c], q[c][i], v);
+        Hr[j + i - B] = v;
+      }
     }
 #pragma unroll
     for (int c = 0; c < B; ++c) Hr[NP - B + c] = beta[c];
@@ -715,18 +730,28 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
 // ------------------------------------------------------------------------------------------------
 // contacts: robot geoms vs axis-aligned stone boxes
 
-__device__ void emit_contact(EnvS& s, int slot, int link, int stone, int foot, const float* P, const float* n,
-                             float sep, float r) {
-  if (slot >= MAXC) return;
-  s.clink[slot] = link; s.cstone[slot] = stone; s.cfoot[slot] = foot; s.csep[slot] = sep;
+__device__ void emit_contact(EnvS& s, int slot, int ncap, int link, int link2, int stone, int foot, const float* P,
+                             const float* n, float sep, float r) {
+  if (slot >= ncap) return;
+  s.clink[slot] = link; s.clink2[slot] = link2; s.cstone[slot] = stone; s.cfoot[slot] = foot; s.csep[slot] = sep;
   for (int k = 0; k < 3; ++k) { s.cn[slot][k] = n[k]; s.cpt[slot][k] = P[k] - n[k] * r; }
 }
 
-__device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
+// At most ncap contacts, in priority order (oracle/physics.c collide() emits the same list):
+//   1. the priority geoms (the feet: geoms [0, num_priority_geoms)) against the candidate stones,
+//      stone-major, geom-minor;  2. every other geom against the candidate stones, likewise;
+//   3. robot self-contacts, one per self-collision pair in table order.
+__device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane, int ncap) {
   const as_model_t& m = K.model;
   const float* h = K.sim.stone_half;
   const float margin = K.sim.margin;
-  const int nst = K.task.num_steps, ng = m.num_geoms;
+  const int nst = K.task.num_steps, ng = m.num_geoms, npri = m.num_priority_geoms, nsp = m.num_self_pairs;
+  // self-collision pair words of this lane (pairs lane, lane + 32, ...), loaded first so that their
+  // latency hides behind the stone contacts
+  constexpr int kSelfW = AS_MAX_SELF_PAIRS / G;
+  int spw[kSelfW];
+#pragma unroll
+  for (int i = 0; i < kSelfW; ++i) spw[i] = G * i + lane < nsp ? m.self_pair[G * i + lane] : 0;
   // geom segment in the O frame (lane = geom), formed once for all candidate stones
   const bool gv = lane < ng;
   const int g = gv ? lane : 0;
@@ -744,7 +769,7 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   const float mid[3] = {0.5f * (a[0] + bb[0]), 0.5f * (a[1] + bb[1]), 0.5f * (a[2] + bb[2])};
   // broadphase (lane = stone): stone boxes that come within the contact margin of the robot's
   // bounding box (union of the geoms' boxes).  Conservative: every pair the narrowphase would
-  // turn into a contact survives, so the contact set and order match the oracle's broadphase.
+  // turn into a contact survives, so the contact set and order match the oracle's.
   float blo[3], bhi[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -767,21 +792,21 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
   uint32_t mine = (uint32_t)(bal >> (32 * half));
   if (isc) s.cand[__popc(mine & ((1u << lane) - 1u))] = lane;
   const int ncand = __popc(mine);
-  __syncthreads();
-  // narrowphase in two passes.  (A) lane = geom, loop over the candidate stones: the cheap
-  // bounding test (spheres: the exact separation) appends the surviving (stone, geom) pairs to a
-  // list in LDS, stone-major and geom-minor -- the oracle's emission order.  (B) lane = pair, in
-  // chunks of kPairsPerChunk: the exact test (capsules: slope bisection for the segment's closest
+  // narrowphase in two passes.  (A) lane = geom, loop over the candidate stones (once for the
+  // priority geoms, once for the rest): the cheap bounding test (spheres: the exact separation)
+  // appends the surviving (stone, geom) pairs to a list in LDS, in emission order.  (B) lane = pair,
+  // in chunks of kPairsPerChunk: the exact test (capsules: slope bisection for the segment's closest
   // point) and the contacts, emitted in list order by a prefix sum.  A chunk is flushed as soon as
   // kPairsPerChunk pairs are pending, so the list never exceeds 32 + 22 entries, and the search
-  // stops once this env has MAXC contacts.
+  // stops once this env has ncap contacts.
   {
-    float* gs = s.x.col.g[lane];  // staging of this lane's geom for pass B
+    float* gs = s.x.col.g[lane];  // staging of this lane's geom for pass B and the self pairs
     if (gv) {
       gs[0] = a[0]; gs[1] = a[1]; gs[2] = a[2];
       gs[3] = bb[0]; gs[4] = bb[1]; gs[5] = bb[2];
       gs[6] = r;
       gs[7] = __int_as_float(gtype | ((foot + 1) << 4) | (link << 8));
+      *reinterpret_cast<v4f*>(s.x.col.bs[lane]) = v4f{mid[0], mid[1], mid[2], 0.5f * L + r};
     }
   }
   int* pl = s.x.col.pl;
@@ -847,9 +872,9 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
     }
     int total;
     const int slot = base + half_scan3(cnt, total);
-    if (cnt > 0) emit_contact(s, slot, plink, pst, pfoot, P0, N0, SEP0, pr);
-    if (cnt > 1) emit_contact(s, slot + 1, plink, pst, pfoot, P1, N1, SEP1, pr);
-    if (cnt > 2) emit_contact(s, slot + 2, plink, pst, pfoot, P2, N2, SEP2, pr);
+    if (cnt > 0) emit_contact(s, slot, ncap, plink, -1, pst, pfoot, P0, N0, SEP0, pr);
+    if (cnt > 1) emit_contact(s, slot + 1, ncap, plink, -1, pst, pfoot, P1, N1, SEP1, pr);
+    if (cnt > 2) emit_contact(s, slot + 2, ncap, plink, -1, pst, pfoot, P2, N2, SEP2, pr);
     base += total;
     // shift the unprocessed tail (< 32 entries) to the front
     const int rest = pend - npairs;
@@ -860,24 +885,94 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane) {
     __syncthreads();
   };
   __syncthreads();
+  // pass A (lane = geom): one bounding test per (candidate stone, geom), kept as a per-stone mask of
+  // the surviving geoms; the masks then become the pair list class by class (feet first),
+  // stone-major, geom-minor
+  uint32_t* cneed = s.x.col.need;
+#pragma unroll 1
   for (int ci = 0; ci < ncand; ++ci) {
-    if (base >= MAXC) break;  // later contacts would be dropped anyway
     const int st = s.cand[ci];
     float c[3], nr[3];
     for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * st + k] - s.root_pos[k];
     bool need = false;
-    if (gv) {
-      need = gtype == 0 ? sd_box(a, c, h, nr) - r < margin : sd_box(mid, c, h, nr) <= 0.5f * L + r + margin;
-    }
+    if (gv) need = gtype == 0 ? sd_box(a, c, h, nr) - r < margin : sd_box(mid, c, h, nr) <= 0.5f * L + r + margin;
     const uint32_t bl = (uint32_t)(__ballot(need) >> (32 * half));
-    if (need) pl[pend + __popc(bl & ((1u << lane) - 1u))] = (st << 8) | lane;
-    pend += __popc(bl);
-    __syncthreads();
-    if (pend >= kPairsPerChunk) flush(kPairsPerChunk);
+    if (lane == 0) cneed[ci] = bl;
   }
-  if (pend > 0 && base < MAXC) flush(pend);
   __syncthreads();
-  if (lane == 0) s.ncontact = base < MAXC ? base : MAXC;
+  const uint32_t primask = npri >= 32 ? ~0u : (1u << npri) - 1u;
+#pragma unroll 1
+  for (int cls = 0; cls < 2; ++cls) {
+#pragma unroll 1
+    for (int ci = 0; ci < ncand; ++ci) {
+      if (base >= ncap) break;  // later contacts would be dropped anyway
+      const uint32_t bl = cneed[ci] & (cls == 0 ? primask : ~primask);
+      if ((bl >> lane) & 1u) pl[pend + __popc(bl & ((1u << lane) - 1u))] = (s.cand[ci] << 8) | lane;
+      pend += __popc(bl);  // no barrier: the single wave's LDS operations complete in issue order
+      if (pend >= kPairsPerChunk) flush(kPairsPerChunk);
+    }
+  }
+  if (pend > 0 && base < ncap) flush(pend);
+  // self-contacts.  (A) lane = pair: the bounding-sphere filter; the surviving pairs are appended to
+  // the pending list in table order.  (B) lane = pending pair, in chunks of G: the capsule-capsule
+  // closest points (include/as_detmath.h, shared with the oracle), emitted in list order.
+  pend = 0;
+  auto flush_self = [&](int npairs) {
+    const bool act = lane < npairs;
+    const int e = pl[act ? lane : 0];
+    const int g1 = e & 0xff, g2 = e >> 8;
+    int cnt = 0, l1 = 0, l2 = 0;
+    float P[3], n[3], sep = 0.f;
+    if (act) {
+      const float* q1 = s.x.col.g[g1];
+      const float* q2 = s.x.col.g[g2];
+      sep = as_capsule_contact(q1, q1 + 3, q1[6], q2, q2 + 3, q2[6], P, n);
+      cnt = sep < margin;
+      l1 = __float_as_int(q1[7]) >> 8;
+      l2 = __float_as_int(q2[7]) >> 8;
+    }
+    int total;
+    const int slot = base + half_scan3(cnt, total);
+    if (cnt) emit_contact(s, slot, ncap, l1, l2, -1, -1, P, n, sep, 0.f);
+    base += total;
+    const int rest = pend - npairs;
+    const int tail = lane < rest ? pl[npairs + lane] : 0;
+    __syncthreads();
+    if (lane < rest) pl[lane] = tail;
+    pend = rest;
+    __syncthreads();
+  };
+  // all filter tests first (their LDS reads overlap), then the list is appended to without a
+  // barrier per word (LDS operations of the single wave complete in issue order)
+  uint32_t hbl[kSelfW];
+#pragma unroll
+  for (int i = 0; i < kSelfW; ++i) {
+    const bool pv = G * i + lane < nsp;
+    const int g1 = spw[i] & 0xff, g2 = spw[i] >> 8;
+    const v4f s1 = *reinterpret_cast<const v4f*>(s.x.col.bs[g1]);
+    const v4f s2 = *reinterpret_cast<const v4f*>(s.x.col.bs[g2]);
+    const float m1[3] = {s1.x, s1.y, s1.z}, m2[3] = {s2.x, s2.y, s2.z};
+    hbl[i] = (uint32_t)(__ballot(pv && as_sphere_bound(m1, s1.w, m2, s2.w, margin)) >> (32 * half));
+  }
+  // a rolled loop (one copy of flush_self: code size is instruction-cache footprint); word i of
+  // the register arrays by a select chain
+#pragma unroll 1
+  for (int i = 0; i < kSelfW; ++i) {
+    if (G * i >= nsp || base >= ncap) break;
+    uint32_t bl = hbl[0];
+    int w = spw[0];
+#pragma unroll
+    for (int k = 1; k < kSelfW; ++k) {
+      bl = i == k ? hbl[k] : bl;
+      w = i == k ? spw[k] : w;
+    }
+    if ((bl >> lane) & 1u) pl[pend + __popc(bl & ((1u << lane) - 1u))] = w;
+    pend += __popc(bl);
+    if (pend >= G) flush_self(G);
+  }
+  if (pend > 0 && base < ncap) flush_self(pend);
+  __syncthreads();
+  if (lane == 0) s.ncontact = base < ncap ? base : ncap;
   __syncthreads();
 }
 
@@ -895,7 +990,7 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
 // caller; normal and limit rows clamp it to [0, inf), tangent rows to +-mu * (latest normal
 // impulse ln) -- one v_med3 for both (a tangent row's target is 0).  Updates the row's impulse
 // (and ln on a normal row) and returns the impulse change.
-__device__ __forceinline__ float pgs_clamp(const float4& mt, float t, float mu, float& lam, float& ln) {
+__device__ __forceinline__ float pgs_clamp(const v4f& mt, float t, float mu, float& lam, float& ln) {
   // bounds as one FMA each from ln (tangent: mu_r = mu, off = 0; otherwise mu_r = 0, off = inf;
   // 0 * ln + 0 keeps the normal rows' lower bound +0)
   const bool tangent = mt.z == 1.f;
@@ -909,7 +1004,7 @@ __device__ __forceinline__ float pgs_clamp(const float4& mt, float t, float mu, 
 
 template <int NV>
 __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, uint32_t* mask_out,
-                        Stamp& ts, int tune) {
+                        Stamp& ts) {
   // Opaque copies of the constants pointer and the lane id: everything derived from them below
   // (model-table loads, LDS addresses, lane masks) is loop-invariant, and without this the
   // compiler hoists all of it out of the substep loop and spills it.
@@ -948,29 +1043,9 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   }
   __syncthreads();
   ts.mark(kStSolve);
-  // ---- constraints
-  collide(K, s, lane);
-  ts.mark(kStCollide);
-  const int nc = s.ncontact;
-  if (lane < nc) {  // contact rows 3c..3c+2: normal, tangent 1, tangent 2
-    float t1[3], t2[3];
-    tangents(s.cn[lane], t1, t2);
-    const float* dirs[3] = {s.cn[lane], t1, t2};
-    float sp = s.csep[lane];
-    for (int d = 0; d < 3; ++d) {
-      int r = 3 * lane + d;
-      for (int k = 0; k < 3; ++k) s.cdir[lane][d][k] = dirs[d][k];
-      s.rlink[r] = s.clink[lane];
-      s.rsign[r] = 0.f;
-      s.rmeta[r][1] = d == 0 ? (sp < 0.f ? fminf(K.sim.baumgarte * fmaxf(-sp - K.sim.slop, 0.f) / dt,
-                                                   K.sim.max_depen_vel)
-                                         : -sp / dt)
-                             : 0.f;
-      s.rmeta[r][2] = d == 0 ? 0.f : 1.f;
-    }
-  }
-  const int crow = 3 * nc;
-  // joint-limit rows: lane h (hinge) emits lower then upper, in hinge order
+  // ---- constraints.  Joint-limit rows first counted (every one is kept), then the contacts fill the
+  //      remaining rows, at most MAXC; rows are ordered contacts (normal, tangent, tangent), then the
+  //      limits (lane h = hinge: lower then upper, in hinge order)
   int lo_v = 0, hi_v = 0;
   float err_lo = 0.f, err_hi = 0.f;
   if (lane < nh) {
@@ -980,8 +1055,33 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     lo_v = pred < tp.lo;
     hi_v = pred > tp.hi;
   }
-  int total;
-  int slot = crow + half_scan3(lo_v + hi_v, total);
+  int ltotal;
+  const int lpos = half_scan3(lo_v + hi_v, ltotal);
+  const int nlim = ltotal < MAXR ? ltotal : MAXR;
+  const int ncap = (MAXR - nlim) / 3 < MAXC ? (MAXR - nlim) / 3 : MAXC;
+  collide(K, s, lane, ncap);
+  ts.mark(kStCollide);
+  const int nc = s.ncontact;
+  if (lane < nc) {  // contact rows 3c..3c+2: normal, tangent 1, tangent 2
+    float t1[3], t2[3];
+    tangents(s.cn[lane], t1, t2);
+    const float* dirs[3] = {s.cn[lane], t1, t2};
+    float sp = s.csep[lane];
+    const int lk = s.clink[lane] | ((s.clink2[lane] + 1) << 8);
+    for (int d = 0; d < 3; ++d) {
+      int r = 3 * lane + d;
+      for (int k = 0; k < 3; ++k) s.cdir[lane][d][k] = dirs[d][k];
+      s.rlink[r] = lk;
+      s.rsign[r] = 0.f;
+      s.rmeta[r][1] = d == 0 ? (sp < 0.f ? fminf(K.sim.baumgarte * fmaxf(-sp - K.sim.slop, 0.f) / dt,
+                                                   K.sim.max_depen_vel)
+                                         : -sp / dt)
+                             : 0.f;
+      s.rmeta[r][2] = d == 0 ? 0.f : 1.f;
+    }
+  }
+  const int crow = 3 * nc;
+  int slot = crow + lpos;
   for (int sd = 0; sd < 2; ++sd) {
     int viol = sd == 0 ? lo_v : hi_v;
     if (!viol) continue;
@@ -994,7 +1094,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     }
     ++slot;
   }
-  const int nrow = crow + total < MAXR ? crow + total : MAXR;
+  const int nrow = crow + nlim;
   if (lane == 0) s.nrow = nrow;
   ts.count(nrow, nc);
   __syncthreads();
@@ -1013,7 +1113,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   // issue slots and set the launch's tail.  The heavier wave of the pair takes precedence for the
   // rest of this substep and the fixed-cost phases of the next (scalar branch: s_setprio is not
   // masked by EXEC, so exactly one of them may execute).
-  if (tune != 1) {
+  {
     const int lvl = __builtin_amdgcn_readfirstlane(maxrow) / kPrioRows;
     if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
     else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
@@ -1047,15 +1147,21 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       float f6[6];  // spatial force direction [P x d; d]
       cross3(P, dir[u], f6);
       f6[3] = dir[u][0]; f6[4] = dir[u][1]; f6[5] = dir[u][2];
-      const bool onpath = lk[u] >= 0 && ((dsub >> (lk[u] & 31)) & 1u);
+      // a self-contact's second link (bits 8.., + 1) takes the opposite impulse: dofs on both paths
+      // give jcon - jcon = 0 (oracle contact_row)
+      const bool con = lk[u] >= 0;
+      const int l2 = (lk[u] >> 8) - 1;
+      const bool on1 = con && ((dsub >> (lk[u] & 31)) & 1u);
+      const bool on2 = con && l2 >= 0 && ((dsub >> (l2 & 31)) & 1u);
       const float jcon = dot6(Sj, f6);
-      float jv = onpath ? jcon : (-1 - lk[u] == lane ? sg[u] : 0.f);
+      float jv = con ? (on1 ? jcon : 0.f) - (on2 ? jcon : 0.f) : (-1 - lk[u] == lane ? sg[u] : 0.f);
       jv = (r < nrow && lane < NV) ? jv : 0.f;
       if (lane < LDJ) s.x.k.Jm[r][lane] = jv;
     }
   }
   __syncthreads();
-  // W rows, one group per iteration; each row's dot product runs as two interleaved partial sums.
+  // W rows, one group per iteration (unrolled, so that lane j's W column stays in registers
+  // for the PGS sweep); each row's dot product runs as two interleaved partial sums.
   // Hr is zero on lanes >= NV, so their W entries are zero; they read J column 0 (keeps every LDS
   // address in bounds).  Per group, the half-wave reduces A_rr = J_r . W_r of its rows and the
   // in-group couplings A_10, A_20, A_21 (A_sr = J_s . W_r) that the PGS sweep uses; lane r keeps
@@ -1063,42 +1169,52 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   const int jc = lane < NV ? lane : 0;
   const float jmask = lane < NV ? 1.f : 0.f;
   float arr = 0.f, acp = 0.f;
-#pragma unroll 1
-  for (int r0 = 0; r0 < maxrow; r0 += kRowGroup) {
-    float w[kRowGroup][2];
-    float jown[kRowGroup];
+  float Wc[MAXR];
 #pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      jown[u] = s.x.k.Jm[r0 + u][jc];
-      w[u][0] = w[u][1] = 0.f;
-    }
+  for (int r = 0; r < MAXR; ++r) Wc[r] = 0.f;
 #pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      const float4* jr = reinterpret_cast<const float4*>(s.x.k.Jm[r0 + u]);  // 16-B aligned rows
-      float jrow[LDJ];
+  for (int r0 = 0; r0 < MAXR; r0 += kRowGroup) {
+    // a uniform skip, not an exit: a loop with one exit and a constant trip count unrolls fully
+    if (r0 < maxrow) {
+      // the group's row index passes through an empty asm that also takes the W of the group two
+      // back, so at most two groups of J-row reads are in flight (hoisted further they spill)
+      int rr = r0;
+      if (r0 >= 2 * kRowGroup) asm volatile("" : "+v"(rr) : "v"(Wc[r0 - kRowGroup - 1]));
+      float w[kRowGroup][2];
+      float jown[kRowGroup];
 #pragma unroll
-      for (int q = 0; q < LDJ / 4; ++q) {
-        const float4 t = jr[q];
-        jrow[4 * q] = t.x; jrow[4 * q + 1] = t.y; jrow[4 * q + 2] = t.z; jrow[4 * q + 3] = t.w;
+      for (int u = 0; u < kRowGroup; ++u) {
+        jown[u] = s.x.k.Jm[rr + u][jc];
+        w[u][0] = w[u][1] = 0.f;
       }
 #pragma unroll
-      for (int k = 0; k < NV; ++k) w[u][k & 1] = fmaf(Hr[k], jrow[k], w[u][k & 1]);
-    }
-    float wu[kRowGroup], a[2 * kRowGroup];
+      for (int u = 0; u < kRowGroup; ++u) {
+        const v4f* jr = reinterpret_cast<const v4f*>(s.x.k.Jm[rr + u]);  // 16-B aligned rows
+        float jrow[LDJ];
 #pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      wu[u] = w[u][0] + w[u][1];
-      if (lane < LDJ) s.x.k.Wm[r0 + u][lane] = wu[u];
-      a[u] = jown[u] * wu[u];
-    }
-    a[3] = jown[1] * wu[0];  // A_10, kept by row r0
-    a[4] = jown[2] * wu[0];  // A_20, kept by row r0 + 1
-    a[5] = jown[2] * wu[1];  // A_21, kept by row r0 + 2
-    half_sum_n(a);
+        for (int q = 0; q < LDJ / 4; ++q) {
+          const v4f t = jr[q];
+          jrow[4 * q] = t.x; jrow[4 * q + 1] = t.y; jrow[4 * q + 2] = t.z; jrow[4 * q + 3] = t.w;
+        }
 #pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      arr = lane == r0 + u ? a[u] : arr;
-      acp = lane == r0 + u ? a[kRowGroup + u] : acp;
+        for (int k = 0; k < NV; ++k) w[u][k & 1] = fmaf(Hr[k], jrow[k], w[u][k & 1]);
+      }
+      float wu[kRowGroup], a[2 * kRowGroup];
+#pragma unroll
+      for (int u = 0; u < kRowGroup; ++u) {
+        wu[u] = w[u][0] + w[u][1];
+        Wc[r0 + u] = wu[u];
+        a[u] = jown[u] * wu[u];
+      }
+      a[3] = jown[1] * wu[0];  // A_10, kept by row r0
+      a[4] = jown[2] * wu[0];  // A_20, kept by row r0 + 1
+      a[5] = jown[2] * wu[1];  // A_21, kept by row r0 + 2
+      half_sum_n(a);
+#pragma unroll
+      for (int u = 0; u < kRowGroup; ++u) {
+        arr = lane == r0 + u ? a[u] : arr;
+        acp = lane == r0 + u ? a[kRowGroup + u] : acp;
+      }
     }
   }
   if (lane < MAXR && lane < (maxrow + kRowGroup - 1) / kRowGroup * kRowGroup) {
@@ -1120,39 +1236,45 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   float mu = K.sim.friction;
   asm volatile("" : "+v"(mu));
   const int iters = K.sim.pgs_iters;
-  float Jc[MAXR], Wc[MAXR], lamr[MAXR];
+  float Jc[MAXR], lamr[MAXR];
 #pragma unroll
   for (int r = 0; r < MAXR; ++r) {
     Jc[r] = s.x.k.Jm[r][jc] * jmask;
-    Wc[r] = s.x.k.Wm[r][jc] * jmask;
     lamr[r] = 0.f;
   }
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
     float ln = 0.f;
+    float uprev = uj;
 #pragma unroll
     for (int r = 0; r < MAXR; r += kRowGroup) {
-      if (r >= maxrow) break;
-      const float4 m0 = *reinterpret_cast<const float4*>(s.rmeta[r]);
-      const float4 m1 = *reinterpret_cast<const float4*>(s.rmeta[r + 1]);
-      const float4 m2 = *reinterpret_cast<const float4*>(s.rmeta[r + 2]);
-      float vg[3] = {Jc[r] * uj, Jc[r + 1] * uj, Jc[r + 2] * uj};
-      half_sum_n(vg);
-      // t_s = lambda_s + (target_s - v_s - sum_{r<s} A_sr dl_r) x_s, with the parts that do not
-      // depend on this sweep's impulse changes formed first: the chain from one row's dl to the
-      // next row's clamp is a single FMA
-      const float k10 = m1.x * m0.w, k20 = m2.x * m1.w, k21 = m2.x * m2.w;  // x_s A_sr
-      float t1 = fmaf(-vg[1], m1.x, fmaf(m1.y, m1.x, lamr[r + 1]));
-      float t2 = fmaf(-vg[2], m2.x, fmaf(m2.y, m2.x, lamr[r + 2]));
-      const float d0 = pgs_clamp(m0, fmaf(-vg[0], m0.x, fmaf(m0.y, m0.x, lamr[r])), mu, lamr[r], ln);
-      t1 = fmaf(-k10, d0, t1);
-      t2 = fmaf(-k20, d0, t2);
-      uj = fmaf(Wc[r], d0, uj);
-      const float d1 = pgs_clamp(m1, t1, mu, lamr[r + 1], ln);
-      t2 = fmaf(-k21, d1, t2);
-      uj = fmaf(Wc[r + 1], d1, uj);
-      const float d2 = pgs_clamp(m2, t2, mu, lamr[r + 2], ln);
-      uj = fmaf(Wc[r + 2], d2, uj);
+      if (r < maxrow) {
+        // the group's metadata reads are pinned behind the previous group's start (its u): one
+        // group of reads ahead, none hoisted out of the sweep loop (30 rows would not fit)
+        int rr = r;
+        asm volatile("" : "+v"(rr) : "v"(uprev));
+        uprev = uj;
+        const v4f m0 = *reinterpret_cast<const v4f*>(s.rmeta[rr]);
+        const v4f m1 = *reinterpret_cast<const v4f*>(s.rmeta[rr + 1]);
+        const v4f m2 = *reinterpret_cast<const v4f*>(s.rmeta[rr + 2]);
+        float vg[3] = {Jc[r] * uj, Jc[r + 1] * uj, Jc[r + 2] * uj};
+        half_sum_n(vg);
+        // t_s = lambda_s + (target_s - v_s - sum_{r<s} A_sr dl_r) x_s, with the parts that do not
+        // depend on this sweep's impulse changes formed first: the chain from one row's dl to the
+        // next row's clamp is a single FMA
+        const float k10 = m1.x * m0.w, k20 = m2.x * m1.w, k21 = m2.x * m2.w;  // x_s A_sr
+        float t1 = fmaf(-vg[1], m1.x, fmaf(m1.y, m1.x, lamr[r + 1]));
+        float t2 = fmaf(-vg[2], m2.x, fmaf(m2.y, m2.x, lamr[r + 2]));
+        const float d0 = pgs_clamp(m0, fmaf(-vg[0], m0.x, fmaf(m0.y, m0.x, lamr[r])), mu, lamr[r], ln);
+        t1 = fmaf(-k10, d0, t1);
+        t2 = fmaf(-k20, d0, t2);
+        uj = fmaf(Wc[r], d0, uj);
+        const float d1 = pgs_clamp(m1, t1, mu, lamr[r + 1], ln);
+        t2 = fmaf(-k21, d1, t2);
+        uj = fmaf(Wc[r + 1], d1, uj);
+        const float d2 = pgs_clamp(m2, t2, mu, lamr[r + 2], ln);
+        uj = fmaf(Wc[r + 2], d2, uj);
+      }
     }
   }
   float lam = 0.f;
@@ -1333,7 +1455,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const bool do_physics = P.mode == kModeStep || P.mode == kModePhysics;
   // ---- physics
   if (do_physics) {
-    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, mask, ts, P.tune);
+    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, mask, ts);
     fk<false>(K, s, lane, tp);  // FK of the final pose for body_pos_w (articulation_data.py:439)
     if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
   }

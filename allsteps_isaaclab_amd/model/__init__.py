@@ -2,8 +2,10 @@
 
 ``load_model()`` flattens ``walker3d.json`` into the fixed-size arrays of the C-ABI model struct
 (``include/allsteps.h`` :c:type:`as_model_t`): links in topological (parent-before-child) order,
-link 0 the floating root, link i >= 1 carrying hinge dof i-1; geoms ordered feet first so that the
-contact cap (``AS_MAX_CONTACTS``) never drops a foot contact in favour of another body's.
+link 0 the floating root, link i >= 1 carrying hinge dof i-1; geoms ordered feet first
+(``num_priority_geoms``): their stone contacts are emitted before every other geom's, so the contact cap
+(``AS_MAX_CONTACTS``) never drops a foot contact in favour of another body's; and the self-collision
+pair table (``self_pair``).
 """
 
 from __future__ import annotations
@@ -15,6 +17,7 @@ import numpy as np
 
 MAX_LINKS = 32
 MAX_GEOMS = 32
+MAX_SELF_PAIRS = 256  # include/allsteps.h AS_MAX_SELF_PAIRS
 HERE = os.path.dirname(os.path.abspath(__file__))
 WALKER_JSON = os.path.join(HERE, "walker3d.json")
 ANYMAL_C_JSON = os.path.join(HERE, "anymal_c.json")  # BASELINE C5 quadruped (authored approximation)
@@ -99,12 +102,48 @@ def load_model(path: str = WALKER_JSON) -> dict:
         m["geom_p0"][k] = g["p0"]
         m["geom_p1"][k] = g["p1"]
         m["geom_name"].append(g["name"])
+    m["num_priority_geoms"] = sum(1 for t in geoms if t[0] == 0)
+    m["self_pair"], m["num_self_pairs"] = self_collision_pairs(links, [(t[2], t[3]) for t in geoms])
     m["torso_link"] = bl[j.get("torso", "torso")]
     m["foot_link"] = np.array(foot_link, np.int32)
     m["link_names"] = [L["name"] for L in links]
     m["dof_names"] = list(j["cfg_dof_order"])
     m["total_mass"] = float(j["total_mass"])
     return m
+
+
+def self_collision_pairs(links: list, geoms: list) -> tuple[np.ndarray, int]:
+    """Geom pairs (g1 < g2, ascending) the robot collides with itself: ``walker3d.py:27``
+    ``enabled_self_collisions=True`` on a robot imported from ``walker3d.xml``.
+
+    A pair is kept when its geoms sit on different weld bodies (a jointed MJCF body together with the
+    joint-less bodies merged into it: head / torso on the root, the hands on the forearms) that are not
+    parent and child (PhysX never collides the two links of a joint; MuJoCo's parent filter), and when
+    the MJCF filter bits admit it: ``(contype1 & conaffinity2) | (contype2 & conaffinity1)``
+    (``walker3d.xml:5,34,41,44``: torso / butt carry 1, waist 2, everything else 3).
+    Packed as ``g1 | g2 << 8`` (``include/allsteps.h`` ``as_model_t.self_pair``)."""
+    def weld_parent(i: int):
+        body = links[i]["body"]
+        while links[i]["parent"] >= 0 and links[links[i]["parent"]]["body"] == body:
+            i = links[i]["parent"]
+        p = links[i]["parent"]
+        return links[p]["body"] if p >= 0 else None
+
+    out = []
+    for g1 in range(len(geoms)):
+        for g2 in range(g1 + 1, len(geoms)):
+            (l1, a), (l2, b) = geoms[g1], geoms[g2]
+            w1, w2 = links[l1]["body"], links[l2]["body"]
+            if w1 == w2 or weld_parent(l1) == w2 or weld_parent(l2) == w1:
+                continue
+            if not ((a.get("contype", 1) & b.get("conaffinity", 1)) | (b.get("contype", 1) & a.get("conaffinity", 1))):
+                continue
+            out.append(g1 | (g2 << 8))
+    if len(out) > MAX_SELF_PAIRS:
+        raise ValueError(f"{len(out)} self-collision pairs > {MAX_SELF_PAIRS}")
+    arr = np.zeros(MAX_SELF_PAIRS, np.int32)
+    arr[: len(out)] = out
+    return arr, len(out)
 
 
 def joint_limits_cfg(m: dict) -> np.ndarray:

@@ -123,12 +123,16 @@ def combine(parts):
 class _Defaults:
     def __init__(self, root: ET.Element):
         self.joint = {}
+        self.geom = {}
         self.classes = {}
         d = root.find("default")
         if d is not None:
             j = d.find("joint")
             if j is not None:
                 self.joint = dict(j.attrib)
+            g = d.find("geom")
+            if g is not None:
+                self.geom = dict(g.attrib)
             for cls in d.findall("default"):
                 cj = cls.find("joint")
                 self.classes[cls.get("class")] = dict(cj.attrib) if cj is not None else {}
@@ -140,6 +144,9 @@ class _Defaults:
         if cls is not None and key in self.classes.get(cls, {}):
             return self.classes[cls][key]
         return self.joint.get(key, fallback)
+
+    def geom_attr(self, g: ET.Element, key: str, fallback=None):
+        return g.get(key, self.geom.get(key, fallback))
 
 
 def compile_mjcf(path: str, opts: dict | None = None) -> dict:
@@ -159,15 +166,18 @@ def compile_mjcf(path: str, opts: dict | None = None) -> dict:
         for g in body.findall("geom"):
             gtype = g.get("type", "sphere")
             size = _floats(g.get("size"))
+            # MuJoCo collision filter bits (default 1 / 1; walker3d.xml:5 sets 3 / 3, torso / butt 1, waist 2)
+            filt = {"contype": int(defaults.geom_attr(g, "contype", "1")),
+                    "conaffinity": int(defaults.geom_attr(g, "conaffinity", "1"))}
             if gtype == "sphere":
                 p = np.array(_floats(g.get("pos", "0 0 0"), 3))
                 out.append({"name": g.get("name"), "type": "sphere", "radius": size[0],
-                            "p0": (R_off @ p + p_off).tolist(), "p1": (R_off @ p + p_off).tolist()})
+                            "p0": (R_off @ p + p_off).tolist(), "p1": (R_off @ p + p_off).tolist(), **filt})
             elif gtype == "capsule":
                 ft = _floats(g.get("fromto"), 6)
                 a, b = np.array(ft[:3]), np.array(ft[3:])
                 out.append({"name": g.get("name"), "type": "capsule", "radius": size[0],
-                            "p0": (R_off @ a + p_off).tolist(), "p1": (R_off @ b + p_off).tolist()})
+                            "p0": (R_off @ a + p_off).tolist(), "p1": (R_off @ b + p_off).tolist(), **filt})
             else:
                 raise ValueError(f"unsupported geom type {gtype}")
         return out

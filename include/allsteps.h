@@ -29,12 +29,16 @@
 extern "C" {
 #endif
 
-#define AS_ABI_VERSION 1
+#define AS_ABI_VERSION 2
 #define AS_MAX_LINKS 32
 #define AS_MAX_GEOMS 32
+#define AS_MAX_SELF_PAIRS 256
 #define AS_NUM_STONES 20
-#define AS_MAX_CONTACTS 8
-#define AS_MAX_ROWS 24
+/* Constraint budget per env and substep: every active joint-limit row is kept (a walker has at most
+ * 21, one side per hinge); contacts fill the remaining rows three at a time up to AS_MAX_CONTACTS, in
+ * priority order: feet on stones, other geoms on stones, robot self-contacts. */
+#define AS_MAX_CONTACTS 10
+#define AS_MAX_ROWS 30
 #define AS_OBS_DIM 59
 #define AS_ACT_DIM 21
 
@@ -71,6 +75,9 @@ typedef struct {
   float geom_p1[AS_MAX_GEOMS][3];
   int32_t torso_link;
   int32_t foot_link[2];
+  int32_t num_priority_geoms;         /* geoms [0, n) (the feet) emit their stone contacts first */
+  int32_t num_self_pairs;             /* self-collision geom pairs (walker3d.py:27 enabled_self_collisions) */
+  int32_t self_pair[AS_MAX_SELF_PAIRS]; /* g1 | g2 << 8, g1 < g2, ascending (model/__init__.py) */
 } as_model_t;
 
 /* Physics constants (simulation_cfg.py; walker3d.py:21-46; allsteps_env_cfg.py:62). */

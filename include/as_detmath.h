@@ -139,4 +139,71 @@ AS_HD void as_axis_angle_mat(const float* a, float ang, float* R) {
   R[6] = fmaf(tx, a[2], -(s * a[1])); R[7] = fmaf(ty, a[2], s * a[0]);   R[8] = fmaf(tz, a[2], c);
 }
 
+/* ---- robot self-collision (walker3d.py:27 enabled_self_collisions; shared by kernel and oracle) */
+
+AS_HD float as_clamp01(float x) { return fminf(fmaxf(x, 0.f), 1.f); }
+
+/* Pair filter: the bounding spheres (segment midpoint m, half length + radius R) of two geoms come
+ * within `margin`.  Conservative for the exact test below up to rounding; both sides apply it in the
+ * same arithmetic, so they keep the same pairs. */
+AS_HD int as_sphere_bound(const float* m1, float R1, const float* m2, float R2, float margin) {
+  const float d0 = m1[0] - m2[0], d1 = m1[1] - m2[1], d2 = m1[2] - m2[2];
+  const float lim = R1 + R2 + margin;
+  return d0 * d0 + d1 * d1 + d2 * d2 <= lim * lim;
+}
+
+/* Contact of two capsules (a sphere is a capsule with a == b): closest points of the segments
+ * [a1, b1] and [a2, b2] (Ericson, Real-Time Collision Detection, 5.1.9: s, t clamped to [0, 1]),
+ * separation |c1 - c2| - r1 - r2 (returned), unit normal n from geom 2 towards geom 1 (+z if the axes
+ * touch), contact point P midway between the two surfaces along n. */
+AS_HD float as_capsule_contact(const float* a1, const float* b1, float r1, const float* a2, const float* b2,
+                               float r2, float* P, float* n) {
+  float d1[3], d2[3], r[3];
+  for (int k = 0; k < 3; ++k) {
+    d1[k] = b1[k] - a1[k];
+    d2[k] = b2[k] - a2[k];
+    r[k] = a1[k] - a2[k];
+  }
+  const float a = as_dot3(d1, d1), e = as_dot3(d2, d2), f = as_dot3(d2, r);
+  const float eps = 1e-12f;
+  float s = 0.f, t = 0.f;
+  if (a <= eps) {
+    t = e <= eps ? 0.f : as_clamp01(f / e);
+  } else {
+    const float c = as_dot3(d1, r);
+    if (e <= eps) {
+      s = as_clamp01(-c / a);
+    } else {
+      const float b = as_dot3(d1, d2);
+      const float den = fmaf(a, e, -(b * b));
+      s = den > 0.f ? as_clamp01(fmaf(b, f, -(c * e)) / den) : 0.f;
+      t = fmaf(b, s, f) / e;
+      if (t < 0.f) {
+        t = 0.f;
+        s = as_clamp01(-c / a);
+      } else if (t > 1.f) {
+        t = 1.f;
+        s = as_clamp01((b - c) / a);
+      }
+    }
+  }
+  float c1[3], c2[3], w[3];
+  for (int k = 0; k < 3; ++k) {
+    c1[k] = fmaf(s, d1[k], a1[k]);
+    c2[k] = fmaf(t, d2[k], a2[k]);
+    w[k] = c1[k] - c2[k];
+  }
+  const float dist = sqrtf(as_dot3(w, w));
+  if (dist > 1e-9f) {
+    const float inv = 1.0f / dist;
+    n[0] = w[0] * inv; n[1] = w[1] * inv; n[2] = w[2] * inv;
+  } else {
+    n[0] = 0.f; n[1] = 0.f; n[2] = 1.f;
+  }
+  const float sep = dist - r1 - r2;
+  const float off = fmaf(0.5f, sep, r2);
+  for (int k = 0; k < 3; ++k) P[k] = fmaf(off, n[k], c2[k]);
+  return sep;
+}
+
 #endif /* AS_DETMATH_H */

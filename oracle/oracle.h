@@ -30,8 +30,16 @@ extern "C" {
 #define OR_MAX_GEOMS 32
 #define OR_MAX_STONES 20
 #define OR_NDOF_ROOT 6
-#define OR_MAX_CONTACTS 8
-#define OR_MAX_ROWS 24
+#define OR_MAX_SELF_PAIRS 256
+/* include/allsteps.h AS_MAX_CONTACTS / AS_MAX_ROWS: limits always kept, contacts fill the remaining
+ * rows (feet on stones, others, self).  Overridable only for the cap-sizing statistics build
+ * (scripts/contact_stats.py, -DOR_STATS), never for parity. */
+#ifndef OR_MAX_CONTACTS
+#define OR_MAX_CONTACTS 10
+#endif
+#ifndef OR_MAX_ROWS
+#define OR_MAX_ROWS 30
+#endif
 
 /* Model tables compiled from walker3d.xml (allsteps_isaaclab_amd/model/walker3d.json). */
 typedef struct {
@@ -59,6 +67,9 @@ typedef struct {
   float geom_p1[OR_MAX_GEOMS][3];
   int32_t torso_link;
   int32_t foot_link[2];              /* right, left */
+  int32_t num_priority_geoms;        /* geoms [0, n) emit their stone contacts first */
+  int32_t num_self_pairs;            /* self-collision pairs g1 | g2 << 8 (model/__init__.py) */
+  int32_t self_pair[OR_MAX_SELF_PAIRS];
 } or_model_t;
 
 /* Simulation constants (walker3d.py:21-46, simulation_cfg.py, allsteps_env_cfg.py:62). */
@@ -164,6 +175,12 @@ void or_bias_forces(const or_model_t* m, const float root_pos[3], const float ro
 void or_philox_uniform(uint64_t seed, uint32_t env, uint32_t episode, int k, float* out);
 /* every env's course at `level` from the Philox "Ston" stream of (seed, env, episode[e] or 0) */
 void or_stones_philox(const or_task_t* task, int n, int level, uint64_t seed, const uint32_t* episode, float* stones);
+
+#ifdef OR_STATS
+/* per-substep histograms (single-threaded runs): [0] contacts the narrowphase found (before the cap),
+ * [1] active joint-limit rows, [2] contacts kept, [3] self-contacts found */
+extern long long or_stats_hist[6][256]; /* [4]: self-contacts per pair index, [5]: pairs past the sphere filter */
+#endif
 
 #ifdef __cplusplus
 }

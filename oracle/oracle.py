@@ -16,7 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liballsteps_oracle.so")
 
-MAXL, MAXG = 32, 32
+MAXL, MAXG, MAXSP = 32, 32, 256
 f3 = C.c_float * 3
 
 
@@ -30,7 +30,8 @@ class OrModel(C.Structure):
         ("gear", C.c_float * MAXL), ("num_geoms", C.c_int32), ("geom_link", C.c_int32 * MAXG),
         ("geom_type", C.c_int32 * MAXG), ("geom_foot", C.c_int32 * MAXG), ("geom_radius", C.c_float * MAXG),
         ("geom_p0", (C.c_float * 3) * MAXG), ("geom_p1", (C.c_float * 3) * MAXG), ("torso_link", C.c_int32),
-        ("foot_link", C.c_int32 * 2),
+        ("foot_link", C.c_int32 * 2), ("num_priority_geoms", C.c_int32), ("num_self_pairs", C.c_int32),
+        ("self_pair", C.c_int32 * MAXSP),
     ]
 
 
@@ -138,6 +139,9 @@ def make_model(m: dict) -> OrModel:
         for i, row in enumerate(m[name]):
             arr[i][:] = [float(x) for x in row]
     M.num_geoms = m["num_geoms"]
+    M.num_priority_geoms = int(m["num_priority_geoms"])
+    M.num_self_pairs = int(m["num_self_pairs"])
+    M.self_pair[:] = [int(x) for x in m["self_pair"]]
     M.torso_link = int(m["torso_link"])
     M.foot_link[:] = [int(x) for x in m["foot_link"]]
     return M

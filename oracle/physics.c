@@ -383,39 +383,46 @@ static float sd_box(const float p[3], const float c[3], const float h[3], float 
   return d[ax];
 }
 
+#ifdef OR_STATS
+long long or_stats_hist[6][256];
+#endif
+
 typedef struct {
-  int n;
-  int link[OR_MAX_CONTACTS], stone[OR_MAX_CONTACTS], foot[OR_MAX_CONTACTS];
+  int n, tried, tried_self; /* tried: contacts found before the cap (statistics) */
+  int link[OR_MAX_CONTACTS], link2[OR_MAX_CONTACTS], stone[OR_MAX_CONTACTS], foot[OR_MAX_CONTACTS];
   float pt[OR_MAX_CONTACTS][3], nrm[OR_MAX_CONTACTS][3], sep[OR_MAX_CONTACTS];
 } contacts_t;
 
-static void add_contact(contacts_t* C, int link, int stone, int foot, const float P[3], const float nrm[3], float sep,
-                        float r) {
-  if (C->n >= OR_MAX_CONTACTS) return;
+/* link2 = -1 for a stone contact (the stone is kinematic), else the second robot link of a
+ * self-contact (stone = foot = -1), which takes the opposite impulse */
+static void add_contact(contacts_t* C, int ncap, int link, int link2, int stone, int foot, const float P[3],
+                        const float nrm[3], float sep, float r) {
+  C->tried++;
+  C->tried_self += stone < 0;
+  if (C->n >= ncap) return;
   int c = C->n++;
-  C->link[c] = link; C->stone[c] = stone; C->foot[c] = foot; C->sep[c] = sep;
+  C->link[c] = link; C->link2[c] = link2; C->stone[c] = stone; C->foot[c] = foot; C->sep[c] = sep;
   for (int k = 0; k < 3; ++k) { C->nrm[c][k] = nrm[k]; C->pt[c][k] = P[k] - nrm[k] * r; }
 }
 
 #define BISECT_ITERS 12
 
+/* Contacts of one substep, at most ncap, in priority order (the HIP kernel's collide() emits the same
+ * list):
+ *   1. the priority geoms (the feet, geoms [0, num_priority_geoms)) against the candidate stones,
+ *      stone-major (ascending), geom-minor;
+ *   2. every other geom against the candidate stones, stone-major, geom-minor;
+ *   3. robot self-contacts, one per self-collision pair in table order (model self_pair). */
 static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, const float* stones_rel, int nst,
-                    contacts_t* C) {
-  C->n = 0;
+                    int ncap, contacts_t* C) {
+  C->n = C->tried = C->tried_self = 0;
+#ifdef OR_STATS
+  ncap = OR_MAX_CONTACTS; /* find everything, keep ncap (below) */
+#endif
   const float* h = sim->stone_half;
-  /* broadphase: stones whose box is within 1.8 m of the root link origin (O) */
-  int cand[OR_MAX_STONES], nc = 0;
-  for (int s = 0; s < nst; ++s) {
-    const float* c = stones_rel + 3 * s;
-    float o = 0.f;
-    for (int k = 0; k < 3; ++k) {
-      float d = fabsf(c[k]) - h[k];
-      if (d > 0.f) o += d * d;
-    }
-    if (o < 1.8f * 1.8f) cand[nc++] = s;
-  }
-  /* geom segments in the O frame */
-  float ga[OR_MAX_GEOMS][3], gb[OR_MAX_GEOMS][3], gL[OR_MAX_GEOMS];
+  /* geom segments in the O frame, their midpoints / lengths, and the robot's bounding box */
+  float ga[OR_MAX_GEOMS][3], gb[OR_MAX_GEOMS][3], gL[OR_MAX_GEOMS], gm[OR_MAX_GEOMS][3];
+  float blo[3] = {1e30f, 1e30f, 1e30f}, bhi[3] = {-1e30f, -1e30f, -1e30f};
   for (int g = 0; g < m->num_geoms; ++g) {
     int l = m->geom_link[g];
     float t0[3], t1[3];
@@ -425,46 +432,88 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
     const float* a = ga[g];
     const float* b = gb[g];
     gL[g] = sqrtf((b[0] - a[0]) * (b[0] - a[0]) + (b[1] - a[1]) * (b[1] - a[1]) + (b[2] - a[2]) * (b[2] - a[2]));
-  }
-  /* narrowphase: candidate stones in ascending order, geoms in index order within a stone (the HIP
-   * kernel runs one geom per lane and loops over the candidates) */
-  for (int ci = 0; ci < nc; ++ci) {
-    int s = cand[ci];
-    const float* c = stones_rel + 3 * s;
-    for (int g = 0; g < m->num_geoms; ++g) {
-      int l = m->geom_link[g];
-      float r = m->geom_radius[g];
-      const float* a = ga[g];
-      const float* b = gb[g];
-      float L = gL[g];
-      float nr[3];
-      if (m->geom_type[g] == 0) {
-        float sd = sd_box(a, c, h, nr) - r;
-        if (sd < sim->margin) add_contact(C, l, s, m->geom_foot[g], a, nr, sd, r);
-        continue;
-      }
-      /* capsule: bounding test on the segment midpoint */
-      float mid[3] = {0.5f * (a[0] + b[0]), 0.5f * (a[1] + b[1]), 0.5f * (a[2] + b[2])};
-      if (sd_box(mid, c, h, nr) > 0.5f * L + r + sim->margin) continue;
-      float n0[3], n1[3];
-      float s0 = sd_box(a, c, h, n0) - r;
-      float s1 = sd_box(b, c, h, n1) - r;
-      /* minimum of the (convex) sd along the segment: bisection on the sign of its slope
-       * (sd_box_slope), BISECT_ITERS rounds, the HIP kernel's form */
-      float lo = 0.f, hi = 1.f;
-      for (int it = 0; it < BISECT_ITERS; ++it) {
-        const float t = 0.5f * (lo + hi);
-        if (sd_box_slope(a, b, t, c, h) > 0.f) hi = t; else lo = t;
-      }
-      float ts = 0.5f * (lo + hi), Ps[3], ns[3];
-      for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (b[k] - a[k]);
-      float ss = sd_box(Ps, c, h, ns) - r;
-      if (s0 < sim->margin) add_contact(C, l, s, m->geom_foot[g], a, n0, s0, r);
-      if (s1 < sim->margin) add_contact(C, l, s, m->geom_foot[g], b, n1, s1, r);
-      float smin = s0 < s1 ? s0 : s1;
-      if (ss < sim->margin && ss < smin - 0.002f) add_contact(C, l, s, m->geom_foot[g], Ps, ns, ss, r);
+    for (int k = 0; k < 3; ++k) gm[g][k] = 0.5f * (a[k] + b[k]);
+    const float r = m->geom_radius[g];
+    for (int k = 0; k < 3; ++k) {
+      const float e = m->geom_type[g] == 0 ? a[k] : fminf(a[k], b[k]);
+      const float f = m->geom_type[g] == 0 ? a[k] : fmaxf(a[k], b[k]);
+      blo[k] = fminf(blo[k], e - r);
+      bhi[k] = fmaxf(bhi[k], f + r);
     }
   }
+  /* broadphase: stones whose box comes within the margin of the robot's bounding box (conservative:
+   * every (stone, geom) pair the narrowphase would turn into a contact survives) */
+  int cand[OR_MAX_STONES], nc = 0;
+  for (int s = 0; s < nst; ++s) {
+    const float* c = stones_rel + 3 * s;
+    int in = 1;
+    for (int k = 0; k < 3; ++k)
+      in = in && (c[k] - h[k] <= bhi[k] + sim->margin) && (c[k] + h[k] >= blo[k] - sim->margin);
+    if (in) cand[nc++] = s;
+  }
+  const int npri = m->num_priority_geoms;
+  for (int cls = 0; cls < 2; ++cls) {
+    const int g0 = cls == 0 ? 0 : npri, g1 = cls == 0 ? npri : m->num_geoms;
+    for (int ci = 0; ci < nc && C->n < ncap; ++ci) {
+      int s = cand[ci];
+      const float* c = stones_rel + 3 * s;
+      for (int g = g0; g < g1; ++g) {
+        int l = m->geom_link[g];
+        float r = m->geom_radius[g];
+        const float* a = ga[g];
+        const float* b = gb[g];
+        float nr[3];
+        if (m->geom_type[g] == 0) {
+          float sd = sd_box(a, c, h, nr) - r;
+          if (sd < sim->margin) add_contact(C, ncap, l, -1, s, m->geom_foot[g], a, nr, sd, r);
+          continue;
+        }
+        /* capsule: bounding test on the segment midpoint */
+        float nm[3];
+        if (sd_box(gm[g], c, h, nm) > 0.5f * gL[g] + r + sim->margin) continue;
+        float n0[3], n1[3];
+        float s0 = sd_box(a, c, h, n0) - r;
+        float s1 = sd_box(b, c, h, n1) - r;
+        /* minimum of the (convex) sd along the segment: bisection on the sign of its slope
+         * (sd_box_slope), BISECT_ITERS rounds, the HIP kernel's form */
+        float lo = 0.f, hi = 1.f;
+        for (int it = 0; it < BISECT_ITERS; ++it) {
+          const float t = 0.5f * (lo + hi);
+          if (sd_box_slope(a, b, t, c, h) > 0.f) hi = t; else lo = t;
+        }
+        float ts = 0.5f * (lo + hi), Ps[3], ns[3];
+        for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (b[k] - a[k]);
+        float ss = sd_box(Ps, c, h, ns) - r;
+        if (s0 < sim->margin) add_contact(C, ncap, l, -1, s, m->geom_foot[g], a, n0, s0, r);
+        if (s1 < sim->margin) add_contact(C, ncap, l, -1, s, m->geom_foot[g], b, n1, s1, r);
+        float smin = s0 < s1 ? s0 : s1;
+        if (ss < sim->margin && ss < smin - 0.002f) add_contact(C, ncap, l, -1, s, m->geom_foot[g], Ps, ns, ss, r);
+      }
+    }
+  }
+  /* self-contacts: bounding-sphere filter, then the capsule-capsule closest points (as_detmath.h) */
+#ifdef OR_STATS
+  int nbound = 0;
+#endif
+  for (int p = 0; p < m->num_self_pairs && C->n < ncap; ++p) {
+    const int g1 = m->self_pair[p] & 0xff, g2 = m->self_pair[p] >> 8;
+    const float R1 = 0.5f * gL[g1] + m->geom_radius[g1], R2 = 0.5f * gL[g2] + m->geom_radius[g2];
+    if (!as_sphere_bound(gm[g1], R1, gm[g2], R2, sim->margin)) continue;
+#ifdef OR_STATS
+    nbound++;
+#endif
+    float P[3], n[3];
+    const float sep = as_capsule_contact(ga[g1], gb[g1], m->geom_radius[g1], ga[g2], gb[g2], m->geom_radius[g2], P, n);
+    if (sep < sim->margin) {
+#ifdef OR_STATS
+      or_stats_hist[4][p]++;
+#endif
+      add_contact(C, ncap, m->geom_link[g1], m->geom_link[g2], -1, -1, P, n, sep, 0.f);
+    }
+  }
+#ifdef OR_STATS
+  or_stats_hist[5][nbound < 255 ? nbound : 255]++;
+#endif
 }
 
 /* ---------------------------------------------------------------- one env step (decimation substeps) */
@@ -480,14 +529,25 @@ typedef struct {
   float lam[OR_MAX_ROWS];
 } rows_t;
 
-static void contact_row(const or_model_t* m, const kin_t* K, int link, const float P[3], const float d[3], float* J) {
+/* J_j = S_j . f6 (f6 = [P x d; d]) for the dofs on link's path, minus the same for link2's path (a
+ * self-contact's second body takes the opposite impulse; dofs on both paths cancel to 0) */
+static void contact_row(const or_model_t* m, const kin_t* K, int link, int link2, const float P[3], const float d[3],
+                        float* J) {
   float f6[6];
   cross(P, d, f6);
   f6[3] = d[0]; f6[4] = d[1]; f6[5] = d[2];
-  for (int j = 0; j < K->nv; ++j) J[j] = 0.f;
+  int on1[NV_MAX] = {0}, on2[NV_MAX] = {0};
   int chain[NV_MAX];
   int nc = chain_dofs(m, link, chain);
-  for (int t = 0; t < nc; ++t) J[chain[t]] = dot6(K->S[chain[t]], f6);
+  for (int t = 0; t < nc; ++t) on1[chain[t]] = 1;
+  if (link2 >= 0) {
+    nc = chain_dofs(m, link2, chain);
+    for (int t = 0; t < nc; ++t) on2[chain[t]] = 1;
+  }
+  for (int j = 0; j < K->nv; ++j) {
+    const float v = dot6(K->S[j], f6);
+    J[j] = (on1[j] ? v : 0.f) - (on2[j] ? v : 0.f);
+  }
 }
 
 static void tangents(const float n[3], float t1[3], float t2[3]) {
@@ -513,16 +573,38 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
   matvec_n(H, nv, b, acc);
   for (int j = 0; j < nv; ++j) u[j] = fmaf(dt, acc[j], u[j]);
 
-  /* constraints */
+  /* constraints: joint-limit rows first counted (all of them are kept), then the contacts fill the
+   * remaining rows; rows are ordered contacts (normal, tangent, tangent) then limits (hinge order,
+   * lower before upper) */
+  int lim_dof[OR_MAX_ROWS], lim_side[OR_MAX_ROWS], nlim = 0;
+  for (int i = 1; i <= nh; ++i) {
+    int j = OR_NDOF_ROOT + i - 1;
+    float qv = q_int[i - 1], pred = qv + dt * u[j];
+    for (int side = 0; side < 2; ++side) {
+      int viol = side == 0 ? pred < m->lower[i] : pred > m->upper[i];
+      if (!viol || nlim >= OR_MAX_ROWS) continue;
+      lim_dof[nlim] = i;
+      lim_side[nlim++] = side;
+    }
+  }
+  int ncap = (OR_MAX_ROWS - nlim) / 3;
+  if (ncap > OR_MAX_CONTACTS) ncap = OR_MAX_CONTACTS;
   float stones_rel[OR_MAX_STONES * 3];
   for (int s = 0; s < nst; ++s)
     for (int k = 0; k < 3; ++k) stones_rel[3 * s + k] = stones_w[3 * s + k] - root_pos[k];
   contacts_t Cn;
-  collide(m, sim, &K, stones_rel, nst, &Cn);
+  collide(m, sim, &K, stones_rel, nst, ncap, &Cn);
+#ifdef OR_STATS
+  or_stats_hist[0][Cn.tried < 255 ? Cn.tried : 255]++;
+  or_stats_hist[1][nlim]++;
+  or_stats_hist[3][Cn.tried_self < 255 ? Cn.tried_self : 255]++;
+  if (Cn.n > ncap) Cn.n = ncap;
+  or_stats_hist[2][Cn.n]++;
+#endif
   static __thread rows_t Rw;
   rows_t* R = &Rw;
   R->nrow = 0;
-  for (int c = 0; c < Cn.n && R->nrow + 3 <= OR_MAX_ROWS; ++c) {
+  for (int c = 0; c < Cn.n; ++c) {
     float t1[3], t2[3];
     tangents(Cn.nrm[c], t1, t2);
     const float* dirs[3] = {Cn.nrm[c], t1, t2};
@@ -530,7 +612,7 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
       int r = R->nrow++;
       R->type[r] = d == 0 ? 0 : 1;
       R->contact[r] = c;
-      contact_row(m, &K, Cn.link[c], Cn.pt[c], dirs[d], R->J[r]);
+      contact_row(m, &K, Cn.link[c], Cn.link2[c], Cn.pt[c], dirs[d], R->J[r]);
       float s = Cn.sep[c];
       if (d == 0)
         R->target[r] = s < 0.f ? fminf(sim->baumgarte * fmaxf(-s - sim->slop, 0.f) / dt, sim->max_depen_vel)
@@ -539,20 +621,16 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
         R->target[r] = 0.f;
     }
   }
-  for (int i = 1; i <= nh && R->nrow < OR_MAX_ROWS; ++i) {
-    int j = OR_NDOF_ROOT + i - 1;
-    float qv = q_int[i - 1], pred = qv + dt * u[j];
-    for (int side = 0; side < 2 && R->nrow < OR_MAX_ROWS; ++side) {
-      float err = side == 0 ? m->lower[i] - qv : qv - m->upper[i];
-      int viol = side == 0 ? pred < m->lower[i] : pred > m->upper[i];
-      if (!viol) continue;
-      int r = R->nrow++;
-      R->type[r] = 2;
-      R->contact[r] = -1;
-      for (int k = 0; k < nv; ++k) R->J[r][k] = 0.f;
-      R->J[r][j] = side == 0 ? 1.f : -1.f;
-      R->target[r] = err > 0.f ? fminf(sim->baumgarte * err / dt, sim->max_depen_vel) : err / dt;
-    }
+  for (int l = 0; l < nlim; ++l) {
+    const int i = lim_dof[l], side = lim_side[l], j = OR_NDOF_ROOT + i - 1;
+    const float qv = q_int[i - 1];
+    float err = side == 0 ? m->lower[i] - qv : qv - m->upper[i];
+    int r = R->nrow++;
+    R->type[r] = 2;
+    R->contact[r] = -1;
+    for (int k = 0; k < nv; ++k) R->J[r][k] = 0.f;
+    R->J[r][j] = side == 0 ? 1.f : -1.f;
+    R->target[r] = err > 0.f ? fminf(sim->baumgarte * err / dt, sim->max_depen_vel) : err / dt;
   }
   /* W_r = H^-1 J_r^T: per entry two interleaved partial sums (even / odd k, fmaf chains), added at
    * the end; the projections A_rr = J_r . W_r and the in-triplet couplings A_sr = J_s . W_r
@@ -628,9 +706,8 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
   mask[0] = mask[1] = 0u;
   for (int c = 0; c < Cn.n; ++c) {
     if (Cn.foot[c] < 0) continue;
-    if (3 * c >= R->nrow) break;
     float fx = 0.f, fy = 0.f, fz = 0.f;
-    for (int c2 = 0; c2 < Cn.n && 3 * c2 < R->nrow; ++c2) {
+    for (int c2 = 0; c2 < Cn.n; ++c2) {
       if (Cn.foot[c2] != Cn.foot[c] || Cn.stone[c2] != Cn.stone[c]) continue;
       float l = R->lam[3 * c2];
       fx += l * Cn.nrm[c2][0]; fy += l * Cn.nrm[c2][1]; fz += l * Cn.nrm[c2][2];

@@ -47,11 +47,17 @@ def launch_summary(r, top=6):
     return out
 
 
-def main(n=4096, steps=30, warm=10):
+def main(n=4096, steps=30, warm=10, no_self=False):
     cfg = AllstepsEnvCfg()
     cfg.scene.num_envs = n
     cfg.sim.device = "cuda:0"
-    env = AllstepsEnv(cfg)
+    model = None
+    if no_self:  # ablation: the same kernel without self-collision pairs
+        from allsteps_isaaclab_amd.model import load_model
+
+        model = load_model()
+        model["num_self_pairs"] = 0
+    env = AllstepsEnv(cfg, model=model)
     env.reset()
     gen = torch.Generator(device="cuda").manual_seed(0)
     acts = torch.rand(steps + warm, n, 21, device="cuda", generator=gen) * 2 - 1
@@ -75,7 +81,7 @@ def main(n=4096, steps=30, warm=10):
     per = {PHASES[k]: int(ph[:, :, k].mean()) for k in range(NP)}
     s = max(sum(per.values()), 1)
     print(json.dumps({
-        "n": n, "launches": steps, "cycles_per_wave_step": s,
+        "n": n, "no_self": no_self, "launches": steps, "cycles_per_wave_step": s,
         "max_wave_step_total_mean": int(tot.max(axis=1).mean()), "max_wave_step_total": int(tot.max()),
         "total_pct": {q: int(np.percentile(tot, q)) for q in (10, 50, 90, 99)},
         "corr_total_rows": round(float(np.corrcoef(tot.ravel(), rows)[0, 1]), 3),
@@ -87,5 +93,5 @@ def main(n=4096, steps=30, warm=10):
 
 
 if __name__ == "__main__":
-    main()
-    main(n=512)
+    main(no_self="noself" in sys.argv[1:])
+    main(n=512, no_self="noself" in sys.argv[1:])

@@ -41,7 +41,9 @@ def _worker(rank: int, world: int, port: int, q):
             res = gather.gather(_rank_rollout(rank))
         fake_env = types.SimpleNamespace(curr_target_index=torch.full((6,), 1 + 3 * rank, dtype=torch.int32))
         mean = global_curriculum_mean(fake_env)
-        q.put((rank, info.rank, info.world, {k: v.clone() for k, v in res.items()}, mean))
+        # numpy copies travel by value: torch tensors would be shared through /dev/shm files that vanish
+        # when this process exits before the parent unpickles them
+        q.put((rank, info.rank, info.world, {k: v.numpy().copy() for k, v in res.items()}, mean))
     finally:
         dist.destroy_process_group()
 
@@ -59,6 +61,7 @@ def test_rollout_gather_world2():
         assert p.exitcode == 0
     expect = {k: torch.cat([_rank_rollout(r)[k] for r in range(world)], dim=1) for k in _rank_rollout(0)}
     for rank, info_rank, info_world, res, mean in out:
+        res = {k: torch.from_numpy(v) for k, v in res.items()}
         assert info_rank == rank and info_world == world
         for k, v in expect.items():
             assert res[k].dtype == v.dtype and res[k].shape == v.shape, k
