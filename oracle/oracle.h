@@ -176,6 +176,28 @@ void or_philox_uniform(uint64_t seed, uint32_t env, uint32_t episode, int k, flo
 /* every env's course at `level` from the Philox "Ston" stream of (seed, env, episode[e] or 0) */
 void or_stones_philox(const or_task_t* task, int n, int level, uint64_t seed, const uint32_t* episode, float* stones);
 
+/* ---- known-answer probe: the constraint set and contact impulses of ONE substep ---- */
+typedef struct {
+  int32_t nfound;       /* contacts the narrowphase finds (no cap, no early exit) */
+  int32_t nself_found;  /* of which robot self-contacts */
+  int32_t ncap;         /* contact budget left by the limit rows: min(MAX_CONTACTS, (MAX_ROWS - nlim) / 3) */
+  int32_t nlim;         /* joint-limit rows (all kept) */
+  int32_t ncontact;     /* contacts kept */
+  int32_t link[OR_MAX_CONTACTS], link2[OR_MAX_CONTACTS], stone[OR_MAX_CONTACTS], foot[OR_MAX_CONTACTS];
+  float sep[OR_MAX_CONTACTS], nrm[OR_MAX_CONTACTS][3];
+  float lam_n[OR_MAX_CONTACTS]; /* normal impulse after the PGS sweeps (force = lam_n / dt) */
+  uint32_t mask[2];             /* contact-sensor bits of this substep */
+  /* over ALL substeps of the env step: stone contact impulses summed per stone and in total (the
+   * environment's push on the robot; self-contacts are internal and excluded) */
+  float stone_impulse[OR_MAX_STONES][3];
+  float net_impulse[3];
+  int32_t recorded;             /* internal: the first substep has been recorded */
+} or_probe_t;
+/* Run one env step's physics (all substeps) of env e (act_clamped in cfg order) on a copy of its
+ * state and report its first substep plus the impulse sums; `st` is not modified. */
+void or_probe_substep(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_state_t* st, int e,
+                      const float* act_clamped, or_probe_t* out);
+
 #ifdef OR_STATS
 /* per-substep histograms (single-threaded runs): [0] contacts the narrowphase found (before the cap),
  * [1] active joint-limit rows, [2] contacts kept, [3] self-contacts found */

@@ -56,6 +56,19 @@ class OrTask(C.Structure):
     ]
 
 
+MAXC = 10  # oracle.h OR_MAX_CONTACTS
+
+
+class OrProbe(C.Structure):
+    _fields_ = [
+        ("nfound", C.c_int32), ("nself_found", C.c_int32), ("ncap", C.c_int32), ("nlim", C.c_int32),
+        ("ncontact", C.c_int32), ("link", C.c_int32 * MAXC), ("link2", C.c_int32 * MAXC),
+        ("stone", C.c_int32 * MAXC), ("foot", C.c_int32 * MAXC), ("sep", C.c_float * MAXC),
+        ("nrm", (C.c_float * 3) * MAXC), ("lam_n", C.c_float * MAXC), ("mask", C.c_uint32 * 2),
+        ("stone_impulse", (C.c_float * 3) * 20), ("net_impulse", C.c_float * 3), ("recorded", C.c_int32),
+    ]
+
+
 FP = C.POINTER(C.c_float)
 IP = C.POINTER(C.c_int32)
 UP = C.POINTER(C.c_uint32)
@@ -101,6 +114,7 @@ def lib() -> C.CDLL:
         L.or_bias_forces.argtypes = [V, FP, FP, FP, FP, C.c_float, FP]
         L.or_philox_uniform.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, FP]
         L.or_physics_step.argtypes = [V, V, V, V, C.c_int, FP]
+        L.or_probe_substep.argtypes = [V, V, V, V, C.c_int, FP, V]
     return _LIB
 
 
@@ -281,6 +295,23 @@ class Oracle:
         for e in range(st.n):
             row = np.ascontiguousarray(a[e])
             self.L.or_physics_step(C.byref(self.model), C.byref(self.sim), C.byref(self.task), st.ptr, e, fp(row))
+
+    def probe(self, st: OracleState, e: int = 0, actions=None) -> dict:
+        """The constraint set and contact impulses of env e's first substep, plus the stone impulses
+        summed over the env step's substeps (or_probe_substep); the state is not advanced."""
+        nh = self.m["num_hinges"]
+        a = np.zeros(nh, np.float32) if actions is None else np.clip(np.asarray(actions, np.float32), -1, 1)
+        P = OrProbe()
+        self.L.or_probe_substep(C.byref(self.model), C.byref(self.sim), C.byref(self.task), st.ptr, e,
+                                fp(np.ascontiguousarray(a)), C.byref(P))
+        k = P.ncontact
+        return {"nfound": P.nfound, "nself_found": P.nself_found, "ncap": P.ncap, "nlim": P.nlim, "ncontact": k,
+                "link": np.array(P.link[:k]), "link2": np.array(P.link2[:k]), "stone": np.array(P.stone[:k]),
+                "foot": np.array(P.foot[:k]), "sep": np.array(P.sep[:k], np.float32),
+                "nrm": np.array([list(P.nrm[c]) for c in range(k)], np.float32).reshape(k, 3),
+                "lam_n": np.array(P.lam_n[:k], np.float32), "mask": (P.mask[0], P.mask[1]),
+                "stone_impulse": np.array([list(P.stone_impulse[s]) for s in range(20)], np.float32),
+                "net_impulse": np.array(list(P.net_impulse), np.float32)}
 
     def reset_all(self, st: OracleState, seed: int = 42, reset_draws=None):
         obs = np.zeros((st.n, 59), np.float32)

@@ -387,8 +387,10 @@ static float sd_box(const float p[3], const float c[3], const float h[3], float 
 long long or_stats_hist[6][256];
 #endif
 
+static __thread or_probe_t* g_probe; /* or_probe_substep: record this substep, find every contact */
+
 typedef struct {
-  int n, tried, tried_self; /* tried: contacts found before the cap (statistics) */
+  int n, tried, tried_self; /* tried: contacts found before the cap (statistics, probe) */
   int link[OR_MAX_CONTACTS], link2[OR_MAX_CONTACTS], stone[OR_MAX_CONTACTS], foot[OR_MAX_CONTACTS];
   float pt[OR_MAX_CONTACTS][3], nrm[OR_MAX_CONTACTS][3], sep[OR_MAX_CONTACTS];
 } contacts_t;
@@ -419,6 +421,9 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
 #ifdef OR_STATS
   ncap = OR_MAX_CONTACTS; /* find everything, keep ncap (below) */
 #endif
+  const int keep = ncap;          /* add_contact keeps ncap; the loops stop there unless probing */
+  if (g_probe) ncap = 1 << 30;
+
   const float* h = sim->stone_half;
   /* geom segments in the O frame, their midpoints / lengths, and the robot's bounding box */
   float ga[OR_MAX_GEOMS][3], gb[OR_MAX_GEOMS][3], gL[OR_MAX_GEOMS], gm[OR_MAX_GEOMS][3];
@@ -465,7 +470,7 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
         float nr[3];
         if (m->geom_type[g] == 0) {
           float sd = sd_box(a, c, h, nr) - r;
-          if (sd < sim->margin) add_contact(C, ncap, l, -1, s, m->geom_foot[g], a, nr, sd, r);
+          if (sd < sim->margin) add_contact(C, keep, l, -1, s, m->geom_foot[g], a, nr, sd, r);
           continue;
         }
         /* capsule: bounding test on the segment midpoint */
@@ -484,10 +489,10 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
         float ts = 0.5f * (lo + hi), Ps[3], ns[3];
         for (int k = 0; k < 3; ++k) Ps[k] = a[k] + ts * (b[k] - a[k]);
         float ss = sd_box(Ps, c, h, ns) - r;
-        if (s0 < sim->margin) add_contact(C, ncap, l, -1, s, m->geom_foot[g], a, n0, s0, r);
-        if (s1 < sim->margin) add_contact(C, ncap, l, -1, s, m->geom_foot[g], b, n1, s1, r);
+        if (s0 < sim->margin) add_contact(C, keep, l, -1, s, m->geom_foot[g], a, n0, s0, r);
+        if (s1 < sim->margin) add_contact(C, keep, l, -1, s, m->geom_foot[g], b, n1, s1, r);
         float smin = s0 < s1 ? s0 : s1;
-        if (ss < sim->margin && ss < smin - 0.002f) add_contact(C, ncap, l, -1, s, m->geom_foot[g], Ps, ns, ss, r);
+        if (ss < sim->margin && ss < smin - 0.002f) add_contact(C, keep, l, -1, s, m->geom_foot[g], Ps, ns, ss, r);
       }
     }
   }
@@ -508,7 +513,7 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
 #ifdef OR_STATS
       or_stats_hist[4][p]++;
 #endif
-      add_contact(C, ncap, m->geom_link[g1], m->geom_link[g2], -1, -1, P, n, sep, 0.f);
+      add_contact(C, keep, m->geom_link[g1], m->geom_link[g2], -1, -1, P, n, sep, 0.f);
     }
   }
 #ifdef OR_STATS
@@ -594,6 +599,15 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
     for (int k = 0; k < 3; ++k) stones_rel[3 * s + k] = stones_w[3 * s + k] - root_pos[k];
   contacts_t Cn;
   collide(m, sim, &K, stones_rel, nst, ncap, &Cn);
+  if (g_probe && !g_probe->recorded) {
+    or_probe_t* P = g_probe;
+    P->nfound = Cn.tried; P->nself_found = Cn.tried_self; P->ncap = ncap; P->nlim = nlim; P->ncontact = Cn.n;
+    for (int c = 0; c < Cn.n; ++c) {
+      P->link[c] = Cn.link[c]; P->link2[c] = Cn.link2[c]; P->stone[c] = Cn.stone[c]; P->foot[c] = Cn.foot[c];
+      P->sep[c] = Cn.sep[c];
+      for (int k = 0; k < 3; ++k) P->nrm[c][k] = Cn.nrm[c][k];
+    }
+  }
 #ifdef OR_STATS
   or_stats_hist[0][Cn.tried < 255 ? Cn.tried : 255]++;
   or_stats_hist[1][nlim]++;
@@ -715,6 +729,22 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
     float fn = sqrtf(fx * fx + fy * fy + fz * fz) / dt;
     if (fn > 1e-4f) mask[Cn.foot[c]] |= 1u << Cn.stone[c];
   }
+  if (g_probe) {
+    or_probe_t* P = g_probe;
+    if (!P->recorded) {
+      for (int c = 0; c < Cn.n; ++c) P->lam_n[c] = R->lam[3 * c];
+      P->mask[0] = mask[0];
+      P->mask[1] = mask[1];
+      P->recorded = 1;
+    }
+    for (int c = 0; c < Cn.n; ++c) {
+      if (Cn.stone[c] < 0) continue;
+      for (int k = 0; k < 3; ++k) {
+        P->stone_impulse[Cn.stone[c]][k] += R->lam[3 * c] * Cn.nrm[c][k];
+        P->net_impulse[k] += R->lam[3 * c] * Cn.nrm[c][k];
+      }
+    }
+  }
   /* clamp joint speeds, integrate */
   for (int i = 0; i < nh; ++i) {
     float* v = &u[OR_NDOF_ROOT + i];
@@ -799,6 +829,31 @@ void or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* 
 }
 
 /* ---------------------------------------------------------------- env-level API */
+
+void or_probe_substep(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_state_t* st, int e,
+                      const float* act_clamped, or_probe_t* out) {
+  /* the env's state as or_physics_step loads it, one substep, nothing written back */
+  const int n = st->n, nh = m->num_hinges;
+  float rp[3], rq[4], q_int[OR_MAX_LINKS], u[NV_MAX], tau[OR_MAX_LINKS], stones[OR_MAX_STONES * 3];
+  for (int k = 0; k < 3; ++k) rp[k] = F(st->root_pos, k, n, e);
+  for (int k = 0; k < 4; ++k) rq[k] = F(st->root_quat, k, n, e);
+  for (int k = 0; k < 3; ++k) { u[k] = F(st->root_lin, k, n, e); u[3 + k] = F(st->root_ang, k, n, e); }
+  float gain = task->gain_curriculum[st->curriculum[0]];
+  for (int k = 0; k < nh; ++k) {
+    int i = m->cfg_dof_link[k] - 1;
+    q_int[i] = F(st->q, k, n, e);
+    u[OR_NDOF_ROOT + i] = F(st->qd, k, n, e);
+    tau[i] = gain * m->gear[k] * act_clamped[k];
+  }
+  const int nst = task->num_steps;
+  for (int s = 0; s < nst; ++s)
+    for (int k = 0; k < 3; ++k) stones[3 * s + k] = F(st->stones, s * 3 + k, n, e);
+  memset(out, 0, sizeof(*out));
+  uint32_t mask[2] = {0u, 0u};
+  g_probe = out;
+  for (int sub = 0; sub < sim->substeps; ++sub) substep(m, sim, rp, rq, q_int, u, tau, stones, nst, mask);
+  g_probe = NULL;
+}
 
 void or_env_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
                  const float* actions, const float* reset_draws, uint64_t seed, float* obs, float* rew,

@@ -1,0 +1,104 @@
+"""HIP kernels on the constraint-budget states and the physics known-answer models (-m gpu).
+
+* the walker fixtures of tests/golden/constraint_states.npz (self-contact arm, crowded feet, fallen
+  with limit rows), 64 envs each with per-env random actions: every state field and contact flag
+  bit-identical to the oracle after each of 5 physics steps;
+* the pendulum and the resting / falling / wedged spheres of tests/test_oracle_kats.py (padded to 21
+  hinges, tests/_models.py): the same known answers on the GPU, bit-identical to the oracle.
+"""
+
+import numpy as np
+import pytest
+
+from _models import (GpuPhysics, PEND_ROOT, STONE_TOP, constraint_fixture, level0_stones, pendulum_model,
+                     put_oracle, sphere_model)
+from test_oracle_kats import check_pendulum, pendulum_series
+
+pytestmark = pytest.mark.gpu
+
+FLOAT_FIELDS = ("root_pos", "root_quat", "root_lin", "root_ang", "q", "qd", "body_pos")
+
+
+def _assert_same(g, st, what):
+    for k in FLOAT_FIELDS:
+        assert np.array_equal(g[k], st[k]), (what, k, np.abs(g[k] - st[k]).max())
+    assert np.array_equal(g["contact_mask"].view(np.uint32), st["contact_mask"]), (what, "contact_mask")
+
+
+@pytest.mark.parametrize("name", ["self_arm", "crowded", "fallen"])
+def test_constraint_states_bit_exact(orc, name):
+    n, steps = 64, 5
+    snap = constraint_fixture(name)
+    st = orc.state(n)
+    for e in range(n):
+        put_oracle(st, snap, e)
+    gpu = GpuPhysics(orc.m, n)
+    gpu.load_oracle(st)
+    rng = np.random.default_rng(3)
+    for t in range(steps):
+        act = rng.uniform(-1, 1, (n, 21)).astype(np.float32)
+        act[0] = 0.0  # env 0: the fixture's own motion
+        gpu.step(act)
+        orc.physics_step(st, act)
+        _assert_same(gpu.get(), st, f"{name} step {t}")
+    if name == "self_arm":  # the self-contact pushed the arm out of the torso on the GPU as well
+        q_arm = [orc.m["dof_names"].index(k) for k in ("right_shoulder_x", "right_shoulder_y", "right_shoulder_z",
+                                                        "right_elbow")]
+        assert np.abs(gpu.get()["q"][q_arm, 0] - snap["q"][q_arm]).max() > 1e-3
+    gpu.close()
+
+
+def test_pendulum_gpu(oracle_mod):
+    theta0 = 0.3
+    m = pendulum_model()
+    orc = oracle_mod.Oracle(model=m)
+    st = orc.state(1)
+    st["stones"][:] = level0_stones(1)
+    st["root_pos"][:, 0] = PEND_ROOT
+    st["q"][0, 0] = theta0
+    gpu = GpuPhysics(m, 1)
+    gpu.load_oracle(st)
+    act = np.zeros((1, 21), np.float32)
+    s = {}
+
+    def step():
+        gpu.step(act)
+        s.update(gpu.get())
+        orc.physics_step(st, act)
+        _assert_same(s, st, "pendulum")
+
+    class View:  # pendulum_series reads the GPU state after each step
+        def __getitem__(self, k):
+            return s[k]
+
+    q, qd, root = pendulum_series(step, View(), 240)
+    check_pendulum(q, qd, root, theta0)
+    assert s["contact_mask"][0, 0] == 1 << 2 and s["contact_mask"][1, 0] == 0
+    gpu.close()
+
+
+@pytest.mark.parametrize("case", ["resting", "falling", "wedged"])
+def test_sphere_flags_gpu(oracle_mod, case):
+    r = 0.2 if case == "wedged" else 0.1
+    m, _ = sphere_model(r)
+    orc = oracle_mod.Oracle(model=m)
+    st = orc.state(1)
+    st["stones"][:] = level0_stones(1)
+    pos = {"resting": [0.75 * 3 + 0.05, 0.1, STONE_TOP + 0.1 + 0.02],
+           "falling": [0.75 * 3 + 0.05, 0.1, STONE_TOP + 0.1 + 0.5],
+           "wedged": [0.75 * 3 + 0.375, 0.0, STONE_TOP + 0.16]}[case]
+    st["root_pos"][:, 0] = pos
+    gpu = GpuPhysics(m, 1)
+    gpu.load_oracle(st)
+    act = np.zeros((1, 21), np.float32)
+    steps = {"resting": 60, "falling": 5, "wedged": 90}[case]
+    for _ in range(steps):
+        gpu.step(act)
+        orc.physics_step(st, act)
+        g = gpu.get()
+        _assert_same(g, st, case)
+        if case == "falling":
+            assert g["contact_mask"][:, 0].tolist() == [0, 0]
+    want = {"resting": 1 << 3, "falling": 0, "wedged": (1 << 3) | (1 << 4)}[case]
+    assert int(g["contact_mask"][0, 0]) == want and int(g["contact_mask"][1, 0]) == 0
+    gpu.close()
