@@ -1,0 +1,48 @@
+"""Shim of ``isaaclab_tasks.utils.hydra.hydra_task_config`` without hydra (absent offline): the
+decorated ``main(env_cfg, agent_cfg)`` receives the task's registry configs with the command line's
+hydra-style overrides applied (``env.<path>=<value>`` / ``agent.<path>=<value>``, values parsed as
+YAML scalars), which is how Isaac Lab's hydra integration addresses the two configs."""
+
+from __future__ import annotations
+
+import functools
+import sys
+
+from allsteps_isaaclab_amd.registry import load_cfg_from_registry
+
+
+def _set(obj, path: list[str], value) -> None:
+    for k in path[:-1]:
+        obj = obj[k] if isinstance(obj, dict) else getattr(obj, k)
+    if isinstance(obj, dict):
+        obj[path[-1]] = value
+    else:
+        setattr(obj, path[-1], value)
+
+
+def apply_overrides(env_cfg, agent_cfg, overrides: list[str]) -> None:
+    import yaml
+
+    for ov in overrides:
+        key, sep, val = ov.partition("=")
+        if not sep or "." not in key:
+            raise ValueError(f"unsupported override {ov!r} (expected env.<path>=<value> or agent.<path>=<value>)")
+        root, *path = key.lstrip("+").split(".")
+        target = {"env": env_cfg, "agent": agent_cfg}.get(root)
+        if target is None:
+            raise ValueError(f"override {ov!r} must start with env. or agent.")
+        _set(target, path, yaml.safe_load(val))
+
+
+def hydra_task_config(task_name: str, agent_cfg_entry_point: str):
+    def decorator(func):
+        @functools.wraps(func)
+        def wrapper(*args, **kwargs):
+            env_cfg = load_cfg_from_registry(task_name, "env_cfg_entry_point")
+            agent_cfg = load_cfg_from_registry(task_name, agent_cfg_entry_point)
+            apply_overrides(env_cfg, agent_cfg, [a for a in sys.argv[1:] if "=" in a and not a.startswith("-")])
+            return func(env_cfg, agent_cfg, *args, **kwargs)
+
+        return wrapper
+
+    return decorator

@@ -242,18 +242,19 @@ __device__ __forceinline__ float half_max(float v) {
 // With p[kWaveRecFlag] != 0 each wave also writes a record of its own (the last launch's waves:
 // phase cycles, total, start / end time, HW_ID / XCC_ID, rows and contacts summed over substeps per
 // env) at p + kWaveRecBase + block * kWaveRecWords, for tail analysis (scripts/stamps.py).
-constexpr int kWaveRecFlag = 31, kWaveRecBase = 64, kWaveRecWords = 24;
-static_assert(16 + kNumStamps <= kWaveRecFlag && kNumStamps + 9 <= kWaveRecWords, "stamp slots");
+constexpr int kWaveRecFlag = 31, kWaveRecBase = 64, kWaveRecWords = 26;
+static_assert(16 + kNumStamps <= kWaveRecFlag && kNumStamps + 11 <= kWaveRecWords, "stamp slots");
 struct Stamp {
   unsigned long long* p;
   unsigned long long* acc;  // LDS, kNumStamps
   unsigned long long t;
-  unsigned long long t0 = 0ull;
+  unsigned long long t0 = 0ull, rt0 = 0ull;  // s_memtime / s_memrealtime (100 MHz) at the start
   unsigned rows = 0u, cons = 0u;
   __device__ void start() {
     if (p) {
       if (threadIdx.x < kNumStamps) acc[threadIdx.x] = 0ull;
       t = t0 = __builtin_amdgcn_s_memtime();
+      rt0 = __builtin_amdgcn_s_memrealtime();
     }
   }
   __device__ void count(int nrow, int nc) {
@@ -285,6 +286,7 @@ struct Stamp {
         if (k < kNumStamps) rec[k] = acc[k];
         if (k == 0) {
           rec[kNumStamps] = tot; rec[kNumStamps + 1] = t0; rec[kNumStamps + 2] = now;
+          rec[kNumStamps + 9] = rt0; rec[kNumStamps + 10] = __builtin_amdgcn_s_memrealtime();
           rec[kNumStamps + 3] = hw; rec[kNumStamps + 4] = xcc;
           rec[kNumStamps + 5] = rows; rec[kNumStamps + 7] = cons;
         }

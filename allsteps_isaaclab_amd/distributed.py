@@ -37,12 +37,22 @@ class ShardInfo:
         return base_seed + self.rank
 
 
+def _local_device(local: int) -> int:
+    """The device index of a local rank: itself, except in the shared-GPU rehearsal
+    (ALLSTEPS_DIST_BACKEND=gloo: more ranks than GPUs), where ranks wrap onto the visible devices as
+    bench.py maps them."""
+    if os.environ.get("ALLSTEPS_DIST_BACKEND") == "gloo" and torch.cuda.is_available():
+        return local % max(torch.cuda.device_count(), 1)
+    return local
+
+
 def shard_info() -> ShardInfo:
-    """Rank / world / local rank from torch.distributed (or the launcher's environment)."""
+    """Rank / world / local rank (device index) from torch.distributed (or the launcher's environment)."""
     if dist.is_available() and dist.is_initialized():
-        return ShardInfo(dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", dist.get_rank())))
+        return ShardInfo(dist.get_rank(), dist.get_world_size(),
+                         _local_device(int(os.environ.get("LOCAL_RANK", dist.get_rank()))))
     return ShardInfo(int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
-                     int(os.environ.get("LOCAL_RANK", 0)))
+                     _local_device(int(os.environ.get("LOCAL_RANK", 0))))
 
 
 def init_process_group(backend: str | None = None) -> ShardInfo:

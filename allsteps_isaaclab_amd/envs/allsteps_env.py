@@ -99,9 +99,10 @@ class AllstepsEnv(DirectRLEnv):
                  env_id_offset: int = 0, model: dict | None = None, **kwargs):
         cfg = cfg if cfg is not None else AllstepsEnvCfg()
         super().__init__(cfg, render_mode, **kwargs)
-        if self._device.type != "cuda":
+        if self._device.type != "cuda" or not torch.cuda.is_available():
             raise _native.NativeError(
-                f"AllstepsEnv runs on the HIP backend only (device={self._device}); there is no CPU fallback")
+                f"AllstepsEnv runs on the HIP backend only (device={self._device}, HIP device available: "
+                f"{torch.cuda.is_available()}); there is no CPU fallback")
         self.model = model if model is not None else load_model()
         n = self.num_envs
         dev = self._device

@@ -37,6 +37,8 @@ def register(id: str, entry_point: str, disable_env_checker: bool = True, kwargs
     try:  # pragma: no cover - gymnasium absent in this image
         import gymnasium
 
+        if getattr(gymnasium, "ALLSTEPS_COMPAT", False):  # the opt-in shim (compat/site) IS this registry
+            return
         if id not in gymnasium.registry:
             gymnasium.register(id=id, entry_point=entry_point, disable_env_checker=disable_env_checker,
                                kwargs=dict(kwargs or {}))

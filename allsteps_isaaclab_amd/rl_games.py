@@ -20,38 +20,17 @@ from .envs.direct_rl_env import DirectRLEnv
 from .envs.spaces import Box
 
 try:  # pragma: no cover - depends on the image
+    import rl_games as _rlg  # type: ignore
+
+    if getattr(_rlg, "ALLSTEPS_COMPAT", False):  # our own opt-in shim (compat/site/rl_games)
+        raise ImportError
     from rl_games.common import env_configurations, vecenv  # type: ignore
     from rl_games.common.vecenv import IVecEnv  # type: ignore
 
     HAVE_RL_GAMES = True
-except Exception:  # rl_games absent: minimal stand-ins
+except Exception:  # rl_games absent: the stand-ins of _vecenv
     HAVE_RL_GAMES = False
-
-    class IVecEnv:  # noqa: D101 - rl_games.common.ivecenv.IVecEnv surface
-        pass
-
-    class _Configurations:
-        def __init__(self):
-            self.configurations: dict[str, dict] = {}
-
-        def register(self, name: str, config: dict):
-            self.configurations[name] = config
-
-    class _VecEnvRegistry:
-        """rl_games.common.vecenv: ``register(type_name, creator)`` / ``create_vec_env(config_name, n)``."""
-
-        def __init__(self):
-            self.vecenv_config: dict = {}
-
-        def register(self, config_name: str, func) -> None:
-            self.vecenv_config[config_name] = func
-
-        def create_vec_env(self, config_name: str, num_actors: int, **kwargs):
-            vec_env_name = env_configurations.configurations[config_name]["vecenv_type"]
-            return self.vecenv_config[vec_env_name](config_name, num_actors, **kwargs)
-
-    env_configurations = _Configurations()
-    vecenv = _VecEnvRegistry()
+    from ._vecenv import IVecEnv, env_configurations, vecenv
 
 
 class RlGamesVecEnvWrapper(IVecEnv):

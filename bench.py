@@ -12,12 +12,15 @@ scaling, no collective in the step).  value = all ranks' env-steps / max-over-ra
 Extra objects on the JSON line:
   roofline     -- k_step (the dominant kernel): algorithmic bytes per launch / its average duration
                   from HIP events recorded around every 10th launch of the timed region on its own
-                  stream (events on every launch would add their own launch gaps), vs 8 TB/s HBM.
+                  stream (events on every launch would add their own launch gaps), vs 8 TB/s HBM;
+                  `latency`: per-wave cycle records of 20 launches after the timed region (mean /
+                  slowest wave vs the launch span, the slowest wave's phases: scripts/stamps.py).
   cpu_baseline -- rank 0, N = 1: the CPU oracle (oracle/, a port of the same step) timed on this
                   host's cores on a bounded sample.
-  train        -- rank 0, N = 1 (BASELINE C4 per GPU, SURVEY §8d "env+PPO separately"): env-steps/s
-                  of the PPO trainer (scripts/bench_train.py: reference agent config, 32768 envs,
-                  horizon 32, 10 mini-epochs) -- reported beside `value`, never as `value`.
+  train        -- every rank (BASELINE C4, SURVEY §8d "env+PPO separately"): env-steps/s of the PPO
+                  trainer over all ranks (scripts/bench_train.py: reference agent config, 32768 envs
+                  per rank, horizon 32, 10 mini-epochs; N > 1: the --distributed path) -- reported
+                  beside `value`, never as `value`.
   c5           -- rank 0, N = 1 (BASELINE C5): the quadruped (model/anymal_c.xml) on the stones,
                   physics only, 16384 envs (scripts/bench_quadruped.py) -- beside `value`.
 """
@@ -55,7 +58,8 @@ def parse():
     p.add_argument("--num-envs", type=int, default=4096)
     p.add_argument("--level", type=int, default=0, help="stone curriculum level (C3: 9)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=None,
+                   help="oracle OpenMP threads (default: OMP_NUM_THREADS, else nproc; BASELINE.md §3)")
     p.add_argument("--no-train", action="store_true", help="skip the env+PPO trainer measurement")
     p.add_argument("--train-envs", type=int, default=32768)
     p.add_argument("--no-c5", action="store_true", help="skip the quadruped (BASELINE C5) physics measurement")
@@ -85,12 +89,35 @@ def measured_hbm_peak(device) -> float | None:
         return None
 
 
-def cpu_baseline(num_envs: int, level: int, threads: int) -> dict:
-    """The oracle (CPU port of the same step) on the host cores, bounded sample (~10-30 s CPU)."""
+def host_cpu() -> dict:
+    """nproc (affinity), os.cpu_count(), the CPU model and socket count (lscpu's fields, from
+    /proc/cpuinfo) of the host the CPU baseline runs on."""
+    model, sockets = None, set()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k = k.strip()
+                if k == "model name" and model is None:
+                    model = v.strip()
+                elif k == "physical id":
+                    sockets.add(v.strip())
+    except OSError:
+        pass
+    return {"nproc": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count(), "model": model,
+            "sockets": len(sockets) or None}
+
+
+def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int = 50) -> dict:
+    """The oracle (CPU port of the same step) on the host cores, bounded sample (~20 CPU-s), timed
+    after `warm_steps` steps past the from-reset transient (the falling start)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
 
+    host = host_cpu()
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS") or host["nproc"])
     O.build()
     orc = O.Oracle()
     n = num_envs  # the sample is bounded by time (~20 CPU-s), not by size
@@ -106,7 +133,8 @@ def cpu_baseline(num_envs: int, level: int, threads: int) -> dict:
     orc.reset_all(st, seed=42)
     rng = np.random.default_rng(42)
     acts = [rng.uniform(-1, 1, (n, 21)).astype(np.float32) for _ in range(4)]
-    orc.env_step(st, acts[0], nthreads=threads)  # warm
+    for t in range(warm_steps):  # past the from-reset transient: envs fall, reset, walk at random
+        orc.env_step(st, acts[t % 4], nthreads=threads)
     steps, t0 = 0, time.perf_counter()
     while True:
         orc.env_step(st, acts[steps % 4], nthreads=threads)
@@ -115,8 +143,9 @@ def cpu_baseline(num_envs: int, level: int, threads: int) -> dict:
         if el * threads > 20.0 or steps >= 200:
             break
     return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ C port, {n} envs x {steps} steps (level {level}, from reset, U(-1,1) actions), "
-                      f"OpenMP {threads} threads, {el:.2f} s wall"}
+            "host": host,
+            "sample": f"oracle/ C port, {n} envs x {steps} steps (level {level}, U(-1,1) actions, timed after "
+                      f"{warm_steps} warm-up steps), OpenMP {threads} threads, {el:.2f} s wall"}
 
 
 def main():
@@ -174,6 +203,16 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     resets = int(env.reset_buf.sum().item())
+    # latency side of k_step (after the timed region, on the same envs): per-wave records of 20 launches
+    latency = None
+    if rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import stamps
+
+        try:
+            latency = stamps.latency_summary(stamps.wave_records(env, actions[:20]))
+        except Exception as e:  # reported, never fatal for the env metric
+            latency = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         value = n * world * K / el
@@ -208,22 +247,30 @@ def main():
                          "kernel": "k_step", "bytes_per_env": K_STEP_BYTES,
                          "peak_measured": measured_hbm_peak(device),
                          "peak_measured_method": "in-tree STREAM copy (as_hbm_copy), read + write GB/s",
-                         "valu_issue_frac": pmc.get("valu_issue_frac")},
+                         "valu_issue_frac": pmc.get("valu_issue_frac"),
+                         # latency-bound kernel: the launch lasts as long as its slowest wave
+                         "latency": latency},
             "cpu_baseline": None,
             "resets_last_step": resets,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(n, args.level, args.cpu_threads)
     env.close()
-    if rank == 0:
-        if world == 1 and not args.no_train:
-            sys.path.insert(0, os.path.join(ROOT, "scripts"))
-            import bench_train
+    if not args.no_train:
+        # env + PPO (BASELINE C4: 32768 envs per rank; at N ranks the trainer's --distributed path, one
+        # RCCL all-reduce of [grads | kl] per minibatch): every rank trains, rank 0 reports
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import bench_train
 
-            try:
-                line["train"] = bench_train.measure(args.train_envs, epochs=2, warmup=2, verbose=False)
-            except Exception as e:  # reported, never fatal for the env metric
-                line["train"] = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            train = bench_train.measure(args.train_envs, epochs=2, warmup=2, verbose=False, distributed=world > 1)
+        except Exception as e:  # reported, never fatal for the env metric
+            train = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            line["train"] = train
+        elif "error" in train:
+            print(f"bench rank {rank}: train leg failed: {train['error']}", file=sys.stderr, flush=True)
+    if rank == 0:
         if world == 1 and not args.no_c5:
             sys.path.insert(0, os.path.join(ROOT, "scripts"))
             import bench_quadruped

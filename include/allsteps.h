@@ -205,10 +205,10 @@ int as_profile_read(as_env_t* env, double* step_kernel_ms, double* obs_kernel_ms
  * s_memtime cycles of each of its 15 phases (load, fk, rnea, H rows, H^-1 sweep, solve, collide,
  * rows, W, pgs, integrate, final fk, task, reset, store) to slots 0..14; slot 15 keeps the largest
  * single-wave total of any launch and slots 16..30 the largest single-wave cycles of each phase
- * (atomicMax).  If slot 31 is non-zero on entry, the buffer must hold 64 + 24 * ceil(num_envs / 2)
- * words and each wave instead stores (no atomics) a 24-word record of its own at 64 + 24 * block
- * (phases, total, start / end s_memtime, HW_ID, XCC_ID, rows and contacts per env), overwritten
- * by every launch (scripts/stamps.py).  Pass NULL to switch off. */
+ * (atomicMax).  If slot 31 is non-zero on entry, the buffer must hold 64 + 26 * ceil(num_envs / 2)
+ * words and each wave instead stores (no atomics) a 26-word record of its own at 64 + 26 * block
+ * (phases, total, start / end s_memtime, HW_ID, XCC_ID, rows and contacts per env, start / end
+ * s_memrealtime), overwritten by every launch (scripts/stamps.py).  Pass NULL to switch off. */
 int as_debug_stamps(as_env_t* env, uint64_t* stamps_dev);
 
 /* Graph-safe stepping (on != 0): every as_step / as_task_step / as_reset_* uses the SAME counter bank,

@@ -19,8 +19,11 @@ sys.path.insert(0, os.path.join(ROOT, "scripts", "reinforcement_learning", "rl_g
 
 
 def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int | None = None,
-            log_root: str = "/tmp/bench_train_logs", verbose: bool = True) -> dict:
+            log_root: str = "/tmp/bench_train_logs", verbose: bool = True, distributed: bool = False) -> dict:
+    """num_envs per rank; with distributed=True (under torch.distributed.run) every rank trains with
+    train.py --distributed and the result counts all ranks' env-steps over the slowest rank's time."""
     import torch
+    import torch.distributed as dist
 
     import train
     from allsteps_isaaclab_amd.learning import a2c_continuous as A
@@ -45,6 +48,8 @@ def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int 
                 str(epochs + warmup), "--seed", "42", "--log_root", log_root]
         if level is not None:
             argv += ["--stone_level", str(level)]
+        if distributed:
+            argv += ["--distributed"]
         if verbose:
             runner, _ = train.main(argv)
         else:  # keep stdout to the caller's single JSON line
@@ -57,11 +62,18 @@ def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int 
         A.A2CAgent.train_epoch = orig
     agent = runner.agent
     t = samples[warmup:]
-    frames = agent.batch_size * len(t)
+    world = dist.get_world_size() if distributed and dist.is_initialized() else 1
+    frames = agent.horizon_length * num_envs * world * len(t)
     wall = sum(x[0] for x in t)
+    if world > 1:  # the slowest rank's time
+        dev = agent.device if dist.get_backend() == "nccl" else "cpu"
+        w = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w.item())
     return {
         "metric": "env-steps/sec incl. PPO update (rl_games agent config), Allsteps-v0",
-        "value": round(frames / wall, 1), "unit": "env-steps/s", "n_gpus": 1, "num_envs": num_envs,
+        "value": round(frames / wall, 1), "unit": "env-steps/s", "n_gpus": world, "num_envs": num_envs,
+        "global_envs": num_envs * world, "multi_gpu_mode": getattr(agent, "multi_gpu_mode", None) if world > 1 else None,
         "epochs": len(t), "horizon": agent.horizon_length, "minibatch": agent.minibatch_size,
         "mini_epochs": agent.mini_epochs_num, "s_per_epoch": round(wall / len(t), 4),
         "play_s": round(sum(x[1] for x in t) / len(t), 4), "update_s": round(sum(x[2] for x in t) / len(t), 4),

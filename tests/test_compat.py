@@ -1,0 +1,96 @@
+"""The opt-in import shims (allsteps_isaaclab_amd.compat): the reference's own rl_games train / play
+scripts run unchanged over this package (north_star "train.py runs unchanged").
+
+The reference scripts are read from /root/reference when present (this container only: the reference
+never travels to the GPU box) and executed AS THEY ARE through ``python -m allsteps_isaaclab_amd.compat``.
+Without a HIP device they get through every line before the environment -- argument parsing, the
+AppLauncher, the rl_games / isaaclab / isaaclab_tasks / hydra imports, the registry cfgs with hydra
+overrides, the log dumps (train.py:76-134; play.py:71-111) -- and stop at gym.make with the product's
+loud NativeError (no CPU fallback).
+"""
+
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_RLG = "/root/reference/scripts/reinforcement_learning/rl_games"
+needs_ref = pytest.mark.skipif(not os.path.isdir(REF_RLG), reason="reference scripts absent (GPU box)")
+
+
+def _py(code: str, cwd: str, extra_path: str | None = None) -> subprocess.CompletedProcess:
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in (ROOT, extra_path) if p))
+    return subprocess.run([sys.executable, "-c", code], cwd=cwd, env=env, capture_output=True, text=True, timeout=120)
+
+
+def test_shims_are_opt_in(tmp_path):
+    r = _py("import importlib.util as u; print([u.find_spec(m) is None for m in "
+            "('isaaclab', 'isaaclab_rl', 'isaaclab_tasks', 'rl_games')])", str(tmp_path))
+    assert r.returncode == 0 and r.stdout.strip() == "[True, True, True, True]", r.stdout + r.stderr
+    r = _py("from allsteps_isaaclab_amd import compat; compat.install()\n"
+            "import isaaclab.app, isaaclab.envs, isaaclab_rl.rl_games, isaaclab_tasks, rl_games.torch_runner\n"
+            "from isaaclab_tasks.utils.hydra import hydra_task_config\n"
+            "from rl_games.common import env_configurations, vecenv\n"
+            "import allsteps_isaaclab_amd.rl_games as R, allsteps_isaaclab_amd._vecenv as V\n"
+            "assert R.vecenv is V.vecenv and R.env_configurations is V.env_configurations\n"
+            "import gymnasium; print(gymnasium.spec('Allsteps-v0').entry_point)", str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip() == "allsteps_isaaclab_amd.envs.allsteps_env:AllstepsEnv"
+
+
+def test_install_never_shadows_a_real_package(tmp_path):
+    fake = tmp_path / "real"
+    (fake / "rl_games").mkdir(parents=True)
+    (fake / "rl_games" / "__init__.py").write_text("REAL = True\n")
+    r = _py("from allsteps_isaaclab_amd import compat; print(compat.install())\n"
+            "import rl_games; print(getattr(rl_games, 'REAL', False))", str(tmp_path), extra_path=str(fake))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["['rl_games']", "True"]
+
+
+def test_hydra_overrides(tmp_path):
+    r = _py("from allsteps_isaaclab_amd import compat; compat.install()\n"
+            "import sys; sys.argv = ['x', '--headless', 'env.scene.num_envs=128', 'agent.params.config.horizon_length=16']\n"
+            "from isaaclab_tasks.utils.hydra import hydra_task_config\n"
+            "@hydra_task_config('Allsteps-v0', 'rl_games_cfg_entry_point')\n"
+            "def main(env_cfg, agent_cfg):\n"
+            "    print(env_cfg.scene.num_envs, agent_cfg['params']['config']['horizon_length'])\n"
+            "main()", str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split() == ["128", "16"]
+
+
+def _run_reference(script: str, args: list[str], cwd) -> subprocess.CompletedProcess:
+    env = dict(os.environ, PYTHONPATH=ROOT, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", ""))
+    return subprocess.run([sys.executable, "-m", "allsteps_isaaclab_amd.compat", os.path.join(REF_RLG, script), *args],
+                          cwd=str(cwd), env=env, capture_output=True, text=True, timeout=300)
+
+
+@needs_ref
+def test_reference_train_py_runs_unchanged_to_the_env(tmp_path):
+    r = _run_reference("train.py", ["--task", "Allsteps-v0", "--headless", "--num_envs", "64", "--max_iterations",
+                                    "1", "agent.params.config.minibatch_size=2048"], tmp_path)
+    assert r.returncode != 0
+    assert "NativeError: AllstepsEnv runs on the HIP backend only" in r.stderr, r.stderr[-3000:]
+    runs = list((tmp_path / "logs" / "rl_games" / "allsteps").iterdir())
+    assert len(runs) == 1
+    params = sorted(p.name for p in (runs[0] / "params").iterdir())
+    assert params == ["agent.pkl", "agent.yaml", "env.pkl", "env.yaml"]
+    import yaml
+
+    agent = yaml.safe_load((runs[0] / "params" / "agent.yaml").read_text())
+    assert agent["params"]["config"]["minibatch_size"] == 2048 and agent["params"]["config"]["max_epochs"] == 1
+    env = yaml.safe_load((runs[0] / "params" / "env.yaml").read_text())
+    assert env["scene"]["num_envs"] == 64
+
+
+@needs_ref
+def test_reference_play_py_runs_unchanged_to_the_env(tmp_path):
+    (tmp_path / "model.pth").write_bytes(b"")
+    r = _run_reference("play.py", ["--task", "Allsteps-v0", "--headless", "--num_envs", "16", "--checkpoint",
+                                   "model.pth"], tmp_path)
+    assert r.returncode != 0
+    assert "NativeError: AllstepsEnv runs on the HIP backend only" in r.stderr, r.stderr[-3000:]
+    assert "Loading model checkpoint from" in r.stdout or "Loading experiment" in r.stdout

@@ -404,7 +404,7 @@ def test_c3_large_config_invariants():
 def test_bench_two_ranks_one_gpu():
     """Rehearsal of the driver's multi-GPU bench launch (torch.distributed.run, one process per rank,
     barrier + max-over-ranks timing) with two ranks sharing cuda:0 over gloo: rank 0 prints ONE JSON
-    line whose value counts both ranks' envs."""
+    line whose value counts both ranks' envs, with the env + PPO `train` leg measured on both ranks."""
     import json
     import os
     import socket
@@ -418,11 +418,15 @@ def test_bench_two_ranks_one_gpu():
     env = dict(os.environ, ALLSTEPS_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20",
-           "--warmup", "3", "--num-envs", "256", "--no-cpu-baseline", "--no-train"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
+           "--warmup", "3", "--num-envs", "256", "--no-cpu-baseline", "--no-c5", "--train-envs", "1024"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = lines[0]
     assert line["n_gpus"] == 2 and line["config"]["global_envs"] == 512 and line["scaling"] == "weak"
     assert abs(line["value"] - 512 * 20 / (line["ms_per_step"] * 20 / 1e3)) / line["value"] < 1e-2
+    # C4's env + PPO leg runs at N ranks too (the trainer's --distributed path), counting both ranks
+    tr = line["train"]
+    assert "error" not in tr, (tr, r.stderr[-2000:])
+    assert tr["n_gpus"] == 2 and tr["global_envs"] == 2048 and tr["value"] > 0
