@@ -18,13 +18,13 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 
 MAXL, MAXG, MAXSP = 32, 32, 256
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 EXPORTED_SYMBOLS = [
     "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
     "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask", "as_set_graph_safe",
-    "as_profile_sampled", "as_hbm_copy",
+    "as_profile_sampled", "as_hbm_copy", "as_set_actuator", "as_set_quad_task", "as_quad_step", "as_quad_reset_all",
 ]
 
 
@@ -74,7 +74,24 @@ VP = C.c_void_p
 class AsState(C.Structure):
     _fields_ = [(name, VP) for name in (
         "root_pos", "root_quat", "root_lin", "root_ang", "q", "qd", "stones", "pot", "old_pot", "foot_contact",
-        "body_pos", "idx", "prev", "next", "count", "swing", "ep_len", "episode", "contact_mask", "curriculum")]
+        "body_pos", "idx", "prev", "next", "count", "swing", "ep_len", "episode", "contact_mask", "curriculum",
+        "contact_mask_hind")]
+
+
+class AsActuator(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("action_scale", C.c_float), ("default_q", C.c_float * 21),
+                ("stiffness", C.c_float), ("damping", C.c_float), ("saturation_effort", C.c_float),
+                ("effort_limit", C.c_float), ("velocity_limit", C.c_float)]
+
+
+class AsQuadTask(C.Structure):
+    _fields_ = [("stop_frames", C.c_int32), ("alive", C.c_float), ("action_cost", C.c_float), ("death", C.c_float),
+                ("min_height", C.c_float), ("up_z_min", C.c_float), ("max_episode_length", C.c_int32),
+                ("step_dt", C.c_float), ("stand_height", C.c_float), ("joint_noise", C.c_float)]
+
+
+ACT_TORQUE, ACT_DC_MOTOR = 0, 1
+QUAD_OBS_DIM = 51
 
 
 # (field, rows, dtype) of the SoA state, in as_state_t order
@@ -120,6 +137,10 @@ def load() -> C.CDLL:
     L.as_step_counters.argtypes = [V, C.POINTER(V)]
     L.as_get_curriculum_host.argtypes = [V, C.POINTER(I32)]
     L.as_hbm_copy.argtypes = [V, V, I64, V]
+    L.as_set_actuator.argtypes = [V, V]
+    L.as_set_quad_task.argtypes = [V, V]
+    L.as_quad_step.argtypes = [V, V, V, V, V, V, V]
+    L.as_quad_reset_all.argtypes = [V, V, V]
     L.as_last_error.restype = C.c_char_p
     for name in EXPORTED_SYMBOLS:
         if name != "as_last_error":
@@ -282,6 +303,7 @@ class NativeEnv:
         for name, _, _ in STATE_LAYOUT:
             setattr(S, name, state[name].data_ptr())
         S.curriculum = state["curriculum"].data_ptr()
+        S.contact_mask_hind = state["contact_mask_hind"].data_ptr() if "contact_mask_hind" in state else None
         self._state = S
         h = C.c_void_p()
         check(self.L.as_create(n, C.byref(self._model), C.byref(self._sim), C.byref(self._task), C.byref(S),
@@ -327,6 +349,31 @@ class NativeEnv:
 
     def physics_step(self, actions, stream=None):
         check(self.L.as_physics_step(self.h, actions.data_ptr(), stream), "as_physics_step")
+
+    def set_actuator(self, mode: int, action_scale: float = 0.0, default_q=(), stiffness: float = 0.0,
+                     damping: float = 0.0, saturation_effort: float = 0.0, effort_limit: float = 0.0,
+                     velocity_limit: float = 0.0):
+        A = AsActuator()
+        A.mode, A.action_scale = mode, action_scale
+        A.default_q[: len(default_q)] = [float(x) for x in default_q]
+        A.stiffness, A.damping = stiffness, damping
+        A.saturation_effort, A.effort_limit, A.velocity_limit = saturation_effort, effort_limit, velocity_limit
+        self._act = A
+        check(self.L.as_set_actuator(self.h, C.byref(A)), "as_set_actuator")
+
+    def set_quad_task(self, **kw):
+        Q = AsQuadTask()
+        for k, v in kw.items():
+            setattr(Q, k, v)
+        self._quad = Q
+        check(self.L.as_set_quad_task(self.h, C.byref(Q)), "as_set_quad_task")
+
+    def quad_step(self, actions, obs, rew, term, trunc, stream=None):
+        check(self.L.as_quad_step(self.h, actions.data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),
+                                  trunc.data_ptr(), stream), "as_quad_step")
+
+    def quad_reset_all(self, obs, stream=None):
+        check(self.L.as_quad_reset_all(self.h, obs.data_ptr(), stream), "as_quad_reset_all")
 
     def generate_stones(self, level: int, draws=None, stream=None):
         check(self.L.as_generate_stones(self.h, level, draws.data_ptr() if draws is not None else None, stream),

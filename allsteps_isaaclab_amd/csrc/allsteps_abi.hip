@@ -58,6 +58,8 @@ struct as_env {
   uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_fix
   int32_t num_steps;
   int32_t nv;
+  as::Consts host;        // host copy of consts_dev (as_set_actuator / as_set_quad_task re-upload it)
+  int32_t quad_ready = 0; // as_set_quad_task called
   // optional per-launch timing (as_profile): event triples around k_step / k_obs
   std::vector<hipEvent_t> ev;
   unsigned long long* stamps = nullptr;  // diagnostic (as_debug_stamps)
@@ -116,6 +118,8 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   h.sim = *sim;
   h.task = *task;
   h.nv = 6 + model->num_hinges;
+  h.act.mode = AS_ACT_TORQUE;
+  h.st_has_hind = state->contact_mask_hind != nullptr;
   const int nl = model->num_links;
   for (int i = 0; i < nl; ++i) {
     int pa = model->parent[i];
@@ -156,6 +160,7 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   env->st = *state;
   env->num_steps = task->num_steps;
   env->nv = h.nv;
+  env->host = h;
   if (hipMalloc(&env->consts_dev, sizeof(as::Consts)) != hipSuccess ||
       hipMalloc(&env->counters_dev, 2 * as::kCntBank * sizeof(int32_t)) != hipSuccess ||
       hipMalloc(&env->side_dev, (size_t)as::kSideWords * num_envs * sizeof(uint32_t)) != hipSuccess) {
@@ -319,6 +324,68 @@ int as_reset_mask(as_env_t* env, const uint8_t* mask, float* obs, const float* r
 int as_physics_step(as_env_t* env, const float* actions, void* stream) {
   if (!env || !actions) return fail(AS_ERR_INVALID, "as_physics_step: null argument");
   return run(env, as::kModePhysics, actions, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int as_set_actuator(as_env_t* env, const as_actuator_t* act) {
+  if (!env || !act) return fail(AS_ERR_INVALID, "as_set_actuator: null argument");
+  if (act->mode != AS_ACT_TORQUE && act->mode != AS_ACT_DC_MOTOR) return fail(AS_ERR_INVALID, "as_set_actuator: mode");
+  if (act->mode == AS_ACT_DC_MOTOR && !(act->velocity_limit > 0.f && act->effort_limit >= 0.f))
+    return fail(AS_ERR_INVALID, "as_set_actuator: the DC motor needs velocity_limit > 0 and effort_limit >= 0");
+  HIP_TRY(hipSetDevice(env->device));
+  env->host.act = *act;
+  // ordered on the null stream with respect to every earlier launch (hipMemcpy synchronises)
+  HIP_TRY(hipMemcpy(env->consts_dev, &env->host, sizeof(as::Consts), hipMemcpyHostToDevice));
+  return AS_OK;
+}
+
+int as_set_quad_task(as_env_t* env, const as_quad_task_t* q) {
+  if (!env || !q) return fail(AS_ERR_INVALID, "as_set_quad_task: null argument");
+  if (env->host.model.num_hinges != 12 || 15 + 3 * env->host.model.num_hinges != AS_QUAD_OBS_DIM)
+    return fail(AS_ERR_INVALID, "as_set_quad_task: the task is defined for a 12-hinge quadruped");
+  if (!env->st.contact_mask_hind) return fail(AS_ERR_INVALID, "as_set_quad_task: state->contact_mask_hind is NULL");
+  if (q->stop_frames < 1 || q->max_episode_length < 1 || !(q->step_dt > 0.f) || env->num_steps < 3)
+    return fail(AS_ERR_INVALID, "as_set_quad_task: stop_frames / max_episode_length / step_dt / num_steps");
+  HIP_TRY(hipSetDevice(env->device));
+  env->host.quad = *q;
+  HIP_TRY(hipMemcpy(env->consts_dev, &env->host, sizeof(as::Consts), hipMemcpyHostToDevice));
+  env->quad_ready = 1;
+  return AS_OK;
+}
+
+static int quad(as_env_t* env, int reset_all, const float* actions, float* obs, float* reward, uint8_t* term,
+                uint8_t* trunc, void* stream) {
+  if (!env->quad_ready) return fail(AS_ERR_INVALID, "as_quad_*: call as_set_quad_task first");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!reset_all) {
+    const int rc = run(env, as::kModePhysics, actions, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+    if (rc != AS_OK) return rc;
+  }
+  as::QuadArgs a{};
+  a.consts = env->consts_dev;
+  a.st = env->st;
+  a.n = env->n;
+  a.reset_all = reset_all;
+  a.actions = actions;
+  a.obs = obs;
+  a.reward = reward;
+  a.terminated = term;
+  a.truncated = trunc;
+  a.seed = env->seed;
+  a.env_offset = env->env_offset;
+  HIP_TRY(as::launch_quad(a, s));
+  return AS_OK;
+}
+
+int as_quad_step(as_env_t* env, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                 uint8_t* truncated, void* stream) {
+  if (!env || !actions || !obs || !reward || !terminated || !truncated)
+    return fail(AS_ERR_INVALID, "as_quad_step: null argument");
+  return quad(env, 0, actions, obs, reward, terminated, truncated, stream);
+}
+
+int as_quad_reset_all(as_env_t* env, float* obs, void* stream) {
+  if (!env || !obs) return fail(AS_ERR_INVALID, "as_quad_reset_all: null argument");
+  return quad(env, 1, nullptr, obs, nullptr, nullptr, nullptr, stream);
 }
 
 int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* stream) {

@@ -21,7 +21,10 @@ struct Consts {
   as_model_t model;
   as_sim_t sim;
   as_task_t task;
+  as_actuator_t act;               // as_set_actuator (mode AS_ACT_TORQUE after as_create)
+  as_quad_task_t quad;             // as_set_quad_task (BASELINE C5)
   int32_t nv;
+  int32_t st_has_hind;             // the state carries contact_mask_hind (sensors 2, 3)
   int32_t max_path;                // longest root->link path, root excluded (links)
   int32_t max_sub;                 // largest subtree of a non-root link, itself excluded
   uint32_t root_kids;              // links whose parent is the root
@@ -74,6 +77,21 @@ constexpr int kSideRegen = kSideState + kSideObs;  // 1 = reset env due new ston
 constexpr int kSideWords = kSideRegen + 1;
 constexpr int kCntLevel = 2;  // counter-bank word: the curriculum level k_step saw (k_obs regen level)
 
+// k_quad (BASELINE C5 task epilogue, one env per lane)
+struct QuadArgs {
+  const Consts* consts;
+  as_state_t st;
+  int32_t n;
+  int32_t reset_all;           // 1: reset every env (as_quad_reset_all), no task step
+  const float* actions;        // [n][nh]
+  float* obs;                  // [n][AS_QUAD_OBS_DIM]
+  float* reward;
+  uint8_t* terminated;
+  uint8_t* truncated;
+  uint64_t seed;
+  int64_t env_offset;
+};
+
 struct ObsArgs {
   const Consts* consts;
   as_state_t st;
@@ -100,6 +118,7 @@ bool step_supported_nv(int nv);
 hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream);
 hipError_t launch_obs(const ObsArgs& a, hipStream_t stream);
 hipError_t launch_stones(const StonesArgs& a, hipStream_t stream);
+hipError_t launch_quad(const QuadArgs& a, hipStream_t stream);
 // zero n int32 words with a kernel (graph-safe stepping: a kernel node instead of a memset node)
 hipError_t launch_zero(int32_t* p, int n, hipStream_t stream);
 size_t step_lds_bytes();

@@ -133,12 +133,13 @@ struct EnvS {
   float u[NVMAX];
   float qi[LMAX];       // hinge angles, link order (link i -> qi[i-1])
   float tau[LMAX];
+  float qt[LMAX];       // AS_ACT_DC_MOTOR: joint position targets (link order)
   float act[AS_ACT_DIM];
   float stones[NST * 3];
   float root_pos[3], root_quat[4];
   int cand[NST];
   int ncand, ncontact, nrow;
-  uint32_t mask[2];
+  uint32_t mask[4];     // contact sensors 0..3 (2, 3: a quadruped's hind feet)
 };
 
 struct Smem {
@@ -1005,7 +1006,7 @@ __device__ __forceinline__ float pgs_clamp(const v4f& mt, float t, float mu, flo
 }
 
 template <int NV>
-__device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, uint32_t* mask_out,
+__device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, uint32_t (&mask_out)[4],
                         Stamp& ts) {
   // Opaque copies of the constants pointer and the lane id: everything derived from them below
   // (model-table loads, LDS addresses, lane masks) is loop-invariant, and without this the
@@ -1018,7 +1019,12 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   const as_model_t& m = K.model;
   const float dt = K.sim.dt;
   const int nh = m.num_hinges;
-  fk<true>(K, s, lane, tp);
+  if (K.act.mode == AS_ACT_DC_MOTOR && lane < nh) {  // the actuator runs in every substep (lane = hinge)
+    const as_actuator_t& A = K.act;
+    s.tau[lane] = as_dc_motor(s.qt[lane], s.qi[lane], s.u[6 + lane], A.stiffness, A.damping, A.saturation_effort,
+                              A.effort_limit, A.velocity_limit);
+  }
+  fk<true>(K, s, lane, tp);  // (its first barrier publishes tau before the dynamics read it)
   ts.mark(kStFK);
   dynamics(K, s, lane, tp, K.sim.gravity);
   ts.mark(kStLinkQ);
@@ -1292,7 +1298,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   //      lambda_n n over the contacts with its (foot, stone) pair in ascending order, and the
   //      per-foot stone bits are OR-reduced over the half-wave
   {
-    uint32_t b0 = 0u, b1 = 0u;
+    uint32_t b[4] = {0u, 0u, 0u, 0u};
     if (lane < nc && 3 * lane < nrow) {
       const int f = s.cfoot[lane], st = s.cstone[lane];
       if (f >= 0) {
@@ -1305,12 +1311,16 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
           fz += same ? l * s.cn[c2][2] : 0.f;
         }
         if (sqrtf(fx * fx + fy * fy + fz * fz) / dt > 1e-4f) {
-          if (f == 0) b0 = 1u << st; else b1 = 1u << st;
+          b[f & 3] = 1u << st;
         }
       }
     }
-    mask_out[0] = half_or(b0);
-    mask_out[1] = half_or(b1);
+    mask_out[0] = half_or(b[0]);
+    mask_out[1] = half_or(b[1]);
+    if (K.st_has_hind) {  // wave-uniform: only a state with the hind-feet masks (quadruped)
+      mask_out[2] = half_or(b[2]);
+      mask_out[3] = half_or(b[3]);
+    }
   }
   // ---- integrate
   if (lane < nh) {
@@ -1449,9 +1459,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     a = fminf(fmaxf(a, -1.f), 1.f);                      // allsteps_env.py:267-268
     s.act[lane] = a;
     s.tau[i] = gain * m.gear[lane] * a;                  // allsteps_env.py:273
+    s.qt[i] = K.act.action_scale * a + K.act.default_q[lane];  // AS_ACT_DC_MOTOR (anymal_c_env.py:73-74)
   }
   for (int k = lane; k < 3 * T.num_steps; k += G) s.stones[k] = st.stones[k * n + e];
-  uint32_t mask[2] = {st.contact_mask[e], st.contact_mask[n + e]};
+  uint32_t mask[4] = {st.contact_mask[e], st.contact_mask[n + e], 0u, 0u};
   __syncthreads();
   ts.mark(kStLoad);
   const bool do_physics = P.mode == kModeStep || P.mode == kModePhysics;
@@ -1459,7 +1470,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   if (do_physics) {
     for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, mask, ts);
     fk<false>(K, s, lane, tp);  // FK of the final pose for body_pos_w (articulation_data.py:439)
-    if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
+    if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; s.mask[2] = mask[2]; s.mask[3] = mask[3]; }
   }
   ts.mark(kStFKFinal);
   if (lane == 0 && !do_physics) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
@@ -1699,6 +1710,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (lane == 0) {
       st.contact_mask[e] = s.mask[0];
       st.contact_mask[n + e] = s.mask[1];
+      if (st.contact_mask_hind) {
+        st.contact_mask_hind[e] = s.mask[2];
+        st.contact_mask_hind[n + e] = s.mask[3];
+      }
       if (P.mode != kModePhysics) {
         st.idx[e] = idx; st.prev[e] = prev; st.next[e] = next; st.count[e] = count; st.swing[e] = swing;
         st.ep_len[e] = ep_len; st.pot[e] = pot; st.old_pot[e] = old_pot;
@@ -1811,6 +1826,134 @@ __global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= P.n) return;
   gen_stones(T, P.level, P.seed, (uint32_t)(P.env_offset + e), 0u, P.draws, P.stones, P.n, e);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_quad: the BASELINE C5 task epilogue (include/allsteps.h as_quad_task_t), one env per lane, after
+// the physics substeps of k_step<18> (AS_ACT_DC_MOTOR); oracle/quad.c or_quad_post_physics is its
+// serial restatement.  Coalesced SoA loads / stores (64-thread workgroups, like k_obs).
+constexpr uint32_t kQuadTag = 0x51756164u;  // "Quad": reset-draw stream of the quadruped task
+
+__global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
+  const Consts& K = *(const Consts*)(CK*)P.consts;
+  const as_model_t& m = K.model;
+  const as_quad_task_t& Q = K.quad;
+  const int e = blockIdx.x * 64 + threadIdx.x;
+  if (e >= P.n) return;
+  const int n = P.n, nh = m.num_hinges, N = K.task.num_steps;
+  const as_state_t& st = P.st;
+  const float half_z = K.sim.stone_half[2];
+  auto stone = [&](int k, int c) { return st.stones[(3 * k + c) * n + e]; };
+  float rp[3], rq[4], lin[3], ang[3], a[AS_ACT_DIM];
+  for (int k = 0; k < 3; ++k) {
+    rp[k] = st.root_pos[k * n + e];
+    lin[k] = st.root_lin[k * n + e];
+    ang[k] = st.root_ang[k * n + e];
+  }
+  for (int k = 0; k < 4; ++k) rq[k] = st.root_quat[k * n + e];
+  for (int k = 0; k < nh; ++k) {
+    const float x = P.reset_all ? 0.f : P.actions[(size_t)e * nh + k];
+    a[k] = fminf(fmaxf(x, -1.f), 1.f);
+  }
+  int idx = st.idx[e], count = st.count[e], ep_len = st.ep_len[e];
+  uint32_t episode = st.episode[e];
+  float pot = st.pot[e], old_pot = st.old_pot[e];
+  bool term = false, trunc = false;
+  if (!P.reset_all) {
+    ep_len += 1;
+    // target tick: a front foot (sensor 0 / 1) pushing on the target stone for stop_frames steps
+    const uint32_t front = st.contact_mask[e] | st.contact_mask[n + e];
+    if ((front >> idx) & 1u) count += 1;
+    if (count >= Q.stop_frames) {
+      idx = min(idx + 1, N - 1);
+      count = 0;
+    }
+    old_pot = pot;
+    const float dx = stone(idx, 0) - rp[0], dy = stone(idx, 1) - rp[1];
+    pot = -sqrtf(dx * dx + dy * dy) / Q.step_dt;
+    const float down[3] = {0.f, 0.f, -1.f};
+    float gb[3];
+    quat_rotate_inverse(rq, down, gb);
+    term = gb[2] > -Q.up_z_min || rp[2] < stone(idx, 2) + Q.min_height;
+    trunc = ep_len >= Q.max_episode_length;
+    float a2 = 0.f;
+    for (int k = 0; k < nh; ++k) a2 += a[k] * a[k];
+    const float progress = pot - old_pot;
+    P.reward[e] = term ? Q.death : progress + Q.alive - Q.action_cost * a2;
+    P.terminated[e] = term;
+    P.truncated[e] = trunc;
+  }
+  float q[AS_ACT_DIM], qd[AS_ACT_DIM];
+  for (int k = 0; k < nh; ++k) {
+    q[k] = st.q[k * n + e];
+    qd[k] = st.qd[k * n + e];
+  }
+  if (P.reset_all || term || trunc) {
+    // the stand pose over stones 0 (hind feet) and 1 (front feet), joints + U(-1, 1) * noise
+    float blk[4];
+    for (int k = 0; k < nh; ++k) {
+      if ((k & 3) == 0) philox_block(P.seed, (uint32_t)(P.env_offset + e), episode, (uint32_t)(k >> 2), kQuadTag, blk);
+      q[k] = K.act.default_q[k] + Q.joint_noise * (2.f * blk[k & 3] - 1.f);
+      qd[k] = 0.f;
+      st.q[k * n + e] = q[k];
+      st.qd[k * n + e] = 0.f;
+    }
+    episode += 1u;
+    rp[0] = 0.5f * (stone(0, 0) + stone(1, 0));
+    rp[1] = 0.5f * (stone(0, 1) + stone(1, 1));
+    rp[2] = fmaxf(stone(0, 2), stone(1, 2)) + half_z + Q.stand_height;
+    rq[0] = 1.f; rq[1] = rq[2] = rq[3] = 0.f;
+    for (int k = 0; k < 3; ++k) {
+      lin[k] = ang[k] = 0.f;
+      st.root_pos[k * n + e] = rp[k];
+      st.root_lin[k * n + e] = 0.f;
+      st.root_ang[k * n + e] = 0.f;
+    }
+    for (int k = 0; k < 4; ++k) st.root_quat[k * n + e] = rq[k];
+    idx = min(2, N - 1);
+    count = 0;
+    ep_len = 0;
+    const float dx = stone(idx, 0) - rp[0], dy = stone(idx, 1) - rp[1];
+    pot = -sqrtf(dx * dx + dy * dy) / Q.step_dt;
+    old_pot = pot;
+    st.contact_mask[e] = 0u;
+    st.contact_mask[n + e] = 0u;
+    st.contact_mask_hind[e] = 0u;
+    st.contact_mask_hind[n + e] = 0u;
+  }
+  st.idx[e] = idx;
+  st.count[e] = count;
+  st.ep_len[e] = ep_len;
+  st.episode[e] = episode;
+  st.pot[e] = pot;
+  st.old_pot[e] = old_pot;
+  // observation [51]: lin / ang velocity (body), projected gravity, stones idx / idx + 1 relative to
+  // the root (body), q - default, qd, actions
+  float* o = P.obs + (size_t)e * AS_QUAD_OBS_DIM;
+  float v[3];
+  quat_rotate_inverse(rq, lin, v);
+  o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+  quat_rotate_inverse(rq, ang, v);
+  o[3] = v[0]; o[4] = v[1]; o[5] = v[2];
+  const float down[3] = {0.f, 0.f, -1.f};
+  quat_rotate_inverse(rq, down, v);
+  o[6] = v[0]; o[7] = v[1]; o[8] = v[2];
+  for (int t = 0; t < 2; ++t) {
+    const int k = min(idx + t, N - 1);
+    const float d[3] = {stone(k, 0) - rp[0], stone(k, 1) - rp[1], stone(k, 2) - rp[2]};
+    quat_rotate_inverse(rq, d, v);
+    o[9 + 3 * t] = v[0]; o[10 + 3 * t] = v[1]; o[11 + 3 * t] = v[2];
+  }
+  for (int k = 0; k < nh; ++k) {
+    o[15 + k] = q[k] - K.act.default_q[k];
+    o[15 + nh + k] = qd[k];
+    o[15 + 2 * nh + k] = a[k];
+  }
+}
+
+hipError_t launch_quad(const QuadArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL(k_quad, dim3((a.n + 63) / 64), dim3(64), 0, stream, a);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1,4 +1,4 @@
-"""BASELINE C5: an ANYmal-C-like quadruped on the ALLSTEPS stones, physics only.
+"""BASELINE C5: an ANYmal-C-like quadruped on the ALLSTEPS stones.
 
 The reference's C5 row ("Anymal-C quadruped on ALLSTEPS stones, 16384 envs, 4-foot contact, different
 DoF count") has no model source offline (the ANYmal-C USD and actuator net are Nucleus-only,
@@ -10,8 +10,17 @@ the same SoA state and stone courses as the walker, four feet in contact with tw
 
 ``QuadrupedStonesEnv`` owns the device state; ``step(actions)`` applies tau = 1.2 * gear * clip(a)
 (the Allsteps actuation, gear 80/1.2 N m) for ``decimation`` substeps of 1/240 s.  ``stand_actions``
-is a joint-space PD on top of it (the ANYmal default stance), used by the tests and the bench to keep
-the robots standing on the stones.  There is no CPU fallback: the HIP library is required.
+is a joint-space PD on top of it (the ANYmal default stance), used by the physics tests to keep the
+robots standing on the stones.
+
+``AnymalCStonesEnv`` is the C5 task (include/allsteps.h ``as_quad_task_t``): actions are
+joint position targets ``default_q + 0.5 a`` (``anymal_c_env.py:73-74``) tracked in every physics
+substep by IsaacLab's DC motor model with the ANYdrive 3 "simple" gains (``anymal.py``
+``ANYDRIVE_3_SIMPLE_ACTUATOR_CFG``: kp 40, kd 5, saturation 120 N m, effort limit 80 N m, velocity
+limit 7.5 rad/s; ``actuator_pd.py:184-199, 264-275``), all four feet carry contact sensors, and the
+task epilogue (target stones, potentials, rewards, dones, in-kernel resets, the 51-float
+observation) runs in ``k_quad`` after the physics.  There is no CPU fallback: the HIP library is
+required.
 """
 
 from __future__ import annotations
@@ -66,6 +75,7 @@ class QuadrupedStonesEnv:
             dt = torch.float32 if t == "f" else torch.int32
             self.state[name] = torch.zeros((rows, n) if rows > 1 else (n,), dtype=dt, device=dev)
         self.state["curriculum"] = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.state["contact_mask_hind"] = torch.zeros((2, n), dtype=torch.int32, device=dev)  # sensors RH, LH
         with torch.cuda.device(dev):
             self._native = _native.NativeEnv(n, self.model, self.cfg, self.state, seed,
                                              dev.index if dev.index is not None else torch.cuda.current_device())
@@ -82,6 +92,7 @@ class QuadrupedStonesEnv:
         s["root_quat"][0] = 1.0
         s["q"][: self.num_dof] = self.q_stand.view(-1, 1)
         s["contact_mask"].zero_()
+        s["contact_mask_hind"].zero_()
         s["stones"][:] = stones if stones is not None else torch.as_tensor(level0_stones(n), device=self.device)
 
     def stand_actions(self, kp: float = 150.0, kd: float = 4.0) -> torch.Tensor:
@@ -103,10 +114,56 @@ class QuadrupedStonesEnv:
 
     @property
     def contact_mask(self) -> torch.Tensor:
-        """(N, 2) stone bitmasks of the two sensor feet (RF, LF) in the last substep."""
-        return self.state["contact_mask"].T
+        """(N, 4) stone bitmasks of the four sensor feet (RF, LF, RH, LH) in the last substep."""
+        return torch.cat([self.state["contact_mask"], self.state["contact_mask_hind"]], dim=0).T
 
     def close(self) -> None:
         if getattr(self, "_native", None) is not None:
             self._native.close()
             self._native = None
+
+
+# ANYdrive 3 with the DC motor model (isaaclab_assets/robots/anymal.py ANYDRIVE_3_SIMPLE_ACTUATOR_CFG) and
+# the ANYmal-C flat task's action scale (anymal_c_env_cfg.py: action_scale = 0.5)
+ANYDRIVE_3_SIMPLE = {"stiffness": 40.0, "damping": 5.0, "saturation_effort": 120.0, "effort_limit": 80.0,
+                     "velocity_limit": 7.5}
+ACTION_SCALE = 0.5
+# the C5 task constants (include/allsteps.h as_quad_task_t; authored, DESIGN.md §7b)
+QUAD_TASK = {"stop_frames": 2, "alive": 0.5, "action_cost": 0.005, "death": -2.0, "min_height": 0.25,
+             "up_z_min": 0.5, "max_episode_length": 1000, "step_dt": 4.0 / 240.0, "stand_height": 0.584,
+             "joint_noise": 0.05}
+
+
+class AnymalCStonesEnv(QuadrupedStonesEnv):
+    """BASELINE C5 task env: ``reset() -> obs``, ``step(actions) -> (obs, reward, terminated, truncated,
+    extras)`` with everything on the device (as_quad_reset_all / as_quad_step)."""
+
+    def __init__(self, num_envs: int, device: str = "cuda:0", seed: int = 42, cfg: AllstepsEnvCfg | None = None,
+                 task: dict | None = None):
+        self.task_cfg = dict(QUAD_TASK, **(task or {}))
+        super().__init__(num_envs, device, seed, cfg)
+        n, dev = self.num_envs, self.device
+        self._native.set_actuator(_native.ACT_DC_MOTOR, action_scale=ACTION_SCALE,
+                                  default_q=self.q_stand.cpu().tolist(), **ANYDRIVE_3_SIMPLE)
+        self._native.set_quad_task(**self.task_cfg)
+        self.obs_buf = torch.zeros((n, _native.QUAD_OBS_DIM), dtype=torch.float32, device=dev)
+        self.reward_buf = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.terminated_buf = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.truncated_buf = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.task_reset()
+
+    def task_reset(self) -> torch.Tensor:
+        self._native.quad_reset_all(self.obs_buf, stream=torch.cuda.current_stream(self.device).cuda_stream)
+        return self.obs_buf
+
+    def step(self, actions: torch.Tensor):
+        if actions.shape != (self.num_envs, self.num_dof) or actions.dtype != torch.float32:
+            raise ValueError(f"actions must be float32 ({self.num_envs}, {self.num_dof}), got "
+                             f"{tuple(actions.shape)} {actions.dtype}")
+        self._native.quad_step(actions.contiguous(), self.obs_buf, self.reward_buf, self.terminated_buf,
+                               self.truncated_buf, stream=torch.cuda.current_stream(self.device).cuda_stream)
+        return self.obs_buf, self.reward_buf, self.terminated_buf.bool(), self.truncated_buf.bool(), {}
+
+    @property
+    def target_index(self) -> torch.Tensor:
+        return self.state["idx"]

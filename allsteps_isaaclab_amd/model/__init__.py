@@ -105,7 +105,8 @@ def load_model(path: str = WALKER_JSON) -> dict:
     m["num_priority_geoms"] = sum(1 for t in geoms if t[0] == 0)
     m["self_pair"], m["num_self_pairs"] = self_collision_pairs(links, [(t[2], t[3]) for t in geoms])
     m["torso_link"] = bl[j.get("torso", "torso")]
-    m["foot_link"] = np.array(foot_link, np.int32)
+    m["foot_link"] = np.array(foot_link[:2], np.int32)  # body_pos FK slots (as_model_t.foot_link[2])
+    m["sensor_links"] = list(foot_link)
     m["link_names"] = [L["name"] for L in links]
     m["dof_names"] = list(j["cfg_dof_order"])
     m["total_mass"] = float(j["total_mass"])

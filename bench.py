@@ -21,8 +21,9 @@ Extra objects on the JSON line:
                   trainer over all ranks (scripts/bench_train.py: reference agent config, 32768 envs
                   per rank, horizon 32, 10 mini-epochs; N > 1: the --distributed path) -- reported
                   beside `value`, never as `value`.
-  c5           -- rank 0, N = 1 (BASELINE C5): the quadruped (model/anymal_c.xml) on the stones,
-                  physics only, 16384 envs (scripts/bench_quadruped.py) -- beside `value`.
+  c5           -- rank 0, N = 1 (BASELINE C5): the quadruped (model/anymal_c.xml) stepping-stone task
+                  (DC motor actuator in every substep, four foot sensors, task epilogue and resets in
+                  the timed loop), 16384 envs (scripts/bench_quadruped.py) -- beside `value`.
 """
 
 from __future__ import annotations
@@ -62,7 +63,7 @@ def parse():
                    help="oracle OpenMP threads (default: OMP_NUM_THREADS, else nproc; BASELINE.md §3)")
     p.add_argument("--no-train", action="store_true", help="skip the env+PPO trainer measurement")
     p.add_argument("--train-envs", type=int, default=32768)
-    p.add_argument("--no-c5", action="store_true", help="skip the quadruped (BASELINE C5) physics measurement")
+    p.add_argument("--no-c5", action="store_true", help="skip the quadruped (BASELINE C5) task measurement")
     return p.parse_args()
 
 

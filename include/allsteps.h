@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define AS_ABI_VERSION 2
+#define AS_ABI_VERSION 3
 #define AS_MAX_LINKS 32
 #define AS_MAX_GEOMS 32
 #define AS_MAX_SELF_PAIRS 256
@@ -41,6 +41,7 @@ extern "C" {
 #define AS_MAX_ROWS 30
 #define AS_OBS_DIM 59
 #define AS_ACT_DIM 21
+#define AS_QUAD_OBS_DIM 51
 
 enum {
   AS_OK = 0,
@@ -69,7 +70,8 @@ typedef struct {
   int32_t num_geoms;
   int32_t geom_link[AS_MAX_GEOMS];
   int32_t geom_type[AS_MAX_GEOMS];    /* 0 sphere, 1 capsule */
-  int32_t geom_foot[AS_MAX_GEOMS];    /* -1, 0 right foot, 1 left foot (contact sensors) */
+  int32_t geom_foot[AS_MAX_GEOMS];    /* contact sensor 0..3 or -1 (walker: 0 right, 1 left foot;
+                                         quadruped: RF, LF, RH, LH) */
   float geom_radius[AS_MAX_GEOMS];
   float geom_p0[AS_MAX_GEOMS][3];
   float geom_p1[AS_MAX_GEOMS][3];
@@ -146,7 +148,45 @@ typedef struct {
   uint32_t* episode;    /* [n] reset counter: Philox stream of the reset draws */
   uint32_t* contact_mask; /* [2][n] per-foot bitmask of stones with force > eps, last substep */
   int32_t* curriculum;  /* [1] */
+  uint32_t* contact_mask_hind; /* [2][n] contact sensors 2 and 3 (a quadruped's hind feet), or NULL */
 } as_state_t;
+
+/* Actuation of the physics step (as_set_actuator; as_create starts in AS_ACT_TORQUE).
+ *   AS_ACT_TORQUE:   tau = gain_curriculum[level] * gear * clip(a, -1, 1)  (the Allsteps walker,
+ *                    allsteps_env.py:267-274, an ImplicitActuator with kp = kd = 0);
+ *   AS_ACT_DC_MOTOR: joint position targets q* = default_q + action_scale * clip(a, -1, 1)
+ *                    (anymal_c_env.py:73-78), tracked by IsaacLab's DCMotor actuator evaluated in
+ *                    every physics substep: tau = kp (q* - q) + kd (0 - qd)  (IdealPD,
+ *                    actuator_pd.py:184-199), clipped to [tau_min(qd), tau_max(qd)] with
+ *                    tau_max = clip(sat (1 - qd / v_max), 0, effort_limit),
+ *                    tau_min = clip(sat (-1 - qd / v_max), -effort_limit, 0)  (actuator_pd.py:264-275). */
+enum { AS_ACT_TORQUE = 0, AS_ACT_DC_MOTOR = 1 };
+typedef struct {
+  int32_t mode;
+  float action_scale;
+  float default_q[AS_ACT_DIM];   /* cfg dof order */
+  float stiffness, damping;
+  float saturation_effort, effort_limit, velocity_limit;
+} as_actuator_t;
+
+/* The BASELINE C5 task: a quadruped crossing the Allsteps stones (authored here -- the reference has
+ * no quadruped stepping-stone task; its ANYmal-C task is flat-ground velocity tracking).  Per env step,
+ * after the physics substeps: episode counter; target tick (a front foot -- sensor 0 or
+ * 1 -- pushing on target stone idx for stop_frames steps advances idx); potential -|stone[idx] - root|_xy
+ * / step_dt; terminated = body tilted past up_z_min or below the target stone + min_height; truncated at
+ * max_episode_length; reward = (pot - old_pot) + alive - action_cost sum(a^2), death on termination;
+ * reset of done envs to the stand pose over stones 0 / 1 (+ U(-1,1) * joint_noise, Philox); observation
+ * [51] = root linear / angular velocity (body frame), projected gravity, stones idx and idx + 1 relative
+ * to the root (body frame), q - default_q, qd, the clipped actions. */
+typedef struct {
+  int32_t stop_frames;
+  float alive, action_cost, death;
+  float min_height, up_z_min;
+  int32_t max_episode_length;
+  float step_dt;
+  float stand_height;       /* root z above the higher of stones 0 / 1's top face at reset */
+  float joint_noise;
+} as_quad_task_t;
 
 typedef struct as_env as_env_t;
 
@@ -187,6 +227,17 @@ int as_set_seed(as_env_t* env, uint64_t seed);
 
 /* Physics only (decimation substeps, no task logic): for known-answer tests and profiling. */
 int as_physics_step(as_env_t* env, const float* actions, void* stream);
+
+/* Select the actuation of the physics step (AS_ACT_TORQUE / AS_ACT_DC_MOTOR, see as_actuator_t). */
+int as_set_actuator(as_env_t* env, const as_actuator_t* act_host);
+/* BASELINE C5: the quadruped stepping-stone task (as_quad_task_t).  as_quad_step = physics substeps
+ * (with the handle's actuator) + the task epilogue of every env, reset of done envs and the
+ * observation [n][AS_QUAD_OBS_DIM]; as_quad_reset_all resets every env.  Needs a model whose sensor
+ * feet 0..3 are the four feet and state->contact_mask_hind != NULL. */
+int as_set_quad_task(as_env_t* env, const as_quad_task_t* task_host);
+int as_quad_step(as_env_t* env, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                 uint8_t* truncated, void* stream);
+int as_quad_reset_all(as_env_t* env, float* obs, void* stream);
 
 /* _generate_foot_steps_allsteps (allsteps_env.py:125-174) on the device at curriculum `level`;
  * draws: [5][n][20] U[0,1) (NULL = Philox stream (seed, env, 0xF007)). Writes state->stones. */

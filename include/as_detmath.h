@@ -139,6 +139,19 @@ AS_HD void as_axis_angle_mat(const float* a, float ang, float* R) {
   R[6] = fmaf(tx, a[2], -(s * a[1])); R[7] = fmaf(ty, a[2], s * a[0]);   R[8] = fmaf(tz, a[2], c);
 }
 
+/* ---- actuators (include/allsteps.h as_actuator_t) */
+
+/* IsaacLab's DCMotor on a position target (actuator_pd.py:184-199, 264-275), torch's float32 order:
+ * tau = kp (q* - q) + kd (0 - qd) + 0, clipped to [clip(sat (-1 - qd / vmax), -lim, 0),
+ * clip(sat (1 - qd / vmax), 0, lim)] */
+AS_HD float as_dc_motor(float qt, float q, float qd, float kp, float kd, float sat, float lim, float vmax) {
+  const float tau = kp * (qt - q) + kd * (0.f - qd) + 0.f;
+  const float r = qd / vmax;
+  const float hi = fminf(fmaxf(sat * (1.f - r), 0.f), lim);
+  const float lo = fminf(fmaxf(sat * (-1.f - r), -lim), 0.f);
+  return fminf(fmaxf(tau, lo), hi);
+}
+
 /* ---- robot self-collision (walker3d.py:27 enabled_self_collisions; shared by kernel and oracle) */
 
 AS_HD float as_clamp01(float x) { return fminf(fmaxf(x, 0.f), 1.f); }

@@ -120,7 +120,26 @@ typedef struct {
   uint32_t *episode;                                   /* [n] reset counter (RNG stream) */
   uint32_t *contact_mask;                              /* [2][n] stone bitmask, last substep */
   int32_t *curriculum;                                 /* [1] */
+  uint32_t *contact_mask_hind;                         /* [2][n] sensors 2, 3 (quadruped) or NULL */
 } or_state_t;
+
+/* include/allsteps.h as_actuator_t / as_quad_task_t, field for field */
+typedef struct {
+  int32_t mode; /* 0 torque (tau = gain gear a), 1 DC motor on position targets */
+  float action_scale;
+  float default_q[21];
+  float stiffness, damping;
+  float saturation_effort, effort_limit, velocity_limit;
+} or_actuator_t;
+typedef struct {
+  int32_t stop_frames;
+  float alive, action_cost, death;
+  float min_height, up_z_min;
+  int32_t max_episode_length;
+  float step_dt;
+  float stand_height;
+  float joint_noise;
+} or_quad_task_t;
 
 /* ---- math helpers (isaaclab/utils/math.py) ---- */
 void or_euler_xyz_from_quat(const float q[4], float* roll, float* pitch, float* yaw);
@@ -159,6 +178,19 @@ void or_fk_bodies(const or_model_t* m, const float root_pos[3], const float root
                   float body_pos[9]);
 void or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
                      int env, const float* act_clamped);
+/* the same with an actuator (act NULL = torque mode): AS_ACT_DC_MOTOR recomputes the joint torques from
+ * the position targets default_q + action_scale a in every substep */
+void or_physics_step_act(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
+                         or_state_t* st, int env, const float* act_clamped);
+void or_dc_motor_batch(int n, const float* qt, const float* q, const float* qd, const or_actuator_t* act, float* tau);
+/* ---- BASELINE C5 quadruped task (quad.c; the HIP k_quad kernel's restatement) ---- */
+void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
+                          const or_quad_task_t* q, or_state_t* st, const float* actions, int reset_all,
+                          uint64_t seed, float* obs, float* rew, uint8_t* term, uint8_t* trunc);
+/* physics substeps (DC motor) + task epilogue, every env; actions [n][12] */
+void or_quad_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
+                  const or_quad_task_t* q, or_state_t* st, const float* actions, uint64_t seed, float* obs,
+                  float* rew, uint8_t* term, uint8_t* trunc, int nthreads);
 /* full env step: physics (decimation substeps) + task logic; obs [n][59] */
 void or_env_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
                  const float* actions, const float* reset_draws, uint64_t seed, float* obs, float* rew,
@@ -173,6 +205,7 @@ void or_mass_matrix(const or_model_t* m, const float root_pos[3], const float ro
 void or_bias_forces(const or_model_t* m, const float root_pos[3], const float root_quat[4], const float* q_int,
                     const float* u /* nv */, float gravity, float* C /* nv */);
 void or_philox_uniform(uint64_t seed, uint32_t env, uint32_t episode, int k, float* out);
+void or_philox_block(uint64_t seed, uint32_t env, uint32_t episode, uint32_t b, uint32_t tag, float out[4]);
 /* every env's course at `level` from the Philox "Ston" stream of (seed, env, episode[e] or 0) */
 void or_stones_philox(const or_task_t* task, int n, int level, uint64_t seed, const uint32_t* episode, float* stones);
 

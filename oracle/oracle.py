@@ -79,8 +79,20 @@ class OrState(C.Structure):
         ("n", C.c_int32), ("root_pos", FP), ("root_quat", FP), ("root_lin", FP), ("root_ang", FP), ("q", FP),
         ("qd", FP), ("stones", FP), ("pot", FP), ("old_pot", FP), ("foot_contact", FP), ("body_pos", FP),
         ("idx", IP), ("prev", IP), ("next", IP), ("count", IP), ("swing", IP), ("ep_len", IP), ("episode", UP),
-        ("contact_mask", UP), ("curriculum", IP),
+        ("contact_mask", UP), ("curriculum", IP), ("contact_mask_hind", UP),
     ]
+
+
+class OrActuator(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("action_scale", C.c_float), ("default_q", C.c_float * 21),
+                ("stiffness", C.c_float), ("damping", C.c_float), ("saturation_effort", C.c_float),
+                ("effort_limit", C.c_float), ("velocity_limit", C.c_float)]
+
+
+class OrQuadTask(C.Structure):
+    _fields_ = [("stop_frames", C.c_int32), ("alive", C.c_float), ("action_cost", C.c_float), ("death", C.c_float),
+                ("min_height", C.c_float), ("up_z_min", C.c_float), ("max_episode_length", C.c_int32),
+                ("step_dt", C.c_float), ("stand_height", C.c_float), ("joint_noise", C.c_float)]
 
 
 def build() -> str:
@@ -115,6 +127,12 @@ def lib() -> C.CDLL:
         L.or_philox_uniform.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, FP]
         L.or_physics_step.argtypes = [V, V, V, V, C.c_int, FP]
         L.or_probe_substep.argtypes = [V, V, V, V, C.c_int, FP, V]
+        L.or_physics_step_act.argtypes = [V, V, V, V, V, C.c_int, FP]
+        L.or_dc_motor_batch.argtypes = [C.c_int, FP, FP, FP, V, FP]
+        L.or_quad_post_physics.argtypes = [V, V, V, V, V, V, FP, C.c_int, C.c_uint64, FP, FP,
+                                           C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]
+        L.or_quad_step.argtypes = [V, V, V, V, V, V, FP, C.c_uint64, FP, FP, C.POINTER(C.c_uint8),
+                                   C.POINTER(C.c_uint8), C.c_int]
     return _LIB
 
 
@@ -227,7 +245,7 @@ class OracleState:
     FIELDS_F = {"root_pos": 3, "root_quat": 4, "root_lin": 3, "root_ang": 3, "q": 21, "qd": 21, "stones": 60,
                 "pot": 1, "old_pot": 1, "foot_contact": 2, "body_pos": 9}
     FIELDS_I = {"idx": 1, "prev": 1, "next": 1, "count": 1, "swing": 1, "ep_len": 1}
-    FIELDS_U = {"episode": 1, "contact_mask": 2}
+    FIELDS_U = {"episode": 1, "contact_mask": 2, "contact_mask_hind": 2}
 
     def __init__(self, n: int):
         self.n = n
@@ -295,6 +313,32 @@ class Oracle:
         for e in range(st.n):
             row = np.ascontiguousarray(a[e])
             self.L.or_physics_step(C.byref(self.model), C.byref(self.sim), C.byref(self.task), st.ptr, e, fp(row))
+
+    def physics_step_act(self, st: OracleState, act: OrActuator, actions):
+        """Physics only with an actuator (or_physics_step_act)."""
+        a = np.clip(np.ascontiguousarray(actions, np.float32), -1, 1)
+        for e in range(st.n):
+            row = np.ascontiguousarray(a[e])
+            self.L.or_physics_step_act(C.byref(self.model), C.byref(self.sim), C.byref(self.task), C.byref(act),
+                                       st.ptr, e, fp(row))
+
+    def quad_step(self, st: OracleState, act: OrActuator, q: OrQuadTask, actions, seed: int = 42, nthreads: int = 1):
+        n = st.n
+        obs = np.zeros((n, 51), np.float32)
+        rew = np.zeros(n, np.float32)
+        term = np.zeros(n, np.uint8)
+        trunc = np.zeros(n, np.uint8)
+        self.L.or_quad_step(C.byref(self.model), C.byref(self.sim), C.byref(self.task), C.byref(act), C.byref(q),
+                            st.ptr, fp(np.ascontiguousarray(actions, np.float32)), seed, fp(obs), fp(rew), u8p(term),
+                            u8p(trunc), nthreads)
+        return obs, rew, term.astype(bool), trunc.astype(bool)
+
+    def quad_reset_all(self, st: OracleState, act: OrActuator, q: OrQuadTask, seed: int = 42):
+        obs = np.zeros((st.n, 51), np.float32)
+        z = np.zeros(1, np.float32)
+        self.L.or_quad_post_physics(C.byref(self.model), C.byref(self.sim), C.byref(self.task), C.byref(act),
+                                    C.byref(q), st.ptr, fp(z), 1, seed, fp(obs), None, None, None)
+        return obs
 
     def probe(self, st: OracleState, e: int = 0, actions=None) -> dict:
         """The constraint set and contact impulses of env e's first substep, plus the stone impulses

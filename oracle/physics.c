@@ -564,8 +564,13 @@ static void tangents(const float n[3], float t1[3], float t2[3]) {
   cross(n, t1, t2);
 }
 
-static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3], float root_quat[4], float* q_int,
-                    float* u, const float* tau_int, const float* stones_w, int nst, uint32_t mask[2]) {
+static void substep(const or_model_t* m, const or_sim_t* sim, const or_actuator_t* act, const float* qt_int,
+                    float root_pos[3], float root_quat[4], float* q_int, float* u, float* tau_int,
+                    const float* stones_w, int nst, uint32_t mask[4]) {
+  if (act && act->mode == 1) /* the DC motor runs in every substep (as_dc_motor, include/as_detmath.h) */
+    for (int i = 0; i < m->num_hinges; ++i)
+      tau_int[i] = as_dc_motor(qt_int[i], q_int[i], u[OR_NDOF_ROOT + i], act->stiffness, act->damping,
+                               act->saturation_effort, act->effort_limit, act->velocity_limit);
   kin_t K;
   kinematics(m, root_quat, q_int, &K);
   const int nv = K.nv, nh = m->num_hinges;
@@ -717,7 +722,7 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
     }
   }
   /* contact sensor flags of this substep: |sum_n lambda_n n| / dt > eps per (foot, stone) */
-  mask[0] = mask[1] = 0u;
+  mask[0] = mask[1] = mask[2] = mask[3] = 0u;
   for (int c = 0; c < Cn.n; ++c) {
     if (Cn.foot[c] < 0) continue;
     float fx = 0.f, fy = 0.f, fz = 0.f;
@@ -727,7 +732,7 @@ static void substep(const or_model_t* m, const or_sim_t* sim, float root_pos[3],
       fx += l * Cn.nrm[c2][0]; fy += l * Cn.nrm[c2][1]; fz += l * Cn.nrm[c2][2];
     }
     float fn = sqrtf(fx * fx + fy * fy + fz * fz) / dt;
-    if (fn > 1e-4f) mask[Cn.foot[c]] |= 1u << Cn.stone[c];
+    if (fn > 1e-4f) mask[Cn.foot[c] & 3] |= 1u << Cn.stone[c];
   }
   if (g_probe) {
     or_probe_t* P = g_probe;
@@ -789,26 +794,28 @@ void or_fk_bodies(const or_model_t* m, const float root_pos[3], const float root
     for (int k = 0; k < 3; ++k) body_pos[3 * b + k] = root_pos[k] + K.p[ls[b]][k];
 }
 
-void or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st, int e,
-                     const float* act_clamped) {
+void or_physics_step_act(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
+                         or_state_t* st, int e, const float* act_clamped) {
   const int n = st->n, nh = m->num_hinges;
-  float rp[3], rq[4], q_int[OR_MAX_LINKS], u[NV_MAX], tau[OR_MAX_LINKS], stones[OR_MAX_STONES * 3];
+  float rp[3], rq[4], q_int[OR_MAX_LINKS], u[NV_MAX], tau[OR_MAX_LINKS], qt[OR_MAX_LINKS], stones[OR_MAX_STONES * 3];
   for (int k = 0; k < 3; ++k) rp[k] = F(st->root_pos, k, n, e);
   for (int k = 0; k < 4; ++k) rq[k] = F(st->root_quat, k, n, e);
   for (int k = 0; k < 3; ++k) { u[k] = F(st->root_lin, k, n, e); u[3 + k] = F(st->root_ang, k, n, e); }
-  /* ENV:270-274 _apply_action: tau = gain[curriculum] * gear * a (ImplicitActuator pass-through) */
+  /* ENV:270-274 _apply_action: tau = gain[curriculum] * gear * a (ImplicitActuator pass-through); with a
+   * DC motor, position targets default + scale a (anymal_c_env.py:73-74) */
   float gain = task->gain_curriculum[st->curriculum[0]];
   for (int k = 0; k < nh; ++k) {
     int i = m->cfg_dof_link[k] - 1;
     q_int[i] = F(st->q, k, n, e);
     u[OR_NDOF_ROOT + i] = F(st->qd, k, n, e);
     tau[i] = gain * m->gear[k] * act_clamped[k];
+    qt[i] = act ? act->action_scale * act_clamped[k] + act->default_q[k] : 0.f;
   }
   const int nst = task->num_steps;
   for (int s = 0; s < nst; ++s)
     for (int k = 0; k < 3; ++k) stones[3 * s + k] = F(st->stones, s * 3 + k, n, e);
-  uint32_t mask[2] = {0u, 0u};
-  for (int s = 0; s < sim->substeps; ++s) substep(m, sim, rp, rq, q_int, u, tau, stones, nst, mask);
+  uint32_t mask[4] = {0u, 0u, 0u, 0u};
+  for (int s = 0; s < sim->substeps; ++s) substep(m, sim, act, qt, rp, rq, q_int, u, tau, stones, nst, mask);
   for (int k = 0; k < 3; ++k) {
     F(st->root_pos, k, n, e) = rp[k];
     F(st->root_lin, k, n, e) = u[k];
@@ -822,10 +829,26 @@ void or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* 
   }
   F(st->contact_mask, 0, n, e) = mask[0];
   F(st->contact_mask, 1, n, e) = mask[1];
+  if (st->contact_mask_hind) {
+    F(st->contact_mask_hind, 0, n, e) = mask[2];
+    F(st->contact_mask_hind, 1, n, e) = mask[3];
+  }
   float bp[9], qc[OR_MAX_LINKS];
   for (int k = 0; k < nh; ++k) qc[k] = F(st->q, k, n, e);
   or_fk_bodies(m, rp, rq, qc, bp);
   for (int c = 0; c < 9; ++c) F(st->body_pos, c, n, e) = bp[c];
+}
+
+/* known-answer hook: the DC motor torque of include/as_detmath.h for n inputs */
+void or_dc_motor_batch(int n, const float* qt, const float* q, const float* qd, const or_actuator_t* act, float* tau) {
+  for (int i = 0; i < n; ++i)
+    tau[i] = as_dc_motor(qt[i], q[i], qd[i], act->stiffness, act->damping, act->saturation_effort, act->effort_limit,
+                         act->velocity_limit);
+}
+
+void or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st, int e,
+                     const float* act_clamped) {
+  or_physics_step_act(m, sim, task, NULL, st, e, act_clamped);
 }
 
 /* ---------------------------------------------------------------- env-level API */
@@ -849,9 +872,9 @@ void or_probe_substep(const or_model_t* m, const or_sim_t* sim, const or_task_t*
   for (int s = 0; s < nst; ++s)
     for (int k = 0; k < 3; ++k) stones[3 * s + k] = F(st->stones, s * 3 + k, n, e);
   memset(out, 0, sizeof(*out));
-  uint32_t mask[2] = {0u, 0u};
+  uint32_t mask[4] = {0u, 0u, 0u, 0u};
   g_probe = out;
-  for (int sub = 0; sub < sim->substeps; ++sub) substep(m, sim, rp, rq, q_int, u, tau, stones, nst, mask);
+  for (int sub = 0; sub < sim->substeps; ++sub) substep(m, sim, NULL, NULL, rp, rq, q_int, u, tau, stones, nst, mask);
   g_probe = NULL;
 }
 

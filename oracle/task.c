@@ -184,6 +184,14 @@ static void philox4x32_10(uint32_t ctr[4], const uint32_t key_in[2]) {
   }
 }
 
+/* 4 uniforms of block b of the (env, episode) stream with counter tag `tag` (the kernels' philox_block) */
+void or_philox_block(uint64_t seed, uint32_t env, uint32_t episode, uint32_t b, uint32_t tag, float out[4]) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t ctr[4] = {env, episode, b, tag};
+  philox4x32_10(ctr, key);
+  for (int j = 0; j < 4; ++j) out[j] = (float)(ctr[j] >> 8) * (1.0f / 16777216.0f);
+}
+
 /* draws k = 0..21 of env `env`'s `episode`-th reset: U[0,1) with 24-bit mantissa */
 void or_philox_uniform(uint64_t seed, uint32_t env, uint32_t episode, int k, float* out) {
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};

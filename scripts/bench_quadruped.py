@@ -1,11 +1,12 @@
-"""BASELINE C5 throughput: the quadruped (model/anymal_c.xml) on the stones, physics only, 1 GPU.
+"""BASELINE C5 throughput: the quadruped (model/anymal_c.xml) on the stones with its task, 1 GPU.
 
     python scripts/bench_quadruped.py [--num_envs 16384] [--steps 500] [--warmup 20]
 
-A step = 4 substeps of k_step<18> for every env (as_physics_step) under a joint PD on the ANYmal
-stance plus fresh U(-0.3, 0.3) perturbation actions (pre-drawn on the device); the PD's few torch
-elementwise ops are inside the timed region.  No task / resets (the reference has no Allsteps task
-for ANYmal), so this is the physics half of C5 only.  Prints one JSON line.
+A step = ``AnymalCStonesEnv.step`` = as_quad_step: 4 substeps of k_step<18> for every env with the DC
+motor actuator evaluated in each substep (position targets default + 0.5 a), then k_quad (target
+stones, potentials, rewards, dones, in-kernel resets, the 51-float observation).  Actions: U(-1, 1),
+fresh every step (pre-drawn on the device).  Episodes end and reset inside the timed region.  Prints
+one JSON line.
 """
 
 from __future__ import annotations
@@ -23,26 +24,28 @@ import torch  # noqa: E402
 
 
 def measure(num_envs: int = 16384, steps: int = 500, warmup: int = 20, device: str = "cuda:0") -> dict:
-    from allsteps_isaaclab_amd.envs.quadruped import QuadrupedStonesEnv
+    from allsteps_isaaclab_amd.envs.quadruped import AnymalCStonesEnv
 
-    env = QuadrupedStonesEnv(num_envs, device)
+    env = AnymalCStonesEnv(num_envs, device)
     gen = torch.Generator(device=device).manual_seed(7)
-    noise = (torch.rand(steps + warmup, num_envs, 12, device=device, generator=gen) * 2 - 1) * 0.3
+    acts = torch.rand(steps + warmup, num_envs, 12, device=device, generator=gen) * 2 - 1
     for t in range(warmup):
-        env.step(env.stand_actions() + noise[steps + t])
+        env.step(acts[steps + t])
     torch.cuda.synchronize(device)
+    dones = torch.zeros((), dtype=torch.int64, device=device)
     t0 = time.perf_counter()
     for t in range(steps):
-        env.step(env.stand_actions() + noise[t])
+        _, _, term, trunc, _ = env.step(acts[t])
+        dones += (term | trunc).sum()
     torch.cuda.synchronize(device)
     el = time.perf_counter() - t0
-    standing = float((env.root_pos[:, 2] > 0.5).float().mean())
     env.close()
-    return {"metric": "env-steps/sec, quadruped (ANYmal-C approximation) on ALLSTEPS stones, physics only",
+    return {"metric": "env-steps/sec, quadruped (ANYmal-C approximation) stepping-stone task (DC motor, 4 foot "
+                      "sensors, resets in the loop)",
             "value": round(num_envs * steps / el, 1), "unit": "env-steps/s", "n_gpus": 1, "num_envs": num_envs,
-            "steps": steps, "ms_per_step": round(el / steps * 1e3, 4), "dof": 12, "kernel": "k_step<18>",
-            "standing_fraction_end": round(standing, 4),
-            "data": "synthetic (PD stance + U(-0.3,0.3) perturbations, level-0 stones)"}
+            "steps": steps, "ms_per_step": round(el / steps * 1e3, 4), "dof": 12, "kernels": "k_step<18> + k_quad",
+            "resets_per_step": round(float(dones.item()) / steps, 1),
+            "data": "synthetic (U(-1,1) actions, level-0 stones, stand-pose resets)"}
 
 
 def main():

@@ -52,9 +52,10 @@ def test_quadruped_model_tables(qmodel):
     assert 45.0 < m["total_mass"] < 52.0
     # the four feet are the first geoms (a foot contact is never dropped for a body contact)
     assert m["geom_name"][:4] == ["LF_FOOT", "LH_FOOT", "RF_FOOT", "RH_FOOT"]
-    # sensor feet: RF -> 0, LF -> 1, the others unsensed
+    # sensor feet: RF -> 0, LF -> 1, RH -> 2, LH -> 3
     foot = dict(zip(m["geom_name"], m["geom_foot"][: m["num_geoms"]]))
-    assert foot["RF_FOOT"] == 0 and foot["LF_FOOT"] == 1 and foot["LH_FOOT"] == -1 and foot["base_geom"] == -1
+    assert foot["RF_FOOT"] == 0 and foot["LF_FOOT"] == 1 and foot["RH_FOOT"] == 2 and foot["LH_FOOT"] == 3
+    assert foot["base_geom"] == -1
     np.testing.assert_allclose(m["gear"][:12], 80.0 / 1.2, rtol=1e-6)
 
 

@@ -1,0 +1,196 @@
+"""BASELINE C5 as a task: the ANYmal-C-like quadruped on the stones with IsaacLab's DC motor actuator in
+every physics substep, four foot sensors and the stepping-stone task epilogue (include/allsteps.h
+as_quad_task_t, oracle/quad.c, the HIP k_quad kernel).
+
+CPU: the DC motor torque against IsaacLab's formulas (actuator_pd.py:184-199, 264-275) restated in torch
+float32; the task epilogue's rules on constructed states (target tick, potentials, tilt / height
+termination, truncation, resets).  GPU: the whole C5 step (physics + task) at the C5 size (16384 envs)
+bit-identical to the oracle over 20 steps, every state field, observation, reward and done flag.
+"""
+
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from allsteps_isaaclab_amd.envs.quadruped import ACTION_SCALE, ANYDRIVE_3_SIMPLE, QUAD_TASK, level0_stones, stand_pose
+
+
+@pytest.fixture(scope="module")
+def qmodel():
+    from allsteps_isaaclab_amd.model import ANYMAL_C_JSON, load_model
+
+    return load_model(ANYMAL_C_JSON)
+
+
+@pytest.fixture(scope="module")
+def qorc(oracle_mod, qmodel):
+    return oracle_mod.Oracle(model=qmodel)
+
+
+def _act_struct(oracle_mod, qmodel):
+    A = oracle_mod.OrActuator()
+    A.mode = 1
+    A.action_scale = ACTION_SCALE
+    A.default_q[:12] = [float(x) for x in stand_pose(qmodel["dof_names"])]
+    for k, v in ANYDRIVE_3_SIMPLE.items():
+        setattr(A, k, v)
+    return A
+
+
+def _task_struct(oracle_mod):
+    Q = oracle_mod.OrQuadTask()
+    for k, v in QUAD_TASK.items():
+        setattr(Q, k, v)
+    return Q
+
+
+def test_dc_motor_matches_isaaclab_formulas(oracle_mod, qmodel):
+    """actuator_pd.py IdealPD (tau = kp (q* - q) + kd (qd* - qd) + tau_ff) + DCMotor._clip_effort, in
+    torch float32 on the CPU, vs the kernel / oracle arithmetic (as_dc_motor) -- bit for bit."""
+    rng = np.random.default_rng(0)
+    n = 4096
+    qt = rng.uniform(-2, 2, n).astype(np.float32)
+    q = rng.uniform(-2, 2, n).astype(np.float32)
+    qd = rng.uniform(-12, 12, n).astype(np.float32)  # past the 7.5 rad/s limit on purpose
+    A = _act_struct(oracle_mod, qmodel)
+    tau = np.zeros(n, np.float32)
+    L = oracle_mod.lib()
+    L.or_dc_motor_batch(n, oracle_mod.fp(qt), oracle_mod.fp(q), oracle_mod.fp(qd), C.byref(A), oracle_mod.fp(tau))
+    T = {k: torch.from_numpy(v) for k, v in (("qt", qt), ("q", q), ("qd", qd))}
+    kp, kd = torch.tensor(A.stiffness), torch.tensor(A.damping)
+    computed = kp * (T["qt"] - T["q"]) + kd * (torch.zeros(n) - T["qd"]) + torch.zeros(n)
+    sat, lim, vlim = A.saturation_effort, A.effort_limit, A.velocity_limit
+    max_e = torch.clip(sat * (1.0 - T["qd"] / vlim), min=torch.zeros(n), max=torch.full((n,), lim))
+    min_e = torch.clip(sat * (-1.0 - T["qd"] / vlim), min=torch.full((n,), -lim), max=torch.zeros(n))
+    ref = torch.clip(computed, min=min_e, max=max_e).numpy()
+    np.testing.assert_array_equal(tau, ref)
+    assert (np.abs(tau) <= lim).all() and (tau[qd > 7.5 * (1 + 80 / 120)] <= 0).all()
+
+
+def _post(qorc, oracle_mod, qmodel, st, actions, reset_all=False):
+    n = st.n
+    obs = np.zeros((n, 51), np.float32)
+    rew = np.zeros(n, np.float32)
+    term = np.zeros(n, np.uint8)
+    trunc = np.zeros(n, np.uint8)
+    O = oracle_mod
+    qorc.L.or_quad_post_physics(C.byref(qorc.model), C.byref(qorc.sim), C.byref(qorc.task),
+                                C.byref(_act_struct(O, qmodel)), C.byref(_task_struct(O)), st.ptr,
+                                O.fp(np.ascontiguousarray(actions, np.float32)), int(reset_all), 42, O.fp(obs),
+                                O.fp(rew), O.u8p(term), O.u8p(trunc))
+    return obs, rew, term.astype(bool), trunc.astype(bool)
+
+
+def _stand_state(qorc, oracle_mod, qmodel, n):
+    st = qorc.state(n)
+    st["stones"][:] = level0_stones(n)
+    _post(qorc, oracle_mod, qmodel, st, np.zeros((n, 12), np.float32), reset_all=True)
+    return st
+
+
+def test_task_reset_pose_and_observation(qorc, oracle_mod, qmodel):
+    n = 8
+    st = _stand_state(qorc, oracle_mod, qmodel, n)
+    q0 = stand_pose(qmodel["dof_names"])
+    assert np.abs(st["q"][:12].T - q0).max() <= QUAD_TASK["joint_noise"]
+    np.testing.assert_allclose(st["root_pos"][:, 0], [0.375, 0.0, 0.1125 + QUAD_TASK["stand_height"]], atol=1e-6)
+    assert (st["idx"] == 2).all() and (st["episode"] == 1).all()
+    obs, *_ = _post(qorc, oracle_mod, qmodel, st, np.zeros((n, 12), np.float32), reset_all=True)
+    np.testing.assert_allclose(obs[:, 6:9], [[0, 0, -1]] * n, atol=1e-7)      # projected gravity, upright
+    np.testing.assert_allclose(obs[0, 9:12], [1.5 - 0.375, 0.0, -0.1125 - 0.584], atol=1e-5)  # stone 2, body frame
+    np.testing.assert_allclose(obs[0, 12:15], [2.25 - 0.375, 0.0, -0.1125 - 0.584], atol=1e-5)
+    # different envs, different Philox joint noise; the same env and episode, the same draws
+    assert np.abs(st["q"][:12, 0] - st["q"][:12, 1]).max() > 0
+
+
+def test_task_tick_potential_and_dones(qorc, oracle_mod, qmodel):
+    n = 6
+    st = _stand_state(qorc, oracle_mod, qmodel, n)
+    a = np.zeros((n, 12), np.float32)
+    # env 0: RF on the target stone (2) for stop_frames steps -> target 3
+    # env 1: a hind foot on stone 2 -> no tick (front feet only)
+    # env 2: tilted 70 degrees about x -> terminated (death reward), reset
+    # env 3: body 0.2 m above the target stone's centre -> terminated
+    # env 4: at the episode limit -> truncated, reset, not terminated
+    # env 5: actions cost: reward = progress + alive - cost sum(a^2)
+    ang = np.deg2rad(70.0)
+    for step in range(QUAD_TASK["stop_frames"]):
+        st["contact_mask"][0, 0] = 1 << 2
+        st["contact_mask_hind"][0, 1] = 1 << 2
+        if step == QUAD_TASK["stop_frames"] - 1:
+            st["root_quat"][:, 2] = [np.cos(ang / 2), np.sin(ang / 2), 0, 0]
+            st["root_pos"][2, 3] = 0.2
+            st["ep_len"][4] = QUAD_TASK["max_episode_length"] - 1
+            a[5] = 0.5
+        pot_before = st["pot"].copy()
+        obs, rew, term, trunc = _post(qorc, oracle_mod, qmodel, st, a)
+    assert st["idx"][0] == 3 and st["count"][0] == 0
+    assert st["idx"][1] == 2 and st["count"][1] == 0
+    assert term.tolist() == [False, False, True, True, False, False]
+    assert trunc.tolist() == [False, False, False, False, True, False]
+    assert rew[2] == QUAD_TASK["death"] and rew[3] == QUAD_TASK["death"]
+    # done envs were reset: stand pose, target 2, episode counter advanced
+    for e in (2, 3, 4):
+        assert st["idx"][e] == 2 and st["ep_len"][e] == 0 and st["episode"][e] == 2
+        np.testing.assert_array_equal(st["root_quat"][:, e], [1, 0, 0, 0])
+    # reward of a live env: potential progress + alive - action cost
+    prog = np.float32(st["pot"][5]) - np.float32(pot_before[5])
+    expect = prog + np.float32(QUAD_TASK["alive"]) - np.float32(QUAD_TASK["action_cost"]) * np.float32(12 * 0.25)
+    assert abs(rew[5] - expect) < 1e-5
+
+
+def test_task_stands_on_four_feet(qorc, oracle_mod, qmodel):
+    """zero actions = the default-pose targets: the DC motors (kp 40, kd 5) hold the stance on stones 0 / 1
+    for a second, all four foot sensors see their stone, nothing terminates.  (On this authored model
+    the soft gains let the stance creep forward over a few seconds -- a policy has to hold it.)"""
+    n = 4
+    st = _stand_state(qorc, oracle_mod, qmodel, n)
+    act, Q = _act_struct(oracle_mod, qmodel), _task_struct(oracle_mod)
+    for _ in range(60):
+        obs, rew, term, trunc = qorc.quad_step(st, act, Q, np.zeros((n, 12), np.float32))
+        assert not term.any()
+    sensors = [qmodel["geom_name"][g] for g in range(qmodel["num_geoms"]) if qmodel["geom_foot"][g] >= 0]
+    assert sorted(sensors) == ["LF_FOOT", "LH_FOOT", "RF_FOOT", "RH_FOOT"]
+    assert (st["contact_mask"] == 1 << 1).all() and (st["contact_mask_hind"] == 1 << 0).all()
+    assert np.abs(st["root_lin"]).max() < 0.1 and (st["root_pos"][2] > 0.6).all()
+
+
+# ------------------------------------------------------------------------------------------------ GPU
+
+
+@pytest.mark.gpu
+def test_c5_task_gpu_bit_exact_vs_oracle(qorc, oracle_mod, qmodel):
+    from allsteps_isaaclab_amd.envs.quadruped import AnymalCStonesEnv
+
+    n, steps = 16384, 20  # BASELINE C5
+    env = AnymalCStonesEnv(n, "cuda:0")
+    gen = torch.Generator(device="cuda:0").manual_seed(7)
+    for _ in range(60):  # a second of random actions on the GPU first: robots falling and resetting
+        env.step((torch.rand(n, 12, device="cuda:0", generator=gen) * 2.4 - 1.2).contiguous())
+    torch.cuda.synchronize()
+    st = qorc.state(n)
+    for k, v in env.state.items():
+        if k != "curriculum":
+            st[k][...] = v.cpu().numpy().reshape(st[k].shape).view(st[k].dtype)
+    act, Q = _act_struct(oracle_mod, qmodel), _task_struct(oracle_mod)
+    total_resets = 0
+    for t in range(steps):
+        a = (torch.rand(n, 12, device="cuda:0", generator=gen) * 2.4 - 1.2).contiguous()
+        obs_g, rew_g, term_g, trunc_g, _ = env.step(a)
+        torch.cuda.synchronize()
+        obs_c, rew_c, term_c, trunc_c = qorc.quad_step(st, act, Q, a.cpu().numpy(), seed=42, nthreads=16)
+        g = {k: v.cpu().numpy() for k, v in env.state.items()}
+        bad = [k for k in st.a if k != "curriculum"
+               and not np.array_equal(g[k].view(st[k].dtype).reshape(st[k].shape), st[k])]
+        resets = int((term_c | trunc_c).sum())
+        total_resets += resets
+        print(f"[c5 exact] step {t}: {len(bad)} state fields differ {bad}, resets {resets}, "
+              f"front-foot contacts {int((st['contact_mask'] != 0).any(axis=0).sum())}")
+        assert not bad
+        np.testing.assert_array_equal(obs_g.cpu().numpy(), obs_c)
+        np.testing.assert_array_equal(rew_g.cpu().numpy(), rew_c)
+        assert np.array_equal(term_g.cpu().numpy(), term_c) and np.array_equal(trunc_g.cpu().numpy(), trunc_c)
+    assert total_resets > 0  # robots fall and reset inside the compared steps: the reset path is exercised
+    env.close()
