@@ -143,7 +143,8 @@ def test_quadruped_gpu_matches_oracle(qorc, qmodel, warm):
     torch.cuda.synchronize()
     qorc.physics_step(st, act.cpu().numpy())
     g = {k: v.cpu().numpy() for k, v in env.state.items()}
-    mask_eq = (g["contact_mask"].view(np.uint32) == st["contact_mask"]).all(axis=0)
+    mask_eq = ((g["contact_mask"].view(np.uint32) == st["contact_mask"]).all(axis=0)
+               & (g["contact_mask_hind"].view(np.uint32) == st["contact_mask_hind"]).all(axis=0))
     print(f"quadruped parity warm={warm}: contact bits differ on {np.count_nonzero(~mask_eq)} of {n} envs")
     assert mask_eq.all(), f"contact bits differ on {np.count_nonzero(~mask_eq)} envs"
     # the same float32 operations in the same order on both sides (include/as_detmath.h): bit-exact
@@ -162,7 +163,8 @@ def test_quadruped_gpu_stance_and_c5_size_properties():
     torch.cuda.synchronize()
     z = env.root_pos[:, 2]
     assert bool(((z > 0.64) & (z < 0.70)).all())
-    assert bool((env.contact_mask == 2).all()), "front feet must rest on stone 1"
+    # sensors RF, LF on stone 1; RH, LH on stone 0
+    assert bool((env.contact_mask == torch.tensor([2, 2, 1, 1], device="cuda:0", dtype=torch.int32)).all())
     # perturbed stepping (the bench's protocol): every env stays finite, nearly all keep standing,
     # and no base (capsule radius 0.12) sinks into a stone it is above (a robot may legitimately
     # slip into the 0.25 m gap between stones and fall below their tops)
