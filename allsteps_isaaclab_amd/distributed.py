@@ -17,6 +17,7 @@ collective inside ``env.step``.
 
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 
@@ -62,7 +63,8 @@ def init_process_group(backend: str | None = None) -> ShardInfo:
     if info.world > 1 and not dist.is_initialized():
         if backend is None:  # ALLSTEPS_DIST_BACKEND overrides (e.g. gloo for ranks sharing one GPU in tests)
             backend = os.environ.get("ALLSTEPS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-        kw = {}
+        # a rank that dies or stalls ends the others' collectives after this long instead of hanging them
+        kw = {"timeout": datetime.timedelta(seconds=float(os.environ.get("ALLSTEPS_DIST_TIMEOUT_S", "600")))}
         if backend == "nccl":
             torch.cuda.set_device(info.local_rank)
             kw["device_id"] = torch.device(f"cuda:{info.local_rank}")

@@ -19,8 +19,9 @@ Extra objects on the JSON line:
                   host's cores on a bounded sample.
   train        -- every rank (BASELINE C4, SURVEY §8d "env+PPO separately"): env-steps/s of the PPO
                   trainer over all ranks (scripts/bench_train.py: reference agent config, 32768 envs
-                  per rank, horizon 32, 10 mini-epochs; N > 1: the --distributed path) -- reported
-                  beside `value`, never as `value`.
+                  per rank, horizon 32, 10 mini-epochs; N > 1: the --distributed path), one child
+                  process per rank with a time limit (train_leg) -- reported beside `value`, never as
+                  `value`.
   c5           -- rank 0, N = 1 (BASELINE C5): the quadruped (model/anymal_c.xml) stepping-stone task
                   (DC motor actuator in every substep, four foot sensors, task epilogue and resets in
                   the timed loop), 16384 envs (scripts/bench_quadruped.py) -- beside `value`.
@@ -29,6 +30,7 @@ Extra objects on the JSON line:
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -149,6 +151,46 @@ def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int
                       f"{warm_steps} warm-up steps), OpenMP {threads} threads, {el:.2f} s wall"}
 
 
+def train_leg(args, world: int, rank: int, backend: str, device, timeout_s: float = 300.0) -> dict:
+    """env + PPO (BASELINE C4) in a child process per rank (scripts/bench_train.py; at N ranks its own
+    process group on a fresh port, the trainer's --distributed path: one RCCL all-reduce of
+    [grads | kl] per minibatch).  A child that fails or stalls is killed after `timeout_s` and reported
+    as an error: the env metric on the line never waits on the trainer's collectives."""
+    import signal
+    import socket
+    import subprocess
+
+    port = 0
+    if rank == 0:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+    if world > 1:  # every rank's child joins rank 0's port
+        t = torch.tensor([port], dtype=torch.int64, device=device if backend == "nccl" else "cpu")
+        dist.broadcast(t, 0)
+        port = int(t.item())
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="False",
+               ALLSTEPS_DIST_TIMEOUT_S=str(int(timeout_s)))
+    cmd = [sys.executable, os.path.join(ROOT, "scripts", "bench_train.py"), "--num_envs", str(args.train_envs),
+           "--epochs", "2", "--warmup", "2", "--quiet"] + (["--distributed"] if world > 1 else [])
+    p = subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        return {"error": f"train child exceeded {timeout_s:.0f} s and was killed"}
+    if p.returncode != 0:
+        return {"error": f"train child exit {p.returncode}: {err.strip()[-600:]}"}
+    if rank != 0:
+        return {}
+    try:
+        return json.loads(out.strip().splitlines()[-1])
+    except (IndexError, ValueError):
+        return {"error": f"train child printed no result line: {out[-300:]} {err[-300:]}"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -161,10 +203,11 @@ def main():
     torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        timeout = datetime.timedelta(seconds=600)  # a stalled rank ends the job instead of hanging it
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=device, timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
 
     from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv
     from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
@@ -257,16 +300,10 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(n, args.level, args.cpu_threads)
     env.close()
+    del env, actions
+    torch.cuda.empty_cache()
     if not args.no_train:
-        # env + PPO (BASELINE C4: 32768 envs per rank; at N ranks the trainer's --distributed path, one
-        # RCCL all-reduce of [grads | kl] per minibatch): every rank trains, rank 0 reports
-        sys.path.insert(0, os.path.join(ROOT, "scripts"))
-        import bench_train
-
-        try:
-            train = bench_train.measure(args.train_envs, epochs=2, warmup=2, verbose=False, distributed=world > 1)
-        except Exception as e:  # reported, never fatal for the env metric
-            train = {"error": f"{type(e).__name__}: {e}"}
+        train = train_leg(args, world, rank, backend, device)
         if rank == 0:
             line["train"] = train
         elif "error" in train:

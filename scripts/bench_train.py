@@ -87,8 +87,17 @@ def main():
     ap.add_argument("--epochs", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--level", type=int, default=None, help="initial stone curriculum level (C3: 9)")
+    ap.add_argument("--distributed", action="store_true", help="one rank per GPU under torch.distributed.run")
+    ap.add_argument("--quiet", action="store_true", help="only the result line (rank 0)")
     args = ap.parse_args()
-    print(json.dumps(measure(args.num_envs, args.epochs, args.warmup, args.level)))
+    out = measure(args.num_envs, args.epochs, args.warmup, args.level, verbose=not args.quiet,
+                  distributed=args.distributed)
+    import torch.distributed as dist
+
+    if not (dist.is_initialized() and dist.get_rank() != 0):
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
