@@ -38,6 +38,7 @@ constexpr int kPairsPerChunk = G;   // one lane per (stone, geom) pair in the ex
 static_assert(kPairsPerChunk - 1 + G <= 64, "pending pair list (PhaseScratch::col.pl)");
 constexpr int kSweepB = 4;        // pivot block of the H^-1 sweep
 typedef float v4f __attribute__((ext_vector_type(4)));  // native 16-B vector (LDS b128 accesses)
+typedef float v2f __attribute__((ext_vector_type(2)));  // register pair (packed FP32 math)
 
 static_assert(NVMAX <= G, "one lane per generalized velocity");
 static_assert(LMAX <= G, "one lane per link");
@@ -1107,13 +1108,6 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   ts.count(nrow, nc);
   __syncthreads();
   if (threadIdx.x == 0) sm.maxrow = max(sm.env[0].nrow, sm.env[1].nrow);
-  ts.mark(kStRows);
-  // ---- J and W = H^-1 J^T columns (lane = dof j), kept in LDS [row][dof]:
-  //      J_rj = S_j . f6_r on the contact link's path (ancestor bitmask), +-1 at a limited dof
-  float Sj[6];
-  const int jl = lane < NV ? lane : 0;
-#pragma unroll
-  for (int a = 0; a < 6; ++a) Sj[a] = s.S[jl][a];
   __syncthreads();
   const int maxrow = sm.maxrow;
   // Issue priority by constraint load: the two waves of a SIMD are arbitrated by priority, then
@@ -1128,46 +1122,57 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
   }
-  const uint32_t dsub = tp.dsub;
-  // Rows are handled in groups of three (a contact's normal / tangent / tangent triplet, or three
-  // consecutive limit rows; MAXR is a multiple of 3).  Rows of the last group at or past maxrow are
-  // written as zero / ignored.
-  static_assert(MAXR % kRowGroup == 0, "row groups");
-#pragma unroll 1
-  for (int r0 = 0; r0 < maxrow; r0 += kRowGroup) {
-    // all inputs of the group are read before any row is stored, so the group's reads overlap
-    const int c = r0 / 3;  // contact of the triplet (r0 < 3 MAXC = MAXR)
-    float P[3], dir[kRowGroup][3], sg[kRowGroup];
-    int lk[kRowGroup];
+  // ---- J rows, one lane per row (lane r < MAXR), kept in LDS [row][dof]: a contact row is
+  //      J_rj = S_j . f6_r for the dofs whose link lies on the path root..link(r) (lpath of the
+  //      row's link; dof j < 6 moves every link), minus the same on the second link's path for a
+  //      self contact; a limit row is +-1 at its dof.  Every row < MAXR is written (zero past nrow),
+  //      all rows at once: no per-row LDS round trip, no loop.
+  {
+    const int rr = lane < MAXR ? lane : 0;
+    const int c = rr / 3, u = rr - 3 * c;
+    const int lk = s.rlink[rr];
+    const float sg = s.rsign[rr];
+    float P[3], f6[6];  // spatial force direction [P x d; d]
 #pragma unroll
-    for (int k = 0; k < 3; ++k) P[k] = s.cpt[c][k];
-#pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      lk[u] = s.rlink[r0 + u];
-      sg[u] = s.rsign[r0 + u];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dir[u][k] = s.cdir[c][u][k];
+    for (int k = 0; k < 3; ++k) {
+      P[k] = s.cpt[c][k];
+      f6[3 + k] = s.cdir[c][u][k];
     }
+    cross3(P, f6 + 3, f6);
+    const bool con = lk >= 0;
+    const int l2 = (lk >> 8) - 1;
+    // Every lane loads and computes everything; the selects are bit masks (exact: x & ~0 = x,
+    // x & 0 = +0), so that no branch around the loads serialises one LDS round trip per column.
+    const uint32_t pm1 = sm.topo[con ? lk & 31 : 0].lpath & (con ? ~0u : 0u);
+    const uint32_t pm2 = sm.topo[con && l2 >= 0 ? l2 & 31 : 0].lpath & (con && l2 >= 0 ? ~0u : 0u);
+    const uint32_t live = lane < nrow ? ~0u : 0u;
 #pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      const int r = r0 + u;
-      // branch-free: contact row -> S_j . f6 on the link's path; limit row -> +-1 at its dof
-      float f6[6];  // spatial force direction [P x d; d]
-      cross3(P, dir[u], f6);
-      f6[3] = dir[u][0]; f6[4] = dir[u][1]; f6[5] = dir[u][2];
-      // a self-contact's second link (bits 8.., + 1) takes the opposite impulse: dofs on both paths
-      // give jcon - jcon = 0 (oracle contact_row)
-      const bool con = lk[u] >= 0;
-      const int l2 = (lk[u] >> 8) - 1;
-      const bool on1 = con && ((dsub >> (lk[u] & 31)) & 1u);
-      const bool on2 = con && l2 >= 0 && ((dsub >> (l2 & 31)) & 1u);
-      const float jcon = dot6(Sj, f6);
-      float jv = con ? (on1 ? jcon : 0.f) - (on2 ? jcon : 0.f) : (-1 - lk[u] == lane ? sg[u] : 0.f);
-      jv = (r < nrow && lane < NV) ? jv : 0.f;
-      if (lane < LDJ) s.x.k.Jm[r][lane] = jv;
+    for (int q = 0; q < LDJ / 4; ++q) {
+      float jq[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = 4 * q + e;
+        if (j < NV) {
+          const v4f s0 = *reinterpret_cast<const v4f*>(&s.S[j][0]);
+          const v4f s1 = *reinterpret_cast<const v4f*>(&s.S[j][4]);
+          const float Sj[6] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y};
+          const uint32_t jb = __float_as_uint(dot6(Sj, f6));
+          const int lnk = j < 6 ? 0 : j - 5;  // the link dof j moves with
+          // contact row: (on path 1 ? jcon : 0) - (on path 2 ? jcon : 0), +0 on a limit row (pm = 0);
+          // limit row: sign at its dof, +0 elsewhere and on every contact row (lk >= 0 > -1 - lk)
+          const float jc1 = __uint_as_float(jb & (0u - ((pm1 >> lnk) & 1u)));
+          const float jc2 = __uint_as_float(jb & (0u - ((pm2 >> lnk) & 1u)));
+          const uint32_t jl = __float_as_uint(sg) & (-1 - lk == j ? ~0u : 0u);
+          jq[e] = __uint_as_float(((__float_as_uint(jc1 - jc2)) | jl) & live);
+        } else {
+          jq[e] = 0.f;
+        }
+      }
+      if (lane < MAXR) *reinterpret_cast<v4f*>(&s.x.k.Jm[lane][4 * q]) = v4f{jq[0], jq[1], jq[2], jq[3]};
     }
   }
   __syncthreads();
+  ts.mark(kStRows);
   // W rows, one group per iteration (unrolled, so that lane j's W column stays in registers
   // for the PGS sweep); each row's dot product runs as two interleaved partial sums.
   // Hr is zero on lanes >= NV, so their W entries are zero; they read J column 0 (keeps every LDS
@@ -1177,6 +1182,9 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   const int jc = lane < NV ? lane : 0;
   const float jmask = lane < NV ? 1.f : 0.f;
   float arr = 0.f, acp = 0.f;
+  v2f H2[(NV + 1) / 2];  // row `lane` of H^-1 in (even, odd) pairs
+#pragma unroll
+  for (int k = 0; k < (NV + 1) / 2; ++k) H2[k] = v2f{Hr[2 * k], 2 * k + 1 < NV ? Hr[2 * k + 1] : 0.f};
   float Wc[MAXR];
 #pragma unroll
   for (int r = 0; r < MAXR; ++r) Wc[r] = 0.f;
@@ -1188,29 +1196,30 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       // back, so at most two groups of J-row reads are in flight (hoisted further they spill)
       int rr = r0;
       if (r0 >= 2 * kRowGroup) asm volatile("" : "+v"(rr) : "v"(Wc[r0 - kRowGroup - 1]));
-      float w[kRowGroup][2];
+      // the two partial sums (even / odd k) as one packed pair: (w_e, w_o) += (H_k, H_k+1) (J_k, J_k+1)
+      // is v_pk_fma_f32 on register pairs as they come from the b128 reads, no repacking moves
+      v2f w[kRowGroup];
       float jown[kRowGroup];
 #pragma unroll
       for (int u = 0; u < kRowGroup; ++u) {
         jown[u] = s.x.k.Jm[rr + u][jc];
-        w[u][0] = w[u][1] = 0.f;
+        w[u] = v2f{0.f, 0.f};
       }
 #pragma unroll
       for (int u = 0; u < kRowGroup; ++u) {
         const v4f* jr = reinterpret_cast<const v4f*>(s.x.k.Jm[rr + u]);  // 16-B aligned rows
-        float jrow[LDJ];
 #pragma unroll
         for (int q = 0; q < LDJ / 4; ++q) {
           const v4f t = jr[q];
-          jrow[4 * q] = t.x; jrow[4 * q + 1] = t.y; jrow[4 * q + 2] = t.z; jrow[4 * q + 3] = t.w;
+          if (4 * q + 1 < NV) w[u] = __builtin_elementwise_fma(H2[2 * q], t.xy, w[u]);
+          if (4 * q + 3 < NV) w[u] = __builtin_elementwise_fma(H2[2 * q + 1], t.zw, w[u]);
+          else if (4 * q + 2 < NV) w[u].x = fmaf(H2[2 * q + 1].x, t.z, w[u].x);
         }
-#pragma unroll
-        for (int k = 0; k < NV; ++k) w[u][k & 1] = fmaf(Hr[k], jrow[k], w[u][k & 1]);
       }
       float wu[kRowGroup], a[2 * kRowGroup];
 #pragma unroll
       for (int u = 0; u < kRowGroup; ++u) {
-        wu[u] = w[u][0] + w[u][1];
+        wu[u] = w[u].x + w[u].y;
         Wc[r0 + u] = wu[u];
         a[u] = jown[u] * wu[u];
       }
