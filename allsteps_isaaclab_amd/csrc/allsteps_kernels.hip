@@ -696,6 +696,16 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
       const v4f d = *reinterpret_cast<const v4f*>(Pb[a]);
       D[a][0] = d.x; D[a][1] = d.y; D[a][2] = d.z; D[a][3] = d.w;
     }
+    // the first kPre column blocks of the pivot rows are read before the block inverse, and the
+    // scheduling barrier keeps them there: their LDS latency runs under the inverse's division chain
+    // (left alone, the scheduler sinks every Q read below it)
+    constexpr int kPre = 3;
+    v4f qpre[kPre][B];
+#pragma unroll
+    for (int jb = 0; jb < kPre; ++jb)
+#pragma unroll
+      for (int c = 0; c < B; ++c) qpre[jb][c] = *reinterpret_cast<const v4f*>(&Q[c][B + 4 * jb]);
+    __builtin_amdgcn_sched_barrier(0);
     block_inverse<B>(D);
     float alpha = 1.f, beta[B];
 #pragma unroll
@@ -714,7 +724,8 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
       float q[B][4];
 #pragma unroll
       for (int c = 0; c < B; ++c) {
-        const v4f x = *reinterpret_cast<const v4f*>(&Q[c][j]);
+        const int jb = (j - B) / 4;
+        const v4f x = jb < kPre ? qpre[jb < kPre ? jb : 0][c] : *reinterpret_cast<const v4f*>(&Q[c][j]);
         q[c][0] = x.x; q[c][1] = x.y; q[c][2] = x.z; q[c][3] = x.w;
       }
 #pragma unroll
@@ -1185,9 +1196,9 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   v2f H2[(NV + 1) / 2];  // row `lane` of H^-1 in (even, odd) pairs
 #pragma unroll
   for (int k = 0; k < (NV + 1) / 2; ++k) H2[k] = v2f{Hr[2 * k], 2 * k + 1 < NV ? Hr[2 * k + 1] : 0.f};
-  float Wc[MAXR];
+  float Wc[MAXR], Jc[MAXR];  // lane j's W and J columns, for the PGS sweep
 #pragma unroll
-  for (int r = 0; r < MAXR; ++r) Wc[r] = 0.f;
+  for (int r = 0; r < MAXR; ++r) Wc[r] = Jc[r] = 0.f;
 #pragma unroll
   for (int r0 = 0; r0 < MAXR; r0 += kRowGroup) {
     // a uniform skip, not an exit: a loop with one exit and a constant trip count unrolls fully
@@ -1221,6 +1232,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       for (int u = 0; u < kRowGroup; ++u) {
         wu[u] = w[u].x + w[u].y;
         Wc[r0 + u] = wu[u];
+        Jc[r0 + u] = jown[u] * jmask;
         a[u] = jown[u] * wu[u];
       }
       a[3] = jown[1] * wu[0];  // A_10, kept by row r0
@@ -1244,7 +1256,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   // ---- projected Gauss-Seidel (lane j holds u_j; every lane of an env holds all its impulses).
   // Rows in order: contacts as (normal, tangent, tangent) triplets, then joint limits; a tangent
   // row's bound uses the impulse of the most recent normal row (ln).  Lane j's J / W columns of
-  // every row sit in registers (loaded once, up front).  A group of three rows takes the three
+  // every row sit in registers (kept from the W pass).  A group of three rows takes the three
   // velocities J_r . u from the u at its start (three independent reductions) and adds the
   // in-group coupling A_sr dlambda_r of the rows before it, which is the Gauss-Seidel sweep row by
   // row (J_s . (u + W_r dl_r) = J_s . u + A_sr dl_r) with one reduction latency per group instead
@@ -1253,12 +1265,9 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   float mu = K.sim.friction;
   asm volatile("" : "+v"(mu));
   const int iters = K.sim.pgs_iters;
-  float Jc[MAXR], lamr[MAXR];
+  float lamr[MAXR];
 #pragma unroll
-  for (int r = 0; r < MAXR; ++r) {
-    Jc[r] = s.x.k.Jm[r][jc] * jmask;
-    lamr[r] = 0.f;
-  }
+  for (int r = 0; r < MAXR; ++r) lamr[r] = 0.f;
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
     float ln = 0.f;
