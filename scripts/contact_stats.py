@@ -28,6 +28,7 @@ def build_stats_lib() -> str:
     src = os.path.join(ROOT, "oracle")
     subprocess.run(["gcc", "-O2", "-mfma", "-fPIC", "-std=c11", "-ffp-contract=off", "-shared", "-DOR_STATS",
                     "-DOR_MAX_CONTACTS=64", "-o", out, os.path.join(src, "task.c"), os.path.join(src, "physics.c"),
+                    os.path.join(src, "quad.c"),
                     "-lm"], check=True)
     return out
 
