@@ -124,7 +124,10 @@ struct EnvS {
   float b[32];          // tau - C
   PhaseScratch x;
   float rlam[MAXR];     // PGS impulses
-  alignas(16) float rmeta[MAXR][4]; // per row: 1/A_rr, target, type (0 normal, 1 tangent, 2 limit)
+  // per row: 1/A_rr, target, bound parameter, in-group coupling.  The bound parameter is what the
+  // PGS needs of the row's group: on row 1 of a group mu for a contact triplet (0 otherwise), on
+  // row 2 the upper-bound offset, 0 for a contact triplet (+-mu ln) and +inf otherwise ([0, inf))
+  alignas(16) float rmeta[MAXR][4];
   float cdir[MAXC][3][3];  // contact frame: normal, tangent 1, tangent 2
   int rlink[MAXR];      // contact rows: link | (link2 + 1) << 8 (link2 = -1: stone); limit rows: -1 - dof
   float rsign[MAXR];
@@ -1000,23 +1003,6 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
   cross3(n, t1, t2);
 }
 
-// ------------------------------------------------------------------------------------------------
-// One projected Gauss-Seidel row: t = lambda_old + (target - J_r . u) / A_rr is formed by the
-// caller; normal and limit rows clamp it to [0, inf), tangent rows to +-mu * (latest normal
-// impulse ln) -- one v_med3 for both (a tangent row's target is 0).  Updates the row's impulse
-// (and ln on a normal row) and returns the impulse change.
-__device__ __forceinline__ float pgs_clamp(const v4f& mt, float t, float mu, float& lam, float& ln) {
-  // bounds as one FMA each from ln (tangent: mu_r = mu, off = 0; otherwise mu_r = 0, off = inf;
-  // 0 * ln + 0 keeps the normal rows' lower bound +0)
-  const bool tangent = mt.z == 1.f;
-  const float mu_r = tangent ? mu : 0.f, off = tangent ? 0.f : __builtin_inff();
-  const float l1 = __builtin_amdgcn_fmed3f(t, fmaf(-mu_r, ln, 0.f), fmaf(mu_r, ln, off));
-  ln = mt.z == 0.f ? l1 : ln;
-  const float d = l1 - lam;
-  lam = l1;
-  return d;
-}
-
 template <int NV>
 __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, uint32_t (&mask_out)[4],
                         Stamp& ts) {
@@ -1097,7 +1083,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
                                                    K.sim.max_depen_vel)
                                          : -sp / dt)
                              : 0.f;
-      s.rmeta[r][2] = d == 0 ? 0.f : 1.f;
+      s.rmeta[r][2] = d == 1 ? K.sim.friction : 0.f;
     }
   }
   const int crow = 3 * nc;
@@ -1110,7 +1096,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       s.rlink[slot] = -1 - (6 + lane);
       s.rsign[slot] = sd == 0 ? 1.f : -1.f;
       s.rmeta[slot][1] = err > 0.f ? fminf(K.sim.baumgarte * err / dt, K.sim.max_depen_vel) : err / dt;
-      s.rmeta[slot][2] = 2.f;
+      s.rmeta[slot][2] = slot % 3 == 2 ? __builtin_inff() : 0.f;
     }
     ++slot;
   }
@@ -1249,7 +1235,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   if (lane < MAXR && lane < (maxrow + kRowGroup - 1) / kRowGroup * kRowGroup) {
     s.rmeta[lane][0] = lane < nrow ? 1.0f / (arr + 1e-9f) : 0.f;
     s.rmeta[lane][3] = acp;
-    if (lane >= nrow) { s.rmeta[lane][1] = 0.f; s.rmeta[lane][2] = 0.f; }
+    if (lane >= nrow) { s.rmeta[lane][1] = 0.f; s.rmeta[lane][2] = lane % 3 == 2 ? __builtin_inff() : 0.f; }
   }
   __syncthreads();
   ts.mark(kStWsolve);
@@ -1262,8 +1248,6 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   // row (J_s . (u + W_r dl_r) = J_s . u + A_sr dl_r) with one reduction latency per group instead
   // of one per row.  The row loop is unrolled with an exit per group; rows in [maxrow, group end)
   // have zero J / W / metadata and leave everything unchanged.
-  float mu = K.sim.friction;
-  asm volatile("" : "+v"(mu));
   const int iters = K.sim.pgs_iters;
   float lamr[MAXR];
 #pragma unroll
@@ -1291,14 +1275,29 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
         const float k10 = m1.x * m0.w, k20 = m2.x * m1.w, k21 = m2.x * m2.w;  // x_s A_sr
         float t1 = fmaf(-vg[1], m1.x, fmaf(m1.y, m1.x, lamr[r + 1]));
         float t2 = fmaf(-vg[2], m2.x, fmaf(m2.y, m2.x, lamr[r + 2]));
-        const float d0 = pgs_clamp(m0, fmaf(-vg[0], m0.x, fmaf(m0.y, m0.x, lamr[r])), mu, lamr[r], ln);
+        // Row types by group: a contact triplet is (normal, tangent, tangent), every other group holds
+        // limit rows (or the zero rows past nrow); contacts come first.  So row 0 always clamps to
+        // [0, inf) and sets ln (read only by this triplet's tangents), and rows 1 and 2 share one pair
+        // of bounds, +-mu ln for a contact triplet and [0, inf) otherwise -- the bounds pgs_clamp forms
+        // row by row, bit for bit (fmaf(-0, ln, 0) = +0 for the finite ln >= 0); the two bound
+        // parameters were stored with the rows (EnvS::rmeta), so no type test runs in the sweep.
+        const float mu_g = m1.z, off_g = m2.z;
+        const float l0 = __builtin_amdgcn_fmed3f(fmaf(-vg[0], m0.x, fmaf(m0.y, m0.x, lamr[r])), 0.f, __builtin_inff());
+        const float d0 = l0 - lamr[r];
+        lamr[r] = l0;
+        ln = l0;
+        const float blo = fmaf(-mu_g, ln, 0.f), bhi = fmaf(mu_g, ln, off_g);
         t1 = fmaf(-k10, d0, t1);
         t2 = fmaf(-k20, d0, t2);
         uj = fmaf(Wc[r], d0, uj);
-        const float d1 = pgs_clamp(m1, t1, mu, lamr[r + 1], ln);
+        const float l1 = __builtin_amdgcn_fmed3f(t1, blo, bhi);
+        const float d1 = l1 - lamr[r + 1];
+        lamr[r + 1] = l1;
         t2 = fmaf(-k21, d1, t2);
         uj = fmaf(Wc[r + 1], d1, uj);
-        const float d2 = pgs_clamp(m2, t2, mu, lamr[r + 2], ln);
+        const float l2 = __builtin_amdgcn_fmed3f(t2, blo, bhi);
+        const float d2 = l2 - lamr[r + 2];
+        lamr[r + 2] = l2;
         uj = fmaf(Wc[r + 2], d2, uj);
       }
     }
