@@ -713,12 +713,18 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
       for (int c = 0; c < B; ++c) qpre[jb][c] = *reinterpret_cast<const v4f*>(&Q[c][B + 4 * jb]);
     __builtin_amdgcn_sched_barrier(0);
     block_inverse<B>(D);
+    // packed pairs written out (the file is built without the SLP vectorizer, which elsewhere paid
+    // for its pairs with register moves); per element the same operations in the same order
     float alpha = 1.f, beta[B];
+    v2f vb[B / 2] = {v2f{0.f, 0.f}, v2f{0.f, 0.f}};
+#pragma unroll
+    for (int e = 0; e < B; ++e)
+#pragma unroll
+      for (int c2 = 0; c2 < B / 2; ++c2)
+        vb[c2] = __builtin_elementwise_fma(v2f{Hr[e], Hr[e]}, v2f{D[e][2 * c2], D[e][2 * c2 + 1]}, vb[c2]);
 #pragma unroll
     for (int c = 0; c < B; ++c) {
-      float v = 0.f;
-#pragma unroll
-      for (int e = 0; e < B; ++e) v = fmaf(Hr[e], D[e][c], v);
+      const float v = c & 1 ? vb[c / 2].y : vb[c / 2].x;
       float pv = -D[0][c];
 #pragma unroll
       for (int e = 1; e < B; ++e) pv = t == e ? -D[e][c] : pv;
@@ -727,20 +733,19 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
     if (piv) alpha = 0.f;
 #pragma unroll
     for (int j = B; j < NP; j += 4) {
-      float q[B][4];
+      v4f x[B];
 #pragma unroll
       for (int c = 0; c < B; ++c) {
         const int jb = (j - B) / 4;
-        const v4f x = jb < kPre ? qpre[jb < kPre ? jb : 0][c] : *reinterpret_cast<const v4f*>(&Q[c][j]);
-        q[c][0] = x.x; q[c][1] = x.y; q[c][2] = x.z; q[c][3] = x.w;
+        x[c] = jb < kPre ? qpre[jb < kPre ? jb : 0][c] : *reinterpret_cast<const v4f*>(&Q[c][j]);
       }
+      v2f lo = v2f{alpha, alpha} * v2f{Hr[j], Hr[j + 1]}, hi = v2f{alpha, alpha} * v2f{Hr[j + 2], Hr[j + 3]};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float v = alpha * Hr[j + i];
-#pragma unroll
-        for (int c = 0; c < B; ++c) v = fmaf(-beta[c], q[c][i], v);
-        Hr[j + i - B] = v;
+      for (int c = 0; c < B; ++c) {
+        lo = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[c].xy, lo);
+        hi = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[c].zw, hi);
       }
+      Hr[j - B] = lo.x; Hr[j + 1 - B] = lo.y; Hr[j + 2 - B] = hi.x; Hr[j + 3 - B] = hi.y;
     }
 #pragma unroll
     for (int c = 0; c < B; ++c) Hr[NP - B + c] = beta[c];
@@ -1101,10 +1106,10 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       for (int k = 0; k < 3; ++k) s.cdir[lane][d][k] = dirs[d][k];
       s.rlink[r] = lk;
       s.rsign[r] = 0.f;
-      s.rmeta[r][1] = d == 0 ? (sp < 0.f ? fminf(K.sim.baumgarte * fmaxf(-sp - K.sim.slop, 0.f) / dt,
-                                                   K.sim.max_depen_vel)
-                                         : -sp / dt)
-                             : 0.f;
+      // one division for both branches: (sp < 0 ? min(b max(-sp - slop, 0) / dt, vmax) : -sp / dt)
+      const float num = sp < 0.f ? K.sim.baumgarte * fmaxf(-sp - K.sim.slop, 0.f) : -sp;
+      const float tv = num / dt;
+      s.rmeta[r][1] = d == 0 ? (sp < 0.f ? fminf(tv, K.sim.max_depen_vel) : tv) : 0.f;
       s.rmeta[r][2] = d == 1 ? K.sim.friction : 0.f;
     }
   }
@@ -1117,7 +1122,8 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       float err = sd == 0 ? err_lo : err_hi;
       s.rlink[slot] = -1 - (6 + lane);
       s.rsign[slot] = sd == 0 ? 1.f : -1.f;
-      s.rmeta[slot][1] = err > 0.f ? fminf(K.sim.baumgarte * err / dt, K.sim.max_depen_vel) : err / dt;
+      const float tv = (err > 0.f ? K.sim.baumgarte * err : err) / dt;  // one division, both branches
+      s.rmeta[slot][1] = err > 0.f ? fminf(tv, K.sim.max_depen_vel) : tv;
       s.rmeta[slot][2] = slot % 3 == 2 ? __builtin_inff() : 0.f;
     }
     ++slot;
