@@ -763,11 +763,37 @@ __device__ void emit_contact(EnvS& s, int slot, int ncap, int link, int link2, i
   for (int k = 0; k < 3; ++k) { s.cn[slot][k] = n[k]; s.cpt[slot][k] = P[k] - n[k] * r; }
 }
 
+// Per-lane geom constants (lane = geom), read from the constants block once per launch and kept in
+// registers across the substeps (inside collide they were lane-varying global loads every substep,
+// one L2 round trip on the phase's critical path).
+struct GeomC {
+  int link, type, foot;
+  float r, p0[3], p1[3];
+};
+__device__ __forceinline__ GeomC load_geom(const Consts& K, int lane) {
+  const as_model_t& m = K.model;
+  const int g = lane < m.num_geoms ? lane : 0;
+  GeomC c;
+  c.link = m.geom_link[g];
+  c.type = m.geom_type[g];
+  c.foot = m.geom_foot[g];
+  c.r = m.geom_radius[g];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    c.p0[k] = m.geom_p0[g][k];
+    c.p1[k] = m.geom_p1[g][k];
+  }
+  // opaque: the values are not rematerialised from memory inside the substep loop
+  asm volatile("" : "+v"(c.link), "+v"(c.type), "+v"(c.foot), "+v"(c.r));
+  asm volatile("" : "+v"(c.p0[0]), "+v"(c.p0[1]), "+v"(c.p0[2]), "+v"(c.p1[0]), "+v"(c.p1[1]), "+v"(c.p1[2]));
+  return c;
+}
+
 // At most ncap contacts, in priority order (oracle/physics.c collide() emits the same list):
 //   1. the priority geoms (the feet: geoms [0, num_priority_geoms)) against the candidate stones,
 //      stone-major, geom-minor;  2. every other geom against the candidate stones, likewise;
 //   3. robot self-contacts, one per self-collision pair in table order.
-__device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane, int ncap) {
+__device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane, int ncap, const GeomC& gc) {
   const as_model_t& m = K.model;
   const float* h = K.sim.stone_half;
   const float margin = K.sim.margin;
@@ -780,14 +806,13 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane, int 
   for (int i = 0; i < kSelfW; ++i) spw[i] = G * i + lane < nsp ? m.self_pair[G * i + lane] : 0;
   // geom segment in the O frame (lane = geom), formed once for all candidate stones
   const bool gv = lane < ng;
-  const int g = gv ? lane : 0;
-  const int link = m.geom_link[g], gtype = m.geom_type[g], foot = m.geom_foot[g];
-  const float r = m.geom_radius[g];
+  const int link = gc.link, gtype = gc.type, foot = gc.foot;
+  const float r = gc.r;
   float a[3], bb[3];
   {
     float t0[3], t1[3];
-    matvec3(s.R[link], m.geom_p0[g], t0);
-    matvec3(s.R[link], m.geom_p1[g], t1);
+    matvec3(s.R[link], gc.p0, t0);
+    matvec3(s.R[link], gc.p1, t1);
     for (int k = 0; k < 3; ++k) { a[k] = s.p[link][k] + t0[k]; bb[k] = s.p[link][k] + t1[k]; }
   }
   const float L = sqrtf((bb[0] - a[0]) * (bb[0] - a[0]) + (bb[1] - a[1]) * (bb[1] - a[1]) +
@@ -1031,8 +1056,8 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
 }
 
 template <int NV>
-__device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, uint32_t (&mask_out)[4],
-                        Stamp& ts) {
+__device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, const GeomC& gc,
+                        uint32_t (&mask_out)[4], Stamp& ts) {
   // Opaque copies of the constants pointer and the lane id: everything derived from them below
   // (model-table loads, LDS addresses, lane masks) is loop-invariant, and without this the
   // compiler hoists all of it out of the substep loop and spills it.
@@ -1092,7 +1117,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   const int lpos = half_scan3(lo_v + hi_v, ltotal);
   const int nlim = ltotal < MAXR ? ltotal : MAXR;
   const int ncap = (MAXR - nlim) / 3 < MAXC ? (MAXR - nlim) / 3 : MAXC;
-  collide(K, s, lane, ncap);
+  collide(K, s, lane, ncap, gc);
   ts.mark(kStCollide);
   const int nc = s.ncontact;
   if (lane < nc) {  // contact rows 3c..3c+2: normal, tangent 1, tangent 2
@@ -1513,7 +1538,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const bool do_physics = P.mode == kModeStep || P.mode == kModePhysics;
   // ---- physics
   if (do_physics) {
-    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, mask, ts);
+    const GeomC gc = load_geom(K, lane);
+    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, gc, mask, ts);
     fk<false>(K, s, lane, tp);  // FK of the final pose for body_pos_w (articulation_data.py:439)
     if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; s.mask[2] = mask[2]; s.mask[3] = mask[3]; }
   }
