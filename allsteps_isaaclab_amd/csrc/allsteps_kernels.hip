@@ -585,14 +585,12 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
 // Row j of the joint-space inertia H (lane j):
 //   H_jk = S_k . (Ic_link(j) S_j)  if dof k is on the path of link(j) (k ancestor-or-self),
 //        = S_j . (Ic_link(k) S_k)  if dof j is on the path of link(k),   else 0;  + armature.
-// The masks come from the constants (one global load each per lane): with an LDS copy in
-// Smem::topo the scheduler clusters all 12 NV LDS reads of S and Fh up front and spills.
+// The masks are per-lane registers loaded once per launch (GeomC): with an LDS copy in Smem::topo
+// the scheduler clusters all 12 NV LDS reads of S and Fh up front and spills.
 template <int NV>
-__device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, float (&Hr)[NV]) {
+__device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, uint32_t anc_j, uint32_t jon,
+                      float (&Hr)[NV]) {
   const int j = lane < NV ? lane : 0;
-  const int lj = j < 6 ? 0 : j - 5;
-  const uint32_t anc_j = K.ancmask[lj];
-  const uint32_t jon = K.ddesc[j];
   float Sj[6], Fj[6];
 #pragma unroll
   for (int a = 0; a < 6; ++a) { Sj[a] = s.S[j][a]; Fj[a] = s.x.d.Fh[j][a]; }
@@ -763,12 +761,13 @@ __device__ void emit_contact(EnvS& s, int slot, int ncap, int link, int link2, i
   for (int k = 0; k < 3; ++k) { s.cn[slot][k] = n[k]; s.cpt[slot][k] = P[k] - n[k] * r; }
 }
 
-// Per-lane geom constants (lane = geom), read from the constants block once per launch and kept in
-// registers across the substeps (inside collide they were lane-varying global loads every substep,
-// one L2 round trip on the phase's critical path).
+// Per-lane constants read from the constants block once per launch and kept in registers across the
+// substeps (lane-varying global loads every substep were an L2 round trip at the head of collide and
+// of the H rows): the geom of lane g, and the H-row masks of dof lane j.
 struct GeomC {
   int link, type, foot;
   float r, p0[3], p1[3];
+  uint32_t anc, jon;  // h_row: dofs on the path of dof j's link; dofs whose path holds j
 };
 __device__ __forceinline__ GeomC load_geom(const Consts& K, int lane) {
   const as_model_t& m = K.model;
@@ -783,8 +782,11 @@ __device__ __forceinline__ GeomC load_geom(const Consts& K, int lane) {
     c.p0[k] = m.geom_p0[g][k];
     c.p1[k] = m.geom_p1[g][k];
   }
+  const int j = lane < K.nv ? lane : 0;
+  c.anc = K.ancmask[j < 6 ? 0 : j - 5];
+  c.jon = K.ddesc[j];
   // opaque: the values are not rematerialised from memory inside the substep loop
-  asm volatile("" : "+v"(c.link), "+v"(c.type), "+v"(c.foot), "+v"(c.r));
+  asm volatile("" : "+v"(c.link), "+v"(c.type), "+v"(c.foot), "+v"(c.r), "+v"(c.anc), "+v"(c.jon));
   asm volatile("" : "+v"(c.p0[0]), "+v"(c.p0[1]), "+v"(c.p0[2]), "+v"(c.p1[0]), "+v"(c.p1[1]), "+v"(c.p1[2]));
   return c;
 }
@@ -1080,7 +1082,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   ts.mark(kStLinkQ);
   constexpr int NP = (NV + kSweepB - 1) / kSweepB * kSweepB;  // sweep order, padded with identity
   float Hr[NP];
-  h_row<NV>(K, s, lane, tp, *reinterpret_cast<float(*)[NV]>(Hr));
+  h_row<NV>(K, s, lane, tp, gc.anc, gc.jon, *reinterpret_cast<float(*)[NV]>(Hr));
 #pragma unroll
   for (int j = NV; j < NP; ++j) Hr[j] = lane == j ? 1.f : 0.f;
   ts.mark(kStDyn);
