@@ -1057,6 +1057,63 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
   cross3(n, t1, t2);
 }
 
+// PGS sweeps over NG row groups (see substep): rows in order, contacts as (normal, tangent, tangent)
+// triplets, then joint limits; lane j holds u_j and every lane of an env all its impulses.  A group
+// takes its three velocities J_r . u from the u at its start (three interleaved half-wave reductions)
+// and adds the in-group couplings A_sr dlambda_r of the rows before it -- the Gauss-Seidel sweep row
+// by row (J_s . (u + W_r dl_r) = J_s . u + A_sr dl_r) with one reduction latency per group.
+template <int NG>
+__device__ __forceinline__ void pgs_sweeps(const EnvS& s, int iters, float& uj, float (&lamr)[MAXR],
+                                           const float (&Jc)[MAXR], const float (&Wc)[MAXR]) {
+#pragma unroll 1
+  for (int it = 0; it < iters; ++it) {
+    float uprev = uj;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int r = kRowGroup * g;
+      // the group's metadata reads are pinned behind the previous group's start (its u): one
+      // group of reads ahead, none hoisted out of the sweep loop (30 rows would not fit)
+      int rr = r;
+      asm volatile("" : "+v"(rr) : "v"(uprev));
+      uprev = uj;
+      const v4f m0 = *reinterpret_cast<const v4f*>(s.rmeta[rr]);
+      const v4f m1 = *reinterpret_cast<const v4f*>(s.rmeta[rr + 1]);
+      const v4f m2 = *reinterpret_cast<const v4f*>(s.rmeta[rr + 2]);
+      float vg[3] = {Jc[r] * uj, Jc[r + 1] * uj, Jc[r + 2] * uj};
+      half_sum_n(vg);
+      // t_s = lambda_s + (target_s - v_s - sum_{r<s} A_sr dl_r) x_s, with the parts that do not
+      // depend on this sweep's impulse changes formed first: the chain from one row's dl to the
+      // next row's clamp is a single FMA
+      const float k10 = m1.x * m0.w, k20 = m2.x * m1.w, k21 = m2.x * m2.w;  // x_s A_sr
+      float t1 = fmaf(-vg[1], m1.x, fmaf(m1.y, m1.x, lamr[r + 1]));
+      float t2 = fmaf(-vg[2], m2.x, fmaf(m2.y, m2.x, lamr[r + 2]));
+      // Row types by group: a contact triplet is (normal, tangent, tangent), every other group holds
+      // limit rows (or the zero rows past nrow); contacts come first.  So row 0 always clamps to
+      // [0, inf) and its impulse ln bounds only this triplet's tangents, and rows 1 and 2 share one
+      // pair of bounds, +-mu ln for a contact triplet and [0, inf) otherwise -- the bounds a per-row
+      // clamp forms, bit for bit (fmaf(-0, ln, 0) = +0 for the finite ln >= 0); the two bound
+      // parameters were stored with the rows (EnvS::rmeta), so no type test runs in the sweep.
+      const float mu_g = m1.z, off_g = m2.z;
+      const float l0 = __builtin_amdgcn_fmed3f(fmaf(-vg[0], m0.x, fmaf(m0.y, m0.x, lamr[r])), 0.f, __builtin_inff());
+      const float d0 = l0 - lamr[r];
+      lamr[r] = l0;
+      const float blo = fmaf(-mu_g, l0, 0.f), bhi = fmaf(mu_g, l0, off_g);
+      t1 = fmaf(-k10, d0, t1);
+      t2 = fmaf(-k20, d0, t2);
+      uj = fmaf(Wc[r], d0, uj);
+      const float l1 = __builtin_amdgcn_fmed3f(t1, blo, bhi);
+      const float d1 = l1 - lamr[r + 1];
+      lamr[r + 1] = l1;
+      t2 = fmaf(-k21, d1, t2);
+      uj = fmaf(Wc[r + 1], d1, uj);
+      const float l2 = __builtin_amdgcn_fmed3f(t2, blo, bhi);
+      const float d2 = l2 - lamr[r + 2];
+      lamr[r + 2] = l2;
+      uj = fmaf(Wc[r + 2], d2, uj);
+    }
+  }
+}
+
 template <int NV>
 __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, const GeomC& gc,
                         uint32_t (&mask_out)[4], Stamp& ts) {
@@ -1307,55 +1364,21 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   float lamr[MAXR];
 #pragma unroll
   for (int r = 0; r < MAXR; ++r) lamr[r] = 0.f;
-#pragma unroll 1
-  for (int it = 0; it < iters; ++it) {
-    float ln = 0.f;
-    float uprev = uj;
-#pragma unroll
-    for (int r = 0; r < MAXR; r += kRowGroup) {
-      if (r < maxrow) {
-        // the group's metadata reads are pinned behind the previous group's start (its u): one
-        // group of reads ahead, none hoisted out of the sweep loop (30 rows would not fit)
-        int rr = r;
-        asm volatile("" : "+v"(rr) : "v"(uprev));
-        uprev = uj;
-        const v4f m0 = *reinterpret_cast<const v4f*>(s.rmeta[rr]);
-        const v4f m1 = *reinterpret_cast<const v4f*>(s.rmeta[rr + 1]);
-        const v4f m2 = *reinterpret_cast<const v4f*>(s.rmeta[rr + 2]);
-        float vg[3] = {Jc[r] * uj, Jc[r + 1] * uj, Jc[r + 2] * uj};
-        half_sum_n(vg);
-        // t_s = lambda_s + (target_s - v_s - sum_{r<s} A_sr dl_r) x_s, with the parts that do not
-        // depend on this sweep's impulse changes formed first: the chain from one row's dl to the
-        // next row's clamp is a single FMA
-        const float k10 = m1.x * m0.w, k20 = m2.x * m1.w, k21 = m2.x * m2.w;  // x_s A_sr
-        float t1 = fmaf(-vg[1], m1.x, fmaf(m1.y, m1.x, lamr[r + 1]));
-        float t2 = fmaf(-vg[2], m2.x, fmaf(m2.y, m2.x, lamr[r + 2]));
-        // Row types by group: a contact triplet is (normal, tangent, tangent), every other group holds
-        // limit rows (or the zero rows past nrow); contacts come first.  So row 0 always clamps to
-        // [0, inf) and sets ln (read only by this triplet's tangents), and rows 1 and 2 share one pair
-        // of bounds, +-mu ln for a contact triplet and [0, inf) otherwise -- the bounds pgs_clamp forms
-        // row by row, bit for bit (fmaf(-0, ln, 0) = +0 for the finite ln >= 0); the two bound
-        // parameters were stored with the rows (EnvS::rmeta), so no type test runs in the sweep.
-        const float mu_g = m1.z, off_g = m2.z;
-        const float l0 = __builtin_amdgcn_fmed3f(fmaf(-vg[0], m0.x, fmaf(m0.y, m0.x, lamr[r])), 0.f, __builtin_inff());
-        const float d0 = l0 - lamr[r];
-        lamr[r] = l0;
-        ln = l0;
-        const float blo = fmaf(-mu_g, ln, 0.f), bhi = fmaf(mu_g, ln, off_g);
-        t1 = fmaf(-k10, d0, t1);
-        t2 = fmaf(-k20, d0, t2);
-        uj = fmaf(Wc[r], d0, uj);
-        const float l1 = __builtin_amdgcn_fmed3f(t1, blo, bhi);
-        const float d1 = l1 - lamr[r + 1];
-        lamr[r + 1] = l1;
-        t2 = fmaf(-k21, d1, t2);
-        uj = fmaf(Wc[r + 1], d1, uj);
-        const float l2 = __builtin_amdgcn_fmed3f(t2, blo, bhi);
-        const float d2 = l2 - lamr[r + 2];
-        lamr[r + 2] = l2;
-        uj = fmaf(Wc[r + 2], d2, uj);
-      }
-    }
+  // one instantiation per group count (maxrow is wave-uniform): the groups run without a skip test,
+  // so the sweep state needs no copies at per-group joins
+  static_assert(MAXR / kRowGroup == 10, "group-count dispatch");
+  switch ((__builtin_amdgcn_readfirstlane(maxrow) + kRowGroup - 1) / kRowGroup) {
+    case 1: pgs_sweeps<1>(s, iters, uj, lamr, Jc, Wc); break;
+    case 2: pgs_sweeps<2>(s, iters, uj, lamr, Jc, Wc); break;
+    case 3: pgs_sweeps<3>(s, iters, uj, lamr, Jc, Wc); break;
+    case 4: pgs_sweeps<4>(s, iters, uj, lamr, Jc, Wc); break;
+    case 5: pgs_sweeps<5>(s, iters, uj, lamr, Jc, Wc); break;
+    case 6: pgs_sweeps<6>(s, iters, uj, lamr, Jc, Wc); break;
+    case 7: pgs_sweeps<7>(s, iters, uj, lamr, Jc, Wc); break;
+    case 8: pgs_sweeps<8>(s, iters, uj, lamr, Jc, Wc); break;
+    case 9: pgs_sweeps<9>(s, iters, uj, lamr, Jc, Wc); break;
+    case 10: pgs_sweeps<10>(s, iters, uj, lamr, Jc, Wc); break;
+    default: break;
   }
   float lam = 0.f;
 #pragma unroll
