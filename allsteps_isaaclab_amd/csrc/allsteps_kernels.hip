@@ -1057,6 +1057,61 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
   cross3(n, t1, t2);
 }
 
+// W = H^-1 J^T over NG row groups (see substep): lane j's W and J columns go to registers for the
+// PGS; per group the half-wave reduces A_rr = J_r . W_r and the in-group couplings A_10, A_20, A_21
+// (A_sr = J_s . W_r), lane r keeping those of row r.
+template <int NV, int NG>
+__device__ __forceinline__ void w_pass(EnvS& s, int lane, const v2f (&H2)[(NV + 1) / 2], float (&Wc)[MAXR],
+                                       float (&Jc)[MAXR], float& arr, float& acp) {
+  const int jc = lane < NV ? lane : 0;
+  const float jmask = lane < NV ? 1.f : 0.f;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int r0 = kRowGroup * g;
+    // the group's row index passes through an empty asm that also takes the W of the group two
+    // back, so at most two groups of J-row reads are in flight (hoisted further they spill)
+    int rr = r0;
+    if (r0 >= 2 * kRowGroup) asm volatile("" : "+v"(rr) : "v"(Wc[r0 >= 2 * kRowGroup ? r0 - kRowGroup - 1 : 0]));
+    // the two partial sums (even / odd k) as one packed pair: (w_e, w_o) += (H_k, H_k+1) (J_k, J_k+1)
+    // is v_pk_fma_f32 on register pairs as they come from the b128 reads, no repacking moves
+    v2f w[kRowGroup];
+    float jown[kRowGroup];
+#pragma unroll
+    for (int u = 0; u < kRowGroup; ++u) {
+      jown[u] = s.x.k.Jm[rr + u][jc];
+      w[u] = v2f{0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kRowGroup; ++u) {
+      const v4f* jr = reinterpret_cast<const v4f*>(s.x.k.Jm[rr + u]);  // 16-B aligned rows
+#pragma unroll
+      for (int q = 0; q < LDJ / 4; ++q) {
+        const v4f t = jr[q];
+        if (4 * q + 1 < NV) w[u] = __builtin_elementwise_fma(H2[2 * q], t.xy, w[u]);
+        if (4 * q + 3 < NV) w[u] = __builtin_elementwise_fma(H2[2 * q + 1], t.zw, w[u]);
+        else if (4 * q + 2 < NV) w[u].x = fmaf(H2[2 * q + 1].x, t.z, w[u].x);
+      }
+    }
+    float wu[kRowGroup], a[2 * kRowGroup];
+#pragma unroll
+    for (int u = 0; u < kRowGroup; ++u) {
+      wu[u] = w[u].x + w[u].y;
+      Wc[r0 + u] = wu[u];
+      Jc[r0 + u] = jown[u] * jmask;
+      a[u] = jown[u] * wu[u];
+    }
+    a[3] = jown[1] * wu[0];  // A_10, kept by row r0
+    a[4] = jown[2] * wu[0];  // A_20, kept by row r0 + 1
+    a[5] = jown[2] * wu[1];  // A_21, kept by row r0 + 2
+    half_sum_n(a);
+#pragma unroll
+    for (int u = 0; u < kRowGroup; ++u) {
+      arr = lane == r0 + u ? a[u] : arr;
+      acp = lane == r0 + u ? a[kRowGroup + u] : acp;
+    }
+  }
+}
+
 // PGS sweeps over NG row groups (see substep): rows in order, contacts as (normal, tangent, tangent)
 // triplets, then joint limits; lane j holds u_j and every lane of an env all its impulses.  A group
 // takes its three velocities J_r . u from the u at its start (three interleaved half-wave reductions)
@@ -1288,8 +1343,6 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   // address in bounds).  Per group, the half-wave reduces A_rr = J_r . W_r of its rows and the
   // in-group couplings A_10, A_20, A_21 (A_sr = J_s . W_r) that the PGS sweep uses; lane r keeps
   // the values of row r, and the reciprocals are formed at once, one row per lane.
-  const int jc = lane < NV ? lane : 0;
-  const float jmask = lane < NV ? 1.f : 0.f;
   float arr = 0.f, acp = 0.f;
   v2f H2[(NV + 1) / 2];  // row `lane` of H^-1 in (even, odd) pairs
 #pragma unroll
@@ -1297,52 +1350,20 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   float Wc[MAXR], Jc[MAXR];  // lane j's W and J columns, for the PGS sweep
 #pragma unroll
   for (int r = 0; r < MAXR; ++r) Wc[r] = Jc[r] = 0.f;
-#pragma unroll
-  for (int r0 = 0; r0 < MAXR; r0 += kRowGroup) {
-    // a uniform skip, not an exit: a loop with one exit and a constant trip count unrolls fully
-    if (r0 < maxrow) {
-      // the group's row index passes through an empty asm that also takes the W of the group two
-      // back, so at most two groups of J-row reads are in flight (hoisted further they spill)
-      int rr = r0;
-      if (r0 >= 2 * kRowGroup) asm volatile("" : "+v"(rr) : "v"(Wc[r0 - kRowGroup - 1]));
-      // the two partial sums (even / odd k) as one packed pair: (w_e, w_o) += (H_k, H_k+1) (J_k, J_k+1)
-      // is v_pk_fma_f32 on register pairs as they come from the b128 reads, no repacking moves
-      v2f w[kRowGroup];
-      float jown[kRowGroup];
-#pragma unroll
-      for (int u = 0; u < kRowGroup; ++u) {
-        jown[u] = s.x.k.Jm[rr + u][jc];
-        w[u] = v2f{0.f, 0.f};
-      }
-#pragma unroll
-      for (int u = 0; u < kRowGroup; ++u) {
-        const v4f* jr = reinterpret_cast<const v4f*>(s.x.k.Jm[rr + u]);  // 16-B aligned rows
-#pragma unroll
-        for (int q = 0; q < LDJ / 4; ++q) {
-          const v4f t = jr[q];
-          if (4 * q + 1 < NV) w[u] = __builtin_elementwise_fma(H2[2 * q], t.xy, w[u]);
-          if (4 * q + 3 < NV) w[u] = __builtin_elementwise_fma(H2[2 * q + 1], t.zw, w[u]);
-          else if (4 * q + 2 < NV) w[u].x = fmaf(H2[2 * q + 1].x, t.z, w[u].x);
-        }
-      }
-      float wu[kRowGroup], a[2 * kRowGroup];
-#pragma unroll
-      for (int u = 0; u < kRowGroup; ++u) {
-        wu[u] = w[u].x + w[u].y;
-        Wc[r0 + u] = wu[u];
-        Jc[r0 + u] = jown[u] * jmask;
-        a[u] = jown[u] * wu[u];
-      }
-      a[3] = jown[1] * wu[0];  // A_10, kept by row r0
-      a[4] = jown[2] * wu[0];  // A_20, kept by row r0 + 1
-      a[5] = jown[2] * wu[1];  // A_21, kept by row r0 + 2
-      half_sum_n(a);
-#pragma unroll
-      for (int u = 0; u < kRowGroup; ++u) {
-        arr = lane == r0 + u ? a[u] : arr;
-        acp = lane == r0 + u ? a[kRowGroup + u] : acp;
-      }
-    }
+  // one instantiation per row-group count (maxrow is wave-uniform), as for the PGS below
+  const int ngroups = (__builtin_amdgcn_readfirstlane(maxrow) + kRowGroup - 1) / kRowGroup;
+  switch (ngroups) {
+    case 1: w_pass<NV, 1>(s, lane, H2, Wc, Jc, arr, acp); break;
+    case 2: w_pass<NV, 2>(s, lane, H2, Wc, Jc, arr, acp); break;
+    case 3: w_pass<NV, 3>(s, lane, H2, Wc, Jc, arr, acp); break;
+    case 4: w_pass<NV, 4>(s, lane, H2, Wc, Jc, arr, acp); break;
+    case 5: w_pass<NV, 5>(s, lane, H2, Wc, Jc, arr, acp); break;
+    case 6: w_pass<NV, 6>(s, lane, H2, Wc, Jc, arr, acp); break;
+    case 7: w_pass<NV, 7>(s, lane, H2, Wc, Jc, arr, acp); break;
+    case 8: w_pass<NV, 8>(s, lane, H2, Wc, Jc, arr, acp); break;
+    case 9: w_pass<NV, 9>(s, lane, H2, Wc, Jc, arr, acp); break;
+    case 10: w_pass<NV, 10>(s, lane, H2, Wc, Jc, arr, acp); break;
+    default: break;
   }
   if (lane < MAXR && lane < (maxrow + kRowGroup - 1) / kRowGroup * kRowGroup) {
     s.rmeta[lane][0] = lane < nrow ? 1.0f / (arr + 1e-9f) : 0.f;
