@@ -4,7 +4,9 @@
   with limit rows), 64 envs each with per-env random actions: every state field and contact flag
   bit-identical to the oracle after each of 5 physics steps;
 * the pendulum and the resting / falling / wedged spheres of tests/test_oracle_kats.py (padded to 21
-  hinges, tests/_models.py): the same known answers on the GPU, bit-identical to the oracle.
+  hinges, tests/_models.py): the same known answers on the GPU, bit-identical to the oracle;
+* a clump of 14 crossing capsules (91 overlapping self pairs): more pairs pass the bounding-sphere
+  filter than the kernel's one-pass list holds, so its word-by-word path runs -- bit-identical too.
 """
 
 import numpy as np
@@ -101,4 +103,52 @@ def test_sphere_flags_gpu(oracle_mod, case):
             assert g["contact_mask"][:, 0].tolist() == [0, 0]
     want = {"resting": 1 << 3, "falling": 0, "wedged": (1 << 3) | (1 << 4)}[case]
     assert int(g["contact_mask"][0, 0]) == want and int(g["contact_mask"][1, 0]) == 0
+    gpu.close()
+
+
+def _clump_model(nlinks: int = 14) -> dict:
+    """nlinks capsules on sibling hinge links, all near the root origin in a star of directions:
+    every one of the C(nlinks, 2) self pairs overlaps, so more pairs pass the bounding-sphere filter
+    than the kernel's one-pass pair list holds (64) and it takes the word-by-word path."""
+    from _models import padded_model
+
+    root = {"mass": 10.0, "com": (0.0, 0.0, 0.0), "inertia": (0.1, 0.1, 0.1)}
+    links, geoms = [root], []
+    rng = np.random.default_rng(5)
+    for i in range(nlinks):
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        links.append({"parent": 0, "offset": (0.0, 0.0, 0.0), "axis": tuple(np.roll((1.0, 0.0, 0.0), i % 3)),
+                      "mass": 0.5, "com": tuple(0.05 * d), "inertia": (1e-3, 1e-3, 1e-3), "lower": -3.0,
+                      "upper": 3.0})
+        o = 0.01 * rng.normal(size=3)  # off the common centre: no two axes meet (a zero distance has no normal)
+        geoms.append({"link": i + 1, "type": 1, "radius": 0.03, "p0": tuple(o - 0.15 * d), "p1": tuple(o + 0.15 * d)})
+    m = padded_model(links, geoms)
+    pairs = [(a, b) for a in range(nlinks) for b in range(a + 1, nlinks)]
+    m["num_self_pairs"] = len(pairs)
+    for p, (a, b) in enumerate(pairs):
+        m["self_pair"][p] = a | (b << 8)
+    return m
+
+
+def test_self_pairs_past_the_list_capacity(oracle_mod):
+    m = _clump_model()
+    assert m["num_self_pairs"] > 64
+    n, steps = 4, 3
+    orc = oracle_mod.Oracle(model=m)
+    st = orc.state(n)
+    st["stones"][:] = level0_stones(n)
+    st["root_pos"][:, :] = np.array([[1.5], [0.0], [2.0]], np.float32)  # in the air: self-contacts only
+    gpu = GpuPhysics(m, n)
+    gpu.load_oracle(st)
+    rng = np.random.default_rng(11)
+    moved = 0.0
+    for t in range(steps):
+        act = rng.uniform(-1, 1, (n, 21)).astype(np.float32)
+        gpu.step(act)
+        orc.physics_step(st, act)
+        g = gpu.get()
+        _assert_same(g, st, f"clump step {t}")
+        moved = max(moved, float(np.abs(g["qd"][:14]).max()))
+    assert moved > 0.0  # the self-contacts (at most the budget's 10) push the links apart
     gpu.close()
