@@ -1057,6 +1057,25 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
   cross3(n, t1, t2);
 }
 
+// Contact-sensor flag of lane c's contact (c < nce, a foot contact): |sum lambda_n n| / dt over the
+// contacts c2 < nce with its (foot, stone) pair, in ascending order; NC = the wave's larger nce.
+template <int NC>
+__device__ __forceinline__ void contact_flag(const EnvS& s, int lane, int nce, float dt, uint32_t (&b)[4]) {
+  static_assert(NC <= MAXC, "contacts");
+  const int cl = lane < MAXC ? lane : 0;
+  const int f = s.cfoot[cl], st = s.cstone[cl];
+  float fx = 0.f, fy = 0.f, fz = 0.f;
+#pragma unroll
+  for (int c2 = 0; c2 < NC; ++c2) {
+    const bool same = c2 < nce && s.cfoot[c2] == f && s.cstone[c2] == st;
+    const float l = s.lamn[c2];
+    fx += same ? l * s.cn[c2][0] : 0.f;
+    fy += same ? l * s.cn[c2][1] : 0.f;
+    fz += same ? l * s.cn[c2][2] : 0.f;
+  }
+  if (lane < nce && f >= 0 && sqrtf(fx * fx + fy * fy + fz * fz) / dt > 1e-4f) b[f & 3] = 1u << st;
+}
+
 // W = H^-1 J^T over NG row groups (see substep): lane j's W and J columns go to registers for the
 // PGS; per group the half-wave reduces A_rr = J_r . W_r and the in-group couplings A_10, A_20, A_21
 // (A_sr = J_s . W_r), lane r keeping those of row r.
@@ -1414,22 +1433,23 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   //      lambda_n n over the contacts with its (foot, stone) pair in ascending order, and the
   //      per-foot stone bits are OR-reduced over the half-wave
   {
+    // (one instantiation per wave-uniform contact count, the sum unrolled so all its reads issue at
+    // once; the terms past an env's own count add +0 to a sum that is never -0: the same bits)
     uint32_t b[4] = {0u, 0u, 0u, 0u};
-    if (lane < nc && 3 * lane < nrow) {
-      const int f = s.cfoot[lane], st = s.cstone[lane];
-      if (f >= 0) {
-        float fx = 0.f, fy = 0.f, fz = 0.f;
-        for (int c2 = 0; c2 < nc && 3 * c2 < nrow; ++c2) {
-          const bool same = s.cfoot[c2] == f && s.cstone[c2] == st;
-          const float l = s.lamn[c2];
-          fx += same ? l * s.cn[c2][0] : 0.f;
-          fy += same ? l * s.cn[c2][1] : 0.f;
-          fz += same ? l * s.cn[c2][2] : 0.f;
-        }
-        if (sqrtf(fx * fx + fy * fy + fz * fz) / dt > 1e-4f) {
-          b[f & 3] = 1u << st;
-        }
-      }
+    const int nce = min(nc, (nrow + kRowGroup - 1) / kRowGroup);  // contacts whose normal row was solved
+    const int ncw = max(__builtin_amdgcn_readlane(nce, 0), __builtin_amdgcn_readlane(nce, 32));
+    switch (ncw) {
+      case 1: contact_flag<1>(s, lane, nce, dt, b); break;
+      case 2: contact_flag<2>(s, lane, nce, dt, b); break;
+      case 3: contact_flag<3>(s, lane, nce, dt, b); break;
+      case 4: contact_flag<4>(s, lane, nce, dt, b); break;
+      case 5: contact_flag<5>(s, lane, nce, dt, b); break;
+      case 6: contact_flag<6>(s, lane, nce, dt, b); break;
+      case 7: contact_flag<7>(s, lane, nce, dt, b); break;
+      case 8: contact_flag<8>(s, lane, nce, dt, b); break;
+      case 9: contact_flag<9>(s, lane, nce, dt, b); break;
+      case 10: contact_flag<10>(s, lane, nce, dt, b); break;
+      default: break;
     }
     mask_out[0] = half_or(b[0]);
     mask_out[1] = half_or(b[1]);
