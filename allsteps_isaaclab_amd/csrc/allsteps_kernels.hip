@@ -700,10 +700,10 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
       const v4f d = *reinterpret_cast<const v4f*>(Pb[a]);
       D[a][0] = d.x; D[a][1] = d.y; D[a][2] = d.z; D[a][3] = d.w;
     }
-    // the first kPre column blocks of the pivot rows are read before the block inverse, and the
+    // the first kPre (all) column blocks of the pivot rows are read before the block inverse, and the
     // scheduling barrier keeps them there: their LDS latency runs under the inverse's division chain
     // (left alone, the scheduler sinks every Q read below it)
-    constexpr int kPre = 3;
+    constexpr int kPre = 6;
     v4f qpre[kPre][B];
 #pragma unroll
     for (int jb = 0; jb < kPre; ++jb)
