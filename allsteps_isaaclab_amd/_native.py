@@ -192,9 +192,11 @@ def build_native(verbose: bool = False) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     # -ffp-contract=off: no implicit FMA contraction -- every FMA of the physics path is an explicit
     # fmaf() in the order include/as_detmath.h fixes, so the oracle (built the same way) rounds
-    # identically and HIP <-> oracle parity is bit-exact
+    # identically and HIP <-> oracle parity is bit-exact.  -fno-slp-vectorize: the SLP pairs of the
+    # step kernel's scalar code cost more register moves than they save (launch -2 %);
+    # the packed math that pays (sweep, W rows) is written out as 2-vectors
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-ffp-contract=off", "-I", INCLUDE, "-o", LIB_PATH] + srcs
+           "-ffp-contract=off", "-fno-slp-vectorize", "-I", INCLUDE, "-o", LIB_PATH] + srcs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
