@@ -590,6 +590,9 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
 template <int NV>
 __device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, uint32_t anc_j, uint32_t jon,
                       float (&Hr)[NV]) {
+  // opaque per substep: the 2 x 27 column masks derived from them would otherwise be hoisted out of
+  // the substep loop as SGPR pairs and spilled to VGPR lanes (a readlane per column per substep)
+  asm volatile("" : "+v"(anc_j), "+v"(jon));
   const int j = lane < NV ? lane : 0;
   float Sj[6], Fj[6];
 #pragma unroll
