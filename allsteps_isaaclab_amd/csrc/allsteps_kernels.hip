@@ -345,21 +345,47 @@ __device__ __forceinline__ void path_sum(uint32_t mask, int n_max, float (&acc)[
 // level barriers: the tree depth only sets the length of the longest lane's loop.
 // kDyn: also the link's spatial quantities for the dynamics (COM, spatial inertia at O, motion
 // subspace of its hinge, S_i qd_i) from the registers of the walk, and the six root columns.
+// Per-lane joint constants of the local transform (lane = link), read once per launch and kept in
+// registers across the substeps (as lane-varying global loads they were an L2 round trip at the head
+// of every substep's FK)
+struct LinkC {
+  float oq[4], ax[3], an[3], op[3];
+};
+__device__ __forceinline__ LinkC load_link(const Consts& K, int lane) {
+  const as_model_t& m = K.model;
+  const int i = lane >= 1 && lane < m.num_links ? lane : 0;
+  LinkC c;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) c.oq[k] = m.offset_quat[i][k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    c.ax[k] = m.axis[i][k];
+    c.an[k] = m.anchor[i][k];
+    c.op[k] = m.offset_pos[i][k];
+  }
+  return c;
+}
+
 template <bool kDyn>
-__device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Topo& tp) {
+__device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Topo& tp, LinkC lc) {
   const as_model_t& m = K.model;
   const int nl = m.num_links;
   DynScratch& d = s.x.d;
+  // opaque per call: nothing derived from them is hoisted out of the substep loop
+  asm volatile("" : "+v"(lc.oq[0]), "+v"(lc.oq[1]), "+v"(lc.oq[2]), "+v"(lc.oq[3]), "+v"(lc.ax[0]),
+               "+v"(lc.ax[1]), "+v"(lc.ax[2]));
+  asm volatile("" : "+v"(lc.an[0]), "+v"(lc.an[1]), "+v"(lc.an[2]), "+v"(lc.op[0]), "+v"(lc.op[1]),
+               "+v"(lc.op[2]));
   if (lane >= 1 && lane < nl) {
     const int i = lane;
     float Roff[9], Rj[9], Ro[3], t[3], tmp[3];
-    quat_to_mat(m.offset_quat[i], Roff);
-    axis_angle_mat(m.axis[i], s.qi[i - 1], Rj);
+    quat_to_mat(lc.oq, Roff);
+    axis_angle_mat(lc.ax, s.qi[i - 1], Rj);
     matmul3(Roff, Rj, d.Rl[i]);
-    matvec3(Rj, m.anchor[i], Ro);
-    for (int k = 0; k < 3; ++k) t[k] = m.anchor[i][k] - Ro[k];
+    matvec3(Rj, lc.an, Ro);
+    for (int k = 0; k < 3; ++k) t[k] = lc.an[k] - Ro[k];
     matvec3(Roff, t, tmp);
-    for (int k = 0; k < 3; ++k) d.Rl[i][9 + k] = tmp[k] + m.offset_pos[i][k];
+    for (int k = 0; k < 3; ++k) d.Rl[i][9 + k] = tmp[k] + lc.op[k];
   }
   __syncthreads();
   float R0[9];
@@ -1193,7 +1219,7 @@ __device__ __forceinline__ void pgs_sweeps(const EnvS& s, int iters, float& uj, 
 
 template <int NV>
 __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, const GeomC& gc,
-                        uint32_t (&mask_out)[4], Stamp& ts) {
+                        const LinkC& lc, uint32_t (&mask_out)[4], Stamp& ts) {
   // Opaque copies of the constants pointer and the lane id: everything derived from them below
   // (model-table loads, LDS addresses, lane masks) is loop-invariant, and without this the
   // compiler hoists all of it out of the substep loop and spills it.
@@ -1210,7 +1236,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     s.tau[lane] = as_dc_motor(s.qt[lane], s.qi[lane], s.u[6 + lane], A.stiffness, A.damping, A.saturation_effort,
                               A.effort_limit, A.velocity_limit);
   }
-  fk<true>(K, s, lane, tp);  // (its first barrier publishes tau before the dynamics read it)
+  fk<true>(K, s, lane, tp, lc);  // (its first barrier publishes tau before the dynamics read it)
   ts.mark(kStFK);
   dynamics(K, s, lane, tp, K.sim.gravity);
   ts.mark(kStLinkQ);
@@ -1605,11 +1631,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   __syncthreads();
   ts.mark(kStLoad);
   const bool do_physics = P.mode == kModeStep || P.mode == kModePhysics;
+  const LinkC lc = load_link(K, lane);
   // ---- physics
   if (do_physics) {
     const GeomC gc = load_geom(K, lane);
-    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, gc, mask, ts);
-    fk<false>(K, s, lane, tp);  // FK of the final pose for body_pos_w (articulation_data.py:439)
+    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, gc, lc, mask, ts);
+    fk<false>(K, s, lane, tp, lc);  // FK of the final pose for body_pos_w (articulation_data.py:439)
     if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; s.mask[2] = mask[2]; s.mask[3] = mask[3]; }
   }
   ts.mark(kStFKFinal);
@@ -1762,7 +1789,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       episode += 1u;
     }
     __syncthreads();
-    fk<false>(K, s, lane, tp);  // body_pos of the reset pose (write_joint_state_to_sim invalidates FK)
+    fk<false>(K, s, lane, tp, lc);  // body_pos of the reset pose (write_joint_state_to_sim invalidates FK)
     if (done) {
       const int ls[3] = {m.torso_link, m.foot_link[0], m.foot_link[1]};
       for (int b = 0; b < 3; ++b)
