@@ -446,8 +446,8 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
       B[9] = Iw[5] - mass * c[1] * c[2];
       if (i > 0) {
         float a[3], o[3];
-        matvec3(R, m.axis[i], a);
-        matvec3(R, m.anchor[i], o);
+        matvec3(R, lc.ax, a);
+        matvec3(R, lc.an, o);
         for (int k = 0; k < 3; ++k) o[k] += p[k];
         float S[6] = {a[0], a[1], a[2], 0.f, 0.f, 0.f};
         cross3(o, a, S + 3);
