@@ -182,20 +182,41 @@ __device__ __forceinline__ float half_sum(float v) {
   return row_pair_sum(v);
 }
 
-// half_sum of N independent values, step by step, so the N butterflies interleave (the DPP
-// results of one value fill the other values' hazard slots).  Same arithmetic as half_sum.
+// Sums over the half-wave of N independent values (the W pass and the PGS), two at a time: the
+// first v_permlane16_swap exchanges row 1 of value a with row 0 of value b, so one add leaves
+// a_l + a_(l+16) in row 0 and b_l + b_(l+16) in row 1; the DPP butterfly then finishes both sums at
+// once (A in every lane of row 0, B in row 1), and a second swap hands A and B to every lane of the
+// half.  A pair costs 8 instructions instead of 14; an odd last value takes the swap with itself
+// first (7).  The tree: the cross-row add, then a balanced tree over the 16 row lanes (oracle
+// tree32); every lane gets the bit-identical value.
 template <int N>
 __device__ __forceinline__ void half_sum_n(float (&v)[N]) {
+  constexpr int P = (N + 1) / 2;
+  float c[P];
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp<0xB1>(v[i]);
+  for (int p = 0; p < P; ++p) {
+    const int b = 2 * p + 1 < N ? 2 * p + 1 : 2 * p;
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_int(v[2 * p]), __float_as_int(v[b]), false, false);
+    c[p] = __int_as_float(s[0]) + __int_as_float(s[1]);
+  }
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp<0x4E>(v[i]);
+  for (int p = 0; p < P; ++p) c[p] += dpp<0xB1>(c[p]);
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp<0x141>(v[i]);
+  for (int p = 0; p < P; ++p) c[p] += dpp<0x4E>(c[p]);
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp<0x140>(v[i]);
+  for (int p = 0; p < P; ++p) c[p] += dpp<0x141>(c[p]);
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = row_pair_sum(v[i]);
+  for (int p = 0; p < P; ++p) c[p] += dpp<0x140>(c[p]);
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    if (2 * p + 1 < N) {
+      const auto s = __builtin_amdgcn_permlane16_swap(__float_as_int(c[p]), __float_as_int(c[p]), false, false);
+      v[2 * p] = __int_as_float(s[0]);
+      v[2 * p + 1] = __int_as_float(s[1]);
+    } else {
+      v[2 * p] = c[p];
+    }
+  }
 }
 
 // Exclusive prefix sum over this env's half-wave of a count c in [0, 3], and the half's total:

@@ -57,14 +57,15 @@ typedef struct {
 #define crm as_crm
 #define crf as_crf
 
-/* Sum of 32 lane values as the kernel's half-wave reduction forms it (half_sum: DPP butterflies
- * over lane pairs, quads, 8-lane halves, 16-lane rows, then the two rows): a balanced binary tree
- * over lanes 0..31 in index order.  Lanes past the row's width carry 0. */
+/* Sum of 32 lane values as the kernel's paired half-wave reduction forms it (half_sum_n: lane l of
+ * row 0 adds lane l + 16 of row 1, then DPP butterflies over lane pairs, quads, 8-lane halves and the
+ * 16-lane row): the cross-row add, then a balanced binary tree over the 16 partial sums in index
+ * order.  Lanes past the row's width carry 0. */
 static float tree32(const float* v) {
-  float a[32];
-  for (int i = 0; i < 32; ++i) a[i] = v[i];
-  for (int w = 1; w < 32; w *= 2)
-    for (int i = 0; i < 32; i += 2 * w) a[i] = a[i] + a[i + w];
+  float a[16];
+  for (int i = 0; i < 16; ++i) a[i] = v[i] + v[i + 16];
+  for (int w = 1; w < 16; w *= 2)
+    for (int i = 0; i < 16; i += 2 * w) a[i] = a[i] + a[i + w];
   return a[0];
 }
 
