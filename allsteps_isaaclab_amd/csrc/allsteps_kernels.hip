@@ -632,34 +632,56 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
 // Row j of the joint-space inertia H (lane j):
 //   H_jk = S_k . (Ic_link(j) S_j)  if dof k is on the path of link(j) (k ancestor-or-self),
 //        = S_j . (Ic_link(k) S_k)  if dof j is on the path of link(k),   else 0;  + armature.
-// The masks are per-lane registers loaded once per launch (GeomC): with an LDS copy in Smem::topo
-// the scheduler clusters all 12 NV LDS reads of S and Fh up front and spills.
+// Lane j forms only the first kind, v_jk = S_k . Fh_j for every k (one dot product per column), and
+// publishes its row masked to its path, (k on path(j)) ? v_jk + arm_jk : +0, in LDS; the second kind
+// of element is then the transposed entry of that matrix (lane k's v_kj for j on path(k): the same
+// products in the same order), one b32 read per column.  The matrix aliases the dynamics scratch:
+// every lane has read its Fh row before the first store (a wave's LDS operations complete in issue
+// order).  Lanes past NV read the all-zero padding column NV.
 template <int NV>
-__device__ void h_row(const Consts& K, const EnvS& s, int lane, const Topo& tp, uint32_t anc_j, uint32_t jon,
-                      float (&Hr)[NV]) {
-  // opaque per substep: the 2 x 27 column masks derived from them would otherwise be hoisted out of
-  // the substep loop as SGPR pairs and spilled to VGPR lanes (a readlane per column per substep)
-  asm volatile("" : "+v"(anc_j), "+v"(jon));
+__device__ __forceinline__ void h_row(const Consts& K, EnvS& s, int lane, const Topo& tp, uint32_t anc_j, float (&Hr)[NV]) {
+  static_assert(NV < LDJ, "padding column");
+  // opaque per substep: the 27 column masks derived from it would otherwise be hoisted out of the
+  // substep loop as SGPR pairs and spilled to VGPR lanes (a readlane per column per substep)
+  asm volatile("" : "+v"(anc_j));
   const int j = lane < NV ? lane : 0;
-  float Sj[6], Fj[6];
+  float Fj[6];
 #pragma unroll
-  for (int a = 0; a < 6; ++a) { Sj[a] = s.S[j][a]; Fj[a] = s.x.d.Fh[j][a]; }
+  for (int a = 0; a < 6; ++a) Fj[a] = s.x.d.Fh[j][a];
   const float arm = tp.arm;
-  // Column k's row index passes through an empty asm that also takes column k - kAhead's result, so
-  // its LDS reads cannot be issued before that column is done: at most kAhead columns of reads are
-  // in flight (left alone, the scheduler issues all 12 NV reads of the loop up front and spills).
+  const uint32_t on = lane < NV ? anc_j : 0u;
+  // Column k's S reads pass through an empty asm that also takes column k - kAhead's result, so at
+  // most kAhead columns of reads are in flight (left alone, the scheduler issues them all up front
+  // and spills).
   constexpr int kAhead = 3;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     int kk = k;
     if (k >= kAhead) asm volatile("" : "+v"(kk) : "v"(Hr[k - kAhead]));
-    const bool k_on_j = (anc_j >> k) & 1u;
-    const bool j_on_k = (jon >> k) & 1u;
-    float v1 = dot6(s.S[kk], Fj);
-    float v2 = dot6(Sj, s.x.d.Fh[kk]);
-    float h = k_on_j ? v1 : (j_on_k ? v2 : 0.f);
+    float h = dot6(s.S[kk], Fj);
     h += k == j ? arm : 0.f;
-    Hr[k] = lane < NV ? h : 0.f;
+    Hr[k] = (on >> k) & 1u ? h : 0.f;
+  }
+  float(*M)[LDJ] = s.x.k.Jm;
+  if (lane < NV) {
+#pragma unroll
+    for (int q = 0; q < LDJ / 4; ++q) {
+      float e[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) e[c] = 4 * q + c < NV ? Hr[4 * q + c] : 0.f;
+      *reinterpret_cast<v4f*>(&M[lane][4 * q]) = v4f{e[0], e[1], e[2], e[3]};
+    }
+  }
+  const int jj = lane < NV ? lane : NV;
+  float t[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) t[k] = M[k][jj];
+  // (a register value, not a load: a select between two loads becomes a load from a selected
+  // address, which puts Hr in scratch)
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    asm volatile("" : "+v"(t[k]));
+    Hr[k] = (on >> k) & 1u ? Hr[k] : t[k];
   }
 }
 
@@ -817,7 +839,7 @@ __device__ void emit_contact(EnvS& s, int slot, int ncap, int link, int link2, i
 struct GeomC {
   int link, type, foot;
   float r, p0[3], p1[3];
-  uint32_t anc, jon;  // h_row: dofs on the path of dof j's link; dofs whose path holds j
+  uint32_t anc;  // h_row: dofs on the path of dof j's link
 };
 __device__ __forceinline__ GeomC load_geom(const Consts& K, int lane) {
   const as_model_t& m = K.model;
@@ -834,9 +856,8 @@ __device__ __forceinline__ GeomC load_geom(const Consts& K, int lane) {
   }
   const int j = lane < K.nv ? lane : 0;
   c.anc = K.ancmask[j < 6 ? 0 : j - 5];
-  c.jon = K.ddesc[j];
   // opaque: the values are not rematerialised from memory inside the substep loop
-  asm volatile("" : "+v"(c.link), "+v"(c.type), "+v"(c.foot), "+v"(c.r), "+v"(c.anc), "+v"(c.jon));
+  asm volatile("" : "+v"(c.link), "+v"(c.type), "+v"(c.foot), "+v"(c.r), "+v"(c.anc));
   asm volatile("" : "+v"(c.p0[0]), "+v"(c.p0[1]), "+v"(c.p0[2]), "+v"(c.p1[0]), "+v"(c.p1[1]), "+v"(c.p1[2]));
   return c;
 }
@@ -1263,7 +1284,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   ts.mark(kStLinkQ);
   constexpr int NP = (NV + kSweepB - 1) / kSweepB * kSweepB;  // sweep order, padded with identity
   float Hr[NP];
-  h_row<NV>(K, s, lane, tp, gc.anc, gc.jon, *reinterpret_cast<float(*)[NV]>(Hr));
+  h_row<NV>(K, s, lane, tp, gc.anc, *reinterpret_cast<float(*)[NV]>(Hr));
 #pragma unroll
   for (int j = NV; j < NP; ++j) Hr[j] = lane == j ? 1.f : 0.f;
   ts.mark(kStDyn);
