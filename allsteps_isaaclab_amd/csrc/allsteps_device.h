@@ -36,26 +36,27 @@ AS_DEV void task_cross3(const float* a, const float* b, float* o) {
 }
 
 // signed distance from p to an axis-aligned box (center c, half extents h); outward normal
-// Slope sign carrier of t -> sd_box(a + t (b - a)) (convex in t): outside the box the derivative
-// of the squared distance / 2, sum_k o_k s_k D_k; inside the derivative of the deepest slab term,
-// s_ax D_ax (ties to the lowest axis).  Only its sign is used (oracle sd_box_slope).
+// Slope sign carrier of t -> sd_box(a + t (b - a)) (convex in t): outside the box (some slab
+// distance d_k > 0) sum_k o_k s_k D_k, half the derivative of the squared distance; inside the
+// derivative of the deepest slab term, s_ax D_ax (ties to the lowest axis).  Only its sign is used
+// (oracle sd_box_slope, same operations): the offset a - c and D are loop-invariant in the bisection,
+// so a round is one FMA per axis for the point, a max3 for the outside test and an FMA chain for the sum.
 AS_DEV float sd_box_slope(const float* a, const float* b, float t, const float* c, const float* h) {
   float d[3], sD[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const float D = b[k] - a[k];
-    const float r = a[k] + t * D - c[k];
+    const float r = fmaf(t, D, a[k] - c[k]);
     sD[k] = r >= 0.f ? D : -D;
     d[k] = fabsf(r) - h[k];
   }
   const float o0 = fmaxf(d[0], 0.f), o1 = fmaxf(d[1], 0.f), o2 = fmaxf(d[2], 0.f);
-  const float out2 = o0 * o0 + o1 * o1 + o2 * o2;
-  const float g_out = o0 * sD[0] + o1 * sD[1] + o2 * sD[2];
+  const float g_out = fmaf(o2, sD[2], fmaf(o1, sD[1], o0 * sD[0]));
   int ax = 0;
   if (d[1] > d[ax]) ax = 1;
   if (d[2] > d[ax]) ax = 2;
   const float g_in = ax == 0 ? sD[0] : (ax == 1 ? sD[1] : sD[2]);
-  return out2 > 0.f ? g_out : g_in;
+  return fmaxf(d[0], fmaxf(d[1], d[2])) > 0.f ? g_out : g_in;
 }
 
 AS_DEV float sd_box(const float* p, const float* c, const float* h, float* nrm) {

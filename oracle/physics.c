@@ -342,20 +342,22 @@ static void matvec_n(const float* A, int n, const float* b, float* x) {
 /* ---------------------------------------------------------------- collision (boxes, spheres, capsules) */
 
 /* signed distance from p to an axis-aligned box (center c, half extents h); normal out of box */
-/* Slope sign carrier of t -> sd_box(a + t (b - a)), convex in t: outside the box sum_k o_k s_k D_k
- * (half the derivative of the squared distance), inside s_ax D_ax of the deepest slab (ties to the
- * lowest axis).  Only its sign is used. */
+/* Slope sign carrier of t -> sd_box(a + t (b - a)), convex in t: outside the box (some slab
+ * distance d_k > 0) sum_k o_k s_k D_k (half the derivative of the squared distance, o_k = max(d_k, 0)),
+ * inside s_ax D_ax of the deepest slab (ties to the lowest axis).  Only its sign is used.  The point
+ * offset is fmaf(t, D, a - c), the sum an fmaf chain: the HIP kernel's form (allsteps_device.h). */
 static float sd_box_slope(const float a[3], const float b[3], float t, const float c[3], const float h[3]) {
   float d[3], sD[3];
   for (int k = 0; k < 3; ++k) {
     const float D = b[k] - a[k];
-    const float r = a[k] + t * D - c[k];
+    const float r = fmaf(t, D, a[k] - c[k]);
     sD[k] = r >= 0.f ? D : -D;
     d[k] = fabsf(r) - h[k];
   }
-  float o0 = d[0] > 0.f ? d[0] : 0.f, o1 = d[1] > 0.f ? d[1] : 0.f, o2 = d[2] > 0.f ? d[2] : 0.f;
-  float out2 = o0 * o0 + o1 * o1 + o2 * o2;
-  if (out2 > 0.f) return o0 * sD[0] + o1 * sD[1] + o2 * sD[2];
+  if (fmaxf(d[0], fmaxf(d[1], d[2])) > 0.f) {
+    float o0 = d[0] > 0.f ? d[0] : 0.f, o1 = d[1] > 0.f ? d[1] : 0.f, o2 = d[2] > 0.f ? d[2] : 0.f;
+    return fmaf(o2, sD[2], fmaf(o1, sD[1], o0 * sD[0]));
+  }
   int ax = 0;
   if (d[1] > d[ax]) ax = 1;
   if (d[2] > d[ax]) ax = 2;
