@@ -1155,25 +1155,30 @@ __device__ __forceinline__ void w_pass(EnvS& s, int lane, const v2f (&H2)[(NV + 
                                        float (&Jc)[MAXR], float& arr, float& acp) {
   const int jc = lane < NV ? lane : 0;
   const float jmask = lane < NV ? 1.f : 0.f;
+  typedef __attribute__((address_space(3))) const v4f* lds_v4p;
+  typedef __attribute__((address_space(3))) const float* lds_fp;
+  lds_v4p jrow = (lds_v4p)(&s.x.k.Jm[0][0]);  // 16-B aligned rows
+  lds_fp jcol = (lds_fp)(&s.x.k.Jm[0][jc]);
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int r0 = kRowGroup * g;
-    // the group's row index passes through an empty asm that also takes the W of the group two
-    // back, so at most two groups of J-row reads are in flight (hoisted further they spill)
-    int rr = r0;
-    if (r0 >= 2 * kRowGroup) asm volatile("" : "+v"(rr) : "v"(Wc[r0 >= 2 * kRowGroup ? r0 - kRowGroup - 1 : 0]));
+    // the group's LDS pointers pass through an empty asm that also takes the W of the group two
+    // back, so at most two groups of J-row reads are in flight (hoisted further they spill); the
+    // reads keep immediate offsets from the pinned pointers
+    if (r0 >= 2 * kRowGroup)
+      asm volatile("" : "+v"(jrow), "+v"(jcol) : "v"(Wc[r0 >= 2 * kRowGroup ? r0 - kRowGroup - 1 : 0]));
     // the two partial sums (even / odd k) as one packed pair: (w_e, w_o) += (H_k, H_k+1) (J_k, J_k+1)
     // is v_pk_fma_f32 on register pairs as they come from the b128 reads, no repacking moves
     v2f w[kRowGroup];
     float jown[kRowGroup];
 #pragma unroll
     for (int u = 0; u < kRowGroup; ++u) {
-      jown[u] = s.x.k.Jm[rr + u][jc];
+      jown[u] = jcol[(r0 + u) * LDJ];
       w[u] = v2f{0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < kRowGroup; ++u) {
-      const v4f* jr = reinterpret_cast<const v4f*>(s.x.k.Jm[rr + u]);  // 16-B aligned rows
+      const lds_v4p jr = jrow + (r0 + u) * (LDJ / 4);
 #pragma unroll
       for (int q = 0; q < LDJ / 4; ++q) {
         const v4f t = jr[q];
@@ -1210,6 +1215,8 @@ __device__ __forceinline__ void w_pass(EnvS& s, int lane, const v2f (&H2)[(NV + 
 template <int NG>
 __device__ __forceinline__ void pgs_sweeps(const EnvS& s, int iters, float& uj, float (&lamr)[MAXR],
                                            const float (&Jc)[MAXR], const float (&Wc)[MAXR]) {
+  typedef __attribute__((address_space(3))) const v4f* lds_v4p;
+  lds_v4p meta = (lds_v4p)(&s.rmeta[0][0]);
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
     float uprev = uj;
@@ -1217,19 +1224,19 @@ __device__ __forceinline__ void pgs_sweeps(const EnvS& s, int iters, float& uj, 
     for (int g = 0; g < NG; ++g) {
       const int r = kRowGroup * g;
       // the group's metadata reads are pinned behind the previous group's start (its u): one
-      // group of reads ahead, none hoisted out of the sweep loop (30 rows would not fit)
-      int rr = r;
-      asm volatile("" : "+v"(rr) : "v"(uprev));
+      // group of reads ahead, none hoisted out of the sweep loop (30 rows would not fit).  The pin
+      // is on the LDS row pointer itself, so the reads keep immediate offsets (no address VALU).
+      asm volatile("" : "+v"(meta) : "v"(uprev));
       uprev = uj;
-      const v4f m0 = *reinterpret_cast<const v4f*>(s.rmeta[rr]);
-      const v4f m1 = *reinterpret_cast<const v4f*>(s.rmeta[rr + 1]);
-      const v4f m2 = *reinterpret_cast<const v4f*>(s.rmeta[rr + 2]);
+      const v4f m0 = meta[r];
+      const v4f m1 = meta[r + 1];
+      const v4f m2 = meta[r + 2];
       float vg[3] = {Jc[r] * uj, Jc[r + 1] * uj, Jc[r + 2] * uj};
       half_sum_n(vg);
       // t_s = lambda_s + (target_s - v_s - sum_{r<s} A_sr dl_r) x_s, with the parts that do not
       // depend on this sweep's impulse changes formed first: the chain from one row's dl to the
       // next row's clamp is a single FMA
-      const float k10 = m1.x * m0.w, k20 = m2.x * m1.w, k21 = m2.x * m2.w;  // x_s A_sr
+      const float k10 = m0.w, k20 = m1.w, k21 = m2.w;  // x_s A_sr, formed after the W pass
       float t1 = fmaf(-vg[1], m1.x, fmaf(m1.y, m1.x, lamr[r + 1]));
       float t2 = fmaf(-vg[2], m2.x, fmaf(m2.y, m2.x, lamr[r + 2]));
       // Row types by group: a contact triplet is (normal, tangent, tangent), every other group holds
@@ -1457,8 +1464,12 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   }
   if (lane < MAXR && lane < (maxrow + kRowGroup - 1) / kRowGroup * kRowGroup) {
     s.rmeta[lane][0] = lane < nrow ? 1.0f / (arr + 1e-9f) : 0.f;
-    s.rmeta[lane][3] = acp;
     if (lane >= nrow) { s.rmeta[lane][1] = 0.f; s.rmeta[lane][2] = lane % 3 == 2 ? __builtin_inff() : 0.f; }
+    // the PGS coupling factors x_s A_sr, formed once here instead of in every sweep: row r0 keeps
+    // x_1 A_10, row r0 + 1 x_2 A_20, row r0 + 2 x_2 A_21 (x of the partner row read back from LDS:
+    // the wave's LDS operations complete in issue order)
+    const int partner = lane % 3 == 2 ? lane : lane + 1;
+    s.rmeta[lane][3] = s.rmeta[partner][0] * acp;
   }
   __syncthreads();
   ts.mark(kStWsolve);
