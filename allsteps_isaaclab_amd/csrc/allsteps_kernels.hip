@@ -340,14 +340,24 @@ __device__ __forceinline__ int take_bit(uint32_t& m, bool& valid) {
   return l;
 }
 
+// The dynamics walks read an invalid slot from row kZeroRow of their tables, which holds +0 (written
+// in every substep by lane kZeroRow): adding it is the +0 a select would add, without the select.
+// num_hinges <= AS_ACT_DIM keeps that row past every model's links.
+constexpr int kZeroRow = LMAX - 1;
+static_assert(AS_ACT_DIM + 1 <= kZeroRow, "zero row past the links");
+__device__ __forceinline__ int take_bit_z(uint32_t& m) {
+  const int l = m != 0u ? __builtin_ctz(m) : kZeroRow;
+  m &= m - 1u;
+  return l;
+}
+
 // acc += sum of rows[l] over the set bits l of `mask`, ascending, U rows per iteration.
 template <int W, int U>
 __device__ __forceinline__ void path_sum(uint32_t mask, int n_max, float (&acc)[W], const float (*rows)[W]) {
   for (int it = 0; it < n_max; it += U) {
-    bool v[U];
     int l[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) l[u] = take_bit(mask, v[u]);
+    for (int u = 0; u < U; ++u) l[u] = take_bit_z(mask);
     float x[U][W];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -356,7 +366,7 @@ __device__ __forceinline__ void path_sum(uint32_t mask, int n_max, float (&acc)[
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int k = 0; k < W; ++k) acc[k] += v[u] ? x[u][k] : 0.f;
+      for (int k = 0; k < W; ++k) acc[k] += x[u][k];
   }
 }
 
@@ -481,6 +491,12 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
       }
     }
   }
+  if (kDyn && lane == kZeroRow) {  // the walks' +0 rows (see take_bit_z)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) d.Ib[kZeroRow][k] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d.Sq[kZeroRow][k] = 0.f;
+  }
   if (kDyn) {
     // root columns need the root COM c0 = R0 com_0 (p_0 = 0): every lane forms it itself
     float c0[3];
@@ -540,6 +556,13 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
       for (int k = 0; k < 6; ++k) d.b.cr[lane][k] = cr[k];
     }
   }
+  if (lane == kZeroRow) {  // the walks' +0 rows (see take_bit_z); FK's Rl, which b aliases, is dead
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      d.b.cr[kZeroRow][k] = 0.f;
+      d.b.f[kZeroRow][k] = 0.f;
+    }
+  }
   __syncthreads();
   float f[6], Ib[10];
   if (lane < nl) {
@@ -565,10 +588,9 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
     uint32_t sub = tp.lsub & ~(1u << lane);
     constexpr int kSubU = 4;
     for (int it = 0; it < K.max_sub; it += kSubU) {  // kSubU subtree links per iteration
-      bool v[kSubU];
       int l[kSubU];
 #pragma unroll
-      for (int u = 0; u < kSubU; ++u) l[u] = take_bit(sub, v[u]);
+      for (int u = 0; u < kSubU; ++u) l[u] = take_bit_z(sub);
       float fl[kSubU][6], Il[kSubU][10];
 #pragma unroll
       for (int u = 0; u < kSubU; ++u) {
@@ -580,9 +602,9 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
 #pragma unroll
       for (int u = 0; u < kSubU; ++u) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) f[k] += v[u] ? fl[u][k] : 0.f;
+        for (int k = 0; k < 6; ++k) f[k] += fl[u][k];
 #pragma unroll
-        for (int k = 0; k < 10; ++k) Ib[k] += v[u] ? Il[u][k] : 0.f;
+        for (int k = 0; k < 10; ++k) Ib[k] += Il[u][k];
       }
     }
 #pragma unroll
