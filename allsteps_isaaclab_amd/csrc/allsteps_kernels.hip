@@ -78,6 +78,7 @@ union alignas(16) PhaseScratch {
     alignas(16) float bs[32][4];  //  bounding sphere (segment midpoint, half length + radius)
     int pl[64];         //          pending (stone << 8 | geom) pairs (< 32 + G), then self pairs
     uint32_t need[NST]; //          per candidate stone: geoms past the bounding test
+    alignas(16) float cc[NST][4];  //   per candidate stone: its center relative to the root
   } col;
   struct alignas(16) {
     float q[kSweepB][32];       // sweep: the pivot rows of a round (without the pivot columns)
@@ -925,18 +926,24 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane, int 
     bhi[k] = half_max(gv ? f + r : -1e30f) + margin;
   }
   bool isc = false;
+  float cst[3] = {0.f, 0.f, 0.f};
   if (lane < nst) {
     isc = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const float c = s.stones[3 * lane + k] - s.root_pos[k];
-      isc = isc && (c - h[k] <= bhi[k]) && (c + h[k] >= blo[k]);
+      cst[k] = s.stones[3 * lane + k] - s.root_pos[k];
+      isc = isc && (cst[k] - h[k] <= bhi[k]) && (cst[k] + h[k] >= blo[k]);
     }
   }
   uint64_t bal = __ballot(isc);
   const int half = (threadIdx.x >> 5) & 1;
   uint32_t mine = (uint32_t)(bal >> (32 * half));
-  if (isc) s.cand[__popc(mine & ((1u << lane) - 1u))] = lane;
+  if (isc) {
+    const int pos = __popc(mine & ((1u << lane) - 1u));
+    s.cand[pos] = lane;
+    // the candidate's relative center for pass A (one 16-B broadcast read per candidate there)
+    *reinterpret_cast<v4f*>(s.x.col.cc[pos]) = v4f{cst[0], cst[1], cst[2], 0.f};
+  }
   const int ncand = __popc(mine);
   // narrowphase in two passes.  (A) lane = geom, loop over the candidate stones (once for the
   // priority geoms, once for the rest): the cheap bounding test (spheres: the exact separation)
@@ -1035,13 +1042,17 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane, int 
   // the surviving geoms; the masks then become the pair list class by class (feet first),
   // stone-major, geom-minor
   uint32_t* cneed = s.x.col.need;
+  const float pa[3] = {gtype == 0 ? a[0] : mid[0], gtype == 0 ? a[1] : mid[1], gtype == 0 ? a[2] : mid[2]};
+  const float cap_lim = 0.5f * L + r + margin;
 #pragma unroll 1
   for (int ci = 0; ci < ncand; ++ci) {
-    const int st = s.cand[ci];
-    float c[3], nr[3];
-    for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * st + k] - s.root_pos[k];
+    const v4f cv = *reinterpret_cast<const v4f*>(s.x.col.cc[ci]);
+    const float c[3] = {cv.x, cv.y, cv.z};
+    float nr[3];
+    // one distance per lane: the sphere's center, or the capsule's midpoint for its bounding test
+    const float sd = sd_box(pa, c, h, nr);
     bool need = false;
-    if (gv) need = gtype == 0 ? sd_box(a, c, h, nr) - r < margin : sd_box(mid, c, h, nr) <= 0.5f * L + r + margin;
+    if (gv) need = gtype == 0 ? sd - r < margin : sd <= cap_lim;
     const uint32_t bl = (uint32_t)(__ballot(need) >> (32 * half));
     if (lane == 0) cneed[ci] = bl;
   }
