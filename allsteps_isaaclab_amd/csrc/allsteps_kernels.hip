@@ -236,31 +236,45 @@ __device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
 }
 
-__device__ __forceinline__ uint32_t half_or(uint32_t v) {
-  v |= dpp_u<0xB1>(v);
-  v |= dpp_u<0x4E>(v);
-  v |= dpp_u<0x141>(v);
-  v |= dpp_u<0x140>(v);
-  const auto p = __builtin_amdgcn_permlane16_swap((int)v, (int)v, false, false);
-  return (uint32_t)p[0] | (uint32_t)p[1];
+// OR over the half-wave of two values at once (the pairing of half_sum_n)
+__device__ __forceinline__ void half_or2(uint32_t& x, uint32_t& y) {
+  const auto s = __builtin_amdgcn_permlane16_swap((int)x, (int)y, false, false);
+  uint32_t c = (uint32_t)s[0] | (uint32_t)s[1];
+  c |= dpp_u<0xB1>(c);
+  c |= dpp_u<0x4E>(c);
+  c |= dpp_u<0x141>(c);
+  c |= dpp_u<0x140>(c);
+  const auto t = __builtin_amdgcn_permlane16_swap((int)c, (int)c, false, false);
+  x = (uint32_t)t[0];
+  y = (uint32_t)t[1];
 }
 
-__device__ __forceinline__ float half_min(float v) {
-  v = fminf(v, dpp<0xB1>(v));
-  v = fminf(v, dpp<0x4E>(v));
-  v = fminf(v, dpp<0x141>(v));
-  v = fminf(v, dpp<0x140>(v));
-  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
-  return fminf(__int_as_float(p[0]), __int_as_float(p[1]));
-}
-
-__device__ __forceinline__ float half_max(float v) {
-  v = fmaxf(v, dpp<0xB1>(v));
-  v = fmaxf(v, dpp<0x4E>(v));
-  v = fmaxf(v, dpp<0x141>(v));
-  v = fmaxf(v, dpp<0x140>(v));
-  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
-  return fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
+// half_min of N values two at a time (the pairing of half_sum_n; min is exact, so any order gives
+// the same value)
+template <int N>
+__device__ __forceinline__ void half_min_n(float (&v)[N]) {
+  static_assert(N % 2 == 0, "pairs");
+  constexpr int P = N / 2;
+  float c[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_int(v[2 * p]), __float_as_int(v[2 * p + 1]), false, false);
+    c[p] = fminf(__int_as_float(s[0]), __int_as_float(s[1]));
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) c[p] = fminf(c[p], dpp<0xB1>(c[p]));
+#pragma unroll
+  for (int p = 0; p < P; ++p) c[p] = fminf(c[p], dpp<0x4E>(c[p]));
+#pragma unroll
+  for (int p = 0; p < P; ++p) c[p] = fminf(c[p], dpp<0x141>(c[p]));
+#pragma unroll
+  for (int p = 0; p < P; ++p) c[p] = fminf(c[p], dpp<0x140>(c[p]));
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_int(c[p]), __float_as_int(c[p]), false, false);
+    v[2 * p] = __int_as_float(s[0]);
+    v[2 * p + 1] = __int_as_float(s[1]);
+  }
 }
 
 // diagnostic phase stamps (off when p == nullptr): each wave accumulates its s_memtime deltas per
@@ -917,13 +931,20 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane, int 
   // broadphase (lane = stone): stone boxes that come within the contact margin of the robot's
   // bounding box (union of the geoms' boxes).  Conservative: every pair the narrowphase would
   // turn into a contact survives, so the contact set and order match the oracle's.
-  float blo[3], bhi[3];
+  // the six extents reduced in three pairs, the maxima as minima of the negated values (exact)
+  float blo[3], bhi[3], ext[6];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const float e = gtype == 0 ? a[k] : fminf(a[k], bb[k]);
     const float f = gtype == 0 ? a[k] : fmaxf(a[k], bb[k]);
-    blo[k] = half_min(gv ? e - r : 1e30f) - margin;
-    bhi[k] = half_max(gv ? f + r : -1e30f) + margin;
+    ext[k] = gv ? e - r : 1e30f;
+    ext[3 + k] = gv ? -(f + r) : 1e30f;
+  }
+  half_min_n(ext);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    blo[k] = ext[k] - margin;
+    bhi[k] = -ext[3 + k] + margin;
   }
   bool isc = false;
   float cst[3] = {0.f, 0.f, 0.f};
@@ -1566,11 +1587,13 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       case 10: contact_flag<10>(s, lane, nce, dt, b); break;
       default: break;
     }
-    mask_out[0] = half_or(b[0]);
-    mask_out[1] = half_or(b[1]);
+    half_or2(b[0], b[1]);
+    mask_out[0] = b[0];
+    mask_out[1] = b[1];
     if (K.st_has_hind) {  // wave-uniform: only a state with the hind-feet masks (quadruped)
-      mask_out[2] = half_or(b[2]);
-      mask_out[3] = half_or(b[3]);
+      half_or2(b[2], b[3]);
+      mask_out[2] = b[2];
+      mask_out[3] = b[3];
     }
   }
   // ---- integrate
