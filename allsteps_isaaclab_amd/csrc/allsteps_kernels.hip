@@ -738,45 +738,45 @@ __device__ __forceinline__ void h_row(const Consts& K, EnvS& s, int lane, const 
 // sequential pivots, so the chain on each sweep round's critical path is two divisions deep.
 //   M = [A B; C D]:  Ai = A^-1, X = Ai B, Y = C Ai, S = D - C X, Si = S^-1,
 //   M^-1 = [Ai + (X Si) Y, -(X Si); -(Si Y), Si]       (oracle/physics.c block_inverse: same order)
-__device__ __forceinline__ void inv2(float a, float b, float c, float d, float (&o)[2][2]) {
+// The 2x2 blocks are kept as rows of packed pairs: a row of a product is one v_pk_mul + one
+// v_pk_fma (per element the same mul and fmaf as the scalar form), the Schur difference and the
+// final sum one v_pk_add each.
+__device__ __forceinline__ void inv2(float a, float b, float c, float d, v2f (&o)[2]) {
   const float id = 1.0f / fmaf(a, d, -(b * c));
-  o[0][0] = d * id; o[0][1] = -b * id; o[1][0] = -c * id; o[1][1] = a * id;
+  o[0] = v2f{d, -b} * v2f{id, id};
+  o[1] = v2f{-c, a} * v2f{id, id};
 }
-__device__ __forceinline__ void mul2(const float (&x)[2][2], const float (&y)[2][2], float (&o)[2][2]) {
+__device__ __forceinline__ void mul2(const v2f (&x)[2], const v2f (&y)[2], v2f (&o)[2]) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) o[i][j] = fmaf(x[i][1], y[1][j], x[i][0] * y[0][j]);
+    o[i] = __builtin_elementwise_fma(v2f{x[i].y, x[i].y}, y[1], v2f{x[i].x, x[i].x} * y[0]);
 }
 template <int B>
 __device__ __forceinline__ void block_inverse(float (&M)[B][B]) {  // M <- M^-1 (SPD)
   static_assert(B == 4, "2x2-block Schur inverse");
-  const float A[2][2] = {{M[0][0], M[0][1]}, {M[1][0], M[1][1]}};
-  const float Bm[2][2] = {{M[0][2], M[0][3]}, {M[1][2], M[1][3]}};
-  const float C[2][2] = {{M[2][0], M[2][1]}, {M[3][0], M[3][1]}};
-  const float D[2][2] = {{M[2][2], M[2][3]}, {M[3][2], M[3][3]}};
-  float Ai[2][2], X[2][2], Y[2][2], CX[2][2], S[2][2], Si[2][2], XS[2][2], XSY[2][2], SY[2][2];
-  inv2(A[0][0], A[0][1], A[1][0], A[1][1], Ai);
+  const v2f A[2] = {v2f{M[0][0], M[0][1]}, v2f{M[1][0], M[1][1]}};
+  const v2f Bm[2] = {v2f{M[0][2], M[0][3]}, v2f{M[1][2], M[1][3]}};
+  const v2f C[2] = {v2f{M[2][0], M[2][1]}, v2f{M[3][0], M[3][1]}};
+  const v2f D[2] = {v2f{M[2][2], M[2][3]}, v2f{M[3][2], M[3][3]}};
+  v2f Ai[2], X[2], Y[2], CX[2], S[2], Si[2], XS[2], XSY[2], SY[2];
+  inv2(A[0].x, A[0].y, A[1].x, A[1].y, Ai);
   mul2(Ai, Bm, X);
   mul2(C, Ai, Y);
   mul2(C, X, CX);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) S[i][j] = D[i][j] - CX[i][j];
-  inv2(S[0][0], S[0][1], S[1][0], S[1][1], Si);
+  for (int i = 0; i < 2; ++i) S[i] = D[i] - CX[i];
+  inv2(S[0].x, S[0].y, S[1].x, S[1].y, Si);
   mul2(X, Si, XS);
   mul2(XS, Y, XSY);
   mul2(Si, Y, SY);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      M[i][j] = Ai[i][j] + XSY[i][j];
-      M[i][2 + j] = -XS[i][j];
-      M[2 + i][j] = -SY[i][j];
-      M[2 + i][2 + j] = Si[i][j];
-    }
+  for (int i = 0; i < 2; ++i) {
+    const v2f top = Ai[i] + XSY[i];
+    M[i][0] = top.x; M[i][1] = top.y;
+    M[i][2] = -XS[i].x; M[i][3] = -XS[i].y;
+    M[2 + i][0] = -SY[i].x; M[2 + i][1] = -SY[i].y;
+    M[2 + i][2] = Si[i].x; M[2 + i][3] = Si[i].y;
+  }
 }
 
 template <int NP, int B>
