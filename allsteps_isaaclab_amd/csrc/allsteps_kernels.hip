@@ -437,9 +437,16 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
   float R0[9];
   quat_to_mat(s.root_quat, R0);
   if (lane < nl) {
-    float R[9], p[3] = {0.f, 0.f, 0.f};
+    // The running rotation as packed pairs of its first two rows (P[k] = (R_0k, R_1k)) plus the
+    // third row: R Tl and R t are then one v_pk_mul + two v_pk_fma per column for two rows (the
+    // matmul3 / matvec3 fmaf chains element by element), the third row scalar.
+    v2f P[3], pp = v2f{0.f, 0.f};
+    float r2[3], p2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) R[k] = R0[k];
+    for (int k = 0; k < 3; ++k) {
+      P[k] = v2f{R0[k], R0[3 + k]};
+      r2[k] = R0[6 + k];
+    }
     // kPathU path links per iteration: their local transforms are loaded before the products
     constexpr int kPathU = 4;
     uint32_t path = tp.lpath & ~1u;
@@ -455,14 +462,37 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
         for (int k = 0; k < 12; ++k) Tl[u][k] = d.Rl[l[u]][k];
 #pragma unroll
       for (int u = 0; u < kPathU; ++u) {
-        float Rn[9], wp[3];
-        matmul3(R, Tl[u], Rn);
-        matvec3(R, Tl[u] + 9, wp);
+        const float* T = Tl[u];
+        v2f Pn[3];
+        float r2n[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) p[k] = v[u] ? p[k] + wp[k] : p[k];
+        for (int j = 0; j < 3; ++j) {
+          Pn[j] = __builtin_elementwise_fma(P[2], v2f{T[6 + j], T[6 + j]},
+                                            __builtin_elementwise_fma(P[1], v2f{T[3 + j], T[3 + j]},
+                                                                      P[0] * v2f{T[j], T[j]}));
+          r2n[j] = fmaf(r2[2], T[6 + j], fmaf(r2[1], T[3 + j], r2[0] * T[j]));
+        }
+        const v2f wpp = __builtin_elementwise_fma(P[2], v2f{T[11], T[11]},
+                                                  __builtin_elementwise_fma(P[1], v2f{T[10], T[10]},
+                                                                            P[0] * v2f{T[9], T[9]}));
+        const float wp2 = fmaf(r2[2], T[11], fmaf(r2[1], T[10], r2[0] * T[9]));
+        const v2f ps = pp + wpp;
+        pp = v2f{v[u] ? ps.x : pp.x, v[u] ? ps.y : pp.y};
+        p2 = v[u] ? p2 + wp2 : p2;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) R[k] = v[u] ? Rn[k] : R[k];
+        for (int j = 0; j < 3; ++j) {
+          P[j] = v2f{v[u] ? Pn[j].x : P[j].x, v[u] ? Pn[j].y : P[j].y};
+          r2[j] = v[u] ? r2n[j] : r2[j];
+        }
       }
+    }
+    float R[9];
+    const float p[3] = {pp.x, pp.y, p2};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      R[j] = P[j].x;
+      R[3 + j] = P[j].y;
+      R[6 + j] = r2[j];
     }
 #pragma unroll
     for (int k = 0; k < 9; ++k) s.R[lane][k] = R[k];
