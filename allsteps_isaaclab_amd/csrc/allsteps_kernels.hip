@@ -1231,62 +1231,94 @@ __device__ __forceinline__ void contact_flag(const EnvS& s, int lane, int nce, f
   if (lane < nce && f >= 0 && sqrtf(fx * fx + fy * fy + fz * fz) / dt > 1e-4f) b[f & 3] = 1u << st;
 }
 
-// W = H^-1 J^T over NG row groups (see substep): lane j's W and J columns go to registers for the
-// PGS; per group the half-wave reduces A_rr = J_r . W_r and the in-group couplings A_10, A_20, A_21
-// (A_sr = J_s . W_r), lane r keeping those of row r.
-template <int NV, int NG>
-__device__ __forceinline__ void w_pass(EnvS& s, int lane, const v2f (&H2)[(NV + 1) / 2], float (&Wc)[MAXR],
-                                       float (&Jc)[MAXR], float& arr, float& acp) {
-  const int jc = lane < NV ? lane : 0;
-  const float jmask = lane < NV ? 1.f : 0.f;
-  typedef __attribute__((address_space(3))) const v4f* lds_v4p;
-  typedef __attribute__((address_space(3))) const float* lds_fp;
-  lds_v4p jrow = (lds_v4p)(&s.x.k.Jm[0][0]);  // 16-B aligned rows
-  lds_fp jcol = (lds_fp)(&s.x.k.Jm[0][jc]);
+// Dot product of two padded rows held as packed pairs: two interleaved partial sums (even / odd
+// element, fmaf chains ascending; v_pk_fma_f32 is the two fmafs), added at the end.  oracle/physics.c
+// dot_pairs is the same arithmetic.
+template <int NPR>
+__device__ __forceinline__ float dot_pairs(const v2f (&a)[NPR], const v2f (&b)[NPR]) {
+  v2f p = v2f{0.f, 0.f};
 #pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    const int r0 = kRowGroup * g;
-    // the group's LDS pointers pass through an empty asm that also takes the W of the group two
-    // back, so at most two groups of J-row reads are in flight (hoisted further they spill); the
-    // reads keep immediate offsets from the pinned pointers
-    if (r0 >= 2 * kRowGroup)
-      asm volatile("" : "+v"(jrow), "+v"(jcol) : "v"(Wc[r0 >= 2 * kRowGroup ? r0 - kRowGroup - 1 : 0]));
-    // the two partial sums (even / odd k) as one packed pair: (w_e, w_o) += (H_k, H_k+1) (J_k, J_k+1)
-    // is v_pk_fma_f32 on register pairs as they come from the b128 reads, no repacking moves
-    v2f w[kRowGroup];
-    float jown[kRowGroup];
+  for (int i = 0; i < NPR; ++i) p = __builtin_elementwise_fma(a[i], b[i], p);
+  return p.x + p.y;
+}
+
+// W = H^-1 J^T for both envs of the wave on the matrix cores: v_mfma_f32_32x32x1_2b_f32 holds one
+// 32 x 32 block per env (block b = lanes 32b..32b+31), K = 1 per instruction, so step k takes lane r's
+// J_rk as the A operand (the lane built row r: no data movement) and lane j's (H^-1)_jk as the B
+// operand (lane j holds row j of H^-1 after the sweep), and after NV steps block b holds
+//   W_r[j] = sum_k J_rk (H^-1)_jk,   an fmaf chain over k ascending (gfx950 f32 MFMA numerics:
+// bit for bit D = fma(a_k, b_k, C) per step -- scripts/probes/mfma_2b_probe.hip checks the layout and
+// the chain on hardware; oracle/physics.c forms the same chain).  The result's layout (register v of
+// block b: row 8(v/4) + 4h + v%4 on lane half h, column j = lane % 32) is brought to "lane j holds W_rj
+// for every row r of its own env" by one v_permlane32_swap per register pair (blocks 0 and 1 trade
+// their upper / lower halves).  The projections then need W by rows: lane j stores its column into
+// the J image (after lane j has read its J column, the PGS's Jc), and
+//   lane r forms A_rr = J_r . W_r and the in-triplet projections A_sr = J_s . W_r (r < s; lane s, from
+//   the W rows of the two rows before it): each row's PGS coupling x_s A_sr is formed and stored by
+//   that lane (no lane reads another lane's LDS result without a barrier in between).
+// Cost per substep: NV MFMAs (64 cycles each on the SIMD's matrix pipe), independent of the row
+// count; the LDS carries only the transposes.
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+template <int NV>
+__device__ __forceinline__ void w_rows(EnvS& s, int lane, int nrow, const float* Hr, const v2f (&Jr)[LDJ / 2],
+                                       float (&Jc)[MAXR], float (&Wc)[MAXR]) {
+  static_assert(NV < LDJ, "padding column NV");
+  static_assert(MAXR <= 32, "rows of one MFMA block");
+  constexpr int NQ = (NV + 3) / 4;  // 16-B quads of a row that hold dofs
+  float(*M)[LDJ] = s.x.k.Jm;
+  const int jc = lane < NV ? lane : NV;  // column NV is +0 in the J image
 #pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      jown[u] = jcol[(r0 + u) * LDJ];
-      w[u] = v2f{0.f, 0.f};
-    }
+  for (int r = 0; r < MAXR; ++r) Jc[r] = M[r][jc];
+  f32x32 acc = {};
 #pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      const lds_v4p jr = jrow + (r0 + u) * (LDJ / 4);
+  for (int k = 0; k < NV; ++k) {
+    const float jk = k & 1 ? Jr[k >> 1].y : Jr[k >> 1].x;
+    acc = __builtin_amdgcn_mfma_f32_32x32x1f32(jk, Hr[k], acc, 0, 0, 0);
+  }
+  float wr[32];
 #pragma unroll
-      for (int q = 0; q < LDJ / 4; ++q) {
-        const v4f t = jr[q];
-        if (4 * q + 1 < NV) w[u] = __builtin_elementwise_fma(H2[2 * q], t.xy, w[u]);
-        if (4 * q + 3 < NV) w[u] = __builtin_elementwise_fma(H2[2 * q + 1], t.zw, w[u]);
-        else if (4 * q + 2 < NV) w[u].x = fmaf(H2[2 * q + 1].x, t.z, w[u].x);
-      }
-    }
-    float wu[kRowGroup], a[2 * kRowGroup];
+  for (int v = 0; v < 16; ++v) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(acc[v]), __float_as_int(acc[16 + v]), false, false);
+    const int r0 = 8 * (v >> 2) + (v & 3);
+    wr[r0] = __int_as_float(p[0]);
+    wr[r0 + 4] = __int_as_float(p[1]);
+  }
 #pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      wu[u] = w[u].x + w[u].y;
-      Wc[r0 + u] = wu[u];
-      Jc[r0 + u] = jown[u] * jmask;
-      a[u] = jown[u] * wu[u];
-    }
-    a[3] = jown[1] * wu[0];  // A_10, kept by row r0
-    a[4] = jown[2] * wu[0];  // A_20, kept by row r0 + 1
-    a[5] = jown[2] * wu[1];  // A_21, kept by row r0 + 2
-    half_sum_n(a);
+  for (int r = 0; r < MAXR; ++r) Wc[r] = wr[r];
+  __syncthreads();  // every lane's J column reads are done
+  if (lane < LDJ) {
 #pragma unroll
-    for (int u = 0; u < kRowGroup; ++u) {
-      arr = lane == r0 + u ? a[u] : arr;
-      acp = lane == r0 + u ? a[kRowGroup + u] : acp;
+    for (int r = 0; r < MAXR; ++r) M[r][lane] = wr[r];
+  }
+  __syncthreads();
+  v2f jn[2 * NQ];
+#pragma unroll
+  for (int i = 0; i < 2 * NQ; ++i) jn[i] = Jr[i];
+  const int r0 = lane < MAXR ? lane : 0;
+  const int r1 = lane >= 1 ? min(lane - 1, MAXR - 1) : 0, r2 = lane >= 2 ? min(lane - 2, MAXR - 1) : 0;
+  v2f w0[2 * NQ], w1[2 * NQ], w2[2 * NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const v4f c = *reinterpret_cast<const v4f*>(&M[r0][4 * q]);
+    const v4f a = *reinterpret_cast<const v4f*>(&M[r1][4 * q]);
+    const v4f b = *reinterpret_cast<const v4f*>(&M[r2][4 * q]);
+    w0[2 * q] = c.xy; w0[2 * q + 1] = c.zw;
+    w1[2 * q] = a.xy; w1[2 * q + 1] = a.zw;
+    w2[2 * q] = b.xy; w2[2 * q + 1] = b.zw;
+  }
+  const float arr = dot_pairs(jn, w0);  // A_{lane, lane}
+  const float a1 = dot_pairs(jn, w1);   // A_{lane, lane-1}
+  const float a2 = dot_pairs(jn, w2);   // A_{lane, lane-2}
+  if (lane < MAXR) {
+    const float x = lane < nrow ? 1.0f / (arr + 1e-9f) : 0.f;
+    s.rmeta[lane][0] = x;
+    if (lane >= nrow) { s.rmeta[lane][1] = 0.f; s.rmeta[lane][2] = lane % 3 == 2 ? __builtin_inff() : 0.f; }
+    // the PGS coupling factors x_s A_sr: row r0 holds x_1 A_10, row r0 + 1 x_2 A_20, row r0 + 2 x_2 A_21
+    const int t = lane % 3;
+    if (t == 1) s.rmeta[lane - 1][3] = x * a1;
+    if (t == 2) {
+      s.rmeta[lane - 1][3] = x * a2;
+      s.rmeta[lane][3] = x * a1;
     }
   }
 }
@@ -1471,7 +1503,9 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   //      J_rj = S_j . f6_r for the dofs whose link lies on the path root..link(r) (lpath of the
   //      row's link; dof j < 6 moves every link), minus the same on the second link's path for a
   //      self contact; a limit row is +-1 at its dof.  Every row < MAXR is written (zero past nrow),
-  //      all rows at once: no per-row LDS round trip, no loop.
+  //      all rows at once: no per-row LDS round trip, no loop.  Lane r keeps its row in registers
+  //      for W_r (w_rows).
+  v2f Jr[LDJ / 2];
   {
     const int rr = lane < MAXR ? lane : 0;
     const int c = rr / 3, u = rr - 3 * c;
@@ -1513,48 +1547,17 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
           jq[e] = 0.f;
         }
       }
+      Jr[2 * q] = v2f{jq[0], jq[1]};
+      Jr[2 * q + 1] = v2f{jq[2], jq[3]};
       if (lane < MAXR) *reinterpret_cast<v4f*>(&s.x.k.Jm[lane][4 * q]) = v4f{jq[0], jq[1], jq[2], jq[3]};
     }
   }
   __syncthreads();
   ts.mark(kStRows);
-  // W rows, one group per iteration (unrolled, so that lane j's W column stays in registers
-  // for the PGS sweep); each row's dot product runs as two interleaved partial sums.
-  // Hr is zero on lanes >= NV, so their W entries are zero; they read J column 0 (keeps every LDS
-  // address in bounds).  Per group, the half-wave reduces A_rr = J_r . W_r of its rows and the
-  // in-group couplings A_10, A_20, A_21 (A_sr = J_s . W_r) that the PGS sweep uses; lane r keeps
-  // the values of row r, and the reciprocals are formed at once, one row per lane.
-  float arr = 0.f, acp = 0.f;
-  v2f H2[(NV + 1) / 2];  // row `lane` of H^-1 in (even, odd) pairs
-#pragma unroll
-  for (int k = 0; k < (NV + 1) / 2; ++k) H2[k] = v2f{Hr[2 * k], 2 * k + 1 < NV ? Hr[2 * k + 1] : 0.f};
-  float Wc[MAXR], Jc[MAXR];  // lane j's W and J columns, for the PGS sweep
-#pragma unroll
-  for (int r = 0; r < MAXR; ++r) Wc[r] = Jc[r] = 0.f;
-  // one instantiation per row-group count (maxrow is wave-uniform), as for the PGS below
-  const int ngroups = (__builtin_amdgcn_readfirstlane(maxrow) + kRowGroup - 1) / kRowGroup;
-  switch (ngroups) {
-    case 1: w_pass<NV, 1>(s, lane, H2, Wc, Jc, arr, acp); break;
-    case 2: w_pass<NV, 2>(s, lane, H2, Wc, Jc, arr, acp); break;
-    case 3: w_pass<NV, 3>(s, lane, H2, Wc, Jc, arr, acp); break;
-    case 4: w_pass<NV, 4>(s, lane, H2, Wc, Jc, arr, acp); break;
-    case 5: w_pass<NV, 5>(s, lane, H2, Wc, Jc, arr, acp); break;
-    case 6: w_pass<NV, 6>(s, lane, H2, Wc, Jc, arr, acp); break;
-    case 7: w_pass<NV, 7>(s, lane, H2, Wc, Jc, arr, acp); break;
-    case 8: w_pass<NV, 8>(s, lane, H2, Wc, Jc, arr, acp); break;
-    case 9: w_pass<NV, 9>(s, lane, H2, Wc, Jc, arr, acp); break;
-    case 10: w_pass<NV, 10>(s, lane, H2, Wc, Jc, arr, acp); break;
-    default: break;
-  }
-  if (lane < MAXR && lane < (maxrow + kRowGroup - 1) / kRowGroup * kRowGroup) {
-    s.rmeta[lane][0] = lane < nrow ? 1.0f / (arr + 1e-9f) : 0.f;
-    if (lane >= nrow) { s.rmeta[lane][1] = 0.f; s.rmeta[lane][2] = lane % 3 == 2 ? __builtin_inff() : 0.f; }
-    // the PGS coupling factors x_s A_sr, formed once here instead of in every sweep: row r0 keeps
-    // x_1 A_10, row r0 + 1 x_2 A_20, row r0 + 2 x_2 A_21 (x of the partner row read back from LDS:
-    // the wave's LDS operations complete in issue order)
-    const int partner = lane % 3 == 2 ? lane : lane + 1;
-    s.rmeta[lane][3] = s.rmeta[partner][0] * acp;
-  }
+  // W = H^-1 J^T, A_rr and the in-triplet couplings (w_rows: one row per lane); lane j's W and J
+  // columns go to registers for the PGS.  Hr is zero on lanes >= NV.
+  float Wc[MAXR], Jc[MAXR];
+  w_rows<NV>(s, lane, nrow, Hr, Jr, Jc, Wc);
   __syncthreads();
   ts.mark(kStWsolve);
   // ---- projected Gauss-Seidel (lane j holds u_j; every lane of an env holds all its impulses).

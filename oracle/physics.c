@@ -69,6 +69,17 @@ static float tree32(const float* v) {
   return a[0];
 }
 
+/* Dot product over n (even) entries as the kernel's dot_pairs forms it: two interleaved fmaf chains
+ * (even / odd entries, ascending), added at the end. */
+static float dot_pairs(const float* a, const float* b, int n) {
+  float e = 0.f, o = 0.f;
+  for (int k = 0; k < n; k += 2) {
+    e = fmaf(a[k], b[k], e);
+    o = fmaf(a[k + 1], b[k + 1], o);
+  }
+  return e + o;
+}
+
 static int is_ancestor(const or_model_t* m, int a, int l) {
   while (l > a) l = m->parent[l];
   return l == a;
@@ -654,10 +665,13 @@ static void substep(const or_model_t* m, const or_sim_t* sim, const or_actuator_
     R->J[r][j] = side == 0 ? 1.f : -1.f;
     R->target[r] = err > 0.f ? fminf(sim->baumgarte * err / dt, sim->max_depen_vel) : err / dt;
   }
-  /* W_r = H^-1 J_r^T: per entry two interleaved partial sums (even / odd k, fmaf chains), added at
-   * the end; the projections A_rr = J_r . W_r and the in-triplet couplings A_sr = J_s . W_r
-   * (s > r in the same row triplet) as 32-lane trees (the kernel's W loop, substep()). */
+  /* W_r = H^-1 J_r^T (the kernel's w_rows(): f32 MFMA, bit for bit an fmaf chain): W_r[i] = sum_k J_rk
+   * (H^-1)_ik as one fmaf chain over k ascending, row i of H^-1 as the sweep left it; rows are padded
+   * with +0 to the 16-B width npad.  The projections
+   * A_rr = J_r . W_r and the in-triplet couplings A_sr = J_s . W_r (s > r in the same row triplet) as
+   * two interleaved partial sums over the padded width (dot_pairs). */
   const int ngrp = (R->nrow + 2) / 3, nr3 = 3 * ngrp;
+  const int npad = (nv + 3) / 4 * 4;
   for (int r = R->nrow; r < nr3; ++r) {
     for (int k = 0; k < NV_MAX; ++k) R->J[r][k] = 0.f;
     R->type[r] = 0;
@@ -665,27 +679,20 @@ static void substep(const or_model_t* m, const or_sim_t* sim, const or_actuator_
   }
   float cpl[OR_MAX_ROWS + 3];
   for (int r = 0; r < nr3; ++r) {
-    for (int i = 0; i < nv; ++i) {
-      float w0 = 0.f, w1 = 0.f;
-      for (int k = 0; k < nv; ++k) {
-        if (k & 1) w1 = fmaf(H[i * nv + k], R->J[r][k], w1);
-        else w0 = fmaf(H[i * nv + k], R->J[r][k], w0);
-      }
-      R->W[r][i] = w0 + w1;
+    for (int k = nv; k < npad; ++k) R->J[r][k] = 0.f;
+    for (int i = 0; i < npad; ++i) {
+      float w = 0.f;
+      if (i < nv)
+        for (int k = 0; k < nv; ++k) w = fmaf(R->J[r][k], H[i * nv + k], w);
+      R->W[r][i] = w;
     }
-    float pr[32] = {0.f};
-    for (int k = 0; k < nv; ++k) pr[k] = R->J[r][k] * R->W[r][k];
-    R->Ad[r] = r < R->nrow ? 1.0f / (tree32(pr) + 1e-9f) : 0.f;
+    R->Ad[r] = r < R->nrow ? 1.0f / (dot_pairs(R->J[r], R->W[r], npad) + 1e-9f) : 0.f;
     R->lam[r] = 0.f;
   }
   for (int g = 0; g < ngrp; ++g) {
     const int r0 = 3 * g;
     const int ps[3][2] = {{1, 0}, {2, 0}, {2, 1}}; /* (s, r): A_10, A_20, A_21 */
-    for (int c = 0; c < 3; ++c) {
-      float pr[32] = {0.f};
-      for (int k = 0; k < nv; ++k) pr[k] = R->J[r0 + ps[c][0]][k] * R->W[r0 + ps[c][1]][k];
-      cpl[r0 + c] = tree32(pr);
-    }
+    for (int c = 0; c < 3; ++c) cpl[r0 + c] = dot_pairs(R->J[r0 + ps[c][0]], R->W[r0 + ps[c][1]], npad);
   }
   /* projected Gauss-Seidel, row triplets (the kernel's PGS loop): the three velocities J_r . u of a
    * triplet come from the u at its start, rows 2 and 3 add the in-triplet couplings of this sweep's
