@@ -48,7 +48,7 @@ static_assert(MAXR <= 3 * MAXC, "a row index / 3 is a valid contact slot");
 // ------------------------------------------------------------------------------------------------
 // per-env LDS scratch.  Occupancy at 4096 envs is set by LDS: two envs per 64-lane workgroup must
 // stay <= 20 KB so that 8 workgroups (2 waves/SIMD) fit a CU and 4096 envs run in one round.  The
-// phase-local arrays therefore share one union: FK (Rl) -> dynamics (c, Ib, Ic, Fh, V, A, F) ->
+// phase-local arrays therefore share one union: FK (Rl) -> dynamics (c, Ib, Ic, V, A, F) ->
 // sweep (piv) -> constraint rows (Jm, Wm); each phase ends before the next one writes.
 constexpr int kPrioRows = 6;          // constraint rows per issue-priority level (see substep)
 constexpr int kRowGroup = 3;          // constraint rows per J / W / PGS group (a contact triplet)
@@ -57,7 +57,6 @@ struct DynScratch {
   float c[LMAX][3];
   float Ib[LMAX][10];
   float Ic[LMAX][10];
-  alignas(16) float Fh[NVMAX][8];  // Ic_link(j) S_j (CRBA column forces), rows padded to 32 B
   float Sq[LMAX][6];    // S_i qd_i, later the subtree force sums F_i
   union {
     float Rl[LMAX][12]; // FK: local joint transforms (R 9, p 3); dead before cr / f are written
@@ -573,7 +572,8 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
 //   F_0  = f_0 + sum_{children c of the root, ascending} F_c, likewise Ic_0
 // (oracle/physics.c uses the same summation orders).  Then per dof j: C_j = S_j . F_link(j),
 // b_j = tau_j - C_j (returned, also in LDS), Fh_j = Ic_link(j) S_j.
-__device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, const Topo& tp, float gravity) {
+__device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, const Topo& tp, float gravity,
+                                          float (&Sj)[6], float (&Fj)[6]) {
   const as_model_t& m = K.model;
   const int nl = m.num_links, nv = K.nv;
   DynScratch& d = s.x.d;
@@ -688,45 +688,62 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
     const float Cj = dot6(S, F);
     bj = (j < 6 ? 0.f : s.tau[j - 6]) - Cj;
     s.b[j] = bj;
-    inertia_mul(Ic, S, d.Fh[j]);
-  } else if (lane < 32) {
-    s.b[lane] = 0.f;
+    inertia_mul(Ic, S, Fj);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Sj[k] = S[k];
+  } else {
+    if (lane < 32) s.b[lane] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Sj[k] = Fj[k] = 0.f;
   }
   __syncthreads();
   return bj;
 }
 
+// Two-block f32 MFMA (v_mfma_f32_32x32x1_2b_f32): one 32 x 32 block per env (block b = lanes
+// 32b..32b+31), K = 1 per instruction, lane l supplying A[l % 32][k] and B[k][l % 32] of its own env;
+// the result is bit for bit an fmaf chain over k (scripts/probes/mfma_2b_probe.hip).  Register v of
+// block b holds row 8(v/4) + 4h + v%4 on lane half h, column lane % 32; one v_permlane32_swap per
+// register pair (blocks 0 and 1 trade halves) leaves lane n with column n of its own env's block.
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+__device__ __forceinline__ void mfma_columns(const f32x32& acc, float (&col)[32]) {
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(acc[v]), __float_as_int(acc[16 + v]), false, false);
+    const int r0 = 8 * (v >> 2) + (v & 3);
+    col[r0] = __int_as_float(p[0]);
+    col[r0 + 4] = __int_as_float(p[1]);
+  }
+}
+
 // Row j of the joint-space inertia H (lane j):
 //   H_jk = S_k . (Ic_link(j) S_j)  if dof k is on the path of link(j) (k ancestor-or-self),
 //        = S_j . (Ic_link(k) S_k)  if dof j is on the path of link(k),   else 0;  + armature.
-// Lane j forms only the first kind, v_jk = S_k . Fh_j for every k (one dot product per column), and
-// publishes its row masked to its path, (k on path(j)) ? v_jk + arm_jk : +0, in LDS; the second kind
-// of element is then the transposed entry of that matrix (lane k's v_kj for j on path(k): the same
-// products in the same order), one b32 read per column.  The matrix aliases the dynamics scratch:
-// every lane has read its Fh row before the first store (a wave's LDS operations complete in issue
-// order).  Lanes past NV read the all-zero padding column NV.
+// Every product P_kj = S_k . Fh_j (Fh_j = Ic_link(j) S_j) comes from six K steps of the two-block
+// f32 MFMA (one block per env; A: lane k's S_k, B: lane j's Fh_j, both in registers from dynamics):
+// P_kj is an fmaf chain over the six spatial components (oracle/physics.c chain6).  After the
+// column shuffle lane j holds P_kj for every k: the path-side entries of its row.  Lane j publishes
+// its row masked to its path, (k on path(j)) ? P_kj (+ armature on the diagonal) : +0, in LDS; the
+// other side is the transposed entry of that matrix (lane k's P_jk for j on path(k)), one b32 read
+// per column.  Lanes past NV read the all-zero padding column NV.
 template <int NV>
-__device__ __forceinline__ void h_row(const Consts& K, EnvS& s, int lane, const Topo& tp, uint32_t anc_j, float (&Hr)[NV]) {
+__device__ __forceinline__ void h_row(EnvS& s, int lane, const Topo& tp, uint32_t anc_j, const float (&Sj)[6],
+                                      const float (&Fj)[6], float (&Hr)[NV]) {
   static_assert(NV < LDJ, "padding column");
   // opaque per substep: the 27 column masks derived from it would otherwise be hoisted out of the
   // substep loop as SGPR pairs and spilled to VGPR lanes (a readlane per column per substep)
   asm volatile("" : "+v"(anc_j));
   const int j = lane < NV ? lane : 0;
-  float Fj[6];
+  f32x32 acc = {};
 #pragma unroll
-  for (int a = 0; a < 6; ++a) Fj[a] = s.x.d.Fh[j][a];
+  for (int a = 0; a < 6; ++a) acc = __builtin_amdgcn_mfma_f32_32x32x1f32(Sj[a], Fj[a], acc, 0, 0, 0);
+  float col[32];
+  mfma_columns(acc, col);
   const float arm = tp.arm;
   const uint32_t on = lane < NV ? anc_j : 0u;
-  // Column k's S reads pass through an empty asm that also takes column k - kAhead's result, so at
-  // most kAhead columns of reads are in flight (left alone, the scheduler issues them all up front
-  // and spills).
-  constexpr int kAhead = 3;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    int kk = k;
-    if (k >= kAhead) asm volatile("" : "+v"(kk) : "v"(Hr[k - kAhead]));
-    float h = dot6(s.S[kk], Fj);
-    h += k == j ? arm : 0.f;
+    const float h = k == j ? col[k] + arm : col[k];
     Hr[k] = (on >> k) & 1u ? h : 0.f;
   }
   float(*M)[LDJ] = s.x.k.Jm;
@@ -1258,7 +1275,6 @@ __device__ __forceinline__ float dot_pairs(const v2f (&a)[NPR], const v2f (&b)[N
 //   that lane (no lane reads another lane's LDS result without a barrier in between).
 // Cost per substep: NV MFMAs (64 cycles each on the SIMD's matrix pipe), independent of the row
 // count; the LDS carries only the transposes.
-typedef float f32x32 __attribute__((ext_vector_type(32)));
 template <int NV>
 __device__ __forceinline__ void w_rows(EnvS& s, int lane, int nrow, const float* Hr, const v2f (&Jr)[LDJ / 2],
                                        float (&Jc)[MAXR], float (&Wc)[MAXR]) {
@@ -1276,13 +1292,7 @@ __device__ __forceinline__ void w_rows(EnvS& s, int lane, int nrow, const float*
     acc = __builtin_amdgcn_mfma_f32_32x32x1f32(jk, Hr[k], acc, 0, 0, 0);
   }
   float wr[32];
-#pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(acc[v]), __float_as_int(acc[16 + v]), false, false);
-    const int r0 = 8 * (v >> 2) + (v & 3);
-    wr[r0] = __int_as_float(p[0]);
-    wr[r0 + 4] = __int_as_float(p[1]);
-  }
+  mfma_columns(acc, wr);
 #pragma unroll
   for (int r = 0; r < MAXR; ++r) Wc[r] = wr[r];
   __syncthreads();  // every lane's J column reads are done
@@ -1403,11 +1413,12 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   }
   fk<true>(K, s, lane, tp, lc);  // (its first barrier publishes tau before the dynamics read it)
   ts.mark(kStFK);
-  dynamics(K, s, lane, tp, K.sim.gravity);
+  float Sj[6], Fj[6];  // dof lane j: S_j and Ic_link(j) S_j for the H rows
+  dynamics(K, s, lane, tp, K.sim.gravity, Sj, Fj);
   ts.mark(kStLinkQ);
   constexpr int NP = (NV + kSweepB - 1) / kSweepB * kSweepB;  // sweep order, padded with identity
   float Hr[NP];
-  h_row<NV>(K, s, lane, tp, gc.anc, *reinterpret_cast<float(*)[NV]>(Hr));
+  h_row<NV>(s, lane, tp, gc.anc, Sj, Fj, *reinterpret_cast<float(*)[NV]>(Hr));
 #pragma unroll
   for (int j = NV; j < NP; ++j) Hr[j] = lane == j ? 1.f : 0.f;
   ts.mark(kStDyn);

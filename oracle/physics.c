@@ -182,6 +182,14 @@ static int chain_dofs(const or_model_t* m, int link, int* out) {
   return n;
 }
 
+/* S_k . F as the kernel's two-block MFMA forms it (h_row): one fmaf chain over the six spatial
+ * components, ascending, from +0 */
+static float chain6(const float* s, const float* f) {
+  float a = 0.f;
+  for (int c = 0; c < 6; ++c) a = fmaf(s[c], f[c], a);
+  return a;
+}
+
 static void crba(const or_model_t* m, const kin_t* K, float* H) {
   const int nv = K->nv;
   memset(H, 0, sizeof(float) * (size_t)nv * nv);
@@ -194,7 +202,7 @@ static void crba(const or_model_t* m, const kin_t* K, float* H) {
     for (int t = 0; t < nc; ++t) {
       int k = chain[t];
       if (k > j) continue; /* fill lower triangle (k <= j) and mirror */
-      float h = dot6(K->S[k], Fj);
+      float h = chain6(K->S[k], Fj);
       H[j * nv + k] = h;
       H[k * nv + j] = h;
     }
@@ -204,7 +212,7 @@ static void crba(const or_model_t* m, const kin_t* K, float* H) {
   for (int j = 0; j < OR_NDOF_ROOT; ++j) {
     float Fj[6];
     inertia_mul(K->Ic[0], K->S[j], Fj);
-    for (int k = j + 1; k < OR_NDOF_ROOT; ++k) H[j * nv + k] = dot6(K->S[k], Fj);
+    for (int k = j + 1; k < OR_NDOF_ROOT; ++k) H[j * nv + k] = chain6(K->S[k], Fj);
   }
   for (int i = 1; i < m->num_links; ++i) {
     int j = OR_NDOF_ROOT + i - 1;
