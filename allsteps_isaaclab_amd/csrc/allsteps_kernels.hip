@@ -1536,6 +1536,21 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     const uint32_t pm1 = sm.topo[con ? lk & 31 : 0].lpath & (con ? ~0u : 0u);
     const uint32_t pm2 = sm.topo[con && l2 >= 0 ? l2 & 31 : 0].lpath & (con && l2 >= 0 ? ~0u : 0u);
     const uint32_t live = lane < nrow ? ~0u : 0u;
+    // S_j . f6_r for every (dof j, row r) of both envs: six K steps of the two-block MFMA (A: lane j's
+    // own motion subspace row, B: lane r's f6), an fmaf chain over the components (oracle chain6);
+    // after the column shuffle lane r holds its row's products for every dof
+    float Pj[32];
+    {
+      const int jo = lane < NV ? lane : 0;
+      const v4f s0 = *reinterpret_cast<const v4f*>(&s.S[jo][0]);
+      const v4f s1 = *reinterpret_cast<const v4f*>(&s.S[jo][4]);
+      const float z = lane < NV ? 1.f : 0.f;
+      const float Sa[6] = {s0.x * z, s0.y * z, s0.z * z, s0.w * z, s1.x * z, s1.y * z};
+      f32x32 acc = {};
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc = __builtin_amdgcn_mfma_f32_32x32x1f32(Sa[a], f6[a], acc, 0, 0, 0);
+      mfma_columns(acc, Pj);
+    }
 #pragma unroll
     for (int q = 0; q < LDJ / 4; ++q) {
       float jq[4];
@@ -1543,10 +1558,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       for (int e = 0; e < 4; ++e) {
         const int j = 4 * q + e;
         if (j < NV) {
-          const v4f s0 = *reinterpret_cast<const v4f*>(&s.S[j][0]);
-          const v4f s1 = *reinterpret_cast<const v4f*>(&s.S[j][4]);
-          const float Sj[6] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y};
-          const uint32_t jb = __float_as_uint(dot6(Sj, f6));
+          const uint32_t jb = __float_as_uint(Pj[j]);
           const int lnk = j < 6 ? 0 : j - 5;  // the link dof j moves with
           // contact row: (on path 1 ? jcon : 0) - (on path 2 ? jcon : 0), +0 on a limit row (pm = 0);
           // limit row: sign at its dof, +0 elsewhere and on every contact row (lk >= 0 > -1 - lk)

@@ -572,7 +572,7 @@ static void contact_row(const or_model_t* m, const kin_t* K, int link, int link2
     for (int t = 0; t < nc; ++t) on2[chain[t]] = 1;
   }
   for (int j = 0; j < K->nv; ++j) {
-    const float v = dot6(K->S[j], f6);
+    const float v = chain6(K->S[j], f6);  /* the kernel's MFMA chain */
     J[j] = (on1[j] ? v : 0.f) - (on2[j] ? v : 0.f);
   }
 }
