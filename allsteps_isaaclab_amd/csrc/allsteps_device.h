@@ -85,24 +85,18 @@ AS_DEV float sd_box(const float* p, const float* c, const float* h, float* nrm) 
 
 // ---------------------------------------------------------------- isaaclab.utils.math (math.py)
 
-// math.py:413-444 euler_xyz_from_quat, "% 2pi" = torch.remainder (fmod + sign fix)
-AS_DEV float rem2pi(float a) {
-  const float b = 6.28318530717958647692f;
-  float r = fmodf(a, b);
-  if (r != 0.0f && (r < 0.0f)) r += b;
-  return r;
-}
-
+// math.py:413-444 euler_xyz_from_quat (roll, pitch), "% 2pi" = torch.remainder; atan2 / asin / remainder
+// are the shared deterministic forms of include/as_detmath.h (the oracle computes the same bits)
 AS_DEV void euler_rp_from_quat(const float* q, float* roll, float* pitch) {
   float qw = q[0], qx = q[1], qy = q[2], qz = q[3];
   float sin_roll = 2.0f * (qw * qx + qy * qz);
   float cos_roll = 1.0f - 2.0f * (qx * qx + qy * qy);
-  float r = atan2f(sin_roll, cos_roll);
+  float r = as_atan2f(sin_roll, cos_roll);
   float sin_pitch = 2.0f * (qw * qy - qz * qx);
   float p = fabsf(sin_pitch) >= 1.0f ? 1.57079632679489661923f * (sin_pitch > 0.0f ? 1.0f : -1.0f)
-                                    : asinf(sin_pitch);
-  *roll = rem2pi(r);
-  *pitch = rem2pi(p);
+                                    : as_asinf(sin_pitch);
+  *roll = as_rem2pi(r);
+  *pitch = as_rem2pi(p);
 }
 
 // math.py:605-625 quat_rotate_inverse

@@ -1859,7 +1859,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     float energy_cost = T.energy * en;
     float limit_cost = (float)nlim * T.joint_limit;
     bool cond = u.reached && count == 1 && idx < T.num_steps - 1;
-    float step_rew = cond ? 50.0f * expf(-u.dist_s / 0.25f) : 0.f;
+    float step_rew = cond ? 50.0f * as_expf(-u.dist_s / 0.25f) : 0.f;  // shared deterministic exp
     bool bonus_c = idx == T.num_steps - 1 && u.body_dist < 0.15f;
     float total = T.alive + progress;
     total = total - roll_cost;

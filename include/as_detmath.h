@@ -128,6 +128,76 @@ AS_HD void as_sincosf(float x, float* sn, float* cs) {
   *cs = ((q + 1) & 2) ? -c1 : c1;
 }
 
+/* ---- the task path's transcendentals (allsteps_env.py rewards / observations).  Same construction
+ * as as_sincosf: range reduction and minimax polynomials from +, *, fmaf, division and sqrtf only,
+ * all correctly rounded on both sides, so the device and the host produce the same bits.  Accuracy
+ * (vs double precision): as_atan2f <= 2.5 ulp, as_asinf <= 3 ulp, as_expf <= 2 ulp on the domains
+ * the task uses (Cephes-style coefficients; tests/test_detmath.py measures them). */
+
+/* atan(t) for t in [0, 1]: t > tan(pi/8) is reduced by atan(t) = pi/4 + atan((t - 1) / (t + 1)) */
+AS_HD float as_atan01f(float t) {
+  const int red = t > 0.414213562f;
+  const float z = red ? (t - 1.0f) / (t + 1.0f) : t;
+  const float z2 = z * z;
+  float p = fmaf(8.05374449538e-2f, z2, -1.38776856032e-1f);
+  p = fmaf(p, z2, 1.99777106478e-1f);
+  p = fmaf(p, z2, -3.33329491539e-1f);
+  const float y = fmaf(p * z2, z, z);
+  return red ? y + 0.785398163397448309616f : y;
+}
+
+/* atan2(y, x) with C's signed-zero cases (atan2(+-0, +0) = +-0, atan2(+-0, -0) = +-pi); quadrants
+ * from |y| vs |x| and the signs; the pi/2 and pi complements in two parts (hi + lo) */
+AS_HD float as_atan2f(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const int ysign = signbit(y) != 0;
+  if (ax == 0.0f && ay == 0.0f) {
+    const float r = signbit(x) ? 3.14159265358979323846f : 0.0f;
+    return ysign ? -r : r;
+  }
+  const int swap = ay > ax;
+  const float a = as_atan01f(swap ? ax / ay : ay / ax);
+  float r = swap ? (1.57079637050628662109f - a) + -4.37113900018624283e-08f : a;
+  if (signbit(x)) r = (3.14159274101257324219f - r) + -8.74227800037248566e-08f;
+  return ysign ? -r : r;
+}
+
+/* asin(s) for |s| < 1: |s| > 0.5 uses asin(s) = pi/2 - 2 asin(sqrt((1 - |s|) / 2)) */
+AS_HD float as_asinf(float s) {
+  const float a = fabsf(s);
+  const int big = a > 0.5f;
+  const float z = big ? 0.5f * (1.0f - a) : a * a;
+  const float x = big ? sqrtf(z) : a;
+  float p = fmaf(4.2163199048e-2f, z, 2.4181311049e-2f);
+  p = fmaf(p, z, 4.5470025998e-2f);
+  p = fmaf(p, z, 7.4953002686e-2f);
+  p = fmaf(p, z, 1.6666752422e-1f);
+  float r = fmaf(p * z, x, x);
+  if (big) r = (1.57079637050628662109f - (r + r)) + -4.37113900018624283e-08f;
+  return signbit(s) ? -r : r;
+}
+
+/* exp(x) for x <= 0 (the step reward's exp(-d / 0.25)): k = rint(x log2 e), r = x - k ln 2 in two
+ * fmaf steps, a degree-6 polynomial for e^r on [-ln2/2, ln2/2], scaled by 2^k (ldexpf, exact for the
+ * normal results kept here); x < -87 (e^x below the normal range) gives +0 */
+AS_HD float as_expf(float x) {
+  if (x < -87.0f) return 0.0f;
+  const float k = rintf(x * 1.44269504088896341f);
+  float r = fmaf(-k, 0.693359375f, x);
+  r = fmaf(-k, -2.12194440e-4f, r);
+  float p = fmaf(1.9875691500e-4f, r, 1.3981999507e-3f);
+  p = fmaf(p, r, 8.3334519073e-3f);
+  p = fmaf(p, r, 4.1665795894e-2f);
+  p = fmaf(p, r, 1.6666665459e-1f);
+  p = fmaf(p, r, 5.0000001201e-1f);
+  const float y = fmaf(p, r * r, r) + 1.0f;
+  return ldexpf(y, (int)k);
+}
+
+/* torch.remainder(a, 2 pi) for |a| <= pi (euler_xyz_from_quat's atan2 / asin results, math.py:444):
+ * fmod is the identity there, so the remainder is a + 2 pi for a < 0 and a otherwise (-0 stays -0) */
+AS_HD float as_rem2pi(float a) { return a < 0.0f ? a + 6.28318530717958647692f : a; }
+
 /* Rodrigues rotation about the unit axis a by ang (as_sincosf) */
 AS_HD void as_axis_angle_mat(const float* a, float ang, float* R) {
   float s, c;

@@ -151,6 +151,7 @@ float or_unscale_transform(float x, float lo, float hi);
 
 /* ---- batched helpers for the golden tests ---- */
 void or_math_batch(int n, const float* q, const float* v, float* rpy, float* qri, float* qr);
+void or_detmath_eval(int fn, int n, const float* a, const float* b, float* out);
 void or_sft_batch(int n, const float* t01, const float* q01, const float* t02, float* out);
 void or_footsteps(const or_task_t* task, int n, int level, const float* draws /* [5][n][20] */,
                   float* pos /* [n][20][3] */, float* dphi /* [n][20] */);

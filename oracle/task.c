@@ -13,36 +13,33 @@
 #include <string.h>
 
 #include "oracle.h"
+#include "../include/as_detmath.h"
 
 #define PI_F 3.14159265358979323846f
 
 /* ------------------------------------------------------------------ math helpers (MATH) */
 
-/* MATH:413-444 euler_xyz_from_quat: atan2/asin, then "% 2pi" (torch.remainder: fmod + sign fix). */
-static float rem2pi(float a) {
-  const float b = (float)(2.0 * 3.14159265358979323846);
-  float r = fmodf(a, b);
-  if (r != 0.0f && ((r < 0.0f) != (b < 0.0f))) r += b;
-  return r;
-}
-
+/* MATH:413-444 euler_xyz_from_quat: atan2/asin, then "% 2pi" (torch.remainder).  The transcendentals
+ * are the shared deterministic forms of include/as_detmath.h (the HIP kernel computes the same bits;
+ * within a few ulp of torch's, tests/test_oracle_golden.py); the remainder is the identity + 2 pi
+ * fold on their [-pi, pi] range. */
 void or_euler_xyz_from_quat(const float q[4], float* roll, float* pitch, float* yaw) {
   float qw = q[0], qx = q[1], qy = q[2], qz = q[3];
   float sin_roll = 2.0f * (qw * qx + qy * qz);
   float cos_roll = 1.0f - 2.0f * (qx * qx + qy * qy);
-  float r = atan2f(sin_roll, cos_roll);
+  float r = as_atan2f(sin_roll, cos_roll);
   float sin_pitch = 2.0f * (qw * qy - qz * qx);
   float p;
   if (fabsf(sin_pitch) >= 1.0f) /* copysign(pi/2, sin_pitch): |mag| * sign(x)  (MATH:121-140) */
     p = (float)(3.14159265358979323846 / 2.0) * (sin_pitch > 0.0f ? 1.0f : -1.0f);
   else
-    p = asinf(sin_pitch);
+    p = as_asinf(sin_pitch);
   float sin_yaw = 2.0f * (qw * qz + qx * qy);
   float cos_yaw = 1.0f - 2.0f * (qy * qy + qz * qz);
-  float y = atan2f(sin_yaw, cos_yaw);
-  *roll = rem2pi(r);
-  *pitch = rem2pi(p);
-  *yaw = rem2pi(y);
+  float y = as_atan2f(sin_yaw, cos_yaw);
+  *roll = as_rem2pi(r);
+  *pitch = as_rem2pi(p);
+  *yaw = as_rem2pi(y);
 }
 
 static void cross3(const float a[3], const float b[3], float o[3]) {
@@ -156,9 +153,12 @@ void or_footsteps(const or_task_t* task, int n, int level, const float* draws, f
       if (k == 0) { dr = 0.f; dph = 0.f; dth = half_pi; }         /* ENV:144-146 */
       if (k == 1 || k == 2) { dr = 0.75f; dph = 0.f; dth = half_pi; } /* ENV:148-150 */
       phi += dph;                                                 /* ENV:155 cumsum */
-      float dx = dr * sinf(dth) * cosf(phi);                      /* ENV:157-159 */
-      float dy = dr * sinf(dth) * sinf(phi);
-      float dz = dr * cosf(dth);
+      float st_, ct_, sp, cp;                                     /* the kernel's shared sin / cos */
+      as_sincosf(dth, &st_, &ct_);
+      as_sincosf(phi, &sp, &cp);
+      float dx = dr * st_ * cp;                                   /* ENV:157-159 */
+      float dy = dr * st_ * sp;
+      float dz = dr * ct_;
       x += dx; y += dy; z += dz;                                  /* ENV:165-167 */
       pos[(e * N + k) * 3 + 0] = x;
       pos[(e * N + k) * 3 + 1] = y;
@@ -225,9 +225,12 @@ static void stones_philox(const or_task_t* task, int n, int e, int level, uint64
     if (k == 0) { dr = 0.f; dph = 0.f; dth = half_pi; }
     if (k == 1 || k == 2) { dr = 0.75f; dph = 0.f; dth = half_pi; }
     phi += dph;
-    x += dr * sinf(dth) * cosf(phi);
-    y += dr * sinf(dth) * sinf(phi);
-    z += dr * cosf(dth);
+    float st_, ct_, sp, cp;
+    as_sincosf(dth, &st_, &ct_);
+    as_sincosf(phi, &sp, &cp);
+    x += dr * st_ * cp;
+    y += dr * st_ * sp;
+    z += dr * ct_;
     stones[(size_t)(3 * k + 0) * n + e] = x;
     stones[(size_t)(3 * k + 1) * n + e] = y;
     stones[(size_t)(3 * k + 2) * n + e] = z;
@@ -352,6 +355,17 @@ static void write_obs(const or_task_t* task, const or_state_t* st, int e, const 
   for (int i = 0; i < 9; ++i) o[50 + i] = u->targets_b[i];
 }
 
+/* Sum of n <= 32 per-dof terms (lane k = cfg dof k) as the HIP kernel forms it (k_step half_sum: DPP
+ * butterflies = balanced pairwise trees over lanes 0..15 and 16..31, then row 0 + row 1; lanes past n
+ * add +0).  torch sums in its own reduction order; the golden vectors absorb the difference. */
+static float half_tree32(const float* v, int n) {
+  float a[32] = {0.0f};
+  for (int i = 0; i < n; ++i) a[i] = v[i];
+  for (int w = 1; w < 16; w *= 2)
+    for (int i = 0; i < 32; i += 2 * w) a[i] = a[i] + a[i + w];
+  return a[0] + a[16];
+}
+
 /* ENV:347-394 _get_rewards for one env. */
 static float reward(const or_task_t* task, const or_state_t* st, int e, const useful_t* u, const float* a,
                     int terminated) {
@@ -365,11 +379,12 @@ static float reward(const or_task_t* task, const or_state_t* st, int e, const us
   float lv[3] = {F(st->root_lin, 0, n, e), F(st->root_lin, 1, n, e), F(st->root_lin, 2, n, e)};
   float speed = norm3(lv[0], lv[1], lv[2]);
   float speed_cost = speed > 1.6f ? speed - 1.6f : 0.0f;
-  float ss = 0.0f, en = 0.0f;
+  float sq[21], ea[21];
   for (int k = 0; k < 21; ++k) {
-    ss += a[k] * a[k];
-    en += fabsf(F(st->qd, k, n, e) * a[k]);
+    sq[k] = a[k] * a[k];
+    ea[k] = fabsf(F(st->qd, k, n, e) * a[k]);
   }
+  const float ss = half_tree32(sq, 21), en = half_tree32(ea, 21); /* the kernel's lane tree */
   float action_cost = task->action * sqrtf(ss);
   float energy_cost = task->energy * en;
   int nlim = 0;
@@ -377,7 +392,7 @@ static float reward(const or_task_t* task, const or_state_t* st, int e, const us
   float limit_cost = (float)nlim * task->joint_limit;
   int cond = u->reached && (st->count[e] == 1) && (st->idx[e] < task->num_steps - 1);
   float dist = u->dist_f[st->swing[e]];
-  float step_rew = cond ? 50.0f * expf(-dist / 0.25f) : 0.0f;
+  float step_rew = cond ? 50.0f * as_expf(-dist / 0.25f) : 0.0f;     /* shared deterministic exp */
   int bonus_cond = (st->idx[e] == task->num_steps - 1) && (u->body_dist_xy < 0.15f);
   float bonus = bonus_cond ? 10.0f : 0.0f;
   float total = alive + progress;
@@ -550,4 +565,22 @@ void or_task_post_physics(const or_model_t* model, const or_task_t* task, or_sta
   for (int e = 0; e < n; ++e) write_obs(task, st, e, &u[e], obs + (size_t)e * 59); /* DRL:373 */
   free(u);
   free(done);
+}
+
+/* ------------------------------------------------------------------ shared transcendentals (tests) */
+
+/* Evaluate one of include/as_detmath.h's deterministic functions on n inputs (tests/test_detmath.py
+ * measures their accuracy): fn 0 atan2(a, b), 1 asin(a), 2 exp(a), 3 sin(a), 4 cos(a), 5 rem2pi(a). */
+void or_detmath_eval(int fn, int n, const float* a, const float* b, float* out) {
+  for (int i = 0; i < n; ++i) {
+    float s, c;
+    switch (fn) {
+      case 0: out[i] = as_atan2f(a[i], b[i]); break;
+      case 1: out[i] = as_asinf(a[i]); break;
+      case 2: out[i] = as_expf(a[i]); break;
+      case 3: as_sincosf(a[i], &s, &c); out[i] = s; break;
+      case 4: as_sincosf(a[i], &s, &c); out[i] = c; break;
+      default: out[i] = as_rem2pi(a[i]); break;
+    }
+  }
 }

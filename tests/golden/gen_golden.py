@@ -17,6 +17,8 @@ Fixtures (all float32 / int64 / bool numpy arrays, ``np.load(allow_pickle=False)
                      scale/unscale_transform on random and edge-case inputs
   task_seq.npz    -- a 40-step post-physics sequence of DirectRLEnv.step (dones -> rewards ->
                      reset -> obs) on 24 envs, every input and output per step
+  gates.npz       -- one such step on 32 envs whose roll / pitch straddle the reward gates
+                     (allsteps_env.py:356-359) by 10 ulp .. 0.01 rad (task_seq's keys, T = 1)
   mirror.npz      -- get_symmetric_states_rl_games / _rsl_rl
   rlg_wrapper.npz -- RlGamesVecEnvWrapper.step I/O on a fake env
 """
@@ -457,6 +459,106 @@ def gen_task_seq(mod, math_mod, out: dict):
           f"{int((torch.stack(S['idx'])[1:] != torch.stack(S['idx'])[:-1]).sum())}")
 
 
+def _quat_from_rp(roll, pitch):
+    """float32 unit quaternions (w, x, y, z) for intrinsic roll about x then pitch about y (yaw 0),
+    formed in float64"""
+    r = torch.as_tensor(roll, dtype=torch.float64) / 2
+    p = torch.as_tensor(pitch, dtype=torch.float64) / 2
+    cr, sr, cp, sp = torch.cos(r), torch.sin(r), torch.cos(p), torch.sin(p)
+    return torch.stack([cr * cp, sr * cp, cr * sp, -sr * sp], -1).to(torch.float32)
+
+
+def gen_gates(mod, math_mod, out: dict):
+    """One post-physics step (dones -> rewards -> obs, no resets) on states whose roll / pitch straddle
+    the reward's gates (allsteps_env.py:356-359: roll > 0.4, pitch > 0.4, and the "% 2pi" fold of a
+    small negative angle to ~2pi) by 10 ulp to 0.01 rad; the rest of the state calm.
+    Same keys as task_seq (T = 1)."""
+    offs = [-1e-2, -1e-4, -2e-6, -3e-7, 3e-7, 2e-6, 1e-4, 1e-2]
+    rolls, pitches = [], []
+    for d in offs:                          # roll about the 0.4 gate
+        rolls.append(0.4 + d); pitches.append(0.0)
+    for d in offs:                          # pitch about the 0.4 gate
+        rolls.append(0.0); pitches.append(0.4 + d)
+    for d in offs:                          # both near zero: negative values fold to ~2pi
+        rolls.append(d * 0.1); pitches.append(-d * 0.1)
+    for d in offs:                          # both about 0.4 at once
+        rolls.append(0.4 + d); pitches.append(0.4 - d)
+    n = len(rolls)
+    g = torch.Generator().manual_seed(1234)
+    env = build_env(mod, n, g)
+    rec0 = RandRecorder(torch.Generator().manual_seed(0))
+    saved = mod.torch
+    mod.torch = rec0
+    try:
+        pos, _, _ = env._generate_foot_steps_allsteps()
+    finally:
+        mod.torch = saved
+    env.steps_pos[:] = pos
+    env.curr_target_index[:] = torch.randint(1, 15, (n,), generator=g)
+    env.prev_target_index[:] = torch.clamp(env.curr_target_index - 1, 0, 19)
+    env.next_target_index[:] = torch.clamp(env.curr_target_index + 1, 0, 19)
+    env.swing_leg[:] = torch.randint(0, 2, (n,), generator=g)
+    env.episode_length_buf[:] = torch.randint(0, 40, (n,), generator=g)
+    env.potentials[:] = -(torch.rand(n, generator=g) * 50)
+    env.old_potentials[:] = env.potentials - 0.5
+    init = {
+        "idx": env.curr_target_index.clone(), "prev": env.prev_target_index.clone(),
+        "next": env.next_target_index.clone(), "count": env.target_reach_count.clone(),
+        "swing": env.swing_leg.clone(), "ep_len": env.episode_length_buf.clone(),
+        "pot": env.potentials.clone(), "old_pot": env.old_potentials.clone(),
+        "curriculum": env.curriculum.clone(),
+    }
+    rec = RandRecorder(g)
+    saved_env_torch, saved_math_torch = mod.torch, math_mod.torch
+    mod.torch = rec
+    math_mod.torch = rec
+    bi = BODY_NAMES.index
+    try:
+        synth_physics(env, g, 0, calm=True)
+        d = env.robot.data
+        d.root_state_w[:, 3:7] = _quat_from_rp(rolls, pitches)
+        d.root_state_w[:, 7:10] *= 0.3                      # no speed termination
+        d.root_state_w[:, 2] = 1.3
+        d.body_pos_w[:, bi("torso")] = d.root_state_w[:, :3]
+        act = (torch.rand(n, 21, generator=g) * 2 - 1) * 1.3
+        S = {"actions": act.clone(), "root_state": d.root_state_w.clone(), "joint_pos": d.joint_pos.clone(),
+             "joint_vel": d.joint_vel.clone(), "torso": d.body_pos_w[:, bi("torso")].clone(),
+             "rfoot": d.body_pos_w[:, bi("right_foot")].clone(), "lfoot": d.body_pos_w[:, bi("left_foot")].clone(),
+             "fm_r": env.sensor_right.data.force_matrix_w[:, 0].clone(),
+             "fm_l": env.sensor_left.data.force_matrix_w[:, 0].clone()}
+        env._pre_physics_step(act)
+        env.episode_length_buf += 1
+        env.reset_terminated[:], env.reset_time_outs[:] = env._get_dones()
+        reset_buf = env.reset_terminated | env.reset_time_outs
+        assert not bool(reset_buf.any()), "the gate states must not terminate"
+        rew = env._get_rewards()
+        obs = env._get_observations()["policy"]
+        S.update({"terminated": env.reset_terminated.clone(), "truncated": env.reset_time_outs.clone(),
+                  "reward": rew.clone(), "obs": obs.clone(), "any_reset": torch.tensor(False),
+                  "reset_draws": torch.zeros(n, 22), "post_root_state": d.root_state_w.clone(),
+                  "post_joint_pos": d.joint_pos.clone(), "post_joint_vel": d.joint_vel.clone(),
+                  "post_torso": d.body_pos_w[:, bi("torso")].clone(),
+                  "post_rfoot": d.body_pos_w[:, bi("right_foot")].clone(),
+                  "post_lfoot": d.body_pos_w[:, bi("left_foot")].clone(),
+                  "idx": env.curr_target_index.clone(), "prev": env.prev_target_index.clone(),
+                  "next": env.next_target_index.clone(), "count": env.target_reach_count.clone(),
+                  "swing": env.swing_leg.clone(), "pot": env.potentials.clone(), "old_pot": env.old_potentials.clone(),
+                  "ep_len": env.episode_length_buf.clone(), "curriculum": env.curriculum.clone(),
+                  "foot_contact": env.foot_contact.clone()})
+        r, p, _ = math_mod.euler_xyz_from_quat(d.root_state_w[:, 3:7])
+    finally:
+        mod.torch, math_mod.torch = saved_env_torch, saved_math_torch
+    for k, v in S.items():
+        out["seq_" + k] = v[None].numpy()
+    for k, v in init.items():
+        out["init_" + k] = v.numpy()
+    out["steps_pos"] = env.steps_pos.numpy()
+    out["joint_limits"] = joint_limits()
+    out["gate_roll"], out["gate_pitch"] = r.numpy(), p.numpy()
+    print(f"gates: {n} envs, roll in [{float(r.min()):.7f}, {float(r.max()):.7f}], "
+          f"roll gate on {int((r > 0.4).sum())}, pitch gate on {int((p > 0.4).sum())}")
+
+
 def gen_mirror(mod, out: dict):
     g = torch.Generator().manual_seed(11)
     env = types.SimpleNamespace()
@@ -532,13 +634,15 @@ def gen_rlg_wrapper(out: dict):
 def main():
     torch.set_num_threads(1)
     mod, math_mod = refload.load_allsteps_env()
-    fs, mt, ts, mi, rg = {}, {}, {}, {}, {}
+    fs, mt, ts, gt, mi, rg = {}, {}, {}, {}, {}, {}
     gen_footsteps(mod, fs)
     gen_math(math_mod, mt)
     gen_task_seq(mod, math_mod, ts)
+    gen_gates(mod, math_mod, gt)
     gen_mirror(mod, mi)
     gen_rlg_wrapper(rg)
-    for name, d in (("footsteps", fs), ("math", mt), ("task_seq", ts), ("mirror", mi), ("rlg_wrapper", rg)):
+    for name, d in (("footsteps", fs), ("math", mt), ("task_seq", ts), ("gates", gt), ("mirror", mi),
+                    ("rlg_wrapper", rg)):
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **d)
         print(f"wrote {path} ({os.path.getsize(path)} B, {len(d)} arrays)")

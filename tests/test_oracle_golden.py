@@ -80,10 +80,14 @@ def _load_seq_state(orc, g):
     return st, n
 
 
-def test_task_sequence(orc, oracle_mod):
-    """40-step DirectRLEnv.step post-physics sequence: dones -> rewards -> resets -> obs."""
+@pytest.mark.parametrize("fixture", ["task_seq", "gates"])
+def test_task_sequence(orc, oracle_mod, fixture):
+    """task_seq: 40-step DirectRLEnv.step post-physics sequence: dones -> rewards -> resets -> obs.
+    gates: one step on states whose roll / pitch straddle the reward gates (allsteps_env.py:356-359)
+    by 10 ulp .. 0.01 rad: the oracle's gate decisions are the reference's (a flipped gate moves the
+    reward by ~0.4, far outside the tolerance)."""
     O = oracle_mod
-    g = golden("task_seq")
+    g = golden(fixture)
     st, n = _load_seq_state(orc, g)
     T = g["seq_obs"].shape[0]
     post = {}
@@ -144,7 +148,12 @@ def test_task_sequence(orc, oracle_mod):
         np.testing.assert_array_equal(np.signbit(st["root_quat"].T), np.signbit(prs[:, 3:7]), msg)
         np.testing.assert_allclose(st["q"].T, g["seq_post_joint_pos"][t], rtol=1e-6, atol=1e-6, err_msg=msg)
         np.testing.assert_array_equal(st["qd"].T, g["seq_post_joint_vel"][t], msg)
-    assert 0 < steps_with_reset < T
+    if fixture == "task_seq":
+        assert 0 < steps_with_reset < T
+    else:
+        assert np.array_equal(obs[:, 1] > 0.4, g["gate_roll"] > 0.4)
+        assert np.array_equal(obs[:, 2] > 0.4, g["gate_pitch"] > 0.4)
+        assert 0 < int((g["gate_roll"] > 0.4).sum()) < len(obs)
 
 
 def test_philox_uniform_range(orc):
