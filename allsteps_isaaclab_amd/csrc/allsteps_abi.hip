@@ -102,6 +102,28 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
                         state->ep_len, state->episode, state->contact_mask, state->curriculum};
   for (const void* p : ptrs)
     if (!p) return fail(AS_ERR_INVALID, "as_create: null state field");
+  // every model field the kernels index with: a malformed model is rejected here instead of becoming
+  // an out-of-bounds LDS / register access (geoms: 32 LDS slots, foot id packed in 4 bits into the
+  // per-foot sensor masks; self pairs: 8-bit geom indices, 6 words per lane)
+  if (model->num_priority_geoms < 0 || model->num_priority_geoms > model->num_geoms)
+    return fail(AS_ERR_INVALID, "as_create: num_priority_geoms outside [0, num_geoms]");
+  const int max_foot = state->contact_mask_hind ? 3 : 1;
+  for (int g = 0; g < model->num_geoms; ++g) {
+    if (model->geom_link[g] < 0 || model->geom_link[g] >= model->num_links)
+      return fail(AS_ERR_INVALID, "as_create: geom_link[" + std::to_string(g) + "] outside [0, num_links)");
+    if (model->geom_type[g] != 0 && model->geom_type[g] != 1)
+      return fail(AS_ERR_INVALID, "as_create: geom_type[" + std::to_string(g) + "] not 0 (sphere) / 1 (capsule)");
+    if (model->geom_foot[g] < -1 || model->geom_foot[g] > max_foot)
+      return fail(AS_ERR_INVALID, "as_create: geom_foot[" + std::to_string(g) + "] outside [-1, " +
+                                      std::to_string(max_foot) + "] (2, 3 need contact_mask_hind)");
+  }
+  if (model->num_self_pairs < 0 || model->num_self_pairs > AS_MAX_SELF_PAIRS)
+    return fail(AS_ERR_INVALID, "as_create: num_self_pairs outside [0, AS_MAX_SELF_PAIRS]");
+  for (int i = 0; i < model->num_self_pairs; ++i) {
+    const int w = model->self_pair[i], g1 = w & 0xff, g2 = w >> 8;
+    if (w < 0 || g1 >= g2 || g2 >= model->num_geoms)
+      return fail(AS_ERR_INVALID, "as_create: self_pair[" + std::to_string(i) + "] is not g1 | g2 << 8 with g1 < g2 < num_geoms");
+  }
 
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(AS_ERR_NO_DEVICE, "as_create: no HIP device");
@@ -334,6 +356,9 @@ int as_set_actuator(as_env_t* env, const as_actuator_t* act) {
   HIP_TRY(hipSetDevice(env->device));
   env->host.act = *act;
   // ordered on the null stream with respect to every earlier launch (hipMemcpy synchronises)
+  // setup call, not stream-ordered: every launch still queued on any stream (torch's pool streams are
+  // non-blocking, so a plain hipMemcpy would not wait for them) finishes before the block changes
+  HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(env->consts_dev, &env->host, sizeof(as::Consts), hipMemcpyHostToDevice));
   return AS_OK;
 }
@@ -347,6 +372,9 @@ int as_set_quad_task(as_env_t* env, const as_quad_task_t* q) {
     return fail(AS_ERR_INVALID, "as_set_quad_task: stop_frames / max_episode_length / step_dt / num_steps");
   HIP_TRY(hipSetDevice(env->device));
   env->host.quad = *q;
+  // setup call, not stream-ordered: every launch still queued on any stream (torch's pool streams are
+  // non-blocking, so a plain hipMemcpy would not wait for them) finishes before the block changes
+  HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(env->consts_dev, &env->host, sizeof(as::Consts), hipMemcpyHostToDevice));
   env->quad_ready = 1;
   return AS_OK;

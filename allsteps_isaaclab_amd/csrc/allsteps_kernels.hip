@@ -2220,7 +2220,8 @@ __global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
     q[k] = st.q[k * n + e];
     qd[k] = st.qd[k * n + e];
   }
-  if (P.reset_all || term || trunc) {
+  const bool was_reset = P.reset_all || term || trunc;
+  if (was_reset) {
     // the stand pose over stones 0 (hind feet) and 1 (front feet), joints + U(-1, 1) * noise
     float blk[4];
     for (int k = 0; k < nh; ++k) {
@@ -2279,7 +2280,7 @@ __global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
   for (int k = 0; k < nh; ++k) {
     o[15 + k] = q[k] - K.act.default_q[k];
     o[15 + nh + k] = qd[k];
-    o[15 + 2 * nh + k] = a[k];
+    o[15 + 2 * nh + k] = was_reset ? 0.f : a[k];  // _reset_idx zeroes _actions (anymal_c_env.py:171-172)
   }
 }
 

@@ -228,7 +228,10 @@ int as_set_seed(as_env_t* env, uint64_t seed);
 /* Physics only (decimation substeps, no task logic): for known-answer tests and profiling. */
 int as_physics_step(as_env_t* env, const float* actions, void* stream);
 
-/* Select the actuation of the physics step (AS_ACT_TORQUE / AS_ACT_DC_MOTOR, see as_actuator_t). */
+/* Select the actuation of the physics step (AS_ACT_TORQUE / AS_ACT_DC_MOTOR, see as_actuator_t).
+ * as_set_actuator and as_set_quad_task are setup calls: they synchronize the device (every queued
+ * launch on every stream finishes first) and then rewrite the handle's constants block.  Not graph-
+ * safe: a captured graph keeps reading the block and sees the new values on its next replay. */
 int as_set_actuator(as_env_t* env, const as_actuator_t* act_host);
 /* BASELINE C5: the quadruped stepping-stone task (as_quad_task_t).  as_quad_step = physics substeps
  * (with the handle's actuator) + the task epilogue of every env, reset of done envs and the

@@ -69,7 +69,8 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
       q[k] = F(st->q, k, n, e);
       qd[k] = F(st->qd, k, n, e);
     }
-    if (reset_all || term || trunc) {
+    const int was_reset = reset_all || term || trunc;
+    if (was_reset) {
       float blk[4];
       for (int k = 0; k < nh; ++k) {
         if ((k & 3) == 0) or_philox_block(seed, (uint32_t)e, episode, (uint32_t)(k >> 2), QUAD_TAG, blk);
@@ -123,7 +124,7 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
     for (int k = 0; k < nh; ++k) {
       o[15 + k] = q[k] - act->default_q[k];
       o[15 + nh + k] = qd[k];
-      o[15 + 2 * nh + k] = a[k];
+      o[15 + 2 * nh + k] = was_reset ? 0.f : a[k]; /* _reset_idx zeroes _actions (anymal_c_env.py:171-172) */
     }
 #undef STONE
   }

@@ -139,3 +139,63 @@ def test_ppo_structs_match_header(cname, pyname):
         if decl:
             names += [p.strip().split()[-1] for p in decl.split(",")]
     assert [f[0] for f in getattr(fused, pyname)._fields_] == names
+
+
+def _valid_args():
+    """Model / sim / task / state structs of the walker, as the env builds them (no device needed:
+    as_create validates every field before it touches HIP)."""
+    import numpy as np
+
+    from allsteps_isaaclab_amd import _native
+    from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
+    from allsteps_isaaclab_amd.model import load_model
+
+    cfg = AllstepsEnvCfg()
+    m = load_model()
+    M, S, T = _native.make_model(m), _native.make_sim(cfg), _native.make_task(cfg, m["dof_names"])
+    st = _native.AsState()
+    buf = np.zeros(64, np.float32)
+    for name, _ in st._fields_:
+        setattr(st, name, buf.ctypes.data)
+    st.contact_mask_hind = None
+    return M, S, T, st, buf
+
+
+@pytest.mark.parametrize("field,mutate,msg", [
+    ("num_self_pairs", lambda M: setattr(M, "num_self_pairs", 257), b"num_self_pairs"),
+    ("num_self_pairs<0", lambda M: setattr(M, "num_self_pairs", -1), b"num_self_pairs"),
+    ("self_pair order", lambda M: M.self_pair.__setitem__(0, 5 | (3 << 8)), b"self_pair[0]"),
+    ("self_pair range", lambda M: M.self_pair.__setitem__(1, 2 | (200 << 8)), b"self_pair[1]"),
+    ("num_priority_geoms", lambda M: setattr(M, "num_priority_geoms", 33), b"num_priority_geoms"),
+    ("geom_foot", lambda M: M.geom_foot.__setitem__(3, 2), b"geom_foot[3]"),
+    ("geom_foot<-1", lambda M: M.geom_foot.__setitem__(4, -2), b"geom_foot[4]"),
+    ("geom_link", lambda M: M.geom_link.__setitem__(0, 22), b"geom_link[0]"),
+    ("geom_type", lambda M: M.geom_type.__setitem__(1, 2), b"geom_type[1]"),
+])
+def test_create_rejects_malformed_model(field, mutate, msg):
+    """as_create rejects every model field the kernels index with: AS_ERR_INVALID and a
+    message naming the field, before any device call."""
+    from allsteps_isaaclab_amd import _native
+
+    L = _native.load()
+    M, S, T, st, _buf = _valid_args()
+    mutate(M)
+    h = C.c_void_p()
+    rc = L.as_create(4, C.byref(M), C.byref(S), C.byref(T), C.byref(st), 0, 0, 0, C.byref(h))
+    assert rc == -1, (field, rc)
+    assert msg in L.as_last_error(), L.as_last_error()
+
+
+def test_create_accepts_the_walker_model_up_to_the_device():
+    """The unmodified walker passes validation: without a device the error is the device's."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from allsteps_isaaclab_amd import _native
+
+    L = _native.load()
+    M, S, T, st, _buf = _valid_args()
+    h = C.c_void_p()
+    rc = L.as_create(4, C.byref(M), C.byref(S), C.byref(T), C.byref(st), 0, 0, 0, C.byref(h))
+    assert rc == -3, L.as_last_error()

@@ -94,3 +94,64 @@ def test_reference_play_py_runs_unchanged_to_the_env(tmp_path):
     assert r.returncode != 0
     assert "NativeError: AllstepsEnv runs on the HIP backend only" in r.stderr, r.stderr[-3000:]
     assert "Loading model checkpoint from" in r.stdout or "Loading experiment" in r.stdout
+
+
+# The shimmed call sequence of the reference train.py (train.py:76-178), run on the device.  The
+# reference script itself never travels to the GPU box, so this driver (written here, not copied) makes
+# the same calls in the same order through the same import names: hydra_task_config over the registry
+# cfgs, gym.make, RlGamesVecEnvWrapper, the vecenv / env_configurations registrations, Runner with
+# IsaacAlgoObserver, the a2c_continuous_mirroring builder, load / reset / run.
+_DRIVER = '''
+import math, os, sys
+import gymnasium as gym
+from rl_games.common import env_configurations, vecenv
+from rl_games.common.algo_observer import IsaacAlgoObserver
+from rl_games.torch_runner import Runner
+from isaaclab_rl.rl_games import RlGamesGpuEnv, RlGamesVecEnvWrapper
+import isaaclab_tasks  # noqa: F401
+from isaaclab_tasks.utils.hydra import hydra_task_config
+from isaaclab_tasks.direct.allsteps.learning import a2c_ppo_mirroring
+
+@hydra_task_config("Allsteps-v0", "rl_games_cfg_entry_point")
+def main(env_cfg, agent_cfg):
+    env_cfg.scene.num_envs = 64
+    env_cfg.sim.device = "cuda:0"
+    agent_cfg["params"]["config"]["max_epochs"] = 1
+    env_cfg.seed = agent_cfg["params"]["seed"]
+    root = os.path.abspath(os.path.join("logs", "rl_games", agent_cfg["params"]["config"]["name"]))
+    agent_cfg["params"]["config"]["train_dir"] = root
+    agent_cfg["params"]["config"]["full_experiment_name"] = "gpu_flow"
+    rl_device = agent_cfg["params"]["config"]["device"]
+    clip_obs = agent_cfg["params"]["env"].get("clip_observations", math.inf)
+    clip_actions = agent_cfg["params"]["env"].get("clip_actions", math.inf)
+    env = gym.make("Allsteps-v0", cfg=env_cfg, render_mode=None)
+    env = RlGamesVecEnvWrapper(env, rl_device, clip_obs, clip_actions)
+    vecenv.register("IsaacRlgWrapper", lambda config_name, num_actors, **kw: RlGamesGpuEnv(config_name, num_actors, **kw))
+    env_configurations.register("rlgpu", {"vecenv_type": "IsaacRlgWrapper", "env_creator": lambda **kw: env})
+    agent_cfg["params"]["config"]["num_actors"] = env.unwrapped.num_envs
+    runner = Runner(IsaacAlgoObserver())
+    runner.algo_factory.register_builder("a2c_continuous_mirroring", lambda **kw: a2c_ppo_mirroring.A2CAgentSymmetry(**kw))
+    runner.load(agent_cfg)
+    runner.reset()
+    runner.run({"train": True, "play": False, "sigma": None})
+    env.close()
+    print("FLOW_OK")
+
+main()
+'''
+
+
+@pytest.mark.gpu
+def test_shimmed_train_flow_on_gpu(tmp_path):
+    """ADVICE r02: the compat path end to end on the device -- the rl_games.torch_runner shim,
+    IsaacAlgoObserver, isaaclab_rl's RlGamesVecEnvWrapper / RlGamesGpuEnv and the mirror-agent builder
+    -- one PPO epoch at 64 envs (agent minibatch 64 x 32 steps), and a checkpoint written."""
+    script = tmp_path / "flow.py"
+    script.write_text(_DRIVER)
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "allsteps_isaaclab_amd.compat", str(script), "--headless",
+                        "agent.params.config.minibatch_size=2048"], cwd=str(tmp_path), env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "FLOW_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+    ckpts = list((tmp_path / "logs" / "rl_games" / "allsteps" / "gpu_flow" / "nn").glob("*.pth"))
+    assert ckpts, "no checkpoint written"

@@ -131,6 +131,9 @@ def test_task_tick_potential_and_dones(qorc, oracle_mod, qmodel):
     assert term.tolist() == [False, False, True, True, False, False]
     assert trunc.tolist() == [False, False, False, False, True, False]
     assert rew[2] == QUAD_TASK["death"] and rew[3] == QUAD_TASK["death"]
+    # reset envs observe zero actions (anymal_c_env.py:171-172 zeroes _actions in _reset_idx); live ones theirs
+    assert (obs[[2, 3, 4], 15 + 24:] == 0).all()
+    assert (obs[5, 15 + 24:] == 0.5).all()
     # done envs were reset: stand pose, target 2, episode counter advanced
     for e in (2, 3, 4):
         assert st["idx"][e] == 2 and st["ep_len"][e] == 0 and st["episode"][e] == 2
