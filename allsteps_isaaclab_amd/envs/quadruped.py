@@ -13,14 +13,8 @@ the same SoA state and stone courses as the walker, four feet in contact with tw
 is a joint-space PD on top of it (the ANYmal default stance), used by the physics tests to keep the
 robots standing on the stones.
 
-``AnymalCStonesEnv`` is the C5 task (include/allsteps.h ``as_quad_task_t``): actions are
-joint position targets ``default_q + 0.5 a`` (``anymal_c_env.py:73-74``) tracked in every physics
-substep by IsaacLab's DC motor model with the ANYdrive 3 "simple" gains (``anymal.py``
-``ANYDRIVE_3_SIMPLE_ACTUATOR_CFG``: kp 40, kd 5, saturation 120 N m, effort limit 80 N m, velocity
-limit 7.5 rad/s; ``actuator_pd.py:184-199, 264-275``), all four feet carry contact sensors, and the
-task epilogue (target stones, potentials, rewards, dones, in-kernel resets, the 51-float
-observation) runs in ``k_quad`` after the physics.  There is no CPU fallback: the HIP library is
-required.
+The C5 task env (the DC motor actuator, the stepping-stone task epilogue, ANYmal-C's simulation
+settings, the direct-workflow surface) is ``envs/anymal_c_stones_env.py`` (``Allsteps-AnymalC-v0``).
 """
 
 from __future__ import annotations
@@ -31,6 +25,8 @@ import torch
 from .. import _native
 from ..model import ANYMAL_C_JSON, load_model
 from .allsteps_env_cfg import AllstepsEnvCfg
+from .anymal_c_stones_env import level0_stones  # noqa: F401  (re-exported for the physics tests)
+from .anymal_c_stones_env import stand_pose as _stand_pose
 
 # ANYmal default stance (IsaacLab ANYMAL_C_CFG init_state: HAA 0, front HFE 0.4 / KFE -0.8, hind HFE
 # -0.4 / KFE 0.8), in the model's cfg DOF order
@@ -42,20 +38,7 @@ ACT_SCALE = 80.0  # N m per unit action (1.2 * gear)
 
 
 def stand_pose(dof_names: list[str]) -> np.ndarray:
-    q = np.zeros(len(dof_names), np.float32)
-    for k, name in enumerate(dof_names):
-        leg, joint = name.split("_")
-        q[k] = STAND_Q["HAA"] if joint == "HAA" else STAND_Q[f"{leg[1]}_{joint}"]
-    return q
-
-
-def level0_stones(n: int, num_steps: int = 20) -> np.ndarray:
-    """steps_pos of curriculum level 0 ([3 * num_steps][n]): x = 0.75 k, y = 0, z = 0.75 k cos(pi/2)."""
-    st = np.zeros((3 * num_steps, n), np.float32)
-    for k in range(num_steps):
-        st[3 * k] = 0.75 * k
-        st[3 * k + 2] = np.float32(k * 0.75) * np.cos(np.float32(np.pi / 2), dtype=np.float32)
-    return st
+    return _stand_pose(dof_names, STAND_Q)
 
 
 class QuadrupedStonesEnv:
@@ -121,49 +104,3 @@ class QuadrupedStonesEnv:
         if getattr(self, "_native", None) is not None:
             self._native.close()
             self._native = None
-
-
-# ANYdrive 3 with the DC motor model (isaaclab_assets/robots/anymal.py ANYDRIVE_3_SIMPLE_ACTUATOR_CFG) and
-# the ANYmal-C flat task's action scale (anymal_c_env_cfg.py: action_scale = 0.5)
-ANYDRIVE_3_SIMPLE = {"stiffness": 40.0, "damping": 5.0, "saturation_effort": 120.0, "effort_limit": 80.0,
-                     "velocity_limit": 7.5}
-ACTION_SCALE = 0.5
-# the C5 task constants (include/allsteps.h as_quad_task_t; authored)
-QUAD_TASK = {"stop_frames": 2, "alive": 0.5, "action_cost": 0.005, "death": -2.0, "min_height": 0.25,
-             "up_z_min": 0.5, "max_episode_length": 1000, "step_dt": 4.0 / 240.0, "stand_height": 0.584,
-             "joint_noise": 0.05}
-
-
-class AnymalCStonesEnv(QuadrupedStonesEnv):
-    """BASELINE C5 task env: ``reset() -> obs``, ``step(actions) -> (obs, reward, terminated, truncated,
-    extras)`` with everything on the device (as_quad_reset_all / as_quad_step)."""
-
-    def __init__(self, num_envs: int, device: str = "cuda:0", seed: int = 42, cfg: AllstepsEnvCfg | None = None,
-                 task: dict | None = None):
-        self.task_cfg = dict(QUAD_TASK, **(task or {}))
-        super().__init__(num_envs, device, seed, cfg)
-        n, dev = self.num_envs, self.device
-        self._native.set_actuator(_native.ACT_DC_MOTOR, action_scale=ACTION_SCALE,
-                                  default_q=self.q_stand.cpu().tolist(), **ANYDRIVE_3_SIMPLE)
-        self._native.set_quad_task(**self.task_cfg)
-        self.obs_buf = torch.zeros((n, _native.QUAD_OBS_DIM), dtype=torch.float32, device=dev)
-        self.reward_buf = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.terminated_buf = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self.truncated_buf = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self.task_reset()
-
-    def task_reset(self) -> torch.Tensor:
-        self._native.quad_reset_all(self.obs_buf, stream=torch.cuda.current_stream(self.device).cuda_stream)
-        return self.obs_buf
-
-    def step(self, actions: torch.Tensor):
-        if actions.shape != (self.num_envs, self.num_dof) or actions.dtype != torch.float32:
-            raise ValueError(f"actions must be float32 ({self.num_envs}, {self.num_dof}), got "
-                             f"{tuple(actions.shape)} {actions.dtype}")
-        self._native.quad_step(actions.contiguous(), self.obs_buf, self.reward_buf, self.terminated_buf,
-                               self.truncated_buf, stream=torch.cuda.current_stream(self.device).cuda_stream)
-        return self.obs_buf, self.reward_buf, self.terminated_buf.bool(), self.truncated_buf.bool(), {}
-
-    @property
-    def target_index(self) -> torch.Tensor:
-        return self.state["idx"]

@@ -86,3 +86,16 @@ register(
         "rl_games_cfg_entry_point": "allsteps_isaaclab_amd.agents:rl_games_ppo_cfg.yaml",
     },
 )
+
+# BASELINE C5: the ANYmal-C quadruped on the stones, on ANYmal-C's simulation settings (authored task id:
+# the reference registers its ANYmal-C tasks as Isaac-Velocity-*-Anymal-C-Direct-v0, flat-ground velocity
+# tracking, anymal_c/__init__.py:17-41)
+register(
+    id="Allsteps-AnymalC-v0",
+    entry_point="allsteps_isaaclab_amd.envs.anymal_c_stones_env:AnymalCStonesEnv",
+    disable_env_checker=True,
+    kwargs={
+        "env_cfg_entry_point": "allsteps_isaaclab_amd.envs.anymal_c_stones_env_cfg:AnymalCStonesEnvCfg",
+        "rl_games_cfg_entry_point": "allsteps_isaaclab_amd.agents:rl_games_anymal_c_stones_ppo_cfg.yaml",
+    },
+)

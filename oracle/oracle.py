@@ -192,15 +192,23 @@ def torch_linspace_f32(start: float, end: float, steps: int) -> np.ndarray:
 def make_task(cfg, dof_names: list) -> OrTask:
     from allsteps_isaaclab_amd.envs.allsteps_env_cfg import running_start_pose
 
+    # a cfg without the walker's task table (the C5 quadruped: AnymalCStonesEnvCfg) takes the walker's
+    # defaults for it -- as_task_t is then only the stones / timing block, the quad task is as_quad_task_t
+    base = cfg
+    if not hasattr(cfg, "alive_reward_scale"):
+        from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
+
+        cfg = AllstepsEnvCfg()
+
     T = OrTask()
-    T.num_steps = cfg.num_steps
+    T.num_steps = base.num_steps
     T.step_radius = cfg.step_radius
     T.stop_frames = cfg.stop_frames
     T.eps = cfg.epsilon
     T.alive, T.energy, T.action = cfg.alive_reward_scale, cfg.energy_cost_scale, cfg.actions_cost_scale
     T.joint_limit, T.death = cfg.joint_at_limit_cost_scale, cfg.death_cost
     T.dof_vel_scale, T.fall_abs = cfg.dof_vel_scale, cfg.termination_height_absolute
-    T.step_dt = float(np.float32(cfg.sim.dt * cfg.decimation))
+    T.step_dt = float(np.float32(base.sim.dt * base.decimation))
     T.max_episode_length = cfg.max_episode_length
     T.max_curriculum = cfg.max_curriculum
     T.curriculum_threshold = cfg.curriculum_progress_threshold

@@ -2,7 +2,8 @@
 
     python scripts/bench_quadruped.py [--num_envs 16384] [--steps 500] [--warmup 20]
 
-A step = ``AnymalCStonesEnv.step`` = as_quad_step: 4 substeps of k_step<18> for every env with the DC
+A step = ``AnymalCStonesEnv.step`` (``Allsteps-AnymalC-v0``, ANYmal-C's sim settings: dt 1/200, friction
+1.0, max depenetration velocity 1.0) = as_quad_step: 4 substeps of k_step<18> for every env with the DC
 motor actuator evaluated in each substep (position targets default + 0.5 a), then k_quad (target
 stones, potentials, rewards, dones, in-kernel resets, the 51-float observation).  Actions: U(-1, 1),
 fresh every step (pre-drawn on the device).  Episodes end and reset inside the timed region.  Prints
@@ -24,9 +25,13 @@ import torch  # noqa: E402
 
 
 def measure(num_envs: int = 16384, steps: int = 500, warmup: int = 20, device: str = "cuda:0") -> dict:
-    from allsteps_isaaclab_amd.envs.quadruped import AnymalCStonesEnv
+    from allsteps_isaaclab_amd import registry
 
-    env = AnymalCStonesEnv(num_envs, device)
+    cfg = registry.load_cfg_from_registry("Allsteps-AnymalC-v0", "env_cfg_entry_point")
+    cfg.scene.num_envs = num_envs
+    cfg.sim.device = device
+    env = registry.make("Allsteps-AnymalC-v0", cfg=cfg)
+    env.reset()
     gen = torch.Generator(device=device).manual_seed(7)
     acts = torch.rand(steps + warmup, num_envs, 12, device=device, generator=gen) * 2 - 1
     for t in range(warmup):
@@ -42,6 +47,11 @@ def measure(num_envs: int = 16384, steps: int = 500, warmup: int = 20, device: s
     env.close()
     return {"metric": "env-steps/sec, quadruped (ANYmal-C approximation) stepping-stone task (DC motor, 4 foot "
                       "sensors, resets in the loop)",
+            "task": "Allsteps-AnymalC-v0",
+            "config": {"env_cfg": "AnymalCStonesEnvCfg", "dt": cfg.sim.dt, "decimation": cfg.decimation,
+                       "friction": cfg.sim.friction, "friction_combine": "multiply (1.0 x 1.0)",
+                       "max_depenetration_velocity": cfg.sim.max_depenetration_velocity,
+                       "soft_joint_pos_limit_factor": cfg.robot.soft_joint_pos_limit_factor},
             "value": round(num_envs * steps / el, 1), "unit": "env-steps/s", "n_gpus": 1, "num_envs": num_envs,
             "steps": steps, "ms_per_step": round(el / steps * 1e3, 4), "dof": 12, "kernels": "k_step<18> + k_quad",
             "resets_per_step": round(float(dones.item()) / steps, 1),

@@ -39,6 +39,27 @@ def test_train_script_runs_on_allsteps(tmp_path):
 
 
 @pytest.mark.gpu
+def test_train_script_runs_on_c5_quadruped(tmp_path):
+    """BASELINE C5 is trainable: train.py drives Allsteps-AnymalC-v0 (ANYmal-C's sim settings, DC motor,
+    four foot sensors) through RlGamesVecEnvWrapper and the PPO agent of its registry cfg (3 x 128 ELU,
+    horizon 24) -- the fused update on a non-walker trunk -- and writes a checkpoint."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts", "reinforcement_learning", "rl_games"))
+    import train
+
+    runner, _ = train.main(["--task", "Allsteps-AnymalC-v0", "--headless", "--num_envs", "1024", "--max_iterations",
+                            "2", "--seed", "3", "--log_root", str(tmp_path)])
+    agent = runner.agent
+    assert agent.epoch_num == 2 and agent.frame == 2 * 1024 * 24
+    assert agent.obs_shape[0] == 51 and agent.actions_num == 12
+    for k in ("a_loss", "c_loss", "kl", "entropy", "lr"):
+        assert math.isfinite(agent.last_stats[k]), (k, agent.last_stats)
+    assert torch.isfinite(agent.flat.params).all()
+    assert agent.tensor_dict["obses"].abs().sum() > 0
+    nn_dir = os.path.join(agent.experiment_dir, "nn")
+    assert any(f.endswith(".pth") for f in os.listdir(nn_dir))
+
+
+@pytest.mark.gpu
 def test_symmetry_agent_doubles_batch(tmp_path):
     from allsteps_isaaclab_amd import registry
     from allsteps_isaaclab_amd.learning.a2c_ppo_mirroring import A2CAgentSymmetry

@@ -14,7 +14,12 @@ import numpy as np
 import pytest
 import torch
 
-from allsteps_isaaclab_amd.envs.quadruped import ACTION_SCALE, ANYDRIVE_3_SIMPLE, QUAD_TASK, level0_stones, stand_pose
+from allsteps_isaaclab_amd.envs.anymal_c_stones_env import level0_stones
+from allsteps_isaaclab_amd.envs.anymal_c_stones_env_cfg import AnymalCStonesEnvCfg
+from allsteps_isaaclab_amd.envs.quadruped import stand_pose
+
+CFG = AnymalCStonesEnvCfg()
+QUAD_TASK = CFG.quad_task()
 
 
 @pytest.fixture(scope="module")
@@ -26,15 +31,15 @@ def qmodel():
 
 @pytest.fixture(scope="module")
 def qorc(oracle_mod, qmodel):
-    return oracle_mod.Oracle(model=qmodel)
+    return oracle_mod.Oracle(cfg=CFG, model=qmodel)  # ANYmal-C's simulation settings (dt 1/200, mu 1.0, ...)
 
 
 def _act_struct(oracle_mod, qmodel):
     A = oracle_mod.OrActuator()
     A.mode = 1
-    A.action_scale = ACTION_SCALE
+    A.action_scale = CFG.action_scale
     A.default_q[:12] = [float(x) for x in stand_pose(qmodel["dof_names"])]
-    for k, v in ANYDRIVE_3_SIMPLE.items():
+    for k, v in CFG.actuator().items():
         setattr(A, k, v)
     return A
 
@@ -163,12 +168,46 @@ def test_task_stands_on_four_feet(qorc, oracle_mod, qmodel):
 # ------------------------------------------------------------------------------------------------ GPU
 
 
+def test_c5_cfg_is_anymal_c():
+    """C5 runs on ANYmal-C's settings (anymal_c_env_cfg.py AnymalCFlatEnvCfg, anymal.py ANYMAL_C_CFG), not
+    the walker's: dt 1/200, friction 1.0 ("multiply" of 1.0 and 1.0), max depenetration velocity 1.0,
+    soft joint limit factor 0.95, 20-s episodes of 1000 steps."""
+    import allsteps_isaaclab_amd.envs.anymal_c_stones_env_cfg as M
+    from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
+
+    c = AnymalCStonesEnvCfg()
+    assert not isinstance(c, AllstepsEnvCfg) and not hasattr(c, "alive_reward_scale")
+    assert c.sim.dt == 1.0 / 200.0 and c.decimation == 4 and c.sim.friction == 1.0
+    assert c.sim.max_depenetration_velocity == 1.0 and c.sim.solver_position_iteration_count == 4
+    assert c.robot.soft_joint_pos_limit_factor == 0.95 and c.max_episode_length == 1000
+    assert c.scene.num_envs == 16384 and c.action_space == 12 and c.observation_space == 51
+    assert np.float32(c.quad_task()["step_dt"]) == np.float32(4 / 200)
+    o = __import__("oracle").Oracle(cfg=c, model=__import__("allsteps_isaaclab_amd.model", fromlist=["x"]).load_model(
+        __import__("allsteps_isaaclab_amd.model", fromlist=["x"]).ANYMAL_C_JSON))
+    assert np.float32(o.sim.dt) == np.float32(1 / 200) and o.sim.friction == 1.0 and o.sim.max_depen_vel == 1.0
+    del M
+
+
+def test_c5_registered_behind_the_env_surface():
+    from allsteps_isaaclab_amd import registry
+
+    s = registry.spec("Allsteps-AnymalC-v0")
+    assert s.entry_point.endswith("anymal_c_stones_env:AnymalCStonesEnv")
+    cfg = registry.load_cfg_from_registry("Allsteps-AnymalC-v0", "env_cfg_entry_point")
+    assert isinstance(cfg, AnymalCStonesEnvCfg)
+    agent = registry.load_cfg_from_registry("Allsteps-AnymalC-v0", "rl_games_cfg_entry_point")
+    assert agent["params"]["network"]["mlp"]["units"] == [128, 128, 128]
+    assert agent["params"]["config"]["minibatch_size"] == 24576
+
+
 @pytest.mark.gpu
 def test_c5_task_gpu_bit_exact_vs_oracle(qorc, oracle_mod, qmodel):
-    from allsteps_isaaclab_amd.envs.quadruped import AnymalCStonesEnv
+    from allsteps_isaaclab_amd import registry
 
     n, steps = 16384, 20  # BASELINE C5
-    env = AnymalCStonesEnv(n, "cuda:0")
+    env = registry.make("Allsteps-AnymalC-v0")  # AnymalCStonesEnvCfg: ANYmal-C's dt / friction / depenetration
+    assert env.num_envs == n and env.physics_dt == 1.0 / 200.0
+    env.reset()
     gen = torch.Generator(device="cuda:0").manual_seed(7)
     for _ in range(60):  # a second of random actions on the GPU first: robots falling and resetting
         env.step((torch.rand(n, 12, device="cuda:0", generator=gen) * 2.4 - 1.2).contiguous())
@@ -182,6 +221,7 @@ def test_c5_task_gpu_bit_exact_vs_oracle(qorc, oracle_mod, qmodel):
     for t in range(steps):
         a = (torch.rand(n, 12, device="cuda:0", generator=gen) * 2.4 - 1.2).contiguous()
         obs_g, rew_g, term_g, trunc_g, _ = env.step(a)
+        obs_g = obs_g["policy"]
         torch.cuda.synchronize()
         obs_c, rew_c, term_c, trunc_c = qorc.quad_step(st, act, Q, a.cpu().numpy(), seed=42, nthreads=16)
         g = {k: v.cpu().numpy() for k, v in env.state.items()}
