@@ -65,6 +65,8 @@ def parse():
                    help="oracle OpenMP threads (default: OMP_NUM_THREADS, else nproc; BASELINE.md §3)")
     p.add_argument("--no-train", action="store_true", help="skip the env+PPO trainer measurement")
     p.add_argument("--train-envs", type=int, default=32768)
+    p.add_argument("--multi-gpu-mode", dest="multi_gpu_mode", choices=("allgather", "allreduce"), default="allgather",
+                   help="N > 1 train leg: RCCL all-gather of rollouts (north star, default) or gradient all-reduce")
     p.add_argument("--no-c5", action="store_true", help="skip the quadruped (BASELINE C5) task measurement")
     return p.parse_args()
 
@@ -111,19 +113,28 @@ def host_cpu() -> dict:
             "sockets": len(sockets) or None}
 
 
-def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int = 50) -> dict:
-    """The oracle (CPU port of the same step) on the host cores, bounded sample (~20 CPU-s), timed
-    after `warm_steps` steps past the from-reset transient (the falling start)."""
+def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int = 50,
+                 min_wall_s: float = 5.0, min_steps: int = 50, max_wall_s: float = 60.0) -> dict:
+    """The oracle (CPU port of the same step) on the host cores, timed after `warm_steps` steps past the
+    from-reset transient (the falling start): at least `min_wall_s` of wall clock and `min_steps` steps
+    (so C3's 32768 envs get >= 50 steps), at most `max_wall_s`.
+
+    Threads: OMP_NUM_THREADS when set, else nproc.  On the GPU box OMP_NUM_THREADS is
+    the job's CPU share per GPU (16) and is kept: nproc there counts every CPU of the host, which other
+    jobs share, so more threads would measure contention, not the port."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
 
     host = host_cpu()
+    env_threads = os.environ.get("OMP_NUM_THREADS")
     if threads is None:
-        threads = int(os.environ.get("OMP_NUM_THREADS") or host["nproc"])
+        threads = int(env_threads or host["nproc"])
+    why = ("OMP_NUM_THREADS (the job's CPU share; nproc counts the whole shared host)" if env_threads
+           else "nproc")
     O.build()
     orc = O.Oracle()
-    n = num_envs  # the sample is bounded by time (~20 CPU-s), not by size
+    n = num_envs
     st = orc.state(n)
     if level == 0:
         for k in range(20):
@@ -143,18 +154,19 @@ def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int
         orc.env_step(st, acts[steps % 4], nthreads=threads)
         steps += 1
         el = time.perf_counter() - t0
-        if el * threads > 20.0 or steps >= 200:
+        if (el >= min_wall_s and steps >= min_steps) or el >= max_wall_s:
             break
     return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "host": host,
+            "threads_from": why, "host": host,
             "sample": f"oracle/ C port, {n} envs x {steps} steps (level {level}, U(-1,1) actions, timed after "
                       f"{warm_steps} warm-up steps), OpenMP {threads} threads, {el:.2f} s wall"}
 
 
 def train_leg(args, world: int, rank: int, backend: str, device, timeout_s: float = 300.0) -> dict:
     """env + PPO (BASELINE C4) in a child process per rank (scripts/bench_train.py; at N ranks its own
-    process group on a fresh port, the trainer's --distributed path: one RCCL all-reduce of
-    [grads | kl] per minibatch).  A child that fails or stalls is killed after `timeout_s` and reported
+    process group on a fresh port, the trainer's --distributed path with --multi_gpu_mode allgather:
+    one RCCL all-gather of the rollout tensors per epoch, identical replicated updates -- the north
+    star's exchange; --multi-gpu-mode allreduce selects rl_games' gradient all-reduce instead).  A child that fails or stalls is killed after `timeout_s` and reported
     as an error: the env metric on the line never waits on the trainer's collectives."""
     import signal
     import socket
@@ -172,7 +184,9 @@ def train_leg(args, world: int, rank: int, backend: str, device, timeout_s: floa
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="False",
                ALLSTEPS_DIST_TIMEOUT_S=str(int(timeout_s)))
     cmd = [sys.executable, os.path.join(ROOT, "scripts", "bench_train.py"), "--num_envs", str(args.train_envs),
-           "--epochs", "2", "--warmup", "2", "--quiet"] + (["--distributed"] if world > 1 else [])
+           "--epochs", "2", "--warmup", "2", "--quiet"]
+    if world > 1:  # north star: the RCCL all-gather of rollout tensors at the PPO boundary
+        cmd += ["--distributed", "--multi_gpu_mode", args.multi_gpu_mode]
     p = subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                          start_new_session=True)
     try:

@@ -19,9 +19,13 @@ sys.path.insert(0, os.path.join(ROOT, "scripts", "reinforcement_learning", "rl_g
 
 
 def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int | None = None,
-            log_root: str = "/tmp/bench_train_logs", verbose: bool = True, distributed: bool = False) -> dict:
+            log_root: str = "/tmp/bench_train_logs", verbose: bool = True, distributed: bool = False,
+            multi_gpu_mode: str = "allgather") -> dict:
     """num_envs per rank; with distributed=True (under torch.distributed.run) every rank trains with
-    train.py --distributed and the result counts all ranks' env-steps over the slowest rank's time."""
+    train.py --distributed --multi_gpu_mode <mode> and the result counts all ranks' env-steps over the
+    slowest rank's time.  "allgather" (default) is the north star's exchange: one RCCL all-gather of the
+    rollout tensors at the PPO boundary, identical replicated updates; "allreduce" is rl_games' own
+    (per-rank minibatches, averaged gradients)."""
     import torch
     import torch.distributed as dist
 
@@ -49,7 +53,7 @@ def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int 
         if level is not None:
             argv += ["--stone_level", str(level)]
         if distributed:
-            argv += ["--distributed"]
+            argv += ["--distributed", "--multi_gpu_mode", multi_gpu_mode]
         if verbose:
             runner, _ = train.main(argv)
         else:  # keep stdout to the caller's single JSON line
@@ -90,10 +94,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--level", type=int, default=None, help="initial stone curriculum level (C3: 9)")
     ap.add_argument("--distributed", action="store_true", help="one rank per GPU under torch.distributed.run")
+    ap.add_argument("--multi_gpu_mode", choices=("allgather", "allreduce"), default="allgather",
+                    help="--distributed exchange: RCCL all-gather of rollouts (north star) or gradient all-reduce")
     ap.add_argument("--quiet", action="store_true", help="only the result line (rank 0)")
     args = ap.parse_args()
     out = measure(args.num_envs, args.epochs, args.warmup, args.level, verbose=not args.quiet,
-                  distributed=args.distributed)
+                  distributed=args.distributed, multi_gpu_mode=args.multi_gpu_mode)
     import torch.distributed as dist
 
     if not (dist.is_initialized() and dist.get_rank() != 0):

@@ -434,3 +434,4 @@ def test_bench_two_ranks_one_gpu():
     tr = line["train"]
     assert "error" not in tr, (tr, r.stderr[-2000:])
     assert tr["n_gpus"] == 2 and tr["global_envs"] == 2048 and tr["value"] > 0
+    assert tr["multi_gpu_mode"] == "allgather"  # north star: RCCL all-gather of rollouts at the PPO boundary
