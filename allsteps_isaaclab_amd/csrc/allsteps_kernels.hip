@@ -73,14 +73,19 @@ union alignas(16) PhaseScratch {
   DynScratch d;
   float obs[64];        // epilogue: observation row staging
   struct {
-    float g[32][8];     // collide: geom segment endpoints, radius, packed type/foot/link
+    // collide: geom segment endpoints, radius, packed type/foot/link; row stride 12 floats (16-B
+    // aligned): geoms g and g + 8 land on different banks of the pair passes' gathered reads
+    alignas(16) float g[32][12];
     alignas(16) float bs[32][4];  //  bounding sphere (segment midpoint, half length + radius)
     int pl[64];         //          pending (stone << 8 | geom) pairs (< 32 + G), then self pairs
     uint32_t need[NST]; //          per candidate stone: geoms past the bounding test
     alignas(16) float cc[NST][4];  //   per candidate stone: its center relative to the root
   } col;
   struct alignas(16) {
-    float q[kSweepB][32];       // sweep: the pivot rows of a round (without the pivot columns)
+    // sweep: the pivot rows of a round (without the pivot columns).  Row stride 36 floats: the four
+    // pivot lanes' 16-B stores then start 4 banks apart (a 32-float stride put all four on the same
+    // four banks of ds_write_b128's (a/4) mod 32 banking: a 4-way conflict on every store)
+    float q[kSweepB][36];
     float pb[kSweepB][kSweepB]; //        and the pivot block H_PP
   } sw;                 // aliases d.c / d.Ib, dead by then
   ConScratch k;
@@ -120,7 +125,10 @@ struct EnvS {
   float R[LMAX][9];
   float p[LMAX][3];
   float c0[3];          // root COM (relative), kept past the dynamics phase for integration
-  alignas(16) float S[NVMAX][8];  // motion subspace [w; v_O] per dof, rows padded to 32 B (b128 reads)
+  // motion subspace [w; v_O] per dof.  Rows of 12 floats (48 B, two 16-B stores / loads): 16 lanes at
+  // that stride cover 16 distinct 16-B slots of the 64 read banks and 8 of the 32 write banks, where a
+  // 32-B stride put dofs j and j + 4 (stores) or j + 8 (loads) on the same banks
+  alignas(16) float S[NVMAX][12];
   float b[32];          // tau - C
   PhaseScratch x;
   float rlam[MAXR];     // PGS impulses
@@ -527,11 +535,10 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
         float S[6] = {a[0], a[1], a[2], 0.f, 0.f, 0.f};
         cross3(o, a, S + 3);
         const float qd = s.u[6 + i - 1];
+        *reinterpret_cast<v4f*>(&s.S[6 + i - 1][0]) = v4f{S[0], S[1], S[2], S[3]};
+        *reinterpret_cast<v4f*>(&s.S[6 + i - 1][4]) = v4f{S[4], S[5], 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          s.S[6 + i - 1][k] = S[k];
-          d.Sq[i][k] = S[k] * qd;
-        }
+        for (int k = 0; k < 6; ++k) d.Sq[i][k] = S[k] * qd;
       }
     }
   }
@@ -557,8 +564,8 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
         S[k] = 1.f;
         cross3(c0, e, S + 3);
       }
-#pragma unroll
-      for (int a = 0; a < 6; ++a) s.S[lane][a] = S[a];
+      *reinterpret_cast<v4f*>(&s.S[lane][0]) = v4f{S[0], S[1], S[2], S[3]};
+      *reinterpret_cast<v4f*>(&s.S[lane][4]) = v4f{S[4], S[5], 0.f, 0.f};
     }
   }
   __syncthreads();
@@ -836,7 +843,7 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
   for (int p = 0; p < NP; p += B) {
     // one buffer: LDS operations of a wave complete in issue order, so the next round's writes
     // cannot overtake this round's reads
-    float(&Q)[kSweepB][32] = s.x.sw.q;
+    float(&Q)[kSweepB][36] = s.x.sw.q;
     float(&Pb)[kSweepB][kSweepB] = s.x.sw.pb;
     const int t = lane - p;
     const bool piv = (unsigned)t < (unsigned)B;

@@ -245,7 +245,7 @@ def test_anymal_stance_gpu_bit_exact(oracle_mod):
     orc, st, q0 = _quad_stand(oracle_mod)
     env = QuadrupedStonesEnv(1, "cuda:0")
     for k, v in env.state.items():
-        if k in st and k != "curriculum":
+        if k in st.a and k != "curriculum":
             a = np.ascontiguousarray(st[k]).reshape(v.shape)
             v.copy_(torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a))
     for t in range(STEPS_10S):
