@@ -53,13 +53,29 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {  // round to nearest 
     return uint16_t(u >> 16);
 }
 
+__device__ __forceinline__ float f16_to_f32(uint16_t h) { return float(__builtin_bit_cast(_Float16, h)); }
+
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {  // v_cvt_f16_f32: round to nearest even, inf past 65504
+    return __builtin_bit_cast(uint16_t, static_cast<_Float16>(f));
+}
+
+// element types of the low-precision buffers: PPO_DT_F32 (0), PPO_DT_BF16 (1), PPO_DT_F16 (2)
+template <int T>
+__device__ __forceinline__ float lp_to_f32(uint16_t h) { return T == PPO_DT_F16 ? f16_to_f32(h) : bf16_to_f32(h); }
+template <int T>
+__device__ __forceinline__ uint16_t f32_to_lp(float f) { return T == PPO_DT_F16 ? f32_to_f16(f) : f32_to_bf16(f); }
+
 __device__ __forceinline__ float load_as_f32(const void* p, int64_t i, int dtype) {
-    return dtype ? bf16_to_f32(static_cast<const uint16_t*>(p)[i]) : static_cast<const float*>(p)[i];
+    if (dtype == PPO_DT_BF16) return bf16_to_f32(static_cast<const uint16_t*>(p)[i]);
+    if (dtype == PPO_DT_F16) return f16_to_f32(static_cast<const uint16_t*>(p)[i]);
+    return static_cast<const float*>(p)[i];
 }
 
 __device__ __forceinline__ void store_from_f32(void* p, int64_t i, int dtype, float x) {
-    if (dtype)
+    if (dtype == PPO_DT_BF16)
         static_cast<uint16_t*>(p)[i] = f32_to_bf16(x);
+    else if (dtype == PPO_DT_F16)
+        static_cast<uint16_t*>(p)[i] = f32_to_f16(x);
     else
         static_cast<float*>(p)[i] = x;
 }
@@ -171,7 +187,7 @@ __global__ void __launch_bounds__(256) k_obs_stats_update(const double* __restri
 
 __global__ void k_obs_normalize(const float* __restrict__ x, const int32_t* __restrict__ mb_idx, int mb_rows, int cols,
                                 const double* __restrict__ mean, const double* __restrict__ var, float eps,
-                                void* __restrict__ out, int out_cols, int out_stride, int out_bf16) {
+                                void* __restrict__ out, int out_cols, int out_stride, int out_dtype) {
     const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= int64_t(mb_rows) * out_cols) return;
     const int r = int(e / out_cols), c = int(e % out_cols);
@@ -183,7 +199,7 @@ __global__ void k_obs_normalize(const float* __restrict__ x, const int32_t* __re
         y = (v - float(mean[c])) / sqrtf(float(var[c]) + eps);
         y = fminf(fmaxf(y, -5.f), 5.f);
     }
-    store_from_f32(out, i, out_bf16, y);
+    store_from_f32(out, i, out_dtype, y);
 }
 
 // ------------------------------------------------------------------------------ PPO losses
@@ -205,13 +221,15 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
     const float* __restrict__ head, const float* __restrict__ logstd, int mb_rows, const int32_t* __restrict__ mb_idx,
     const float* __restrict__ actions, float* __restrict__ ds_mu, float* __restrict__ ds_sigma,
     const float* __restrict__ old_nlp, const float* __restrict__ adv_, const float* __restrict__ old_v,
-    const float* __restrict__ ret_, ppo_loss_cfg_t cfg, float* __restrict__ dhead, float* __restrict__ partials) {
+    const float* __restrict__ ret_, ppo_loss_cfg_t cfg, const float* __restrict__ grad_scale, float* __restrict__ dhead,
+    float* __restrict__ partials) {
     static_assert(A + 1 <= 32, "one 32-lane group per row");
     constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
     constexpr int G = kLossThreads / 32;
     __shared__ float red[G][NV];
     const int j = threadIdx.x % 32, grp = threadIdx.x / 32;
-    const float inv_b = 1.f / float(mb_rows);
+    // the loss scale (a power of two, GradScaler) enters every gradient through the 1/B factor: exact
+    const float inv_b = (grad_scale ? *grad_scale : 1.f) * (1.f / float(mb_rows));
     const int64_t base = int64_t(*mb_idx) * mb_rows;
     const bool act_lane = j < A;
     const float ls = act_lane ? logstd[j] : 0.f;
@@ -329,7 +347,8 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
 }
 
 __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ partials, int nblk, int A, int mb_rows,
-                                                      float entropy_coef, float* __restrict__ g_hb,
+                                                      float entropy_coef, const float* __restrict__ grad_scale,
+                                                      float* __restrict__ g_hb,
                                                       float* __restrict__ g_ls, float* __restrict__ stats,
                                                       const int32_t* __restrict__ stat_idx, float* __restrict__ kl_out) {
     const int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
@@ -351,7 +370,8 @@ __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ 
     if (k <= A) {
         g_hb[k] = s;
     } else if (k <= 2 * A) {
-        g_ls[k - A - 1] = s - entropy_coef;  // - entropy_coef * mean(entropy): d/d logstd_j = -entropy_coef
+        // - entropy_coef * mean(entropy): d/d logstd_j = -entropy_coef (times the loss scale)
+        g_ls[k - A - 1] = s - entropy_coef * (grad_scale ? *grad_scale : 1.f);
     } else {
         const int st = k - 2 * A - 1;
         const float mean = s / float(mb_rows);
@@ -369,10 +389,10 @@ template <int T>
 __device__ __forceinline__ void load4(const void* p, int64_t i, float (&x)[4]) {
     if (T) {
         const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p) + i);
-        x[0] = bf16_to_f32(uint16_t(u.x & 0xffffu));
-        x[1] = bf16_to_f32(uint16_t(u.x >> 16));
-        x[2] = bf16_to_f32(uint16_t(u.y & 0xffffu));
-        x[3] = bf16_to_f32(uint16_t(u.y >> 16));
+        x[0] = lp_to_f32<T>(uint16_t(u.x & 0xffffu));
+        x[1] = lp_to_f32<T>(uint16_t(u.x >> 16));
+        x[2] = lp_to_f32<T>(uint16_t(u.y & 0xffffu));
+        x[3] = lp_to_f32<T>(uint16_t(u.y >> 16));
     } else {
         const float4 u = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
         x[0] = u.x;
@@ -382,7 +402,7 @@ __device__ __forceinline__ void load4(const void* p, int64_t i, float (&x)[4]) {
     }
 }
 
-// four adjacent columns per thread (8-B bf16 / 16-B fp32 loads), row phases across the block
+// four adjacent columns per thread (8-B bf16 / fp16, 16-B fp32 loads), row phases across the block
 template <int DH_T, int H_T, int DZ_T>
 __global__ void __launch_bounds__(kEluThreads) k_elu_bwd(const void* __restrict__ dh, const void* __restrict__ h,
                                                          void* __restrict__ dz, int rows, int cols,
@@ -407,8 +427,8 @@ __global__ void __launch_bounds__(kEluThreads) k_elu_bwd(const void* __restrict_
                 uint16_t b[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    b[k] = f32_to_bf16(z[k]);
-                    z[k] = bf16_to_f32(b[k]);  // bias grad from the stored (GEMM-visible) dz
+                    b[k] = f32_to_lp<DZ_T>(z[k]);
+                    z[k] = lp_to_f32<DZ_T>(b[k]);  // bias grad from the stored (GEMM-visible) dz
                 }
                 *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dz) + i) =
                     make_uint2(uint32_t(b[0]) | (uint32_t(b[1]) << 16), uint32_t(b[2]) | (uint32_t(b[3]) << 16));
@@ -612,7 +632,7 @@ __global__ void __launch_bounds__(256) k_sqnorm(const float* __restrict__ g, int
     __shared__ float red[256 / kWave];
     float s = 0.f;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
-        s += g[i] * g[i];
+        s += __builtin_isfinite(g[i]) ? g[i] * g[i] : __builtin_inff();  // a non-finite grad: inf (found_inf)
     s = wave_sum(s);
     if (threadIdx.x % kWave == 0) red[threadIdx.x / kWave] = s;
     __syncthreads();
@@ -633,9 +653,11 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
                                                        const float* __restrict__ np, int nnp, float max_norm,
                                                        const double* __restrict__ lr_p, const double* __restrict__ step_p,
                                                        float b1, float b2, float eps, SegTable segs,
-                                                       uint16_t* __restrict__ mirror) {
+                                                       uint16_t* __restrict__ mirror, int mirror_dtype,
+                                                       const float* __restrict__ scaler) {
     __shared__ float red[kAdamThreads / kWave];
-    __shared__ float coef_s, step_size_s, bc2_sqrt_s;
+    __shared__ float coef_s, step_size_s, bc2_sqrt_s, inv_scale_s;
+    __shared__ int skip_s;
     float s = 0.f;
     for (int k = threadIdx.x; k < nnp; k += kAdamThreads) s += np[k];
     s = wave_sum(s);
@@ -644,8 +666,13 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     if (threadIdx.x == 0) {
         float t = 0.f;
         for (int w = 0; w < kAdamThreads / kWave; ++w) t += red[w];
+        // GradScaler: grads carry the loss scale (a power of two); a non-finite one skips the step
+        // (scaler.step), otherwise they are unscaled exactly before the clip (scaler.unscale_)
+        const float inv_scale = scaler ? 1.f / scaler[0] : 1.f;
+        skip_s = scaler && !__builtin_isfinite(t);
+        inv_scale_s = inv_scale;
         // torch.nn.utils.clip_grad_norm_: coef = max_norm / (total_norm + 1e-6), clamped to 1
-        coef_s = max_norm > 0.f ? fminf(max_norm / (sqrtf(t) + 1e-6f), 1.f) : 1.f;
+        coef_s = max_norm > 0.f ? fminf(max_norm / (sqrtf(t) * inv_scale + 1e-6f), 1.f) : 1.f;
         // bias corrections once per block (fp64 pow / sqrt are long instruction sequences)
         const double ts = *step_p + 1.0;
         step_size_s = float(*lr_p / (1.0 - pow(double(b1), ts)));
@@ -656,8 +683,8 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     const float step_size = step_size_s;
     const float bc2_sqrt = bc2_sqrt_s;
     const int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x;
-    if (i >= n) return;
-    const float gi = g[i] * coef;
+    if (i >= n || skip_s) return;
+    const float gi = (g[i] * inv_scale_s) * coef;
     const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
     const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
     m[i] = mi;
@@ -671,15 +698,32 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
             if (i >= sg.off && i < sg.off + sg.len) {
                 const int64_t j = i - sg.off;
                 const int64_t r = j / sg.cols, c = j % sg.cols;
-                mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] = f32_to_bf16(pi);
+                mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] =
+                    mirror_dtype == PPO_DT_F16 ? f32_to_f16(pi) : f32_to_bf16(pi);
             }
         }
     }
 }
 
 __global__ void k_tail(double* lr, const float* kl, float thr, double min_lr, double max_lr, double* step,
-                       int32_t* mb_idx, int nmb, int32_t* stat_idx) {
+                       int32_t* mb_idx, int nmb, int32_t* stat_idx, float* scaler, const float* np, int nnp,
+                       int growth_interval) {
     if (threadIdx.x != 0) return;
+    bool skipped = false;
+    if (scaler) {  // GradScaler.update: backoff 0.5 on a skipped step, growth 2 after growth_interval good ones
+        float t = 0.f;
+        for (int k = 0; k < nnp; ++k) t += np[k];
+        skipped = !__builtin_isfinite(t);
+        if (skipped) {
+            scaler[0] *= 0.5f;
+            scaler[1] = 0.f;
+        } else if (scaler[1] + 1.f >= float(growth_interval)) {
+            scaler[0] *= 2.f;
+            scaler[1] = 0.f;
+        } else {
+            scaler[1] += 1.f;
+        }
+    }
     if (thr > 0.f) {
         const double k = double(*kl);
         double cur = *lr, nxt = cur;
@@ -687,7 +731,7 @@ __global__ void k_tail(double* lr, const float* kl, float thr, double min_lr, do
         if (k < 0.5 * double(thr)) nxt = fmin(cur * 1.5, max_lr);
         *lr = nxt;
     }
-    *step += 1.0;
+    if (!skipped) *step += 1.0;  // a skipped optimizer.step() leaves Adam's step count
     *mb_idx = (*mb_idx + 1) % nmb;
     *stat_idx += 1;
 }
@@ -722,11 +766,12 @@ int ppo_obs_stats_update(const double* partials, int32_t nblk, int32_t cols, int
 
 int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_t cols, const double* running_mean,
                       const double* running_var, float eps, void* out, int32_t out_cols, int32_t out_stride,
-                      int32_t out_bf16, void* stream) {
+                      int32_t out_dtype, void* stream) {
     if (out_cols < cols || out_stride < out_cols) return fail(-1, "ppo_obs_normalize: need cols <= out_cols <= out_stride");
+    if (out_dtype < PPO_DT_F32 || out_dtype > PPO_DT_F16) return fail(-1, "ppo_obs_normalize: bad out_dtype");
     const int64_t n = int64_t(mb_rows) * out_cols;
     hipLaunchKernelGGL(k_obs_normalize, dim3(unsigned((n + 255) / 256)), dim3(256), 0, S(stream), x, mb_idx, mb_rows,
-                       cols, running_mean, running_var, eps, out, out_cols, out_stride, out_bf16);
+                       cols, running_mean, running_var, eps, out, out_cols, out_stride, out_dtype);
     return launched("k_obs_normalize");
 }
 
@@ -738,12 +783,13 @@ int ppo_loss_blocks(int32_t mb_rows) {
 int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
                   const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
                   const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
-                  float* dhead, float* partials, void* stream) {
+                  const float* grad_scale, float* dhead, float* partials, void* stream) {
     const dim3 grid(ppo_loss_blocks(mb_rows)), block(kLossThreads);
 #define PPO_LOSS_CASE(AA)                                                                                        \
     case AA:                                                                                                     \
         hipLaunchKernelGGL(k_loss_grad<AA>, grid, block, 0, S(stream), head, logstd, mb_rows, mb_idx, actions, \
-                           ds_mu, ds_sigma, old_neglogp, advantages, old_values, returns, cfg, dhead, partials); \
+                           ds_mu, ds_sigma, old_neglogp, advantages, old_values, returns, cfg, grad_scale, dhead,  \
+                           partials);                                                                           \
         break;
     switch (A) {
         PPO_LOSS_CASE(2)
@@ -757,12 +803,11 @@ int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_
 }
 
 int ppo_loss_finalize(const float* partials, int32_t nblk, int32_t A, int32_t mb_rows, float entropy_coef,
-                      float* grad_head_bias, float* grad_logstd, float* stats, const int32_t* stat_idx, float* kl_out,
-                      void* stream) {
+                      const float* grad_scale, float* grad_head_bias, float* grad_logstd, float* stats,
+                      const int32_t* stat_idx, float* kl_out, void* stream) {
     if (A <= 0 || A > PPO_MAX_ACT) return fail(-1, "ppo_loss_finalize: bad action dim");
     hipLaunchKernelGGL(k_loss_finalize, dim3(2 * A + 1 + PPO_LOSS_NSTAT), dim3(kWave), 0, S(stream), partials, nblk, A,
-                       mb_rows, entropy_coef,
-                       grad_head_bias, grad_logstd, stats, stat_idx, kl_out);
+                       mb_rows, entropy_coef, grad_scale, grad_head_bias, grad_logstd, stats, stat_idx, kl_out);
     return launched("k_loss_finalize");
 }
 
@@ -772,14 +817,24 @@ int ppo_elu_bwd(const void* dh, int32_t dh_dtype, const void* h, int32_t h_dtype
                 int32_t rows, int32_t cols, float* partials, void* stream) {
     if (cols % 64 || cols > 4 * kEluThreads) return fail(-1, "ppo_elu_bwd: cols must be a multiple of 64, <= 4096");
     const dim3 grid(ppo_elu_bwd_blocks(rows)), block(kEluThreads);
-    const int code = dh_dtype * 4 + h_dtype * 2 + dz_dtype;
+    const int code = dh_dtype * 9 + h_dtype * 3 + dz_dtype;
+#define PPO_ELU_CASE(A, B, C)                                                                                          \
+    case A * 9 + B * 3 + C:                                                                                            \
+        hipLaunchKernelGGL((k_elu_bwd<A, B, C>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials);         \
+        break;
     switch (code) {
-        case 0: hipLaunchKernelGGL((k_elu_bwd<0, 0, 0>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
-        case 1: hipLaunchKernelGGL((k_elu_bwd<0, 0, 1>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
-        case 3: hipLaunchKernelGGL((k_elu_bwd<0, 1, 1>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
-        case 7: hipLaunchKernelGGL((k_elu_bwd<1, 1, 1>), grid, block, 0, S(stream), dh, h, dz, rows, cols, partials); break;
-        default: return fail(-1, "ppo_elu_bwd: dtype combination (dh, h, dz) must be (f32,f32,f32), (f32,f32,bf16), (f32,bf16,bf16) or (bf16,bf16,bf16)");
+        PPO_ELU_CASE(0, 0, 0)
+        PPO_ELU_CASE(0, 0, 1)
+        PPO_ELU_CASE(0, 1, 1)
+        PPO_ELU_CASE(1, 1, 1)
+        PPO_ELU_CASE(0, 0, 2)
+        PPO_ELU_CASE(0, 2, 2)
+        PPO_ELU_CASE(2, 2, 2)
+        default:
+            return fail(-1, "ppo_elu_bwd: dtype combination (dh, h, dz) must be (f32,f32,f32), (f32,f32,lp), "
+                            "(f32,lp,lp) or (lp,lp,lp) with lp bf16 or fp16");
     }
+#undef PPO_ELU_CASE
     return launched("k_elu_bwd");
 }
 
@@ -854,10 +909,13 @@ int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream) {
 
 int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials, int32_t nblk_norm,
              float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,
-             const ppo_seg_t* segs_host, int32_t nseg, void* mirror_bf16, void* stream) {
+             const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, const float* scaler,
+             void* stream) {
     if (nseg < 0 || nseg > PPO_MAX_SEG) return fail(-1, "ppo_adam: too many mirror segments");
+    if (mirror && mirror_dtype != PPO_DT_BF16 && mirror_dtype != PPO_DT_F16)
+        return fail(-1, "ppo_adam: mirror_dtype must be bf16 or fp16");
     SegTable t{};
-    t.n = mirror_bf16 ? nseg : 0;
+    t.n = mirror ? nseg : 0;
     for (int k = 0; k < t.n; ++k) {
         t.s[k] = segs_host[k];
         const int64_t rows = t.s[k].cols > 0 ? t.s[k].len / t.s[k].cols : 0;
@@ -866,15 +924,17 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
     }
     hipLaunchKernelGGL(k_adam, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0, S(stream),
                        p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
-                       static_cast<uint16_t*>(mirror_bf16));
+                       static_cast<uint16_t*>(mirror), mirror_dtype, scaler);
     return launched("k_adam");
 }
 
 int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,
-             int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, void* stream) {
+             int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, float* scaler, const float* sqnorm_partials,
+             int32_t nblk_norm, int32_t growth_interval, void* stream) {
     if (n_minibatches <= 0) return fail(-1, "ppo_tail: n_minibatches must be positive");
+    if (scaler && (!sqnorm_partials || growth_interval <= 0)) return fail(-1, "ppo_tail: the scaler needs the norm partials");
     hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, S(stream), lr, kl, kl_threshold, min_lr, max_lr, step, mb_idx,
-                       n_minibatches, stat_idx);
+                       n_minibatches, stat_idx, scaler, sqnorm_partials, nblk_norm, growth_interval);
     return launched("k_tail");
 }
 

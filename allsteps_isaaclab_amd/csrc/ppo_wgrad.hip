@@ -27,6 +27,7 @@ void set_error(const char* msg);
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -45,25 +46,57 @@ constexpr int kLdsBytes = 2 * kStage;    // 147456 B (one workgroup per CU)
 
 char g_err[256];
 
+// the 16-bit element type (PPO_DT_BF16 / PPO_DT_F16): fragment vector, MFMA, the all-ones operand
+template <int DT>
+struct Lp;
+template <>
+struct Lp<PPO_DT_BF16> {
+    typedef bf16x8 v8;
+    static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ v8 one() {
+        v8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (__bf16)1.0f;
+        return o;
+    }
+};
+template <>
+struct Lp<PPO_DT_F16> {
+    typedef f16x8 v8;
+    static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ v8 one() {
+        v8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (_Float16)1.0f;
+        return o;
+    }
+};
+
+template <int DT>
 union Frag {
-    bf16x8 v;
+    typename Lp<DT>::v8 v;
     s16x4 h[2];
 };
 
 // 32x32x16 operand from a row-major [k][col] LDS image: lane l gets column col0 + (l & 31) at rows
 // kb + 8 (l >> 5) + 0..7 (two 4-row transposed reads; the same k order for both operands)
-__device__ __forceinline__ bf16x8 tr_frag(const char* img, int pitch, int col0, int kb, int lane) {
+template <int DT>
+__device__ __forceinline__ typename Lp<DT>::v8 tr_frag(const char* img, int pitch, int col0, int kb, int lane) {
     const int g = (lane >> 4) & 3, i = lane & 15, q = i >> 2, p = i & 3;
     const int row = kb + 8 * (g >> 1) + q;
     const int col = col0 + 16 * (g & 1) + 4 * p;
     const char* a = img + row * pitch + col * 2;
-    Frag f;
+    Frag<DT> f;
     f.h[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
     f.h[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * pitch));
     return f.v;
 }
 
-// stage loads: rows [r0, r0 + kKT) of a [rows][stride] bf16 matrix, columns [0, cols); rows past
+// stage loads: rows [r0, r0 + kKT) of a [rows][stride] 16-bit matrix, columns [0, cols); rows past
 // `rend` are zero (the pad rows then add nothing to the MFMA sums)
 template <int COLS>
 struct Stager {
@@ -92,8 +125,9 @@ struct Stager {
 // KIN input features: 256 (trunk layers, 8 column tiles: wave = 2 o-blocks of 4 tiles x 4 c-blocks
 // of 2 tiles) or 64 (layer 0: 2 column tiles, wave = one o-tile x both c-tiles).  The bias sums of
 // o-tile obase + cblock ride along as one MFMA against an all-ones B operand.
-template <int KIN>
+template <int KIN, int DT>
 __device__ __forceinline__ void wgrad_layer(const ppo_wgrad_t& a, int l, char* lds) {
+    typedef typename Lp<DT>::v8 V8;
     constexpr int NCT = KIN / 32;
     constexpr int CBLK = NCT / 2;            // c-blocks of 2 tiles
     constexpr int OTW = CBLK;                // o-tiles per wave (8 waves cover 8 o-tiles x NCT)
@@ -111,9 +145,7 @@ __device__ __forceinline__ void wgrad_layer(const ppo_wgrad_t& a, int l, char* l
     f32x16 acc[OTW][2], accb = {};
 #pragma unroll
     for (int t = 0; t < OTW; ++t) acc[t][0] = acc[t][1] = f32x16{};
-    bf16x8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+    const V8 ones = Lp<DT>::one();
 
     Stager<kOut> sd;
     Stager<KIN> sh;
@@ -132,20 +164,19 @@ __device__ __forceinline__ void wgrad_layer(const ppo_wgrad_t& a, int l, char* l
         __syncthreads();
 #pragma unroll
         for (int ks = 0; ks < kKT / 16; ++ks) {
-            bf16x8 af[OTW], bfr[2];
+            V8 af[OTW], bfr[2];
 #pragma unroll
-            for (int t = 0; t < OTW; ++t) af[t] = tr_frag(img, kPitchDz, (obase + t) * 32, ks * 16, lane);
+            for (int t = 0; t < OTW; ++t) af[t] = tr_frag<DT>(img, kPitchDz, (obase + t) * 32, ks * 16, lane);
 #pragma unroll
-            for (int u = 0; u < 2; ++u) bfr[u] = tr_frag(img + kStageDz, PH, (2 * cb + u) * 32, ks * 16, lane);
+            for (int u = 0; u < 2; ++u) bfr[u] = tr_frag<DT>(img + kStageDz, PH, (2 * cb + u) * 32, ks * 16, lane);
 #pragma unroll
             for (int t = 0; t < OTW; ++t)
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
-                    acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bfr[u], acc[t][u], 0, 0, 0);
-            bf16x8 ab = af[0];  // af[cb] without a dynamically indexed register array
+                for (int u = 0; u < 2; ++u) acc[t][u] = Lp<DT>::mma(af[t], bfr[u], acc[t][u]);
+            V8 ab = af[0];  // af[cb] without a dynamically indexed register array
 #pragma unroll
             for (int t = 1; t < OTW; ++t) ab = cb == t ? af[t] : ab;
-            accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, ones, accb, 0, 0, 0);
+            accb = Lp<DT>::mma(ab, ones, accb);
         }
     }
     // D[o][c]: c = lane & 31 on the lane, o = 8 (r >> 2) + 4 (lane >> 5) + (r & 3) in register r
@@ -169,20 +200,22 @@ __device__ __forceinline__ void wgrad_layer(const ppo_wgrad_t& a, int l, char* l
     }
 }
 
+template <int DT>
 __global__ void __launch_bounds__(kThreads, 1) k_wgrad(ppo_wgrad_t a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int l = blockIdx.y;
     if (a.kin[l] == 64)
-        wgrad_layer<64>(a, l, lds);
+        wgrad_layer<64, DT>(a, l, lds);
     else
-        wgrad_layer<256>(a, l, lds);
+        wgrad_layer<256, DT>(a, l, lds);
 }
 
 }  // namespace
 
 extern "C" int ppo_weight_grads(const ppo_wgrad_t* args_host, void* stream) {
     const ppo_wgrad_t* a = args_host;
-    bool ok = a && a->rows > 0 && a->splits > 0 && a->splits <= a->rows && a->layers > 0 && a->layers <= 5;
+    bool ok = a && a->rows > 0 && a->splits > 0 && a->splits <= a->rows && a->layers > 0 && a->layers <= 5 &&
+              (a->dtype == PPO_DT_BF16 || a->dtype == PPO_DT_F16);
     for (int l = 0; ok && l < a->layers; ++l)
         ok = a->dz[l] && a->hin[l] && a->part[l] && (a->kin[l] == 64 || a->kin[l] == 256) &&
              a->hin_stride[l] >= a->kin[l] + 1 && a->hin_stride[l] % 8 == 0 &&
@@ -192,18 +225,24 @@ extern "C" int ppo_weight_grads(const ppo_wgrad_t* args_host, void* stream) {
         ppo_detail::set_error(g_err);
         return -1;
     }
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_wgrad), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kLdsBytes) != hipSuccess) {
+    const bool f16 = a->dtype == PPO_DT_F16;
+    static bool attr[2] = {false, false};
+    if (!attr[f16]) {
+        const void* k = f16 ? reinterpret_cast<const void*>(k_wgrad<PPO_DT_F16>)
+                            : reinterpret_cast<const void*>(k_wgrad<PPO_DT_BF16>);
+        if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) != hipSuccess) {
             snprintf(g_err, sizeof(g_err), "ppo_weight_grads: cannot reserve %d B of LDS", kLdsBytes);
             ppo_detail::set_error(g_err);
             return -2;
         }
-        attr = true;
+        attr[f16] = true;
     }
-    hipLaunchKernelGGL(k_wgrad, dim3(a->splits, a->layers), dim3(kThreads), kLdsBytes,
-                       static_cast<hipStream_t>(stream), *a);
+    if (f16)
+        hipLaunchKernelGGL(k_wgrad<PPO_DT_F16>, dim3(a->splits, a->layers), dim3(kThreads), kLdsBytes,
+                           static_cast<hipStream_t>(stream), *a);
+    else
+        hipLaunchKernelGGL(k_wgrad<PPO_DT_BF16>, dim3(a->splits, a->layers), dim3(kThreads), kLdsBytes,
+                           static_cast<hipStream_t>(stream), *a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         snprintf(g_err, sizeof(g_err), "k_wgrad: %s", hipGetErrorString(e));

@@ -29,8 +29,11 @@ MI355X-specific design (no change of the maths):
   exchange is ONE RCCL all-reduce per minibatch of [grads | kl] (rl_games: a cat + all-reduce +
   per-parameter copy, then a second all-reduce + broadcast for the KL / LR), the norm clip is one
   reduction and Adam one pass over the buffer.
-* ``mixed_precision``: bf16 autocast for the 256-wide trunk GEMMs (MFMA) instead of fp16 + loss
-  scaler; the mu / value heads run in fp32 (bf16 mu would put ~0.4 % noise into the PPO ratio).
+* ``mixed_precision``: as rl_games, fp16 autocast for the 256-wide trunk GEMMs (MFMA) with
+  ``torch.cuda.amp.GradScaler``'s dynamic loss scale (2^16, x2 after 2000 good steps, x0.5 and the
+  step skipped on a non-finite gradient) held on the device, so no host sync is added; the mu / value
+  heads run in fp32 (a 16-bit mu would put ~0.4 % noise into the PPO ratio).  ``mixed_precision_dtype:
+  bfloat16`` selects bf16 instead.
 * Multi-GPU: ``multi_gpu_mode: allreduce`` (default, rl_games ``multi_gpu`` semantics: per-rank
   minibatches, averaged gradients) or ``allgather`` (BASELINE north star: the rollout tensors of all
   ranks are all-gathered over RCCL at the PPO boundary and every rank runs the identical update on
@@ -46,6 +49,7 @@ import time
 import torch
 import torch.distributed as dist
 
+from .fused import SCALER_GROWTH_INTERVAL, SCALER_INIT
 from .models import FlatParams, ModelA2CContinuousLogStd
 
 
@@ -309,6 +313,12 @@ class A2CAgent:
         self.normalize_value = bool(config.get("normalize_value", False))
         self.value_bootstrap = bool(config.get("value_bootstrap", False))
         self.mixed_precision = bool(config.get("mixed_precision", False)) and self.device.type == "cuda"
+        mpd = config.get("mixed_precision_dtype", "float16")
+        if mpd not in ("float16", "bfloat16"):
+            raise ValueError(f"mixed_precision_dtype must be float16 or bfloat16, got {mpd!r}")
+        self.mixed_precision_dtype = torch.float16 if mpd == "float16" else torch.bfloat16
+        # GradScaler(enabled=mixed_precision) state on the device: [scale, growth tracker]
+        self.scaler_state = (torch.tensor([SCALER_INIT, 0.0], device=self.device) if self.mixed_precision else None)
         self.max_epochs = int(config.get("max_epochs", -1))
         self.save_freq = int(config.get("save_frequency", 0))
         self.save_best_after = int(config.get("save_best_after", 100))
@@ -394,8 +404,9 @@ class A2CAgent:
         if self.fused_update:
             from .fused import FusedPPOUpdate
 
-            self.fused = FusedPPOUpdate(self, compute_dtype=torch.bfloat16 if self.mixed_precision else torch.float32,
-                                        use_graphs=bool(self.config.get("hip_graphs", True)))
+            self.fused = FusedPPOUpdate(self, compute_dtype=self.mixed_precision_dtype if self.mixed_precision
+                                        else torch.float32, use_graphs=bool(self.config.get("hip_graphs", True)),
+                                        scaler=self.scaler_state)
             self._ds_static: dict = {}
             if self._play_graphs is not None:
                 self.fused.init_rollout(N, int(self.params.get("seed", 0)) * 7919 + self.rank)
@@ -595,7 +606,7 @@ class A2CAgent:
         return_batch = input_dict["returns"]
         actions = input_dict["actions"]
         obs = input_dict["obs"]
-        with torch.autocast(device_type=self.device.type, dtype=torch.bfloat16, enabled=self.mixed_precision):
+        with torch.autocast(device_type=self.device.type, dtype=self.mixed_precision_dtype, enabled=self.mixed_precision):
             res = self.model({"is_train": True, "prev_actions": actions, "obs": obs})
             neglogp, values, entropy = res["prev_neglogp"], res["values"], res["entropy"]
             mu, sigma = res["mus"], res["sigmas"]
@@ -611,18 +622,44 @@ class A2CAgent:
             loss = (a_loss + 0.5 * c_loss * self.critic_coef - entropy * self.entropy_coef
                     + b_loss * float(self.bounds_loss_coef or 0.0))
         self.flat.zero_grad()
-        loss.backward()
+        if self.scaler_state is not None:
+            (loss * self.scaler_state[0]).backward()  # scaler.scale(loss).backward()
+        else:
+            loss.backward()
         with torch.no_grad():
             kl = policy_kl(mu.detach().float(), sigma.detach().float(), old_mu, old_sigma, True)
             self._kl_slot.copy_(kl.reshape(1))
         self._exchange_grads()
-        if self.truncate_grads:
-            g = self.flat.grads
-            coef = torch.clamp(self.grad_norm / (torch.linalg.vector_norm(g) + 1e-6), max=1.0)
-            g.mul_(coef)
-        self.optimizer.step()
+        skip = False
+        if self.scaler_state is not None:  # scaler.unscale_ / scaler.step / scaler.update
+            with torch.no_grad():
+                g = self.flat.grads
+                found_inf = ~torch.isfinite(g).all()
+                g.mul_(1.0 / self.scaler_state[0])
+                skip = bool(found_inf.item())  # (GradScaler.step reads found_inf on the host too)
+                self._scaler_update(skip)
+        if not skip:
+            if self.truncate_grads:
+                g = self.flat.grads
+                coef = torch.clamp(self.grad_norm / (torch.linalg.vector_norm(g) + 1e-6), max=1.0)
+                g.mul_(coef)
+            self.optimizer.step()
         return (a_loss.detach(), c_loss.detach(), entropy.detach(), self._kl_slot[0].clone(),
                 mu.detach(), sigma.detach(), b_loss.detach())
+
+    @torch.no_grad()
+    def _scaler_update(self, found_inf: bool) -> None:
+        """GradScaler.update (backoff 0.5, growth 2 after SCALER_GROWTH_INTERVAL good steps in a row); the
+        fused path does the same in ppo_tail."""
+        st = self.scaler_state
+        if found_inf:
+            st[0] *= 0.5
+            st[1] = 0.0
+        elif float(st[1]) + 1.0 >= SCALER_GROWTH_INTERVAL:
+            st[0] *= 2.0
+            st[1] = 0.0
+        else:
+            st[1] += 1.0
 
     def train_epoch(self):
         self.model.eval()
@@ -782,6 +819,10 @@ class A2CAgent:
         state = self.get_weights()
         state.update(epoch=self.epoch_num, frame=self.frame, last_mean_rewards=self.last_mean_rewards,
                      optimizer=self.optimizer.state_dict(), env_state=None)
+        if self.scaler_state is not None:  # rl_games: state['scaler'] = self.scaler.state_dict()
+            state["scaler"] = {"scale": float(self.scaler_state[0]), "growth_factor": 2.0, "backoff_factor": 0.5,
+                               "growth_interval": SCALER_GROWTH_INTERVAL,
+                               "_growth_tracker": int(self.scaler_state[1])}
         return state
 
     def save(self, fn: str) -> None:
@@ -797,3 +838,7 @@ class A2CAgent:
         opt = ckpt.get("optimizer")
         if isinstance(opt, dict) and "exp_avg" in opt:
             self.optimizer.load_state_dict(opt)
+        sc = ckpt.get("scaler")
+        if self.scaler_state is not None and isinstance(sc, dict) and "scale" in sc:
+            self.scaler_state[0] = float(sc["scale"])
+            self.scaler_state[1] = float(sc.get("_growth_tracker", 0))

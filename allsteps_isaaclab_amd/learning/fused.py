@@ -6,14 +6,18 @@ rl_games 1.6.1 (``a2c_continuous.py::calc_gradients`` + ``trancate_gradients_and
 adaptive LR from the KL -- ~300 kernel launches and several host round trips per minibatch.  Here
 the same maths is an explicit forward / backward:
 
-* trunk (59 -> 256 x 5, ELU) in bf16 on hipBLASLt: ``addmm`` forward, ``dz @ W`` for the input
+* trunk (59 -> 256 x 5, ELU) in fp16 (rl_games' autocast type; bf16 selectable) on the fused MFMA
+  kernels, or on hipBLASLt: ``addmm`` forward, ``dz @ W`` for the input
   gradients, and the weight gradients as a **split-K** batched GEMM (``bmm`` over S row chunks,
   fp32 out, summed) -- the library's single ``dz^T h`` with K = 32768 and a 256 x 256 output runs on 16
   workgroups (measured 113 us vs 29 us split, scripts/mlp_microbench.py);
 * heads (mu | value, 22 x 256) and everything after them in fp32;
 * ``libppo_hip.so`` (include/ppo.h) for the rest: obs normaliser update + normalise, the fused
   loss / KL / head-gradient kernel, ELU backward with bias-gradient partials, clip + Adam over the flat
-  buffer (writing the bf16 trunk mirror), adaptive LR and the device minibatch counter;
+  buffer (writing the fp16 / bf16 trunk mirror), adaptive LR and the device minibatch counter;
+* ``mixed_precision``'s ``torch.cuda.amp.GradScaler`` on the device: the loss scale (2^16, x2 after
+  2000 good steps, x0.5 and the step skipped on a non-finite gradient) enters the head gradients and
+  leaves in the Adam kernel -- the fp16 input gradients of the trunk do not underflow;
 * graph A = forward + losses + backward (gradients and the KL land in the flat [grads | kl] bucket),
   graph B = clip + Adam + LR; in multi-GPU ``allreduce`` mode the RCCL all-reduce of the bucket runs
   between them.  Minibatch rows are addressed through a device counter, so one graph serves every
@@ -33,7 +37,10 @@ import torch.nn.functional as F
 from .._native import PPO_LIB_PATH, NativeError
 
 _LIB = None
-PPO_ABI_VERSION = 1
+PPO_ABI_VERSION = 2
+PPO_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+SCALER_GROWTH_INTERVAL = 2000  # torch.cuda.amp.GradScaler defaults (rl_games builds it with defaults)
+SCALER_INIT = 2.0 ** 16
 PPO_LOSS_NSTAT = 5
 
 
@@ -51,18 +58,20 @@ class PpoReduceJob(C.Structure):
 class PpoMlpFwd(C.Structure):
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p * 5), ("b", C.c_void_p * 5), ("wh", C.c_void_p),
                 ("bh", C.c_void_p), ("h", C.c_void_p * 4), ("h5", C.c_void_p), ("head", C.c_void_p),
-                ("rows", C.c_int32), ("nh", C.c_int32), ("x_stride", C.c_int32), ("h_stride", C.c_int32)]
+                ("rows", C.c_int32), ("nh", C.c_int32), ("x_stride", C.c_int32), ("h_stride", C.c_int32),
+                ("dtype", C.c_int32)]
 
 
 class PpoMlpBwd(C.Structure):
     _fields_ = [("dhead", C.c_void_p), ("wh", C.c_void_p), ("wt", C.c_void_p * 4), ("h5", C.c_void_p),
                 ("h", C.c_void_p * 4), ("dz", C.c_void_p * 5), ("rows", C.c_int32), ("nh", C.c_int32),
-                ("h_stride", C.c_int32)]
+                ("h_stride", C.c_int32), ("dtype", C.c_int32)]
 
 
 class PpoWgrad(C.Structure):
     _fields_ = [("dz", C.c_void_p * 5), ("hin", C.c_void_p * 5), ("part", C.c_void_p * 5), ("kin", C.c_int32 * 5),
-                ("hin_stride", C.c_int32 * 5), ("rows", C.c_int32), ("splits", C.c_int32), ("layers", C.c_int32)]
+                ("hin_stride", C.c_int32 * 5), ("rows", C.c_int32), ("splits", C.c_int32), ("layers", C.c_int32),
+                ("dtype", C.c_int32)]
 
 
 class PpoSeg(C.Structure):
@@ -91,12 +100,12 @@ def load() -> C.CDLL:
     L.ppo_obs_stats.argtypes = [V, V, I32, I32, V, V]
     L.ppo_obs_stats_update.argtypes = [V, I32, I32, I32, V, V, V, V]
     L.ppo_obs_normalize.argtypes = [V, V, I32, I32, V, V, F32, V, I32, I32, I32, V]
-    L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V]
-    L.ppo_loss_finalize.argtypes = [V, I32, I32, I32, F32, V, V, V, V, V, V]
+    L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V, V]
+    L.ppo_loss_finalize.argtypes = [V, I32, I32, I32, F32, V, V, V, V, V, V, V]
     L.ppo_elu_bwd.argtypes = [V, I32, V, I32, V, I32, I32, I32, V, V]
     L.ppo_sqnorm.argtypes = [V, I64, V, V]
-    L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, V]
-    L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V]
+    L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32, V, V]
+    L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V, V, I32, I32, V]
     L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
     L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
     L.ppo_counter_add.argtypes = [V, I64, V]
@@ -135,7 +144,8 @@ def _split(rows: int) -> int:
 class FusedPPOUpdate:
     """Owns the static buffers and the two graphs of one agent's minibatch step."""
 
-    def __init__(self, agent, compute_dtype: torch.dtype = torch.bfloat16, use_graphs: bool = True):
+    def __init__(self, agent, compute_dtype: torch.dtype = torch.float16, use_graphs: bool = True,
+                 scaler: torch.Tensor | None = None):
         self.L = load()
         self.agent = agent
         self.dev = agent.device
@@ -151,9 +161,14 @@ class FusedPPOUpdate:
         self.obs_dim = agent.obs_shape[0]
         self.mb = agent.dataset.minibatch_size
         self.n_mb = len(agent.dataset)
+        if compute_dtype not in PPO_DT:
+            raise ValueError(f"compute_dtype must be float32, bfloat16 or float16, got {compute_dtype}")
         self.dt = compute_dtype
-        self.bf16 = compute_dtype == torch.bfloat16
-        self.k0 = (self.obs_dim + 7) // 8 * 8 if self.bf16 else self.obs_dim  # 16-B aligned bf16 rows
+        self.lp = compute_dtype != torch.float32   # 16-bit trunk (mixed_precision)
+        self.dt_code = PPO_DT[compute_dtype]
+        # the loss scaler state [scale, growth tracker] (device fp32; GradScaler), shared with the agent
+        self.scaler = scaler
+        self.k0 = (self.obs_dim + 7) // 8 * 8 if self.lp else self.obs_dim  # 16-B aligned 16-bit rows
         self.use_graphs = use_graphs
         flat = agent.flat
         self.flat = flat
@@ -162,8 +177,8 @@ class FusedPPOUpdate:
         wmax = max(widths[1:])
         if any(w != wmax for w in widths[1:]):
             raise NotImplementedError("the fused update expects equal hidden widths (the agent's [256] x 5)")
-        # fused MFMA trunk (csrc/ppo_mlp.hip): bf16 mirror, 59 -> 256 x 5 ELU, heads <= 32
-        self.mfma_trunk = bool(self.bf16 and len(self.linears) == 5 and widths[1:] == [256] * 5 and self.k0 == 64
+        # fused MFMA trunk (csrc/ppo_mlp.hip): 16-bit mirror, 59 -> 256 x 5 ELU, heads <= 32
+        self.mfma_trunk = bool(self.lp and len(self.linears) == 5 and widths[1:] == [256] * 5 and self.k0 == 64
                                and self.A + 1 <= 32 and getattr(agent, "config", {}).get("mfma_trunk", True))
         L = self.L
         if self.mfma_trunk:
@@ -178,7 +193,7 @@ class FusedPPOUpdate:
             self.dzs = [torch.empty(B, 256, device=dev, dtype=dt) for _ in range(5)]
         else:
             self.h = [torch.zeros(B, w, device=dev, dtype=dt) for w in widths]
-            self.h_last_f = torch.empty(B, widths[-1], device=dev) if self.bf16 else self.h[-1]
+            self.h_last_f = torch.empty(B, widths[-1], device=dev) if self.lp else self.h[-1]
             self.dz = torch.empty(B, wmax, device=dev, dtype=dt)
             self.dh = torch.empty(B, wmax, device=dev, dtype=dt)
             self.dh_last = torch.empty(B, widths[-1], device=dev)  # fp32 from the heads
@@ -212,15 +227,15 @@ class FusedPPOUpdate:
         if net.value.weight.data_ptr() != self.Wh[self.A].data_ptr() or \
                 net.value.bias.data_ptr() != self.bh[self.A:].data_ptr():
             raise RuntimeError("flat layout: value head must follow the mu head (fused_param_order)")
-        # bf16 trunk mirror (row-padded first layer), written by the Adam kernel
+        # 16-bit trunk mirror (row-padded first layer), written by the Adam kernel
         segs, moff = [], 0
         self.W_lp, self.b_lp = [], []
-        if self.bf16:
+        if self.lp:
             sizes = [m.out_features * (self.k0 if i == 0 else m.in_features) + m.out_features
                      for i, m in enumerate(self.linears)]
             if self.mfma_trunk:  # + W^T of layers 1..4 for the backward chain
                 sizes += [m.weight.numel() for m in self.linears[1:]]
-            self.mirror = torch.zeros(sum(sizes), device=dev, dtype=torch.bfloat16)
+            self.mirror = torch.zeros(sum(sizes), device=dev, dtype=dt)
             for i, m in enumerate(self.linears):
                 kin = self.k0 if i == 0 else m.in_features
                 segs.append(PpoSeg(flat.offset(m.weight), m.weight.numel(), moff, m.in_features, kin, 0))
@@ -247,6 +262,7 @@ class FusedPPOUpdate:
                 o = flat.offset(self.linears[i].bias)
                 a.b[i] = flat.params[o:o + 256].data_ptr()
             a.wh, a.bh, a.nh = self.Wh.data_ptr(), self.bh.data_ptr(), self.A + 1
+            a.dtype = self.dt_code
             self._mlp_args = a
             bw = PpoMlpBwd()
             bw.dhead, bw.wh, bw.nh = self.dhead.data_ptr(), self.Wh.data_ptr(), self.A + 1
@@ -256,6 +272,7 @@ class FusedPPOUpdate:
             for k in range(5):
                 bw.dz[k] = self.dzs[k].data_ptr()
             bw.h5, bw.rows, bw.h_stride = self.h_last_f.data_ptr(), B, self.h[1].stride(0)
+            bw.dtype = self.dt_code
             self._mlp_bwd_args = bw
             # split-K partials of the weight / bias gradients, (S, 256, 72 | 264) fp32 per layer
             self.mfma_wgrad = bool(getattr(agent, "config", {}).get("mfma_wgrad", True))
@@ -264,7 +281,7 @@ class FusedPPOUpdate:
             for k in range(5):
                 wg.dz[k], wg.hin[k], wg.part[k] = self.dzs[k].data_ptr(), self.h[k].data_ptr(), self.wg_part[k].data_ptr()
                 wg.kin[k], wg.hin_stride[k] = 64 if k == 0 else 256, self.h[k].shape[1]
-            wg.rows, wg.splits, wg.layers = B, self.S, 5
+            wg.rows, wg.splits, wg.layers, wg.dtype = B, self.S, 5, self.dt_code
             self._wgrad_args = wg
         self.segs = (PpoSeg * max(len(segs), 1))(*segs)
         self.nseg = len(segs)
@@ -286,7 +303,7 @@ class FusedPPOUpdate:
 
     # ------------------------------------------------------------------ helpers
     def refresh_mirror(self) -> None:
-        """Rewrite the bf16 trunk mirror from the fp32 parameters (after restore / broadcast)."""
+        """Rewrite the 16-bit trunk mirror from the fp32 parameters (after restore / broadcast)."""
         if self.mirror is None:
             return
         with torch.no_grad():
@@ -312,15 +329,15 @@ class FusedPPOUpdate:
 
     # ------------------------------------------------------------------ the two halves
     def _trunk(self, x, idx, rows, h, h_last_f, head) -> None:
-        """Normalise rows [idx*rows, (idx+1)*rows) of x, run the trunk (bf16 mirror or fp32 weights) and
+        """Normalise rows [idx*rows, (idx+1)*rows) of x, run the trunk (16-bit mirror or fp32 weights) and
         the fp32 heads into head = [mu | value]."""
         L, s, rms = self.L, self._stream(), self.rms
         _check(L.ppo_obs_normalize(_p(x), _p(idx), rows, self.obs_dim, _p(rms.running_mean), _p(rms.running_var),
-                                   rms.epsilon, _p(h[0]), self.k0, h[0].stride(0), int(self.bf16), s),
+                                   rms.epsilon, _p(h[0]), self.k0, h[0].stride(0), self.dt_code, s),
                "ppo_obs_normalize")
         if self.mfma_trunk:
             # one launch: 5 x (MFMA + bias + ELU) with the activations chained in registers, fp32 heads;
-            # stores layers 1..4 (bf16) and layer 5 (fp32) only when h has room for them (training)
+            # stores layers 1..4 (16-bit) and layer 5 (fp32) only when h has room for them (training)
             a = self._mlp_args
             a.x, a.x_stride = h[0].data_ptr(), h[0].stride(0)
             a.h_stride = h[1].stride(0) if len(h) > 1 else 256
@@ -348,7 +365,7 @@ class FusedPPOUpdate:
             self.hr_last_f = None
         else:
             self.hr = [torch.zeros(n_envs, w, device=dev, dtype=dt) for w in widths]
-            self.hr_last_f = torch.empty(n_envs, widths[-1], device=dev) if self.bf16 else self.hr[-1]
+            self.hr_last_f = torch.empty(n_envs, widths[-1], device=dev) if self.lp else self.hr[-1]
         self.head_r = torch.empty(n_envs, self.A + 1, device=dev)
         self.zero_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.step_ctr = torch.zeros(1, device=dev, dtype=torch.int64)
@@ -358,7 +375,7 @@ class FusedPPOUpdate:
     def policy_act(self, obs: torch.Tensor, out: dict) -> None:
         """ModelA2CContinuousLogStd eval forward + sample for the rollout, written into
         out['actions' | 'neglogpacs' | 'values' | 'mus' | 'sigmas'] (contiguous, rows = n_envs).
-        Same trunk precision as the training forward (bf16 mirror when mixed_precision)."""
+        Same trunk precision as the training forward (16-bit mirror when mixed_precision)."""
         if not obs.is_contiguous() or obs.shape[0] != self.N:
             raise ValueError("policy_act: obs must be contiguous (n_envs, obs_dim)")
         self._trunk(obs, self.zero_idx, self.N, self.hr, self.hr_last_f, self.head_r)
@@ -426,11 +443,11 @@ class FusedPPOUpdate:
         # biases, log-sigma, kl; the reduce jobs: every weight and bias gradient)
         _check(L.ppo_loss_grad(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
                                _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
-                               _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.dhead),
-                               _p(self.loss_partials), s), "ppo_loss_grad")
+                               _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.scaler),
+                               _p(self.dhead), _p(self.loss_partials), s), "ppo_loss_grad")
         _check(L.ppo_loss_finalize(_p(self.loss_partials), self.loss_partials.shape[0], A, B,
-                                   self.loss_cfg.entropy_coef, _p(self.gbh), _p(self.gls), _p(self.stats),
-                                   _p(self.stat_idx), _p(self.flat.extra), s), "ppo_loss_finalize")
+                                   self.loss_cfg.entropy_coef, _p(self.scaler), _p(self.gbh), _p(self.gls),
+                                   _p(self.stats), _p(self.stat_idx), _p(self.flat.extra), s), "ppo_loss_finalize")
         S = self.S
         hl = self.h_last_f
         jobs, keep = [], []
@@ -449,7 +466,7 @@ class FusedPPOUpdate:
         job(pw, self.gWh, S, A + 1, hl.shape[1], hl.shape[1], hl.shape[1])
         torch.mm(self.dhead, self.Wh, out=self.dh_last)
         dh, dh_t = self.dh_last, 0
-        dt_code = int(self.bf16)
+        dt_code = self.dt_code
         nblk = self.elu_partials.shape[1]
         for i in reversed(range(nl)):
             m = self.linears[i]
@@ -465,7 +482,7 @@ class FusedPPOUpdate:
             hin = self.h[i]
             kin = hin.shape[1]
             gw = torch.bmm(dz.view(S, B // S, n_out).transpose(1, 2), hin.view(S, B // S, kin),
-                           out_dtype=torch.float32) if self.bf16 else \
+                           out_dtype=torch.float32) if self.lp else \
                 torch.bmm(dz.view(S, B // S, n_out).transpose(1, 2), hin.view(S, B // S, kin))
             job(gw, self.gW[i], S, n_out, kin, m.in_features, m.in_features)
             if i > 0:
@@ -514,9 +531,11 @@ class FusedPPOUpdate:
         _check(L.ppo_adam(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
                           _p(self.norm_partials), self.norm_partials.numel(),
                           ag.grad_norm if ag.truncate_grads else 0.0, _p(ag.lr), _p(opt.step_t), opt.beta1, opt.beta2,
-                          opt.eps, self.segs, self.nseg, _p(self.mirror), s), "ppo_adam")
+                          opt.eps, self.segs, self.nseg, _p(self.mirror), self.dt_code if self.lp else 1,
+                          _p(self.scaler), s), "ppo_adam")
         _check(L.ppo_tail(_p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr, self.max_lr,
-                          _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), s), "ppo_tail")
+                          _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), _p(self.scaler),
+                          _p(self.norm_partials), self.norm_partials.numel(), SCALER_GROWTH_INTERVAL, s), "ppo_tail")
 
     # ------------------------------------------------------------------ graphs
     def _run(self, key, fn) -> None:

@@ -59,7 +59,7 @@ class A2CNetwork(nn.Module):
 
     def forward(self, obs: torch.Tensor):
         out = self.actor_mlp(obs.flatten(1))
-        # heads in fp32 even under bf16 autocast: mu feeds the PPO ratio exp(old_neglogp - neglogp)
+        # heads in fp32 even under fp16 / bf16 autocast: mu feeds the PPO ratio exp(old_neglogp - neglogp)
         with torch.autocast(device_type=out.device.type, enabled=False):
             out = out.float()
             value = self.value_act(self.value(out))

@@ -15,7 +15,10 @@
  *                                         writes mu / sigma back into the dataset (update_mu_sigma)
  *   ppo_elu_bwd                           ELU backward (output form) + per-block bias-grad partials
  *   ppo_sqnorm / ppo_adam                 clip_grad_norm_ + Adam over the flat parameter buffer, and
- *                                         the bf16 mirror of the trunk weights for the next forward
+ *                                         the bf16 / fp16 mirror of the trunk weights for the next
+ *                                         forward; with a loss scaler (rl_games mixed_precision:
+ *                                         torch.cuda.amp.GradScaler) the unscale, the skip of a step
+ *                                         with non-finite gradients and the scale update
  *   ppo_tail                              adaptive LR from the (rank-averaged) KL; minibatch counter
  *   ppo_mlp_forward / ppo_mlp_backward    the whole trunk forward / input-gradient chain (MFMA)
  *   ppo_weight_grads                      split-K weight + bias gradients of all trunk layers (MFMA)
@@ -35,7 +38,11 @@
 extern "C" {
 #endif
 
-#define PPO_ABI_VERSION 1
+#define PPO_ABI_VERSION 2
+/* element types of the low-precision (trunk) buffers */
+#define PPO_DT_F32 0
+#define PPO_DT_BF16 1
+#define PPO_DT_F16 2
 #define PPO_MAX_ACT 32
 #define PPO_MAX_SEG 16
 #define PPO_LOSS_NSTAT 5 /* a_loss, c_loss, b_loss, entropy, kl */
@@ -66,30 +73,32 @@ int ppo_obs_stats_update(const double* partials, int32_t nblk, int32_t cols, int
                          double* running_var, double* count, void* stream);
 /* out[r*out_stride + c] = clamp((x[row][c] - mean[c]) / sqrt(var[c] + eps), -5, 5) for c < cols, 0 for
  * cols <= c < out_cols (columns out_cols .. out_stride-1 are left untouched, e.g. a constant ones column);
- * out_bf16 selects bf16 (else fp32) output */
+ * out_dtype: PPO_DT_F32, PPO_DT_BF16 or PPO_DT_F16 */
 int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, int32_t cols, const double* running_mean,
                       const double* running_var, float eps, void* out, int32_t out_cols, int32_t out_stride,
-                      int32_t out_bf16, void* stream);
+                      int32_t out_dtype, void* stream);
 
 /* Per-row PPO losses and head gradients.  head = [mu(0..A-1) | value(A)] (mb_rows x (A+1), fp32);
  * logstd (A); dataset rows (selected by mb_idx): actions / mu / sigma (A each), old_neglogp,
  * advantages, old_values, returns (1 each).  Writes dhead (mb_rows x (A+1)) = d loss / d head,
  * new mu / sigma into the dataset rows, and per-block partials[nblk][2A+1+PPO_LOSS_NSTAT]
- * (sum over rows of dhead columns, d loss / d logstd, the five statistics); nblk = ppo_loss_blocks(). */
+ * (sum over rows of dhead columns, d loss / d logstd, the five statistics); nblk = ppo_loss_blocks().
+ * grad_scale (device fp32, a power of two; NULL = 1): every gradient is of scale * loss (GradScaler). */
 int ppo_loss_blocks(int32_t mb_rows);
 int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
                   const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
                   const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
-                  float* dhead, float* partials, void* stream);
+                  const float* grad_scale, float* dhead, float* partials, void* stream);
 /* sum the partials: bias grads of the heads -> grad_head_bias (A+1), logstd grads (+ -entropy_coef) ->
  * grad_logstd (A); the statistics (means) -> stats[stat_idx][PPO_LOSS_NSTAT] (stat_idx from device);
- * the KL also -> kl_out (the slot that rides in the gradient all-reduce) */
+ * the KL also -> kl_out (the slot that rides in the gradient all-reduce); grad_scale as ppo_loss_grad */
 int ppo_loss_finalize(const float* partials, int32_t nblk, int32_t A, int32_t mb_rows, float entropy_coef,
-                      float* grad_head_bias, float* grad_logstd, float* stats, const int32_t* stat_idx, float* kl_out,
-                      void* stream);
+                      const float* grad_scale, float* grad_head_bias, float* grad_logstd, float* stats,
+                      const int32_t* stat_idx, float* kl_out, void* stream);
 
 /* dz = dh * (h > 0 ? 1 : h + 1) (ELU alpha 1, output form), rows x cols (cols multiple of 64);
- * dtype of dh / h / dz: 0 fp32, 1 bf16 (dh_dtype, h_dtype, dz_dtype); per-block column partial sums
+ * dtype of dh / h / dz: PPO_DT_* (fp32, or one low-precision type lp in bf16 / fp16: (f32,f32,f32),
+ * (f32,f32,lp), (f32,lp,lp), (lp,lp,lp)); per-block column partial sums
  * of dz into partials[nblk][cols] (nblk = ppo_elu_bwd_blocks(rows)) */
 int ppo_elu_bwd_blocks(int32_t rows);
 int ppo_elu_bwd(const void* dh, int32_t dh_dtype, const void* h, int32_t h_dtype, void* dz, int32_t dz_dtype,
@@ -119,11 +128,12 @@ int ppo_policy_sample(const float* head, const float* logstd, int32_t A, int32_t
 /* *ctr += inc (one thread; orders after the kernels that read it) */
 int ppo_counter_add(int64_t* ctr, int64_t inc, void* stream);
 
-/* Fused actor-critic trunk forward on MFMA (bf16 in, fp32 accumulate): 5 layers x 256, ELU, then the
- * fp32 heads.  x: rows x 64 bf16 (normalised obs, zero-padded 59 -> 64; row stride x_stride >= 64);
- * w[0]: 256 x 64 bf16, w[1..4]: 256 x 256 bf16 (the trunk mirror); b[l]: 256 fp32; wh: nh x 256 fp32
+/* Fused actor-critic trunk forward on MFMA (lp in, fp32 accumulate; lp = dtype: PPO_DT_BF16 on
+ * v_mfma_f32_32x32x16_bf16, PPO_DT_F16 on v_mfma_f32_32x32x16_f16 -- rl_games' fp16 autocast): 5 layers
+ * x 256, ELU, then the fp32 heads.  x: rows x 64 lp (normalised obs, zero-padded 59 -> 64; row stride
+ * x_stride >= 64); w[0]: 256 x 64 lp, w[1..4]: 256 x 256 lp (the trunk mirror); b[l]: 256 fp32; wh: nh x 256 fp32
  * ([mu.w | value.w]), bh: nh fp32 (nh <= 32).  Outputs (row-major, NULL = skip): h[0..3] = layers
- * 1..4 (bf16, columns 0..255 of rows with stride h_stride >= 256, a multiple of 8; columns beyond are
+ * 1..4 (lp, columns 0..255 of rows with stride h_stride >= 256, a multiple of 8; columns beyond are
  * not touched),
  * h5 = layer 5 in fp32 (rows x 256), head = rows x nh fp32.  Each wave keeps its 32 rows' activations
  * in registers between layers (an MFMA accumulator tile is the next layer's B operand); each layer's
@@ -138,15 +148,16 @@ typedef struct {
     float* h5;
     float* head;
     int32_t rows, nh, x_stride, h_stride;
+    int32_t dtype; /* PPO_DT_BF16 or PPO_DT_F16 */
 } ppo_mlp_fwd_t;
 int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream);
 
 /* Fused backward of the trunk's input-gradient chain (the weight gradients stay split-K GEMMs):
  *   dh5 = Wh^T dhead (exact f32 MFMA), dz4 = dh5 * elu'(h5),
- *   for l = 4..1: dz_{l-1} = (W_l^T dz_l) * elu'(h_l)   (bf16 MFMA, W_l^T from wt[l-1])
+ *   for l = 4..1: dz_{l-1} = (W_l^T dz_l) * elu'(h_l)   (lp MFMA, W_l^T from wt[l-1])
  * with elu'(y) = 1 if y > 0 else y + 1 (output form).  dhead: rows x nh fp32; wh: nh x 256 fp32;
- * wt[k]: W_{k+1}^T (256 x 256 bf16, row = input feature); h5: rows x 256 fp32; h[k]: layer k+1
- * activations (bf16, row stride h_stride); outputs dz[l] (l = 0..4): rows x 256 bf16. */
+ * wt[k]: W_{k+1}^T (256 x 256 lp, row = input feature); h5: rows x 256 fp32; h[k]: layer k+1
+ * activations (lp, row stride h_stride); outputs dz[l] (l = 0..4): rows x 256 lp.  lp = dtype. */
 typedef struct {
     const float* dhead;
     const float* wh;
@@ -155,6 +166,7 @@ typedef struct {
     const uint16_t* h[4];
     uint16_t* dz[5];
     int32_t rows, nh, h_stride;
+    int32_t dtype; /* PPO_DT_BF16 or PPO_DT_F16 */
 } ppo_mlp_bwd_t;
 int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream);
 
@@ -163,7 +175,7 @@ int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream);
  * split-K `torch.bmm(dz^T, [h | 1])` calls):
  *   part[l][s][o][c]   = sum_{b in split s} dz[l][b][o] * hin[l][b][c]   (o < 256, c < kin[l])
  *   part[l][s][o][kin] = sum_{b in split s} dz[l][b][o]                   (bias column)
- * dz[l]: rows x 256 bf16; hin[l]: rows x hin_stride[l] bf16 (kin[l] = 64 or 256 features); part[l]:
+ * dz[l]: rows x 256 lp; hin[l]: rows x hin_stride[l] lp (kin[l] = 64 or 256 features; lp = dtype); part[l]:
  * splits x 256 x hin_stride[l] fp32 (columns past kin[l] untouched).  Split s covers rows
  * [rows*s/splits, rows*(s+1)/splits); the partials are summed by ppo_reduce_rows. */
 typedef struct {
@@ -173,6 +185,7 @@ typedef struct {
     int32_t kin[5];
     int32_t hin_stride[5];
     int32_t rows, splits, layers;
+    int32_t dtype; /* PPO_DT_BF16 or PPO_DT_F16 */
 } ppo_wgrad_t;
 int ppo_weight_grads(const ppo_wgrad_t* args_host, void* stream);
 
@@ -189,18 +202,25 @@ int ppo_rollout_post(const float* reward, const uint8_t* done, const uint8_t* ti
 /* meters: mean[3] (reward, shaped reward, length), size[3] (current_size) */
 int ppo_meter_update(const float* partials, int32_t nblk, float max_size, float* mean3, float* size3, void* stream);
 
-/* ||g||^2 partials (fp32, nblk = ppo_sqnorm_blocks()) */
+/* ||g||^2 partials (fp32, nblk = ppo_sqnorm_blocks()); a non-finite g makes its partial +inf */
 int ppo_sqnorm_blocks(void);
 int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream);
 /* clip (max_norm > 0: g *= min(1, max_norm / (||g|| + 1e-6))) + Adam (torch.optim.Adam, amsgrad off,
- * weight_decay 0) with device lr / step (fp64); writes the bf16 mirror of the listed segments */
+ * weight_decay 0) with device lr / step (fp64); writes the mirror (mirror_dtype PPO_DT_BF16 / PPO_DT_F16)
+ * of the listed segments.  scaler (device fp32 [scale, growth tracker], NULL = none): the gradients
+ * carry the loss scale -- a non-finite norm skips the whole update (GradScaler.step), otherwise
+ * g / scale (exact: a power of two) is what is clipped and applied (GradScaler.unscale_) */
 int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials, int32_t nblk_norm,
              float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,
-             const ppo_seg_t* segs_host, int32_t nseg, void* mirror_bf16, void* stream);
+             const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, const float* scaler,
+             void* stream);
 /* adaptive LR (rl_games AdaptiveScheduler; kl_threshold <= 0: identity) from kl (device fp32), then
- * step += 1 (Adam's count; ppo_adam used step + 1), mb_idx = (mb_idx + 1) % n_minibatches, stat_idx += 1 */
+ * step += 1 (Adam's count; ppo_adam used step + 1) unless the scaler skipped the step,
+ * mb_idx = (mb_idx + 1) % n_minibatches, stat_idx += 1; with a scaler, GradScaler.update from the same
+ * norm partials: scale *= 0.5 after a skipped step, *= 2 after growth_interval good ones in a row */
 int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,
-             int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, void* stream);
+             int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, float* scaler, const float* sqnorm_partials,
+             int32_t nblk_norm, int32_t growth_interval, void* stream);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,7 @@ for i in range(5):
 for i in range(4):
     a.h[i] = hs[i].data_ptr()
 a.wh, a.bh, a.h5, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), h5.data_ptr(), head.data_ptr(), B, 22
-a.x_stride, a.h_stride = 64, 256
+a.x_stride, a.h_stride, a.dtype = 64, 256, 1  # bf16 (PPO_DT_BF16)
 
 
 def fused(store=True):

@@ -22,7 +22,7 @@ a = FU.PpoWgrad()
 for k in range(5):
     a.dz[k], a.hin[k], a.part[k] = dz[k].data_ptr(), hin[k].data_ptr(), part[k].data_ptr()
     a.kin[k], a.hin_stride[k] = 64 if k == 0 else 256, widths[k]
-a.rows, a.splits, a.layers = B, S, 5
+a.rows, a.splits, a.layers, a.dtype = B, S, 5, 1  # bf16 (PPO_DT_BF16)
 
 
 def kernel():

@@ -103,7 +103,7 @@ class _SpacesOnlyEnv:
         return self._info
 
 
-def _agents_and_batch(n_envs, mixed, tmp):
+def _agents_and_batch(n_envs, mixed, tmp, mp_dtype="float16"):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _toy_env import agent_params
     from allsteps_isaaclab_amd.learning.a2c_continuous import A2CAgent
@@ -113,6 +113,7 @@ def _agents_and_batch(n_envs, mixed, tmp):
                          minibatch_size=n_envs * 8, horizon_length=16)
         p["network"]["mlp"]["units"] = [256, 256, 256, 256, 256]
         p["config"]["vec_env"] = _SpacesOnlyEnv(n_envs)
+        p["config"]["mixed_precision_dtype"] = mp_dtype
         torch.manual_seed(11)
         a = A2CAgent("run", p)
         a.init_tensors()
@@ -192,9 +193,16 @@ def test_fused_minibatch_step_matches_autograd_fp32(tmp_path, graphs):
 
 
 @pytest.mark.gpu
-def test_fused_bf16_step_close_to_fp32_autograd(tmp_path):
-    ref, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path)
+@pytest.mark.parametrize("mp_dtype,tol", [("float16", 1e-2), ("bfloat16", 3e-2)])
+def test_fused_lowp_step_close_to_fp32_autograd(tmp_path, mp_dtype, tol):
+    """mixed_precision (rl_games: fp16 autocast + GradScaler; bf16 selectable): the fused 16-bit
+    trunk's gradients against the fp32 autograd step, after the loss scale is divided out (the fused
+    step leaves scaled gradients in the bucket; the Adam kernel unscales them).  fp16 keeps 3 more
+    mantissa bits than bf16, hence the tighter bound."""
+    ref, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path, mp_dtype=mp_dtype)
+    assert fus.fused.dt == (torch.float16 if mp_dtype == "float16" else torch.bfloat16)
     ref.mixed_precision = False
+    ref.scaler_state = None
     ref.truncate_grads = False
     saved = ref.optimizer.step
     ref.optimizer.step = lambda: None
@@ -203,10 +211,59 @@ def test_fused_bf16_step_close_to_fp32_autograd(tmp_path):
     fus.fused.begin_epoch()
     fus.fused.step_a(True)
     torch.cuda.synchronize()
+    scale = float(fus.scaler_state[0])
+    assert scale == 2.0 ** 16
     gr, gf = _grads(ref), _grads(fus)
     for k in gr:
-        rel = (gr[k] - gf[k]).norm().item() / (gr[k].norm().item() + 1e-12)
-        assert rel < 3e-2, (k, rel)
+        g = gf[k] / scale
+        rel = (gr[k] - g).norm().item() / (gr[k].norm().item() + 1e-12)
+        assert rel < tol, (k, rel)
+
+
+@pytest.mark.gpu
+def test_fused_loss_scaler_skips_and_grows(tmp_path):
+    """GradScaler semantics on the device (ppo_adam / ppo_tail): a non-finite gradient skips the whole
+    Adam step (parameters, moments and the step count unchanged) and halves the scale; after
+    SCALER_GROWTH_INTERVAL good steps in a row the scale doubles; a good step applies g / scale."""
+    from allsteps_isaaclab_amd.learning.fused import SCALER_GROWTH_INTERVAL
+
+    _, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path)
+    fus.fused.use_graphs = False
+    fus.fused.begin_epoch()
+    fus.fused.step_a(True)
+    torch.cuda.synchronize()
+    p0 = fus.flat.params.clone()
+    m0 = fus.optimizer.exp_avg.clone()
+    step0 = float(fus.optimizer.step_t)
+    good = fus.flat.grads.clone()
+    fus.flat.grads[3] = float("inf")
+    fus.fused.step_b()
+    torch.cuda.synchronize()
+    assert torch.equal(fus.flat.params, p0) and torch.equal(fus.optimizer.exp_avg, m0)
+    assert float(fus.optimizer.step_t) == step0
+    assert float(fus.scaler_state[0]) == 2.0 ** 15 and float(fus.scaler_state[1]) == 0.0
+    # a good step at the end of a growth interval: unscaled update, then the scale doubles
+    fus.flat.grads.copy_(good / 2.0)  # the gradients of the halved scale
+    fus.scaler_state[1] = SCALER_GROWTH_INTERVAL - 1
+    lr0 = fus.lr.clone()  # the adaptive LR moves after the Adam kernel, in ppo_tail
+    fus.fused.step_b()
+    torch.cuda.synchronize()
+    assert float(fus.optimizer.step_t) == step0 + 1
+    assert float(fus.scaler_state[0]) == 2.0 ** 16 and float(fus.scaler_state[1]) == 0.0
+    assert not torch.equal(fus.flat.params, p0)
+    # the update equals an fp32 Adam step on g / scale (FlatAdam, the same clip)
+    ref = fus.flat.params.clone()
+    fus.flat.params.copy_(p0)
+    fus.optimizer.exp_avg.copy_(m0)
+    fus.optimizer.exp_avg_sq.zero_()
+    fus.optimizer.step_t.fill_(step0)
+    fus.lr.copy_(lr0)
+    g = good / 2.0 / 2.0 ** 15
+    if fus.truncate_grads:
+        g = g * torch.clamp(fus.grad_norm / (torch.linalg.vector_norm(g) + 1e-6), max=1.0)
+    fus.flat.grads.copy_(g)
+    fus.optimizer.step()
+    torch.testing.assert_close(ref, fus.flat.params, rtol=1e-5, atol=1e-7)
 
 
 @pytest.mark.gpu
@@ -320,32 +377,30 @@ def test_play_script_restores_trained_checkpoint(tmp_path):
     assert out["steps"] == 200 and out["episodes"] > 0 and math.isfinite(out["mean_reward"])
 
 
-def _bf16_round(t):
-    return t.to(torch.bfloat16).float()
-
-
 @pytest.mark.gpu
-@pytest.mark.parametrize("rows", [32768, 1000])
-def test_fused_mlp_forward_kernel(rows):
+@pytest.mark.parametrize("rows,dt", [(32768, torch.bfloat16), (1000, torch.bfloat16), (32768, torch.float16),
+                                     (1000, torch.float16)])
+def test_fused_mlp_forward_kernel(rows, dt):
     """ppo_mlp_forward (MFMA, activations chained in registers) vs an fp32 torch statement of the same
-    rounding points: each hidden layer rounded to bf16 once, layer 5 and the heads in fp32."""
+    rounding points: each hidden layer rounded to the 16-bit type once, layer 5 and the heads in fp32."""
     import ctypes as C
 
     from allsteps_isaaclab_amd.learning import fused as FU
 
     L = FU.load()
+    tol = 0.05 if dt == torch.bfloat16 else 0.01
     g = torch.Generator(device="cuda:0").manual_seed(3)
     dev = "cuda:0"
     x = torch.zeros(rows, 64, device=dev)
     x[:, :59] = torch.randn(rows, 59, device=dev, generator=g).clamp(-5, 5)
-    xb = x.to(torch.bfloat16)
-    ws = [(torch.randn(256, 64 if i == 0 else 256, device=dev, generator=g) / (8 if i == 0 else 16)).to(torch.bfloat16)
+    xb = x.to(dt)
+    ws = [(torch.randn(256, 64 if i == 0 else 256, device=dev, generator=g) / (8 if i == 0 else 16)).to(dt)
           for i in range(5)]
     ws[0][:, 59:] = 0
     bs = [torch.randn(256, device=dev, generator=g) * 0.1 for _ in range(5)]
     wh = torch.randn(22, 256, device=dev, generator=g) / 16
     bh = torch.randn(22, device=dev, generator=g) * 0.1
-    hs = [torch.empty(rows, 256, device=dev, dtype=torch.bfloat16) for _ in range(4)]
+    hs = [torch.empty(rows, 256, device=dev, dtype=dt) for _ in range(4)]
     h5 = torch.empty(rows, 256, device=dev)
     head = torch.empty(rows, 22, device=dev)
     a = FU.PpoMlpFwd()
@@ -356,7 +411,7 @@ def test_fused_mlp_forward_kernel(rows):
     for i in range(4):
         a.h[i] = hs[i].data_ptr()
     a.wh, a.bh, a.h5, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), h5.data_ptr(), head.data_ptr(), rows, 22
-    a.x_stride, a.h_stride = 64, 256
+    a.x_stride, a.h_stride, a.dtype = 64, 256, FU.PPO_DT[dt]
     FU._check(L.ppo_mlp_forward(C.byref(a), torch.cuda.current_stream().cuda_stream), "ppo_mlp_forward")
     torch.cuda.synchronize()
     hin = xb.float()
@@ -365,9 +420,10 @@ def test_fused_mlp_forward_kernel(rows):
         y = torch.nn.functional.elu(z)
         if i < 4:
             got = hs[i].float()
-            assert (got - _bf16_round(y)).abs().max().item() < 0.05, i
-            frac = ((got - _bf16_round(y)).abs() > 1e-6).float().mean().item()
-            assert frac < 0.02, (i, frac)  # only bf16 rounding-boundary flips
+            yr = y.to(dt).float()
+            assert (got - yr).abs().max().item() < tol, i
+            frac = ((got - yr).abs() > 1e-6).float().mean().item()
+            assert frac < 0.02, (i, frac)  # only rounding-boundary flips
             hin = got  # chain on the kernel's own rounding, as the kernel does
         else:
             torch.testing.assert_close(h5, y, rtol=2e-3, atol=2e-3)
@@ -376,12 +432,14 @@ def test_fused_mlp_forward_kernel(rows):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rows,splits", [(32768, 32), (1000, 3), (64, 1)])
-def test_weight_grads_kernel(rows, splits):
-    """ppo_weight_grads (MFMA, transposed LDS reads) vs fp32 torch on the same bf16 inputs: per split
-    s, part[s] = dz[rows of s]^T [hin | 1] over columns 0..kin (the products of two bf16 values are
-    exact in fp32; only the summation order differs).  Columns past the bias column stay untouched;
-    ragged splits (rows not a multiple of splits or of the 64-row stage) are covered."""
+@pytest.mark.parametrize("rows,splits,dt", [(32768, 32, torch.bfloat16), (1000, 3, torch.bfloat16),
+                                            (64, 1, torch.bfloat16), (32768, 32, torch.float16),
+                                            (1000, 3, torch.float16)])
+def test_weight_grads_kernel(rows, splits, dt):
+    """ppo_weight_grads (MFMA, transposed LDS reads) vs fp32 torch on the same 16-bit inputs: per split
+    s, part[s] = dz[rows of s]^T [hin | 1] over columns 0..kin (the products of two bf16 or two fp16
+    values are exact in fp32; only the summation order differs).  Columns past the bias column stay
+    untouched; ragged splits (rows not a multiple of splits or of the 64-row stage) are covered."""
     import ctypes as C
 
     from allsteps_isaaclab_amd.learning import fused as FU
@@ -390,14 +448,14 @@ def test_weight_grads_kernel(rows, splits):
     dev = "cuda:0"
     g = torch.Generator(device=dev).manual_seed(5)
     widths = [72] + [264] * 4
-    dz = [torch.randn(rows, 256, device=dev, generator=g).to(torch.bfloat16) for _ in range(5)]
-    hin = [torch.randn(rows, w, device=dev, generator=g).to(torch.bfloat16) for w in widths]
+    dz = [torch.randn(rows, 256, device=dev, generator=g).to(dt) for _ in range(5)]
+    hin = [torch.randn(rows, w, device=dev, generator=g).to(dt) for w in widths]
     part = [torch.full((splits, 256, w), float("nan"), device=dev) for w in widths]
     a = FU.PpoWgrad()
     for k in range(5):
         a.dz[k], a.hin[k], a.part[k] = dz[k].data_ptr(), hin[k].data_ptr(), part[k].data_ptr()
         a.kin[k], a.hin_stride[k] = 64 if k == 0 else 256, widths[k]
-    a.rows, a.splits, a.layers = rows, splits, 5
+    a.rows, a.splits, a.layers, a.dtype = rows, splits, 5, FU.PPO_DT[dt]
     FU._check(L.ppo_weight_grads(C.byref(a), torch.cuda.current_stream().cuda_stream), "ppo_weight_grads")
     torch.cuda.synchronize()
     for k in range(5):

@@ -156,6 +156,30 @@ def _make_agent(n=64, seed=0, **over):
     return A.A2CAgent("run", params)
 
 
+def test_loss_scaler_update_is_grad_scaler():
+    """A2CAgent._scaler_update == torch.amp.GradScaler.update's rule (defaults: backoff 0.5, growth 2
+    after 2000 good steps in a row, tracker reset on either event) -- the rule ppo_tail applies on the
+    device in the fused path."""
+    from allsteps_isaaclab_amd.learning.fused import SCALER_GROWTH_INTERVAL, SCALER_INIT
+
+    class S:
+        scaler_state = torch.tensor([SCALER_INIT, 0.0])
+
+    s = S()
+    A.A2CAgent._scaler_update(s, True)
+    assert s.scaler_state.tolist() == [SCALER_INIT / 2, 0.0]
+    for _ in range(SCALER_GROWTH_INTERVAL - 1):
+        A.A2CAgent._scaler_update(s, False)
+    assert s.scaler_state.tolist() == [SCALER_INIT / 2, SCALER_GROWTH_INTERVAL - 1]
+    A.A2CAgent._scaler_update(s, False)
+    assert s.scaler_state.tolist() == [SCALER_INIT, 0.0]
+    import inspect
+
+    d = inspect.signature(torch.amp.GradScaler.__init__).parameters  # the defaults rl_games gets
+    assert (d["init_scale"].default, d["growth_factor"].default, d["backoff_factor"].default,
+            d["growth_interval"].default) == (SCALER_INIT, 2.0, 0.5, SCALER_GROWTH_INTERVAL)
+
+
 def test_state_dict_uses_rl_games_names(tmp_path):
     agent = _make_agent()
     keys = set(agent.model.state_dict())
