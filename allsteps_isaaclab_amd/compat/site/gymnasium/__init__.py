@@ -1,6 +1,6 @@
 """Minimal ``gymnasium`` shim (gymnasium is absent offline): ``register`` / ``make`` / ``spec`` /
 ``registry`` over allsteps_isaaclab_amd.registry, ``spaces`` over allsteps_isaaclab_amd.envs.spaces.
-``wrappers.RecordVideo`` raises: there is no renderer in the MI355X build."""
+``wrappers.RecordVideo`` records ``env.render()`` frames (envs/record_video.py)."""
 
 from allsteps_isaaclab_amd.envs import spaces  # noqa: F401
 from allsteps_isaaclab_amd.registry import make, register, spec  # noqa: F401

@@ -1,6 +1,4 @@
-"""Shim of ``gymnasium.wrappers``: video recording needs a renderer, which the MI355X build has not."""
+"""Shim of ``gymnasium.wrappers``: ``RecordVideo`` is allsteps_isaaclab_amd.envs.record_video's (GIF frames
+of the software renderer, envs/render.py)."""
 
-
-class RecordVideo:
-    def __init__(self, *args, **kwargs):
-        raise RuntimeError("--video: there is no renderer in the MI355X build (DESIGN.md §8)")
+from allsteps_isaaclab_amd.envs.record_video import RecordVideo  # noqa: F401

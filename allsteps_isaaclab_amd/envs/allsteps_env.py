@@ -175,6 +175,14 @@ class AllstepsEnv(DirectRLEnv):
         """Per-env curriculum level (all envs share one level in the reference, allsteps_env.py:472)."""
         return self.state["curriculum"].expand(self.num_envs)
 
+    def _render_rgb(self, env_id: int):
+        from .render import render_frame
+
+        st = {k: self.state[k][..., env_id].detach().cpu().numpy() for k in ("root_pos", "root_quat", "q", "stones")}
+        half = [0.5 * v for v in self.cfg.step_size]
+        return render_frame(self.model, st["root_pos"], st["root_quat"], st["q"], st["stones"].reshape(-1, 3), half,
+                            target=int(self.state["idx"][env_id]))
+
     @property
     def steps_pos(self) -> torch.Tensor:
         """(N, 20, 3) stepping-stone centres, env-local frame."""

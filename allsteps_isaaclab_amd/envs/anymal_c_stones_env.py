@@ -106,6 +106,14 @@ class AnymalCStonesEnv(DirectRLEnv):
         """(N, 4) stone bitmasks of the four sensor feet (RF, LF, RH, LH) in the last substep."""
         return torch.cat([self.state["contact_mask"], self.state["contact_mask_hind"]], dim=0).T
 
+    def _render_rgb(self, env_id: int):
+        from .render import render_frame
+
+        st = {k: self.state[k][..., env_id].detach().cpu().numpy() for k in ("root_pos", "root_quat", "q", "stones")}
+        half = [0.5 * v for v in self.cfg.step_size]
+        return render_frame(self.model, st["root_pos"], st["root_quat"], st["q"], st["stones"].reshape(-1, 3), half,
+                            target=int(self.state["idx"][env_id]))
+
     def get_state(self) -> dict:
         return {k: v.clone() for k, v in self.state.items()}
 

@@ -21,7 +21,7 @@ class DirectRLEnv:
     """Base class of direct-workflow environments (direct_rl_env.py:53-670)."""
 
     is_vector_env = True
-    metadata: dict = {"render_modes": [None], "isaac_sim_version": None}
+    metadata: dict = {"render_modes": [None, "rgb_array"], "isaac_sim_version": None}
 
     def __init__(self, cfg, render_mode: str | None = None, **kwargs):
         self.cfg = cfg
@@ -108,9 +108,16 @@ class DirectRLEnv:
         return seed
 
     def render(self, recompute: bool = False):
+        """``rgb_array``: an (H, W, 3) uint8 frame of env 0 (envs/render.py; direct_rl_env.py:508-548
+        returns the viewport capture there).  None without a render mode."""
         if self.render_mode is None:
             return None
-        raise NotImplementedError(f"render_mode={self.render_mode!r} is not supported (headless backend)")
+        if self.render_mode != "rgb_array":
+            raise NotImplementedError(f"render_mode={self.render_mode!r}: only 'rgb_array' is supported (headless)")
+        return self._render_rgb(0)
+
+    def _render_rgb(self, env_id: int):
+        raise NotImplementedError(f"{type(self).__name__} has no renderer")
 
     def close(self):
         self._is_closed = True

@@ -5,7 +5,10 @@ in ``RlGamesVecEnvWrapper``, register it as ``rlgpu``, ``runner.create_player()`
 ``agent.restore(checkpoint)``, then step ``obs -> agent.get_action(obs, is_deterministic) ->
 env.step`` in inference mode.  There is no simulator app to keep running, so the loop runs
 ``--steps`` steps (the reference runs until the app window closes) and prints the mean episode
-reward / length of the episodes that finished.  ``--video`` is not supported (no renderer).
+reward / length of the episodes that finished.  ``--video`` (play.py:111-127, 189-193) makes the env with
+``render_mode="rgb_array"``, wraps it in ``RecordVideo`` (step 0 trigger, ``--video_length`` frames of env
+0, written under ``<run dir>/videos/play`` -- as an animated GIF: no MP4 encoder in this image) and stops
+after ``--video_length`` steps.
 Checkpoints are rl_games' layout ({'model': state_dict, ...}), so a checkpoint trained by the
 reference's rl_games loads here and vice versa.
 
@@ -49,8 +52,6 @@ def main(argv=None):
     from allsteps_isaaclab_amd.rl_games import RlGamesGpuEnv, RlGamesVecEnvWrapper, env_configurations, vecenv
 
     args = parse_args(argv)
-    if args.video:
-        raise SystemExit("--video: there is no renderer in the MI355X build")
     env_cfg = registry.load_cfg_from_registry(args.task, "env_cfg_entry_point")
     agent_cfg = registry.load_cfg_from_registry(args.task, "rl_games_cfg_entry_point")
     env_cfg.scene.num_envs = args.num_envs if args.num_envs is not None else env_cfg.scene.num_envs
@@ -59,8 +60,16 @@ def main(argv=None):
     rl_device = params["config"]["device"]
     clip_obs = params["env"].get("clip_observations", math.inf)
     clip_actions = params["env"].get("clip_actions", math.inf)
-    env = RlGamesVecEnvWrapper(registry.make(args.task, cfg=env_cfg, render_mode=None), rl_device, clip_obs,
-                               clip_actions)
+    env = registry.make(args.task, cfg=env_cfg, render_mode="rgb_array" if args.video else None)
+    video = None
+    if args.video:
+        from allsteps_isaaclab_amd.envs.record_video import RecordVideo
+
+        log_dir = os.path.dirname(os.path.dirname(os.path.abspath(args.checkpoint)))
+        env = video = RecordVideo(env, video_folder=os.path.join(log_dir, "videos", "play"),
+                                  step_trigger=lambda step: step == 0, video_length=args.video_length,
+                                  disable_logger=True)
+    env = RlGamesVecEnvWrapper(env, rl_device, clip_obs, clip_actions)
     vecenv.register("IsaacRlgWrapper", lambda config_name, num_actors, **kw: RlGamesGpuEnv(config_name, num_actors, **kw))
     env_configurations.register("rlgpu", {"vecenv_type": "IsaacRlgWrapper", "env_creator": lambda **kw: env})
     params["load_checkpoint"] = True
@@ -81,7 +90,8 @@ def main(argv=None):
     cur_r = torch.zeros(n, device=env.unwrapped.device)
     cur_l = torch.zeros(n, device=env.unwrapped.device)
     sums = torch.zeros(3, device=env.unwrapped.device)  # reward, length, episodes
-    for _ in range(args.steps):
+    steps = min(args.steps, args.video_length) if args.video else args.steps
+    for _ in range(steps):
         t0 = time.time()
         with torch.inference_mode():
             obs = agent.obs_to_torch(obs)
@@ -97,10 +107,12 @@ def main(argv=None):
         if args.real_time and sleep > 0:
             time.sleep(sleep)
     r, l, k = sums.tolist()
-    out = {"steps": args.steps, "num_envs": n, "episodes": int(k), "mean_reward": r / max(k, 1.0),
-           "mean_length": l / max(k, 1.0), "deterministic": deterministic}
-    print(json.dumps(out))
     env.close()
+    out = {"steps": steps, "num_envs": n, "episodes": int(k), "mean_reward": r / max(k, 1.0),
+           "mean_length": l / max(k, 1.0), "deterministic": deterministic}
+    if video is not None:
+        out["video"] = video.saved
+    print(json.dumps(out))
     return out
 
 

@@ -375,6 +375,15 @@ def test_play_script_restores_trained_checkpoint(tmp_path):
     ckpt = os.path.join(nn_dir, sorted(os.listdir(nn_dir))[0])
     out = play.main(["--task", "Allsteps-v0", "--num_envs", "256", "--checkpoint", ckpt, "--steps", "200"])
     assert out["steps"] == 200 and out["episodes"] > 0 and math.isfinite(out["mean_reward"])
+    # --video (play.py:111-127): env 0's rgb_array frames from step 0, --video_length of them, then stop
+    from PIL import Image
+
+    out = play.main(["--task", "Allsteps-v0", "--num_envs", "64", "--checkpoint", ckpt, "--video",
+                     "--video_length", "24"])
+    assert out["steps"] == 24 and len(out["video"]) == 1
+    assert os.path.dirname(out["video"][0]) == os.path.join(os.path.dirname(nn_dir), "videos", "play")
+    im = Image.open(out["video"][0])
+    assert im.n_frames == 24 and im.size == (640, 360)
 
 
 @pytest.mark.gpu
