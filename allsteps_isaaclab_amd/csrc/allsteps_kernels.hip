@@ -82,12 +82,11 @@ union alignas(16) PhaseScratch {
     alignas(16) float cc[NST][4];  //   per candidate stone: its center relative to the root
   } col;
   struct alignas(16) {
-    // sweep: the pivot rows of a round (without the pivot columns).  Row stride 36 floats: the four
-    // pivot lanes' 16-B stores then start 4 banks apart (a 32-float stride put all four on the same
-    // four banks of ds_write_b128's (a/4) mod 32 banking: a 4-way conflict on every store)
-    float q[kSweepB][36];
-    float pb[kSweepB][kSweepB]; //        and the pivot block H_PP
-  } sw;                 // aliases d.c / d.Ib, dead by then
+    // sweep: every lane's (rotated) row, rewritten each round, so the publishing stores need no
+    // pivot-lane branch; rows are read by the next round's pivot indices.  Row stride 28 floats: the
+    // 8-lane groups of a ds_write_b128 then cover 8 distinct 4-bank quads
+    float rows[G][28];
+  } sw;                 // aliases the dynamics scratch, dead by then
   ConScratch k;
 };
 
@@ -833,47 +832,45 @@ __device__ __forceinline__ void block_inverse(float (&M)[B][B]) {  // M <- M^-1 
   }
 }
 
+// Software-pipelined and branch-free.  Every lane publishes its whole rotated row each round (no
+// pivot-lane branch: the sweep is one basic block, so the scheduler can interleave across rounds), and
+// its new leading quad -- the next round's pivot columns -- first: right after that store every lane
+// reads the next pivot block back and inverts it, and the 4x4 inverse's division chain overlaps the
+// round's remaining column updates instead of heading the next round.  Per element the operations
+// and their order are those of oracle/physics.c sweep_inverse: only the issue order changes.
 template <int NP, int B>
 __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
   static_assert(NP % B == 0, "padded order");
-  // unrolled over the 7 rounds: the column rotation is then register renaming (a rolled loop moved
-  // every row register back each round) and the pivot lanes / padding are known per round --
-  // 1.3 k instead of 2.0 k VALU instructions per sweep
+  static_assert(B == 4, "16-B pivot rows");
+  static_assert(NP <= 28, "row buffer stride");
+  // LDS operations of a wave complete in issue order: a round's stores cannot overtake the previous
+  // round's reads of the same rows.  Explicit 16-B accesses on a native 4-vector type (float4 is a
+  // struct whose copies SROA splits into b96 + b32 pairs)
+  float(*Rw)[28] = s.x.sw.rows;
+  v4f* own = reinterpret_cast<v4f*>(Rw[lane]);
+#pragma unroll
+  for (int j = 0; j < NP; j += 4) own[j / 4] = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
+  __syncthreads();
+  float D[B][B];
+#pragma unroll
+  for (int a = 0; a < B; ++a) {
+    const v4f d = *reinterpret_cast<const v4f*>(Rw[a]);
+    D[a][0] = d.x; D[a][1] = d.y; D[a][2] = d.z; D[a][3] = d.w;
+  }
+  block_inverse<B>(D);
+  // unrolled over the 7 rounds: the column rotation is then register renaming and the pivot lanes /
+  // padding are known per round
 #pragma unroll
   for (int p = 0; p < NP; p += B) {
-    // one buffer: LDS operations of a wave complete in issue order, so the next round's writes
-    // cannot overtake this round's reads
-    float(&Q)[kSweepB][36] = s.x.sw.q;
-    float(&Pb)[kSweepB][kSweepB] = s.x.sw.pb;
     const int t = lane - p;
     const bool piv = (unsigned)t < (unsigned)B;
-    // explicit 16-B LDS accesses on a native 4-vector type (float4 is a struct whose copies SROA
-    // splits; the stores then come out as b96 + b32 pairs whenever the rotated row does not sit in
-    // aligned register quads)
-    static_assert(B == 4, "16-B pivot rows");
-    if (piv) {
-      *reinterpret_cast<v4f*>(Pb[t]) = v4f{Hr[0], Hr[1], Hr[2], Hr[3]};
+    constexpr int NQ = NP / 4 - 1;  // column quads past the pivot columns
+    // the pivot rows' other columns (stored last round, or above for p = 0)
+    v4f x[NQ][B];
 #pragma unroll
-      for (int j = B; j < NP; j += 4) *reinterpret_cast<v4f*>(&Q[t][j]) = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
-    }
-    __syncthreads();
-    float D[B][B];
+    for (int jb = 0; jb < NQ; ++jb)
 #pragma unroll
-    for (int a = 0; a < B; ++a) {
-      const v4f d = *reinterpret_cast<const v4f*>(Pb[a]);
-      D[a][0] = d.x; D[a][1] = d.y; D[a][2] = d.z; D[a][3] = d.w;
-    }
-    // the first kPre (all) column blocks of the pivot rows are read before the block inverse, and the
-    // scheduling barrier keeps them there: their LDS latency runs under the inverse's division chain
-    // (left alone, the scheduler sinks every Q read below it)
-    constexpr int kPre = 6;
-    v4f qpre[kPre][B];
-#pragma unroll
-    for (int jb = 0; jb < kPre; ++jb)
-#pragma unroll
-      for (int c = 0; c < B; ++c) qpre[jb][c] = *reinterpret_cast<const v4f*>(&Q[c][B + 4 * jb]);
-    __builtin_amdgcn_sched_barrier(0);
-    block_inverse<B>(D);
+      for (int c = 0; c < B; ++c) x[jb][c] = *reinterpret_cast<const v4f*>(&Rw[p + c][B + 4 * jb]);
     // packed pairs written out (the file is built without the SLP vectorizer, which elsewhere paid
     // for its pairs with register moves); per element the same operations in the same order
     float alpha = 1.f, beta[B];
@@ -892,24 +889,40 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
       beta[c] = piv ? pv : v;
     }
     if (piv) alpha = 0.f;
+    float Dn[B][B];
 #pragma unroll
-    for (int j = B; j < NP; j += 4) {
-      v4f x[B];
-#pragma unroll
-      for (int c = 0; c < B; ++c) {
-        const int jb = (j - B) / 4;
-        x[c] = jb < kPre ? qpre[jb < kPre ? jb : 0][c] : *reinterpret_cast<const v4f*>(&Q[c][j]);
-      }
+    for (int jb = 0; jb < NQ; ++jb) {
+      const int j = B + 4 * jb;
       v2f lo = v2f{alpha, alpha} * v2f{Hr[j], Hr[j + 1]}, hi = v2f{alpha, alpha} * v2f{Hr[j + 2], Hr[j + 3]};
 #pragma unroll
       for (int c = 0; c < B; ++c) {
-        lo = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[c].xy, lo);
-        hi = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[c].zw, hi);
+        lo = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[jb][c].xy, lo);
+        hi = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[jb][c].zw, hi);
       }
       Hr[j - B] = lo.x; Hr[j + 1 - B] = lo.y; Hr[j + 2 - B] = hi.x; Hr[j + 3 - B] = hi.y;
+      if (jb == 0 && p + B < NP) {
+        // the next round's pivot block: published, read back and inverted under the rest of the round
+        own[0] = v4f{lo.x, lo.y, hi.x, hi.y};
+        __builtin_amdgcn_wave_barrier();  // one wave: the store above reaches LDS before these reads
+#pragma unroll
+        for (int a = 0; a < B; ++a) {
+          const v4f d = *reinterpret_cast<const v4f*>(Rw[p + B + a]);
+          Dn[a][0] = d.x; Dn[a][1] = d.y; Dn[a][2] = d.z; Dn[a][3] = d.w;
+        }
+        block_inverse<B>(Dn);
+      }
     }
 #pragma unroll
     for (int c = 0; c < B; ++c) Hr[NP - B + c] = beta[c];
+    if (p + B < NP) {
+#pragma unroll
+      for (int j = B; j < NP; j += 4) own[j / 4] = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int a = 0; a < B; ++a)
+#pragma unroll
+        for (int c = 0; c < B; ++c) D[a][c] = Dn[a][c];
+    }
   }
   __syncthreads();
 }
