@@ -62,8 +62,11 @@ struct DynScratch {
     float Rl[LMAX][12]; // FK: local joint transforms (R 9, p 3); dead before cr / f are written
     struct {
       float cr[LMAX][6];  // V_i x_m S_i qd_i
-      float f[LMAX][6];   // body forces of the RNEA
     } b;
+    // subtree sums: body force (6) and spatial inertia (10) of every link, transposed and split by
+    // link parity ([quantity][l & 1][l >> 1]: the MFMA's A operand runs, read as 16-B vectors),
+    // written after the last read of cr
+    alignas(16) float xt[16][2][LMAX / 2];
   };
 };
 struct alignas(16) ConScratch {
@@ -570,13 +573,31 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
   __syncthreads();
 }
 
+// Two-block f32 MFMA (v_mfma_f32_32x32x1_2b_f32): one 32 x 32 block per env (block b = lanes
+// 32b..32b+31), K = 1 per instruction, lane l supplying A[l % 32][k] and B[k][l % 32] of its own env;
+// the result is bit for bit an fmaf chain over k (scripts/probes/mfma_2b_probe.hip).  Register v of
+// block b holds row 8(v/4) + 4h + v%4 on lane half h, column lane % 32; one v_permlane32_swap per
+// register pair (blocks 0 and 1 trade halves) leaves lane n with column n of its own env's block.
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+__device__ __forceinline__ void mfma_columns(const f32x32& acc, float (&col)[32]) {
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(acc[v]), __float_as_int(acc[16 + v]), false, false);
+    const int r0 = 8 * (v >> 2) + (v & 3);
+    col[r0] = __int_as_float(p[0]);
+    col[r0 + 4] = __int_as_float(p[1]);
+  }
+}
+
 // RNEA bias forces (qdd = 0) and composite inertias by path / subtree walks (lanes = links):
 //   V_i  = V_0 + sum_{l on path, root->i} S_l qd_l            (= V_parent + S_i qd_i)
 //   A_i  = A_0 + sum_{l on path} V_l x_m S_l qd_l             (= A_parent + V_i x S_i qd_i)
 //   f_i  = I_i A_i + V_i x_f I_i V_i - gravity wrench
-//   F_i  = f_i + sum_{l in subtree(i), l > i, ascending} f_l  (non-root links), likewise Ic_i
-//   F_0  = f_0 + sum_{children c of the root, ascending} F_c, likewise Ic_0
-// (oracle/physics.c uses the same summation orders).  Then per dof j: C_j = S_j . F_link(j),
+//   F_i  = sum_{l in subtree(i) (i included), ascending} f_l,  likewise Ic_i from the I_l
+// The subtree sums are one matrix product per env on the matrix cores: with X the 16 x LMAX table of
+// every link's (f, I) and M_il = [l in subtree(i)], the two-block f32 MFMA forms (X M^T) over LMAX K
+// steps, an fmaf chain over l ascending from +0 for every (quantity, link) -- the root's row is the
+// whole tree (oracle/physics.c subtree_sums restates the chain).  Then per dof j: C_j = S_j . F_link(j),
 // b_j = tau_j - C_j (returned, also in LDS), Fh_j = Ic_link(j) S_j.
 __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, const Topo& tp, float gravity,
                                           float (&Sj)[6], float (&Fj)[6]) {
@@ -607,12 +628,9 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
       for (int k = 0; k < 6; ++k) d.b.cr[lane][k] = cr[k];
     }
   }
-  if (lane == kZeroRow) {  // the walks' +0 rows (see take_bit_z); FK's Rl, which b aliases, is dead
+  if (lane == kZeroRow) {  // the walks' +0 row (see take_bit_z); FK's Rl, which b aliases, is dead
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      d.b.cr[kZeroRow][k] = 0.f;
-      d.b.f[kZeroRow][k] = 0.f;
-    }
+    for (int k = 0; k < 6; ++k) d.b.cr[kZeroRow][k] = 0.f;
   }
   __syncthreads();
   float f[6], Ib[10];
@@ -631,37 +649,53 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
       f[k] = IA[k] + x[k] - cxmg[k];
       f[3 + k] = IA[3 + k] + x[3 + k] - mg[k];
     }
+  }
+  // every link's (f, I) into the transposed table; links past nl (and the lanes up to LMAX) add +0
+  if (lane < LMAX) {
+    const bool lv = lane < nl;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) d.b.f[lane][k] = f[k];
+    for (int k = 0; k < 6; ++k) d.xt[k][lane & 1][lane >> 1] = lv ? f[k] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) d.xt[6 + k][lane & 1][lane >> 1] = lv ? Ib[k] : 0.f;
   }
   __syncthreads();
-  if (lane >= 1 && lane < nl) {
-    uint32_t sub = tp.lsub & ~(1u << lane);
-    constexpr int kSubU = 4;
-    for (int it = 0; it < K.max_sub; it += kSubU) {  // kSubU subtree links per iteration
-      int l[kSubU];
+  {
+    // Both envs in one single-block v_mfma_f32_32x32x2_f32 (K = 2 per instruction, an fmaf chain over
+    // its two K entries in order: scripts/probes/mfma_x2_probe.hip): row r = 16 env + quantity, column
+    // = link i, instruction t takes link slots 2t (lanes 0-31) and 2t + 1 (lanes 32-63).  A operand:
+    // lane l supplies X_env(r)[r % 16][2t + l / 32] (r = l % 32, the env's table in LDS); B operand:
+    // lane l supplies M_{i, 2t + l / 32}, i = l % 32.  D row r, column i sits at register v of lane
+    // half h with r = 8 (v / 4) + 4 h + v % 4: one v_permlane32_swap per register pair leaves lane
+    // (env e, link i) with its 16 sums.
+    const int tid = threadIdx.x, h = tid >> 5, r = tid & 31;
+    EnvS* envs = &s - h;  // sm.env[0]
+    const float* xr = envs[r >> 4].x.d.xt[r & 15][h];
+    float xa[LMAX / 2];
 #pragma unroll
-      for (int u = 0; u < kSubU; ++u) l[u] = take_bit_z(sub);
-      float fl[kSubU][6], Il[kSubU][10];
-#pragma unroll
-      for (int u = 0; u < kSubU; ++u) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) fl[u][k] = d.b.f[l[u]][k];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) Il[u][k] = d.Ib[l[u]][k];
-      }
-#pragma unroll
-      for (int u = 0; u < kSubU; ++u) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) f[k] += fl[u][k];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) Ib[k] += Il[u][k];
-      }
+    for (int t = 0; t < LMAX / 2; t += 4) {
+      const v4f v = *reinterpret_cast<const v4f*>(xr + t);
+      xa[t] = v.x; xa[t + 1] = v.y; xa[t + 2] = v.z; xa[t + 3] = v.w;
     }
+    const uint32_t sub = (lane < nl ? tp.lsub : 0u) >> h;
+    typedef float f32x16 __attribute__((ext_vector_type(16)));
+    f32x16 acc = {};
 #pragma unroll
-    for (int k = 0; k < 6; ++k) d.Sq[lane][k] = f[k];  // Sq is dead: F_i
+    for (int t = 0; t < LMAX / 2; ++t)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[t], (float)((sub >> (2 * t)) & 1u), acc, 0, 0, 0);
+    float col[16];
 #pragma unroll
-    for (int k = 0; k < 10; ++k) d.Ic[lane][k] = Ib[k];
+    for (int w = 0; w < 8; ++w) {
+      const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_int(acc[w]), __float_as_int(acc[8 + w]), false, false);
+      const int q0 = 8 * (w >> 2) + (w & 3);
+      col[q0] = __int_as_float(pr[0]);
+      col[q0 + 4] = __int_as_float(pr[1]);
+    }
+    if (lane < nl) {  // lane i: F_i (0..5), Ic_i (6..15)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) d.Sq[lane][k] = col[k];  // Sq is dead: F_i
+#pragma unroll
+      for (int k = 0; k < 10; ++k) d.Ic[lane][k] = col[6 + k];
+    }
   }
   __syncthreads();
   float bj = 0.f;
@@ -669,26 +703,10 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
     const int j = lane;
     const int link = j < 6 ? 0 : j - 5;
     float F[6], Ic[10], S[6];
-    if (link == 0) {
 #pragma unroll
-      for (int k = 0; k < 6; ++k) F[k] = d.b.f[0][k];
+    for (int k = 0; k < 6; ++k) F[k] = d.Sq[link][k];
 #pragma unroll
-      for (int k = 0; k < 10; ++k) Ic[k] = d.Ib[0][k];
-      uint32_t kids = K.root_kids;
-      while (kids) {
-        const int c = __builtin_ctz(kids);
-        kids &= kids - 1u;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) F[k] += d.Sq[c][k];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) Ic[k] += d.Ic[c][k];
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) F[k] = d.Sq[link][k];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) Ic[k] = d.Ic[link][k];
-    }
+    for (int k = 0; k < 10; ++k) Ic[k] = d.Ic[link][k];
 #pragma unroll
     for (int k = 0; k < 6; ++k) S[k] = s.S[j][k];
     const float Cj = dot6(S, F);
@@ -704,22 +722,6 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
   }
   __syncthreads();
   return bj;
-}
-
-// Two-block f32 MFMA (v_mfma_f32_32x32x1_2b_f32): one 32 x 32 block per env (block b = lanes
-// 32b..32b+31), K = 1 per instruction, lane l supplying A[l % 32][k] and B[k][l % 32] of its own env;
-// the result is bit for bit an fmaf chain over k (scripts/probes/mfma_2b_probe.hip).  Register v of
-// block b holds row 8(v/4) + 4h + v%4 on lane half h, column lane % 32; one v_permlane32_swap per
-// register pair (blocks 0 and 1 trade halves) leaves lane n with column n of its own env's block.
-typedef float f32x32 __attribute__((ext_vector_type(32)));
-__device__ __forceinline__ void mfma_columns(const f32x32& acc, float (&col)[32]) {
-#pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(acc[v]), __float_as_int(acc[16 + v]), false, false);
-    const int r0 = 8 * (v >> 2) + (v & 3);
-    col[r0] = __int_as_float(p[0]);
-    col[r0 + 4] = __int_as_float(p[1]);
-  }
 }
 
 // Row j of the joint-space inertia H (lane j):

@@ -85,20 +85,23 @@ static int is_ancestor(const or_model_t* m, int a, int l) {
   return l == a;
 }
 
-/* Subtree sums in the order of the HIP kernel (dynamics() in csrc/allsteps_kernels.hip, one lane per
- * link): a non-root link adds the values of its proper descendants, in ascending link index, to its
- * own value; the root adds the totals of its children, in ascending index, to its own. */
+/* Subtree sums as the HIP kernel's matrix product forms them (dynamics() in
+ * csrc/allsteps_kernels.hip: the two-block f32 MFMA over OR_SUBTREE_STEPS K steps, one per link
+ * slot): for every link i, one fmaf chain from +0 over the link slots l ascending,
+ * acc = fmaf(x_l, [l in subtree(i)], acc), with x_l = 0 past the model's links; subtree(i) includes
+ * i, and the root's is the whole tree. */
+#define OR_SUBTREE_STEPS 24 /* the kernel's kMaxLinks */
 static void subtree_sums(const or_model_t* m, int nl, int w, const float* own, float* tot) {
-  for (int i = 1; i < nl; ++i) {
-    for (int k = 0; k < w; ++k) tot[i * w + k] = own[i * w + k];
-    for (int l = i + 1; l < nl; ++l)
-      if (is_ancestor(m, i, l))
-        for (int k = 0; k < w; ++k) tot[i * w + k] += own[l * w + k];
-  }
-  for (int k = 0; k < w; ++k) tot[k] = own[k];
-  for (int c = 1; c < nl; ++c)
-    if (m->parent[c] == 0)
-      for (int k = 0; k < w; ++k) tot[k] += tot[c * w + k];
+  for (int i = 0; i < nl; ++i)
+    for (int k = 0; k < w; ++k) {
+      float acc = 0.f;
+      for (int l = 0; l < OR_SUBTREE_STEPS; ++l) {
+        const float x = l < nl ? own[l * w + k] : 0.f;
+        const float mk = l < nl && is_ancestor(m, i, l) ? 1.f : 0.f;
+        acc = fmaf(x, mk, acc);
+      }
+      tot[i * w + k] = acc;
+    }
 }
 
 /* FK + motion subspace + spatial inertias. q_int: hinge angles in link order (link i -> q_int[i-1]). */
