@@ -91,6 +91,8 @@ union alignas(16) PhaseScratch {
     float rows[G][28];
   } sw;                 // aliases the dynamics scratch, dead by then
   ConScratch k;
+  // contact flags: per contact lambda_n n (3) and its (foot, stone) key, written after the PGS
+  alignas(16) float cf[MAXC][4];
 };
 
 // The constants block is read-only for the whole launch: address space 4 (constant) lets uniform
@@ -133,7 +135,6 @@ struct EnvS {
   alignas(16) float S[NVMAX][12];
   float b[32];          // tau - C
   PhaseScratch x;
-  float rlam[MAXR];     // PGS impulses
   // per row: 1/A_rr, target, bound parameter, in-group coupling.  The bound parameter is what the
   // PGS needs of the row's group: on row 1 of a group mu for a contact triplet (0 otherwise), on
   // row 2 the upper-bound offset, 0 for a contact triplet (+-mu ln) and +inf otherwise ([0, inf))
@@ -141,7 +142,6 @@ struct EnvS {
   float cdir[MAXC][3][3];  // contact frame: normal, tangent 1, tangent 2
   int rlink[MAXR];      // contact rows: link | (link2 + 1) << 8 (link2 = -1: stone); limit rows: -1 - dof
   float rsign[MAXR];
-  float lamn[MAXC];     // normal impulses of the last PGS sweep (contact flags)
   float cpt[MAXC][3], cn[MAXC][3], csep[MAXC];
   int clink[MAXC], clink2[MAXC], cstone[MAXC], cfoot[MAXC];  // clink2 / cstone: -1 unless self / stone
   float u[NVMAX];
@@ -1252,20 +1252,23 @@ __device__ void tangents(const float* n, float* t1, float* t2) {
 }
 
 // Contact-sensor flag of lane c's contact (c < nce, a foot contact): |sum lambda_n n| / dt over the
-// contacts c2 < nce with its (foot, stone) pair, in ascending order; NC = the wave's larger nce.
+// contacts c2 < nce with its (foot, stone) pair, in ascending order; NC = the wave's larger nce.  Each
+// contact's products lambda_n n and its pair key come from one 16-B LDS row (EnvS::x.cf; the same
+// products the per-term form rounded; keys past nce never match), so a term is one read.
 template <int NC>
 __device__ __forceinline__ void contact_flag(const EnvS& s, int lane, int nce, float dt, uint32_t (&b)[4]) {
   static_assert(NC <= MAXC, "contacts");
   const int cl = lane < MAXC ? lane : 0;
   const int f = s.cfoot[cl], st = s.cstone[cl];
+  const int key = __float_as_int(s.x.cf[cl][3]);
   float fx = 0.f, fy = 0.f, fz = 0.f;
 #pragma unroll
   for (int c2 = 0; c2 < NC; ++c2) {
-    const bool same = c2 < nce && s.cfoot[c2] == f && s.cstone[c2] == st;
-    const float l = s.lamn[c2];
-    fx += same ? l * s.cn[c2][0] : 0.f;
-    fy += same ? l * s.cn[c2][1] : 0.f;
-    fz += same ? l * s.cn[c2][2] : 0.f;
+    const v4f v = *reinterpret_cast<const v4f*>(s.x.cf[c2]);
+    const bool same = __float_as_int(v.w) == key;
+    fx += same ? v.x : 0.f;
+    fy += same ? v.y : 0.f;
+    fz += same ? v.z : 0.f;
   }
   if (lane < nce && f >= 0 && sqrtf(fx * fx + fy * fy + fz * fz) / dt > 1e-4f) b[f & 3] = 1u << st;
 }
@@ -1634,13 +1637,20 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     case 10: pgs_sweeps<10>(s, iters, uj, lamr, Jc, Wc); break;
     default: break;
   }
-  float lam = 0.f;
-#pragma unroll
-  for (int r = 0; r < MAXR; ++r) lam = lane == r ? lamr[r] : lam;
-  if (lane < MAXR) s.rlam[lane] = lane < maxrow ? lam : 0.f;
-  __syncthreads();
+  // contact c's normal impulse (row 3c; every lane of an env holds all its impulses) times its normal,
+  // and its (foot, stone) key, one 16-B row per contact for the flags; contacts past the solved
+  // normal rows (nce) get a key no contact has
+  const int nce = min(nc, (nrow + kRowGroup - 1) / kRowGroup);  // contacts whose normal row was solved
   if (lane < NV) s.u[lane] = uj;
-  if (lane < MAXC) s.lamn[lane] = 3 * lane < nrow ? s.rlam[3 * lane] : 0.f;
+  if (lane < MAXC) {
+    float ln = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) ln = lane == c ? lamr[3 * c] : ln;
+    ln = 3 * lane < nrow ? ln : 0.f;
+    const int key = lane < nce ? ((s.cfoot[lane] + 1) << 8) | (s.cstone[lane] + 1) : -1;
+    *reinterpret_cast<v4f*>(s.x.cf[lane]) =
+        v4f{ln * s.cn[lane][0], ln * s.cn[lane][1], ln * s.cn[lane][2], __int_as_float(key)};
+  }
   __syncthreads();
   ts.mark(kStPGS);
   // ---- contact-sensor flags of this substep (force_matrix_w = impulse / dt, > eps): lane c sums
@@ -1650,7 +1660,6 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     // (one instantiation per wave-uniform contact count, the sum unrolled so all its reads issue at
     // once; the terms past an env's own count add +0 to a sum that is never -0: the same bits)
     uint32_t b[4] = {0u, 0u, 0u, 0u};
-    const int nce = min(nc, (nrow + kRowGroup - 1) / kRowGroup);  // contacts whose normal row was solved
     const int ncw = max(__builtin_amdgcn_readlane(nce, 0), __builtin_amdgcn_readlane(nce, 32));
     switch (ncw) {
       case 1: contact_flag<1>(s, lane, nce, dt, b); break;
