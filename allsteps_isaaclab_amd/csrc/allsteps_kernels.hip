@@ -1657,64 +1657,53 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   //      lambda_n n over the contacts with its (foot, stone) pair in ascending order, and the
   //      per-foot stone bits are OR-reduced over the half-wave
   {
-    // (one instantiation per wave-uniform contact count, the sum unrolled so all its reads issue at
-    // once; the terms past an env's own count add +0 to a sum that is never -0: the same bits)
+    // All MAXC terms (one 16-B read each; the terms past an env's own count add +0 to a sum that is
+    // never -0: the same bits) and no per-count dispatch: the flags, the hind-feet masks (zero for a
+    // biped) and the root update below are one basic block, so the scheduler interleaves the root
+    // update's serial chain with the flag sums.
     uint32_t b[4] = {0u, 0u, 0u, 0u};
-    const int ncw = max(__builtin_amdgcn_readlane(nce, 0), __builtin_amdgcn_readlane(nce, 32));
-    switch (ncw) {
-      case 1: contact_flag<1>(s, lane, nce, dt, b); break;
-      case 2: contact_flag<2>(s, lane, nce, dt, b); break;
-      case 3: contact_flag<3>(s, lane, nce, dt, b); break;
-      case 4: contact_flag<4>(s, lane, nce, dt, b); break;
-      case 5: contact_flag<5>(s, lane, nce, dt, b); break;
-      case 6: contact_flag<6>(s, lane, nce, dt, b); break;
-      case 7: contact_flag<7>(s, lane, nce, dt, b); break;
-      case 8: contact_flag<8>(s, lane, nce, dt, b); break;
-      case 9: contact_flag<9>(s, lane, nce, dt, b); break;
-      case 10: contact_flag<10>(s, lane, nce, dt, b); break;
-      default: break;
-    }
+    contact_flag<MAXC>(s, lane, nce, dt, b);
     half_or2(b[0], b[1]);
-    mask_out[0] = b[0];
-    mask_out[1] = b[1];
-    if (K.st_has_hind) {  // wave-uniform: only a state with the hind-feet masks (quadruped)
-      half_or2(b[2], b[3]);
-      mask_out[2] = b[2];
-      mask_out[3] = b[3];
-    }
+    half_or2(b[2], b[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mask_out[k] = b[k];
   }
-  // ---- integrate
+  // ---- integrate.  The root update is formed by every lane of the env (no lane-0 branch; the
+  //      small-angle case by selects, the same values) and stored by lane 0
+  float rq[4], rp[3];
+  {
+    const float* u = s.u;
+    float c0w[3];
+    for (int k = 0; k < 3; ++k) c0w[k] = fmaf(dt, u[k], s.root_pos[k] + s.c0[k]);
+    const float* w = u + 3;
+    const float wn = sqrtf(dot3(w, w));
+    const float th = wn * dt;
+    float sn, cs;
+    as_sincosf(0.5f * th, &sn, &cs);
+    const float sc = sn / wn;
+    const bool big = th > 1e-12f;
+    const float dq[4] = {big ? cs : 1.f, big ? w[0] * sc : 0.5f * dt * w[0], big ? w[1] * sc : 0.5f * dt * w[1],
+                         big ? w[2] * sc : 0.5f * dt * w[2]};
+    const float* q0 = s.root_quat;
+    float nq[4] = {dq[0] * q0[0] - dq[1] * q0[1] - dq[2] * q0[2] - dq[3] * q0[3],
+                   dq[0] * q0[1] + dq[1] * q0[0] + dq[2] * q0[3] - dq[3] * q0[2],
+                   dq[0] * q0[2] - dq[1] * q0[3] + dq[2] * q0[0] + dq[3] * q0[1],
+                   dq[0] * q0[3] + dq[1] * q0[2] - dq[2] * q0[1] + dq[3] * q0[0]};
+    const float qn = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+    for (int k = 0; k < 4; ++k) rq[k] = nq[k] * qn;
+    float Rn[9], cl[3];
+    quat_to_mat(rq, Rn);
+    matvec3(Rn, m.com[0], cl);
+    for (int k = 0; k < 3; ++k) rp[k] = c0w[k] - cl[k];
+  }
   if (lane < nh) {
     float v = fminf(fmaxf(s.u[6 + lane], -K.sim.max_joint_vel), K.sim.max_joint_vel);
     s.u[6 + lane] = v;
     s.qi[lane] = fmaf(dt, v, s.qi[lane]);
   }
   if (lane == 0) {
-    const float* u = s.u;
-    float c0w[3];
-    for (int k = 0; k < 3; ++k) c0w[k] = fmaf(dt, u[k], s.root_pos[k] + s.c0[k]);
-    const float* w = u + 3;
-    float wn = sqrtf(dot3(w, w));
-    float th = wn * dt, dq[4];
-    if (th > 1e-12f) {
-      float sn, cs;
-      as_sincosf(0.5f * th, &sn, &cs);
-      float sc = sn / wn;
-      dq[0] = cs; dq[1] = w[0] * sc; dq[2] = w[1] * sc; dq[3] = w[2] * sc;
-    } else {
-      dq[0] = 1.f; dq[1] = 0.5f * dt * w[0]; dq[2] = 0.5f * dt * w[1]; dq[3] = 0.5f * dt * w[2];
-    }
-    const float* q0 = s.root_quat;
-    float nq[4] = {dq[0] * q0[0] - dq[1] * q0[1] - dq[2] * q0[2] - dq[3] * q0[3],
-                   dq[0] * q0[1] + dq[1] * q0[0] + dq[2] * q0[3] - dq[3] * q0[2],
-                   dq[0] * q0[2] - dq[1] * q0[3] + dq[2] * q0[0] + dq[3] * q0[1],
-                   dq[0] * q0[3] + dq[1] * q0[2] - dq[2] * q0[1] + dq[3] * q0[0]};
-    float qn = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
-    for (int k = 0; k < 4; ++k) s.root_quat[k] = nq[k] * qn;
-    float Rn[9], cl[3];
-    quat_to_mat(s.root_quat, Rn);
-    matvec3(Rn, m.com[0], cl);
-    for (int k = 0; k < 3; ++k) s.root_pos[k] = c0w[k] - cl[k];
+    for (int k = 0; k < 4; ++k) s.root_quat[k] = rq[k];
+    for (int k = 0; k < 3; ++k) s.root_pos[k] = rp[k];
   }
   __syncthreads();
   ts.mark(kStIntegrate);
