@@ -82,8 +82,9 @@ def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int 
         "mini_epochs": agent.mini_epochs_num, "s_per_epoch": round(wall / len(t), 4),
         "play_s": round(sum(x[1] for x in t) / len(t), 4), "update_s": round(sum(x[2] for x in t) / len(t), 4),
         "mixed_precision": agent.mixed_precision, "hip_graphs": agent._play_graphs is not None,
-        "precision": "bf16 MLP trunk on MFMA (fp32 accumulate), fp32 heads / losses / Adam / normalisers; "
-                     "rl_games' mixed_precision=True is fp16 autocast (DESIGN.md §7)",
+        "precision": (("fp16" if agent.mixed_precision_dtype == torch.float16 else "bf16") if agent.mixed_precision
+                      else "fp32") + " MLP trunk on MFMA (fp32 accumulate), fp32 heads / losses / Adam / normalisers, "
+                     "device-side GradScaler (rl_games mixed_precision=True: fp16 autocast; DESIGN.md §7)",
         "data": "synthetic (random-init policy, reference reset distribution)"}
 
 
