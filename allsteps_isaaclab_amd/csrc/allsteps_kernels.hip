@@ -442,6 +442,11 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
     matvec3(Roff, t, tmp);
     for (int k = 0; k < 3; ++k) d.Rl[i][9 + k] = tmp[k] + lc.op[k];
   }
+  if (lane == kZeroRow) {  // the path walk's identity row (the RNEA's +0 row of b.cr, which aliases
+                           // Rl, is written after the walk)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) d.Rl[kZeroRow][k] = k == 0 || k == 4 || k == 8 ? 1.f : 0.f;
+  }
   __syncthreads();
   float R0[9];
   quat_to_mat(s.root_quat, R0);
@@ -456,14 +461,16 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
       P[k] = v2f{R0[k], R0[3 + k]};
       r2[k] = R0[6 + k];
     }
-    // kPathU path links per iteration: their local transforms are loaded before the products
+    // kPathU path links per iteration: their local transforms are loaded before the products.  An
+    // exhausted path reads the identity transform of row kZeroRow (written above): every lane composes
+    // the same padded number of transforms, with no per-link selects (oracle/physics.c kinematics
+    // composes the same identity pads)
     constexpr int kPathU = 4;
     uint32_t path = tp.lpath & ~1u;
     for (int it = 0; it < K.max_path; it += kPathU) {
-      bool v[kPathU];
       int l[kPathU];
 #pragma unroll
-      for (int u = 0; u < kPathU; ++u) l[u] = take_bit(path, v[u]);
+      for (int u = 0; u < kPathU; ++u) l[u] = take_bit_z(path);
       float Tl[kPathU][12];
 #pragma unroll
       for (int u = 0; u < kPathU; ++u)
@@ -485,13 +492,12 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
                                                   __builtin_elementwise_fma(P[1], v2f{T[10], T[10]},
                                                                             P[0] * v2f{T[9], T[9]}));
         const float wp2 = fmaf(r2[2], T[11], fmaf(r2[1], T[10], r2[0] * T[9]));
-        const v2f ps = pp + wpp;
-        pp = v2f{v[u] ? ps.x : pp.x, v[u] ? ps.y : pp.y};
-        p2 = v[u] ? p2 + wp2 : p2;
+        pp = pp + wpp;
+        p2 = p2 + wp2;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          P[j] = v2f{v[u] ? Pn[j].x : P[j].x, v[u] ? Pn[j].y : P[j].y};
-          r2[j] = v[u] ? r2n[j] : r2[j];
+          P[j] = Pn[j];
+          r2[j] = r2n[j];
         }
       }
     }

@@ -41,6 +41,7 @@ typedef struct {
   float S[NV_MAX][6];        /* motion subspace [w; v_O] per dof */
   float Ic[OR_MAX_LINKS][10];/* spatial inertia at O: m, h(3), Io(6) (xx yy zz xy xz yz) */
   float Ib[OR_MAX_LINKS][10];/* single-body spatial inertia at O */
+  float c0[3];               /* root COM from the root quaternion's matrix (root columns, velocities) */
 } kin_t;
 
 /* The primitives of the shared float32 arithmetic specification (include/as_detmath.h): explicit
@@ -104,29 +105,59 @@ static void subtree_sums(const or_model_t* m, int nl, int w, const float* own, f
     }
 }
 
-/* FK + motion subspace + spatial inertias. q_int: hinge angles in link order (link i -> q_int[i-1]). */
+/* Compositions of the kernel's FK path walk (fk in csrc/allsteps_kernels.hip): every link composes
+ * 4 * ceil(max_path / 4) transforms, its own path's (root excluded, ascending) and then identities. */
+static int fk_walk_len(const or_model_t* m) {
+  int mp = 0;
+  for (int i = 1; i < m->num_links; ++i) {
+    int d = 0;
+    for (int l = i; l > 0; l = m->parent[l]) ++d;
+    if (d > mp) mp = d;
+  }
+  return (mp + 3) / 4 * 4;
+}
+
+/* FK + motion subspace + spatial inertias. q_int: hinge angles in link order (link i -> q_int[i-1]).
+ * Link i's pose is the kernel's path walk: R = R_root, p = 0, then for each transform (R_l, t_l) on the
+ * path root -> i (ascending), padded with identities to fk_walk_len: p += R t_l, R = R R_l. */
 static void kinematics(const or_model_t* m, const float root_quat[4], const float* q_int, kin_t* K) {
   const int nl = m->num_links;
   K->nl = nl;
   K->nv = OR_NDOF_ROOT + m->num_hinges;
-  quat_to_mat(root_quat, K->R[0]);
-  K->p[0][0] = K->p[0][1] = K->p[0][2] = 0.f;
+  float R0[9];
+  quat_to_mat(root_quat, R0);
+  float Rl[OR_MAX_LINKS][9], tl[OR_MAX_LINKS][3];
   for (int i = 1; i < nl; ++i) {
-    int pa = m->parent[i];
-    float Roff[9], Rj[9], Rl[9], t[3], Ro[3], tmp[3];
+    float Roff[9], Rj[9], t[3], Ro[3];
     quat_to_mat(m->offset_quat[i], Roff);
     axis_angle_mat(m->axis[i], q_int[i - 1], Rj);
-    matmul3(Roff, Rj, Rl);
+    matmul3(Roff, Rj, Rl[i]);
     /* joint translation t_j = o - Rj o; local origin = offset_pos + Roff t_j */
     matvec3(Rj, m->anchor[i], Ro);
     for (int k = 0; k < 3; ++k) t[k] = m->anchor[i][k] - Ro[k];
-    matvec3(Roff, t, tmp);
-    for (int k = 0; k < 3; ++k) tmp[k] += m->offset_pos[i][k];
-    matmul3(K->R[pa], Rl, K->R[i]);
-    float wp[3];
-    matvec3(K->R[pa], tmp, wp);
-    for (int k = 0; k < 3; ++k) K->p[i][k] = K->p[pa][k] + wp[k];
+    matvec3(Roff, t, tl[i]);
+    for (int k = 0; k < 3; ++k) tl[i][k] += m->offset_pos[i][k];
   }
+  const float I3[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f}, Z3[3] = {0.f, 0.f, 0.f};
+  const int wl = fk_walk_len(m);
+  for (int i = 0; i < nl; ++i) {
+    int chain[OR_MAX_LINKS], n = 0;
+    for (int l = i; l > 0; l = m->parent[l]) chain[n++] = l;  /* deepest first */
+    float R[9], p[3] = {0.f, 0.f, 0.f};
+    memcpy(R, R0, sizeof(R));
+    for (int st = 0; st < wl; ++st) {
+      const float* T = st < n ? Rl[chain[n - 1 - st]] : I3;
+      const float* t = st < n ? tl[chain[n - 1 - st]] : Z3;
+      float wp[3], Rn[9];
+      matvec3(R, t, wp);
+      for (int k = 0; k < 3; ++k) p[k] = p[k] + wp[k];
+      matmul3(R, T, Rn);
+      memcpy(R, Rn, sizeof(R));
+    }
+    memcpy(K->R[i], R, sizeof(R));
+    memcpy(K->p[i], p, sizeof(p));
+  }
+  matvec3(R0, m->com[0], K->c0);
   for (int i = 0; i < nl; ++i) {
     float cw[3];
     matvec3(K->R[i], m->com[i], cw);
@@ -152,8 +183,8 @@ static void kinematics(const or_model_t* m, const float root_quat[4], const floa
     B[8] = Iw[2] - mass * c[0] * c[2];
     B[9] = Iw[5] - mass * c[1] * c[2];
   }
-  /* motion subspace */
-  const float* c0 = K->c[0];
+  /* motion subspace (root columns from the root quaternion's COM, as the kernel's s.c0) */
+  const float* c0 = K->c0;
   for (int k = 0; k < 3; ++k) {
     float* Sl = K->S[k];
     float* Sa = K->S[3 + k];
@@ -224,7 +255,7 @@ static void crba(const or_model_t* m, const kin_t* K, float* H) {
 }
 
 static void link_velocities(const or_model_t* m, const kin_t* K, const float* u, float V[][6]) {
-  const float* c0 = K->c[0];
+  const float* c0 = K->c0;
   float wxc[3];
   cross(c0, u + 3, wxc);
   for (int k = 0; k < 3; ++k) { V[0][k] = u[3 + k]; V[0][3 + k] = u[k] + wxc[k]; }
@@ -779,7 +810,7 @@ static void substep(const or_model_t* m, const or_sim_t* sim, const or_actuator_
     q_int[i] = fmaf(dt, *v, q_int[i]);
   }
   float c0w[3];
-  for (int k = 0; k < 3; ++k) c0w[k] = fmaf(dt, u[k], root_pos[k] + K.c[0][k]);
+  for (int k = 0; k < 3; ++k) c0w[k] = fmaf(dt, u[k], root_pos[k] + K.c0[k]);
   const float* w = u + 3;
   float wn = sqrtf(dot3(w, w));
   float th = wn * dt, dq[4];
