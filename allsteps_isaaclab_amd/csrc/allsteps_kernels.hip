@@ -1522,13 +1522,10 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     }
     ++slot;
   }
-  const int nrow = crow + nlim;
-  if (lane == 0) s.nrow = nrow;
+  const int nrow = crow + nlim;  // uniform over the env's half-wave
   ts.count(nrow, nc);
-  __syncthreads();
-  if (threadIdx.x == 0) sm.maxrow = max(sm.env[0].nrow, sm.env[1].nrow);
-  __syncthreads();
-  const int maxrow = sm.maxrow;
+  const int maxrow = max(__builtin_amdgcn_readlane(nrow, 0), __builtin_amdgcn_readlane(nrow, 32));
+  __syncthreads();  // the row metadata above, for the J build
   // Issue priority by constraint load: the two waves of a SIMD are arbitrated by priority, then
   // age, so a contact-heavy wave that happens to be the younger one would get only the leftover
   // issue slots and set the launch's tail.  The heavier wave of the pair takes precedence for the
