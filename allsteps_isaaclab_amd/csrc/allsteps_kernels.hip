@@ -152,7 +152,6 @@ struct EnvS {
   float stones[NST * 3];
   float root_pos[3], root_quat[4];
   int cand[NST];
-  int ncand, ncontact, nrow;
   uint32_t mask[4];     // contact sensors 0..3 (2, 3: a quadruped's hind feet)
 };
 
@@ -978,7 +977,7 @@ __device__ __forceinline__ GeomC load_geom(const Consts& K, int lane) {
 //   1. the priority geoms (the feet: geoms [0, num_priority_geoms)) against the candidate stones,
 //      stone-major, geom-minor;  2. every other geom against the candidate stones, likewise;
 //   3. robot self-contacts, one per self-collision pair in table order.
-__device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane, int ncap, const GeomC& gc) {
+__device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int ncap, const GeomC& gc) {
   const as_model_t& m = K.model;
   const float* h = K.sim.stone_half;
   const float margin = K.sim.margin;
@@ -1244,8 +1243,7 @@ __device__ __forceinline__ void collide(const Consts& K, EnvS& s, int lane, int 
     if (pend > 0 && base < ncap) flush_self(pend);
   }
   __syncthreads();
-  if (lane == 0) s.ncontact = base < ncap ? base : ncap;
-  __syncthreads();
+  return base < ncap ? base : ncap;  // uniform over the env's half-wave
 }
 
 __device__ void tangents(const float* n, float* t1, float* t2) {
@@ -1486,9 +1484,9 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   const int lpos = half_scan3(lo_v + hi_v, ltotal);
   const int nlim = ltotal < MAXR ? ltotal : MAXR;
   const int ncap = (MAXR - nlim) / 3 < MAXC ? (MAXR - nlim) / 3 : MAXC;
-  collide(K, s, lane, ncap, gc);
+  const int nc = collide(K, s, lane, ncap, gc);
   ts.mark(kStCollide);
-  const int nc = s.ncontact;
+
   if (lane < nc) {  // contact rows 3c..3c+2: normal, tangent 1, tangent 2
     float t1[3], t2[3];
     tangents(s.cn[lane], t1, t2);
