@@ -675,13 +675,19 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
     const int tid = threadIdx.x, h = tid >> 5, r = tid & 31;
     EnvS* envs = &s - h;  // sm.env[0]
     const float* xr = envs[r >> 4].x.d.xt[r & 15][h];
-    float xa[LMAX / 2];
-#pragma unroll
-    for (int t = 0; t < LMAX / 2; t += 4) {
-      const v4f v = *reinterpret_cast<const v4f*>(xr + t);
-      xa[t] = v.x; xa[t + 1] = v.y; xa[t + 2] = v.z; xa[t + 3] = v.w;
-    }
     const uint32_t sub = (lane < nl ? tp.lsub : 0u) >> h;
+    float xa[LMAX / 2];
+    // the three 16-B reads issued together and passed through an empty asm (one wait): left to the
+    // scheduler, each read reused the previous one's registers and waited under the MFMA chain
+    static_assert(LMAX / 2 == 12, "three quads");
+    v4f xq[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) xq[t] = *reinterpret_cast<const v4f*>(xr + 4 * t);
+    asm volatile("" : "+v"(xq[0]), "+v"(xq[1]), "+v"(xq[2]));
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      xa[4 * t] = xq[t].x; xa[4 * t + 1] = xq[t].y; xa[4 * t + 2] = xq[t].z; xa[4 * t + 3] = xq[t].w;
+    }
     typedef float f32x16 __attribute__((ext_vector_type(16)));
     f32x16 acc = {};
 #pragma unroll
@@ -1196,15 +1202,29 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   };
   // all filter tests first (their LDS reads overlap), then the list is appended to without a
   // barrier per word (LDS operations of the single wave complete in issue order)
+  // Every lane reads both spheres of every word (a word past nsp reads geom 0's twice: spw = 0) and
+  // the reads are passed through an empty asm, four words at a time: each batch waits once.  (With
+  // `pv && test` the compiler put each word's reads behind a branch on pv and waited on them word by
+  // word: one LDS latency per word.)
   uint32_t hbl[kSelfW];
+  static_assert(kSelfW % 4 == 0, "batches of four words");
 #pragma unroll
-  for (int i = 0; i < kSelfW; ++i) {
-    const bool pv = G * i + lane < nsp;
-    const int g1 = spw[i] & 0xff, g2 = spw[i] >> 8;
-    const v4f s1 = *reinterpret_cast<const v4f*>(s.x.col.bs[g1]);
-    const v4f s2 = *reinterpret_cast<const v4f*>(s.x.col.bs[g2]);
-    const float m1[3] = {s1.x, s1.y, s1.z}, m2[3] = {s2.x, s2.y, s2.z};
-    hbl[i] = (uint32_t)(__ballot(pv && as_sphere_bound(m1, s1.w, m2, s2.w, margin)) >> (32 * half));
+  for (int i0 = 0; i0 < kSelfW; i0 += 4) {
+    v4f s1[4], s2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s1[i] = *reinterpret_cast<const v4f*>(s.x.col.bs[spw[i0 + i] & 0xff]);
+      s2[i] = *reinterpret_cast<const v4f*>(s.x.col.bs[spw[i0 + i] >> 8]);
+    }
+    asm volatile("" : "+v"(s1[0]), "+v"(s1[1]), "+v"(s1[2]), "+v"(s1[3]), "+v"(s2[0]), "+v"(s2[1]), "+v"(s2[2]),
+                 "+v"(s2[3]));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool pv = G * (i0 + i) + lane < nsp;
+      const float m1[3] = {s1[i].x, s1[i].y, s1[i].z}, m2[3] = {s2[i].x, s2[i].y, s2[i].z};
+      const bool hit = as_sphere_bound(m1, s1[i].w, m2, s2[i].w, margin);
+      hbl[i0 + i] = (uint32_t)(__ballot(pv & hit) >> (32 * half));
+    }
   }
   // The survivors' list positions in table order (word-major, lane-minor) by prefix counts, and all
   // of them written at once when neither env has more than the list holds (64; a random-action run
@@ -1266,9 +1286,18 @@ __device__ __forceinline__ void contact_flag(const EnvS& s, int lane, int nce, f
   const int f = s.cfoot[cl], st = s.cstone[cl];
   const int key = __float_as_int(s.x.cf[cl][3]);
   float fx = 0.f, fy = 0.f, fz = 0.f;
+  // all rows read first and passed through an empty asm, so that one wait covers every read (left to
+  // the scheduler, each read was issued only when the previous term's registers freed: one LDS latency
+  // per term)
+  v4f t[NC];
+#pragma unroll
+  for (int c2 = 0; c2 < NC; ++c2) t[c2] = *reinterpret_cast<const v4f*>(s.x.cf[c2]);
+  static_assert(NC == 10, "operand list below");
+  asm volatile("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]),
+               "+v"(t[8]), "+v"(t[9]));
 #pragma unroll
   for (int c2 = 0; c2 < NC; ++c2) {
-    const v4f v = *reinterpret_cast<const v4f*>(s.x.cf[c2]);
+    const v4f v = t[c2];
     const bool same = __float_as_int(v.w) == key;
     fx += same ? v.x : 0.f;
     fy += same ? v.y : 0.f;
@@ -1314,10 +1343,14 @@ __device__ __forceinline__ void w_rows(EnvS& s, int lane, int nrow, const float*
   const int jc = lane < NV ? lane : NV;  // column NV is +0 in the J image
 #pragma unroll
   for (int r = 0; r < MAXR; ++r) Jc[r] = M[r][jc];
+  // (an empty volatile asm orders memory operations: the J column reads issue here, and their latency
+  // hides under the MFMA chain instead of heading the barrier below)
+  float j0 = Jr[0].x;  // the MFMA chain's first operand, through the asm: the chain starts after it
+  asm volatile("" : "+v"(j0));
   f32x32 acc = {};
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    const float jk = k & 1 ? Jr[k >> 1].y : Jr[k >> 1].x;
+    const float jk = k == 0 ? j0 : k & 1 ? Jr[k >> 1].y : Jr[k >> 1].x;
     acc = __builtin_amdgcn_mfma_f32_32x32x1f32(jk, Hr[k], acc, 0, 0, 0);
   }
   float wr[32];
@@ -1372,20 +1405,30 @@ __device__ __forceinline__ void pgs_sweeps(const EnvS& s, int iters, float& uj, 
                                            const float (&Jc)[MAXR], const float (&Wc)[MAXR]) {
   typedef __attribute__((address_space(3))) const v4f* lds_v4p;
   lds_v4p meta = (lds_v4p)(&s.rmeta[0][0]);
+  // Software-pipelined metadata: group g+1's three rows are read at the head of group g (between two
+  // empty volatile asm statements, which order memory operations: the reads issue before group g's
+  // reductions start) and consumed after group g+1's reductions, so the LDS latency is hidden by a
+  // whole group.  Reading them at the head of their own group left each group waiting on the read
+  // (its destination registers were reused as soon as the unused lane-0 bound field died).  The row
+  // metadata is the same in every sweep, so the last group reads group 0 for the next sweep.
+  v4f n0 = meta[0], n1 = meta[1], n2 = meta[2];
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
-    float uprev = uj;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int r = kRowGroup * g;
-      // the group's metadata reads are pinned behind the previous group's start (its u): one
-      // group of reads ahead, none hoisted out of the sweep loop (30 rows would not fit).  The pin
-      // is on the LDS row pointer itself, so the reads keep immediate offsets (no address VALU).
-      asm volatile("" : "+v"(meta) : "v"(uprev));
-      uprev = uj;
-      const v4f m0 = meta[r];
-      const v4f m1 = meta[r + 1];
-      const v4f m2 = meta[r + 2];
+      // the group's rows pass through the asm: no use of them is hoisted into the previous group
+      // (where it would wait on the read), and every field's register -- m0.z too, a bound that row 0
+      // of a group never uses -- stays allocated to the read until the read has landed
+      v4f m0 = n0, m1 = n1, m2 = n2;
+      asm volatile("" : "+v"(meta), "+v"(uj), "+v"(m0), "+v"(m1), "+v"(m2));
+      {
+        const int rn = g + 1 < NG ? r + kRowGroup : 0;
+        n0 = meta[rn];
+        n1 = meta[rn + 1];
+        n2 = meta[rn + 2];
+      }
+      asm volatile("" : "+v"(uj));
       float vg[3] = {Jc[r] * uj, Jc[r + 1] * uj, Jc[r + 2] * uj};
       half_sum_n(vg);
       // t_s = lambda_s + (target_s - v_s - sum_{r<s} A_sr dl_r) x_s, with the parts that do not
@@ -1554,6 +1597,13 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       P[k] = s.cpt[c][k];
       f6[3 + k] = s.cdir[c][u][k];
     }
+    // lane j's motion-subspace row for the MFMA below, read with the row metadata; the empty volatile
+    // asm orders memory operations, so these reads issue before the path-mask reads that depend on lk
+    // (one LDS latency for both instead of one after the other)
+    const int jo = lane < NV ? lane : 0;
+    const v4f s0 = *reinterpret_cast<const v4f*>(&s.S[jo][0]);
+    const v4f s1 = *reinterpret_cast<const v4f*>(&s.S[jo][4]);
+    asm volatile("");
     cross3(P, f6 + 3, f6);
     const bool con = lk >= 0;
     const int l2 = (lk >> 8) - 1;
@@ -1567,9 +1617,6 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
     // after the column shuffle lane r holds its row's products for every dof
     float Pj[32];
     {
-      const int jo = lane < NV ? lane : 0;
-      const v4f s0 = *reinterpret_cast<const v4f*>(&s.S[jo][0]);
-      const v4f s1 = *reinterpret_cast<const v4f*>(&s.S[jo][4]);
       const float z = lane < NV ? 1.f : 0.f;
       const float Sa[6] = {s0.x * z, s0.y * z, s0.z * z, s0.w * z, s1.x * z, s1.y * z};
       f32x32 acc = {};
