@@ -421,7 +421,7 @@ __device__ __forceinline__ LinkC load_link(const Consts& K, int lane) {
 }
 
 template <bool kDyn>
-__device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Topo& tp, LinkC lc) {
+__device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Topo& tp, LinkC lc, int max_path) {
   const as_model_t& m = K.model;
   const int nl = m.num_links;
   DynScratch& d = s.x.d;
@@ -466,7 +466,7 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
     // composes the same identity pads)
     constexpr int kPathU = 4;
     uint32_t path = tp.lpath & ~1u;
-    for (int it = 0; it < K.max_path; it += kPathU) {
+    for (int it = 0; it < max_path; it += kPathU) {
       int l[kPathU];
 #pragma unroll
       for (int u = 0; u < kPathU; ++u) l[u] = take_bit_z(path);
@@ -605,7 +605,7 @@ __device__ __forceinline__ void mfma_columns(const f32x32& acc, float (&col)[32]
 // whole tree (oracle/physics.c subtree_sums restates the chain).  Then per dof j: C_j = S_j . F_link(j),
 // b_j = tau_j - C_j (returned, also in LDS), Fh_j = Ic_link(j) S_j.
 __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, const Topo& tp, float gravity,
-                                          float (&Sj)[6], float (&Fj)[6]) {
+                                          float (&Sj)[6], float (&Fj)[6], int max_path) {
   const as_model_t& m = K.model;
   const int nl = m.num_links, nv = K.nv;
   DynScratch& d = s.x.d;
@@ -623,7 +623,7 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
     }
   }
   if (lane < nl) {
-    path_sum<6, 4>(tp.lpath & ~1u, K.max_path, V, d.Sq);
+    path_sum<6, 4>(tp.lpath & ~1u, max_path, V, d.Sq);
     if (lane > 0) {
       float Sq[6], cr[6];
 #pragma unroll
@@ -640,7 +640,7 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
   __syncthreads();
   float f[6], Ib[10];
   if (lane < nl) {
-    path_sum<6, 4>(tp.lpath & ~1u, K.max_path, A, d.b.cr);
+    path_sum<6, 4>(tp.lpath & ~1u, max_path, A, d.b.cr);
 #pragma unroll
     for (int k = 0; k < 10; ++k) Ib[k] = d.Ib[lane][k];
     float IA[6], IV[6], x[6];
@@ -983,10 +983,9 @@ __device__ __forceinline__ GeomC load_geom(const Consts& K, int lane) {
 //   1. the priority geoms (the feet: geoms [0, num_priority_geoms)) against the candidate stones,
 //      stone-major, geom-minor;  2. every other geom against the candidate stones, likewise;
 //   3. robot self-contacts, one per self-collision pair in table order.
-__device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int ncap, const GeomC& gc) {
+__device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int ncap, const GeomC& gc, const float* h,
+                                       float margin) {
   const as_model_t& m = K.model;
-  const float* h = K.sim.stone_half;
-  const float margin = K.sim.margin;
   const int nst = K.task.num_steps, ng = m.num_geoms, npri = m.num_priority_geoms, nsp = m.num_self_pairs;
   // self-collision pair words of this lane (pairs lane, lane + 32, ...), loaded first so that their
   // latency hides behind the stone contacts
@@ -1478,15 +1477,22 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   const as_model_t& m = K.model;
   const float dt = K.sim.dt;
   const int nh = m.num_hinges;
+  // Scalars of the model loaded in groups just ahead of the phases that use them, each group passed
+  // through an empty asm: one wait per group instead of a scalar load and a wait beside each use (a
+  // wait on the scalar loads also waits on every LDS read in flight, so each one exposed an LDS
+  // latency too).  Short live ranges: held across the whole substep they pushed the epilogue's SGPRs
+  // into spills.
+  int smp = K.max_path;
+  asm volatile("" : "+s"(smp));
   if (K.act.mode == AS_ACT_DC_MOTOR && lane < nh) {  // the actuator runs in every substep (lane = hinge)
     const as_actuator_t& A = K.act;
     s.tau[lane] = as_dc_motor(s.qt[lane], s.qi[lane], s.u[6 + lane], A.stiffness, A.damping, A.saturation_effort,
                               A.effort_limit, A.velocity_limit);
   }
-  fk<true>(K, s, lane, tp, lc);  // (its first barrier publishes tau before the dynamics read it)
+  fk<true>(K, s, lane, tp, lc, smp);  // (its first barrier publishes tau before the dynamics read it)
   ts.mark(kStFK);
   float Sj[6], Fj[6];  // dof lane j: S_j and Ic_link(j) S_j for the H rows
-  dynamics(K, s, lane, tp, K.sim.gravity, Sj, Fj);
+  dynamics(K, s, lane, tp, K.sim.gravity, Sj, Fj, smp);
   ts.mark(kStLinkQ);
   constexpr int NP = (NV + kSweepB - 1) / kSweepB * kSweepB;  // sweep order, padded with identity
   float Hr[NP];
@@ -1527,7 +1533,10 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   const int lpos = half_scan3(lo_v + hi_v, ltotal);
   const int nlim = ltotal < MAXR ? ltotal : MAXR;
   const int ncap = (MAXR - nlim) / 3 < MAXC ? (MAXR - nlim) / 3 : MAXC;
-  const int nc = collide(K, s, lane, ncap, gc);
+  float sb = K.sim.baumgarte, ssl = K.sim.slop, smd = K.sim.max_depen_vel, sfr = K.sim.friction, smg = K.sim.margin;
+  float sh[3] = {K.sim.stone_half[0], K.sim.stone_half[1], K.sim.stone_half[2]};
+  asm volatile("" : "+s"(sb), "+s"(ssl), "+s"(smd), "+s"(sfr), "+s"(smg), "+s"(sh[0]), "+s"(sh[1]), "+s"(sh[2]));
+  const int nc = collide(K, s, lane, ncap, gc, sh, smg);
   ts.mark(kStCollide);
 
   if (lane < nc) {  // contact rows 3c..3c+2: normal, tangent 1, tangent 2
@@ -1542,10 +1551,10 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       s.rlink[r] = lk;
       s.rsign[r] = 0.f;
       // one division for both branches: (sp < 0 ? min(b max(-sp - slop, 0) / dt, vmax) : -sp / dt)
-      const float num = sp < 0.f ? K.sim.baumgarte * fmaxf(-sp - K.sim.slop, 0.f) : -sp;
+      const float num = sp < 0.f ? sb * fmaxf(-sp - ssl, 0.f) : -sp;
       const float tv = num / dt;
-      s.rmeta[r][1] = d == 0 ? (sp < 0.f ? fminf(tv, K.sim.max_depen_vel) : tv) : 0.f;
-      s.rmeta[r][2] = d == 1 ? K.sim.friction : 0.f;
+      s.rmeta[r][1] = d == 0 ? (sp < 0.f ? fminf(tv, smd) : tv) : 0.f;
+      s.rmeta[r][2] = d == 1 ? sfr : 0.f;
     }
   }
   const int crow = 3 * nc;
@@ -1557,8 +1566,8 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
       float err = sd == 0 ? err_lo : err_hi;
       s.rlink[slot] = -1 - (6 + lane);
       s.rsign[slot] = sd == 0 ? 1.f : -1.f;
-      const float tv = (err > 0.f ? K.sim.baumgarte * err : err) / dt;  // one division, both branches
-      s.rmeta[slot][1] = err > 0.f ? fminf(tv, K.sim.max_depen_vel) : tv;
+      const float tv = (err > 0.f ? sb * err : err) / dt;  // one division, both branches
+      s.rmeta[slot][1] = err > 0.f ? fminf(tv, smd) : tv;
       s.rmeta[slot][2] = slot % 3 == 2 ? __builtin_inff() : 0.f;
     }
     ++slot;
@@ -1869,7 +1878,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   if (do_physics) {
     const GeomC gc = load_geom(K, lane);
     for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, gc, lc, mask, ts);
-    fk<false>(K, s, lane, tp, lc);  // FK of the final pose for body_pos_w (articulation_data.py:439)
+    fk<false>(K, s, lane, tp, lc, K.max_path);  // FK of the final pose for body_pos_w (articulation_data.py:439)
     if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; s.mask[2] = mask[2]; s.mask[3] = mask[3]; }
   }
   ts.mark(kStFKFinal);
@@ -2022,7 +2031,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       episode += 1u;
     }
     __syncthreads();
-    fk<false>(K, s, lane, tp, lc);  // body_pos of the reset pose (write_joint_state_to_sim invalidates FK)
+    fk<false>(K, s, lane, tp, lc, K.max_path);  // body_pos of the reset pose (write_joint_state_to_sim invalidates FK)
     if (done) {
       const int ls[3] = {m.torso_link, m.foot_link[0], m.foot_link[1]};
       for (int b = 0; b < 3; ++b)
