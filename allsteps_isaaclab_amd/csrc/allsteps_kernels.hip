@@ -1878,10 +1878,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   if (do_physics) {
     const GeomC gc = load_geom(K, lane);
     for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, gc, lc, mask, ts);
+  }
+  // This lane's reset constants (joint `lane` in cfg order: its link and limits, the start pose plain and
+  // mirrored), loaded ahead of the final FK so that their global loads (L2 round trips) run under it
+  // instead of heading the reset (the memory clobber keeps them there, not sunk into the reset
+  // branch); the limits then come from the tree plan in LDS.  The task's reward and the observation
+  // use the same link and limits.
+  int rs_li = 1, rs_src = lane;
+  float rs_q = 0.f, rs_qm = 0.f, rs_sg = 1.f, rs_lo = 0.f, rs_hi = 0.f;
+  {
+    // the mirror map through the constant address space (uniform: scalar loads, all issued together),
+    // applied by selects in the reference's order (the later match wins, as the sequential ifs)
+    const __attribute__((address_space(4))) as_task_t* Tc = &((CK*)P.consts)->task;
+    int rmap[9], lmap[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) { rmap[t] = Tc->right_idx[t]; lmap[t] = Tc->left_idx[t]; }
+    const int ng0 = Tc->neg_idx[0], ng1 = Tc->neg_idx[1];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      rs_src = rmap[t] == lane ? lmap[t] : rs_src;
+      rs_src = lmap[t] == lane ? rmap[t] : rs_src;
+    }
+    rs_sg = ng0 == lane || ng1 == lane ? -1.f : 1.f;
+    if (lane < nh) {
+      rs_q = T.init_q[lane] * 1.f;
+      rs_qm = T.init_q[rs_src] * rs_sg;
+      rs_li = m.cfg_dof_link[lane];
+    }
+  }
+  asm volatile("" ::: "memory");
+  if (do_physics) {
     fk<false>(K, s, lane, tp, lc, K.max_path);  // FK of the final pose for body_pos_w (articulation_data.py:439)
     if (lane == 0) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; s.mask[2] = mask[2]; s.mask[3] = mask[3]; }
   }
   ts.mark(kStFKFinal);
+  if (lane < nh) {  // m.lower / upper[li] as copied into the tree plan (Topo: hinge li - 1 is link li)
+    rs_lo = sm.topo[rs_li - 1].lo;
+    rs_hi = sm.topo[rs_li - 1].hi;
+  }
   if (lane == 0 && !do_physics) { s.mask[0] = mask[0]; s.mask[1] = mask[1]; }
   __syncthreads();
   float bp[9];
@@ -1908,11 +1942,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     float a2 = 0.f, en = 0.f;
     int atlim = 0;
     if (lane < nh) {
-      int li = m.cfg_dof_link[lane];
+      const int li = rs_li;
       float a = s.act[lane];
       a2 = a * a;
       en = fabsf(s.u[6 + li - 1] * a);
-      atlim = fabsf(scale_transform(s.qi[li - 1], m.lower[li], m.upper[li])) > 0.99f;
+      atlim = fabsf(scale_transform(s.qi[li - 1], rs_lo, rs_hi)) > 0.99f;
     }
     a2 = half_sum(a2);
     en = half_sum(en);
@@ -1999,21 +2033,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       if (mirror) swing ^= 1;
       if (lane < nh) {
         // joint `lane` (cfg order): running-start pose, mirrored, noise, clip (allsteps_env.py:505-560)
-        int src = lane;
-        float sign = 1.f;
-        if (mirror) {
-          for (int t = 0; t < 9; ++t) {
-            if (T.right_idx[t] == lane) src = T.left_idx[t];
-            if (T.left_idx[t] == lane) src = T.right_idx[t];
-          }
-          if (T.neg_idx[0] == lane || T.neg_idx[1] == lane) sign = -1.f;
-        }
-        float jp = T.init_q[src] * sign;
+        // (the mirror map, start pose and limits were loaded ahead: rs_*)
+        const float sign = mirror ? rs_sg : 1.f;
+        float jp = mirror ? rs_qm : rs_q;
         float jv = 0.f * sign;
-        int li = m.cfg_dof_link[lane];
+        int li = rs_li;
         float x = jp + (dn * (T.noise_hi - T.noise_lo) + T.noise_lo);
-        float sc = fminf(fmaxf(scale_transform(x, m.lower[li], m.upper[li]), T.clip_lo), T.clip_hi);
-        s.qi[li - 1] = unscale_transform(sc, m.lower[li], m.upper[li]);
+        float sc = fminf(fmaxf(scale_transform(x, rs_lo, rs_hi), T.clip_lo), T.clip_hi);
+        s.qi[li - 1] = unscale_transform(sc, rs_lo, rs_hi);
         s.u[6 + li - 1] = jv;
       }
       if (lane < 3) {
@@ -2063,8 +2090,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       ob[49] = fc2[1];
     }
     if (lane < nh) {
-      const int li = m.cfg_dof_link[lane];
-      ob[6 + lane] = scale_transform(s.qi[li - 1], m.lower[li], m.upper[li]);
+      const int li = rs_li;
+      ob[6 + lane] = scale_transform(s.qi[li - 1], rs_lo, rs_hi);
       ob[27 + lane] = fminf(fmaxf(s.u[6 + li - 1] * T.dof_vel_scale, -5.f), 5.f);
     }
     if (lane < 6) {  // lanes 0-2: targets after the second tick, lanes 3-5: after the first
@@ -2106,7 +2133,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     if (lane < 4) st.root_quat[lane * n + e] = s.root_quat[lane];
     if (lane < nh) {
-      int i = m.cfg_dof_link[lane] - 1;
+      int i = rs_li - 1;
       st.q[lane * n + e] = s.qi[i];
       st.qd[lane * n + e] = s.u[6 + i];
     }
