@@ -1,6 +1,9 @@
 """Learning-curve run of the full stack (native env + PPO trainer) on one GPU: the reference agent
 config, N envs, E epochs; prints per-epoch mean episode reward / length / curriculum target index as
-JSON lines (the evidence that physics + task + trainer learn together)."""
+JSON lines (the evidence that physics + task + trainer learn together).
+
+    python scripts/train_curve.py [num_envs] [epochs] [every] [task]   (task: Allsteps-v0 or
+    Allsteps-AnymalC-v0, the C5 quadruped behind the same env surface)"""
 import json
 import os
 import sys
@@ -17,6 +20,7 @@ from allsteps_isaaclab_amd.learning import a2c_continuous as A  # noqa: E402
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 E = int(sys.argv[2]) if len(sys.argv) > 2 else 300
 EVERY = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+TASK = sys.argv[4] if len(sys.argv) > 4 else "Allsteps-v0"
 orig = A.A2CAgent.train_epoch
 t0 = time.perf_counter()
 
@@ -25,11 +29,12 @@ def logged(self):
     out = orig(self)
     if self.epoch_num % EVERY == 0 or self.epoch_num == 1:
         uw = self._uw if getattr(self, "_uw", None) is not None else self.vec_env.env.unwrapped
+        ti = uw.curr_target_index if hasattr(uw, "curr_target_index") else uw.target_index
         rec = {"epoch": self.epoch_num, "frames": self.frame + self.curr_frames, "wall_s": round(time.perf_counter() - t0, 2),
                "mean_reward": round(float(self.game_rewards.mean.reshape(-1)[0]), 3),
                "mean_length": round(float(self.game_lengths.mean.reshape(-1)[0]), 1),
-               "mean_target_index": round(float(uw.curr_target_index.float().mean()), 3),
-               "max_target_index": int(uw.curr_target_index.max()),
+               "mean_target_index": round(float(ti.float().mean()), 3),
+               "max_target_index": int(ti.max()),
                "curriculum": int(uw.state["curriculum"][0]), "lr": float(self.lr), "kl": round(float(out[4]["kl"]), 5)}
         print(json.dumps(rec), flush=True)
     return out
@@ -41,5 +46,5 @@ with open(os.devnull, "w") as dn:
 
     with contextlib.redirect_stdout(sys.stderr):
         pass
-train.main(["--task", "Allsteps-v0", "--num_envs", str(N), "--max_iterations", str(E), "--seed", "42",
+train.main(["--task", TASK, "--num_envs", str(N), "--max_iterations", str(E), "--seed", "42",
             "--log_root", "/tmp/curve_logs"])
