@@ -628,18 +628,35 @@ __global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
 constexpr int kNormBlocks = 256;
 constexpr int kAdamThreads = 256;
 
-__global__ void __launch_bounds__(256) k_sqnorm(const float* __restrict__ g, int64_t n, float* __restrict__ partials) {
-    __shared__ float red[256 / kWave];
-    float s = 0.f;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
-        s += __builtin_isfinite(g[i]) ? g[i] * g[i] : __builtin_inff();  // a non-finite grad: inf (found_inf)
+// block partials of ||g / scale||^2 (partials[b]; NaN / inf propagate as in torch's vector_norm) and
+// of the non-finite element count (partials[gridDim.x + b]: GradScaler's found_inf, an OR over
+// isfinite(g[i]) -- kept apart from the norm so a finite gradient whose square sum overflows is
+// clipped, not skipped).  The scale is a power of two, so g / scale is exact.
+__global__ void __launch_bounds__(256) k_sqnorm(const float* __restrict__ g, int64_t n, const float* __restrict__ scaler,
+                                                float* __restrict__ partials) {
+    __shared__ float red[2][256 / kWave];
+    const float inv_scale = scaler ? 1.f / scaler[0] : 1.f;
+    float s = 0.f, bad = 0.f;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+        const float x = g[i] * inv_scale;
+        s += x * x;
+        bad += __builtin_isfinite(g[i]) ? 0.f : 1.f;
+    }
     s = wave_sum(s);
-    if (threadIdx.x % kWave == 0) red[threadIdx.x / kWave] = s;
+    bad = wave_sum(bad);
+    if (threadIdx.x % kWave == 0) {
+        red[0][threadIdx.x / kWave] = s;
+        red[1][threadIdx.x / kWave] = bad;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        float t = 0.f;
-        for (int w = 0; w < 256 / kWave; ++w) t += red[w];
+        float t = 0.f, b = 0.f;
+        for (int w = 0; w < 256 / kWave; ++w) {
+            t += red[0][w];
+            b += red[1][w];
+        }
         partials[blockIdx.x] = t;
+        partials[gridDim.x + blockIdx.x] = b;
     }
 }
 
@@ -655,24 +672,35 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
                                                        float b1, float b2, float eps, SegTable segs,
                                                        uint16_t* __restrict__ mirror, int mirror_dtype,
                                                        const float* __restrict__ scaler) {
-    __shared__ float red[kAdamThreads / kWave];
+    __shared__ float red[2][kAdamThreads / kWave];
     __shared__ float coef_s, step_size_s, bc2_sqrt_s, inv_scale_s;
     __shared__ int skip_s;
-    float s = 0.f;
-    for (int k = threadIdx.x; k < nnp; k += kAdamThreads) s += np[k];
+    float s = 0.f, bad = 0.f;
+    for (int k = threadIdx.x; k < nnp; k += kAdamThreads) {
+        s += np[k];
+        bad += np[nnp + k];
+    }
     s = wave_sum(s);
-    if (threadIdx.x % kWave == 0) red[threadIdx.x / kWave] = s;
+    bad = wave_sum(bad);
+    if (threadIdx.x % kWave == 0) {
+        red[0][threadIdx.x / kWave] = s;
+        red[1][threadIdx.x / kWave] = bad;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        float t = 0.f;
-        for (int w = 0; w < kAdamThreads / kWave; ++w) t += red[w];
-        // GradScaler: grads carry the loss scale (a power of two); a non-finite one skips the step
-        // (scaler.step), otherwise they are unscaled exactly before the clip (scaler.unscale_)
-        const float inv_scale = scaler ? 1.f / scaler[0] : 1.f;
-        skip_s = scaler && !__builtin_isfinite(t);
-        inv_scale_s = inv_scale;
-        // torch.nn.utils.clip_grad_norm_: coef = max_norm / (total_norm + 1e-6), clamped to 1
-        coef_s = max_norm > 0.f ? fminf(max_norm / (sqrtf(t) * inv_scale + 1e-6f), 1.f) : 1.f;
+        float t = 0.f, b = 0.f;
+        for (int w = 0; w < kAdamThreads / kWave; ++w) {
+            t += red[0][w];
+            b += red[1][w];
+        }
+        // GradScaler: grads carry the loss scale (a power of two); a non-finite element skips the step
+        // (scaler.step's found_inf), otherwise they are unscaled exactly before the clip (unscale_)
+        inv_scale_s = scaler ? 1.f / scaler[0] : 1.f;
+        skip_s = scaler && b > 0.f;
+        // torch.nn.utils.clip_grad_norm_: coef = clamp(max_norm / (total_norm + 1e-6), max=1); the
+        // norm is of the unscaled grads (k_sqnorm); a NaN norm makes coef NaN (clamp keeps NaN)
+        const float c = max_norm / (sqrtf(t) + 1e-6f);
+        coef_s = max_norm > 0.f ? (c < 1.f || c != c ? c : 1.f) : 1.f;
         // bias corrections once per block (fp64 pow / sqrt are long instruction sequences)
         const double ts = *step_p + 1.0;
         step_size_s = float(*lr_p / (1.0 - pow(double(b1), ts)));
@@ -711,9 +739,9 @@ __global__ void k_tail(double* lr, const float* kl, float thr, double min_lr, do
     if (threadIdx.x != 0) return;
     bool skipped = false;
     if (scaler) {  // GradScaler.update: backoff 0.5 on a skipped step, growth 2 after growth_interval good ones
-        float t = 0.f;
-        for (int k = 0; k < nnp; ++k) t += np[k];
-        skipped = !__builtin_isfinite(t);
+        float b = 0.f;
+        for (int k = 0; k < nnp; ++k) b += np[nnp + k];  // k_sqnorm's non-finite counts
+        skipped = b > 0.f;
         if (skipped) {
             scaler[0] *= 0.5f;
             scaler[1] = 0.f;
@@ -902,8 +930,8 @@ int ppo_meter_update(const float* partials, int32_t nblk, float max_size, float*
 
 int ppo_sqnorm_blocks(void) { return kNormBlocks; }
 
-int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream) {
-    hipLaunchKernelGGL(k_sqnorm, dim3(kNormBlocks), dim3(256), 0, S(stream), g, n, partials);
+int ppo_sqnorm(const float* g, int64_t n, const float* scaler, float* partials, void* stream) {
+    hipLaunchKernelGGL(k_sqnorm, dim3(kNormBlocks), dim3(256), 0, S(stream), g, n, scaler, partials);
     return launched("k_sqnorm");
 }
 

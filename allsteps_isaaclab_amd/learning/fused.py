@@ -103,7 +103,7 @@ def load() -> C.CDLL:
     L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V, V]
     L.ppo_loss_finalize.argtypes = [V, I32, I32, I32, F32, V, V, V, V, V, V, V]
     L.ppo_elu_bwd.argtypes = [V, I32, V, I32, V, I32, I32, I32, V, V]
-    L.ppo_sqnorm.argtypes = [V, I64, V, V]
+    L.ppo_sqnorm.argtypes = [V, I64, V, V, V]
     L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32, V, V]
     L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V, V, I32, I32, V]
     L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
@@ -203,7 +203,7 @@ class FusedPPOUpdate:
         self.S = _split(B)
         self.loss_partials = torch.empty(L.ppo_loss_blocks(B), 2 * self.A + 1 + PPO_LOSS_NSTAT, device=dev)
         self.stat_partials = torch.empty(L.ppo_obs_stats_blocks(B) * 2 * 64, device=dev, dtype=torch.float64)
-        self.norm_partials = torch.empty(L.ppo_sqnorm_blocks(), device=dev)
+        self.norm_partials = torch.empty(2 * L.ppo_sqnorm_blocks(), device=dev)  # norm sums | non-finite counts
         self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stat_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stats = torch.zeros(agent.mini_epochs_num * self.n_mb + 1, PPO_LOSS_NSTAT, device=dev)
@@ -526,16 +526,16 @@ class FusedPPOUpdate:
     def _optimizer_step(self) -> None:
         L, s, ag, fl = self.L, self._stream(), self.agent, self.flat
         n = fl.numel
-        _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.norm_partials), s), "ppo_sqnorm")
+        _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.scaler), _p(self.norm_partials), s), "ppo_sqnorm")
         opt = ag.optimizer
         _check(L.ppo_adam(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
-                          _p(self.norm_partials), self.norm_partials.numel(),
+                          _p(self.norm_partials), self.norm_partials.numel() // 2,
                           ag.grad_norm if ag.truncate_grads else 0.0, _p(ag.lr), _p(opt.step_t), opt.beta1, opt.beta2,
                           opt.eps, self.segs, self.nseg, _p(self.mirror), self.dt_code if self.lp else 1,
                           _p(self.scaler), s), "ppo_adam")
         _check(L.ppo_tail(_p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr, self.max_lr,
                           _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), _p(self.scaler),
-                          _p(self.norm_partials), self.norm_partials.numel(), SCALER_GROWTH_INTERVAL, s), "ppo_tail")
+                          _p(self.norm_partials), self.norm_partials.numel() // 2, SCALER_GROWTH_INTERVAL, s), "ppo_tail")
 
     # ------------------------------------------------------------------ graphs
     def _run(self, key, fn) -> None:

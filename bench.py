@@ -10,9 +10,10 @@ episodes terminate and reset naturally inside the timed region.  Envs are sharde
 scaling, no collective in the step).  value = all ranks' env-steps / max-over-ranks wall time.
 
 Extra objects on the JSON line:
-  roofline     -- k_step (the dominant kernel): algorithmic bytes per launch / its average duration
-                  from HIP events recorded around every 10th launch of the timed region on its own
-                  stream (events on every launch would add their own launch gaps), vs 8 TB/s HBM;
+  roofline     -- k_step (the dominant kernel): algorithmic bytes per launch / its duration, the timed
+                  step's wall time less k_obs's HIP-event average (events recorded around every 10th
+                  launch on the env's stream; the k_step event average is reported beside it, see
+                  kernel_times), vs 8 TB/s HBM;
                   `latency`: per-wave cycle records of 20 launches after the timed region (mean /
                   slowest wave vs the launch span, the slowest wave's phases: scripts/stamps.py).
   cpu_baseline -- rank 0, N = 1: the CPU oracle (oracle/, a port of the same step) timed on this
@@ -83,6 +84,22 @@ def pmc_record(num_envs: int) -> dict:
         return {}
 
 
+def kernel_times(ms_per_step: float, k_ms: float, o_ms: float, launches: int) -> dict:
+    """Per-launch durations (ms) of the step's two kernels, from one clock the roofline can trust.
+
+    The HIP events around the sampled launches span each kernel plus its own dispatch, so the k_step
+    and k_obs event averages together exceed the wall time of an unprofiled step.  The
+    roofline therefore uses the wall clock: `k_step_ms` = ms_per_step - the k_obs event average, the
+    part of the timed step that is not k_obs (k_step + its launch gap; it never exceeds the step it
+    belongs to, so k_step_ms + k_obs_event_ms == ms_per_step).  The event average is kept beside it."""
+    n = max(launches, 1)
+    k_ev, o_ev = k_ms / n, o_ms / n
+    return {"k_step_ms": round(ms_per_step - o_ev, 5), "k_step_event_ms": round(k_ev, 5),
+            "k_obs_event_ms": round(o_ev, 5), "sampled_launches": launches,
+            "method": "k_step_ms = wall ms_per_step - k_obs HIP-event average (sampled launches); "
+                      "k_step_event_ms = HIP events around every 10th k_step launch (includes its dispatch)"}
+
+
 def measured_hbm_peak(device) -> float | None:
     """Achievable HBM GB/s of the in-tree STREAM-copy kernel (as_hbm_copy, 2 x 2 GiB buffers)."""
     from allsteps_isaaclab_amd import _native
@@ -113,11 +130,14 @@ def host_cpu() -> dict:
             "sockets": len(sockets) or None}
 
 
-def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int = 50,
-                 min_wall_s: float = 5.0, min_steps: int = 50, max_wall_s: float = 60.0) -> dict:
+def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int = 50, samples: int = 3,
+                 min_wall_s: float = 7.0, min_steps: int = 20, max_wall_s: float = 60.0) -> dict:
     """The oracle (CPU port of the same step) on the host cores, timed after `warm_steps` steps past the
-    from-reset transient (the falling start): at least `min_wall_s` of wall clock and `min_steps` steps
-    (so C3's 32768 envs get >= 50 steps), at most `max_wall_s`.
+    from-reset transient (the falling start), in `samples` back-to-back samples of at least `min_wall_s`
+    of wall clock and `min_steps` steps each (at most `max_wall_s`): >= 21 s of CPU work in all.  The
+    value is the median sample's rate; the spread (min, max) is reported beside it because the host's
+    other tenants share these cores (benchmark_non_rl.py:155-179 times one long run; three samples
+    make the noise visible instead).
 
     Threads: OMP_NUM_THREADS when set, else nproc.  On the GPU box OMP_NUM_THREADS is
     the job's CPU share per GPU (16) and is kept: nproc there counts every CPU of the host, which other
@@ -149,17 +169,26 @@ def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int
     acts = [rng.uniform(-1, 1, (n, 21)).astype(np.float32) for _ in range(4)]
     for t in range(warm_steps):  # past the from-reset transient: envs fall, reset, walk at random
         orc.env_step(st, acts[t % 4], nthreads=threads)
-    steps, t0 = 0, time.perf_counter()
-    while True:
-        orc.env_step(st, acts[steps % 4], nthreads=threads)
-        steps += 1
-        el = time.perf_counter() - t0
-        if (el >= min_wall_s and steps >= min_steps) or el >= max_wall_s:
-            break
-    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+    rates, total_steps, total_s, k = [], 0, 0.0, 0
+    for _ in range(samples):
+        steps, t0 = 0, time.perf_counter()
+        while True:
+            orc.env_step(st, acts[k % 4], nthreads=threads)
+            steps += 1
+            k += 1
+            el = time.perf_counter() - t0
+            if (el >= min_wall_s and steps >= min_steps) or el >= max_wall_s:
+                break
+        rates.append(n * steps / el)
+        total_steps += steps
+        total_s += el
+    med = float(np.median(rates))
+    return {"value": round(med, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "samples": [round(r, 1) for r in rates], "spread": round((max(rates) - min(rates)) / med, 4),
             "threads_from": why, "host": host,
-            "sample": f"oracle/ C port, {n} envs x {steps} steps (level {level}, U(-1,1) actions, timed after "
-                      f"{warm_steps} warm-up steps), OpenMP {threads} threads, {el:.2f} s wall"}
+            "sample": f"oracle/ C port, {n} envs, {samples} samples, {total_steps} steps in {total_s:.2f} s wall "
+                      f"(level {level}, U(-1,1) actions, timed after {warm_steps} warm-up steps), OpenMP {threads} "
+                      f"threads; value = median sample, spread = (max - min) / median"}
 
 
 def train_leg(args, world: int, rank: int, backend: str, device, timeout_s: float = 300.0) -> dict:
@@ -205,14 +234,66 @@ def train_leg(args, world: int, rank: int, backend: str, device, timeout_s: floa
         return {"error": f"train child printed no result line: {out[-300:]} {err[-300:]}"}
 
 
+def launcher_cmd(gpus: int, argv: list[str], port: int) -> list[str]:
+    """The one-process-per-GPU launch of this script (the reference's multi-GPU recipe,
+    docs/source/features/multi_gpu.rst:58, scripts/reinforcement_learning/rl_games/train.py:99-105):
+    torch.distributed.run on one node, rendezvous on 127.0.0.1, the same bench arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def self_launch(gpus: int, argv: list[str]) -> int:
+    """`python bench.py --gpus N` without a launcher: start torch.distributed.run as a CHILD process
+    (never exec: this parent has made no HIP call, and stays that way) and relay its output and exit
+    code.  The child's stdout is inherited, so rank 0's single JSON line is this command's line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.Popen(launcher_cmd(gpus, argv, port), env=env, cwd=ROOT)
+    try:
+        return p.wait()
+    except KeyboardInterrupt:
+        p.terminate()
+        return p.wait()
+
+
+def check_world(gpus: int, environ) -> tuple[int, str | None]:
+    """(world, error): the process group size the ranks will form, and why this invocation must not
+    run.  `--gpus` is the requested GPU count; under a launcher WORLD_SIZE must equal it, so a line
+    can never report a different GPU count than the one asked for."""
+    if gpus < 1:
+        return 0, f"bench: --gpus must be >= 1 (got {gpus})"
+    ws = environ.get("WORLD_SIZE")
+    if ws is None:
+        return gpus, None
+    if int(ws) != gpus:
+        return int(ws), (f"bench: WORLD_SIZE={ws} from the launcher but --gpus {gpus}; pass the same count to "
+                         f"both (or run `python bench.py --gpus N` and let it launch the N ranks itself)")
+    return gpus, None
+
+
 def main():
     args = parse()
+    world, err = check_world(args.gpus, os.environ)
+    if err:
+        print(err, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and world > 1:
+        sys.exit(self_launch(world, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; ALLSTEPS_DIST_BACKEND=gloo lets ranks share one GPU (the rehearsal in
     # tests/test_gpu_parity.py::test_bench_two_ranks_one_gpu), the default is RCCL ("nccl")
     backend = os.environ.get("ALLSTEPS_DIST_BACKEND", "nccl")
+    if backend == "nccl" and local >= torch.cuda.device_count():  # device_count() makes no HIP call
+        print(f"bench: rank {rank} needs GPU {local} but {torch.cuda.device_count()} are visible", file=sys.stderr,
+              flush=True)
+        sys.exit(2)
     device = torch.device(f"cuda:{local % max(torch.cuda.device_count(), 1) if backend == 'gloo' else local}")
     torch.cuda.set_device(device)
     if world > 1:
@@ -274,8 +355,8 @@ def main():
 
     if rank == 0:
         value = n * world * K / el
-        avg_k = k_ms / max(launches, 1) / 1e3  # s per k_step launch
-        achieved = K_STEP_BYTES * n / avg_k / 1e9
+        t = kernel_times(el / K * 1e3, k_ms, o_ms, launches)
+        achieved = K_STEP_BYTES * n / (t["k_step_ms"] / 1e3) / 1e9
         pmc = pmc_record(n)
         line = {
             "metric": BASELINE_METRIC,
@@ -297,9 +378,9 @@ def main():
                 "global_envs": n * world,
                 "parallelism": f"dp{world} (env shards, no collective in step)",
             },
-            "kernels_ms": {"k_step_avg": round(k_ms / max(launches, 1), 5),
-                           "k_obs_avg": round(o_ms / max(launches, 1), 5)},
+            "kernels_ms": t,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "duration_ms": t["k_step_ms"], "duration_method": t["method"],
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc.get("traffic_bytes_per_launch"),
                          "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/traffic_k_step.json)",
                          "kernel": "k_step", "bytes_per_env": K_STEP_BYTES,

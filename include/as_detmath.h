@@ -179,8 +179,10 @@ AS_HD float as_asinf(float s) {
 
 /* exp(x) for x <= 0 (the step reward's exp(-d / 0.25)): k = rint(x log2 e), r = x - k ln 2 in two
  * fmaf steps, a degree-6 polynomial for e^r on [-ln2/2, ln2/2], scaled by 2^k (ldexpf, exact for the
- * normal results kept here); x < -87 (e^x below the normal range) gives +0 */
+ * normal results kept here); x < -87 (e^x below the normal range) gives +0; NaN passes through
+ * (a float-to-int of NaN differs between the device and x86, so it must never reach ldexpf) */
 AS_HD float as_expf(float x) {
+  if (!(x == x)) return x;
   if (x < -87.0f) return 0.0f;
   const float k = rintf(x * 1.44269504088896341f);
   float r = fmaf(-k, 0.693359375f, x);

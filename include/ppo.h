@@ -202,13 +202,15 @@ int ppo_rollout_post(const float* reward, const uint8_t* done, const uint8_t* ti
 /* meters: mean[3] (reward, shaped reward, length), size[3] (current_size) */
 int ppo_meter_update(const float* partials, int32_t nblk, float max_size, float* mean3, float* size3, void* stream);
 
-/* ||g||^2 partials (fp32, nblk = ppo_sqnorm_blocks()); a non-finite g makes its partial +inf */
+/* partials[2 * nblk] (fp32, nblk = ppo_sqnorm_blocks()): [0, nblk) block sums of (g / scale)^2 (scaler
+ * NULL: scale 1; NaN / inf propagate into the norm as in torch), [nblk, 2 nblk) block counts of
+ * non-finite g (GradScaler's found_inf: an OR over isfinite, separate from the norm) */
 int ppo_sqnorm_blocks(void);
-int ppo_sqnorm(const float* g, int64_t n, float* partials, void* stream);
+int ppo_sqnorm(const float* g, int64_t n, const float* scaler, float* partials, void* stream);
 /* clip (max_norm > 0: g *= min(1, max_norm / (||g|| + 1e-6))) + Adam (torch.optim.Adam, amsgrad off,
  * weight_decay 0) with device lr / step (fp64); writes the mirror (mirror_dtype PPO_DT_BF16 / PPO_DT_F16)
  * of the listed segments.  scaler (device fp32 [scale, growth tracker], NULL = none): the gradients
- * carry the loss scale -- a non-finite norm skips the whole update (GradScaler.step), otherwise
+ * carry the loss scale -- a non-finite element skips the whole update (GradScaler.step), otherwise
  * g / scale (exact: a power of two) is what is clipped and applied (GradScaler.unscale_) */
 int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials, int32_t nblk_norm,
              float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,

@@ -6,7 +6,7 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
-T=${TAG:-r03d}
+T=${TAG:-r04}
 mkdir -p gpurun_out
 echo "== gpu suite"; date
 bash scripts/gpu_tests.sh || exit $?
@@ -15,6 +15,8 @@ echo "== C2 profiles"; date
 TAG=$T bash scripts/prof_all.sh || exit $?
 cp gpurun_out/prof_$T/trace/run_kernel_stats.csv gpurun_out/${T}_kernel_stats.csv
 cp gpurun_out/prof_$T/traffic_k_step.json gpurun_out/${T}_traffic_k_step.json
+# the bench lines below read profiles/traffic_k_step.json: refresh it from THIS tree's PMC passes first
+cp gpurun_out/prof_$T/traffic_k_step.json profiles/traffic_k_step.json
 cp gpurun_out/prof_$T/ablate.log gpurun_out/${T}_ablate.log
 echo "== C3 profiles"; date
 NUM_ENVS=32768 BENCH_ARGS="--num-envs 32768 --level 9" STEPS=30 TAG=${T}_c3 bash scripts/profile.sh \

@@ -267,6 +267,63 @@ def test_fused_loss_scaler_skips_and_grows(tmp_path):
 
 
 @pytest.mark.gpu
+def test_fused_loss_scaler_clips_finite_overflowing_norm(tmp_path):
+    """found_inf is an OR over isfinite(g), not a test of the norm: finite scaled gradients whose
+    squared sum overflows fp32 (||g|| * scale > 1.8e19) are unscaled, clipped and applied like
+    torch's GradScaler + clip_grad_norm_ would, and the scale keeps growing (no skip)."""
+    _, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path)
+    fus.fused.use_graphs = False
+    fus.fused.begin_epoch()
+    fus.fused.step_a(True)
+    torch.cuda.synchronize()
+    p0 = fus.flat.params.clone()
+    m0 = fus.optimizer.exp_avg.clone()
+    step0 = float(fus.optimizer.step_t)
+    scale = float(fus.scaler_state[0])
+    tracker = float(fus.scaler_state[1])
+    good = fus.flat.grads.clone()
+    good[3] = 3e19  # finite; its square overflows fp32, its unscaled square does not
+    assert torch.isinf((good * good).sum())
+    fus.flat.grads.copy_(good)
+    lr0 = fus.lr.clone()
+    fus.fused.step_b()
+    torch.cuda.synchronize()
+    assert float(fus.optimizer.step_t) == step0 + 1
+    assert float(fus.scaler_state[0]) == scale and float(fus.scaler_state[1]) == tracker + 1
+    ref = fus.flat.params.clone()
+    assert torch.isfinite(ref).all()
+    fus.flat.params.copy_(p0)
+    fus.optimizer.exp_avg.copy_(m0)
+    fus.optimizer.exp_avg_sq.zero_()
+    fus.optimizer.step_t.fill_(step0)
+    fus.lr.copy_(lr0)
+    g = good / scale
+    if fus.truncate_grads:
+        g = g * torch.clamp(fus.grad_norm / (torch.linalg.vector_norm(g) + 1e-6), max=1.0)
+    fus.flat.grads.copy_(g)
+    fus.optimizer.step()
+    torch.testing.assert_close(ref, fus.flat.params, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_fused_unscaled_nan_gradient_poisons_the_step_like_torch(tmp_path):
+    """Without a scaler (fp32 trunk), clip_grad_norm_ of a NaN gradient gives a NaN norm and a NaN
+    clip coefficient, so torch turns every parameter NaN; the fused path does the same instead of
+    clipping the finite elements to zero."""
+    _, fus = _agents_and_batch(256, mixed=False, tmp=tmp_path)
+    if not fus.truncate_grads:
+        pytest.skip("agent config without grad clipping")
+    fus.fused.use_graphs = False
+    fus.fused.begin_epoch()
+    fus.fused.step_a(True)
+    torch.cuda.synchronize()
+    fus.flat.grads[3] = float("nan")
+    fus.fused.step_b()
+    torch.cuda.synchronize()
+    assert torch.isnan(fus.flat.params).all()
+
+
+@pytest.mark.gpu
 def test_fused_train_epoch_runs_graph_replays(tmp_path):
     ref, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path)
     fus.obs = None

@@ -435,3 +435,31 @@ def test_bench_two_ranks_one_gpu():
     assert "error" not in tr, (tr, r.stderr[-2000:])
     assert tr["n_gpus"] == 2 and tr["global_envs"] == 2048 and tr["value"] > 0
     assert tr["multi_gpu_mode"] == "allgather"  # north star: RCCL all-gather of rollouts at the PPO boundary
+
+
+def test_bench_gpus_flag_launches_ranks_itself():
+    """`python bench.py --gpus 2` with NO launcher in the command (the driver's and a user's plain
+    invocation): bench.py starts torch.distributed.run as a child, the two ranks (sharing cuda:0 over
+    gloo here) form the job, and the relayed line reports both GPUs' envs."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["ALLSTEPS_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "3",
+           "--num-envs", "256", "--no-cpu-baseline", "--no-c5", "--train-envs", "1024"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["config"]["global_envs"] == 2 * line["config"]["num_envs_per_gpu"] == 512
+    tr = line["train"]
+    assert "error" not in tr, (tr, r.stderr[-2000:])
+    assert tr["n_gpus"] == 2 and tr["multi_gpu_mode"] == "allgather"
+    # the roofline's duration fits inside the step it belongs to
+    km = line["kernels_ms"]
+    assert km["k_step_ms"] + km["k_obs_event_ms"] <= 1.02 * line["ms_per_step"]
