@@ -184,19 +184,22 @@ def hbm_copy_bandwidth(device, nbytes: int = 2 << 30, iters: int = 20) -> float:
     return 2.0 * n16 * 16 / (ms * 1e-3) / 1e9
 
 
+# the step library's device-code flags (tests/test_kernel_budget.py compiles with exactly these):
+# -ffp-contract=off: no implicit FMA contraction -- every FMA of the physics path is an explicit fmaf()
+# in the order include/as_detmath.h fixes, so the oracle (built the same way) rounds identically and
+# HIP <-> oracle parity is bit-exact.  -fno-slp-vectorize: the SLP pairs of the step kernel's scalar
+# code cost more register moves than they save (launch -2 %); the packed math that pays
+# (sweep, W rows) is written out as 2-vectors
+STEP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-I", INCLUDE]
+
+
 def build_native(verbose: bool = False) -> str:
     """Compile liballsteps_hip.so and libppo_hip.so for gfx950 in-tree (hipcc)."""
     import subprocess
 
     srcs = [os.path.join(CSRC, f) for f in ("allsteps_kernels.hip", "allsteps_abi.hip")]
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    # -ffp-contract=off: no implicit FMA contraction -- every FMA of the physics path is an explicit
-    # fmaf() in the order include/as_detmath.h fixes, so the oracle (built the same way) rounds
-    # identically and HIP <-> oracle parity is bit-exact.  -fno-slp-vectorize: the SLP pairs of the
-    # step kernel's scalar code cost more register moves than they save (launch -2 %, DESIGN.md §3);
-    # the packed math that pays (sweep, W rows) is written out as 2-vectors
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-ffp-contract=off", "-fno-slp-vectorize", "-I", INCLUDE, "-o", LIB_PATH] + srcs
+    cmd = [hipcc, *STEP_FLAGS, "-fPIC", "-shared", "-Wno-unused-result", "-o", LIB_PATH] + srcs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -233,52 +236,14 @@ def make_model(m: dict) -> AsModel:
     return M
 
 
-def linspace_f32(start: float, end: float, steps: int) -> np.ndarray:
-    """float32 torch.linspace (ATen RangeFactories: start+i*step for the first half, end-(n-1-i)*step after)."""
-    s, e = np.float32(start), np.float32(end)
-    step = (e - s) / np.float32(steps - 1)
-    return np.array([s + step * np.float32(i) if i < steps // 2 else e - step * np.float32(steps - i - 1)
-                     for i in range(steps)], np.float32)
+from .envs.task_table import linspace_f32  # noqa: E402  (re-exported: allsteps_env.py)
 
 
 def make_task(cfg, dof_names: list) -> AsTask:
-    from .envs.allsteps_env_cfg import running_start_pose
+    """as_task_t from the cfg (envs/task_table.py: shared with the oracle, dispatched on the cfg type)."""
+    from allsteps_isaaclab_amd.envs.task_table import fill, task_fields
 
-    # a cfg without the walker's task table (the C5 quadruped: AnymalCStonesEnvCfg) takes the walker's
-    # defaults for it -- as_task_t is then only the stones / timing block, the quad task is as_quad_task_t
-    base = cfg
-    if not hasattr(cfg, "alive_reward_scale"):
-        from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
-
-        cfg = AllstepsEnvCfg()
-
-    T = AsTask()
-    T.num_steps = base.num_steps
-    T.step_radius = cfg.step_radius
-    T.stop_frames = cfg.stop_frames
-    T.eps = cfg.epsilon
-    T.alive, T.energy, T.action = cfg.alive_reward_scale, cfg.energy_cost_scale, cfg.actions_cost_scale
-    T.joint_limit, T.death = cfg.joint_at_limit_cost_scale, cfg.death_cost
-    T.dof_vel_scale, T.fall_abs = cfg.dof_vel_scale, cfg.termination_height_absolute
-    T.step_dt = float(np.float32(base.sim.dt * base.decimation))
-    T.max_episode_length = cfg.max_episode_length
-    T.max_curriculum = cfg.max_curriculum
-    T.curriculum_threshold = cfg.curriculum_progress_threshold
-    T.term_curriculum[:] = [float(x) for x in linspace_f32(0.75, 0.45, cfg.max_curriculum + 1)]
-    T.gain_curriculum[:] = [float(x) for x in linspace_f32(1.2, 1.2, cfg.max_curriculum + 1)]
-    T.init_root[:] = list(cfg.init_root_pos)
-    T.init_q[:] = [float(np.float32(x)) for x in running_start_pose()]
-    if all(x in dof_names for x in (*cfg.right_body_names, *cfg.left_body_names, *cfg.negation_body_names)):
-        J = dof_names.index
-        T.right_idx[:] = [J(x) for x in cfg.right_body_names]
-        T.left_idx[:] = [J(x) for x in cfg.left_body_names]
-        T.neg_idx[:] = [J(x) for x in cfg.negation_body_names]
-    # else: a model without the walker's joints (the C5 quadruped) is stepped physics-only
-    # (as_physics_step), which never reads the reset mirror tables
-    T.noise_lo, T.noise_hi = cfg.initial_joint_angle_range
-    T.clip_lo, T.clip_hi = cfg.initial_joint_angle_clip_range
-    T.regen_footsteps = int(bool(getattr(cfg, "regenerate_footsteps", False)))
-    return T
+    return fill(AsTask(), task_fields(cfg, dof_names))
 
 
 def make_sim(cfg) -> AsSim:

@@ -54,6 +54,8 @@ class AnymalCStonesEnv(DirectRLEnv):
             raise _native.NativeError(f"AnymalCStonesEnv runs on the HIP backend only (device={dev}, HIP device "
                                       f"available: {torch.cuda.is_available()}); there is no CPU fallback")
         self.model = load_model(ANYMAL_C_JSON)
+        if not cfg.robot.enabled_self_collisions:  # ArticulationRootPropertiesCfg.enabled_self_collisions
+            self.model = dict(self.model, num_self_pairs=0, self_pair=[0] * len(self.model["self_pair"]))
         n = self.num_envs
         self.num_dof = self.model["num_hinges"]
         if self.num_dof != cfg.action_space:

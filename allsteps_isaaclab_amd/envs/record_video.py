@@ -28,6 +28,10 @@ class RecordVideo:
         self.saved: list[str] = []
 
     def __getattr__(self, name):  # everything else is the env's
+        # only reached for names not on the wrapper; before __init__ has set `env` (a failed __init__,
+        # copy / pickle) there is nothing to forward to, and looking `env` up here would recurse
+        if name == "env" or "env" not in self.__dict__:
+            raise AttributeError(name)
         return getattr(self.env, name)
 
     @property

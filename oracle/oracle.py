@@ -179,54 +179,11 @@ def make_model(m: dict) -> OrModel:
     return M
 
 
-def torch_linspace_f32(start: float, end: float, steps: int) -> np.ndarray:
-    """float32 torch.linspace (ATen RangeFactories formula)."""
-    s, e = np.float32(start), np.float32(end)
-    step = (e - s) / np.float32(steps - 1)
-    out = np.empty(steps, np.float32)
-    for i in range(steps):
-        out[i] = s + step * np.float32(i) if i < steps // 2 else e - step * np.float32(steps - i - 1)
-    return out
-
-
 def make_task(cfg, dof_names: list) -> OrTask:
-    from allsteps_isaaclab_amd.envs.allsteps_env_cfg import running_start_pose
+    """as_task_t from the cfg (envs/task_table.py: shared with the HIP path, dispatched on the cfg type)."""
+    from allsteps_isaaclab_amd.envs.task_table import fill, task_fields
 
-    # a cfg without the walker's task table (the C5 quadruped: AnymalCStonesEnvCfg) takes the walker's
-    # defaults for it -- as_task_t is then only the stones / timing block, the quad task is as_quad_task_t
-    base = cfg
-    if not hasattr(cfg, "alive_reward_scale"):
-        from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
-
-        cfg = AllstepsEnvCfg()
-
-    T = OrTask()
-    T.num_steps = base.num_steps
-    T.step_radius = cfg.step_radius
-    T.stop_frames = cfg.stop_frames
-    T.eps = cfg.epsilon
-    T.alive, T.energy, T.action = cfg.alive_reward_scale, cfg.energy_cost_scale, cfg.actions_cost_scale
-    T.joint_limit, T.death = cfg.joint_at_limit_cost_scale, cfg.death_cost
-    T.dof_vel_scale, T.fall_abs = cfg.dof_vel_scale, cfg.termination_height_absolute
-    T.step_dt = float(np.float32(base.sim.dt * base.decimation))
-    T.max_episode_length = cfg.max_episode_length
-    T.max_curriculum = cfg.max_curriculum
-    T.curriculum_threshold = cfg.curriculum_progress_threshold
-    T.term_curriculum[:] = [float(x) for x in torch_linspace_f32(0.75, 0.45, cfg.max_curriculum + 1)]
-    T.gain_curriculum[:] = [float(x) for x in torch_linspace_f32(1.2, 1.2, cfg.max_curriculum + 1)]
-    T.init_root[:] = list(cfg.init_root_pos)
-    T.init_q[:] = [float(np.float32(x)) for x in running_start_pose()]
-    if all(x in dof_names for x in (*cfg.right_body_names, *cfg.left_body_names, *cfg.negation_body_names)):
-        J = dof_names.index
-        T.right_idx[:] = [J(x) for x in cfg.right_body_names]
-        T.left_idx[:] = [J(x) for x in cfg.left_body_names]
-        T.neg_idx[:] = [J(x) for x in cfg.negation_body_names]
-    # else: a model without the walker's joints (the C5 quadruped) is stepped physics-only
-    # (as_physics_step), which never reads the reset mirror tables
-    T.noise_lo, T.noise_hi = cfg.initial_joint_angle_range
-    T.clip_lo, T.clip_hi = cfg.initial_joint_angle_clip_range
-    T.regen_footsteps = int(bool(getattr(cfg, "regenerate_footsteps", False)))
-    return T
+    return fill(OrTask(), task_fields(cfg, dof_names))
 
 
 def make_sim(cfg) -> OrSim:

@@ -12,14 +12,10 @@ import re
 import sys
 
 
-def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("asm")
-    p.add_argument("--func", default="_ZN2as6k_stepILi27EEEvNS_8StepArgsE")
-    p.add_argument("--min", type=int, default=8)
-    a = p.parse_args()
-    lines = open(a.asm).read().split("\n")
-    start = next(i for i, l in enumerate(lines) if l.startswith(a.func + ":"))
+def scan(lines: list[str], func: str, min_gap: int = 8) -> list[tuple[str, int, int, str]]:
+    """(block, 1-based line, instructions between issue and wait, instruction) of every LDS read that a
+    `s_waitcnt lgkmcnt(N)` retires fewer than `min_gap` instructions after its issue."""
+    start = next(i for i, l in enumerate(lines) if l.startswith(func + ":"))
     end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
     q = []  # (index of instruction, line) of outstanding LDS ops in issue order
     n = 0
@@ -35,9 +31,7 @@ def main():
         if not s or s.startswith(";") or s.startswith("."):
             continue
         n += 1
-        if s.startswith("ds_") and "ds_swizzle" not in s and "ds_bpermute" not in s and "ds_permute" not in s:
-            q.append((n, i, s))
-        elif s.startswith("ds_"):
+        if s.startswith("ds_"):
             q.append((n, i, s))
         m = re.match(r"s_waitcnt\s+.*lgkmcnt\((\d+)\)", s)
         if m:
@@ -45,8 +39,18 @@ def main():
             done = q[: max(len(q) - keep, 0)]
             q = q[max(len(q) - keep, 0):]
             for (k, li, ins) in done:
-                if n - k < a.min and ins.startswith("ds_read"):
+                if n - k < min_gap and ins.startswith("ds_read"):
                     hits.append((block, li + 1, n - k, ins))
+    return hits
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("asm")
+    p.add_argument("--func", default="_ZN2as6k_stepILi27EEEvNS_8StepArgsE")
+    p.add_argument("--min", type=int, default=8)
+    a = p.parse_args()
+    hits = scan(open(a.asm).read().split("\n"), a.func, a.min)
     for h in hits:
         print(f"{h[0]} line {h[1]}: waited {h[2]} instructions after {h[3]}")
     print(f"{len(hits)} early waits on LDS reads", file=sys.stderr)
