@@ -87,11 +87,14 @@ class AsActuator(C.Structure):
 class AsQuadTask(C.Structure):
     _fields_ = [("stop_frames", C.c_int32), ("alive", C.c_float), ("action_cost", C.c_float), ("death", C.c_float),
                 ("min_height", C.c_float), ("up_z_min", C.c_float), ("max_episode_length", C.c_int32),
-                ("step_dt", C.c_float), ("stand_height", C.c_float), ("joint_noise", C.c_float)]
+                ("step_dt", C.c_float), ("stand_height", C.c_float), ("joint_noise", C.c_float),
+                ("energy_cost", C.c_float), ("step_radius", C.c_float), ("step_reward", C.c_float),
+                ("step_sigma", C.c_float), ("target_bonus", C.c_float), ("bonus_radius", C.c_float),
+                ("foot_offset_y", C.c_float * 4)]
 
 
 ACT_TORQUE, ACT_DC_MOTOR = 0, 1
-QUAD_OBS_DIM = 51
+QUAD_OBS_DIM = 62
 
 
 # (field, rows, dtype) of the SoA state, in as_state_t order
@@ -339,7 +342,10 @@ class NativeEnv:
     def set_quad_task(self, **kw):
         Q = AsQuadTask()
         for k, v in kw.items():
-            setattr(Q, k, v)
+            if isinstance(v, (list, tuple)):
+                getattr(Q, k)[:] = [float(x) for x in v]
+            else:
+                setattr(Q, k, v)
         self._quad = Q
         check(self.L.as_set_quad_task(self.h, C.byref(Q)), "as_set_quad_task")
 

@@ -365,11 +365,17 @@ int as_set_actuator(as_env_t* env, const as_actuator_t* act) {
 
 int as_set_quad_task(as_env_t* env, const as_quad_task_t* q) {
   if (!env || !q) return fail(AS_ERR_INVALID, "as_set_quad_task: null argument");
-  if (env->host.model.num_hinges != 12 || 15 + 3 * env->host.model.num_hinges != AS_QUAD_OBS_DIM)
+  if (env->host.model.num_hinges != 12 || 26 + 3 * env->host.model.num_hinges != AS_QUAD_OBS_DIM)
     return fail(AS_ERR_INVALID, "as_set_quad_task: the task is defined for a 12-hinge quadruped");
   if (!env->st.contact_mask_hind) return fail(AS_ERR_INVALID, "as_set_quad_task: state->contact_mask_hind is NULL");
-  if (q->stop_frames < 1 || q->max_episode_length < 1 || !(q->step_dt > 0.f) || env->num_steps < 3)
-    return fail(AS_ERR_INVALID, "as_set_quad_task: stop_frames / max_episode_length / step_dt / num_steps");
+  if (q->stop_frames < 1 || q->max_episode_length < 1 || !(q->step_dt > 0.f) || env->num_steps < 3 ||
+      !(q->step_sigma > 0.f))
+    return fail(AS_ERR_INVALID, "as_set_quad_task: stop_frames / max_episode_length / step_dt / num_steps / step_sigma");
+  for (int f = 0; f < 4; ++f) {  // k_quad takes each swing foot's tip from its sensor geom
+    bool found = false;
+    for (int g = 0; g < env->host.model.num_geoms; ++g) found = found || env->host.model.geom_foot[g] == f;
+    if (!found) return fail(AS_ERR_INVALID, "as_set_quad_task: the model needs a foot geom for each sensor 0..3");
+  }
   HIP_TRY(hipSetDevice(env->device));
   env->host.quad = *q;
   // setup call, not stream-ordered: every launch still queued on any stream (torch's pool streams are

@@ -5,7 +5,7 @@ One ``step(actions)`` is ``as_quad_step`` on the HIP device: ``decimation`` subs
 (6 + 12 generalized velocities) with IsaacLab's DC motor evaluated in every substep on the position targets
 ``default_q + action_scale * a`` (anymal_c_env.py:73-78), four foot sensors, then ``k_quad``: target
 stones, potentials, rewards, dones, in-kernel resets of done envs (stand pose + Philox joint noise, actions
-observed as zero: anymal_c_env.py:171-172) and the 51-float observation.  Simulation settings are ANYmal-C's
+observed as zero: anymal_c_env.py:171-172) and the 62-float observation.  Simulation settings are ANYmal-C's
 (``AnymalCStonesEnvCfg``: dt 1/200, friction 1.0 multiply, max depenetration velocity 1.0).  There is no
 CPU fallback: without the HIP library or a gfx950 device the constructor raises ``NativeError``.
 """
@@ -102,6 +102,11 @@ class AnymalCStonesEnv(DirectRLEnv):
     @property
     def target_index(self) -> torch.Tensor:
         return self.state["idx"]
+
+    @property
+    def swing_leg(self) -> torch.Tensor:
+        """the swing foot of the gait, sensor order 0..3 = RF, LF, RH, LH (front target idx, hind idx - 1)"""
+        return self.state["swing"]
 
     @property
     def contact_mask(self) -> torch.Tensor:

@@ -15,9 +15,12 @@ The simulation and robot fields follow the reference's ANYmal-C direct task and 
   weights are Nucleus-only (``anymal.py:47``); the DC motor is the documented analytical stand-in.
 
 The stepping-stone task itself is authored (the reference has no quadruped stepping-stone task; DESIGN.md
-§7b): stones as in Allsteps-v0 (20 boxes 0.5 x 0.8 x 0.225 m), a target stone advanced by a front-foot
-contact held for ``stop_frames`` steps, potential-based progress + alive - action cost, death on tilt or
-a base height below the target stone.  The soft joint limits are data (``AnymalCStonesEnv
+§7b): stones as in Allsteps-v0 (20 boxes 0.5 x 0.8 x 0.225 m); the reference's target machine on four feet (the
+swing foot cycles RF, LF, RH, LH; front feet aim at stone idx, hind feet at idx - 1; a swing foot that
+pushes on its stone within ``step_radius`` of its aim point for ``stop_frames`` steps hands over to the
+next foot, and the hind-left foot's completes the cycle: idx + 1); the ALLSTEPS reward terms -- alive,
+potential progress, energy, action cost, step hit 50 exp(-d / 0.25), last-stone bonus, death cost
+(allsteps_env.py:347-394); death on tilt or a base height below the target stone.  The soft joint limits are data (``AnymalCStonesEnv
 .soft_joint_pos_limits``): as in IsaacLab they do not enter the physics (articulation.py:1262-1266 only
 stores them; PhysX gets the hard limits), and the direct ANYmal-C task never reads them.
 """
@@ -62,7 +65,7 @@ class AnymalCStonesEnvCfg:
     decimation: int = 4
     action_scale: float = 0.5
     action_space: int = 12
-    observation_space: int = 51
+    observation_space: int = 62
     state_space: int = 0
     seed: int | None = 42
     is_finite_horizon: bool = False
@@ -75,11 +78,21 @@ class AnymalCStonesEnvCfg:
     num_steps: int = 20
     step_size: tuple = (0.5, 0.8, 0.225)
 
-    # the stepping-stone task (authored; include/allsteps.h as_quad_task_t)
-    stop_frames: int = 2          # steps a front foot must push on the target stone
-    alive_reward: float = 0.5
-    action_cost: float = 0.005    # per sum(a^2)
-    death_reward: float = -2.0
+    # the stepping-stone task (authored; include/allsteps.h as_quad_task_t): the ALLSTEPS target
+    # machine and reward terms (allsteps_env.py:347-394, 418-457) on four feet
+    stop_frames: int = 2          # steps the swing foot must push on its target stone (allsteps_env_cfg: 2)
+    step_radius: float = 0.25     # allsteps_env_cfg.py:97
+    alive_reward: float = 0.5     # authored for the quadruped (the walker's alive_reward_scale is 2.0)
+    energy_cost: float = 0.009    # energy_cost_scale (allsteps_env_cfg.py:222): sum |qd a|
+    action_cost: float = 0.01     # actions_cost_scale (allsteps_env_cfg.py:223): ||a||
+    death_reward: float = -1.0    # death_cost (allsteps_env_cfg.py:228)
+    step_reward: float = 50.0     # allsteps_env.py:380: 50 exp(-d / 0.25) on a fresh reach
+    step_sigma: float = 0.25
+    target_bonus: float = 10.0    # allsteps_env.py:383, last stone with the body within 0.15 m
+    bonus_radius: float = 0.15
+    # aim point of each sensor foot (RF, LF, RH, LH) on its stone: the centre + this lateral offset,
+    # the feet's stance width in model/anymal_c.xml (hip 0.1 + abduction link 0.1 either side)
+    foot_offset_y: tuple = (-0.2, 0.2, -0.2, 0.2)
     min_height: float = 0.25      # base below target stone + this: terminated
     up_z_min: float = 0.5         # projected gravity z above -this (tilt past 60 degrees): terminated
     stand_height: float = 0.584   # reset: base this far above the higher of stones 0 / 1 (top face)
@@ -99,7 +112,9 @@ class AnymalCStonesEnvCfg:
                 "death": self.death_reward, "min_height": self.min_height, "up_z_min": self.up_z_min,
                 "max_episode_length": self.max_episode_length,
                 "step_dt": float(np.float32(self.sim.dt * self.decimation)), "stand_height": self.stand_height,
-                "joint_noise": self.joint_noise}
+                "joint_noise": self.joint_noise, "energy_cost": self.energy_cost, "step_radius": self.step_radius,
+                "step_reward": self.step_reward, "step_sigma": self.step_sigma, "target_bonus": self.target_bonus,
+                "bonus_radius": self.bonus_radius, "foot_offset_y": list(self.foot_offset_y)}
 
     def actuator(self) -> dict:
         r = self.robot

@@ -317,8 +317,10 @@ class A2CAgent:
         if mpd not in ("float16", "bfloat16"):
             raise ValueError(f"mixed_precision_dtype must be float16 or bfloat16, got {mpd!r}")
         self.mixed_precision_dtype = torch.float16 if mpd == "float16" else torch.bfloat16
-        # GradScaler(enabled=mixed_precision) state on the device: [scale, growth tracker]
-        self.scaler_state = (torch.tensor([SCALER_INIT, 0.0], device=self.device) if self.mixed_precision else None)
+        # GradScaler(enabled=mixed_precision) state on the device: [scale, growth tracker].  `grad_scaler:
+        # False` (not an rl_games key; a measurement knob) runs the 16-bit trunk unscaled
+        self.scaler_state = (torch.tensor([SCALER_INIT, 0.0], device=self.device)
+                             if self.mixed_precision and bool(config.get("grad_scaler", True)) else None)
         self.max_epochs = int(config.get("max_epochs", -1))
         self.save_freq = int(config.get("save_frequency", 0))
         self.save_best_after = int(config.get("save_best_after", 100))

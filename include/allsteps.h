@@ -41,7 +41,7 @@ extern "C" {
 #define AS_MAX_ROWS 30
 #define AS_OBS_DIM 59
 #define AS_ACT_DIM 21
-#define AS_QUAD_OBS_DIM 51
+#define AS_QUAD_OBS_DIM 62
 
 enum {
   AS_OK = 0,
@@ -169,15 +169,28 @@ typedef struct {
   float saturation_effort, effort_limit, velocity_limit;
 } as_actuator_t;
 
-/* The BASELINE C5 task: a quadruped crossing the Allsteps stones (authored here -- the reference has
- * no quadruped stepping-stone task; its ANYmal-C task is flat-ground velocity tracking).  Per env step,
- * after the physics substeps: episode counter; target tick (a front foot -- sensor 0 or
- * 1 -- pushing on target stone idx for stop_frames steps advances idx); potential -|stone[idx] - root|_xy
- * / step_dt; terminated = body tilted past up_z_min or below the target stone + min_height; truncated at
- * max_episode_length; reward = (pot - old_pot) + alive - action_cost sum(a^2), death on termination;
+/* The BASELINE C5 task: a quadruped crossing the Allsteps stones with the ALLSTEPS reward terms
+ * (allsteps_env.py:347-394) and the reference's target machine (:418-457) carried over to four feet
+ * (authored here -- the reference has no quadruped stepping-stone task; its ANYmal-C task is flat-ground
+ * velocity tracking).  Per env step, after the physics substeps:
+ *   gait: the swing foot cycles through the sensors 0..3 (RF, LF, RH, LH); a front foot's target is
+ *     stone idx, a hind foot's stone idx - 1 (idx = state.idx, 2 after a reset: hind feet on stone 0,
+ *     front feet on stone 1); the swing foot f's aim point is its target stone's centre + (0,
+ *     foot_offset_y[f]) and its position is the tip of its sensor geom (the capsule end p1, FK from q);
+ *   target tick (allsteps_env.py:418-440): reached = f pushes on its target stone (contact mask bit)
+ *     and its xy distance d to the aim point < step_radius; count += reached; count >= stop_frames:
+ *     count = 0, swing = (swing + 1) mod 4, and after the hind-left foot (swing 3) idx += 1 (clamped);
+ *   potential (:441-448): pot = -|stone[idx] - root|_xy / step_dt;
+ *   terminated = body tilted past up_z_min or below the target stone + min_height; truncated at
+ *     max_episode_length;
+ *   reward (:347-394) = alive + (pot - old_pot) - energy_cost sum|qd a| - action_cost ||a||
+ *     + step_reward exp(-d / step_sigma) on a fresh reach (count == 1, idx < num_steps - 1)
+ *     + target_bonus when idx is the last stone and the root is within bonus_radius of it (xy);
+ *     death on termination;
  * reset of done envs to the stand pose over stones 0 / 1 (+ U(-1,1) * joint_noise, Philox); observation
- * [51] = root linear / angular velocity (body frame), projected gravity, stones idx and idx + 1 relative
- * to the root (body frame), q - default_q, qd, the clipped actions. */
+ * [62] = root linear / angular velocity (body frame), projected gravity, stones idx - 1, idx, idx + 1
+ * relative to the root (body frame), the swing foot one-hot [4], each foot's contact with its own
+ * target stone [4], q - default_q, qd, the clipped actions. */
 typedef struct {
   int32_t stop_frames;
   float alive, action_cost, death;
@@ -186,6 +199,13 @@ typedef struct {
   float step_dt;
   float stand_height;       /* root z above the higher of stones 0 / 1's top face at reset */
   float joint_noise;
+  float energy_cost;        /* energy_cost_scale (allsteps_env_cfg.py:222) */
+  float step_radius;        /* allsteps_env_cfg.py:97 */
+  float step_reward;        /* 50 (allsteps_env.py:380) */
+  float step_sigma;         /* 0.25 */
+  float target_bonus;       /* 10 (allsteps_env.py:383) */
+  float bonus_radius;       /* 0.15 */
+  float foot_offset_y[4];   /* aim point lateral offset per sensor foot (RF, LF, RH, LH) */
 } as_quad_task_t;
 
 typedef struct as_env as_env_t;

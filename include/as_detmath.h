@@ -211,6 +211,43 @@ AS_HD void as_axis_angle_mat(const float* a, float ang, float* R) {
   R[6] = fmaf(tx, a[2], -(s * a[1])); R[7] = fmaf(ty, a[2], s * a[0]);   R[8] = fmaf(tz, a[2], c);
 }
 
+/* World position of the point pl (link frame) on `link`: the root pose (rp, unit quaternion rq), then
+ * the walk root -> link with every link's joint transform as the physics' FK forms it
+ * (oracle/physics.c kinematics): Rl = Roff(offset_quat) Rj(axis, q), tl = offset_pos + Roff (anchor -
+ * Rj anchor); p += R tl, R = R Rl; out = rp + (p + R pl).  The hinge angle of link i is read from the
+ * state column q_col[k * q_stride] of the cfg dof k with cfg_dof_link[k] == i (no per-lane arrays:
+ * one global read per link on the device).  Model tables flattened row-major ([link][3] / [link][4]). */
+AS_HD void as_link_point(const int32_t* parent, const int32_t* cfg_dof_link, int nh, const float* offset_pos,
+                         const float* offset_quat, const float* axis, const float* anchor, const float* q_col,
+                         int q_stride, int link, const float* rp, const float* rq, const float* pl, float* out) {
+  int depth = 0;
+  for (int l = link; l > 0; l = parent[l]) ++depth;
+  float R[9], p[3] = {0.f, 0.f, 0.f};
+  as_quat_to_mat(rq, R);
+  for (int s = depth - 1; s >= 0; --s) {
+    int i = link;
+    for (int j = 0; j < s; ++j) i = parent[i];  /* the ancestor s links above `link` */
+    float qi = 0.f;
+    for (int k = 0; k < nh; ++k)
+      if (cfg_dof_link[k] == i) qi = q_col[k * q_stride];
+    float Roff[9], Rj[9], Rl[9], Ro[3], t[3], tl[3], wp[3], Rn[9];
+    as_quat_to_mat(offset_quat + 4 * i, Roff);
+    as_axis_angle_mat(axis + 3 * i, qi, Rj);
+    as_matmul3(Roff, Rj, Rl);
+    as_matvec3(Rj, anchor + 3 * i, Ro);
+    for (int k = 0; k < 3; ++k) t[k] = anchor[3 * i + k] - Ro[k];
+    as_matvec3(Roff, t, tl);
+    for (int k = 0; k < 3; ++k) tl[k] = tl[k] + offset_pos[3 * i + k];
+    as_matvec3(R, tl, wp);
+    for (int k = 0; k < 3; ++k) p[k] = p[k] + wp[k];
+    as_matmul3(R, Rl, Rn);
+    for (int k = 0; k < 9; ++k) R[k] = Rn[k];
+  }
+  float w[3];
+  as_matvec3(R, pl, w);
+  for (int k = 0; k < 3; ++k) out[k] = rp[k] + (p[k] + w[k]);
+}
+
 /* ---- actuators (include/allsteps.h as_actuator_t) */
 
 /* IsaacLab's DCMotor on a position target (actuator_pd.py:184-199, 264-275), torch's float32 order:

@@ -139,6 +139,8 @@ typedef struct {
   float step_dt;
   float stand_height;
   float joint_noise;
+  float energy_cost, step_radius, step_reward, step_sigma, target_bonus, bonus_radius;
+  float foot_offset_y[4];
 } or_quad_task_t;
 
 /* ---- math helpers (isaaclab/utils/math.py) ---- */
@@ -189,6 +191,8 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
                           const or_quad_task_t* q, or_state_t* st, const float* actions, int reset_all,
                           uint64_t seed, float* obs, float* rew, uint8_t* term, uint8_t* trunc);
 /* physics substeps (DC motor) + task epilogue, every env; actions [n][12] */
+/* test hook: world position of point pl (link frame) on `link` of env e (include/as_detmath.h as_link_point) */
+void or_link_point(const or_model_t* m, const or_state_t* st, int e, int link, const float* pl, float* out);
 void or_quad_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
                   const or_quad_task_t* q, or_state_t* st, const float* actions, uint64_t seed, float* obs,
                   float* rew, uint8_t* term, uint8_t* trunc, int nthreads);

@@ -89,10 +89,16 @@ class OrActuator(C.Structure):
                 ("effort_limit", C.c_float), ("velocity_limit", C.c_float)]
 
 
+QUAD_OBS = 62  # include/allsteps.h AS_QUAD_OBS_DIM
+
+
 class OrQuadTask(C.Structure):
     _fields_ = [("stop_frames", C.c_int32), ("alive", C.c_float), ("action_cost", C.c_float), ("death", C.c_float),
                 ("min_height", C.c_float), ("up_z_min", C.c_float), ("max_episode_length", C.c_int32),
-                ("step_dt", C.c_float), ("stand_height", C.c_float), ("joint_noise", C.c_float)]
+                ("step_dt", C.c_float), ("stand_height", C.c_float), ("joint_noise", C.c_float),
+                ("energy_cost", C.c_float), ("step_radius", C.c_float), ("step_reward", C.c_float),
+                ("step_sigma", C.c_float), ("target_bonus", C.c_float), ("bonus_radius", C.c_float),
+                ("foot_offset_y", C.c_float * 4)]
 
 
 def build() -> str:
@@ -131,6 +137,7 @@ def lib() -> C.CDLL:
         L.or_dc_motor_batch.argtypes = [C.c_int, FP, FP, FP, V, FP]
         L.or_quad_post_physics.argtypes = [V, V, V, V, V, V, FP, C.c_int, C.c_uint64, FP, FP,
                                            C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]
+        L.or_link_point.argtypes = [V, V, C.c_int, C.c_int, FP, FP]
         L.or_quad_step.argtypes = [V, V, V, V, V, V, FP, C.c_uint64, FP, FP, C.POINTER(C.c_uint8),
                                    C.POINTER(C.c_uint8), C.c_int]
     return _LIB
@@ -289,7 +296,7 @@ class Oracle:
 
     def quad_step(self, st: OracleState, act: OrActuator, q: OrQuadTask, actions, seed: int = 42, nthreads: int = 1):
         n = st.n
-        obs = np.zeros((n, 51), np.float32)
+        obs = np.zeros((n, QUAD_OBS), np.float32)
         rew = np.zeros(n, np.float32)
         term = np.zeros(n, np.uint8)
         trunc = np.zeros(n, np.uint8)
@@ -299,7 +306,7 @@ class Oracle:
         return obs, rew, term.astype(bool), trunc.astype(bool)
 
     def quad_reset_all(self, st: OracleState, act: OrActuator, q: OrQuadTask, seed: int = 42):
-        obs = np.zeros((st.n, 51), np.float32)
+        obs = np.zeros((st.n, QUAD_OBS), np.float32)
         z = np.zeros(1, np.float32)
         self.L.or_quad_post_physics(C.byref(self.model), C.byref(self.sim), C.byref(self.task), C.byref(act),
                                     C.byref(q), st.ptr, fp(z), 1, seed, fp(obs), None, None, None)
@@ -368,6 +375,12 @@ class Oracle:
                             fp(np.asarray(root_quat, np.float32)), fp(np.ascontiguousarray(q_cfg, np.float32)),
                             fp(out))
         return out.reshape(3, 3)
+
+    def link_point(self, st: OracleState, e: int, link: int, pl=(0.0, 0.0, 0.0)):
+        """World position of pl (link frame) on `link` of env e (the C5 task's foot-tip FK)."""
+        out = np.zeros(3, np.float32)
+        self.L.or_link_point(C.byref(self.model), st.ptr, e, link, fp(np.asarray(pl, np.float32)), fp(out))
+        return out
 
     def philox(self, seed: int, env: int, episode: int, k: int = 22):
         out = np.zeros(k, np.float32)

@@ -5,17 +5,20 @@
  * include/allsteps.h as_quad_task_t.  The reference has no quadruped stepping-stone task (its ANYmal-C
  * task, isaaclab_tasks/direct/anymal_c/anymal_c_env.py, is flat-ground velocity tracking): the task is
  * authored here from the Allsteps task's pieces (target stones, potentials, allsteps_env.py:347-457)
- * and the ANYmal task's actuation / observation terms (anymal_c_env.py:73-110).  PARITY UNPINNED
+ * and the ANYmal task's actuation / observation terms (anymal_c_env.py:73-110): the ALLSTEPS reward
+ * terms (step hit, progress, energy, alive, target bonus; allsteps_env.py:347-394) and the target machine
+ * (:418-457) carried over to four feet, the swing foot cycling RF, LF, RH, LH.  PARITY UNPINNED
  * against any reference output; the HIP kernel is checked against this file bit for bit.
  */
 #include <math.h>
 #include <stddef.h>
 
 #include "oracle.h"
+#include "../include/as_detmath.h"
 
 #define F(arr, f, n, e) (arr)[(size_t)(f) * (n) + (e)]
 #define QUAD_TAG 0x51756164u /* "Quad" */
-#define QUAD_OBS 51
+#define QUAD_OBS 62
 
 static int imin(int a, int b) { return a < b ? a : b; }
 
@@ -37,30 +40,52 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
       const float x = reset_all ? 0.f : actions[(size_t)e * nh + k];
       a[k] = fminf(fmaxf(x, -1.f), 1.f);
     }
-    int idx = st->idx[e], count = st->count[e], ep_len = st->ep_len[e];
+    int idx = st->idx[e], count = st->count[e], swing = st->swing[e], ep_len = st->ep_len[e];
     uint32_t episode = st->episode[e];
+    uint32_t mk[4] = {F(st->contact_mask, 0, n, e), F(st->contact_mask, 1, n, e), F(st->contact_mask_hind, 0, n, e),
+                      F(st->contact_mask_hind, 1, n, e)};
     float pot = st->pot[e], old_pot = st->old_pot[e];
     int term = 0, trunc = 0;
     if (!reset_all) {
       ep_len += 1;
-      const uint32_t front = F(st->contact_mask, 0, n, e) | F(st->contact_mask, 1, n, e);
-      if ((front >> idx) & 1u) count += 1;
+      /* ENV:418-440 target tick for the swing foot f: front feet aim at stone idx, hind feet at idx - 1;
+       * reached = contact with the target stone and the foot tip within step_radius (xy) of the aim point */
+      const int f = swing, tgt = f < 2 ? idx : idx - 1;
+      int g = 0;
+      for (int j = 0; j < m->num_geoms; ++j)
+        if (m->geom_foot[j] == f) { g = j; break; }
+      float tip[3];
+      as_link_point(m->parent, m->cfg_dof_link, nh, &m->offset_pos[0][0], &m->offset_quat[0][0], &m->axis[0][0],
+                    &m->anchor[0][0], st->q + e, n, m->geom_link[g], rp, rq, m->geom_p1[g], tip);
+      const float fx = tip[0] - STONE(tgt, 0), fy = tip[1] - (STONE(tgt, 1) + Q->foot_offset_y[f]);
+      const float d = sqrtf(fx * fx + fy * fy);
+      const int reached = ((mk[f] >> tgt) & 1u) && d < Q->step_radius;
+      if (reached) count += 1;
       if (count >= Q->stop_frames) {
-        idx = imin(idx + 1, N - 1);
         count = 0;
+        if (swing == 3) idx = imin(idx + 1, N - 1);
+        swing = (swing + 1) & 3;
       }
+      /* ENV:377-380 step reward on a fresh reach */
+      const float step_hit = reached && count == 1 && idx < N - 1 ? Q->step_reward * as_expf(-d / Q->step_sigma) : 0.f;
       old_pot = pot;
       const float dx = STONE(idx, 0) - rp[0], dy = STONE(idx, 1) - rp[1];
-      pot = -sqrtf(dx * dx + dy * dy) / Q->step_dt;
+      const float bd = sqrtf(dx * dx + dy * dy);
+      pot = -bd / Q->step_dt;
       const float down[3] = {0.f, 0.f, -1.f};
       float gb[3];
       or_quat_rotate_inverse(rq, down, gb);
       term = gb[2] > -Q->up_z_min || rp[2] < STONE(idx, 2) + Q->min_height;
       trunc = ep_len >= Q->max_episode_length;
-      float a2 = 0.f;
-      for (int k = 0; k < nh; ++k) a2 += a[k] * a[k];
+      float a2 = 0.f, en = 0.f;
+      for (int k = 0; k < nh; ++k) {
+        a2 += a[k] * a[k];
+        en += fabsf(F(st->qd, k, n, e) * a[k]);
+      }
+      const float bonus = idx == N - 1 && bd < Q->bonus_radius ? Q->target_bonus : 0.f;
       const float progress = pot - old_pot;
-      rew[e] = term ? Q->death : progress + Q->alive - Q->action_cost * a2;
+      rew[e] = term ? Q->death
+                    : (((Q->alive + progress) - Q->energy_cost * en) - Q->action_cost * sqrtf(a2)) + step_hit + bonus;
       term_out[e] = (uint8_t)term;
       trunc_out[e] = (uint8_t)trunc;
     }
@@ -93,15 +118,18 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
       for (int k = 0; k < 4; ++k) F(st->root_quat, k, n, e) = rq[k];
       idx = imin(2, N - 1);
       count = 0;
+      swing = 0;
       ep_len = 0;
       const float dx = STONE(idx, 0) - rp[0], dy = STONE(idx, 1) - rp[1];
       pot = -sqrtf(dx * dx + dy * dy) / Q->step_dt;
       old_pot = pot;
+      for (int k = 0; k < 4; ++k) mk[k] = 0u;
       F(st->contact_mask, 0, n, e) = F(st->contact_mask, 1, n, e) = 0u;
       F(st->contact_mask_hind, 0, n, e) = F(st->contact_mask_hind, 1, n, e) = 0u;
     }
     st->idx[e] = idx;
     st->count[e] = count;
+    st->swing[e] = swing;
     st->ep_len[e] = ep_len;
     st->episode[e] = episode;
     st->pot[e] = pot;
@@ -115,16 +143,21 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
     const float down[3] = {0.f, 0.f, -1.f};
     or_quat_rotate_inverse(rq, down, v);
     o[6] = v[0]; o[7] = v[1]; o[8] = v[2];
-    for (int t = 0; t < 2; ++t) {
-      const int k = imin(idx + t, N - 1);
+    for (int t = 0; t < 3; ++t) {
+      int k = idx - 1 + t;
+      k = k < 0 ? 0 : (k > N - 1 ? N - 1 : k);
       const float d[3] = {STONE(k, 0) - rp[0], STONE(k, 1) - rp[1], STONE(k, 2) - rp[2]};
       or_quat_rotate_inverse(rq, d, v);
       o[9 + 3 * t] = v[0]; o[10 + 3 * t] = v[1]; o[11 + 3 * t] = v[2];
     }
+    for (int f = 0; f < 4; ++f) {
+      o[18 + f] = swing == f ? 1.f : 0.f;
+      o[22 + f] = (mk[f] >> (f < 2 ? idx : idx - 1)) & 1u ? 1.f : 0.f;
+    }
     for (int k = 0; k < nh; ++k) {
-      o[15 + k] = q[k] - act->default_q[k];
-      o[15 + nh + k] = qd[k];
-      o[15 + 2 * nh + k] = was_reset ? 0.f : a[k]; /* _reset_idx zeroes _actions (anymal_c_env.py:171-172) */
+      o[26 + k] = q[k] - act->default_q[k];
+      o[26 + nh + k] = qd[k];
+      o[26 + 2 * nh + k] = was_reset ? 0.f : a[k]; /* _reset_idx zeroes _actions (anymal_c_env.py:171-172) */
     }
 #undef STONE
   }
@@ -145,4 +178,14 @@ void or_quad_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* tas
     or_physics_step_act(m, sim, task, act, st, e, a);
   }
   or_quad_post_physics(m, sim, task, act, q, st, actions, 0, seed, obs, rew, term, trunc);
+}
+
+/* test hook: as_link_point on env e's state (the C5 task's foot-tip FK) */
+void or_link_point(const or_model_t* m, const or_state_t* st, int e, int link, const float* pl, float* out) {
+  const int n = st->n;
+  float rp[3], rq[4];
+  for (int k = 0; k < 3; ++k) rp[k] = F(st->root_pos, k, n, e);
+  for (int k = 0; k < 4; ++k) rq[k] = F(st->root_quat, k, n, e);
+  as_link_point(m->parent, m->cfg_dof_link, m->num_hinges, &m->offset_pos[0][0], &m->offset_quat[0][0],
+                &m->axis[0][0], &m->anchor[0][0], st->q + e, n, link, rp, rq, pl, out);
 }

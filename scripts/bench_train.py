@@ -3,7 +3,7 @@ separately env+PPO"): the reference train.py flow with the reference agent confi
 minibatch 32768, 10 mini-epochs, MLP 5 x 256), timed per epoch after warm-up epochs (the first
 epoch runs eagerly, the second captures the rollout / update HIP graphs).
 
-    python scripts/bench_train.py --num_envs 32768 --epochs 5 --warmup 2
+    python scripts/bench_train.py --num_envs 32768 --epochs 5 --warmup 2 [agent.params.config.<key>=<value> ...]
 
 Prints one JSON line: env-steps/s including the PPO update and the play / update split."""
 
@@ -81,7 +81,8 @@ def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int 
         "epochs": len(t), "horizon": agent.horizon_length, "minibatch": agent.minibatch_size,
         "mini_epochs": agent.mini_epochs_num, "s_per_epoch": round(wall / len(t), 4),
         "play_s": round(sum(x[1] for x in t) / len(t), 4), "update_s": round(sum(x[2] for x in t) / len(t), 4),
-        "mixed_precision": agent.mixed_precision, "hip_graphs": agent._play_graphs is not None,
+        "mixed_precision": agent.mixed_precision, "grad_scaler": agent.scaler_state is not None,
+        "hip_graphs": agent._play_graphs is not None,
         "precision": (("fp16" if agent.mixed_precision_dtype == torch.float16 else "bf16") if agent.mixed_precision
                       else "fp32") + " MLP trunk on MFMA (fp32 accumulate), fp32 heads / losses / Adam / normalisers, "
                      "device-side GradScaler (rl_games mixed_precision=True: fp16 autocast; DESIGN.md §7)",
@@ -98,7 +99,12 @@ def main():
     ap.add_argument("--multi_gpu_mode", choices=("allgather", "allreduce"), default="allgather",
                     help="--distributed exchange: RCCL all-gather of rollouts (north star) or gradient all-reduce")
     ap.add_argument("--quiet", action="store_true", help="only the result line (rank 0)")
-    args = ap.parse_args()
+    # the rest of the command line: hydra-style overrides that train.py applies (agent.<path>=<value>,
+    # env.<path>=<value>), e.g. agent.params.config.mixed_precision_dtype=bfloat16
+    args, extra = ap.parse_known_args()
+    bad = [a for a in extra if "=" not in a or a.startswith("-")]
+    if bad:
+        ap.error(f"unrecognized arguments: {' '.join(bad)}")
     out = measure(args.num_envs, args.epochs, args.warmup, args.level, verbose=not args.quiet,
                   distributed=args.distributed, multi_gpu_mode=args.multi_gpu_mode)
     import torch.distributed as dist

@@ -47,7 +47,10 @@ def _act_struct(oracle_mod, qmodel):
 def _task_struct(oracle_mod):
     Q = oracle_mod.OrQuadTask()
     for k, v in QUAD_TASK.items():
-        setattr(Q, k, v)
+        if isinstance(v, (list, tuple)):
+            getattr(Q, k)[:] = v
+        else:
+            setattr(Q, k, v)
     return Q
 
 
@@ -76,7 +79,7 @@ def test_dc_motor_matches_isaaclab_formulas(oracle_mod, qmodel):
 
 def _post(qorc, oracle_mod, qmodel, st, actions, reset_all=False):
     n = st.n
-    obs = np.zeros((n, 51), np.float32)
+    obs = np.zeros((n, oracle_mod.QUAD_OBS), np.float32)
     rew = np.zeros(n, np.float32)
     term = np.zeros(n, np.uint8)
     trunc = np.zeros(n, np.uint8)
@@ -95,58 +98,128 @@ def _stand_state(qorc, oracle_mod, qmodel, n):
     return st
 
 
+def _tip(qorc, qmodel, st, e, f):
+    """world position of sensor foot f's tip (its geom's capsule end p1) in env e"""
+    g = [j for j in range(qmodel["num_geoms"]) if qmodel["geom_foot"][j] == f][0]
+    return qorc.link_point(st, e, int(qmodel["geom_link"][g]), qmodel["geom_p1"][g])
+
+
 def test_task_reset_pose_and_observation(qorc, oracle_mod, qmodel):
     n = 8
     st = _stand_state(qorc, oracle_mod, qmodel, n)
     q0 = stand_pose(qmodel["dof_names"])
     assert np.abs(st["q"][:12].T - q0).max() <= QUAD_TASK["joint_noise"]
     np.testing.assert_allclose(st["root_pos"][:, 0], [0.375, 0.0, 0.1125 + QUAD_TASK["stand_height"]], atol=1e-6)
-    assert (st["idx"] == 2).all() and (st["episode"] == 1).all()
+    assert (st["idx"] == 2).all() and (st["episode"] == 1).all() and (st["swing"] == 0).all()
     obs, *_ = _post(qorc, oracle_mod, qmodel, st, np.zeros((n, 12), np.float32), reset_all=True)
+    assert obs.shape == (n, 62)
     np.testing.assert_allclose(obs[:, 6:9], [[0, 0, -1]] * n, atol=1e-7)      # projected gravity, upright
-    np.testing.assert_allclose(obs[0, 9:12], [1.5 - 0.375, 0.0, -0.1125 - 0.584], atol=1e-5)  # stone 2, body frame
-    np.testing.assert_allclose(obs[0, 12:15], [2.25 - 0.375, 0.0, -0.1125 - 0.584], atol=1e-5)
+    for t, k in enumerate((1, 2, 3)):  # stones idx - 1, idx, idx + 1 in the body frame
+        np.testing.assert_allclose(obs[0, 9 + 3 * t:12 + 3 * t], [0.75 * k - 0.375, 0.0, -0.1125 - 0.584], atol=1e-5)
+    np.testing.assert_array_equal(obs[:, 18:22], [[1, 0, 0, 0]] * n)  # RF swings first
+    assert (obs[:, 22:26] == 0).all()                                 # contact masks cleared by the reset
     # different envs, different Philox joint noise; the same env and episode, the same draws
     assert np.abs(st["q"][:12, 0] - st["q"][:12, 1]).max() > 0
+    # the feet stand on stones 0 (hind) / 1 (front) at their aim points' lateral offsets
+    for f in range(4):
+        tip = _tip(qorc, qmodel, st, 0, f)
+        assert abs(tip[0] - (0.75 if f < 2 else 0.0)) < 0.15 and abs(tip[1] - QUAD_TASK["foot_offset_y"][f]) < 0.05
 
 
-def test_task_tick_potential_and_dones(qorc, oracle_mod, qmodel):
-    n = 6
+def test_link_point_is_the_physics_fk(qorc, oracle_mod, qmodel):
+    """as_link_point (the task's foot-tip FK) walks the same transforms as the physics' kinematics:
+    a link's origin equals or_fk_bodies' body position bit for bit at random poses."""
+    rng = np.random.default_rng(3)
+    n = 16
+    st = qorc.state(n)
+    st["q"][:12] = rng.uniform(-1, 1, (12, n)).astype(np.float32)
+    st["root_pos"][:] = rng.uniform(-1, 1, (3, n)).astype(np.float32)
+    qt = rng.normal(size=(4, n)).astype(np.float32)
+    st["root_quat"][:] = (qt / np.linalg.norm(qt, axis=0)).astype(np.float32)
+    for e in range(n):
+        bp = qorc.fk_bodies(*(np.ascontiguousarray(x) for x in (st["root_pos"][:, e], st["root_quat"][:, e], st["q"][:12, e])))
+        for b, link in enumerate((qmodel["torso_link"], *qmodel["foot_link"])):
+            np.testing.assert_array_equal(qorc.link_point(st, e, int(link)), bp[b])
+
+
+def _aim_stone_under(st, e, k, tip, f):
+    """move stone k of env e so that foot f's aim point is exactly under its tip"""
+    st["stones"][3 * k, e] = tip[0]
+    st["stones"][3 * k + 1, e] = tip[1] - np.float32(QUAD_TASK["foot_offset_y"][f])
+
+
+def test_task_gait_tick_step_reward_and_cycle(qorc, oracle_mod, qmodel):
+    n = 4
     st = _stand_state(qorc, oracle_mod, qmodel, n)
     a = np.zeros((n, 12), np.float32)
-    # env 0: RF on the target stone (2) for stop_frames steps -> target 3
-    # env 1: a hind foot on stone 2 -> no tick (front feet only)
-    # env 2: tilted 70 degrees about x -> terminated (death reward), reset
-    # env 3: body 0.2 m above the target stone's centre -> terminated
-    # env 4: at the episode limit -> truncated, reset, not terminated
-    # env 5: actions cost: reward = progress + alive - cost sum(a^2)
-    ang = np.deg2rad(70.0)
+    # env 0: RF (swing 0) pushes on its target stone 2, aim point under its tip: a fresh reach pays the
+    #        step reward, stop_frames steps hand the swing to LF with the target unchanged
+    # env 1: the same contact bit but the aim point 0.3 m away: no reach (step_radius 0.25)
+    # env 2: LH (swing 3) on stone idx - 1 = 1 completes the cycle: idx 3, swing back to RF
+    # env 3: RF touching the hind feet's stone 1 only: no reach
+    tip0, tip1 = _tip(qorc, qmodel, st, 0, 0), _tip(qorc, qmodel, st, 1, 0)
+    _aim_stone_under(st, 0, 2, tip0, 0)
+    _aim_stone_under(st, 1, 2, tip1 + np.float32([0.3, 0, 0]), 0)
+    st["swing"][2] = 3
+    _aim_stone_under(st, 2, 1, _tip(qorc, qmodel, st, 2, 3), 3)
+    rewards = []
     for step in range(QUAD_TASK["stop_frames"]):
-        st["contact_mask"][0, 0] = 1 << 2
-        st["contact_mask_hind"][0, 1] = 1 << 2
-        if step == QUAD_TASK["stop_frames"] - 1:
-            st["root_quat"][:, 2] = [np.cos(ang / 2), np.sin(ang / 2), 0, 0]
-            st["root_pos"][2, 3] = 0.2
-            st["ep_len"][4] = QUAD_TASK["max_episode_length"] - 1
-            a[5] = 0.5
+        st["contact_mask"][0, :] = [1 << 2, 1 << 2, 0, 1 << 1]
+        st["contact_mask_hind"][1, 2] = 1 << 1
         pot_before = st["pot"].copy()
         obs, rew, term, trunc = _post(qorc, oracle_mod, qmodel, st, a)
-    assert st["idx"][0] == 3 and st["count"][0] == 0
-    assert st["idx"][1] == 2 and st["count"][1] == 0
-    assert term.tolist() == [False, False, True, True, False, False]
-    assert trunc.tolist() == [False, False, False, False, True, False]
-    assert rew[2] == QUAD_TASK["death"] and rew[3] == QUAD_TASK["death"]
+        assert not term.any() and not trunc.any()
+        rewards.append(rew.copy())
+        if step == 0:  # the fresh reach: 50 exp(-d / 0.25) on top of alive + progress (zero actions)
+            base = np.float32(QUAD_TASK["alive"]) + (st["pot"] - pot_before)
+            assert rew[0] > base[0] + 45 and abs(rew[1] - base[1]) < 1e-5 and abs(rew[3] - base[3]) < 1e-5
+    assert (st["idx"] == [2, 2, 3, 2]).all()
+    assert (st["swing"] == [1, 0, 0, 0]).all() and (st["count"] == 0).all()
+    # the second frame of the same reach pays no step reward
+    assert rewards[1][0] < rewards[0][0] - 45
+    # obs: swing one-hot, and after the cycle env 2's stones are 2 / 3 / 4
+    np.testing.assert_array_equal(obs[0, 18:22], [0, 1, 0, 0])
+    np.testing.assert_array_equal(obs[2, 18:22], [1, 0, 0, 0])
+    np.testing.assert_allclose(obs[2, 12:15], [0.75 * 3 - st["root_pos"][0, 2], 0.0, -st["root_pos"][2, 2] + 0.0],
+                               atol=1e-5)
+
+
+def test_task_potential_costs_and_dones(qorc, oracle_mod, qmodel):
+    n = 5
+    st = _stand_state(qorc, oracle_mod, qmodel, n)
+    a = np.zeros((n, 12), np.float32)
+    # env 0: tilted 70 degrees about x -> terminated (death reward), reset
+    # env 1: body 0.2 m above the target stone's centre -> terminated
+    # env 2: at the episode limit -> truncated, reset, not terminated
+    # env 3: costs: reward = alive + progress - energy_cost sum|qd a| - action_cost ||a||
+    # env 4: the last stone as target with the body over it -> target bonus
+    ang = np.deg2rad(70.0)
+    st["root_quat"][:, 0] = [np.cos(ang / 2), np.sin(ang / 2), 0, 0]
+    st["root_pos"][2, 1] = 0.2
+    st["ep_len"][2] = QUAD_TASK["max_episode_length"] - 1
+    a[3] = 0.5
+    st["qd"][:12, 3] = np.linspace(-2, 2, 12, dtype=np.float32)
+    st["idx"][4] = 19
+    st["root_pos"][:2, 4] = [0.75 * 19 + 0.1, 0.0]
+    qd3 = st["qd"][:12, 3].copy()
+    pot_before = st["pot"].copy()
+    obs, rew, term, trunc = _post(qorc, oracle_mod, qmodel, st, a)
+    assert term.tolist() == [True, True, False, False, False]
+    assert trunc.tolist() == [False, False, True, False, False]
+    assert rew[0] == QUAD_TASK["death"] and rew[1] == QUAD_TASK["death"]
     # reset envs observe zero actions (anymal_c_env.py:171-172 zeroes _actions in _reset_idx); live ones theirs
-    assert (obs[[2, 3, 4], 15 + 24:] == 0).all()
-    assert (obs[5, 15 + 24:] == 0.5).all()
-    # done envs were reset: stand pose, target 2, episode counter advanced
-    for e in (2, 3, 4):
-        assert st["idx"][e] == 2 and st["ep_len"][e] == 0 and st["episode"][e] == 2
+    assert (obs[[0, 1, 2], 26 + 24:] == 0).all()
+    assert (obs[3, 26 + 24:] == 0.5).all()
+    for e in (0, 1, 2):  # done envs were reset: stand pose, target 2, swing RF, episode counter advanced
+        assert st["idx"][e] == 2 and st["swing"][e] == 0 and st["ep_len"][e] == 0 and st["episode"][e] == 2
         np.testing.assert_array_equal(st["root_quat"][:, e], [1, 0, 0, 0])
-    # reward of a live env: potential progress + alive - action cost
-    prog = np.float32(st["pot"][5]) - np.float32(pot_before[5])
-    expect = prog + np.float32(QUAD_TASK["alive"]) - np.float32(QUAD_TASK["action_cost"]) * np.float32(12 * 0.25)
-    assert abs(rew[5] - expect) < 1e-5
+    prog = np.float32(st["pot"][3]) - np.float32(pot_before[3])
+    en = np.float32(np.abs(qd3 * np.float32(0.5)).sum())
+    expect = (np.float32(QUAD_TASK["alive"]) + prog - np.float32(QUAD_TASK["energy_cost"]) * en
+              - np.float32(QUAD_TASK["action_cost"]) * np.sqrt(np.float32(12 * 0.25)))
+    assert abs(rew[3] - expect) < 1e-4
+    prog4 = np.float32(st["pot"][4]) - np.float32(pot_before[4])
+    assert abs(rew[4] - (np.float32(QUAD_TASK["alive"]) + prog4 + np.float32(QUAD_TASK["target_bonus"]))) < 1e-3
 
 
 def test_task_stands_on_four_feet(qorc, oracle_mod, qmodel):
@@ -180,7 +253,7 @@ def test_c5_cfg_is_anymal_c():
     assert c.sim.dt == 1.0 / 200.0 and c.decimation == 4 and c.sim.friction == 1.0
     assert c.sim.max_depenetration_velocity == 1.0 and c.sim.solver_position_iteration_count == 4
     assert c.robot.soft_joint_pos_limit_factor == 0.95 and c.max_episode_length == 1000
-    assert c.scene.num_envs == 16384 and c.action_space == 12 and c.observation_space == 51
+    assert c.scene.num_envs == 16384 and c.action_space == 12 and c.observation_space == 62
     assert np.float32(c.quad_task()["step_dt"]) == np.float32(4 / 200)
     o = __import__("oracle").Oracle(cfg=c, model=__import__("allsteps_isaaclab_amd.model", fromlist=["x"]).load_model(
         __import__("allsteps_isaaclab_amd.model", fromlist=["x"]).ANYMAL_C_JSON))
