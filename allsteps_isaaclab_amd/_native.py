@@ -75,7 +75,7 @@ class AsState(C.Structure):
     _fields_ = [(name, VP) for name in (
         "root_pos", "root_quat", "root_lin", "root_ang", "q", "qd", "stones", "pot", "old_pot", "foot_contact",
         "body_pos", "idx", "prev", "next", "count", "swing", "ep_len", "episode", "contact_mask", "curriculum",
-        "contact_mask_hind")]
+        "contact_mask_hind", "feet")]
 
 
 class AsActuator(C.Structure):
@@ -90,11 +90,11 @@ class AsQuadTask(C.Structure):
                 ("step_dt", C.c_float), ("stand_height", C.c_float), ("joint_noise", C.c_float),
                 ("energy_cost", C.c_float), ("step_radius", C.c_float), ("step_reward", C.c_float),
                 ("step_sigma", C.c_float), ("target_bonus", C.c_float), ("bonus_radius", C.c_float),
-                ("foot_offset_y", C.c_float * 4)]
+                ("foot_progress", C.c_float), ("foot_offset_y", C.c_float * 4)]
 
 
 ACT_TORQUE, ACT_DC_MOTOR = 0, 1
-QUAD_OBS_DIM = 62
+QUAD_OBS_DIM = 64
 
 
 # (field, rows, dtype) of the SoA state, in as_state_t order
@@ -282,6 +282,7 @@ class NativeEnv:
             setattr(S, name, state[name].data_ptr())
         S.curriculum = state["curriculum"].data_ptr()
         S.contact_mask_hind = state["contact_mask_hind"].data_ptr() if "contact_mask_hind" in state else None
+        S.feet = state["feet"].data_ptr() if "feet" in state else None
         self._state = S
         h = C.c_void_p()
         check(self.L.as_create(n, C.byref(self._model), C.byref(self._sim), C.byref(self._task), C.byref(S),

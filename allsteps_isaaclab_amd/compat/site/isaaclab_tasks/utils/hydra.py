@@ -8,30 +8,7 @@ from __future__ import annotations
 import functools
 import sys
 
-from allsteps_isaaclab_amd.registry import load_cfg_from_registry
-
-
-def _set(obj, path: list[str], value) -> None:
-    for k in path[:-1]:
-        obj = obj[k] if isinstance(obj, dict) else getattr(obj, k)
-    if isinstance(obj, dict):
-        obj[path[-1]] = value
-    else:
-        setattr(obj, path[-1], value)
-
-
-def apply_overrides(env_cfg, agent_cfg, overrides: list[str]) -> None:
-    import yaml
-
-    for ov in overrides:
-        key, sep, val = ov.partition("=")
-        if not sep or "." not in key:
-            raise ValueError(f"unsupported override {ov!r} (expected env.<path>=<value> or agent.<path>=<value>)")
-        root, *path = key.lstrip("+").split(".")
-        target = {"env": env_cfg, "agent": agent_cfg}.get(root)
-        if target is None:
-            raise ValueError(f"override {ov!r} must start with env. or agent.")
-        _set(target, path, yaml.safe_load(val))
+from allsteps_isaaclab_amd.registry import apply_overrides, load_cfg_from_registry  # noqa: F401 (re-export)
 
 
 def hydra_task_config(task_name: str, agent_cfg_entry_point: str):

@@ -365,9 +365,10 @@ int as_set_actuator(as_env_t* env, const as_actuator_t* act) {
 
 int as_set_quad_task(as_env_t* env, const as_quad_task_t* q) {
   if (!env || !q) return fail(AS_ERR_INVALID, "as_set_quad_task: null argument");
-  if (env->host.model.num_hinges != 12 || 26 + 3 * env->host.model.num_hinges != AS_QUAD_OBS_DIM)
+  if (env->host.model.num_hinges != 12 || 28 + 3 * env->host.model.num_hinges != AS_QUAD_OBS_DIM)
     return fail(AS_ERR_INVALID, "as_set_quad_task: the task is defined for a 12-hinge quadruped");
-  if (!env->st.contact_mask_hind) return fail(AS_ERR_INVALID, "as_set_quad_task: state->contact_mask_hind is NULL");
+  if (!env->st.contact_mask_hind || !env->st.feet)
+    return fail(AS_ERR_INVALID, "as_set_quad_task: state->contact_mask_hind / state->feet is NULL");
   if (q->stop_frames < 1 || q->max_episode_length < 1 || !(q->step_dt > 0.f) || env->num_steps < 3 ||
       !(q->step_sigma > 0.f))
     return fail(AS_ERR_INVALID, "as_set_quad_task: stop_frames / max_episode_length / step_dt / num_steps / step_sigma");

@@ -1047,11 +1047,11 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   const int ncand = __popc(mine);
   // narrowphase in two passes.  (A) lane = geom, loop over the candidate stones (once for the
   // priority geoms, once for the rest): the cheap bounding test (spheres: the exact separation)
-  // appends the surviving (stone, geom) pairs to a list in LDS, in emission order.  (B) lane = pair of
-  // either env, up to 64 at a time (flush2): the exact test (capsules: slope bisection for the
-  // segment's closest point) and the contacts, emitted in each env's list order by a prefix sum.  B runs
-  // as soon as either env has kPairsPerChunk pairs pending, so a list never exceeds 32 + G entries, and
-  // an env stops collecting pairs once it has ncap contacts.
+  // appends the surviving (stone, geom) pairs to a list in LDS, in emission order.  (B) lane = pair,
+  // in chunks of kPairsPerChunk: the exact test (capsules: slope bisection for the segment's closest
+  // point) and the contacts, emitted in list order by a prefix sum.  A chunk is flushed as soon as
+  // kPairsPerChunk pairs are pending, so the list never exceeds 32 + 22 entries, and the search
+  // stops once this env has ncap contacts.
   {
     float* gs = s.x.col.g[lane];  // staging of this lane's geom for pass B and the self pairs
     if (gv) {
@@ -1064,29 +1064,14 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   }
   int* pl = s.x.col.pl;
   int pend = 0, base = 0;
-  // Pass B runs over BOTH envs' pending pairs at once: wave lane w takes env 0's pair w while w < n0,
-  // then env 1's pairs, so the pairs of a crowded env (a fallen walker: 40+ pairs) fill its partner's
-  // idle lanes instead of costing an extra pass with half the wave masked off.  Each env's contacts
-  // are emitted in its own list order (a prefix count over the lanes holding its pairs): the contact
-  // lists are exactly those of a per-env pass (oracle/physics.c collide).
-  EnvS* const ebase = &s - half;
-  const int wl = (half << 5) | lane;
-  const uint64_t below = (1ull << wl) - 1ull;
-  const int ncap0 = __builtin_amdgcn_readlane(ncap, 0), ncap1 = __builtin_amdgcn_readlane(ncap, 32);
-  auto both = [](int v) { return max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 32)); };
-  auto flush2 = [&]() {
-    const int p0 = __builtin_amdgcn_readlane(pend, 0), p1 = __builtin_amdgcn_readlane(pend, 32);
-    const int n0 = min(p0, 64), n1 = min(p1, 64 - n0);
-    const int which = wl < n0 ? 0 : 1;
-    const int idx = which == 0 ? wl : wl - n0;
-    const bool act = which == 0 || idx < n1;
-    EnvS& se = ebase[which];
+  auto flush = [&](int npairs) {  // pass B over pl[0, npairs) (npairs <= kPairsPerChunk), shift the rest
     int cnt = 0, plink = 0, pst = 0, pfoot = -1;
     float P0[3], N0[3], P1[3], N1[3], P2[3], N2[3], SEP0 = 0.f, SEP1 = 0.f, SEP2 = 0.f, pr = 0.f;
-    const int e = se.x.col.pl[act ? idx : 0];
+    const bool act = lane < npairs;
+    const int e = pl[act ? lane : 0];
     const int gi = e & 0xff;
     pst = e >> 8;
-    const float* gq = se.x.col.g[gi];
+    const float* gq = s.x.col.g[gi];
     const float A[3] = {gq[0], gq[1], gq[2]}, Bb[3] = {gq[3], gq[4], gq[5]};
     pr = gq[6];
     const int meta = __float_as_int(gq[7]);
@@ -1094,7 +1079,7 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
     pfoot = ((meta >> 4) & 15) - 1;
     plink = meta >> 8;
     float c[3];
-    for (int k = 0; k < 3; ++k) c[k] = se.stones[3 * pst + k] - se.root_pos[k];
+    for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * pst + k] - s.root_pos[k];
     // capsule: minimum of the (convex) signed distance along the segment by bisection on the sign
     // of its slope.  Runs for every lane (the result is only used by capsule pairs).
     float lo = 0.f, hi = 1.f;
@@ -1115,50 +1100,40 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
           cnt = 1;
         }
       } else {
-        float n0v[3], n1v[3];
-        float s0 = sd_box(A, c, h, n0v) - pr;
-        float s1 = sd_box(Bb, c, h, n1v) - pr;
+        float n0[3], n1[3];
+        float s0 = sd_box(A, c, h, n0) - pr;
+        float s1 = sd_box(Bb, c, h, n1) - pr;
         float ts = 0.5f * (lo + hi), Ps[3], ns[3];
         for (int k = 0; k < 3; ++k) Ps[k] = A[k] + ts * (Bb[k] - A[k]);
         float ss = sd_box(Ps, c, h, ns) - pr;
         bool e0 = s0 < margin, e1 = s1 < margin;
         bool es = ss < margin && ss < fminf(s0, s1) - 0.002f;
         // pack the emitted contacts in (t=0, t=1, t*) order into slots 0..2
-        for (int k = 0; k < 3; ++k) { P0[k] = A[k]; N0[k] = n0v[k]; }
+        for (int k = 0; k < 3; ++k) { P0[k] = A[k]; N0[k] = n0[k]; }
         SEP0 = s0;
         if (e0) {
-          for (int k = 0; k < 3; ++k) { P1[k] = Bb[k]; N1[k] = n1v[k]; P2[k] = Ps[k]; N2[k] = ns[k]; }
+          for (int k = 0; k < 3; ++k) { P1[k] = Bb[k]; N1[k] = n1[k]; P2[k] = Ps[k]; N2[k] = ns[k]; }
           SEP1 = s1; SEP2 = ss;
           if (!e1) { for (int k = 0; k < 3; ++k) { P1[k] = Ps[k]; N1[k] = ns[k]; } SEP1 = ss; }
         } else {
-          for (int k = 0; k < 3; ++k) { P0[k] = Bb[k]; N0[k] = n1v[k]; P1[k] = Ps[k]; N1[k] = ns[k]; }
+          for (int k = 0; k < 3; ++k) { P0[k] = Bb[k]; N0[k] = n1[k]; P1[k] = Ps[k]; N1[k] = ns[k]; }
           SEP0 = s1; SEP1 = ss;
           if (!e1) { for (int k = 0; k < 3; ++k) { P0[k] = Ps[k]; N0[k] = ns[k]; } SEP0 = ss; }
         }
         cnt = (int)e0 + (int)e1 + (int)es;
       }
     }
-    // per-env prefix counts of cnt in [0, 3] over the lanes holding that env's pairs (two ballots)
-    const uint64_t m0 = n0 >= 64 ? ~0ull : (1ull << n0) - 1ull;
-    const uint64_t m01 = n0 + n1 >= 64 ? ~0ull : (1ull << (n0 + n1)) - 1ull;
-    const uint64_t m1 = m01 & ~m0;
-    const uint64_t b0 = __ballot((cnt & 1) != 0), b1 = __ballot((cnt & 2) != 0);
-    const uint64_t mine = which == 0 ? m0 : m1;
-    const int pos = __popcll(b0 & mine & below) + 2 * __popcll(b1 & mine & below);
-    const int tot0 = __popcll(b0 & m0) + 2 * __popcll(b1 & m0), tot1 = __popcll(b0 & m1) + 2 * __popcll(b1 & m1);
-    const int slot = (which == 0 ? __builtin_amdgcn_readlane(base, 0) : __builtin_amdgcn_readlane(base, 32)) + pos;
-    const int nc = which == 0 ? ncap0 : ncap1;
-    if (cnt > 0) emit_contact(se, slot, nc, plink, -1, pst, pfoot, P0, N0, SEP0, pr);
-    if (cnt > 1) emit_contact(se, slot + 1, nc, plink, -1, pst, pfoot, P1, N1, SEP1, pr);
-    if (cnt > 2) emit_contact(se, slot + 2, nc, plink, -1, pst, pfoot, P2, N2, SEP2, pr);
-    base += half == 0 ? tot0 : tot1;
-    // shift this env's unprocessed tail (< 64 entries) to the front of its list
-    const int take = half == 0 ? n0 : n1;
-    const int rest = pend - take;
-    const int t0 = lane < rest ? pl[take + lane] : 0, t1 = lane + 32 < rest ? pl[take + lane + 32] : 0;
+    int total;
+    const int slot = base + half_scan3(cnt, total);
+    if (cnt > 0) emit_contact(s, slot, ncap, plink, -1, pst, pfoot, P0, N0, SEP0, pr);
+    if (cnt > 1) emit_contact(s, slot + 1, ncap, plink, -1, pst, pfoot, P1, N1, SEP1, pr);
+    if (cnt > 2) emit_contact(s, slot + 2, ncap, plink, -1, pst, pfoot, P2, N2, SEP2, pr);
+    base += total;
+    // shift the unprocessed tail (< 32 entries) to the front
+    const int rest = pend - npairs;
+    const int tail = lane < rest ? pl[npairs + lane] : 0;
     __syncthreads();
-    if (lane < rest) pl[lane] = t0;
-    if (lane + 32 < rest) pl[lane + 32] = t1;
+    if (lane < rest) pl[lane] = tail;
     pend = rest;
     __syncthreads();
   };
@@ -1183,26 +1158,18 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   }
   __syncthreads();
   const uint32_t primask = npri >= 32 ? ~0u : (1u << npri) - 1u;
-  // the pair list, class by class (feet first), stone-major; the loop runs the larger candidate count of
-  // the two envs (wave-uniform), so that the merged pass B can run whenever either list fills a chunk
-  const int ncm = both(ncand);
 #pragma unroll 1
   for (int cls = 0; cls < 2; ++cls) {
 #pragma unroll 1
-    for (int ci = 0; ci < ncm; ++ci) {
-      if (ci < ncand && base < ncap) {
-        const uint32_t bl = cneed[ci] & (cls == 0 ? primask : ~primask);
-        if ((bl >> lane) & 1u) pl[pend + __popc(bl & ((1u << lane) - 1u))] = (s.cand[ci] << 8) | lane;
-        pend += __popc(bl);  // no barrier: the single wave's LDS operations complete in issue order
-      }
-      if (base >= ncap) pend = 0;  // an env at its contact cap: later pairs would be dropped anyway
-      while (both(pend) >= kPairsPerChunk) flush2();  // each run takes 64 pairs: lists stay < 32 + G
+    for (int ci = 0; ci < ncand; ++ci) {
+      if (base >= ncap) break;  // later contacts would be dropped anyway
+      const uint32_t bl = cneed[ci] & (cls == 0 ? primask : ~primask);
+      if ((bl >> lane) & 1u) pl[pend + __popc(bl & ((1u << lane) - 1u))] = (s.cand[ci] << 8) | lane;
+      pend += __popc(bl);  // no barrier: the single wave's LDS operations complete in issue order
+      if (pend >= kPairsPerChunk) flush(kPairsPerChunk);
     }
   }
-  while (both(pend) > 0) {
-    flush2();
-    if (base >= ncap) pend = 0;
-  }
+  if (pend > 0 && base < ncap) flush(pend);
   // self-contacts.  (A) lane = pair: the bounding-sphere filter; the surviving pairs are appended to
   // the pending list in table order.  (B) lane = pending pair, in chunks of G: the capsule-capsule
   // closest points (include/as_detmath.h, shared with the oracle), emitted in list order.
@@ -2303,6 +2270,16 @@ __global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
 // serial restatement.  Coalesced SoA loads / stores (64-thread workgroups, like k_obs).
 constexpr uint32_t kQuadTag = 0x51756164u;  // "Quad": reset-draw stream of the quadruped task
 
+// foot f's tip (its sensor geom's capsule end p1) from the state's q column of env e, root pose (rp, rq)
+__device__ __forceinline__ void quad_tip(const as_model_t& m, const as_state_t& st, int n, int e, int f, const float* rp,
+                                         const float* rq, float* tip) {
+  int g = 0;
+  for (int j = 0; j < m.num_geoms; ++j)
+    if (m.geom_foot[j] == f) { g = j; break; }
+  as_link_point(m.parent, m.cfg_dof_link, m.num_hinges, &m.offset_pos[0][0], &m.offset_quat[0][0], &m.axis[0][0],
+                &m.anchor[0][0], st.q + e, n, m.geom_link[g], rp, rq, m.geom_p1[g], tip);
+}
+
 __global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
   const Consts& K = *(const Consts*)(CK*)P.consts;
   const as_model_t& m = K.model;
@@ -2313,6 +2290,11 @@ __global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
   const as_state_t& st = P.st;
   const float half_z = K.sim.stone_half[2];
   auto stone = [&](int k, int c) { return st.stones[(3 * k + c) * n + e]; };
+  // xy distance of foot f's tip to the aim point on stone k
+  auto aim_dist = [&](int f, int k, const float* tip) {
+    const float fx = tip[0] - stone(k, 0), fy = tip[1] - (stone(k, 1) + Q.foot_offset_y[f]);
+    return sqrtf(fx * fx + fy * fy);
+  };
   float rp[3], rq[4], lin[3], ang[3], a[AS_ACT_DIM];
   for (int k = 0; k < 3; ++k) {
     rp[k] = st.root_pos[k * n + e];
@@ -2324,39 +2306,37 @@ __global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
     const float x = P.reset_all ? 0.f : P.actions[(size_t)e * nh + k];
     a[k] = fminf(fmaxf(x, -1.f), 1.f);
   }
-  int idx = st.idx[e], count = st.count[e], swing = st.swing[e], ep_len = st.ep_len[e];
+  int idx = st.idx[e], ep_len = st.ep_len[e], t[4], c[4];
+  for (int f = 0; f < 4; ++f) {
+    t[f] = st.feet[f * n + e];
+    c[f] = st.feet[(4 + f) * n + e];
+  }
   uint32_t episode = st.episode[e];
   uint32_t mk[4] = {st.contact_mask[e], st.contact_mask[n + e], st.contact_mask_hind[e], st.contact_mask_hind[n + e]};
   float pot = st.pot[e], old_pot = st.old_pot[e];
   bool term = false, trunc = false;
   if (!P.reset_all) {
     ep_len += 1;
-    // target tick (allsteps_env.py:418-440) for the swing foot f: front feet aim at stone idx, hind
-    // feet at idx - 1; reached = f pushes on its target stone, its tip within step_radius (xy) of the
-    // aim point (stone centre + (0, foot_offset_y[f]))
-    const int f = swing, tgt = f < 2 ? idx : idx - 1;
-    const uint32_t mf = f == 0 ? mk[0] : f == 1 ? mk[1] : f == 2 ? mk[2] : mk[3];
-    int g = 0;
-    for (int j = 0; j < m.num_geoms; ++j)
-      if (m.geom_foot[j] == f) { g = j; break; }
-    float tip[3];
-    as_link_point(m.parent, m.cfg_dof_link, nh, &m.offset_pos[0][0], &m.offset_quat[0][0], &m.axis[0][0],
-                  &m.anchor[0][0], st.q + e, n, m.geom_link[g], rp, rq, m.geom_p1[g], tip);
-    const float fx = tip[0] - stone(tgt, 0), fy = tip[1] - (stone(tgt, 1) + Q.foot_offset_y[f]);
-    const float d = sqrtf(fx * fx + fy * fy);
-    const bool reached = ((mf >> tgt) & 1u) && d < Q.step_radius;
-    if (reached) count += 1;
-    if (count >= Q.stop_frames) {  // the next foot of the gait; after the hind-left foot, the next stone
-      count = 0;
-      if (swing == 3) idx = min(idx + 1, N - 1);
-      swing = (swing + 1) & 3;
+    // target tick per foot (allsteps_env.py:418-440) and the step reward of a fresh reach (:377-380)
+    float step_hit = 0.f, fsum = 0.f;
+    for (int f = 0; f < 4; ++f) {
+      float tip[3];
+      quad_tip(m, st, n, e, f, rp, rq, tip);
+      const float d = aim_dist(f, t[f], tip);
+      const bool reached = ((mk[f] >> t[f]) & 1u) && d < Q.step_radius;
+      if (reached) c[f] += 1;
+      if (c[f] >= Q.stop_frames) {
+        c[f] = 0;
+        t[f] = min(t[f] + 1, N - 1);
+      }
+      if (reached && c[f] == 1 && t[f] < N - 1) step_hit += Q.step_reward * as_expf(-d / Q.step_sigma);
+      fsum += aim_dist(f, t[f], tip);  // to the (updated) target: the potential
     }
-    // step reward on a fresh reach (allsteps_env.py:377-380)
-    const float step_hit = reached && count == 1 && idx < N - 1 ? Q.step_reward * as_expf(-d / Q.step_sigma) : 0.f;
+    idx = min(t[0], t[1]);
     old_pot = pot;
     const float dx = stone(idx, 0) - rp[0], dy = stone(idx, 1) - rp[1];
     const float bd = sqrtf(dx * dx + dy * dy);
-    pot = -bd / Q.step_dt;
+    pot = -(bd + Q.foot_progress * fsum) / Q.step_dt;
     const float down[3] = {0.f, 0.f, -1.f};
     float gb[3];
     quat_rotate_inverse(rq, down, gb);
@@ -2402,12 +2382,18 @@ __global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
       st.root_ang[k * n + e] = 0.f;
     }
     for (int k = 0; k < 4; ++k) st.root_quat[k * n + e] = rq[k];
-    idx = min(2, N - 1);
-    count = 0;
-    swing = 0;
     ep_len = 0;
+    float fsum = 0.f;
+    for (int f = 0; f < 4; ++f) {
+      t[f] = min(f < 2 ? 2 : 1, N - 1);
+      c[f] = 0;
+      float tip[3];
+      quad_tip(m, st, n, e, f, rp, rq, tip);  // the reset pose (q written above)
+      fsum += aim_dist(f, t[f], tip);
+    }
+    idx = min(t[0], t[1]);
     const float dx = stone(idx, 0) - rp[0], dy = stone(idx, 1) - rp[1];
-    pot = -sqrtf(dx * dx + dy * dy) / Q.step_dt;
+    pot = -(sqrtf(dx * dx + dy * dy) + Q.foot_progress * fsum) / Q.step_dt;
     old_pot = pot;
     for (int k = 0; k < 4; ++k) mk[k] = 0u;
     st.contact_mask[e] = 0u;
@@ -2416,15 +2402,16 @@ __global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
     st.contact_mask_hind[n + e] = 0u;
   }
   st.idx[e] = idx;
-  st.count[e] = count;
-  st.swing[e] = swing;
+  for (int f = 0; f < 4; ++f) {
+    st.feet[f * n + e] = t[f];
+    st.feet[(4 + f) * n + e] = c[f];
+  }
   st.ep_len[e] = ep_len;
   st.episode[e] = episode;
   st.pot[e] = pot;
   st.old_pot[e] = old_pot;
-  // observation [62]: lin / ang velocity (body), projected gravity, stones idx - 1 / idx / idx + 1
-  // relative to the root (body), swing one-hot, each foot on its own target stone, q - default, qd,
-  // actions
+  // observation [64]: lin / ang velocity (body), projected gravity, each foot's aim point and stone
+  // idx + 1 relative to the root (body), each foot on its target stone, q - default, qd, actions
   float* o = P.obs + (size_t)e * AS_QUAD_OBS_DIM;
   float v[3];
   quat_rotate_inverse(rq, lin, v);
@@ -2434,20 +2421,18 @@ __global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
   const float down[3] = {0.f, 0.f, -1.f};
   quat_rotate_inverse(rq, down, v);
   o[6] = v[0]; o[7] = v[1]; o[8] = v[2];
-  for (int t = 0; t < 3; ++t) {
-    const int k = min(max(idx - 1 + t, 0), N - 1);
-    const float d[3] = {stone(k, 0) - rp[0], stone(k, 1) - rp[1], stone(k, 2) - rp[2]};
+  for (int f = 0; f < 5; ++f) {
+    const int k = f < 4 ? t[f] : min(idx + 1, N - 1);
+    const float oy = f < 4 ? Q.foot_offset_y[f] : 0.f;
+    const float d[3] = {stone(k, 0) - rp[0], (stone(k, 1) + oy) - rp[1], stone(k, 2) - rp[2]};
     quat_rotate_inverse(rq, d, v);
-    o[9 + 3 * t] = v[0]; o[10 + 3 * t] = v[1]; o[11 + 3 * t] = v[2];
+    o[9 + 3 * f] = v[0]; o[10 + 3 * f] = v[1]; o[11 + 3 * f] = v[2];
   }
-  for (int f = 0; f < 4; ++f) {
-    o[18 + f] = swing == f ? 1.f : 0.f;
-    o[22 + f] = (mk[f] >> (f < 2 ? idx : idx - 1)) & 1u ? 1.f : 0.f;
-  }
+  for (int f = 0; f < 4; ++f) o[24 + f] = (mk[f] >> t[f]) & 1u ? 1.f : 0.f;
   for (int k = 0; k < nh; ++k) {
-    o[26 + k] = q[k] - K.act.default_q[k];
-    o[26 + nh + k] = qd[k];
-    o[26 + 2 * nh + k] = was_reset ? 0.f : a[k];  // _reset_idx zeroes _actions (anymal_c_env.py:171-172)
+    o[28 + k] = q[k] - K.act.default_q[k];
+    o[28 + nh + k] = qd[k];
+    o[28 + 2 * nh + k] = was_reset ? 0.f : a[k];  // _reset_idx zeroes _actions (anymal_c_env.py:171-172)
   }
 }
 

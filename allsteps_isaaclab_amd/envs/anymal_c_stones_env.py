@@ -5,7 +5,7 @@ One ``step(actions)`` is ``as_quad_step`` on the HIP device: ``decimation`` subs
 (6 + 12 generalized velocities) with IsaacLab's DC motor evaluated in every substep on the position targets
 ``default_q + action_scale * a`` (anymal_c_env.py:73-78), four foot sensors, then ``k_quad``: target
 stones, potentials, rewards, dones, in-kernel resets of done envs (stand pose + Philox joint noise, actions
-observed as zero: anymal_c_env.py:171-172) and the 62-float observation.  Simulation settings are ANYmal-C's
+observed as zero: anymal_c_env.py:171-172) and the 64-float observation.  Simulation settings are ANYmal-C's
 (``AnymalCStonesEnvCfg``: dt 1/200, friction 1.0 multiply, max depenetration velocity 1.0).  There is no
 CPU fallback: without the HIP library or a gfx950 device the constructor raises ``NativeError``.
 """
@@ -66,6 +66,7 @@ class AnymalCStonesEnv(DirectRLEnv):
                                            dtype=torch.float32 if t == "f" else torch.int32)
         self.state["curriculum"] = torch.zeros(1, dtype=torch.int32, device=dev)
         self.state["contact_mask_hind"] = torch.zeros((2, n), dtype=torch.int32, device=dev)  # sensors RH, LH
+        self.state["feet"] = torch.zeros((8, n), dtype=torch.int32, device=dev)  # per-foot targets | reach counts
         self.state["stones"][:] = torch.as_tensor(level0_stones(n, cfg.num_steps), device=dev)
         with torch.cuda.device(dev):
             self._native = _native.NativeEnv(n, self.model, cfg, self.state, int(cfg.seed or 0),
@@ -104,9 +105,9 @@ class AnymalCStonesEnv(DirectRLEnv):
         return self.state["idx"]
 
     @property
-    def swing_leg(self) -> torch.Tensor:
-        """the swing foot of the gait, sensor order 0..3 = RF, LF, RH, LH (front target idx, hind idx - 1)"""
-        return self.state["swing"]
+    def foot_targets(self) -> torch.Tensor:
+        """(N, 4) target stone of each sensor foot (RF, LF, RH, LH); target_index is the front pair's min"""
+        return self.state["feet"][:4].T
 
     @property
     def contact_mask(self) -> torch.Tensor:

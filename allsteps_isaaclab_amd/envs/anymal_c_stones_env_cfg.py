@@ -15,11 +15,12 @@ The simulation and robot fields follow the reference's ANYmal-C direct task and 
   weights are Nucleus-only (``anymal.py:47``); the DC motor is the documented analytical stand-in.
 
 The stepping-stone task itself is authored (the reference has no quadruped stepping-stone task; DESIGN.md
-§7b): stones as in Allsteps-v0 (20 boxes 0.5 x 0.8 x 0.225 m); the reference's target machine on four feet (the
-swing foot cycles RF, LF, RH, LH; front feet aim at stone idx, hind feet at idx - 1; a swing foot that
-pushes on its stone within ``step_radius`` of its aim point for ``stop_frames`` steps hands over to the
-next foot, and the hind-left foot's completes the cycle: idx + 1); the ALLSTEPS reward terms -- alive,
-potential progress, energy, action cost, step hit 50 exp(-d / 0.25), last-stone bonus, death cost
+§7b): stones as in Allsteps-v0 (20 boxes 0.5 x 0.8 x 0.225 m); the reference's target machine run per foot (every
+foot has its own target stone -- the front feet start aiming at stone 2, the hind feet at stone 1 -- and
+advances it after pushing on it within ``step_radius`` of its aim point for ``stop_frames`` steps; the
+front pair's common target is the env's target index); the ALLSTEPS reward terms -- alive, potential
+progress (body to the target stone, plus ``foot_progress`` x the feet's distances to their aim points),
+energy, action cost, step hit 50 exp(-d / 0.25) per foot, last-stone bonus, death cost
 (allsteps_env.py:347-394); death on tilt or a base height below the target stone.  The soft joint limits are data (``AnymalCStonesEnv
 .soft_joint_pos_limits``): as in IsaacLab they do not enter the physics (articulation.py:1262-1266 only
 stores them; PhysX gets the hard limits), and the direct ANYmal-C task never reads them.
@@ -65,7 +66,7 @@ class AnymalCStonesEnvCfg:
     decimation: int = 4
     action_scale: float = 0.5
     action_space: int = 12
-    observation_space: int = 62
+    observation_space: int = 64
     state_space: int = 0
     seed: int | None = 42
     is_finite_horizon: bool = False
@@ -90,6 +91,7 @@ class AnymalCStonesEnvCfg:
     step_sigma: float = 0.25
     target_bonus: float = 10.0    # allsteps_env.py:383, last stone with the body within 0.15 m
     bonus_radius: float = 0.15
+    foot_progress: float = 0.5    # weight of the feet's distances to their aim points in the potential
     # aim point of each sensor foot (RF, LF, RH, LH) on its stone: the centre + this lateral offset,
     # the feet's stance width in model/anymal_c.xml (hip 0.1 + abduction link 0.1 either side)
     foot_offset_y: tuple = (-0.2, 0.2, -0.2, 0.2)
@@ -114,7 +116,8 @@ class AnymalCStonesEnvCfg:
                 "step_dt": float(np.float32(self.sim.dt * self.decimation)), "stand_height": self.stand_height,
                 "joint_noise": self.joint_noise, "energy_cost": self.energy_cost, "step_radius": self.step_radius,
                 "step_reward": self.step_reward, "step_sigma": self.step_sigma, "target_bonus": self.target_bonus,
-                "bonus_radius": self.bonus_radius, "foot_offset_y": list(self.foot_offset_y)}
+                "bonus_radius": self.bonus_radius, "foot_progress": self.foot_progress,
+                "foot_offset_y": list(self.foot_offset_y)}
 
     def actuator(self) -> dict:
         r = self.robot

@@ -99,3 +99,30 @@ register(
         "rl_games_cfg_entry_point": "allsteps_isaaclab_amd.agents:rl_games_anymal_c_stones_ppo_cfg.yaml",
     },
 )
+
+
+def _set(obj, path: list[str], value) -> None:
+    for k in path[:-1]:
+        obj = obj[k] if isinstance(obj, dict) else getattr(obj, k)
+    if isinstance(obj, dict):
+        obj[path[-1]] = value
+    else:
+        if not hasattr(obj, path[-1]):
+            raise AttributeError(f"{type(obj).__name__} has no field {path[-1]!r}")
+        setattr(obj, path[-1], value)
+
+
+def apply_overrides(env_cfg, agent_cfg, overrides: list[str]) -> None:
+    """Hydra-style command-line overrides (``env.<path>=<value>`` / ``agent.<path>=<value>``, values
+    parsed as YAML scalars) -- how Isaac Lab's hydra integration addresses the two configs."""
+    import yaml
+
+    for ov in overrides:
+        key, sep, val = ov.partition("=")
+        if not sep or "." not in key:
+            raise ValueError(f"unsupported override {ov!r} (expected env.<path>=<value> or agent.<path>=<value>)")
+        root, *path = key.lstrip("+").split(".")
+        target = {"env": env_cfg, "agent": agent_cfg}.get(root)
+        if target is None:
+            raise ValueError(f"override {ov!r} must start with env. or agent.")
+        _set(target, path, yaml.safe_load(val))

@@ -41,7 +41,7 @@ extern "C" {
 #define AS_MAX_ROWS 30
 #define AS_OBS_DIM 59
 #define AS_ACT_DIM 21
-#define AS_QUAD_OBS_DIM 62
+#define AS_QUAD_OBS_DIM 64
 
 enum {
   AS_OK = 0,
@@ -149,6 +149,8 @@ typedef struct {
   uint32_t* contact_mask; /* [2][n] per-foot bitmask of stones with force > eps, last substep */
   int32_t* curriculum;  /* [1] */
   uint32_t* contact_mask_hind; /* [2][n] contact sensors 2 and 3 (a quadruped's hind feet), or NULL */
+  int32_t* feet;        /* [8][n] the quadruped task's per-foot target stones (rows 0..3, sensor order)
+                           and reach counts (rows 4..7), or NULL (the walker) */
 } as_state_t;
 
 /* Actuation of the physics step (as_set_actuator; as_create starts in AS_ACT_TORQUE).
@@ -170,27 +172,28 @@ typedef struct {
 } as_actuator_t;
 
 /* The BASELINE C5 task: a quadruped crossing the Allsteps stones with the ALLSTEPS reward terms
- * (allsteps_env.py:347-394) and the reference's target machine (:418-457) carried over to four feet
- * (authored here -- the reference has no quadruped stepping-stone task; its ANYmal-C task is flat-ground
- * velocity tracking).  Per env step, after the physics substeps:
- *   gait: the swing foot cycles through the sensors 0..3 (RF, LF, RH, LH); a front foot's target is
- *     stone idx, a hind foot's stone idx - 1 (idx = state.idx, 2 after a reset: hind feet on stone 0,
- *     front feet on stone 1); the swing foot f's aim point is its target stone's centre + (0,
- *     foot_offset_y[f]) and its position is the tip of its sensor geom (the capsule end p1, FK from q);
- *   target tick (allsteps_env.py:418-440): reached = f pushes on its target stone (contact mask bit)
- *     and its xy distance d to the aim point < step_radius; count += reached; count >= stop_frames:
- *     count = 0, swing = (swing + 1) mod 4, and after the hind-left foot (swing 3) idx += 1 (clamped);
- *   potential (:441-448): pot = -|stone[idx] - root|_xy / step_dt;
+ * (allsteps_env.py:347-394) and the reference's target machine (:418-457) run per foot (authored here --
+ * the reference has no quadruped stepping-stone task; its ANYmal-C task is flat-ground velocity
+ * tracking).  Per env step, after the physics substeps:
+ *   feet: every sensor foot f (0..3 = RF, LF, RH, LH) has its own target stone t_f (state.feet rows
+ *     0..3; 2 for the front feet and 1 for the hind feet after a reset: they stand on stones 1 / 0) and
+ *     reach count c_f (rows 4..7); its aim point is stone t_f's centre + (0, foot_offset_y[f]), its
+ *     position the tip of its sensor geom (the capsule end p1, FK from q: as_link_point);
+ *   target tick per foot (allsteps_env.py:418-440): reached = f pushes on t_f (contact mask bit) and
+ *     its xy distance d to the aim point < step_radius; c_f += reached; c_f >= stop_frames: c_f = 0,
+ *     t_f += 1 (clamped); the front pair's target idx = min(t_RF, t_LF) (state.idx);
+ *   potential (:441-448): pot = -(|stone[idx] - root|_xy + foot_progress sum_f d_f) / step_dt, d_f
+ *     the foot's distance to its (updated) aim point;
  *   terminated = body tilted past up_z_min or below the target stone + min_height; truncated at
  *     max_episode_length;
  *   reward (:347-394) = alive + (pot - old_pot) - energy_cost sum|qd a| - action_cost ||a||
- *     + step_reward exp(-d / step_sigma) on a fresh reach (count == 1, idx < num_steps - 1)
- *     + target_bonus when idx is the last stone and the root is within bonus_radius of it (xy);
- *     death on termination;
+ *     + sum_f step_reward exp(-d_f / step_sigma) over the feet with a fresh reach (c_f == 1, t_f <
+ *     num_steps - 1) + target_bonus when idx is the last stone and the root is within bonus_radius of
+ *     it (xy); death on termination;
  * reset of done envs to the stand pose over stones 0 / 1 (+ U(-1,1) * joint_noise, Philox); observation
- * [62] = root linear / angular velocity (body frame), projected gravity, stones idx - 1, idx, idx + 1
- * relative to the root (body frame), the swing foot one-hot [4], each foot's contact with its own
- * target stone [4], q - default_q, qd, the clipped actions. */
+ * [64] = root linear / angular velocity (body frame), projected gravity, each foot's aim point and
+ * stone idx + 1 relative to the root (body frame), each foot's contact with its target stone [4],
+ * q - default_q, qd, the clipped actions. */
 typedef struct {
   int32_t stop_frames;
   float alive, action_cost, death;
@@ -205,6 +208,7 @@ typedef struct {
   float step_sigma;         /* 0.25 */
   float target_bonus;       /* 10 (allsteps_env.py:383) */
   float bonus_radius;       /* 0.15 */
+  float foot_progress;      /* weight of the feet's distances in the potential */
   float foot_offset_y[4];   /* aim point lateral offset per sensor foot (RF, LF, RH, LH) */
 } as_quad_task_t;
 

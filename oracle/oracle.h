@@ -121,6 +121,7 @@ typedef struct {
   uint32_t *contact_mask;                              /* [2][n] stone bitmask, last substep */
   int32_t *curriculum;                                 /* [1] */
   uint32_t *contact_mask_hind;                         /* [2][n] sensors 2, 3 (quadruped) or NULL */
+  int32_t *feet;                                       /* [8][n] quadruped per-foot targets / counts or NULL */
 } or_state_t;
 
 /* include/allsteps.h as_actuator_t / as_quad_task_t, field for field */
@@ -139,7 +140,7 @@ typedef struct {
   float step_dt;
   float stand_height;
   float joint_noise;
-  float energy_cost, step_radius, step_reward, step_sigma, target_bonus, bonus_radius;
+  float energy_cost, step_radius, step_reward, step_sigma, target_bonus, bonus_radius, foot_progress;
   float foot_offset_y[4];
 } or_quad_task_t;
 

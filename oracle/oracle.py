@@ -79,7 +79,7 @@ class OrState(C.Structure):
         ("n", C.c_int32), ("root_pos", FP), ("root_quat", FP), ("root_lin", FP), ("root_ang", FP), ("q", FP),
         ("qd", FP), ("stones", FP), ("pot", FP), ("old_pot", FP), ("foot_contact", FP), ("body_pos", FP),
         ("idx", IP), ("prev", IP), ("next", IP), ("count", IP), ("swing", IP), ("ep_len", IP), ("episode", UP),
-        ("contact_mask", UP), ("curriculum", IP), ("contact_mask_hind", UP),
+        ("contact_mask", UP), ("curriculum", IP), ("contact_mask_hind", UP), ("feet", IP),
     ]
 
 
@@ -89,7 +89,7 @@ class OrActuator(C.Structure):
                 ("effort_limit", C.c_float), ("velocity_limit", C.c_float)]
 
 
-QUAD_OBS = 62  # include/allsteps.h AS_QUAD_OBS_DIM
+QUAD_OBS = 64  # include/allsteps.h AS_QUAD_OBS_DIM
 
 
 class OrQuadTask(C.Structure):
@@ -98,7 +98,7 @@ class OrQuadTask(C.Structure):
                 ("step_dt", C.c_float), ("stand_height", C.c_float), ("joint_noise", C.c_float),
                 ("energy_cost", C.c_float), ("step_radius", C.c_float), ("step_reward", C.c_float),
                 ("step_sigma", C.c_float), ("target_bonus", C.c_float), ("bonus_radius", C.c_float),
-                ("foot_offset_y", C.c_float * 4)]
+                ("foot_progress", C.c_float), ("foot_offset_y", C.c_float * 4)]
 
 
 def build() -> str:
@@ -216,7 +216,7 @@ class OracleState:
 
     FIELDS_F = {"root_pos": 3, "root_quat": 4, "root_lin": 3, "root_ang": 3, "q": 21, "qd": 21, "stones": 60,
                 "pot": 1, "old_pot": 1, "foot_contact": 2, "body_pos": 9}
-    FIELDS_I = {"idx": 1, "prev": 1, "next": 1, "count": 1, "swing": 1, "ep_len": 1}
+    FIELDS_I = {"idx": 1, "prev": 1, "next": 1, "count": 1, "swing": 1, "ep_len": 1, "feet": 8}
     FIELDS_U = {"episode": 1, "contact_mask": 2, "contact_mask_hind": 2}
 
     def __init__(self, n: int):

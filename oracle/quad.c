@@ -7,7 +7,7 @@
  * authored here from the Allsteps task's pieces (target stones, potentials, allsteps_env.py:347-457)
  * and the ANYmal task's actuation / observation terms (anymal_c_env.py:73-110): the ALLSTEPS reward
  * terms (step hit, progress, energy, alive, target bonus; allsteps_env.py:347-394) and the target machine
- * (:418-457) carried over to four feet, the swing foot cycling RF, LF, RH, LH.  PARITY UNPINNED
+ * (:418-457) run per foot (each foot its own target stone and reach count).  PARITY UNPINNED
  * against any reference output; the HIP kernel is checked against this file bit for bit.
  */
 #include <math.h>
@@ -18,9 +18,19 @@
 
 #define F(arr, f, n, e) (arr)[(size_t)(f) * (n) + (e)]
 #define QUAD_TAG 0x51756164u /* "Quad" */
-#define QUAD_OBS 62
+#define QUAD_OBS 64
 
 static int imin(int a, int b) { return a < b ? a : b; }
+
+/* foot f's tip (its sensor geom's capsule end p1) in env e, root pose (rp, rq) */
+static void quad_tip(const or_model_t* m, const or_state_t* st, int e, int f, const float* rp, const float* rq,
+                     float* tip) {
+  int g = 0;
+  for (int j = 0; j < m->num_geoms; ++j)
+    if (m->geom_foot[j] == f) { g = j; break; }
+  as_link_point(m->parent, m->cfg_dof_link, m->num_hinges, &m->offset_pos[0][0], &m->offset_quat[0][0],
+                &m->axis[0][0], &m->anchor[0][0], st->q + e, st->n, m->geom_link[g], rp, rq, m->geom_p1[g], tip);
+}
 
 void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
                           const or_quad_task_t* Q, or_state_t* st, const float* actions, int reset_all,
@@ -29,6 +39,9 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
   const float half_z = sim->stone_half[2];
   for (int e = 0; e < n; ++e) {
 #define STONE(k, c) F(st->stones, 3 * (k) + (c), n, e)
+#define AIM_DIST(f, k, tip) \
+  sqrtf(((tip)[0] - STONE(k, 0)) * ((tip)[0] - STONE(k, 0)) + \
+        ((tip)[1] - (STONE(k, 1) + Q->foot_offset_y[f])) * ((tip)[1] - (STONE(k, 1) + Q->foot_offset_y[f])))
     float rp[3], rq[4], lin[3], ang[3], a[21];
     for (int k = 0; k < 3; ++k) {
       rp[k] = F(st->root_pos, k, n, e);
@@ -40,7 +53,11 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
       const float x = reset_all ? 0.f : actions[(size_t)e * nh + k];
       a[k] = fminf(fmaxf(x, -1.f), 1.f);
     }
-    int idx = st->idx[e], count = st->count[e], swing = st->swing[e], ep_len = st->ep_len[e];
+    int idx = st->idx[e], ep_len = st->ep_len[e], t[4], c[4];
+    for (int f = 0; f < 4; ++f) {
+      t[f] = F(st->feet, f, n, e);
+      c[f] = F(st->feet, 4 + f, n, e);
+    }
     uint32_t episode = st->episode[e];
     uint32_t mk[4] = {F(st->contact_mask, 0, n, e), F(st->contact_mask, 1, n, e), F(st->contact_mask_hind, 0, n, e),
                       F(st->contact_mask_hind, 1, n, e)};
@@ -48,30 +65,26 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
     int term = 0, trunc = 0;
     if (!reset_all) {
       ep_len += 1;
-      /* ENV:418-440 target tick for the swing foot f: front feet aim at stone idx, hind feet at idx - 1;
-       * reached = contact with the target stone and the foot tip within step_radius (xy) of the aim point */
-      const int f = swing, tgt = f < 2 ? idx : idx - 1;
-      int g = 0;
-      for (int j = 0; j < m->num_geoms; ++j)
-        if (m->geom_foot[j] == f) { g = j; break; }
-      float tip[3];
-      as_link_point(m->parent, m->cfg_dof_link, nh, &m->offset_pos[0][0], &m->offset_quat[0][0], &m->axis[0][0],
-                    &m->anchor[0][0], st->q + e, n, m->geom_link[g], rp, rq, m->geom_p1[g], tip);
-      const float fx = tip[0] - STONE(tgt, 0), fy = tip[1] - (STONE(tgt, 1) + Q->foot_offset_y[f]);
-      const float d = sqrtf(fx * fx + fy * fy);
-      const int reached = ((mk[f] >> tgt) & 1u) && d < Q->step_radius;
-      if (reached) count += 1;
-      if (count >= Q->stop_frames) {
-        count = 0;
-        if (swing == 3) idx = imin(idx + 1, N - 1);
-        swing = (swing + 1) & 3;
+      /* ENV:418-440 target tick per foot; ENV:377-380 step reward of a fresh reach */
+      float step_hit = 0.f, fsum = 0.f;
+      for (int f = 0; f < 4; ++f) {
+        float tip[3];
+        quad_tip(m, st, e, f, rp, rq, tip);
+        const float d = AIM_DIST(f, t[f], tip);
+        const int reached = ((mk[f] >> t[f]) & 1u) && d < Q->step_radius;
+        if (reached) c[f] += 1;
+        if (c[f] >= Q->stop_frames) {
+          c[f] = 0;
+          t[f] = imin(t[f] + 1, N - 1);
+        }
+        if (reached && c[f] == 1 && t[f] < N - 1) step_hit += Q->step_reward * as_expf(-d / Q->step_sigma);
+        fsum += AIM_DIST(f, t[f], tip);
       }
-      /* ENV:377-380 step reward on a fresh reach */
-      const float step_hit = reached && count == 1 && idx < N - 1 ? Q->step_reward * as_expf(-d / Q->step_sigma) : 0.f;
+      idx = imin(t[0], t[1]);
       old_pot = pot;
       const float dx = STONE(idx, 0) - rp[0], dy = STONE(idx, 1) - rp[1];
       const float bd = sqrtf(dx * dx + dy * dy);
-      pot = -bd / Q->step_dt;
+      pot = -(bd + Q->foot_progress * fsum) / Q->step_dt;
       const float down[3] = {0.f, 0.f, -1.f};
       float gb[3];
       or_quat_rotate_inverse(rq, down, gb);
@@ -116,20 +129,28 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
         F(st->root_ang, k, n, e) = 0.f;
       }
       for (int k = 0; k < 4; ++k) F(st->root_quat, k, n, e) = rq[k];
-      idx = imin(2, N - 1);
-      count = 0;
-      swing = 0;
       ep_len = 0;
+      float fsum = 0.f;
+      for (int f = 0; f < 4; ++f) {
+        t[f] = imin(f < 2 ? 2 : 1, N - 1);
+        c[f] = 0;
+        float tip[3];
+        quad_tip(m, st, e, f, rp, rq, tip); /* the reset pose (q written above) */
+        fsum += AIM_DIST(f, t[f], tip);
+      }
+      idx = imin(t[0], t[1]);
       const float dx = STONE(idx, 0) - rp[0], dy = STONE(idx, 1) - rp[1];
-      pot = -sqrtf(dx * dx + dy * dy) / Q->step_dt;
+      pot = -(sqrtf(dx * dx + dy * dy) + Q->foot_progress * fsum) / Q->step_dt;
       old_pot = pot;
       for (int k = 0; k < 4; ++k) mk[k] = 0u;
       F(st->contact_mask, 0, n, e) = F(st->contact_mask, 1, n, e) = 0u;
       F(st->contact_mask_hind, 0, n, e) = F(st->contact_mask_hind, 1, n, e) = 0u;
     }
     st->idx[e] = idx;
-    st->count[e] = count;
-    st->swing[e] = swing;
+    for (int f = 0; f < 4; ++f) {
+      F(st->feet, f, n, e) = t[f];
+      F(st->feet, 4 + f, n, e) = c[f];
+    }
     st->ep_len[e] = ep_len;
     st->episode[e] = episode;
     st->pot[e] = pot;
@@ -143,22 +164,20 @@ void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_tas
     const float down[3] = {0.f, 0.f, -1.f};
     or_quat_rotate_inverse(rq, down, v);
     o[6] = v[0]; o[7] = v[1]; o[8] = v[2];
-    for (int t = 0; t < 3; ++t) {
-      int k = idx - 1 + t;
-      k = k < 0 ? 0 : (k > N - 1 ? N - 1 : k);
-      const float d[3] = {STONE(k, 0) - rp[0], STONE(k, 1) - rp[1], STONE(k, 2) - rp[2]};
+    for (int f = 0; f < 5; ++f) {
+      const int k = f < 4 ? t[f] : imin(idx + 1, N - 1);
+      const float oy = f < 4 ? Q->foot_offset_y[f] : 0.f;
+      const float d[3] = {STONE(k, 0) - rp[0], (STONE(k, 1) + oy) - rp[1], STONE(k, 2) - rp[2]};
       or_quat_rotate_inverse(rq, d, v);
-      o[9 + 3 * t] = v[0]; o[10 + 3 * t] = v[1]; o[11 + 3 * t] = v[2];
+      o[9 + 3 * f] = v[0]; o[10 + 3 * f] = v[1]; o[11 + 3 * f] = v[2];
     }
-    for (int f = 0; f < 4; ++f) {
-      o[18 + f] = swing == f ? 1.f : 0.f;
-      o[22 + f] = (mk[f] >> (f < 2 ? idx : idx - 1)) & 1u ? 1.f : 0.f;
-    }
+    for (int f = 0; f < 4; ++f) o[24 + f] = (mk[f] >> t[f]) & 1u ? 1.f : 0.f;
     for (int k = 0; k < nh; ++k) {
-      o[26 + k] = q[k] - act->default_q[k];
-      o[26 + nh + k] = qd[k];
-      o[26 + 2 * nh + k] = was_reset ? 0.f : a[k]; /* _reset_idx zeroes _actions (anymal_c_env.py:171-172) */
+      o[28 + k] = q[k] - act->default_q[k];
+      o[28 + nh + k] = qd[k];
+      o[28 + 2 * nh + k] = was_reset ? 0.f : a[k]; /* _reset_idx zeroes _actions (anymal_c_env.py:171-172) */
     }
+#undef AIM_DIST
 #undef STONE
   }
 }

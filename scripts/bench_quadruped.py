@@ -5,7 +5,7 @@
 A step = ``AnymalCStonesEnv.step`` (``Allsteps-AnymalC-v0``, ANYmal-C's sim settings: dt 1/200, friction
 1.0, max depenetration velocity 1.0) = as_quad_step: 4 substeps of k_step<18> for every env with the DC
 motor actuator evaluated in each substep (position targets default + 0.5 a), then k_quad (target
-stones, potentials, rewards, dones, in-kernel resets, the 62-float observation).  Actions: U(-1, 1),
+stones, potentials, rewards, dones, in-kernel resets, the 64-float observation).  Actions: U(-1, 1),
 fresh every step (pre-drawn on the device).  Episodes end and reset inside the timed region.  Prints
 one JSON line.
 """

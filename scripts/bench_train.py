@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "scripts", "reinforcement_learning", "rl_g
 
 def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int | None = None,
             log_root: str = "/tmp/bench_train_logs", verbose: bool = True, distributed: bool = False,
-            multi_gpu_mode: str = "allgather") -> dict:
+            multi_gpu_mode: str = "allgather", overrides: list[str] | None = None) -> dict:
     """num_envs per rank; with distributed=True (under torch.distributed.run) every rank trains with
     train.py --distributed --multi_gpu_mode <mode> and the result counts all ranks' env-steps over the
     slowest rank's time.  "allgather" (default) is the north star's exchange: one RCCL all-gather of the
@@ -54,6 +54,7 @@ def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int 
             argv += ["--stone_level", str(level)]
         if distributed:
             argv += ["--distributed", "--multi_gpu_mode", multi_gpu_mode]
+        argv += list(overrides or [])
         if verbose:
             runner, _ = train.main(argv)
         else:  # keep stdout to the caller's single JSON line
@@ -106,7 +107,7 @@ def main():
     if bad:
         ap.error(f"unrecognized arguments: {' '.join(bad)}")
     out = measure(args.num_envs, args.epochs, args.warmup, args.level, verbose=not args.quiet,
-                  distributed=args.distributed, multi_gpu_mode=args.multi_gpu_mode)
+                  distributed=args.distributed, multi_gpu_mode=args.multi_gpu_mode, overrides=extra)
     import torch.distributed as dist
 
     if not (dist.is_initialized() and dist.get_rank() != 0):

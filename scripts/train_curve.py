@@ -2,8 +2,8 @@
 config, N envs, E epochs; prints per-epoch mean episode reward / length / curriculum target index as
 JSON lines (the evidence that physics + task + trainer learn together).
 
-    python scripts/train_curve.py [num_envs] [epochs] [every] [task]   (task: Allsteps-v0 or
-    Allsteps-AnymalC-v0, the C5 quadruped behind the same env surface)"""
+    python scripts/train_curve.py [num_envs] [epochs] [every] [task] [env.<k>=<v> | agent.<k>=<v> ...]
+    (task: Allsteps-v0 or Allsteps-AnymalC-v0, the C5 quadruped behind the same env surface)"""
 import json
 import os
 import sys
@@ -46,5 +46,6 @@ with open(os.devnull, "w") as dn:
 
     with contextlib.redirect_stdout(sys.stderr):
         pass
+# past the four positional arguments: hydra-style overrides (env.<path>=<value>, agent.<path>=<value>)
 train.main(["--task", TASK, "--num_envs", str(N), "--max_iterations", str(E), "--seed", "42",
-            "--log_root", "/tmp/curve_logs"])
+            "--log_root", "/tmp/curve_logs", *sys.argv[5:]])

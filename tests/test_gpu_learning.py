@@ -50,7 +50,7 @@ def test_train_script_runs_on_c5_quadruped(tmp_path):
                             "2", "--seed", "3", "--log_root", str(tmp_path)])
     agent = runner.agent
     assert agent.epoch_num == 2 and agent.frame == 2 * 1024 * 24
-    assert agent.obs_shape[0] == 51 and agent.actions_num == 12
+    assert agent.obs_shape[0] == 64 and agent.actions_num == 12
     for k in ("a_loss", "c_loss", "kl", "entropy", "lr"):
         assert math.isfinite(agent.last_stats[k]), (k, agent.last_stats)
     assert torch.isfinite(agent.flat.params).all()

@@ -110,20 +110,22 @@ def test_task_reset_pose_and_observation(qorc, oracle_mod, qmodel):
     q0 = stand_pose(qmodel["dof_names"])
     assert np.abs(st["q"][:12].T - q0).max() <= QUAD_TASK["joint_noise"]
     np.testing.assert_allclose(st["root_pos"][:, 0], [0.375, 0.0, 0.1125 + QUAD_TASK["stand_height"]], atol=1e-6)
-    assert (st["idx"] == 2).all() and (st["episode"] == 1).all() and (st["swing"] == 0).all()
+    assert (st["idx"] == 2).all() and (st["episode"] == 1).all()
+    assert (st["feet"][:4].T == [2, 2, 1, 1]).all() and (st["feet"][4:] == 0).all()
     obs, *_ = _post(qorc, oracle_mod, qmodel, st, np.zeros((n, 12), np.float32), reset_all=True)
-    assert obs.shape == (n, 62)
+    assert obs.shape == (n, 64)
     np.testing.assert_allclose(obs[:, 6:9], [[0, 0, -1]] * n, atol=1e-7)      # projected gravity, upright
-    for t, k in enumerate((1, 2, 3)):  # stones idx - 1, idx, idx + 1 in the body frame
-        np.testing.assert_allclose(obs[0, 9 + 3 * t:12 + 3 * t], [0.75 * k - 0.375, 0.0, -0.1125 - 0.584], atol=1e-5)
-    np.testing.assert_array_equal(obs[:, 18:22], [[1, 0, 0, 0]] * n)  # RF swings first
-    assert (obs[:, 22:26] == 0).all()                                 # contact masks cleared by the reset
+    off = QUAD_TASK["foot_offset_y"]
+    for f, k in enumerate((2, 2, 1, 1)):  # each foot's aim point, body frame
+        np.testing.assert_allclose(obs[0, 9 + 3 * f:12 + 3 * f], [0.75 * k - 0.375, off[f], -0.1125 - 0.584], atol=1e-5)
+    np.testing.assert_allclose(obs[0, 21:24], [0.75 * 3 - 0.375, 0.0, -0.1125 - 0.584], atol=1e-5)  # stone idx + 1
+    assert (obs[:, 24:28] == 0).all()                                 # contact masks cleared by the reset
     # different envs, different Philox joint noise; the same env and episode, the same draws
     assert np.abs(st["q"][:12, 0] - st["q"][:12, 1]).max() > 0
     # the feet stand on stones 0 (hind) / 1 (front) at their aim points' lateral offsets
     for f in range(4):
         tip = _tip(qorc, qmodel, st, 0, f)
-        assert abs(tip[0] - (0.75 if f < 2 else 0.0)) < 0.15 and abs(tip[1] - QUAD_TASK["foot_offset_y"][f]) < 0.05
+        assert abs(tip[0] - (0.75 if f < 2 else 0.0)) < 0.15 and abs(tip[1] - off[f]) < 0.05
 
 
 def test_link_point_is_the_physics_fk(qorc, oracle_mod, qmodel):
@@ -148,40 +150,41 @@ def _aim_stone_under(st, e, k, tip, f):
     st["stones"][3 * k + 1, e] = tip[1] - np.float32(QUAD_TASK["foot_offset_y"][f])
 
 
-def test_task_gait_tick_step_reward_and_cycle(qorc, oracle_mod, qmodel):
+def test_task_per_foot_tick_and_step_reward(qorc, oracle_mod, qmodel):
     n = 4
     st = _stand_state(qorc, oracle_mod, qmodel, n)
     a = np.zeros((n, 12), np.float32)
-    # env 0: RF (swing 0) pushes on its target stone 2, aim point under its tip: a fresh reach pays the
-    #        step reward, stop_frames steps hand the swing to LF with the target unchanged
+    # env 0: RF pushes on its target stone 2 with the aim point under its tip: a fresh reach pays the
+    #        step reward; after stop_frames steps RF aims at stone 3, the others keep theirs, idx stays 2
     # env 1: the same contact bit but the aim point 0.3 m away: no reach (step_radius 0.25)
-    # env 2: LH (swing 3) on stone idx - 1 = 1 completes the cycle: idx 3, swing back to RF
-    # env 3: RF touching the hind feet's stone 1 only: no reach
-    tip0, tip1 = _tip(qorc, qmodel, st, 0, 0), _tip(qorc, qmodel, st, 1, 0)
-    _aim_stone_under(st, 0, 2, tip0, 0)
-    _aim_stone_under(st, 1, 2, tip1 + np.float32([0.3, 0, 0]), 0)
-    st["swing"][2] = 3
-    _aim_stone_under(st, 2, 1, _tip(qorc, qmodel, st, 2, 3), 3)
+    # env 2: both front feet reach stone 2 (the aim points of both under their tips): idx -> 3
+    # env 3: LH on its target stone 1: the hind foot advances to stone 2
+    _aim_stone_under(st, 0, 2, _tip(qorc, qmodel, st, 0, 0), 0)
+    _aim_stone_under(st, 1, 2, _tip(qorc, qmodel, st, 1, 0) + np.float32([0.3, 0, 0]), 0)
+    t_rf, t_lf = _tip(qorc, qmodel, st, 2, 0), _tip(qorc, qmodel, st, 2, 1)
+    st["stones"][6:8, 2] = (0.5 * (t_rf + t_lf))[:2]  # RF / LF tips 0.4 apart: their aim points, +-0.2
+    _aim_stone_under(st, 3, 1, _tip(qorc, qmodel, st, 3, 3), 3)
     rewards = []
     for step in range(QUAD_TASK["stop_frames"]):
-        st["contact_mask"][0, :] = [1 << 2, 1 << 2, 0, 1 << 1]
-        st["contact_mask_hind"][1, 2] = 1 << 1
+        st["contact_mask"][0, :] = [1 << 2, 1 << 2, 1 << 2, 0]
+        st["contact_mask"][1, :] = [0, 0, 1 << 2, 0]
+        st["contact_mask_hind"][1, 3] = 1 << 1
         pot_before = st["pot"].copy()
         obs, rew, term, trunc = _post(qorc, oracle_mod, qmodel, st, a)
         assert not term.any() and not trunc.any()
         rewards.append(rew.copy())
-        if step == 0:  # the fresh reach: 50 exp(-d / 0.25) on top of alive + progress (zero actions)
+        if step == 0:  # the fresh reach: 50 exp(-d / 0.25) per foot on top of alive + progress (zero actions)
             base = np.float32(QUAD_TASK["alive"]) + (st["pot"] - pot_before)
-            assert rew[0] > base[0] + 45 and abs(rew[1] - base[1]) < 1e-5 and abs(rew[3] - base[3]) < 1e-5
+            assert rew[0] > base[0] + 45 and abs(rew[1] - base[1]) < 1e-4
+            assert rew[2] > base[2] + 85 and rew[3] > base[3] + 45
+    assert (st["feet"][:4].T == [[3, 2, 1, 1], [2, 2, 1, 1], [3, 3, 1, 1], [2, 2, 1, 2]]).all()
+    assert (st["feet"][4:] == 0).all()
     assert (st["idx"] == [2, 2, 3, 2]).all()
-    assert (st["swing"] == [1, 0, 0, 0]).all() and (st["count"] == 0).all()
     # the second frame of the same reach pays no step reward
-    assert rewards[1][0] < rewards[0][0] - 45
-    # obs: swing one-hot, and after the cycle env 2's stones are 2 / 3 / 4
-    np.testing.assert_array_equal(obs[0, 18:22], [0, 1, 0, 0])
-    np.testing.assert_array_equal(obs[2, 18:22], [1, 0, 0, 0])
-    np.testing.assert_allclose(obs[2, 12:15], [0.75 * 3 - st["root_pos"][0, 2], 0.0, -st["root_pos"][2, 2] + 0.0],
-                               atol=1e-5)
+    assert rewards[1][0] < rewards[0][0] - 40
+    # obs: env 0's RF aim point is now on stone 3; env 2's lookahead stone is idx + 1 = 4
+    np.testing.assert_allclose(obs[0, 9:11], [0.75 * 3 - st["root_pos"][0, 0], QUAD_TASK["foot_offset_y"][0]], atol=1e-5)
+    np.testing.assert_allclose(obs[2, 21], 0.75 * 4 - st["root_pos"][0, 2], atol=1e-5)
 
 
 def test_task_potential_costs_and_dones(qorc, oracle_mod, qmodel):
@@ -200,6 +203,7 @@ def test_task_potential_costs_and_dones(qorc, oracle_mod, qmodel):
     a[3] = 0.5
     st["qd"][:12, 3] = np.linspace(-2, 2, 12, dtype=np.float32)
     st["idx"][4] = 19
+    st["feet"][:2, 4] = 19
     st["root_pos"][:2, 4] = [0.75 * 19 + 0.1, 0.0]
     qd3 = st["qd"][:12, 3].copy()
     pot_before = st["pot"].copy()
@@ -208,10 +212,11 @@ def test_task_potential_costs_and_dones(qorc, oracle_mod, qmodel):
     assert trunc.tolist() == [False, False, True, False, False]
     assert rew[0] == QUAD_TASK["death"] and rew[1] == QUAD_TASK["death"]
     # reset envs observe zero actions (anymal_c_env.py:171-172 zeroes _actions in _reset_idx); live ones theirs
-    assert (obs[[0, 1, 2], 26 + 24:] == 0).all()
-    assert (obs[3, 26 + 24:] == 0.5).all()
-    for e in (0, 1, 2):  # done envs were reset: stand pose, target 2, swing RF, episode counter advanced
-        assert st["idx"][e] == 2 and st["swing"][e] == 0 and st["ep_len"][e] == 0 and st["episode"][e] == 2
+    assert (obs[[0, 1, 2], 28 + 24:] == 0).all()
+    assert (obs[3, 28 + 24:] == 0.5).all()
+    for e in (0, 1, 2):  # done envs were reset: stand pose, targets 2 / 1, episode counter advanced
+        assert st["idx"][e] == 2 and (st["feet"][:4, e] == [2, 2, 1, 1]).all() and st["ep_len"][e] == 0
+        assert st["episode"][e] == 2
         np.testing.assert_array_equal(st["root_quat"][:, e], [1, 0, 0, 0])
     prog = np.float32(st["pot"][3]) - np.float32(pot_before[3])
     en = np.float32(np.abs(qd3 * np.float32(0.5)).sum())
@@ -253,7 +258,7 @@ def test_c5_cfg_is_anymal_c():
     assert c.sim.dt == 1.0 / 200.0 and c.decimation == 4 and c.sim.friction == 1.0
     assert c.sim.max_depenetration_velocity == 1.0 and c.sim.solver_position_iteration_count == 4
     assert c.robot.soft_joint_pos_limit_factor == 0.95 and c.max_episode_length == 1000
-    assert c.scene.num_envs == 16384 and c.action_space == 12 and c.observation_space == 62
+    assert c.scene.num_envs == 16384 and c.action_space == 12 and c.observation_space == 64
     assert np.float32(c.quad_task()["step_dt"]) == np.float32(4 / 200)
     o = __import__("oracle").Oracle(cfg=c, model=__import__("allsteps_isaaclab_amd.model", fromlist=["x"]).load_model(
         __import__("allsteps_isaaclab_amd.model", fromlist=["x"]).ANYMAL_C_JSON))
