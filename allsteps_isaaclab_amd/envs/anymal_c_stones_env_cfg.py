@@ -4,7 +4,8 @@ simulation settings.
 The simulation and robot fields follow the reference's ANYmal-C direct task and asset, not the walker's:
 
 * ``direct/anymal_c/anymal_c_env_cfg.py:51-95`` (``AnymalCFlatEnvCfg``): episode 20 s, decimation 4,
-  action scale 0.5, 12 actions, ``SimulationCfg(dt=1/200)``, physics material static = dynamic friction
+  12 actions (its action scale 0.5 is raised to 1.0 here: the stones' stride needs the range),
+  ``SimulationCfg(dt=1/200)``, physics material static = dynamic friction
   1.0 with the "multiply" combine mode on both the robot's default material and the terrain -- the
   contact friction is 1.0 x 1.0 = 1.0 (the walker uses 0.85 from the "average" combine);
 * ``isaaclab_assets/robots/anymal.py`` ``ANYMAL_C_CFG``: rigid bodies with max_depenetration_velocity
@@ -64,7 +65,10 @@ class AnymalCStonesEnvCfg:
     # env (anymal_c_env_cfg.py AnymalCFlatEnvCfg)
     episode_length_s: float = 20.0
     decimation: int = 4
-    action_scale: float = 0.5
+    # anymal_c_env_cfg.py uses 0.5 for flat-ground velocity tracking; position targets within +-0.5 rad
+    # of the stance cannot make the 0.75 m stride of the stones (the leg must reach 0.45 m behind and
+    # ahead of its hip), and a 1000-epoch run at 0.5 only learns to stand (DESIGN.md §7b, r04d curves)
+    action_scale: float = 1.0
     action_space: int = 12
     observation_space: int = 64
     state_space: int = 0
