@@ -736,11 +736,16 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
 __global__ void k_tail(double* lr, const float* kl, float thr, double min_lr, double max_lr, double* step,
                        int32_t* mb_idx, int nmb, int32_t* stat_idx, float* scaler, const float* np, int nnp,
                        int growth_interval) {
+    // k_sqnorm's non-finite counts, summed by the whole wave (one thread walking the partials serially
+    // was a chain of dependent global loads: 6 us of every minibatch)
+    float b = 0.f;
+    if (scaler) {
+        for (int k = threadIdx.x; k < nnp; k += kWave) b += np[nnp + k];
+        b = wave_sum(b);
+    }
     if (threadIdx.x != 0) return;
     bool skipped = false;
     if (scaler) {  // GradScaler.update: backoff 0.5 on a skipped step, growth 2 after growth_interval good ones
-        float b = 0.f;
-        for (int k = 0; k < nnp; ++k) b += np[nnp + k];  // k_sqnorm's non-finite counts
         skipped = b > 0.f;
         if (skipped) {
             scaler[0] *= 0.5f;
