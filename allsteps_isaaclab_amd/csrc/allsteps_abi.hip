@@ -157,6 +157,15 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
     h.max_path = std::max(h.max_path, __builtin_popcount(h.lpath[i]) - 1);
     if (i > 0) h.max_sub = std::max(h.max_sub, __builtin_popcount(h.lsub[i]) - 1);
   }
+  while ((1 << h.fk_rounds) < h.max_path) ++h.fk_rounds;
+  if (h.fk_rounds > 4) return fail(AS_ERR_INVALID, "as_create: tree deeper than 16 links");
+  for (int i = 0; i < nl; ++i) {
+    int a = i > 0 ? model->parent[i] : 0;
+    for (int r = 0; r < 4; ++r) {  // a = the 2^r-th ancestor (0 past the root)
+      h.jump[i] |= (uint32_t)a << (8 * r);
+      for (int k = 0; k < (1 << r); ++k) a = a > 0 ? model->parent[a] : 0;
+    }
+  }
   for (int k = 0; k < model->num_hinges; ++k) {
     int li = model->cfg_dof_link[k];
     if (li < 1 || li >= model->num_links) return fail(AS_ERR_INVALID, "as_create: cfg_dof_link");

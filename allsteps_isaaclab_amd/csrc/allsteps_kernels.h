@@ -33,6 +33,10 @@ struct Consts {
   uint32_t ancmask[kMaxLinks];     // dofs on the path root..link (root dofs 0-5 always set)
   uint32_t dsub[kMaxDofs];         // links moved by dof j (subtree of its link; root dofs: all)
   uint32_t ddesc[kMaxDofs];        // dofs k whose link path contains dof j (bit k)
+  // FK by pointer jumping (k_step fk): jump[i] byte r = the 2^r-th ancestor of link i, the root (0)
+  // once the path is exhausted; fk_rounds = ceil(log2(max_path)) rounds cover every path
+  uint32_t jump[kMaxLinks];
+  int32_t fk_rounds;
 };
 
 struct StepArgs {

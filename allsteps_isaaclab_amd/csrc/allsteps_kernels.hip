@@ -107,6 +107,7 @@ struct Topo {
   uint32_t dsub;   // links moved by dof lane
   float lo, hi;    // limits of hinge lane (link lane + 1)
   float arm;       // armature of dof lane (0 on the root dofs)
+  uint32_t jump;   // FK pointer jumping: byte r = the 2^r-th ancestor of link lane (Consts::jump)
 };
 
 __device__ Topo load_topo(const Consts& K, int lane) {
@@ -122,6 +123,7 @@ __device__ Topo load_topo(const Consts& K, int lane) {
   t.lo = m.lower[hl];
   t.hi = m.upper[hl];
   t.arm = lane >= 6 && lane < nv ? m.armature[lane - 5] : 0.f;
+  t.jump = lane < nl ? K.jump[l] : 0u;
   return t;
 }
 
@@ -430,84 +432,65 @@ __device__ __forceinline__ void fk(const Consts& K, EnvS& s, int lane, const Top
                "+v"(lc.ax[1]), "+v"(lc.ax[2]));
   asm volatile("" : "+v"(lc.an[0]), "+v"(lc.an[1]), "+v"(lc.an[2]), "+v"(lc.op[0]), "+v"(lc.op[1]),
                "+v"(lc.op[2]));
+  // lane i: its joint's local transform A = (Rl, tl) (rotation row-major, translation), the identity
+  // on the root lane; then pointer jumping over the tree (fk_rounds rounds): A_i <- A_a o A_i with a
+  // the 2^r-th ancestor of i (the root's identity past the path), so after round r A_i is the product
+  // of the 2^(r+1) transforms ending at i, and after the last one the whole path root -> i -- three
+  // dependent compositions for the walker's 8-link paths instead of eight.  (Ra, ta) o (Rb, tb) =
+  // (Ra Rb, ta + Ra tb), as_matmul3 / as_matvec3 operations; oracle/physics.c kinematics forms the same
+  // products in the same association.
+  float A[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) A[k] = k == 0 || k == 4 || k == 8 ? 1.f : 0.f;
   if (lane >= 1 && lane < nl) {
     const int i = lane;
     float Roff[9], Rj[9], Ro[3], t[3], tmp[3];
     quat_to_mat(lc.oq, Roff);
     axis_angle_mat(lc.ax, s.qi[i - 1], Rj);
-    matmul3(Roff, Rj, d.Rl[i]);
+    matmul3(Roff, Rj, A);
     matvec3(Rj, lc.an, Ro);
     for (int k = 0; k < 3; ++k) t[k] = lc.an[k] - Ro[k];
     matvec3(Roff, t, tmp);
-    for (int k = 0; k < 3; ++k) d.Rl[i][9 + k] = tmp[k] + lc.op[k];
+    for (int k = 0; k < 3; ++k) A[9 + k] = tmp[k] + lc.op[k];
   }
-  if (lane == kZeroRow) {  // the path walk's identity row (the RNEA's +0 row of b.cr, which aliases
-                           // Rl, is written after the walk)
+  __syncthreads();  // (also publishes the actuator's tau before the dynamics read it)
+  {
+    const int rounds = __builtin_amdgcn_readfirstlane(K.fk_rounds);
+    const uint32_t jw = tp.jump;
+    typedef __attribute__((address_space(3))) v4f* lds_v4p_t;
+    for (int r = 0; r < rounds; ++r) {
+      // publish this round's A (rows of 12 floats: three 16-B stores), read the ancestor's.  One wave:
+      // its LDS operations complete in issue order, so the reads see this round's stores and the next
+      // round's stores cannot overtake them; the empty asm keeps the compiler from reordering them
+      if (lane < nl) {
+        lds_v4p_t own = (lds_v4p_t)(&d.Rl[lane][0]);
+        own[0] = v4f{A[0], A[1], A[2], A[3]};
+        own[1] = v4f{A[4], A[5], A[6], A[7]};
+        own[2] = v4f{A[8], A[9], A[10], A[11]};
+      }
+      asm volatile("" ::: "memory");
+      const int anc = (jw >> (8 * r)) & 0xff;
+      const lds_v4p_t ar = (lds_v4p_t)(&d.Rl[anc][0]);
+      const v4f q0 = ar[0], q1 = ar[1], q2 = ar[2];
+      asm volatile("" ::: "memory");
+      const float Ra[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x};
+      const float ta[3] = {q2.y, q2.z, q2.w};
+      float Rn[9], w[3];
+      matmul3(Ra, A, Rn);
+      matvec3(Ra, A + 9, w);
 #pragma unroll
-    for (int k = 0; k < 12; ++k) d.Rl[kZeroRow][k] = k == 0 || k == 4 || k == 8 ? 1.f : 0.f;
+      for (int k = 0; k < 9; ++k) A[k] = Rn[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) A[9 + k] = ta[k] + w[k];
+    }
   }
-  __syncthreads();
   float R0[9];
   quat_to_mat(s.root_quat, R0);
   if (lane < nl) {
-    // The running rotation as packed pairs of its first two rows (P[k] = (R_0k, R_1k)) plus the
-    // third row: R Tl and R t are then one v_pk_mul + two v_pk_fma per column for two rows (the
-    // matmul3 / matvec3 fmaf chains element by element), the third row scalar.
-    v2f P[3], pp = v2f{0.f, 0.f};
-    float r2[3], p2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      P[k] = v2f{R0[k], R0[3 + k]};
-      r2[k] = R0[6 + k];
-    }
-    // kPathU path links per iteration: their local transforms are loaded before the products.  An
-    // exhausted path reads the identity transform of row kZeroRow (written above): every lane composes
-    // the same padded number of transforms, with no per-link selects (oracle/physics.c kinematics
-    // composes the same identity pads)
-    constexpr int kPathU = 4;
-    uint32_t path = tp.lpath & ~1u;
-    for (int it = 0; it < max_path; it += kPathU) {
-      int l[kPathU];
-#pragma unroll
-      for (int u = 0; u < kPathU; ++u) l[u] = take_bit_z(path);
-      float Tl[kPathU][12];
-#pragma unroll
-      for (int u = 0; u < kPathU; ++u)
-#pragma unroll
-        for (int k = 0; k < 12; ++k) Tl[u][k] = d.Rl[l[u]][k];
-#pragma unroll
-      for (int u = 0; u < kPathU; ++u) {
-        const float* T = Tl[u];
-        v2f Pn[3];
-        float r2n[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          Pn[j] = __builtin_elementwise_fma(P[2], v2f{T[6 + j], T[6 + j]},
-                                            __builtin_elementwise_fma(P[1], v2f{T[3 + j], T[3 + j]},
-                                                                      P[0] * v2f{T[j], T[j]}));
-          r2n[j] = fmaf(r2[2], T[6 + j], fmaf(r2[1], T[3 + j], r2[0] * T[j]));
-        }
-        const v2f wpp = __builtin_elementwise_fma(P[2], v2f{T[11], T[11]},
-                                                  __builtin_elementwise_fma(P[1], v2f{T[10], T[10]},
-                                                                            P[0] * v2f{T[9], T[9]}));
-        const float wp2 = fmaf(r2[2], T[11], fmaf(r2[1], T[10], r2[0] * T[9]));
-        pp = pp + wpp;
-        p2 = p2 + wp2;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          P[j] = Pn[j];
-          r2[j] = r2n[j];
-        }
-      }
-    }
-    float R[9];
-    const float p[3] = {pp.x, pp.y, p2};
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      R[j] = P[j].x;
-      R[3 + j] = P[j].y;
-      R[6 + j] = r2[j];
-    }
+    // the world pose: R = R0 A_R, p = R0 A_t (relative to the root origin)
+    float R[9], p[3];
+    matmul3(R0, A, R);
+    matvec3(R0, A + 9, p);
 #pragma unroll
     for (int k = 0; k < 9; ++k) s.R[lane][k] = R[k];
 #pragma unroll
@@ -2270,126 +2253,197 @@ __global__ __launch_bounds__(256) void k_stones(StonesArgs P) {
 // serial restatement.  Coalesced SoA loads / stores (64-thread workgroups, like k_obs).
 constexpr uint32_t kQuadTag = 0x51756164u;  // "Quad": reset-draw stream of the quadruped task
 
-// foot f's tip (its sensor geom's capsule end p1) from the state's q column of env e, root pose (rp, rq)
-__device__ __forceinline__ void quad_tip(const as_model_t& m, const as_state_t& st, int n, int e, int f, const float* rp,
-                                         const float* rq, float* tip) {
-  int g = 0;
-  for (int j = 0; j < m.num_geoms; ++j)
-    if (m.geom_foot[j] == f) { g = j; break; }
-  as_link_point(m.parent, m.cfg_dof_link, m.num_hinges, &m.offset_pos[0][0], &m.offset_quat[0][0], &m.axis[0][0],
-                &m.anchor[0][0], st.q + e, n, m.geom_link[g], rp, rq, m.geom_p1[g], tip);
-}
+// k_quad: 64 envs per 256-thread workgroup.  The four feet's tips (FK of a 3-link chain each) run one
+// thread per (env, foot) -- as one thread per env they were 11 % of the C5 step, a quarter of the
+// SIMDs busy -- with the model tables they walk staged in LDS; the task logic then runs one thread
+// per env.  Phases: (1) tips of the stepped state; (2) target ticks, rewards, dones, the reset of done
+// envs (its joint angles also to LDS); (3) tips of the reset pose for the reset envs; (4) their
+// potential, the state and the observation.  Per element the operations are as_link_point's
+// (include/as_detmath.h, shared with oracle/quad.c) in the same order.
+constexpr int kQuadEnvs = 64;
+struct QuadSmem {
+  int32_t parent[AS_MAX_LINKS], link_dof[AS_MAX_LINKS];
+  float off_pos[AS_MAX_LINKS][3], off_quat[AS_MAX_LINKS][4], axis[AS_MAX_LINKS][3], anchor[AS_MAX_LINKS][3];
+  int32_t foot_link[4];
+  float foot_p1[4][3];
+  float tip[kQuadEnvs][4][3];
+  float root[kQuadEnvs][7];   // reset envs: the stand pose (position, quaternion)
+  float qres[kQuadEnvs][AS_ACT_DIM];
+  int32_t reset[kQuadEnvs];
+};
 
-__global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
+__global__ __launch_bounds__(4 * kQuadEnvs) void k_quad(QuadArgs P) {
   const Consts& K = *(const Consts*)(CK*)P.consts;
   const as_model_t& m = K.model;
   const as_quad_task_t& Q = K.quad;
-  const int e = blockIdx.x * 64 + threadIdx.x;
-  if (e >= P.n) return;
+  __shared__ QuadSmem qs;
+  const int tid = threadIdx.x;
   const int n = P.n, nh = m.num_hinges, N = K.task.num_steps;
   const as_state_t& st = P.st;
-  const float half_z = K.sim.stone_half[2];
+  // ---- the model tables of the feet's chains, once per workgroup
+  if (tid == 0) as_link_dof_map(m.cfg_dof_link, nh, AS_MAX_LINKS, qs.link_dof);
+  if (tid < AS_MAX_LINKS) {
+    const int i = tid;
+    qs.parent[i] = m.parent[i];
+    for (int k = 0; k < 3; ++k) {
+      qs.off_pos[i][k] = m.offset_pos[i][k];
+      qs.axis[i][k] = m.axis[i][k];
+      qs.anchor[i][k] = m.anchor[i][k];
+    }
+    for (int k = 0; k < 4; ++k) qs.off_quat[i][k] = m.offset_quat[i][k];
+  }
+  if (tid < 4) {  // sensor foot f's geom: its link and capsule end p1
+    int g = 0;
+    for (int j = 0; j < m.num_geoms; ++j)
+      if (m.geom_foot[j] == tid) { g = j; break; }
+    qs.foot_link[tid] = m.geom_link[g];
+    for (int k = 0; k < 3; ++k) qs.foot_p1[tid][k] = m.geom_p1[g][k];
+  }
+  __syncthreads();
+  // foot f's tip from the joint-angle column q_col[k * stride] and the root pose
+  auto tip_of = [&](int f, const float* q_col, int stride, const float* rp, const float* rq, float* tip) {
+    as_link_point(qs.parent, qs.link_dof, &qs.off_pos[0][0], &qs.off_quat[0][0], &qs.axis[0][0],
+                  &qs.anchor[0][0], q_col, stride, qs.foot_link[f], rp, rq, qs.foot_p1[f], tip);
+  };
+  // ---- (1) tips of the stepped state, thread = (env, foot)
+  {
+    const int le = tid >> 2, f = tid & 3, e = blockIdx.x * kQuadEnvs + le;
+    if (!P.reset_all && e < n) {
+      float rp[3], rq[4];
+      for (int k = 0; k < 3; ++k) rp[k] = st.root_pos[k * n + e];
+      for (int k = 0; k < 4; ++k) rq[k] = st.root_quat[k * n + e];
+      tip_of(f, st.q + e, n, rp, rq, qs.tip[le][f]);
+    }
+  }
+  __syncthreads();
+  // ---- (2) task logic, thread = env
+  const int le = tid, e = blockIdx.x * kQuadEnvs + le;
+  const bool live = tid < kQuadEnvs && e < n;
   auto stone = [&](int k, int c) { return st.stones[(3 * k + c) * n + e]; };
   // xy distance of foot f's tip to the aim point on stone k
   auto aim_dist = [&](int f, int k, const float* tip) {
     const float fx = tip[0] - stone(k, 0), fy = tip[1] - (stone(k, 1) + Q.foot_offset_y[f]);
     return sqrtf(fx * fx + fy * fy);
   };
-  float rp[3], rq[4], lin[3], ang[3], a[AS_ACT_DIM];
-  for (int k = 0; k < 3; ++k) {
-    rp[k] = st.root_pos[k * n + e];
-    lin[k] = st.root_lin[k * n + e];
-    ang[k] = st.root_ang[k * n + e];
-  }
-  for (int k = 0; k < 4; ++k) rq[k] = st.root_quat[k * n + e];
-  for (int k = 0; k < nh; ++k) {
-    const float x = P.reset_all ? 0.f : P.actions[(size_t)e * nh + k];
-    a[k] = fminf(fmaxf(x, -1.f), 1.f);
-  }
-  int idx = st.idx[e], ep_len = st.ep_len[e], t[4], c[4];
-  for (int f = 0; f < 4; ++f) {
-    t[f] = st.feet[f * n + e];
-    c[f] = st.feet[(4 + f) * n + e];
-  }
-  uint32_t episode = st.episode[e];
-  uint32_t mk[4] = {st.contact_mask[e], st.contact_mask[n + e], st.contact_mask_hind[e], st.contact_mask_hind[n + e]};
-  float pot = st.pot[e], old_pot = st.old_pot[e];
-  bool term = false, trunc = false;
-  if (!P.reset_all) {
-    ep_len += 1;
-    // target tick per foot (allsteps_env.py:418-440) and the step reward of a fresh reach (:377-380)
-    float step_hit = 0.f, fsum = 0.f;
-    for (int f = 0; f < 4; ++f) {
-      float tip[3];
-      quad_tip(m, st, n, e, f, rp, rq, tip);
-      const float d = aim_dist(f, t[f], tip);
-      const bool reached = ((mk[f] >> t[f]) & 1u) && d < Q.step_radius;
-      if (reached) c[f] += 1;
-      if (c[f] >= Q.stop_frames) {
-        c[f] = 0;
-        t[f] = min(t[f] + 1, N - 1);
-      }
-      if (reached && c[f] == 1 && t[f] < N - 1) step_hit += Q.step_reward * as_expf(-d / Q.step_sigma);
-      fsum += aim_dist(f, t[f], tip);  // to the (updated) target: the potential
-    }
-    idx = min(t[0], t[1]);
-    old_pot = pot;
-    const float dx = stone(idx, 0) - rp[0], dy = stone(idx, 1) - rp[1];
-    const float bd = sqrtf(dx * dx + dy * dy);
-    pot = -(bd + Q.foot_progress * fsum) / Q.step_dt;
-    const float down[3] = {0.f, 0.f, -1.f};
-    float gb[3];
-    quat_rotate_inverse(rq, down, gb);
-    term = gb[2] > -Q.up_z_min || rp[2] < stone(idx, 2) + Q.min_height;
-    trunc = ep_len >= Q.max_episode_length;
-    float a2 = 0.f, en = 0.f;
-    for (int k = 0; k < nh; ++k) {
-      a2 += a[k] * a[k];
-      en += fabsf(st.qd[k * n + e] * a[k]);
-    }
-    const float bonus = idx == N - 1 && bd < Q.bonus_radius ? Q.target_bonus : 0.f;
-    const float progress = pot - old_pot;
-    P.reward[e] = term ? Q.death
-                       : (((Q.alive + progress) - Q.energy_cost * en) - Q.action_cost * sqrtf(a2)) + step_hit + bonus;
-    P.terminated[e] = term;
-    P.truncated[e] = trunc;
-  }
-  float q[AS_ACT_DIM], qd[AS_ACT_DIM];
-  for (int k = 0; k < nh; ++k) {
-    q[k] = st.q[k * n + e];
-    qd[k] = st.qd[k * n + e];
-  }
-  const bool was_reset = P.reset_all || term || trunc;
-  if (was_reset) {
-    // the stand pose over stones 0 (hind feet) and 1 (front feet), joints + U(-1, 1) * noise
-    float blk[4];
-    for (int k = 0; k < nh; ++k) {
-      if ((k & 3) == 0) philox_block(P.seed, (uint32_t)(P.env_offset + e), episode, (uint32_t)(k >> 2), kQuadTag, blk);
-      q[k] = K.act.default_q[k] + Q.joint_noise * (2.f * blk[k & 3] - 1.f);
-      qd[k] = 0.f;
-      st.q[k * n + e] = q[k];
-      st.qd[k * n + e] = 0.f;
-    }
-    episode += 1u;
-    rp[0] = 0.5f * (stone(0, 0) + stone(1, 0));
-    rp[1] = 0.5f * (stone(0, 1) + stone(1, 1));
-    rp[2] = fmaxf(stone(0, 2), stone(1, 2)) + half_z + Q.stand_height;
-    rq[0] = 1.f; rq[1] = rq[2] = rq[3] = 0.f;
+  float rp[3], rq[4], lin[3], ang[3], a[AS_ACT_DIM], q[AS_ACT_DIM], qd[AS_ACT_DIM];
+  int idx = 0, ep_len = 0, t[4], c[4];
+  uint32_t episode = 0u, mk[4];
+  float pot = 0.f, old_pot = 0.f;
+  bool was_reset = false;
+  if (live) {
     for (int k = 0; k < 3; ++k) {
-      lin[k] = ang[k] = 0.f;
-      st.root_pos[k * n + e] = rp[k];
-      st.root_lin[k * n + e] = 0.f;
-      st.root_ang[k * n + e] = 0.f;
+      rp[k] = st.root_pos[k * n + e];
+      lin[k] = st.root_lin[k * n + e];
+      ang[k] = st.root_ang[k * n + e];
     }
-    for (int k = 0; k < 4; ++k) st.root_quat[k * n + e] = rq[k];
+    for (int k = 0; k < 4; ++k) rq[k] = st.root_quat[k * n + e];
+    for (int k = 0; k < nh; ++k) {
+      const float x = P.reset_all ? 0.f : P.actions[(size_t)e * nh + k];
+      a[k] = fminf(fmaxf(x, -1.f), 1.f);
+    }
+    idx = st.idx[e];
+    ep_len = st.ep_len[e];
+    for (int f = 0; f < 4; ++f) {
+      t[f] = st.feet[f * n + e];
+      c[f] = st.feet[(4 + f) * n + e];
+    }
+    episode = st.episode[e];
+    mk[0] = st.contact_mask[e];
+    mk[1] = st.contact_mask[n + e];
+    mk[2] = st.contact_mask_hind[e];
+    mk[3] = st.contact_mask_hind[n + e];
+    pot = st.pot[e];
+    old_pot = st.old_pot[e];
+    bool term = false, trunc = false;
+    if (!P.reset_all) {
+      ep_len += 1;
+      // target tick per foot (allsteps_env.py:418-440) and the step reward of a fresh reach (:377-380)
+      float step_hit = 0.f, fsum = 0.f;
+      for (int f = 0; f < 4; ++f) {
+        const float* tip = qs.tip[le][f];
+        const float d = aim_dist(f, t[f], tip);
+        const bool reached = ((mk[f] >> t[f]) & 1u) && d < Q.step_radius;
+        if (reached) c[f] += 1;
+        if (c[f] >= Q.stop_frames) {
+          c[f] = 0;
+          t[f] = min(t[f] + 1, N - 1);
+        }
+        if (reached && c[f] == 1 && t[f] < N - 1) step_hit += Q.step_reward * as_expf(-d / Q.step_sigma);
+        fsum += aim_dist(f, t[f], tip);  // to the (updated) target: the potential
+      }
+      idx = min(t[0], t[1]);
+      old_pot = pot;
+      const float dx = stone(idx, 0) - rp[0], dy = stone(idx, 1) - rp[1];
+      const float bd = sqrtf(dx * dx + dy * dy);
+      pot = -(bd + Q.foot_progress * fsum) / Q.step_dt;
+      const float down[3] = {0.f, 0.f, -1.f};
+      float gb[3];
+      quat_rotate_inverse(rq, down, gb);
+      term = gb[2] > -Q.up_z_min || rp[2] < stone(idx, 2) + Q.min_height;
+      trunc = ep_len >= Q.max_episode_length;
+      float a2 = 0.f, en = 0.f;
+      for (int k = 0; k < nh; ++k) {
+        a2 += a[k] * a[k];
+        en += fabsf(st.qd[k * n + e] * a[k]);
+      }
+      const float bonus = idx == N - 1 && bd < Q.bonus_radius ? Q.target_bonus : 0.f;
+      const float progress = pot - old_pot;
+      P.reward[e] = term ? Q.death
+                         : (((Q.alive + progress) - Q.energy_cost * en) - Q.action_cost * sqrtf(a2)) + step_hit + bonus;
+      P.terminated[e] = term;
+      P.truncated[e] = trunc;
+    }
+    for (int k = 0; k < nh; ++k) {
+      q[k] = st.q[k * n + e];
+      qd[k] = st.qd[k * n + e];
+    }
+    was_reset = P.reset_all || term || trunc;
+    if (was_reset) {
+      // the stand pose over stones 0 (hind feet) and 1 (front feet), joints + U(-1, 1) * noise
+      float blk[4];
+      for (int k = 0; k < nh; ++k) {
+        if ((k & 3) == 0) philox_block(P.seed, (uint32_t)(P.env_offset + e), episode, (uint32_t)(k >> 2), kQuadTag, blk);
+        q[k] = K.act.default_q[k] + Q.joint_noise * (2.f * blk[k & 3] - 1.f);
+        qd[k] = 0.f;
+        st.q[k * n + e] = q[k];
+        st.qd[k * n + e] = 0.f;
+        qs.qres[le][k] = q[k];
+      }
+      episode += 1u;
+      rp[0] = 0.5f * (stone(0, 0) + stone(1, 0));
+      rp[1] = 0.5f * (stone(0, 1) + stone(1, 1));
+      rp[2] = fmaxf(stone(0, 2), stone(1, 2)) + K.sim.stone_half[2] + Q.stand_height;
+      rq[0] = 1.f; rq[1] = rq[2] = rq[3] = 0.f;
+      for (int k = 0; k < 3; ++k) {
+        lin[k] = ang[k] = 0.f;
+        st.root_pos[k * n + e] = rp[k];
+        st.root_lin[k * n + e] = 0.f;
+        st.root_ang[k * n + e] = 0.f;
+        qs.root[le][k] = rp[k];
+      }
+      for (int k = 0; k < 4; ++k) {
+        st.root_quat[k * n + e] = rq[k];
+        qs.root[le][3 + k] = rq[k];
+      }
+    }
+  }
+  if (tid < kQuadEnvs) qs.reset[tid] = was_reset;
+  __syncthreads();
+  // ---- (3) tips of the reset pose (joint angles from LDS), thread = (env, foot)
+  {
+    const int le3 = tid >> 2, f = tid & 3;
+    if (qs.reset[le3]) tip_of(f, qs.qres[le3], 1, &qs.root[le3][0], &qs.root[le3][3], qs.tip[le3][f]);
+  }
+  __syncthreads();
+  if (!live) return;
+  // ---- (4) the reset envs' targets and potential; the state and the observation, thread = env
+  if (was_reset) {
     ep_len = 0;
     float fsum = 0.f;
     for (int f = 0; f < 4; ++f) {
       t[f] = min(f < 2 ? 2 : 1, N - 1);
       c[f] = 0;
-      float tip[3];
-      quad_tip(m, st, n, e, f, rp, rq, tip);  // the reset pose (q written above)
-      fsum += aim_dist(f, t[f], tip);
+      fsum += aim_dist(f, t[f], qs.tip[le][f]);
     }
     idx = min(t[0], t[1]);
     const float dx = stone(idx, 0) - rp[0], dy = stone(idx, 1) - rp[1];
@@ -2437,7 +2491,7 @@ __global__ __launch_bounds__(64) void k_quad(QuadArgs P) {
 }
 
 hipError_t launch_quad(const QuadArgs& a, hipStream_t stream) {
-  hipLaunchKernelGGL(k_quad, dim3((a.n + 63) / 64), dim3(64), 0, stream, a);
+  hipLaunchKernelGGL(k_quad, dim3((a.n + kQuadEnvs - 1) / kQuadEnvs), dim3(4 * kQuadEnvs), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@
 #define AS_DETMATH_H
 
 #include <math.h>
+#include <stdint.h>
 
 #if defined(__HIPCC__)
 #define AS_HD __host__ __device__ __forceinline__
@@ -215,9 +216,9 @@ AS_HD void as_axis_angle_mat(const float* a, float ang, float* R) {
  * the walk root -> link with every link's joint transform as the physics' FK forms it
  * (oracle/physics.c kinematics): Rl = Roff(offset_quat) Rj(axis, q), tl = offset_pos + Roff (anchor -
  * Rj anchor); p += R tl, R = R Rl; out = rp + (p + R pl).  The hinge angle of link i is read from the
- * state column q_col[k * q_stride] of the cfg dof k with cfg_dof_link[k] == i (no per-lane arrays:
- * one global read per link on the device).  Model tables flattened row-major ([link][3] / [link][4]). */
-AS_HD void as_link_point(const int32_t* parent, const int32_t* cfg_dof_link, int nh, const float* offset_pos,
+ * state column q_col[link_dof[i] * q_stride], link_dof the inverse of cfg_dof_link (as_link_dof_map).
+ * Model tables flattened row-major ([link][3] / [link][4]). */
+AS_HD void as_link_point(const int32_t* parent, const int32_t* link_dof, const float* offset_pos,
                          const float* offset_quat, const float* axis, const float* anchor, const float* q_col,
                          int q_stride, int link, const float* rp, const float* rq, const float* pl, float* out) {
   int depth = 0;
@@ -227,9 +228,7 @@ AS_HD void as_link_point(const int32_t* parent, const int32_t* cfg_dof_link, int
   for (int s = depth - 1; s >= 0; --s) {
     int i = link;
     for (int j = 0; j < s; ++j) i = parent[i];  /* the ancestor s links above `link` */
-    float qi = 0.f;
-    for (int k = 0; k < nh; ++k)
-      if (cfg_dof_link[k] == i) qi = q_col[k * q_stride];
+    const float qi = q_col[link_dof[i] * q_stride];
     float Roff[9], Rj[9], Rl[9], Ro[3], t[3], tl[3], wp[3], Rn[9];
     as_quat_to_mat(offset_quat + 4 * i, Roff);
     as_axis_angle_mat(axis + 3 * i, qi, Rj);
@@ -246,6 +245,12 @@ AS_HD void as_link_point(const int32_t* parent, const int32_t* cfg_dof_link, int
   float w[3];
   as_matvec3(R, pl, w);
   for (int k = 0; k < 3; ++k) out[k] = rp[k] + (p[k] + w[k]);
+}
+
+/* link_dof[i] = the cfg dof k with cfg_dof_link[k] == i (0 for the root and unused links) */
+AS_HD void as_link_dof_map(const int32_t* cfg_dof_link, int nh, int nlinks, int32_t* link_dof) {
+  for (int i = 0; i < nlinks; ++i) link_dof[i] = 0;
+  for (int k = 0; k < nh; ++k) link_dof[cfg_dof_link[k]] = k;
 }
 
 /* ---- actuators (include/allsteps.h as_actuator_t) */

@@ -105,57 +105,55 @@ static void subtree_sums(const or_model_t* m, int nl, int w, const float* own, f
     }
 }
 
-/* Compositions of the kernel's FK path walk (fk in csrc/allsteps_kernels.hip): every link composes
- * 4 * ceil(max_path / 4) transforms, its own path's (root excluded, ascending) and then identities. */
-static int fk_walk_len(const or_model_t* m) {
-  int mp = 0;
-  for (int i = 1; i < m->num_links; ++i) {
-    int d = 0;
-    for (int l = i; l > 0; l = m->parent[l]) ++d;
-    if (d > mp) mp = d;
-  }
-  return (mp + 3) / 4 * 4;
-}
-
 /* FK + motion subspace + spatial inertias. q_int: hinge angles in link order (link i -> q_int[i-1]).
- * Link i's pose is the kernel's path walk: R = R_root, p = 0, then for each transform (R_l, t_l) on the
- * path root -> i (ascending), padded with identities to fk_walk_len: p += R t_l, R = R R_l. */
+ * Link i's pose is the kernel's pointer jumping (k_step fk): A_i = its joint's local transform (Rl, tl)
+ * (the identity for the root); for r < ceil(log2(max_path)) rounds, every link at once, A_i <- A_a o A_i
+ * with a = the 2^r-th ancestor of i (the root past the path) and the round-r values on both sides;
+ * (Ra, ta) o (Rb, tb) = (Ra Rb, ta + Ra tb).  Then R_i = R0 A_i.R, p_i = R0 A_i.t. */
 static void kinematics(const or_model_t* m, const float root_quat[4], const float* q_int, kin_t* K) {
   const int nl = m->num_links;
   K->nl = nl;
   K->nv = OR_NDOF_ROOT + m->num_hinges;
   float R0[9];
   quat_to_mat(root_quat, R0);
-  float Rl[OR_MAX_LINKS][9], tl[OR_MAX_LINKS][3];
+  float A[OR_MAX_LINKS][12], An[OR_MAX_LINKS][12];
+  int anc[OR_MAX_LINKS], depth_max = 0;
+  for (int i = 0; i < nl; ++i) {
+    for (int k = 0; k < 12; ++k) A[i][k] = k == 0 || k == 4 || k == 8 ? 1.f : 0.f;
+    anc[i] = i > 0 ? m->parent[i] : 0;
+    int dpt = 0;
+    for (int l = i; l > 0; l = m->parent[l]) ++dpt;
+    if (dpt > depth_max) depth_max = dpt;
+  }
   for (int i = 1; i < nl; ++i) {
     float Roff[9], Rj[9], t[3], Ro[3];
     quat_to_mat(m->offset_quat[i], Roff);
     axis_angle_mat(m->axis[i], q_int[i - 1], Rj);
-    matmul3(Roff, Rj, Rl[i]);
+    matmul3(Roff, Rj, A[i]);
     /* joint translation t_j = o - Rj o; local origin = offset_pos + Roff t_j */
     matvec3(Rj, m->anchor[i], Ro);
     for (int k = 0; k < 3; ++k) t[k] = m->anchor[i][k] - Ro[k];
-    matvec3(Roff, t, tl[i]);
-    for (int k = 0; k < 3; ++k) tl[i][k] += m->offset_pos[i][k];
+    matvec3(Roff, t, A[i] + 9);
+    for (int k = 0; k < 3; ++k) A[i][9 + k] += m->offset_pos[i][k];
   }
-  const float I3[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f}, Z3[3] = {0.f, 0.f, 0.f};
-  const int wl = fk_walk_len(m);
-  for (int i = 0; i < nl; ++i) {
-    int chain[OR_MAX_LINKS], n = 0;
-    for (int l = i; l > 0; l = m->parent[l]) chain[n++] = l;  /* deepest first */
-    float R[9], p[3] = {0.f, 0.f, 0.f};
-    memcpy(R, R0, sizeof(R));
-    for (int st = 0; st < wl; ++st) {
-      const float* T = st < n ? Rl[chain[n - 1 - st]] : I3;
-      const float* t = st < n ? tl[chain[n - 1 - st]] : Z3;
-      float wp[3], Rn[9];
-      matvec3(R, t, wp);
-      for (int k = 0; k < 3; ++k) p[k] = p[k] + wp[k];
-      matmul3(R, T, Rn);
-      memcpy(R, Rn, sizeof(R));
+  int rounds = 0;
+  while ((1 << rounds) < depth_max) ++rounds;
+  for (int r = 0; r < rounds; ++r) {
+    int an2[OR_MAX_LINKS];
+    for (int i = 0; i < nl; ++i) {
+      const float* Aa = A[anc[i]];
+      float w[3];
+      matmul3(Aa, A[i], An[i]);
+      matvec3(Aa, A[i] + 9, w);
+      for (int k = 0; k < 3; ++k) An[i][9 + k] = Aa[9 + k] + w[k];
+      an2[i] = anc[anc[i]];
     }
-    memcpy(K->R[i], R, sizeof(R));
-    memcpy(K->p[i], p, sizeof(p));
+    memcpy(A, An, sizeof(float) * 12 * (size_t)nl);
+    for (int i = 0; i < nl; ++i) anc[i] = an2[i];
+  }
+  for (int i = 0; i < nl; ++i) {
+    matmul3(R0, A[i], K->R[i]);
+    matvec3(R0, A[i] + 9, K->p[i]);
   }
   matvec3(R0, m->com[0], K->c0);
   for (int i = 0; i < nl; ++i) {

@@ -28,8 +28,10 @@ static void quad_tip(const or_model_t* m, const or_state_t* st, int e, int f, co
   int g = 0;
   for (int j = 0; j < m->num_geoms; ++j)
     if (m->geom_foot[j] == f) { g = j; break; }
-  as_link_point(m->parent, m->cfg_dof_link, m->num_hinges, &m->offset_pos[0][0], &m->offset_quat[0][0],
-                &m->axis[0][0], &m->anchor[0][0], st->q + e, st->n, m->geom_link[g], rp, rq, m->geom_p1[g], tip);
+  int32_t link_dof[OR_MAX_LINKS];
+  as_link_dof_map(m->cfg_dof_link, m->num_hinges, OR_MAX_LINKS, link_dof);
+  as_link_point(m->parent, link_dof, &m->offset_pos[0][0], &m->offset_quat[0][0], &m->axis[0][0], &m->anchor[0][0],
+                st->q + e, st->n, m->geom_link[g], rp, rq, m->geom_p1[g], tip);
 }
 
 void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
@@ -205,6 +207,8 @@ void or_link_point(const or_model_t* m, const or_state_t* st, int e, int link, c
   float rp[3], rq[4];
   for (int k = 0; k < 3; ++k) rp[k] = F(st->root_pos, k, n, e);
   for (int k = 0; k < 4; ++k) rq[k] = F(st->root_quat, k, n, e);
-  as_link_point(m->parent, m->cfg_dof_link, m->num_hinges, &m->offset_pos[0][0], &m->offset_quat[0][0],
-                &m->axis[0][0], &m->anchor[0][0], st->q + e, n, link, rp, rq, pl, out);
+  int32_t link_dof[OR_MAX_LINKS];
+  as_link_dof_map(m->cfg_dof_link, m->num_hinges, OR_MAX_LINKS, link_dof);
+  as_link_point(m->parent, link_dof, &m->offset_pos[0][0], &m->offset_quat[0][0], &m->axis[0][0], &m->anchor[0][0],
+                st->q + e, n, link, rp, rq, pl, out);
 }

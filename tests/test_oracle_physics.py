@@ -154,3 +154,51 @@ def test_zero_torque_collapse_no_tunnelling(orc):
             lowest = min(lowest, st["body_pos"][5][over].min())
     # foot-frame origin sits 0.025 below the capsule bottom: allow 2 cm of penetration
     assert lowest > 0.1125 - 0.025 - 0.02, lowest
+
+
+def _fk64(m, root_pos, root_quat, q_cfg):
+    """float64 root -> link walk: R_i = R_parent Roff_i Rj_i, p_i = p_parent + R_parent (offset_pos +
+    Roff (anchor - Rj anchor)) -- the textbook recursion the spec's pointer jumping reassociates."""
+    def quat(q):
+        w, x, y, z = q
+        return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                         [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                         [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+    def axang(a, t):
+        a = np.asarray(a, np.float64)
+        K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+        return np.eye(3) + np.sin(t) * K + (1 - np.cos(t)) * K @ K
+
+    nl = m["num_links"]
+    q_int = np.zeros(nl)
+    for k in range(m["num_hinges"]):
+        q_int[m["cfg_dof_link"][k]] = q_cfg[k]
+    R = [None] * nl
+    p = [None] * nl
+    R[0], p[0] = quat(np.asarray(root_quat, np.float64)), np.asarray(root_pos, np.float64)
+    for i in range(1, nl):
+        Roff, Rj = quat(np.asarray(m["offset_quat"][i], np.float64)), axang(m["axis"][i], q_int[i])
+        an = np.asarray(m["anchor"][i], np.float64)
+        t = np.asarray(m["offset_pos"][i], np.float64) + Roff @ (an - Rj @ an)
+        pa = m["parent"][i]
+        R[i], p[i] = R[pa] @ Roff @ Rj, p[pa] + R[pa] @ t
+    return R, p
+
+
+def test_fk_pointer_jumping_matches_a_float64_walk(orc):
+    """The spec's FK (pointer jumping over the tree, float32) places the torso and feet where a float64
+    root -> link recursion does, to float32 rounding, at random poses of the walker."""
+    rng = np.random.default_rng(11)
+    m = orc.m
+    worst = 0.0
+    for _ in range(20):
+        q = rng.uniform(-1.5, 1.5, m["num_hinges"]).astype(np.float32)
+        rp = rng.uniform(-2, 2, 3).astype(np.float32)
+        qt = rng.normal(size=4)
+        rq = (qt / np.linalg.norm(qt)).astype(np.float32)
+        bp = orc.fk_bodies(rp, rq, q)
+        _, p64 = _fk64(m, rp, rq, q)
+        for b, link in enumerate((m["torso_link"], *m["foot_link"])):
+            worst = max(worst, float(np.abs(bp[b] - p64[link]).max()))
+    assert worst < 5e-6, worst
