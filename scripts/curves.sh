@@ -4,7 +4,7 @@
 # One JSON line per logged epoch -> gpurun_out/<TAG>_train_curve_*.jsonl.  Stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-T=${TAG:-r03d}
+T=${TAG:-r04}
 run() {  # name envs epochs every task limit
   echo "== $1"; date
   timeout -k 10 $6 python -u scripts/train_curve.py $2 $3 $4 $5 > gpurun_out/${T}_train_curve_$1.jsonl \
