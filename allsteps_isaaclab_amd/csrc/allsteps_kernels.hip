@@ -2270,6 +2270,7 @@ struct QuadSmem {
   float root[kQuadEnvs][7];   // reset envs: the stand pose (position, quaternion)
   float qres[kQuadEnvs][AS_ACT_DIM];
   int32_t reset[kQuadEnvs];
+  float obs[kQuadEnvs][AS_QUAD_OBS_DIM + 1];  // observation rows, written out coalesced (+1: banks)
 };
 
 __global__ __launch_bounds__(4 * kQuadEnvs) void k_quad(QuadArgs P) {
@@ -2435,59 +2436,66 @@ __global__ __launch_bounds__(4 * kQuadEnvs) void k_quad(QuadArgs P) {
     if (qs.reset[le3]) tip_of(f, qs.qres[le3], 1, &qs.root[le3][0], &qs.root[le3][3], qs.tip[le3][f]);
   }
   __syncthreads();
-  if (!live) return;
   // ---- (4) the reset envs' targets and potential; the state and the observation, thread = env
-  if (was_reset) {
-    ep_len = 0;
-    float fsum = 0.f;
-    for (int f = 0; f < 4; ++f) {
-      t[f] = min(f < 2 ? 2 : 1, N - 1);
-      c[f] = 0;
-      fsum += aim_dist(f, t[f], qs.tip[le][f]);
+  if (live) {
+    if (was_reset) {
+      ep_len = 0;
+      float fsum = 0.f;
+      for (int f = 0; f < 4; ++f) {
+        t[f] = min(f < 2 ? 2 : 1, N - 1);
+        c[f] = 0;
+        fsum += aim_dist(f, t[f], qs.tip[le][f]);
+      }
+      idx = min(t[0], t[1]);
+      const float dx = stone(idx, 0) - rp[0], dy = stone(idx, 1) - rp[1];
+      pot = -(sqrtf(dx * dx + dy * dy) + Q.foot_progress * fsum) / Q.step_dt;
+      old_pot = pot;
+      for (int k = 0; k < 4; ++k) mk[k] = 0u;
+      st.contact_mask[e] = 0u;
+      st.contact_mask[n + e] = 0u;
+      st.contact_mask_hind[e] = 0u;
+      st.contact_mask_hind[n + e] = 0u;
     }
-    idx = min(t[0], t[1]);
-    const float dx = stone(idx, 0) - rp[0], dy = stone(idx, 1) - rp[1];
-    pot = -(sqrtf(dx * dx + dy * dy) + Q.foot_progress * fsum) / Q.step_dt;
-    old_pot = pot;
-    for (int k = 0; k < 4; ++k) mk[k] = 0u;
-    st.contact_mask[e] = 0u;
-    st.contact_mask[n + e] = 0u;
-    st.contact_mask_hind[e] = 0u;
-    st.contact_mask_hind[n + e] = 0u;
+    st.idx[e] = idx;
+    for (int f = 0; f < 4; ++f) {
+      st.feet[f * n + e] = t[f];
+      st.feet[(4 + f) * n + e] = c[f];
+    }
+    st.ep_len[e] = ep_len;
+    st.episode[e] = episode;
+    st.pot[e] = pot;
+    st.old_pot[e] = old_pot;
+    // observation [64]: lin / ang velocity (body), projected gravity, each foot's aim point and stone
+    // idx + 1 relative to the root (body), each foot on its target stone, q - default, qd, actions --
+    // staged in LDS, then the block's rows (contiguous in memory) written by all 256 threads
+    float* o = qs.obs[le];
+    float v[3];
+    quat_rotate_inverse(rq, lin, v);
+    o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+    quat_rotate_inverse(rq, ang, v);
+    o[3] = v[0]; o[4] = v[1]; o[5] = v[2];
+    const float down[3] = {0.f, 0.f, -1.f};
+    quat_rotate_inverse(rq, down, v);
+    o[6] = v[0]; o[7] = v[1]; o[8] = v[2];
+    for (int f = 0; f < 5; ++f) {
+      const int k = f < 4 ? t[f] : min(idx + 1, N - 1);
+      const float oy = f < 4 ? Q.foot_offset_y[f] : 0.f;
+      const float d[3] = {stone(k, 0) - rp[0], (stone(k, 1) + oy) - rp[1], stone(k, 2) - rp[2]};
+      quat_rotate_inverse(rq, d, v);
+      o[9 + 3 * f] = v[0]; o[10 + 3 * f] = v[1]; o[11 + 3 * f] = v[2];
+    }
+    for (int f = 0; f < 4; ++f) o[24 + f] = (mk[f] >> t[f]) & 1u ? 1.f : 0.f;
+    for (int k = 0; k < nh; ++k) {
+      o[28 + k] = q[k] - K.act.default_q[k];
+      o[28 + nh + k] = qd[k];
+      o[28 + 2 * nh + k] = was_reset ? 0.f : a[k];  // _reset_idx zeroes _actions (anymal_c_env.py:171-172)
+    }
   }
-  st.idx[e] = idx;
-  for (int f = 0; f < 4; ++f) {
-    st.feet[f * n + e] = t[f];
-    st.feet[(4 + f) * n + e] = c[f];
-  }
-  st.ep_len[e] = ep_len;
-  st.episode[e] = episode;
-  st.pot[e] = pot;
-  st.old_pot[e] = old_pot;
-  // observation [64]: lin / ang velocity (body), projected gravity, each foot's aim point and stone
-  // idx + 1 relative to the root (body), each foot on its target stone, q - default, qd, actions
-  float* o = P.obs + (size_t)e * AS_QUAD_OBS_DIM;
-  float v[3];
-  quat_rotate_inverse(rq, lin, v);
-  o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
-  quat_rotate_inverse(rq, ang, v);
-  o[3] = v[0]; o[4] = v[1]; o[5] = v[2];
-  const float down[3] = {0.f, 0.f, -1.f};
-  quat_rotate_inverse(rq, down, v);
-  o[6] = v[0]; o[7] = v[1]; o[8] = v[2];
-  for (int f = 0; f < 5; ++f) {
-    const int k = f < 4 ? t[f] : min(idx + 1, N - 1);
-    const float oy = f < 4 ? Q.foot_offset_y[f] : 0.f;
-    const float d[3] = {stone(k, 0) - rp[0], (stone(k, 1) + oy) - rp[1], stone(k, 2) - rp[2]};
-    quat_rotate_inverse(rq, d, v);
-    o[9 + 3 * f] = v[0]; o[10 + 3 * f] = v[1]; o[11 + 3 * f] = v[2];
-  }
-  for (int f = 0; f < 4; ++f) o[24 + f] = (mk[f] >> t[f]) & 1u ? 1.f : 0.f;
-  for (int k = 0; k < nh; ++k) {
-    o[28 + k] = q[k] - K.act.default_q[k];
-    o[28 + nh + k] = qd[k];
-    o[28 + 2 * nh + k] = was_reset ? 0.f : a[k];  // _reset_idx zeroes _actions (anymal_c_env.py:171-172)
-  }
+  __syncthreads();
+  const int e0 = blockIdx.x * kQuadEnvs, rows = min(kQuadEnvs, n - e0);
+  float* ob = P.obs + (size_t)e0 * AS_QUAD_OBS_DIM;
+  for (int x = tid; x < rows * AS_QUAD_OBS_DIM; x += 4 * kQuadEnvs)
+    ob[x] = qs.obs[x / AS_QUAD_OBS_DIM][x % AS_QUAD_OBS_DIM];
 }
 
 hipError_t launch_quad(const QuadArgs& a, hipStream_t stream) {

@@ -5,6 +5,7 @@ import math
 import os
 import sys
 
+import numpy as np
 import pytest
 import torch
 
@@ -608,7 +609,8 @@ def _dist_train_worker(rank, port, mode, tmp, q):
         runner, _ = train.main(["--task", "Allsteps-v0", "--num_envs", "1024", "--max_iterations", "3", "--seed", "7",
                                 "--distributed", "--multi_gpu_mode", mode, "--log_root", f"{tmp}/r{rank}"])
         ag = runner.agent
-        q.put((rank, ag.flat.params.cpu(), float(ag.lr), ag.frame, ag.dataset.minibatch_size,
+        # a numpy copy (pickled by value), not a shared-memory tensor whose descriptor dies with this process
+        q.put((rank, ag.flat.params.detach().cpu().numpy().copy(), float(ag.lr), ag.frame, ag.dataset.minibatch_size,
                int(ag._uw.env_id_offset), bool(ag.fused is not None and ag._play_graphs is not None)))
     finally:
         if dist.is_initialized():
@@ -639,7 +641,7 @@ def test_distributed_fused_trainer_two_ranks_one_gpu(tmp_path, mode):
         assert p.exitcode == 0
     (_, p0, lr0, f0, mb0, off0, fused0), (_, p1, lr1, f1, mb1, off1, _) = res
     assert fused0, "the fused update / rollout graphs must be the path under test"
-    assert torch.equal(p0, p1), f"{mode}: ranks diverged"
+    assert np.array_equal(p0, p1), f"{mode}: ranks diverged"
     assert lr0 == lr1 and f0 == f1 == 3 * 2 * 1024 * 32
     assert (off0, off1) == (0, 1024)
     assert mb0 == (2 * 32768 if mode == "allgather" else 32768)
