@@ -85,11 +85,9 @@ class AnymalCStonesEnv(DirectRLEnv):
         self.soft_joint_pos_limits = self.soft_joint_pos_limits.unsqueeze(0).expand(n, -1, -1)
         self.obs_buf = torch.zeros((n, _native.QUAD_OBS_DIM), dtype=torch.float32, device=dev)
         self.reward_buf = torch.zeros(n, dtype=torch.float32, device=dev)
-        self._term_u8 = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self._trunc_u8 = torch.zeros(n, dtype=torch.uint8, device=dev)
+        # k_quad writes 0 / 1 bytes straight into the bool buffers (torch.bool is one byte, as AllstepsEnv)
         self.reset_terminated = torch.zeros(n, dtype=torch.bool, device=dev)
         self.reset_time_outs = torch.zeros(n, dtype=torch.bool, device=dev)
-        self.reset_buf = torch.zeros(n, dtype=torch.bool, device=dev)
         self.extras = {}
         self._native.quad_reset_all(self.obs_buf, stream=self._stream())
 
@@ -103,6 +101,11 @@ class AnymalCStonesEnv(DirectRLEnv):
     @property
     def target_index(self) -> torch.Tensor:
         return self.state["idx"]
+
+    @property
+    def reset_buf(self) -> torch.Tensor:
+        """terminated | truncated of the last step (formed on demand: no kernel in the step)"""
+        return self.reset_terminated | self.reset_time_outs
 
     @property
     def foot_targets(self) -> torch.Tensor:
@@ -136,10 +139,8 @@ class AnymalCStonesEnv(DirectRLEnv):
         if action.shape != (self.num_envs, self.num_dof):
             raise ValueError(f"actions must be ({self.num_envs}, {self.num_dof}), got {tuple(action.shape)}")
         a = action.to(torch.float32).contiguous()
-        self._native.quad_step(a, self.obs_buf, self.reward_buf, self._term_u8, self._trunc_u8, stream=self._stream())
-        self.reset_terminated.copy_(self._term_u8)
-        self.reset_time_outs.copy_(self._trunc_u8)
-        torch.logical_or(self.reset_terminated, self.reset_time_outs, out=self.reset_buf)
+        self._native.quad_step(a, self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs,
+                               stream=self._stream())
         return {"policy": self.obs_buf}, self.reward_buf, self.reset_terminated, self.reset_time_outs, self.extras
 
     def close(self):
