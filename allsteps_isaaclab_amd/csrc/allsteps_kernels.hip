@@ -1188,10 +1188,15 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   // the reads are passed through an empty asm, four words at a time: each batch waits once.  (With
   // `pv && test` the compiler put each word's reads behind a branch on pv and waited on them word by
   // word: one LDS latency per word.)
+  // Batches past the table (the quadruped's 66 pairs fill one of the two) are skipped by a scalar
+  // branch; their words stay empty.
   uint32_t hbl[kSelfW];
   static_assert(kSelfW % 4 == 0, "batches of four words");
 #pragma unroll
+  for (int i = 0; i < kSelfW; ++i) hbl[i] = 0u;
+#pragma unroll
   for (int i0 = 0; i0 < kSelfW; i0 += 4) {
+    if (G * i0 >= nsp) break;
     v4f s1[4], s2[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -2159,17 +2164,27 @@ __global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
   const int n = P.n;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int any_reset = P.counters[0];
-  // the next launch's bank (this launch reads the other one)
-  for (int k = e; k < kCntBank; k += gridDim.x * blockDim.x) P.next_counters[k] = 0;
-  if (e == 0) {
-    int sum = 0;
-    for (int i = 0; i < kCntSlots; ++i) sum += P.counters[kCntStride * (1 + i)];
-    P.counters[1] = sum;
-    if (any_reset) {  // (regen below recomputes this gate per thread from the bank, race-free)
-      const int c = P.st.curriculum[0];
-      if ((float)sum / (float)n > (float)T.curriculum_threshold) P.st.curriculum[0] = min(c + 1, T.max_curriculum);
+  if (blockIdx.x == 0) {
+    // the gate's inputs in one memory round trip: lane i < kCntSlots reads partial sum i, lane
+    // kCntSlots the curriculum level (all issued before any store: the stores below may alias them)
+    const int t = threadIdx.x;
+    int v = 0;
+    if (t < kCntSlots) v = P.counters[kCntStride * (1 + t)];
+    else if (t == kCntSlots) v = P.st.curriculum[0];
+    const int c = __shfl(v, kCntSlots);
+    int part = t < kCntSlots ? v : 0;
+#pragma unroll
+    for (int off = kCntSlots / 2; off > 0; off >>= 1) part += __shfl_xor(part, off);
+    const int sum = __builtin_amdgcn_readfirstlane(part);  // lanes 0..15 hold the total (exact integers)
+    if (t == 0) {
+      P.counters[1] = sum;
+      // (regen below recomputes this gate per thread from the bank, race-free)
+      if (any_reset && (float)sum / (float)n > (float)T.curriculum_threshold)
+        P.st.curriculum[0] = min(c + 1, T.max_curriculum);
     }
   }
+  // the next launch's bank (this launch reads the other one)
+  for (int k = e; k < kCntBank; k += gridDim.x * blockDim.x) P.next_counters[k] = 0;
   if (any_reset && T.regen_footsteps && e < n && P.side[kSideRegen * n + e]) {
     int sum = 0;
     for (int i = 0; i < kCntSlots; ++i) sum += P.counters[kCntStride * (1 + i)];
