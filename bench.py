@@ -409,7 +409,7 @@ def main():
             import bench_quadruped
 
             try:
-                line["c5"] = bench_quadruped.measure(16384, steps=300, warmup=20, device=str(device))
+                line["c5"] = bench_quadruped.measure(16384, steps=300, warmup=100, device=str(device))
             except Exception as e:  # reported, never fatal for the env metric
                 line["c5"] = {"error": f"{type(e).__name__}: {e}"}
         print(json.dumps(line), flush=True)

@@ -1,6 +1,6 @@
 """BASELINE C5 throughput: the quadruped (model/anymal_c.xml) on the stones with its task, 1 GPU.
 
-    python scripts/bench_quadruped.py [--num_envs 16384] [--steps 500] [--warmup 20]
+    python scripts/bench_quadruped.py [--num_envs 16384] [--steps 500] [--warmup 100]
 
 A step = ``AnymalCStonesEnv.step`` (``Allsteps-AnymalC-v0``, ANYmal-C's sim settings: dt 1/200, friction
 1.0, max depenetration velocity 1.0) = as_quad_step: 4 substeps of k_step<18> for every env with the DC
@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 
-def measure(num_envs: int = 16384, steps: int = 500, warmup: int = 20, device: str = "cuda:0") -> dict:
+def measure(num_envs: int = 16384, steps: int = 500, warmup: int = 100, device: str = "cuda:0") -> dict:
     from allsteps_isaaclab_amd import registry
 
     cfg = registry.load_cfg_from_registry("Allsteps-AnymalC-v0", "env_cfg_entry_point")
@@ -33,9 +33,10 @@ def measure(num_envs: int = 16384, steps: int = 500, warmup: int = 20, device: s
     env = registry.make("Allsteps-AnymalC-v0", cfg=cfg)
     env.reset()
     gen = torch.Generator(device=device).manual_seed(7)
-    acts = torch.rand(steps + warmup, num_envs, 12, device=device, generator=gen) * 2 - 1
+    acts = torch.rand(steps + 20, num_envs, 12, device=device, generator=gen) * 2 - 1
+    # (100 warm-up steps: a cold box's first ~20 steps run at well under half the steady rate)
     for t in range(warmup):
-        env.step(acts[steps + t])
+        env.step(acts[steps + t % 20])
     torch.cuda.synchronize(device)
     # resets counted on every 10th step only: the count's own kernels (or / sum / add, ~4 us each) would
     # otherwise be a few per cent of the step they measure
@@ -67,7 +68,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--num_envs", type=int, default=16384)
     p.add_argument("--steps", type=int, default=500)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=100)
     a = p.parse_args()
     print(json.dumps(measure(a.num_envs, a.steps, a.warmup)), flush=True)
 
