@@ -96,8 +96,9 @@ def kernel_times(ms_per_step: float, k_ms: float, o_ms: float, launches: int) ->
     k_ev, o_ev = k_ms / n, o_ms / n
     return {"k_step_ms": round(ms_per_step - o_ev, 5), "k_step_event_ms": round(k_ev, 5),
             "k_obs_event_ms": round(o_ev, 5), "sampled_launches": launches,
-            "method": "k_step_ms = wall ms_per_step - k_obs HIP-event average (sampled launches); "
-                      "k_step_event_ms = HIP events around every 10th k_step launch (includes its dispatch)"}
+            "method": "k_step_ms = wall ms_per_step - k_obs HIP-event average; the events bracket every 10th "
+                      "k_step / k_obs launch of an untimed stretch run right after the timed loop (none inside "
+                      "it); k_step_event_ms includes the launch's dispatch"}
 
 
 def measured_hbm_peak(device) -> float | None:
@@ -321,9 +322,7 @@ def main():
     for t in range(W):
         env.step(actions[K + t])
     torch.cuda.synchronize(device)
-    # HIP events around every 10th k_step / k_obs launch of the timed region: per-launch events add a
-    # launch gap (~10 us at 4096 envs), so timing every launch would slow the loop it measures
-    env._native.profile_sampled(max(K // 10, 1), 10)
+    env._native.profile(0)  # no HIP events inside the timed loop (each adds a launch gap to its step)
 
     def barrier():
         if world > 1:
@@ -336,7 +335,16 @@ def main():
         env.step(actions[t])
     barrier()
     el = time.perf_counter() - t0
+    # kernel durations: HIP events around every 10th k_step / k_obs launch of a separate, untimed
+    # stretch of the same loop right after the timed one (events inside the timed loop would add
+    # their launch gaps to the steps they sample, ~1 us per step on average)
+    P = min(K, 500)
+    env._native.profile_sampled(max(P // 10, 1), 10)
+    for t in range(P):
+        env.step(actions[t])
+    torch.cuda.synchronize(device)
     k_ms, o_ms, launches = env._native.profile_read()
+    env._native.profile(0)
     if world > 1:
         tt = torch.tensor([el], device=device if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
