@@ -185,21 +185,34 @@ __global__ void __launch_bounds__(256) k_obs_stats_update(const double* __restri
     if (c == 0) *count = cnt + double(mb_rows);
 }
 
-__global__ void k_obs_normalize(const float* __restrict__ x, const int32_t* __restrict__ mb_idx, int mb_rows, int cols,
-                                const double* __restrict__ mean, const double* __restrict__ var, float eps,
-                                void* __restrict__ out, int out_cols, int out_stride, int out_dtype) {
-    const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= int64_t(mb_rows) * out_cols) return;
-    const int r = int(e / out_cols), c = int(e % out_cols);
-    const int64_t i = int64_t(r) * out_stride + c;
-    float y = 0.f;
-    if (c < cols) {
-        const float v = x[(int64_t(*mb_idx) * mb_rows + r) * cols + c];
+// (64 x 4)-thread blocks over 16-row tiles: a thread owns columns c and c + 64 of the tile's rows 4k + ty,
+// so the column's mean and 1 / sqrt(var + eps) denominators are read and formed once per thread and
+// no element needs a 64-bit index division (the one-thread-per-element form spent most of its time there)
+constexpr int kNormCols = 64, kNormRowThreads = 4, kNormTileRows = 16;
+__global__ void __launch_bounds__(kNormCols * kNormRowThreads) k_obs_normalize(
+    const float* __restrict__ x, const int32_t* __restrict__ mb_idx, int mb_rows, int cols,
+    const double* __restrict__ mean, const double* __restrict__ var, float eps, void* __restrict__ out, int out_cols,
+    int out_stride, int out_dtype) {
+    const int r0 = blockIdx.x * kNormTileRows;
+    const int64_t xbase = int64_t(*mb_idx) * mb_rows;
+    for (int c = threadIdx.x; c < out_cols; c += kNormCols) {
+        const bool in = c < cols;
         // rl_games: (x - mean.float()) / sqrt(var.float() + eps), then clamp
-        y = (v - float(mean[c])) / sqrtf(float(var[c]) + eps);
-        y = fminf(fmaxf(y, -5.f), 5.f);
+        const float mf = in ? float(mean[c]) : 0.f;
+        const float den = in ? sqrtf(float(var[c]) + eps) : 1.f;
+#pragma unroll
+        for (int k = 0; k < kNormTileRows / kNormRowThreads; ++k) {
+            const int r = r0 + kNormRowThreads * k + threadIdx.y;
+            if (r >= mb_rows) break;
+            float y = 0.f;
+            if (in) {
+                const float v = x[(xbase + r) * cols + c];
+                y = (v - mf) / den;
+                y = fminf(fmaxf(y, -5.f), 5.f);
+            }
+            store_from_f32(out, int64_t(r) * out_stride + c, out_dtype, y);
+        }
     }
-    store_from_f32(out, i, out_dtype, y);
 }
 
 // ------------------------------------------------------------------------------ PPO losses
@@ -241,16 +254,33 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
     float acc_mu = 0.f, acc_ls = 0.f, acc_v = 0.f;
     float st_a = 0.f, st_c = 0.f, st_b = 0.f, st_e = 0.f, st_k = 0.f;
     const int r_begin = (blockIdx.x * G + grp) * kLossRowsPerGroup;
-    for (int rr = 0; rr < kLossRowsPerGroup; ++rr) {
+    // every row's inputs loaded first (one memory round trip for the group's rows, not one per row)
+    constexpr int R = kLossRowsPerGroup;
+    float hjv[R], av[R], m1v[R], s1v[R], onlp[R], advv[R], ovv[R], retv[R];
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+        const int r = r_begin + rr;
+        const bool ok = r < mb_rows;  // uniform across the group
+        const int64_t row = base + (ok ? r : 0);
+        hjv[rr] = ok && j <= A ? head[int64_t(r) * (A + 1) + j] : 0.f;  // mu_j, or the value on lane A
+        av[rr] = ok && act_lane ? actions[row * A + j] : 0.f;
+        m1v[rr] = ok && act_lane ? ds_mu[row * A + j] : 0.f;
+        s1v[rr] = ok && act_lane ? ds_sigma[row * A + j] : 1.f;
+        onlp[rr] = ok ? old_nlp[row] : 0.f;
+        advv[rr] = ok ? adv_[row] : 0.f;
+        ovv[rr] = ok && j == A ? old_v[row] : 0.f;
+        retv[rr] = ok && j == A ? ret_[row] : 0.f;
+    }
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
         const int r = r_begin + rr;
         if (r >= mb_rows) break;  // uniform across the group
         const int64_t row = base + r;
-        const float* h = head + int64_t(r) * (A + 1);
-        const float hj = j <= A ? h[j] : 0.f;  // mu_j, or the value on lane A
+        const float hj = hjv[rr];
         float d = 0.f, klj = 0.f, blj = 0.f, dbj = 0.f;
         if (act_lane) {
-            d = (actions[row * A + j] - hj) / sg;
-            const float m1 = ds_mu[row * A + j], s1 = ds_sigma[row * A + j];
+            d = (av[rr] - hj) / sg;
+            const float m1 = m1v[rr], s1 = s1v[rr];
             const float dm = m1 - hj;
             // policy_kl(p0 = current, p1 = dataset)
             klj = logf(s1 / sg + 1e-5f) + (sg * sg + dm * dm) / (2.f * (s1 * s1 + 1e-5f)) - 0.5f;
@@ -271,10 +301,10 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
             bl += __shfl_xor(bl, o, 32);
         }
         const float nlp = 0.5f * q + 0.5f * kLog2Pi * float(A) + sum_ls;
-        const float adv = adv_[row];
+        const float adv = advv[rr];
         float a_loss, g_nlp;
         if (cfg.ppo) {
-            const float ratio = expf(old_nlp[row] - nlp);
+            const float ratio = expf(onlp[rr] - nlp);
             const float rc = fminf(fmaxf(ratio, 1.f - cfg.e_clip), 1.f + cfg.e_clip);
             const float u1 = -adv * ratio, u2 = -adv * rc;
             const bool inside = ratio >= 1.f - cfg.e_clip && ratio <= 1.f + cfg.e_clip;
@@ -296,18 +326,18 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
             ds_mu[row * A + j] = hj;  // dataset.update_mu_sigma
             ds_sigma[row * A + j] = sg;
         } else if (j == A) {
-            const float v = hj, vp = old_v[row], R = ret_[row];
+            const float v = hj, vp = ovv[rr], Rt = retv[rr];
             float c_loss, g_v;
             if (cfg.clip_value) {
                 const float dv = v - vp;
                 const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
-                const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
+                const float l1 = (v - Rt) * (v - Rt), l2 = (vc - Rt) * (vc - Rt);
                 const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
-                g_v = max_grad(l1, l2, 2.f * (v - R), inside ? 2.f * (vc - R) : 0.f);
+                g_v = max_grad(l1, l2, 2.f * (v - Rt), inside ? 2.f * (vc - Rt) : 0.f);
                 c_loss = fmaxf(l1, l2);
             } else {
-                c_loss = (R - v) * (R - v);
-                g_v = 2.f * (v - R);
+                c_loss = (Rt - v) * (Rt - v);
+                g_v = 2.f * (v - Rt);
             }
             g_v *= 0.5f * cfg.critic_coef * inv_b;
             dh[A] = g_v;
@@ -802,8 +832,8 @@ int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, in
                       int32_t out_dtype, void* stream) {
     if (out_cols < cols || out_stride < out_cols) return fail(-1, "ppo_obs_normalize: need cols <= out_cols <= out_stride");
     if (out_dtype < PPO_DT_F32 || out_dtype > PPO_DT_F16) return fail(-1, "ppo_obs_normalize: bad out_dtype");
-    const int64_t n = int64_t(mb_rows) * out_cols;
-    hipLaunchKernelGGL(k_obs_normalize, dim3(unsigned((n + 255) / 256)), dim3(256), 0, S(stream), x, mb_idx, mb_rows,
+    hipLaunchKernelGGL(k_obs_normalize, dim3(unsigned((mb_rows + kNormTileRows - 1) / kNormTileRows)),
+                       dim3(kNormCols, kNormRowThreads), 0, S(stream), x, mb_idx, mb_rows,
                        cols, running_mean, running_var, eps, out, out_cols, out_stride, out_dtype);
     return launched("k_obs_normalize");
 }
