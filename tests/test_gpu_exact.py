@@ -126,6 +126,7 @@ def _run(orc, capsys, n, level, steps, warm, seed=42):
     (4096, 0, 20, 120),     # C2 warm: fallen robots, saturated contact sets, resets in flight
     (32768, 9, 20, 0),      # C3 from reset
     (32768, 9, 20, 120),    # C3 warm
+    (1024, 0, 400, 0),      # long horizon: 400 consecutive steps, every env through falls and resets
 ])
 def test_trajectory_bit_exact(orc, capsys, n, level, steps, warm):
     resets, contacts = _run(orc, capsys, n, level, steps, warm)
