@@ -284,15 +284,20 @@ def test_c5_registered_behind_the_env_surface():
 
 
 @pytest.mark.gpu
-def test_c5_task_gpu_bit_exact_vs_oracle(qorc, oracle_mod, qmodel):
+@pytest.mark.parametrize("n,steps,warm", [
+    (16384, 20, 60),  # BASELINE C5 size, after a second of random actions (robots falling and resetting)
+    (1024, 300, 0),   # long horizon: 6 s of simulated time from the stand pose, every step compared
+])
+def test_c5_task_gpu_bit_exact_vs_oracle(qorc, oracle_mod, qmodel, n, steps, warm):
     from allsteps_isaaclab_amd import registry
 
-    n, steps = 16384, 20  # BASELINE C5
-    env = registry.make("Allsteps-AnymalC-v0")  # AnymalCStonesEnvCfg: ANYmal-C's dt / friction / depenetration
+    cfg = registry.load_cfg_from_registry("Allsteps-AnymalC-v0", "env_cfg_entry_point")
+    cfg.scene.num_envs = n
+    env = registry.make("Allsteps-AnymalC-v0", cfg=cfg)  # AnymalCStonesEnvCfg: ANYmal-C's dt / friction / depenetration
     assert env.num_envs == n and env.physics_dt == 1.0 / 200.0
     env.reset()
     gen = torch.Generator(device="cuda:0").manual_seed(7)
-    for _ in range(60):  # a second of random actions on the GPU first: robots falling and resetting
+    for _ in range(warm):
         env.step((torch.rand(n, 12, device="cuda:0", generator=gen) * 2.4 - 1.2).contiguous())
     torch.cuda.synchronize()
     st = qorc.state(n)
@@ -312,7 +317,7 @@ def test_c5_task_gpu_bit_exact_vs_oracle(qorc, oracle_mod, qmodel):
                and not np.array_equal(g[k].view(st[k].dtype).reshape(st[k].shape), st[k])]
         resets = int((term_c | trunc_c).sum())
         total_resets += resets
-        print(f"[c5 exact] step {t}: {len(bad)} state fields differ {bad}, resets {resets}, "
+        print(f"[c5 exact n={n}] step {t}: {len(bad)} state fields differ {bad}, resets {resets}, "
               f"front-foot contacts {int((st['contact_mask'] != 0).any(axis=0).sum())}")
         assert not bad
         np.testing.assert_array_equal(obs_g.cpu().numpy(), obs_c)
