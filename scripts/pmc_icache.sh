@@ -10,7 +10,9 @@ grep -oE "\b(SQC_[A-Z0-9_]+|SQ_IFETCH[A-Z_]*|SQ_INSTS_[A-Z_]+|SQ_WAIT_[A-Z_]+)\b
 cat $OUT/names.txt | tr '\n' ' '; echo
 B="python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-train --no-c5 ${BENCH_ARGS}"
 # two counters per pass (the SQC block's per-pass limit is not documented in the guide)
-for P in "SQC_ICACHE_REQ SQC_ICACHE_MISSES" "SQC_ICACHE_HITS SQC_ICACHE_MISSES_DUPLICATE" "SQ_IFETCH SQ_WAVE_CYCLES" "SQ_IFETCH_LEVEL SQ_INSTS_VALU"; do
+PASSES=${PASSES:-"SQC_ICACHE_REQ:SQC_ICACHE_MISSES SQC_ICACHE_HITS:SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH_LEVEL:SQ_INSTS_VALU"}
+for PP in $PASSES; do
+  P=$(echo $PP | tr ':' ' ')
   ok=1; for c in $P; do grep -qx "$c" $OUT/names.txt || ok=0; done
   [ $ok = 1 ] || { echo "skip $P (not all available)"; continue; }
   T=$(echo $P | tr ' ' '_' | cut -c1-40)
