@@ -705,11 +705,6 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     __shared__ float red[2][kAdamThreads / kWave];
     __shared__ float coef_s, step_size_s, bc2_sqrt_s, inv_scale_s;
     __shared__ int skip_s;
-    // this thread's element, loaded ahead of the barriers: the loads' latency overlaps the norm
-    // reduction and thread 0's fp64 bias corrections
-    const int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x;
-    const bool live = i < n;
-    const float g0 = live ? g[i] : 0.f, m0 = live ? m[i] : 0.f, v0 = live ? v[i] : 0.f, p0 = live ? p[i] : 0.f;
     float s = 0.f, bad = 0.f;
     for (int k = threadIdx.x; k < nnp; k += kAdamThreads) {
         s += np[k];
@@ -745,21 +740,22 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     const float coef = coef_s;
     const float step_size = step_size_s;
     const float bc2_sqrt = bc2_sqrt_s;
-    if (!live || skip_s) return;
-    const float gi = (g0 * inv_scale_s) * coef;
-    const float mi = m0 + (1.f - b1) * (gi - m0);  // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = v0 * b2 + (1.f - b2) * gi * gi;
+    const int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x;
+    if (i >= n || skip_s) return;
+    const float gi = (g[i] * inv_scale_s) * coef;
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
     m[i] = mi;
     v[i] = vi;
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    const float pi = p0 - step_size * (mi / denom);
+    const float pi = p[i] - step_size * (mi / denom);
     p[i] = pi;
     if (mirror) {
         for (int k = 0; k < segs.n; ++k) {
             const ppo_seg_t& sg = segs.s[k];
             if (i >= sg.off && i < sg.off + sg.len) {
-                const int j = int(i - sg.off);  // a segment is one weight matrix (< 2^31 elements)
-                const int r = j / sg.cols, c = j - r * sg.cols;
+                const int64_t j = i - sg.off;
+                const int64_t r = j / sg.cols, c = j % sg.cols;
                 mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] =
                     mirror_dtype == PPO_DT_F16 ? f32_to_f16(pi) : f32_to_bf16(pi);
             }
@@ -988,9 +984,6 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
         const int64_t rows = t.s[k].cols > 0 ? t.s[k].len / t.s[k].cols : 0;
         if (t.s[k].cols <= 0 || t.s[k].mstride < (t.s[k].trans ? rows : t.s[k].cols))
             return fail(-1, "ppo_adam: bad segment");
-        // k_adam indexes a segment and its mirror image in 32 bits
-        if (t.s[k].len >= (int64_t(1) << 31) || int64_t(t.s[k].mstride) * (t.s[k].trans ? t.s[k].cols : rows) >= (int64_t(1) << 31))
-            return fail(-1, "ppo_adam: mirror segment too large for 32-bit indexing");
     }
     hipLaunchKernelGGL(k_adam, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0, S(stream),
                        p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
