@@ -55,7 +55,7 @@ struct as_env {
   int32_t* counters_dev;  // two banks of kCntBank: step t uses bank t % 2, k_obs clears the other
   int32_t bank = 0, last_bank = 0;
   int32_t graph_safe = 0;  // as_set_graph_safe: fixed bank 0 + memset per call
-  uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_fix
+  uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_obs
   int32_t num_steps;
   int32_t nv;
   as::Consts host;        // host copy of consts_dev (as_set_actuator / as_set_quad_task re-upload it)

@@ -47,7 +47,7 @@ struct StepArgs {
   const float* actions;
   float* reward;
   float* obs;                  // [n][59] observation rows (speculative second tick, see k_step)
-  uint32_t* side;              // [kSideWords][n]: tick-#1 state and observation entries for k_fix
+  uint32_t* side;              // [kSideWords][n]: tick-#1 state and observation entries for k_obs
   uint8_t* terminated;
   uint8_t* truncated;
   const float* reset_draws;
@@ -73,7 +73,7 @@ constexpr int kCntSlots = 16;
 constexpr int kCntStride = 16;
 constexpr int kCntBank = kCntStride * (1 + kCntSlots);
 
-// side buffer of k_step -> k_fix: idx, prev, next, count, swing, pot, old_pot, foot_contact[2]
+// side buffer of k_step -> k_obs: idx, prev, next, count, swing, pot, old_pot, foot_contact[2]
 // (tick-#1 state) and foot_contact[2], targets[9] (tick-#1 observation entries 48..58)
 constexpr int kSideState = 9;
 constexpr int kSideObs = 11;

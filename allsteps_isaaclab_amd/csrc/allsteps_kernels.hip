@@ -2058,7 +2058,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   //      re-runs _compute_useful_values for ALL envs when ANY env reset this step -- a launch-wide
   //      condition.  The tick is applied here as if some env reset (true at any realistic env
   //      count); the tick-#1 state and the tick-dependent observation entries (foot contact,
-  //      targets) go to a side buffer, and k_fix restores them in a launch where no env reset.
+  //      targets) go to a side buffer, and k_obs restores them in a launch where no env reset.
   if (P.obs) {
     int i2 = idx, p2 = prev, n2 = next, c2 = count, w2 = swing;
     float pot2 = pot, op2 = old_pot, fc2[2] = {fc[0], fc[1]};
