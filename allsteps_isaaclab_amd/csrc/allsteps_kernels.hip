@@ -50,7 +50,7 @@ static_assert(MAXR <= 3 * MAXC, "a row index / 3 is a valid contact slot");
 // stay <= 20 KB so that 8 workgroups (2 waves/SIMD) fit a CU and 4096 envs run in one round.  The
 // phase-local arrays therefore share one union: FK (Rl) -> dynamics (c, Ib, Ic, V, A, F) ->
 // sweep (piv) -> constraint rows (Jm, Wm); each phase ends before the next one writes.
-constexpr int kPrioRows = 6;          // constraint rows per issue-priority level (see substep)
+constexpr int kPrioRows = 9;          // constraint rows per issue-priority level (see substep; 4 / 6 / 9 / 12 / 15 timed)
 constexpr int kRowGroup = 3;          // constraint rows per J / W / PGS group (a contact triplet)
 constexpr int LDJ = 28;               // J / W row stride (>= NV = 27)
 struct DynScratch {
