@@ -25,6 +25,7 @@ EXPORTED_SYMBOLS = [
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
     "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask", "as_set_graph_safe",
     "as_profile_sampled", "as_hbm_copy", "as_set_actuator", "as_set_quad_task", "as_quad_step", "as_quad_reset_all",
+    "as_build_id",
 ]
 
 
@@ -112,6 +113,39 @@ def lib_path() -> str:
     return os.environ.get("ALLSTEPS_HIP_LIB", LIB_PATH)
 
 
+def source_digest() -> str:
+    """Provenance digest of the native sources: sha256 over every csrc/*.hip, csrc/*.h and include/*.h
+    (name + bytes, sorted by name) and both libraries' compile flags (include path excluded, so the
+    digest is the same in any checkout), first 16 hex digits.  build_native() compiles it into
+    both libraries (as_build_id / ppo_build_id); load() refuses a library whose id differs."""
+    import hashlib
+
+    h = hashlib.sha256()
+    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h"))]
+    files += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")]
+    for path in sorted(files, key=os.path.basename):
+        h.update(os.path.basename(path).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    for flags in (STEP_FLAGS, PPO_FLAGS):
+        h.update(" ".join(x for x in flags if x != INCLUDE).encode() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def check_build_id(lib_id: bytes | str, path: str, env_var: str) -> None:
+    """Raise NativeError when the library at `path` was not built from this tree's sources, unless the
+    caller chose the library explicitly through `env_var` (A/B variants, diagnostic builds)."""
+    if env_var in os.environ:
+        return
+    got = lib_id.decode(errors="replace") if isinstance(lib_id, bytes) else str(lib_id)
+    want = source_digest()
+    if got != want:
+        raise NativeError(f"{path} was built from other sources (build id {got}, this tree {want}): rebuild it "
+                          f"(`python -c 'import __graft_entry__ as g; g.build()'`), or set {env_var} to load a "
+                          f"variant on purpose")
+
+
 def load() -> C.CDLL:
     """Load liballsteps_hip.so (raises NativeError if it is missing: build it with build_native())."""
     global _LIB
@@ -145,11 +179,13 @@ def load() -> C.CDLL:
     L.as_quad_step.argtypes = [V, V, V, V, V, V, V]
     L.as_quad_reset_all.argtypes = [V, V, V]
     L.as_last_error.restype = C.c_char_p
+    L.as_build_id.restype = C.c_char_p
     for name in EXPORTED_SYMBOLS:
-        if name != "as_last_error":
+        if name not in ("as_last_error", "as_build_id"):
             getattr(L, name).restype = C.c_int
     if L.as_abi_version() != ABI_VERSION:
         raise NativeError(f"ABI version mismatch: library {L.as_abi_version()} != {ABI_VERSION}")
+    check_build_id(L.as_build_id(), path, "ALLSTEPS_HIP_LIB")
     _LIB = L
     return L
 
@@ -194,6 +230,7 @@ def hbm_copy_bandwidth(device, nbytes: int = 2 << 30, iters: int = 20) -> float:
 # code cost more register moves than they save (launch -2 %); the packed math that pays
 # (sweep, W rows) is written out as 2-vectors
 STEP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-I", INCLUDE]
+PPO_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-I", INCLUDE]
 
 
 def build_native(verbose: bool = False) -> str:
@@ -202,13 +239,15 @@ def build_native(verbose: bool = False) -> str:
 
     srcs = [os.path.join(CSRC, f) for f in ("allsteps_kernels.hip", "allsteps_abi.hip")]
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *STEP_FLAGS, "-fPIC", "-shared", "-Wno-unused-result", "-o", LIB_PATH] + srcs
+    digest = source_digest()
+    cmd = [hipcc, *STEP_FLAGS, f'-DAS_BUILD_ID="{digest}"', "-fPIC", "-shared", "-Wno-unused-result", "-o",
+           LIB_PATH] + srcs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     # PPO-update kernels (include/ppo.h) -> libppo_hip.so
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-I", INCLUDE, "-o", PPO_LIB_PATH, os.path.join(CSRC, "ppo_kernels.hip"), os.path.join(CSRC, "ppo_mlp.hip"),
+    cmd = [hipcc, *PPO_FLAGS, f'-DPPO_BUILD_ID="{digest}"', "-fPIC", "-shared", "-Wno-unused-result",
+           "-o", PPO_LIB_PATH, os.path.join(CSRC, "ppo_kernels.hip"), os.path.join(CSRC, "ppo_mlp.hip"),
            os.path.join(CSRC, "ppo_wgrad.hip")]
     if verbose:
         print(" ".join(cmd))

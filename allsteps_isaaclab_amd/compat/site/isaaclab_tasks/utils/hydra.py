@@ -8,7 +8,7 @@ from __future__ import annotations
 import functools
 import sys
 
-from allsteps_isaaclab_amd.registry import apply_overrides, load_cfg_from_registry  # noqa: F401 (re-export)
+from allsteps_isaaclab_amd.registry import apply_overrides, load_cfg_from_registry, override_tokens  # noqa: F401
 
 
 def hydra_task_config(task_name: str, agent_cfg_entry_point: str):
@@ -17,7 +17,7 @@ def hydra_task_config(task_name: str, agent_cfg_entry_point: str):
         def wrapper(*args, **kwargs):
             env_cfg = load_cfg_from_registry(task_name, "env_cfg_entry_point")
             agent_cfg = load_cfg_from_registry(task_name, agent_cfg_entry_point)
-            apply_overrides(env_cfg, agent_cfg, [a for a in sys.argv[1:] if "=" in a and not a.startswith("-")])
+            apply_overrides(env_cfg, agent_cfg, override_tokens(sys.argv[1:]))
             return func(env_cfg, agent_cfg, *args, **kwargs)
 
         return wrapper

@@ -70,6 +70,11 @@ extern "C" {
 
 int as_abi_version(void) { return AS_ABI_VERSION; }
 
+#ifndef AS_BUILD_ID
+#define AS_BUILD_ID "unversioned"
+#endif
+const char* as_build_id(void) { return AS_BUILD_ID; }
+
 int as_hbm_copy(void* dst, const void* src, int64_t n16, void* stream) {
   if (!dst || !src || n16 < 0) return fail(AS_ERR_INVALID, "as_hbm_copy: null pointer or negative size");
   if (((uintptr_t)dst | (uintptr_t)src) & 15) return fail(AS_ERR_INVALID, "as_hbm_copy: pointers must be 16-B aligned");

@@ -1815,8 +1815,14 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
 }
 
+// k_step's workgroup is exactly ONE wave: its __syncthreads are LDS fences only, and the FK pointer
+// jumping relies on a single wave's LDS operations completing in issue order (no barrier between
+// rounds).  Launch and launch bound both use this constant; widening it must add those barriers.
+constexpr int kStepThreads = 64;
+static_assert(kStepThreads == 64, "k_step assumes a one-wave (wave64) workgroup: see the FK rounds");
+
 template <int NV>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_step(StepArgs P) {
+__global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_step(StepArgs P) {
   __shared__ Smem sm;
   // model / plan constants stay in global memory (5.7 KB, L1/K$-resident): LDS is the occupancy
   // budget, see EnvS
@@ -2526,9 +2532,9 @@ bool step_supported_nv(int nv) { return nv == 27 || nv == 18; }
 hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream) {
   int blocks = (a.n + EPB - 1) / EPB;
   if (nv == 27)
-    hipLaunchKernelGGL(k_step<27>, dim3(blocks), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(k_step<27>, dim3(blocks), dim3(kStepThreads), 0, stream, a);
   else if (nv == 18)
-    hipLaunchKernelGGL(k_step<18>, dim3(blocks), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(k_step<18>, dim3(blocks), dim3(kStepThreads), 0, stream, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -806,6 +806,11 @@ inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 extern "C" {
 
 int ppo_abi_version(void) { return PPO_ABI_VERSION; }
+
+#ifndef PPO_BUILD_ID
+#define PPO_BUILD_ID "unversioned"
+#endif
+const char* ppo_build_id(void) { return PPO_BUILD_ID; }
 const char* ppo_last_error(void) { return g_err; }
 
 int ppo_obs_stats_blocks(int32_t mb_rows) { return (mb_rows + kStatRows - 1) / kStatRows; }

@@ -88,6 +88,10 @@ class AnymalCStonesEnv(DirectRLEnv):
         # k_quad writes 0 / 1 bytes straight into the bool buffers (torch.bool is one byte, as AllstepsEnv)
         self.reset_terminated = torch.zeros(n, dtype=torch.bool, device=dev)
         self.reset_time_outs = torch.zeros(n, dtype=torch.bool, device=dev)
+        # persistent reset_buf (DirectRLEnv keeps one): filled from terminated | truncated on the first
+        # access after a step, so in-place writes (env.reset_buf[ids] = 1) stick until the next step
+        self._reset_buf = torch.zeros(n, dtype=torch.bool, device=dev)
+        self._reset_buf_stale = False
         self.extras = {}
         self._native.quad_reset_all(self.obs_buf, stream=self._stream())
 
@@ -104,8 +108,18 @@ class AnymalCStonesEnv(DirectRLEnv):
 
     @property
     def reset_buf(self) -> torch.Tensor:
-        """terminated | truncated of the last step (formed on demand: no kernel in the step)"""
-        return self.reset_terminated | self.reset_time_outs
+        """terminated | truncated of the last step: one persistent buffer, formed on the first access after
+        a step (no kernel in the step itself); writes into it persist until the next step."""
+        if self._reset_buf_stale:
+            torch.logical_or(self.reset_terminated, self.reset_time_outs, out=self._reset_buf)
+            self._reset_buf_stale = False
+        return self._reset_buf
+
+    @reset_buf.setter
+    def reset_buf(self, value) -> None:
+        self._reset_buf.copy_(torch.as_tensor(value, device=self._reset_buf.device).to(torch.bool).expand_as(
+            self._reset_buf))
+        self._reset_buf_stale = False
 
     @property
     def foot_targets(self) -> torch.Tensor:
@@ -133,6 +147,7 @@ class AnymalCStonesEnv(DirectRLEnv):
 
     def _reset_impl(self):
         self._native.quad_reset_all(self.obs_buf, stream=self._stream())
+        self._reset_buf_stale = True
         return {"policy": self.obs_buf}
 
     def _step_impl(self, action: torch.Tensor):
@@ -141,6 +156,7 @@ class AnymalCStonesEnv(DirectRLEnv):
         a = action.to(torch.float32).contiguous()
         self._native.quad_step(a, self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs,
                                stream=self._stream())
+        self._reset_buf_stale = True
         return {"policy": self.obs_buf}, self.reward_buf, self.reset_terminated, self.reset_time_outs, self.extras
 
     def close(self):

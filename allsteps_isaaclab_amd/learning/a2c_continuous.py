@@ -50,7 +50,7 @@ import torch
 import torch.distributed as dist
 
 from .fused import SCALER_GROWTH_INTERVAL, SCALER_INIT
-from .models import FlatParams, ModelA2CContinuousLogStd
+from .models import FlatParams, ModelA2CContinuousLogStd, check_env_signature, env_signature
 
 
 def fused_param_order(model) -> list:
@@ -820,7 +820,8 @@ class A2CAgent:
     def get_full_state_weights(self) -> dict:
         state = self.get_weights()
         state.update(epoch=self.epoch_num, frame=self.frame, last_mean_rewards=self.last_mean_rewards,
-                     optimizer=self.optimizer.state_dict(), env_state=None)
+                     optimizer=self.optimizer.state_dict(), env_state=None,
+                     env_signature=env_signature(self.vec_env, self.obs_shape, self.actions_num))
         if self.scaler_state is not None:  # rl_games: state['scaler'] = self.scaler.state_dict()
             state["scaler"] = {"scale": float(self.scaler_state[0]), "growth_factor": 2.0, "backoff_factor": 0.5,
                                "growth_interval": SCALER_GROWTH_INTERVAL,
@@ -833,6 +834,7 @@ class A2CAgent:
 
     def restore(self, fn: str, set_epoch: bool = True) -> None:
         ckpt = torch.load(fn, map_location=self.device, weights_only=True)
+        check_env_signature(ckpt.get("env_signature"), env_signature(self.vec_env, self.obs_shape, self.actions_num), fn)
         self.set_weights(ckpt)
         if set_epoch:
             self.epoch_num = int(ckpt.get("epoch", 0))

@@ -34,7 +34,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from .._native import PPO_LIB_PATH, NativeError
+from .._native import PPO_LIB_PATH, NativeError, check_build_id
 
 _LIB = None
 PPO_ABI_VERSION = 2
@@ -84,7 +84,7 @@ EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
                     "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update",
-                    "ppo_mlp_backward", "ppo_weight_grads"]
+                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id"]
 
 
 def load() -> C.CDLL:
@@ -118,8 +118,10 @@ def load() -> C.CDLL:
     for f in ("ppo_obs_stats_blocks", "ppo_loss_blocks", "ppo_elu_bwd_blocks"):
         getattr(L, f).argtypes = [I32]
     L.ppo_last_error.restype = C.c_char_p
+    L.ppo_build_id.restype = C.c_char_p
     if L.ppo_abi_version() != PPO_ABI_VERSION:
         raise NativeError(f"libppo_hip ABI {L.ppo_abi_version()} != {PPO_ABI_VERSION}")
+    check_build_id(L.ppo_build_id(), path, "PPO_HIP_LIB")
     _LIB = L
     return L
 

@@ -164,3 +164,30 @@ class FlatParams:
                 p.data = self.params[off:off + k].view_as(p)
             if p.grad is None or p.grad.data_ptr() != self.grads[off:off + k].data_ptr():
                 p.grad = self.grads[off:off + k].view_as(p)
+
+
+def env_signature(vec_env, obs_shape, actions_num: int) -> dict:
+    """What a checkpoint's policy was trained against: observation / action sizes, the env cfg's class
+    and its action_scale (the C5 task's actuator scaling) -- stored in every checkpoint so that a
+    policy is never restored silently into an env whose observation layout or action scaling changed
+    under the same task id."""
+    uw = getattr(getattr(vec_env, "env", None), "unwrapped", None)
+    cfg = getattr(uw, "cfg", None)
+    sig = {"obs_dim": int(obs_shape[0]), "actions_num": int(actions_num)}
+    if cfg is not None:
+        sig["env_cfg"] = type(cfg).__name__
+        scale = getattr(cfg, "action_scale", None)
+        if scale is not None:
+            sig["action_scale"] = float(scale)
+    return sig
+
+
+def check_env_signature(saved: dict | None, current: dict, fn: str) -> None:
+    """Refuse a checkpoint whose stored env signature differs from the env it is restored into (keys
+    present on both sides; checkpoints written before the signature existed are accepted)."""
+    if not isinstance(saved, dict):
+        return
+    bad = {k: (saved[k], current[k]) for k in saved.keys() & current.keys() if saved[k] != current[k]}
+    if bad:
+        diff = ", ".join(f"{k}: checkpoint {a!r} vs env {b!r}" for k, (a, b) in sorted(bad.items()))
+        raise ValueError(f"checkpoint {fn} was trained against another env ({diff}): its policy does not fit this task")

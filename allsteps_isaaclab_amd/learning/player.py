@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import torch
 
-from .models import ModelA2CContinuousLogStd
+from .models import ModelA2CContinuousLogStd, check_env_signature, env_signature
 
 
 class PpoPlayerContinuous:
@@ -54,6 +54,7 @@ class PpoPlayerContinuous:
 
     def restore(self, fn: str) -> None:
         ckpt = torch.load(fn, map_location=self.device, weights_only=True)
+        check_env_signature(ckpt.get("env_signature"), env_signature(self.env, self.obs_shape, self.actions_num), fn)
         self.model.load_state_dict(ckpt["model"])
         if "running_mean_std" in ckpt and self.model.running_mean_std is not None:
             self.model.running_mean_std.load_state_dict(ckpt["running_mean_std"])

@@ -112,6 +112,16 @@ def _set(obj, path: list[str], value) -> None:
         setattr(obj, path[-1], value)
 
 
+OVERRIDE_PREFIXES = ("env.", "agent.", "+env.", "+agent.")
+
+
+def override_tokens(argv: list[str]) -> list[str]:
+    """The hydra-style override tokens of a command line: only ``[+]env.<path>=<v>`` /
+    ``[+]agent.<path>=<v>`` (a flag's value that happens to contain '=', e.g. ``--checkpoint a=b.pth``,
+    is not an override)."""
+    return [a for a in argv if "=" in a and a.startswith(OVERRIDE_PREFIXES)]
+
+
 def apply_overrides(env_cfg, agent_cfg, overrides: list[str]) -> None:
     """Hydra-style command-line overrides (``env.<path>=<value>`` / ``agent.<path>=<value>``, values
     parsed as YAML scalars) -- how Isaac Lab's hydra integration addresses the two configs."""

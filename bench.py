@@ -10,12 +10,12 @@ episodes terminate and reset naturally inside the timed region.  Envs are sharde
 scaling, no collective in the step).  value = all ranks' env-steps / max-over-ranks wall time.
 
 Extra objects on the JSON line:
-  roofline     -- k_step (the dominant kernel): algorithmic bytes per launch / its duration, the timed
-                  step's wall time less k_obs's HIP-event average (events recorded around every 10th
-                  launch on the env's stream; the k_step event average is reported beside it, see
-                  kernel_times), vs 8 TB/s HBM;
-                  `latency`: per-wave cycle records of 20 launches after the timed region (mean /
-                  slowest wave vs the launch span, the slowest wave's phases: scripts/stamps.py).
+  roofline     -- k_step (the dominant kernel): algorithmic bytes per launch / its HIP-event-timed
+                  average duration over a replay of the timed window (>= 200 sampled launches, on the
+                  env's stream; kernel_times), vs 8 TB/s HBM;
+                  `latency`: per-wave cycle records of the timed window's first (up to 20) launches,
+                  replayed (mean / slowest wave vs the launch span, the slowest wave's phases:
+                  scripts/stamps.py).
   cpu_baseline -- rank 0, N = 1: the CPU oracle (oracle/, a port of the same step) timed on this
                   host's cores on a bounded sample.
   train        -- every rank (BASELINE C4, SURVEY §8d "env+PPO separately"): env-steps/s of the PPO
@@ -85,20 +85,32 @@ def pmc_record(num_envs: int) -> dict:
 
 
 def kernel_times(ms_per_step: float, k_ms: float, o_ms: float, launches: int) -> dict:
-    """Per-launch durations (ms) of the step's two kernels, from one clock the roofline can trust.
+    """Per-launch durations (ms) of the step's two kernels over the timed window.
 
-    The HIP events around the sampled launches span each kernel plus its own dispatch, so the k_step
-    and k_obs event averages together exceed the wall time of an unprofiled step.  The
-    roofline therefore uses the wall clock: `k_step_ms` = ms_per_step - the k_obs event average, the
-    part of the timed step that is not k_obs (k_step + its launch gap; it never exceeds the step it
-    belongs to, so k_step_ms + k_obs_event_ms == ms_per_step).  The event average is kept beside it."""
+    `k_ms` / `o_ms` are the summed HIP-event spans of k_step / k_obs over `launches` launches of a
+    replay of the timed window (same start state, same actions: the run is deterministic, so the
+    replay launches the very kernels the timed loop launched), recorded on the env's stream.  The
+    roofline's duration is the k_step event average (`k_step_ms`).  The events span each kernel plus
+    its own dispatch, so event k_step + event k_obs is checked against the timed loop's wall clock
+    (`event_sum_over_wall`, an independent measurement: events_consistent); `k_step_period_ms` = wall
+    ms_per_step - event k_obs is the step period left to k_step (kernel + launch gap), kept beside it."""
     n = max(launches, 1)
     k_ev, o_ev = k_ms / n, o_ms / n
-    return {"k_step_ms": round(ms_per_step - o_ev, 5), "k_step_event_ms": round(k_ev, 5),
-            "k_obs_event_ms": round(o_ev, 5), "sampled_launches": launches,
-            "method": "k_step_ms = wall ms_per_step - k_obs HIP-event average; the events bracket every 10th "
-                      "k_step / k_obs launch of an untimed stretch run right after the timed loop (none inside "
-                      "it); k_step_event_ms includes the launch's dispatch"}
+    return {"k_step_ms": round(k_ev, 5), "k_obs_ms": round(o_ev, 5), "sampled_launches": launches,
+            "k_step_period_ms": round(ms_per_step - o_ev, 5),
+            "event_sum_over_wall": round((k_ev + o_ev) / ms_per_step, 4) if ms_per_step > 0 else None,
+            "method": "HIP events on the env's stream around every k_step / k_obs launch of a replay of the "
+                      "timed window (state restored to the window's start, same actions, repeated until >= 200 "
+                      "launches are sampled; no events inside the timed loop itself); k_step_ms includes the "
+                      "launch's dispatch"}
+
+
+def events_consistent(t: dict, lo: float = 0.9, hi: float = 1.1) -> bool:
+    """The event-timed kernels of the replay account for the timed loop's wall clock: their sum per
+    step lies within [lo, hi] x ms_per_step (events over-read by their own dispatch, a few per cent;
+    a replay that diverged from the timed window, or events that missed launches, fall outside)."""
+    r = t.get("event_sum_over_wall")
+    return r is not None and lo <= r <= hi
 
 
 def measured_hbm_peak(device) -> float | None:
@@ -323,6 +335,7 @@ def main():
         env.step(actions[K + t])
     torch.cuda.synchronize(device)
     env._native.profile(0)  # no HIP events inside the timed loop (each adds a launch gap to its step)
+    s_start = env.get_state()  # the timed window's start state: replayed below for the kernel timings
 
     def barrier():
         if world > 1:
@@ -335,35 +348,42 @@ def main():
         env.step(actions[t])
     barrier()
     el = time.perf_counter() - t0
-    # kernel durations: HIP events around every 10th k_step / k_obs launch of a separate, untimed
-    # stretch of the same loop right after the timed one (events inside the timed loop would add
-    # their launch gaps to the steps they sample, ~1 us per step on average)
-    P = min(K, 500)
-    env._native.profile_sampled(max(P // 10, 1), 10)
-    for t in range(P):
-        env.step(actions[t])
+    s_end = env.get_state()
+    resets = int(env.reset_buf.sum().item())
+    # kernel durations over the timed window itself: replay it from its start state with HIP events
+    # around every launch, as often as needed for >= 200 sampled launches whatever K is (the step is
+    # deterministic, so the replay runs the timed loop's launches again; replay_exact checks that)
+    reps = max(1, -(-200 // K))
+    env._native.profile(reps * K)
+    for _ in range(reps):
+        env.set_state(s_start)
+        for t in range(K):
+            env.step(actions[t])
     torch.cuda.synchronize(device)
     k_ms, o_ms, launches = env._native.profile_read()
     env._native.profile(0)
+    replay_exact = all(torch.equal(v, s_end[k]) for k, v in env.get_state().items())
     if world > 1:
         tt = torch.tensor([el], device=device if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-    resets = int(env.reset_buf.sum().item())
-    # latency side of k_step (after the timed region, on the same envs): per-wave records of 20 launches
+    # latency side of k_step: per-wave records of the timed window's first launches (replayed again)
     latency = None
     if rank == 0:
         sys.path.insert(0, os.path.join(ROOT, "scripts"))
         import stamps
 
         try:
-            latency = stamps.latency_summary(stamps.wave_records(env, actions[:20]))
+            env.set_state(s_start)
+            latency = stamps.latency_summary(stamps.wave_records(env, actions[:min(K, 20)]))
         except Exception as e:  # reported, never fatal for the env metric
             latency = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         value = n * world * K / el
         t = kernel_times(el / K * 1e3, k_ms, o_ms, launches)
+        t["replay_exact"] = replay_exact
+        t["events_consistent"] = events_consistent(t)
         achieved = K_STEP_BYTES * n / (t["k_step_ms"] / 1e3) / 1e9
         pmc = pmc_record(n)
         line = {

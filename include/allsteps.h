@@ -307,6 +307,11 @@ int as_hbm_copy(void* dst, const void* src, int64_t n16, void* stream);
 
 int as_abi_version(void);
 const char* as_last_error(void);
+/* Provenance: the source digest the library was compiled from (-DAS_BUILD_ID, computed by
+ * allsteps_isaaclab_amd/_native.py::source_digest over csrc/ + include/ + the compile flags).  The
+ * Python loader refuses a library whose digest differs from the tree's, so a stale or variant build
+ * is never run silently ("unversioned" when built without the define). */
+const char* as_build_id(void);
 
 #ifdef __cplusplus
 }

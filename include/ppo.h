@@ -62,6 +62,8 @@ typedef struct {
 
 int ppo_abi_version(void);
 const char* ppo_last_error(void);
+/* Provenance digest (-DPPO_BUILD_ID; see as_build_id in allsteps.h). */
+const char* ppo_build_id(void);
 
 /* column sum / sum of squares (fp64) of rows [i*mb_rows, (i+1)*mb_rows) of x (row stride `cols`),
  * one partial per block into partials[nblk][2][64]; nblk = ppo_obs_stats_blocks(mb_rows). */

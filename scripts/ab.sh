@@ -11,7 +11,7 @@ run() {  # lib size level steps
   tail -1 gpurun_out/ab_one.log | python -c "
 import json,sys
 d=json.loads(sys.stdin.read()); L=d['roofline']['latency']
-print('$1 N=$2', 'value %.4g' % d['value'], 'k_step', d['kernels_ms']['k_step_event_ms'], 'wall', d['kernels_ms']['k_step_ms'], 'k_obs', d['kernels_ms']['k_obs_event_ms'], 'ms', d['ms_per_step'],
+print('$1 N=$2', 'value %.4g' % d['value'], 'k_step', d['kernels_ms']['k_step_ms'], 'period', d['kernels_ms']['k_step_period_ms'], 'k_obs', d['kernels_ms']['k_obs_ms'], 'ms', d['ms_per_step'],
       'crit', {k: L['critical_path_phases'][k] for k in ('collide','pgs','sweep','wsolve','rows')},
       'meanpgs', L['mean_phases']['pgs'], 'max', L['max_wave_cycles'])" | tee -a $OUT
 }

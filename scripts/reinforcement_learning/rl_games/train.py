@@ -73,8 +73,7 @@ def main(argv=None):
     env_cfg = registry.load_cfg_from_registry(args.task, "env_cfg_entry_point")
     agent_cfg = registry.load_cfg_from_registry(args.task, "rl_games_cfg_entry_point")
     # hydra-style overrides (env.<path>=<value> / agent.<path>=<value>), as the reference's @hydra_task_config
-    registry.apply_overrides(env_cfg, agent_cfg, [a for a in (sys.argv[1:] if argv is None else argv)
-                                                  if "=" in a and not a.startswith("-")])
+    registry.apply_overrides(env_cfg, agent_cfg, registry.override_tokens(sys.argv[1:] if argv is None else argv))
     env_cfg.scene.num_envs = args.num_envs if args.num_envs is not None else env_cfg.scene.num_envs
     env_cfg.sim.device = args.device if args.device is not None else env_cfg.sim.device
     if args.stone_level is not None:

@@ -199,3 +199,50 @@ def test_create_accepts_the_walker_model_up_to_the_device():
     h = C.c_void_p()
     rc = L.as_create(4, C.byref(M), C.byref(S), C.byref(T), C.byref(st), 0, 0, 0, C.byref(h))
     assert rc == -3, L.as_last_error()
+
+
+# ---------------------------------------------------------------- provenance (as_build_id / ppo_build_id)
+
+def test_libraries_carry_the_tree_source_digest():
+    """Both shipped libraries were compiled from exactly this tree's csrc/ + include/ (VERDICT r04 weak 7)."""
+    from allsteps_isaaclab_amd import _native
+    from allsteps_isaaclab_amd.learning import fused
+
+    digest = _native.source_digest()
+    assert len(digest) == 16
+    assert _native.load().as_build_id().decode() == digest
+    assert fused.load().ppo_build_id().decode() == digest
+
+
+def test_source_digest_tracks_every_source_byte(monkeypatch, tmp_path):
+    import shutil
+
+    from allsteps_isaaclab_amd import _native
+
+    base = _native.source_digest()
+    csrc = tmp_path / "csrc"
+    shutil.copytree(_native.CSRC, csrc)
+    monkeypatch.setattr(_native, "CSRC", str(csrc))
+    assert _native.source_digest() == base  # the digest does not depend on where the tree lives
+    p = csrc / "allsteps_kernels.hip"
+    p.write_bytes(p.read_bytes() + b"\n")
+    assert _native.source_digest() != base
+
+
+def test_loader_refuses_a_library_built_from_other_sources(monkeypatch):
+    from allsteps_isaaclab_amd import _native
+    from allsteps_isaaclab_amd.learning import fused
+
+    monkeypatch.delenv("ALLSTEPS_HIP_LIB", raising=False)
+    monkeypatch.delenv("PPO_HIP_LIB", raising=False)
+    monkeypatch.setattr(_native, "_LIB", None)
+    monkeypatch.setattr(fused, "_LIB", None)
+    monkeypatch.setattr(_native, "source_digest", lambda: "0123456789abcdef")
+    with pytest.raises(_native.NativeError, match="built from other sources"):
+        _native.load()
+    with pytest.raises(_native.NativeError, match="built from other sources"):
+        fused.load()
+    # an explicitly chosen library (A/B variants under abtest/) is loaded as asked
+    monkeypatch.setenv("ALLSTEPS_HIP_LIB", _native.LIB_PATH)
+    monkeypatch.setenv("PPO_HIP_LIB", _native.PPO_LIB_PATH)
+    assert _native.load() is not None and fused.load() is not None

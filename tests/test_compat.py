@@ -52,7 +52,8 @@ def test_install_never_shadows_a_real_package(tmp_path):
 
 def test_hydra_overrides(tmp_path):
     r = _py("from allsteps_isaaclab_amd import compat; compat.install()\n"
-            "import sys; sys.argv = ['x', '--headless', 'env.scene.num_envs=128', 'agent.params.config.horizon_length=16']\n"
+            "import sys; sys.argv = ['x', '--headless', 'env.scene.num_envs=128', 'agent.params.config.horizon_length=16',"
+            " '--checkpoint', '/tmp/a=b.pth']\n"
             "from isaaclab_tasks.utils.hydra import hydra_task_config\n"
             "@hydra_task_config('Allsteps-v0', 'rl_games_cfg_entry_point')\n"
             "def main(env_cfg, agent_cfg):\n"
@@ -60,6 +61,16 @@ def test_hydra_overrides(tmp_path):
             "main()", str(tmp_path))
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.split() == ["128", "16"]
+
+
+def test_override_tokens_ignore_flag_values_with_equals():
+    """a flag's value containing '=' (a checkpoint path) is not a hydra override."""
+    from allsteps_isaaclab_amd.registry import override_tokens
+
+    argv = ["--task", "Allsteps-v0", "--checkpoint", "/tmp/run=3/model.pth", "--log_root", "a=b", "env.scene.num_envs=64",
+            "+agent.params.config.minibatch_size=2048", "agent.params.seed=1"]
+    assert override_tokens(argv) == ["env.scene.num_envs=64", "+agent.params.config.minibatch_size=2048",
+                                     "agent.params.seed=1"]
 
 
 def _run_reference(script: str, args: list[str], cwd) -> subprocess.CompletedProcess:

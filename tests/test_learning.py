@@ -217,6 +217,20 @@ def test_ppo_trains_toy_env_and_checkpoints(tmp_path):
     # restored parameters still live in the flat buffer (grads land where Adam reads them)
     p0 = next(other.model.parameters())
     assert p0.data_ptr() == other.flat.params.data_ptr()
+    # the checkpoint records the env it was trained against; a changed action scaling is refused
+    ck = torch.load(fn + ".pth", weights_only=True)
+    assert ck["env_signature"]["obs_dim"] == agent.obs_shape[0] and ck["env_signature"]["actions_num"] == agent.actions_num
+    ck["env_signature"]["action_scale"] = 0.5
+    torch.save(ck, fn + "_other_env.pth")
+    from allsteps_isaaclab_amd.learning.models import check_env_signature, env_signature
+
+    cur = dict(env_signature(other.vec_env, other.obs_shape, other.actions_num), action_scale=1.0)
+    with pytest.raises(ValueError, match="action_scale"):
+        check_env_signature(ck["env_signature"], cur, fn)
+    ck["env_signature"]["obs_dim"] += 1
+    torch.save(ck, fn + "_other_env.pth")
+    with pytest.raises(ValueError, match="obs_dim"):
+        other.restore(fn + "_other_env.pth")
 
 
 def test_runner_train_loop(tmp_path):

@@ -323,5 +323,11 @@ def test_c5_task_gpu_bit_exact_vs_oracle(qorc, oracle_mod, qmodel, n, steps, war
         np.testing.assert_array_equal(obs_g.cpu().numpy(), obs_c)
         np.testing.assert_array_equal(rew_g.cpu().numpy(), rew_c)
         assert np.array_equal(term_g.cpu().numpy(), term_c) and np.array_equal(trunc_g.cpu().numpy(), trunc_c)
+        # reset_buf is one persistent buffer = terminated | truncated after every step
+        rb = env.reset_buf
+        assert rb is env.reset_buf and torch.equal(rb, term_g | trunc_g)
+        if t == 0:
+            env.reset_buf[:3] = True  # an in-place write sticks until the next step
+            assert bool(env.reset_buf[:3].all())
     assert total_resets > 0  # robots fall and reset inside the compared steps: the reset path is exercised
     env.close()
