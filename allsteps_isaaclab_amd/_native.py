@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = [
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
     "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask", "as_set_graph_safe",
     "as_profile_sampled", "as_hbm_copy", "as_set_actuator", "as_set_quad_task", "as_quad_step", "as_quad_reset_all",
-    "as_build_id",
+    "as_build_id", "as_step_counters_host",
 ]
 
 
@@ -173,6 +173,7 @@ def load() -> C.CDLL:
     L.as_generate_stones.argtypes = [V, I32, V, V]
     L.as_step_counters.argtypes = [V, C.POINTER(V)]
     L.as_get_curriculum_host.argtypes = [V, C.POINTER(I32)]
+    L.as_step_counters_host.argtypes = [V, C.POINTER(I32), V]
     L.as_hbm_copy.argtypes = [V, V, I64, V]
     L.as_set_actuator.argtypes = [V, V]
     L.as_set_quad_task.argtypes = [V, V]
@@ -413,6 +414,13 @@ class NativeEnv:
 
     def debug_stamps(self, buf):
         check(self.L.as_debug_stamps(self.h, None if buf is None else buf.data_ptr()), "as_debug_stamps")
+
+    def counters_host(self, stream=None) -> list:
+        """The last step's counter words [any reset, target-index sum, regen level, contacts dropped]
+        (synchronises `stream`)."""
+        out = (C.c_int32 * 4)()
+        check(self.L.as_step_counters_host(self.h, out, stream), "as_step_counters_host")
+        return list(out)
 
     def counters_ptr(self) -> int:
         p = C.c_void_p()

@@ -464,6 +464,15 @@ int as_step_counters(as_env_t* env, const int32_t** counters_dev) {
   return AS_OK;
 }
 
+int as_step_counters_host(as_env_t* env, int32_t* out_host, void* stream) {
+  if (!env || !out_host) return fail(AS_ERR_INVALID, "as_step_counters_host: null argument");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipMemcpyAsync(out_host, env->counters_dev + as::kCntBank * env->last_bank, 4 * sizeof(int32_t),
+                         hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return AS_OK;
+}
+
 int as_get_curriculum_host(as_env_t* env, int32_t* level_host) {
   if (!env || !level_host) return fail(AS_ERR_INVALID, "as_get_curriculum_host: null argument");
   HIP_TRY(hipMemcpy(level_host, env->st.curriculum, sizeof(int32_t), hipMemcpyDeviceToHost));

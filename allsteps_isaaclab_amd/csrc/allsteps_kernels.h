@@ -67,6 +67,8 @@ enum {
 // Step counters, one bank per launch (two banks alternate; k_obs clears the next one):
 //   [0]  any env reset (plain store of 1)
 //   [1]  sum of curr_target_index over all envs, published by k_obs from the partial sums
+//   [2]  kCntLevel (regen_footsteps)
+//   [3]  contacts cut by the row budget in this launch, all envs and substeps (kCntDropped)
 //   [kCntStride * (1 + i)], i < kCntSlots: partial sums, one atomic per wave into slot block % kCntSlots
 //        (one 64-B line each: 4096 same-address atomics serialise at the memory side)
 constexpr int kCntSlots = 16;
@@ -80,6 +82,7 @@ constexpr int kSideObs = 11;
 constexpr int kSideRegen = kSideState + kSideObs;  // 1 = reset env due new stones (regen_footsteps)
 constexpr int kSideWords = kSideRegen + 1;
 constexpr int kCntLevel = 2;  // counter-bank word: the curriculum level k_step saw (k_obs regen level)
+constexpr int kCntDropped = 3;  // counter-bank word: contacts found past the row budget (as_step_counters [3])
 
 // k_quad (BASELINE C5 task epilogue, one env per lane)
 struct QuadArgs {

@@ -155,6 +155,7 @@ struct EnvS {
   float root_pos[3], root_quat[4];
   int cand[NST];
   uint32_t mask[4];     // contact sensors 0..3 (2, 3: a quadruped's hind feet)
+  int ndrop;            // contacts cut by the row budget over this launch's substeps (counters[kCntDropped])
 };
 
 struct Smem {
@@ -962,7 +963,8 @@ __device__ __forceinline__ GeomC load_geom(const Consts& K, int lane) {
   return c;
 }
 
-// At most ncap contacts, in priority order (oracle/physics.c collide() emits the same list):
+// At most ncap contacts, in priority order (oracle/physics.c collide() emits the same list); every
+// pair is still tested past the cap, and the contacts found beyond it are counted in s.ndrop:
 //   1. the priority geoms (the feet: geoms [0, num_priority_geoms)) against the candidate stones,
 //      stone-major, geom-minor;  2. every other geom against the candidate stones, likewise;
 //   3. robot self-contacts, one per self-collision pair in table order.
@@ -1033,8 +1035,8 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   // appends the surviving (stone, geom) pairs to a list in LDS, in emission order.  (B) lane = pair,
   // in chunks of kPairsPerChunk: the exact test (capsules: slope bisection for the segment's closest
   // point) and the contacts, emitted in list order by a prefix sum.  A chunk is flushed as soon as
-  // kPairsPerChunk pairs are pending, so the list never exceeds 32 + 22 entries, and the search
-  // stops once this env has ncap contacts.
+  // kPairsPerChunk pairs are pending, so the list never exceeds 32 + 22 entries; the search runs over
+  // every pair even past ncap contacts (the surplus is counted, not emitted).
   {
     float* gs = s.x.col.g[lane];  // staging of this lane's geom for pass B and the self pairs
     if (gv) {
@@ -1145,14 +1147,13 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   for (int cls = 0; cls < 2; ++cls) {
 #pragma unroll 1
     for (int ci = 0; ci < ncand; ++ci) {
-      if (base >= ncap) break;  // later contacts would be dropped anyway
       const uint32_t bl = cneed[ci] & (cls == 0 ? primask : ~primask);
       if ((bl >> lane) & 1u) pl[pend + __popc(bl & ((1u << lane) - 1u))] = (s.cand[ci] << 8) | lane;
       pend += __popc(bl);  // no barrier: the single wave's LDS operations complete in issue order
       if (pend >= kPairsPerChunk) flush(kPairsPerChunk);
     }
   }
-  if (pend > 0 && base < ncap) flush(pend);
+  if (pend > 0) flush(pend);
   // self-contacts.  (A) lane = pair: the bounding-sphere filter; the surviving pairs are appended to
   // the pending list in table order.  (B) lane = pending pair, in chunks of G: the capsule-capsule
   // closest points (include/as_detmath.h, shared with the oracle), emitted in list order.
@@ -1229,13 +1230,13 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
     for (int i = 0; i < kSelfW; ++i)
       if ((hbl[i] >> lane) & 1u) pl[at[i]] = spw[i];
     pend = tot;
-    while (pend > 0 && base < ncap) flush_self(pend < G ? pend : G);
+    while (pend > 0) flush_self(pend < G ? pend : G);
   } else {
     // a rolled loop (one copy of flush_self: code size is instruction-cache footprint); word i of
     // the register arrays by a select chain
 #pragma unroll 1
     for (int i = 0; i < kSelfW; ++i) {
-      if (G * i >= nsp || base >= ncap) break;
+      if (G * i >= nsp) break;
       uint32_t bl = hbl[0];
       int w = spw[0];
 #pragma unroll
@@ -1247,8 +1248,10 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
       pend += __popc(bl);
       if (pend >= G) flush_self(G);
     }
-    if (pend > 0 && base < ncap) flush_self(pend);
+    if (pend > 0) flush_self(pend);
   }
+  // the search runs to the end: contacts past the cap are found, not emitted, and counted
+  if (lane == 0 && base > ncap) s.ndrop += base - ncap;
   __syncthreads();
   return base < ncap ? base : ncap;  // uniform over the env's half-wave
 }
@@ -1849,6 +1852,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2,
     s.u[3 + lane] = st.root_ang[lane * n + e];
   }
   if (lane < 4) s.root_quat[lane] = st.root_quat[lane * n + e];
+  if (lane == 0) s.ndrop = 0;
   const int cur = st.curriculum[0];
   const float gain = T.gain_curriculum[cur];
   if (lane < nh) {
@@ -1992,8 +1996,12 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2,
     const bool vdone = valid && done;
     const int wsum = __builtin_amdgcn_readlane(cidx, 0) + __builtin_amdgcn_readlane(cidx, 32);
     const bool wdone = __any(vdone);
+    // contacts the row budget cut in this launch (rare: one same-address atomic per wave that had any)
+    const int ndr = valid ? s.ndrop : 0;
+    const int wdrop = __builtin_amdgcn_readlane(ndr, 0) + __builtin_amdgcn_readlane(ndr, 32);
     if (threadIdx.x == 0) {
       atomicAdd(&P.counters[kCntStride * (1 + (int)(blockIdx.x % kCntSlots))], wsum);
+      if (wdrop) atomicAdd(&P.counters[kCntDropped], wdrop);
       if (wdone) P.counters[0] = 1;
       if (T.regen_footsteps) P.counters[kCntLevel] = P.st.curriculum[0];  // same value from every wave
     }

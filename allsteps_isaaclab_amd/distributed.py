@@ -10,9 +10,9 @@ collective inside ``env.step``.
   what the reference does under ``--distributed``); ``global_curriculum_mean`` is the optional
   4-byte all-reduce variant.
 * The only exchange is at the PPO update boundary: ``RolloutGather`` all-gathers a horizon of rollout
-  tensors from every rank in ONE collective per dtype over RCCL (xGMI ring; the payload is packed
-  into a single flat buffer so the ring runs at message sizes where the per-link bandwidth, not
-  latency, is the bound).  With the gloo backend (CPU tests) the same code path runs.
+  tensors from every rank, one collective per tensor straight into its output buffer over RCCL (each
+  is hundreds of KB to hundreds of MB, so the per-link bandwidth, not latency, is the bound).  With
+  the gloo backend (CPU tests) the same code path runs.
 """
 
 from __future__ import annotations
@@ -98,13 +98,16 @@ def global_curriculum_mean(env, group=None) -> float:
 class RolloutGather:
     """All-gather of a PPO horizon of rollout tensors across ranks.
 
-    ``gather({"obs": [H, N, 59], "actions": [H, N, 21], "rewards": [H, N], "dones": [H, N] (bool), ...})``
-    returns the same keys with the env axis (axis 1) concatenated over ranks in rank order
-    ([H, W N, ...]), i.e. global env id order.  Tensors are packed per dtype into one flat send
-    buffer; receive buffers are cached across calls (same shapes every horizon).
+    ``gather({"obs": [N H, 59], "actions": [N H, 21], "dones": [N H] (bool), ...})`` returns the same keys
+    with the env axis concatenated over ranks in rank order, i.e. global env order.  With the env axis
+    outermost (``env_axis=0``: the trainer's env-major flattened batch) the rank-major receive buffer
+    IS that concatenation, so every key is gathered straight into its own cached output tensor with one
+    ``all_gather_into_tensor`` (RCCL) -- no send-side packing and no copy after the collective; the
+    payloads are MB-sized, so the per-collective latency is negligible against the per-link
+    bandwidth.  For another env axis ([H, N, ...]) the parts are concatenated along it (one copy).
     """
 
-    def __init__(self, group=None, env_axis: int = 1):
+    def __init__(self, group=None, env_axis: int = 0):
         self.group = group
         self.env_axis = env_axis
         self._recv: dict = {}
@@ -112,35 +115,30 @@ class RolloutGather:
     def _world(self) -> int:
         return dist.get_world_size(self.group) if dist.is_initialized() else 1
 
+    def _out(self, key, t: torch.Tensor, world: int) -> torch.Tensor:
+        shape = (world * t.shape[0],) + tuple(t.shape[1:])
+        k = (key, t.dtype, shape, t.device)
+        buf = self._recv.get(k)
+        if buf is None:
+            buf = torch.empty(shape, dtype=t.dtype, device=t.device)
+            self._recv[k] = buf
+        return buf
+
     def gather(self, tensors: dict[str, torch.Tensor]) -> dict[str, torch.Tensor]:
         world = self._world()
         if world == 1:
             return dict(tensors)
+        backend = dist.get_backend(self.group)
         out: dict[str, torch.Tensor] = {}
-        by_dtype: dict[torch.dtype, list[str]] = {}
         for k, t in tensors.items():
-            by_dtype.setdefault(t.dtype, []).append(k)
-        for dtype, keys in by_dtype.items():
-            flat = torch.cat([tensors[k].contiguous().reshape(-1) for k in keys])
-            wire = flat.view(torch.uint8) if dtype == torch.bool else flat
-            key = (dtype, wire.numel(), wire.device)
-            recv = self._recv.get(key)
-            if recv is None:
-                recv = torch.empty(world * wire.numel(), dtype=wire.dtype, device=wire.device)
-                self._recv[key] = recv
-            backend = dist.get_backend(self.group)
+            t = t.contiguous()
+            src = t.movedim(self.env_axis, 0).contiguous() if self.env_axis != 0 else t
+            buf = self._out(k, src, world)
+            wire_src = src.view(torch.uint8) if src.dtype == torch.bool else src
+            wire_buf = buf.view(torch.uint8) if buf.dtype == torch.bool else buf
             if backend == "nccl":
-                dist.all_gather_into_tensor(recv, wire, group=self.group)
-            else:
-                dist.all_gather(list(recv.chunk(world)), wire, group=self.group)
-            parts = recv.chunk(world)
-            if dtype == torch.bool:
-                parts = [p.view(torch.bool) for p in parts]
-            off = 0
-            for k in keys:
-                t = tensors[k]
-                n = t.numel()
-                pieces = [p[off:off + n].view(t.shape) for p in parts]
-                out[k] = torch.cat(pieces, dim=self.env_axis)
-                off += n
+                dist.all_gather_into_tensor(wire_buf, wire_src, group=self.group)
+            else:  # gloo (CPU tests, the shared-GPU rehearsal): views of the same buffer, no extra copy
+                dist.all_gather(list(wire_buf.chunk(world)), wire_src, group=self.group)
+            out[k] = buf if self.env_axis == 0 else buf.movedim(0, self.env_axis)
         return out

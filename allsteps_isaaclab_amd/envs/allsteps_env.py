@@ -297,6 +297,13 @@ class AllstepsEnv(DirectRLEnv):
         d = None if draws is None else draws.to(self._device).float().contiguous()
         self._native.generate_stones(int(level), d, stream=self._stream())
 
+    def dropped_contacts(self) -> int:
+        """Contacts the constraint budget (AS_MAX_CONTACTS contacts, AS_MAX_ROWS rows incl. the joint
+        limits) cut in the last step, over all envs and substeps -- PhysX keeps every contact
+        (simulation_cfg.py:110), so this is the step's deviation from it in contact count.  Reads the
+        device counter (as_step_counters word 3): synchronises the env's stream."""
+        return int(self._native.counters_host(self._stream())[3])
+
     def get_state(self) -> dict:
         """Copy of the full SoA state (field -> (rows, N) tensor)."""
         return {k: v.clone() for k, v in self.state.items()}

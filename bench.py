@@ -367,6 +367,13 @@ def main():
         tt = torch.tensor([el], device=device if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+    # contacts the constraint budget cut in the timed window (as_step_counters word 3 per step), on
+    # one more replay: the read synchronises every step, so it stays out of the timed and event loops
+    env.set_state(s_start)
+    dropped = 0
+    for t in range(K):
+        env.step(actions[t])
+        dropped += env.dropped_contacts()
     # latency side of k_step: per-wave records of the timed window's first launches (replayed again)
     latency = None
     if rank == 0:
@@ -419,6 +426,12 @@ def main():
                          "latency": latency},
             "cpu_baseline": None,
             "resets_last_step": resets,
+            # PhysX keeps every contact (simulation_cfg.py:110); this build's 30-row budget cuts these
+            "contacts_dropped": {"total": dropped, "per_step": round(dropped / K, 2),
+                                 "per_env_step": round(dropped / (K * n), 6),
+                                 "method": "as_step_counters word 3 summed over the timed window's K steps "
+                                           "(replayed from its start state): contacts the narrowphase found "
+                                           "beyond the 10-contact / 30-row cap, all envs and substeps"},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(n, args.level, args.cpu_threads)

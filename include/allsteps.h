@@ -295,8 +295,14 @@ int as_debug_stamps(as_env_t* env, uint64_t* stamps_dev);
  * of times.  Off (default): two banks, no memset (lowest eager launch count). */
 int as_set_graph_safe(as_env_t* env, int32_t on);
 
-/* Device counters of the last step: [0] = any env reset, [1] = sum of curr_target_index. */
+/* Device counters of the last step: [0] = any env reset, [1] = sum of curr_target_index, [3] = contacts
+ * the constraint budget cut (found by the narrowphase beyond the AS_MAX_CONTACTS / AS_MAX_ROWS - limit
+ * rows cap, summed over the step's envs and substeps; PhysX keeps every contact,
+ * simulation_cfg.py:110 gpu_max_rigid_contact_count = 2**23).  Valid until the step after next. */
 int as_step_counters(as_env_t* env, const int32_t** counters_dev);
+/* The same four words [0..3] copied to the host after `stream` (the stream the step ran on) drains;
+ * synchronises the stream -- a diagnostic read (tests, bench), never inside a timed step. */
+int as_step_counters_host(as_env_t* env, int32_t* out_host, void* stream);
 int as_get_curriculum_host(as_env_t* env, int32_t* level_host); /* synchronises the stream */
 
 /* Diagnostic (SURVEY §8d "confirm with an in-repo STREAM-copy kernel"): dst[i] = src[i] for

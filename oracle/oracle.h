@@ -180,12 +180,14 @@ void or_task_reset_mask(const or_model_t* model, const or_task_t* task, or_state
 /* ---- physics ---- */
 void or_fk_bodies(const or_model_t* m, const float root_pos[3], const float root_quat[4], const float* q_cfg,
                   float body_pos[9]);
-void or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
-                     int env, const float* act_clamped);
+/* physics of env `env` (decimation substeps); returns the contacts the row budget cut over its substeps
+ * (contacts found - contacts kept: the kernel's as_step_counters word 3 summed over envs) */
+int or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
+                    int env, const float* act_clamped);
 /* the same with an actuator (act NULL = torque mode): AS_ACT_DC_MOTOR recomputes the joint torques from
  * the position targets default_q + action_scale a in every substep */
-void or_physics_step_act(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
-                         or_state_t* st, int env, const float* act_clamped);
+int or_physics_step_act(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
+                        or_state_t* st, int env, const float* act_clamped);
 void or_dc_motor_batch(int n, const float* qt, const float* q, const float* qd, const or_actuator_t* act, float* tau);
 /* ---- BASELINE C5 quadruped task (quad.c; the HIP k_quad kernel's restatement) ---- */
 void or_quad_post_physics(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
@@ -197,10 +199,11 @@ void or_link_point(const or_model_t* m, const or_state_t* st, int e, int link, c
 void or_quad_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
                   const or_quad_task_t* q, or_state_t* st, const float* actions, uint64_t seed, float* obs,
                   float* rew, uint8_t* term, uint8_t* trunc, int nthreads);
-/* full env step: physics (decimation substeps) + task logic; obs [n][59] */
+/* full env step: physics (decimation substeps) + task logic; obs [n][59]; *dropped (if non-null) = the
+ * contacts the row budget cut over all envs and substeps */
 void or_env_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
                  const float* actions, const float* reset_draws, uint64_t seed, float* obs, float* rew,
-                 uint8_t* term, uint8_t* trunc, int32_t* any_reset, int nthreads);
+                 uint8_t* term, uint8_t* trunc, int32_t* any_reset, int64_t* dropped, int nthreads);
 /* reset all envs (env.reset()): ep_len=0 + reset pose + tick #2 semantics + obs */
 void or_env_reset_all(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
                       const float* reset_draws, uint64_t seed, float* obs);

@@ -122,7 +122,9 @@ def lib() -> C.CDLL:
         L.or_task_reset_all.argtypes = [V, V, V, FP, C.c_uint64, FP]
         L.or_task_reset_mask.argtypes = [V, V, V, C.POINTER(C.c_uint8), FP, C.c_uint64, FP]
         L.or_env_step.argtypes = [V, V, V, V, FP, FP, C.c_uint64, FP, FP, C.POINTER(C.c_uint8),
-                                  C.POINTER(C.c_uint8), IP, C.c_int]
+                                  C.POINTER(C.c_uint8), IP, C.POINTER(C.c_int64), C.c_int]
+        L.or_physics_step.restype = C.c_int
+        L.or_physics_step_act.restype = C.c_int
         L.or_env_reset_all.argtypes = [V, V, V, V, FP, C.c_uint64, FP]
         L.or_math_batch.argtypes = [C.c_int, FP, FP, FP, FP, FP]
         L.or_sft_batch.argtypes = [C.c_int, FP, FP, FP, FP]
@@ -274,17 +276,23 @@ class Oracle:
         term = np.zeros(n, np.uint8)
         trunc = np.zeros(n, np.uint8)
         anyr = np.zeros(1, np.int32)
+        drop = C.c_int64(0)
         rd = fp(np.ascontiguousarray(reset_draws, np.float32)) if reset_draws is not None else None
         self.L.or_env_step(C.byref(self.model), C.byref(self.sim), C.byref(self.task), st.ptr, fp(actions), rd,
-                           seed, fp(obs), fp(rew), u8p(term), u8p(trunc), ip(anyr), nthreads)
+                           seed, fp(obs), fp(rew), u8p(term), u8p(trunc), ip(anyr), C.byref(drop), nthreads)
+        self.last_dropped = int(drop.value)  # contacts the row budget cut in this step (as_step_counters [3])
         return obs, rew, term.astype(bool), trunc.astype(bool), bool(anyr[0])
 
-    def physics_step(self, st: OracleState, actions: np.ndarray):
-        """Physics only (decimation substeps), no task logic: for known-answer tests."""
+    def physics_step(self, st: OracleState, actions: np.ndarray) -> int:
+        """Physics only (decimation substeps), no task logic: for known-answer tests.  Returns the
+        contacts the row budget cut over all envs and substeps."""
         a = np.clip(np.ascontiguousarray(actions, np.float32), -1, 1)
+        drop = 0
         for e in range(st.n):
             row = np.ascontiguousarray(a[e])
-            self.L.or_physics_step(C.byref(self.model), C.byref(self.sim), C.byref(self.task), st.ptr, e, fp(row))
+            drop += self.L.or_physics_step(C.byref(self.model), C.byref(self.sim), C.byref(self.task), st.ptr, e,
+                                           fp(row))
+        return drop
 
     def physics_step_act(self, st: OracleState, act: OrActuator, actions):
         """Physics only with an actuator (or_physics_step_act)."""

@@ -475,8 +475,8 @@ static void collide(const or_model_t* m, const or_sim_t* sim, const kin_t* K, co
 #ifdef OR_STATS
   ncap = OR_MAX_CONTACTS; /* find everything, keep ncap (below) */
 #endif
-  const int keep = ncap;          /* add_contact keeps ncap; the loops stop there unless probing */
-  if (g_probe) ncap = 1 << 30;
+  const int keep = ncap;          /* add_contact keeps ncap; the search runs to the end and counts the */
+  ncap = 1 << 30;                 /* contacts past the cap (tried - n: dropped, as_step_counters [3]) */
 
   const float* h = sim->stone_half;
   /* geom segments in the O frame, their midpoints / lengths, and the robot's bounding box */
@@ -618,7 +618,8 @@ static void tangents(const float n[3], float t1[3], float t2[3]) {
   cross(n, t1, t2);
 }
 
-static void substep(const or_model_t* m, const or_sim_t* sim, const or_actuator_t* act, const float* qt_int,
+/* returns the contacts the row budget cut in this substep (found - kept) */
+static int substep(const or_model_t* m, const or_sim_t* sim, const or_actuator_t* act, const float* qt_int,
                     float root_pos[3], float root_quat[4], float* q_int, float* u, float* tau_int,
                     const float* stones_w, int nst, uint32_t mask[4]) {
   if (act && act->mode == 1) /* the DC motor runs in every substep (as_dc_motor, include/as_detmath.h) */
@@ -674,6 +675,7 @@ static void substep(const or_model_t* m, const or_sim_t* sim, const or_actuator_
   if (Cn.n > ncap) Cn.n = ncap;
   or_stats_hist[2][Cn.n]++;
 #endif
+  const int dropped = Cn.tried - Cn.n;
   static __thread rows_t Rw;
   rows_t* R = &Rw;
   R->nrow = 0;
@@ -831,6 +833,7 @@ static void substep(const or_model_t* m, const or_sim_t* sim, const or_actuator_
   quat_to_mat(root_quat, Rn);
   matvec3(Rn, m->com[0], cl);
   for (int k = 0; k < 3; ++k) root_pos[k] = c0w[k] - cl[k];
+  return dropped;
 }
 
 void or_fk_bodies(const or_model_t* m, const float root_pos[3], const float root_quat[4], const float* q_cfg,
@@ -844,8 +847,8 @@ void or_fk_bodies(const or_model_t* m, const float root_pos[3], const float root
     for (int k = 0; k < 3; ++k) body_pos[3 * b + k] = root_pos[k] + K.p[ls[b]][k];
 }
 
-void or_physics_step_act(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
-                         or_state_t* st, int e, const float* act_clamped) {
+int or_physics_step_act(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, const or_actuator_t* act,
+                        or_state_t* st, int e, const float* act_clamped) {
   const int n = st->n, nh = m->num_hinges;
   float rp[3], rq[4], q_int[OR_MAX_LINKS], u[NV_MAX], tau[OR_MAX_LINKS], qt[OR_MAX_LINKS], stones[OR_MAX_STONES * 3];
   for (int k = 0; k < 3; ++k) rp[k] = F(st->root_pos, k, n, e);
@@ -865,7 +868,8 @@ void or_physics_step_act(const or_model_t* m, const or_sim_t* sim, const or_task
   for (int s = 0; s < nst; ++s)
     for (int k = 0; k < 3; ++k) stones[3 * s + k] = F(st->stones, s * 3 + k, n, e);
   uint32_t mask[4] = {0u, 0u, 0u, 0u};
-  for (int s = 0; s < sim->substeps; ++s) substep(m, sim, act, qt, rp, rq, q_int, u, tau, stones, nst, mask);
+  int dropped = 0;
+  for (int s = 0; s < sim->substeps; ++s) dropped += substep(m, sim, act, qt, rp, rq, q_int, u, tau, stones, nst, mask);
   for (int k = 0; k < 3; ++k) {
     F(st->root_pos, k, n, e) = rp[k];
     F(st->root_lin, k, n, e) = u[k];
@@ -887,6 +891,7 @@ void or_physics_step_act(const or_model_t* m, const or_sim_t* sim, const or_task
   for (int k = 0; k < nh; ++k) qc[k] = F(st->q, k, n, e);
   or_fk_bodies(m, rp, rq, qc, bp);
   for (int c = 0; c < 9; ++c) F(st->body_pos, c, n, e) = bp[c];
+  return dropped;
 }
 
 /* known-answer hook: the DC motor torque of include/as_detmath.h for n inputs */
@@ -896,9 +901,9 @@ void or_dc_motor_batch(int n, const float* qt, const float* q, const float* qd, 
                          act->velocity_limit);
 }
 
-void or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st, int e,
-                     const float* act_clamped) {
-  or_physics_step_act(m, sim, task, NULL, st, e, act_clamped);
+int or_physics_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st, int e,
+                    const float* act_clamped) {
+  return or_physics_step_act(m, sim, task, NULL, st, e, act_clamped);
 }
 
 /* ---------------------------------------------------------------- env-level API */
@@ -930,18 +935,20 @@ void or_probe_substep(const or_model_t* m, const or_sim_t* sim, const or_task_t*
 
 void or_env_step(const or_model_t* m, const or_sim_t* sim, const or_task_t* task, or_state_t* st,
                  const float* actions, const float* reset_draws, uint64_t seed, float* obs, float* rew,
-                 uint8_t* term, uint8_t* trunc, int32_t* any_reset, int nthreads) {
+                 uint8_t* term, uint8_t* trunc, int32_t* any_reset, int64_t* dropped, int nthreads) {
   const int n = st->n;
   (void)nthreads;
-#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
+  long long drop = 0;
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static) reduction(+ : drop)
   for (int e = 0; e < n; ++e) {
     float a[OR_MAX_LINKS];
     for (int k = 0; k < m->num_hinges; ++k) {
       float x = actions[(size_t)e * m->num_hinges + k];
       a[k] = x < -1.f ? -1.f : (x > 1.f ? 1.f : x);
     }
-    or_physics_step(m, sim, task, st, e, a);
+    drop += or_physics_step(m, sim, task, st, e, a);
   }
+  if (dropped) *dropped = drop;
   or_task_post_physics(m, task, st, actions, NULL, NULL, reset_draws, seed, NULL, NULL, obs, rew, term, trunc,
                        any_reset);
 }

@@ -11,3 +11,4 @@ timeout -k 10 300 python bench.py --no-train --no-c5 --no-cpu-baseline > gpurun_
 tail -1 gpurun_out/r05a_bench_k1000.log | cut -c1-600
 timeout -k 10 200 python scripts/transient.py 4096 1200 0 > gpurun_out/r05a_transient.log 2>&1 || { tail -5 gpurun_out/r05a_transient.log; exit 1; }
 cat gpurun_out/r05a_transient.log
+TAG=r05a bash scripts/price_exchange.sh || exit 1

@@ -30,15 +30,23 @@ def _rank_rollout(rank: int, H: int = 4, N: int = 6):
     }
 
 
+def _flat(t):
+    """swap_and_flatten01: [H, N, ...] -> env-major [N H, ...]"""
+    return t.transpose(0, 1).reshape((t.shape[0] * t.shape[1],) + tuple(t.shape[2:]))
+
+
 def _worker(rank: int, world: int, port: int, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         info = shard_info()
-        gather = RolloutGather()
+        gather = RolloutGather(env_axis=1)  # [H, N, ...] layout: parts concatenated along the env axis
+        flat_gather = RolloutGather()       # env-major flattened [N H, ...] (the trainer's): direct receive
         res = {}
         for it in range(2):  # second call reuses the cached receive buffers
             res = gather.gather(_rank_rollout(rank))
+            flat = flat_gather.gather({k: _flat(v) for k, v in _rank_rollout(rank).items()})
+        res.update({"flat/" + k: v for k, v in flat.items()})
         fake_env = types.SimpleNamespace(curr_target_index=torch.full((6,), 1 + 3 * rank, dtype=torch.int32))
         mean = global_curriculum_mean(fake_env)
         # numpy copies travel by value: torch tensors would be shared through /dev/shm files that vanish
@@ -60,6 +68,9 @@ def test_rollout_gather_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     expect = {k: torch.cat([_rank_rollout(r)[k] for r in range(world)], dim=1) for k in _rank_rollout(0)}
+    # env-major flattened: rank-major concatenation along axis 0 is the global env order
+    expect.update({"flat/" + k: torch.cat([_flat(_rank_rollout(r)[k]) for r in range(world)], dim=0)
+                   for k in _rank_rollout(0)})
     for rank, info_rank, info_world, res, mean in out:
         res = {k: torch.from_numpy(v) for k, v in res.items()}
         assert info_rank == rank and info_world == world

@@ -6,7 +6,9 @@
 * the pendulum and the resting / falling / wedged spheres of tests/test_oracle_kats.py (padded to 21
   hinges, tests/_models.py): the same known answers on the GPU, bit-identical to the oracle;
 * a clump of 14 crossing capsules (91 overlapping self pairs): more pairs pass the bounding-sphere
-  filter than the kernel's one-pass list holds, so its word-by-word path runs -- bit-identical too.
+  filter than the kernel's one-pass list holds, so its word-by-word path runs -- bit-identical too;
+* the contacts the constraint budget cuts (as_step_counters word 3, env.dropped_contacts()) equal the
+  oracle's count in every step of the "crowded" and "fallen" fixtures through the full env step.
 """
 
 import numpy as np
@@ -152,3 +154,45 @@ def test_self_pairs_past_the_list_capacity(oracle_mod):
         moved = max(moved, float(np.abs(g["qd"][:14]).max()))
     assert moved > 0.0  # the self-contacts (at most the budget's 10) push the links apart
     gpu.close()
+
+
+@pytest.mark.parametrize("name", ["crowded", "fallen"])
+def test_dropped_contacts_equal_oracle(orc, name):
+    """the device count of contacts cut by the 10-contact / 30-row budget (PhysX keeps every
+    one, simulation_cfg.py:110) equals the oracle's in every step, and the fixtures do cut some."""
+    import os
+
+    import torch
+
+    from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv
+    from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg
+
+    n, steps = 64, 5
+    cfg = AllstepsEnvCfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    cfg.seed = 42
+    env = AllstepsEnv(cfg)
+    env.reset()
+    torch.cuda.synchronize()
+    st = orc.state(n)
+    for k, v in env.get_state().items():
+        st[k][...] = v.cpu().numpy().reshape(st[k].shape).view(st[k].dtype)
+    snap = constraint_fixture(name)
+    for e in range(n):
+        put_oracle(st, snap, e)
+    env.set_state({k: st[k].view(np.int32) if st[k].dtype == np.uint32 else st[k] for k in env.get_state()})
+    rng = np.random.default_rng(3)
+    total = 0
+    for t in range(steps):
+        act = rng.uniform(-1, 1, (n, 21)).astype(np.float32)
+        act[0] = 0.0
+        env.step(torch.from_numpy(act).cuda())
+        orc.env_step(st, act, seed=42, nthreads=max(1, min(16, os.cpu_count() or 1)))
+        g = env.dropped_contacts()
+        print(f"[dropped {name}] step {t}: gpu {g} oracle {orc.last_dropped}")
+        assert g == orc.last_dropped, (t, g, orc.last_dropped)
+        total += g
+    _assert_same({k: v.cpu().numpy() for k, v in env.get_state().items()}, st, name)
+    assert total > 0
+    env.close()

@@ -93,7 +93,7 @@ def _run(orc, capsys, n, level, steps, warm, seed=42):
     st = orc.state(n)
     _to_oracle(env, st)
     rng = np.random.default_rng(1000 + n + level + warm)
-    resets = contacts = 0
+    resets = contacts = dropped = 0
     for t in range(steps):
         act = rng.uniform(-1.2, 1.2, (n, 21)).astype(np.float32)
         o_g, r_g, t_g, tr_g, _ = env.step(torch.from_numpy(act).cuda())
@@ -108,16 +108,21 @@ def _run(orc, capsys, n, level, steps, warm, seed=42):
         rg = r_g.cpu().numpy()
         bad["reward"] = np.flatnonzero(rg != r_c)
         nbad = len(set().union(*[set(v.tolist()) for v in bad.values()]))
+        # contacts cut by the constraint budget this step: the device counter == the oracle's count
+        d_g = env.dropped_contacts()
+        assert d_g == orc.last_dropped, (t, d_g, orc.last_dropped)
+        dropped += d_g
         resets += int((t_c | tr_c).sum())
         contacts += int((st["contact_mask"] != 0).any(0).sum())
         with capsys.disabled():
             print(f"[exact n={n} level={level} warm={warm}] step {t}: {nbad} of {n} envs mismatched "
-                  f"(resets {int((t_c | tr_c).sum())}, envs in contact {int((st['contact_mask'] != 0).any(0).sum())})")
+                  f"(resets {int((t_c | tr_c).sum())}, envs in contact {int((st['contact_mask'] != 0).any(0).sum())}, "
+                  f"contacts dropped {d_g} = oracle {orc.last_dropped})")
         assert nbad == 0, f"step {t}: {nbad} envs differ\n" + _describe(gs, st, n, bad) + "\n" + \
             "\n".join(f"  {k}: {len(v)} envs" for k, v in bad.items() if len(v) and k in ("terminated", "truncated",
                                                                                           "obs", "reward"))
     env.close()
-    return resets, contacts
+    return resets, contacts, dropped
 
 
 @pytest.mark.parametrize("n,level,steps,warm", [
@@ -129,8 +134,10 @@ def _run(orc, capsys, n, level, steps, warm, seed=42):
     (1024, 0, 400, 0),      # long horizon: 400 consecutive steps, every env through falls and resets
 ])
 def test_trajectory_bit_exact(orc, capsys, n, level, steps, warm):
-    resets, contacts = _run(orc, capsys, n, level, steps, warm)
+    resets, contacts, dropped = _run(orc, capsys, n, level, steps, warm)
     if n >= 4096:
         assert contacts > 0, "no env ever touched a stone: the trajectory did not exercise the contact path"
+    if n == 32768 and warm:
+        assert dropped > 0, "the C3 warm trajectory never hit the constraint budget: the drop count is untested"
     if warm:
         assert resets > 0, "no env reset during the compared steps"

@@ -594,11 +594,11 @@ def test_rollout_bookkeeping_kernel_matches_reference_ops(tmp_path):
             assert float(mm.current_size) == float(m.current_size)
 
 
-def _dist_train_worker(rank, port, mode, tmp, q):
+def _dist_train_worker(rank, port, mode, tmp, q, num_envs=1024, iters=3):
     import socket  # noqa: F401
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
-                      LOCAL_RANK="0", ALLSTEPS_DIST_BACKEND="gloo")
+                      LOCAL_RANK="0", ALLSTEPS_DIST_BACKEND="gloo", ALLSTEPS_DIST_TIMEOUT_S="900")
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "scripts", "reinforcement_learning", "rl_games"))
     import torch.distributed as dist
@@ -606,23 +606,19 @@ def _dist_train_worker(rank, port, mode, tmp, q):
     import train
 
     try:
-        runner, _ = train.main(["--task", "Allsteps-v0", "--num_envs", "1024", "--max_iterations", "3", "--seed", "7",
-                                "--distributed", "--multi_gpu_mode", mode, "--log_root", f"{tmp}/r{rank}"])
+        runner, _ = train.main(["--task", "Allsteps-v0", "--num_envs", str(num_envs), "--max_iterations", str(iters),
+                                "--seed", "7", "--distributed", "--multi_gpu_mode", mode, "--log_root", f"{tmp}/r{rank}"])
         ag = runner.agent
         # a numpy copy (pickled by value), not a shared-memory tensor whose descriptor dies with this process
         q.put((rank, ag.flat.params.detach().cpu().numpy().copy(), float(ag.lr), ag.frame, ag.dataset.minibatch_size,
-               int(ag._uw.env_id_offset), bool(ag.fused is not None and ag._play_graphs is not None)))
+               int(ag._uw.env_id_offset), bool(ag.fused is not None and ag._play_graphs is not None),
+               ag.dataset.batch_size, (ag.horizon_length, ag.minibatch_size, ag.mini_epochs_num)))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["allreduce", "allgather"])
-def test_distributed_fused_trainer_two_ranks_one_gpu(tmp_path, mode):
-    """The --distributed train.py path with the fused HIP-graph update and rollout graphs, two ranks
-    (gloo, both on cuda:0): the gradient / rollout exchange keeps the ranks' parameters identical,
-    env shards are offset, frames count both ranks."""
+def _two_ranks(tmp_path, mode, num_envs=1024, iters=3, timeout=200):
     import socket
 
     import torch.multiprocessing as mp
@@ -632,19 +628,51 @@ def test_distributed_fused_trainer_two_ranks_one_gpu(tmp_path, mode):
         port = so.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_train_worker, args=(r, port, mode, str(tmp_path), q)) for r in range(2)]
+    procs = [ctx.Process(target=_dist_train_worker, args=(r, port, mode, str(tmp_path), q, num_envs, iters))
+             for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=200) for _ in procs], key=lambda r: r[0])
+    res = sorted([q.get(timeout=timeout) for _ in procs], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, p0, lr0, f0, mb0, off0, fused0), (_, p1, lr1, f1, mb1, off1, _) = res
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["allreduce", "allgather"])
+def test_distributed_fused_trainer_two_ranks_one_gpu(tmp_path, mode):
+    """The --distributed train.py path with the fused HIP-graph update and rollout graphs, two ranks
+    (gloo, both on cuda:0): the gradient / rollout exchange keeps the ranks' parameters identical,
+    env shards are offset, frames count both ranks."""
+    res = _two_ranks(tmp_path, mode)
+    (_, p0, lr0, f0, mb0, off0, fused0, _, _), (_, p1, lr1, f1, mb1, off1, _, _, _) = res
     assert fused0, "the fused update / rollout graphs must be the path under test"
     assert np.array_equal(p0, p1), f"{mode}: ranks diverged"
     assert lr0 == lr1 and f0 == f1 == 3 * 2 * 1024 * 32
     assert (off0, off1) == (0, 1024)
     assert mb0 == (2 * 32768 if mode == "allgather" else 32768)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_c4_per_rank_workload_two_ranks_allgather(tmp_path):
+    """BASELINE C4's per-rank workload -- 32768 envs per rank, the reference agent config (horizon 32,
+    minibatch 32768, 10 mini-epochs: rl_games_ppo_cfg.yaml:48,69-71) -- through train.py --distributed in
+    the north star's allgather mode, two ranks on cuda:0 over gloo, 2 epochs: the ranks stay
+    bit-identical, each rank's update runs on the gathered 2 x per-rank batch with a 2 x minibatch, the
+    env shards are offset by 32768 and the frame count covers both ranks."""
+    n = 32768
+    res = _two_ranks(tmp_path, "allgather", num_envs=n, iters=2, timeout=800)
+    (_, p0, lr0, f0, mb0, off0, fused0, bs0, cfg0), (_, p1, lr1, f1, mb1, off1, _, bs1, _) = res
+    assert cfg0 == (32, 32768, 10), cfg0  # the reference agent config, unmodified
+    assert fused0
+    assert np.array_equal(p0, p1), "C4 allgather: ranks diverged"
+    assert lr0 == lr1
+    assert bs0 == bs1 == 2 * 32 * n  # the gathered batch: both ranks' rollouts
+    assert mb0 == mb1 == 2 * 32768
+    assert (off0, off1) == (0, n)
+    assert f0 == f1 == 2 * 2 * n * 32  # epochs x ranks x envs x horizon
 
 
 @pytest.mark.gpu

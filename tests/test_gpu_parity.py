@@ -487,3 +487,4 @@ def test_bench_single_gpu_driver_shape():
     assert km["events_consistent"], km
     assert line["roofline"]["duration_ms"] == km["k_step_ms"]
     assert "error" not in (line["roofline"]["latency"] or {})
+    assert line["contacts_dropped"]["total"] >= 0

@@ -118,3 +118,23 @@ def test_fixture_states_are_valid(orc, name):
     snap = constraint_fixture(name)
     assert abs(np.linalg.norm(snap["root_quat"]) - 1.0) < 1e-5
     assert np.isfinite(np.concatenate([v.astype(np.float64).ravel() for v in snap.values()])).all()
+
+
+@pytest.mark.parametrize("name", ["fallen", "crowded"])
+def test_dropped_contacts_counted(orc, name):
+    """The oracle searches every pair past the cap and counts what it cuts (as_step_counters word 3 on
+    the device): at least the first substep's found - kept, and the physics-only and full env steps
+    agree on it; cutting does not change which contacts are kept (the probe's list is the same)."""
+    st = _state(orc, name)
+    p = orc.probe(st)
+    first = p["nfound"] - p["ncontact"]
+    assert first > 0
+    st2 = _state(orc, name)
+    act = np.zeros((1, 21), np.float32)
+    drop = orc.physics_step(st2, act)
+    assert drop >= first
+    st3 = _state(orc, name)
+    st3["idx"][:] = 1
+    st3["next"][:] = 2
+    orc.env_step(st3, act)
+    assert orc.last_dropped == drop
