@@ -66,8 +66,10 @@ def parse():
                    help="oracle OpenMP threads (default: OMP_NUM_THREADS, else nproc; BASELINE.md §3)")
     p.add_argument("--no-train", action="store_true", help="skip the env+PPO trainer measurement")
     p.add_argument("--train-envs", type=int, default=32768)
-    p.add_argument("--multi-gpu-mode", dest="multi_gpu_mode", choices=("allgather", "allreduce"), default="allgather",
-                   help="N > 1 train leg: RCCL all-gather of rollouts (north star, default) or gradient all-reduce")
+    p.add_argument("--multi-gpu-mode", dest="multi_gpu_mode", choices=("allgather", "allreduce"), default="allreduce",
+                   help="N > 1 train leg: RCCL gradient all-reduce per minibatch (rl_games --distributed, default: "
+                        "it scales, DESIGN.md §6) or the north star's all-gather of rollouts (every rank then "
+                        "runs the whole update on W x the data)")
     p.add_argument("--no-c5", action="store_true", help="skip the quadruped (BASELINE C5) task measurement")
     return p.parse_args()
 
@@ -206,9 +208,10 @@ def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int
 
 def train_leg(args, world: int, rank: int, backend: str, device, timeout_s: float = 300.0) -> dict:
     """env + PPO (BASELINE C4) in a child process per rank (scripts/bench_train.py; at N ranks its own
-    process group on a fresh port, the trainer's --distributed path with --multi_gpu_mode allgather:
-    one RCCL all-gather of the rollout tensors per epoch, identical replicated updates -- the north
-    star's exchange; --multi-gpu-mode allreduce selects rl_games' gradient all-reduce instead).  A child that fails or stalls is killed after `timeout_s` and reported
+    process group on a fresh port, the trainer's --distributed path with --multi_gpu_mode allreduce:
+    one RCCL all-reduce of the [grads | kl] bucket per minibatch, rl_games' own multi_gpu exchange and
+    the one that scales -- DESIGN.md §6 prices it against the north star's all-gather of rollouts,
+    which replicates the whole update on every rank; --multi-gpu-mode allgather selects that).  A child that fails or stalls is killed after `timeout_s` and reported
     as an error: the env metric on the line never waits on the trainer's collectives."""
     import signal
     import socket

@@ -422,7 +422,8 @@ def test_bench_two_ranks_one_gpu():
     env = dict(os.environ, ALLSTEPS_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20",
-           "--warmup", "3", "--num-envs", "256", "--no-cpu-baseline", "--no-c5", "--train-envs", "1024"]
+           "--warmup", "3", "--num-envs", "256", "--no-cpu-baseline", "--no-c5", "--train-envs", "1024",
+           "--multi-gpu-mode", "allgather"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
@@ -434,7 +435,7 @@ def test_bench_two_ranks_one_gpu():
     tr = line["train"]
     assert "error" not in tr, (tr, r.stderr[-2000:])
     assert tr["n_gpus"] == 2 and tr["global_envs"] == 2048 and tr["value"] > 0
-    assert tr["multi_gpu_mode"] == "allgather"  # north star: RCCL all-gather of rollouts at the PPO boundary
+    assert tr["multi_gpu_mode"] == "allgather"  # the north star's exchange, selected explicitly
 
 
 def test_bench_gpus_flag_launches_ranks_itself():
@@ -459,7 +460,7 @@ def test_bench_gpus_flag_launches_ranks_itself():
     assert line["n_gpus"] == 2 and line["config"]["global_envs"] == 2 * line["config"]["num_envs_per_gpu"] == 512
     tr = line["train"]
     assert "error" not in tr, (tr, r.stderr[-2000:])
-    assert tr["n_gpus"] == 2 and tr["multi_gpu_mode"] == "allgather"
+    assert tr["n_gpus"] == 2 and tr["multi_gpu_mode"] == "allreduce"  # bench default
     # the kernel timings come from a bit-exact replay of each rank's timed window, >= 200 launches
     km = line["kernels_ms"]
     assert km["replay_exact"] and km["sampled_launches"] >= 200
