@@ -1,0 +1,98 @@
+"""A/B of the fused trunk kernels between two builds of libppo_hip.so: the same random
+16-bit inputs through ppo_mlp_forward (and ppo_mlp_backward) of library A and library B; prints the
+largest differences of every output and each library's HIP-event time per launch.
+
+    python scripts/mlp_ab.py LIB_A LIB_B [rows] [dtype: f16 | bf16]
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from allsteps_isaaclab_amd.learning import fused as FU  # noqa: E402
+
+
+def open_lib(path):
+    L = C.CDLL(path)
+    L.ppo_mlp_forward.argtypes = [C.POINTER(FU.PpoMlpFwd), C.c_void_p]
+    L.ppo_mlp_backward.argtypes = [C.POINTER(FU.PpoMlpBwd), C.c_void_p]
+    return L
+
+
+def timed(fn, n=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return round(e0.elapsed_time(e1) / n * 1000, 2)
+
+
+def main():
+    la, lb = sys.argv[1], sys.argv[2]
+    rows = int(sys.argv[3]) if len(sys.argv) > 3 else 32768
+    dt = torch.float16 if (sys.argv[4] if len(sys.argv) > 4 else "f16") == "f16" else torch.bfloat16
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.zeros(rows, 72, device=dev)
+    x[:, :59] = torch.randn(rows, 59, device=dev, generator=g).clamp(-5, 5)
+    x = x.to(dt)
+    ws = [(torch.randn(256, 64 if i == 0 else 256, device=dev, generator=g) / (8 if i == 0 else 16)).to(dt)
+          for i in range(5)]
+    ws[0][:, 59:] = 0
+    wts = [w.t().contiguous() for w in ws[1:]]
+    bs = [torch.randn(256, device=dev, generator=g) * 0.1 for _ in range(5)]
+    wh = torch.randn(22, 256, device=dev, generator=g) / 16
+    bh = torch.randn(22, device=dev, generator=g) * 0.1
+    dhead = torch.randn(rows, 22, device=dev, generator=g) * 0.01
+    out = {}
+    for tag, path in (("A", la), ("B", lb)):
+        L = open_lib(path)
+        hs = [torch.zeros(rows, 264, device=dev, dtype=dt) for _ in range(4)]
+        h5 = torch.zeros(rows, 256, device=dev)
+        head = torch.zeros(rows, 22, device=dev)
+        dzs = [torch.zeros(rows, 256, device=dev, dtype=dt) for _ in range(5)]
+        a = FU.PpoMlpFwd()
+        a.x = x.data_ptr()
+        for i in range(5):
+            a.w[i], a.b[i] = ws[i].data_ptr(), bs[i].data_ptr()
+        for i in range(4):
+            a.h[i] = hs[i].data_ptr()
+        a.wh, a.bh, a.h5, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), h5.data_ptr(), head.data_ptr(), rows, 22
+        a.x_stride, a.h_stride, a.dtype = 72, 264, FU.PPO_DT[dt]
+        b = FU.PpoMlpBwd()
+        b.dhead, b.wh, b.nh, b.rows, b.h_stride, b.dtype = dhead.data_ptr(), wh.data_ptr(), 22, rows, 264, FU.PPO_DT[dt]
+        for k in range(4):
+            b.wt[k], b.h[k] = wts[k].data_ptr(), hs[k].data_ptr()
+        for k in range(5):
+            b.dz[k] = dzs[k].data_ptr()
+        b.h5 = h5.data_ptr()
+        s = torch.cuda.current_stream().cuda_stream
+        fwd = lambda: L.ppo_mlp_forward(C.byref(a), s)  # noqa: E731
+        bwd = lambda: L.ppo_mlp_backward(C.byref(b), s)  # noqa: E731
+        assert fwd() == 0 and bwd() == 0
+        torch.cuda.synchronize()
+        out[tag] = {"h": [t[:, :256].float().clone() for t in hs], "h5": h5.clone(), "head": head.clone(),
+                    "dz": [t.float().clone() for t in dzs], "fwd_us": timed(fwd), "bwd_us": timed(bwd)}
+    A, B = out["A"], out["B"]
+    rep = {"rows": rows, "dtype": str(dt), "fwd_us": [A["fwd_us"], B["fwd_us"]], "bwd_us": [A["bwd_us"], B["bwd_us"]]}
+    for k in ("h", "dz"):
+        rep[k + "_maxdiff"] = [round(float((p - q).abs().max()), 6) for p, q in zip(A[k], B[k])]
+        rep[k + "_frac_diff"] = [round(float(((p - q).abs() > 0).float().mean()), 6) for p, q in zip(A[k], B[k])]
+    rep["h5_maxdiff"] = float((A["h5"] - B["h5"]).abs().max())
+    rep["head_maxdiff"] = float((A["head"] - B["head"]).abs().max())
+    print(json.dumps(rep), flush=True)
+
+
+if __name__ == "__main__":
+    main()
