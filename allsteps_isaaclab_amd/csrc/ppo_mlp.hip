@@ -20,10 +20,6 @@ namespace ppo_detail {
 void set_error(const char* msg);
 }
 
-#ifndef PPO_MLP_DBG
-#define PPO_MLP_DBG 0
-#endif
-
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -55,7 +51,6 @@ constexpr int kWaves = 4;
 constexpr int kRowsPerBlock = 32 * kWaves;
 constexpr int kPad = 8;              // bf16 elements of padding per LDS row (16 B)
 constexpr int kWBytes = kHid * (kHid + kPad) * 2;  // 135168 B: one 256 x 256 layer
-constexpr int kLdsBytes = kWBytes + 5 * kHid * 4;   // + the five bias vectors (fp32)
 
 char g_err[256];  // formatted here, published through ppo_last_error() (ppo_kernels.hip)
 
@@ -150,139 +145,309 @@ __device__ __forceinline__ uint4 pair_chunks(uint2 ga, uint2 gb) {
 // feature of register r of a tile for lane half h
 __device__ __forceinline__ int feat(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// ------------------------------------------------------------------------------ forward (weight-stationary)
+//
+// One workgroup of 8 waves per CU (two waves per SIMD) owns 128 batch rows (4 N-tiles of 32).  Wave w
+// owns output features [32w, 32w + 32) of every layer and keeps ITS slice of the layer's weights in
+// registers (the A fragments: 32 features x K, 16 B per lane per k-step), loaded straight from L2 while
+// the previous layer's epilogue runs -- no weight staging through LDS.  The activations live in LDS
+// (two [128][264] buffers, the B fragments: one ds_read_b128 per MFMA, 1 KB per 32-cycle MFMA per SIMD,
+// half the LDS array's rate): layer l reads one buffer, its epilogue (bias + ELU in fp32, one rounding
+// to the trunk's type) writes the other, one barrier per layer.  The two waves of a SIMD interleave one
+// wave's epilogue with the other's MFMAs.  The heads (mu | value, nh <= 32 outputs) run on the 16-bit
+// layer-5 activations with fp16 / bf16 weights and fp32 accumulation, as rl_games' autocast does
+// (Linear under autocast: 16-bit inputs, fp32 accumulate, 16-bit output + bias), on waves 0..3 (one
+// N-tile each).  The hidden layers are the previous (register-chained) form's arithmetic: the same
+// ascending 16-wide k-steps accumulated in fp32 and the same epilogue; only the position of each
+// product inside an MFMA's 16-element step differs (natural k order instead of the permuted one).
+constexpr int kFWaves = 8;
+constexpr int kFThreads = 64 * kFWaves;
+constexpr int kFRows = 128;               // batch rows per workgroup (4 N-tiles of 32)
+constexpr int kXs = kHid + kPad;          // LDS activation row stride, elements (132 dwords: conflict-free b128)
+constexpr int kXBytes = kFRows * kXs * 2; // 67584 B per activation buffer
+constexpr int kFLds = 2 * kXBytes;        // 135168 B
+
+// A fragments of k-steps [0, NS) for features F0 + i: row F0 + i of a [256][K] 16-bit matrix, k 16s + 8h..+7
+template <int DT, int NS>
+__device__ __forceinline__ void load_wa(const uint16_t* __restrict__ w, int K, int F0, int i, int h,
+                                        typename Lp<DT>::v8 (&wa)[16]) {
+    typedef typename Lp<DT>::v8 V8;
+    const uint16_t* p = w + int64_t(F0 + i) * K + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) wa[s] = *reinterpret_cast<const V8*>(p + 16 * s);
+}
+
+// the heads' A fragments: fp32 wh[o][256] (o < nh, zero rows above) rounded to the trunk's type
 template <int DT>
-__global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
+__device__ __forceinline__ void load_wh(const float* __restrict__ wh, int nh, int i, int h, typename Lp<DT>::v8 (&wa)[16]) {
+    typedef typename Lp<DT>::e E;
+    const bool ok = i < nh;
+    const float* p = wh + (ok ? i : 0) * kHid + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const float4 u = ok ? *reinterpret_cast<const float4*>(p + 16 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 v = ok ? *reinterpret_cast<const float4*>(p + 16 * s + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        wa[s][0] = (E)u.x; wa[s][1] = (E)u.y; wa[s][2] = (E)u.z; wa[s][3] = (E)u.w;
+        wa[s][4] = (E)v.x; wa[s][5] = (E)v.y; wa[s][6] = (E)v.z; wa[s][7] = (E)v.w;
+    }
+}
+
+// bias of features F0 + feat(r, h) (16 per lane)
+__device__ __forceinline__ void load_bias(const float* __restrict__ b, int F0, int h, float (&bv)[16]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const float4 q = *reinterpret_cast<const float4*>(b + F0 + 8 * g + 4 * h);
+        bv[4 * g] = q.x; bv[4 * g + 1] = q.y; bv[4 * g + 2] = q.z; bv[4 * g + 3] = q.w;
+    }
+}
+
+// acc[t] = W_slice (32 x 16 NS) . X[rows 32 (T0 + t) + 0..31] for t < NT; B fragments read from the LDS
+// activation image one k-step ahead of their MFMAs
+template <int DT, int NS, int NT>
+__device__ __forceinline__ void mma_rows(const uint16_t* X, const typename Lp<DT>::v8 (&wa)[16], f32x16 (&acc)[4],
+                                         int T0, int j, int h) {
+    typedef typename Lp<DT>::v8 V8;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+    V8 bf[2][NT];
+    const uint16_t* xr = X + (32 * T0 + j) * kXs + 8 * h;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) bf[0][t] = *reinterpret_cast<const V8*>(xr + 32 * t * kXs);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (s + 1 < NS) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) bf[(s + 1) & 1][t] = *reinterpret_cast<const V8*>(xr + 32 * t * kXs + 16 * (s + 1));
+        }
+        __builtin_amdgcn_sched_barrier(0);  // the next k-step's reads stay ahead of this k-step's MFMAs
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = Lp<DT>::mma(wa[s], bf[s & 1][t], acc[t]);
+    }
+}
+
+#ifndef PPO_FWD_DBG
+#define PPO_FWD_DBG 0  // timing-only builds (scripts/fwd_dbg.sh): 2 no exp, 4 no stores, 16 no MFMA, 32 no ELU / convert
+#endif
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+// a range-checked buffer over `bytes` bytes from p (uniform kernel-argument inputs): stores past the
+// end are dropped by the hardware, so the partial last workgroup needs no per-row branch (a branch
+// would split the block the scheduler interleaves)
+__device__ __forceinline__ Rsrc rsrc(const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes),
+                                             0x00020000);
+}
+
+__device__ __forceinline__ u32x4_t u4(uint4 v) { return u32x4_t{v.x, v.y, v.z, v.w}; }
+
+// ELU (alpha 1) of one tile's fp32 values (bias already in the accumulator), one rounding to the 16-bit
+// type: the next layer's LDS image and, when STORE, the layer's global activations (and, LAST, the
+// fp32 values: h5).  Lane (j, h) holds row j, features F0 + feat(r, h).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// two fp32 values -> one dword of two 16-bit values (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32, round to
+// nearest even)
+template <int DT>
+__device__ __forceinline__ uint32_t pack2(f32x2_t v) {
+    typedef typename Lp<DT>::e E;
+    typedef E e2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, e2));
+}
+
+template <int DT, bool LAST, bool STORE>
+__device__ __forceinline__ void tile_epi(const f32x16& acc, uint16_t* Xn, int rl, int row, Rsrc rh, int h_stride, Rsrc r5,
+                                         int F0, int h) {
+    // ELU in pairs: one packed multiply by log2(e) and one packed add of -1 per two values around the two
+    // hardware exps (exp(z) - 1 = exp2(z log2 e) - 1, as __expf; |error| ~1e-7, far below the 16-bit step)
+    float y[16];
+    uint32_t dw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const f32x2_t z = {acc[2 * k], acc[2 * k + 1]};
+        const f32x2_t zl = z * f32x2_t{1.44269502f, 1.44269502f};
+        const f32x2_t em = f32x2_t{__builtin_amdgcn_exp2f(zl.x), __builtin_amdgcn_exp2f(zl.y)} - f32x2_t{1.f, 1.f};
+        y[2 * k] = z.x > 0.f ? z.x : em.x;
+        y[2 * k + 1] = z.y > 0.f ? z.y : em.y;
+        dw[k] = pack2<DT>(f32x2_t{y[2 * k], y[2 * k + 1]});
+    }
+#if PPO_FWD_DBG & 2
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dw[k] = pack2<DT>(f32x2_t{acc[2 * k], acc[2 * k + 1]});
+#endif
+#if PPO_FWD_DBG & 32
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dw[k] = __builtin_bit_cast(uint32_t, acc[2 * k]) ^ __builtin_bit_cast(uint32_t, acc[2 * k + 1]);
+#endif
+    // dwords 2g, 2g + 1 = features 8g + 4h + 0..3 (register r = 4g + e)
+    const uint4 c01 = pair_chunks(make_uint2(dw[0], dw[1]), make_uint2(dw[2], dw[3]));
+    const uint4 c23 = pair_chunks(make_uint2(dw[4], dw[5]), make_uint2(dw[6], dw[7]));
+    uint16_t* xn = Xn + rl * kXs + F0 + 8 * h;
+    *reinterpret_cast<uint4*>(xn) = c01;
+    *reinterpret_cast<uint4*>(xn + 16) = c23;
+    if (STORE) {
+        if (!LAST) {  // layers 1..4 (16-bit); the fifth layer's values go out in fp32 only (h5)
+            const int off = (row * h_stride + F0 + 8 * h) * 2;
+            __builtin_amdgcn_raw_buffer_store_b128(u4(c01), rh, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(u4(c23), rh, off + 32, 0, 0);
+        } else {
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4_t{__float_as_uint(y[4 * g]), __float_as_uint(y[4 * g + 1]), __float_as_uint(y[4 * g + 2]),
+                            __float_as_uint(y[4 * g + 3])},
+                    r5, (row * kHid + F0 + 8 * g + 4 * h) * 4, 0, 0);
+        }
+    }
+}
+
+// The MFMAs of one N-tile (32 rows) for the wave's 32 features: NS k-steps accumulated onto `c` (the
+// bias), B fragments PD k-steps ahead of their MFMA (an LDS read's latency is ~4 MFMA issue slots);
+// the reads and MFMAs keep their order (sched_barrier), the VALU, LDS writes and stores of an epilogue
+// placed beside them in the source may move across (mask: ALU | VALU | SALU | VMEM write | DS write).
+template <int DT, int NS>
+__device__ __forceinline__ f32x16 mfma_tile(const uint16_t* X, const typename Lp<DT>::v8 (&wa)[16], f32x16 c, int t,
+                                            int j, int h) {
+    typedef typename Lp<DT>::v8 V8;
+    constexpr int PD = NS < 4 ? NS : 4;
+    constexpr int kFloat = 0x1 | 0x2 | 0x4 | 0x40 | 0x200;
+    const uint16_t* xr = X + (32 * t + j) * kXs + 8 * h;
+    V8 b[NS];
+#pragma unroll
+    for (int s = 0; s < PD; ++s) b[s] = *reinterpret_cast<const V8*>(xr + 16 * s);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (s + PD < NS) b[s + PD] = *reinterpret_cast<const V8*>(xr + 16 * (s + PD));
+        __builtin_amdgcn_sched_barrier(kFloat);
+#if PPO_FWD_DBG & 16
+        c[s & 15] += __builtin_bit_cast(float, uint32_t(b[s][0] != b[s][1]));
+#else
+        c = Lp<DT>::mma(wa[s], b[s], c);
+#endif
+        __builtin_amdgcn_sched_barrier(kFloat);
+    }
+    return c;
+}
+
+// One layer of the wave's 32 output features over the workgroup's 4 N-tiles, software-pipelined by
+// tile so that every phase carries matrix work AND epilogue work (exp / convert / stores): phase 0 runs
+// this layer's tile-0 MFMAs beside the PREVIOUS layer's tile-3 epilogue (`pend`, written into rows
+// 96..127 of this layer's input), phase t (1..3) tile t's MFMAs beside tile t - 1's epilogue; tile 3's
+// accumulator is handed on to the next layer (or the last layer's own tail).  Two barriers per layer:
+// before phase 3 (rows 96..127 of the input, which phase 0 completed, are read there) and at the end
+// (rows 0..95 of the output complete; every read of the input done before the layer after the next
+// overwrites it).
+template <int DT, int NS, bool STORE, bool HAS_PREV>
+__device__ __forceinline__ void layer(const uint16_t* Xin, uint16_t* Xout, const typename Lp<DT>::v8 (&wa)[16],
+                                      const float (&bv)[16], f32x16& pend, Rsrc rh_prev, Rsrc rh, int h_stride, int row0,
+                                      int F0, int j, int h) {
+    f32x16 binit;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) binit[r] = bv[r];
+    const f32x16 c0 = mfma_tile<DT, NS>(Xin, wa, binit, 0, j, h);
+    if (HAS_PREV)
+        tile_epi<DT, false, STORE>(pend, const_cast<uint16_t*>(Xin), 96 + j, row0 + 96 + j, rh_prev, h_stride, rh, F0, h);
+    const f32x16 c1 = mfma_tile<DT, NS>(Xin, wa, binit, 1, j, h);
+    tile_epi<DT, false, STORE>(c0, Xout, j, row0 + j, rh, h_stride, rh, F0, h);
+    const f32x16 c2 = mfma_tile<DT, NS>(Xin, wa, binit, 2, j, h);
+    tile_epi<DT, false, STORE>(c1, Xout, 32 + j, row0 + 32 + j, rh, h_stride, rh, F0, h);
+    __syncthreads();
+    const f32x16 c3 = mfma_tile<DT, NS>(Xin, wa, binit, 3, j, h);
+    tile_epi<DT, false, STORE>(c2, Xout, 64 + j, row0 + 64 + j, rh, h_stride, rh, F0, h);
+    pend = c3;
+    __syncthreads();
+}
+
+template <int DT, bool STORE>
+__device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     typedef typename Lp<DT>::e E;
     typedef typename Lp<DT>::v8 V8;
     extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    uint16_t* X0 = lds;
+    uint16_t* X1 = lds + kFRows * kXs;
     const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
-    const int j = lane & 31, h = lane >> 5;
-    const int row = blockIdx.x * kRowsPerBlock + wave * 32 + j;  // this lane's batch row
-    const bool live = row < a.rows;
-    float* lbias = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + kWBytes);
-    {  // the five bias vectors: one independent load per layer per thread (blockDim == kHid)
-        float bl[5];
+    const int j = lane & 31, h = lane >> 5, i = lane & 31;
+    const int F0 = 32 * wave;                 // this wave's output features
+    const int row0 = blockIdx.x * kFRows;
+    const int rows = a.rows;
+    // layer-0 input rows -> X0 (16-B chunks, zero past `rows`)
 #pragma unroll
-        for (int l = 0; l < 5; ++l) bl[l] = a.b[l][threadIdx.x];
-#pragma unroll
-        for (int l = 0; l < 5; ++l) lbias[l * kHid + threadIdx.x] = bl[l];
+    for (int u = 0; u < kFRows * (kK0 / 8) / kFThreads; ++u) {
+        const int c = u * kFThreads + threadIdx.x, r = c / (kK0 / 8), q = c % (kK0 / 8);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (row0 + r < rows) v = *reinterpret_cast<const uint4*>(a.x + int64_t(row0 + r) * a.x_stride + 8 * q);
+        *reinterpret_cast<uint4*>(X0 + r * kXs + 8 * q) = v;
     }
-
-    // layer-0 input fragments (k order permuted as for a chained accumulator)
-    V8 xb[kTiles][2];
+    const int hs = a.h_stride;
+    Rsrc rh[4], r5;
 #pragma unroll
-    for (int kt = 0; kt < kTiles; ++kt) {
+    for (int l = 0; l < 4; ++l) rh[l] = rsrc(STORE ? a.h[l] : nullptr, STORE ? int64_t(rows) * hs * 2 : 0);
+    r5 = rsrc(STORE ? a.h5 : nullptr, STORE ? int64_t(rows) * kHid * 4 : 0);
+    // Weight slices double-buffered in registers (wa / wb): layer l + 1's slice is requested at the start
+    // of layer l, ahead of layer l's activation stores (a load waited for with vmcnt also waits for every
+    // older store of the wave).  Bias vectors likewise one layer ahead.
+    V8 wa[16], wb[16];
+    float ba[16], bb[16];
+    f32x16 pend = {};
+    load_wa<DT, kK0 / 16>(a.w[0], kK0, F0, i, h, wa);
+    load_bias(a.b[0], F0, h, ba);
+    __syncthreads();
+    load_wa<DT, 16>(a.w[1], kHid, F0, i, h, wb);
+    load_bias(a.b[1], F0, h, bb);
+    layer<DT, kK0 / 16, STORE, false>(X0, X1, wa, ba, pend, rh[0], rh[0], hs, row0, F0, j, h);
+    load_wa<DT, 16>(a.w[2], kHid, F0, i, h, wa);
+    load_bias(a.b[2], F0, h, ba);
+    layer<DT, 16, STORE, true>(X1, X0, wb, bb, pend, rh[0], rh[1], hs, row0, F0, j, h);
+    load_wa<DT, 16>(a.w[3], kHid, F0, i, h, wb);
+    load_bias(a.b[3], F0, h, bb);
+    layer<DT, 16, STORE, true>(X0, X1, wa, ba, pend, rh[1], rh[2], hs, row0, F0, j, h);
+    load_wa<DT, 16>(a.w[4], kHid, F0, i, h, wa);
+    load_bias(a.b[4], F0, h, ba);
+    layer<DT, 16, STORE, true>(X1, X0, wb, bb, pend, rh[2], rh[3], hs, row0, F0, j, h);
+    // the fifth layer: fp32 values too (h5); the heads' weights and biases fly under it
+    if (wave < 4) load_wh<DT>(a.wh, a.nh, i, h, wb);
+    float bhv[16];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            Frag<DT> f;
-            f.q[0] = make_uint2(0, 0);
-            f.q[1] = make_uint2(0, 0);
-            if (kt < kK0 / 32 && live) {
-                const uint16_t* p = a.x + int64_t(row) * a.x_stride + kt * 32 + 16 * s + 4 * h;
-                f.q[0] = *reinterpret_cast<const uint2*>(p);
-                f.q[1] = *reinterpret_cast<const uint2*>(p + 8);
-            }
-            xb[kt][s] = f.v;
-        }
-    }
-    f32x16 acc[kTiles];
-    for (int l = 0; l < 5; ++l) {
-        __syncthreads();  // previous layer's LDS reads are done
-        if (!(PPO_MLP_DBG & 1)) {
-            if (l == 0)
-                stage_w<kK0>(lds, a.w[0]);
-            else
-                stage_w<kHid>(lds, a.w[l]);
-        }
+    for (int r = 0; r < 16; ++r) bhv[r] = feat(r, h) < a.nh ? a.bh[feat(r, h)] : 0.f;
+    {
+        f32x16 binit;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) binit[r] = ba[r];
+        const f32x16 c0 = mfma_tile<DT, 16>(X0, wa, binit, 0, j, h);
+        tile_epi<DT, false, STORE>(pend, X0, 96 + j, row0 + 96 + j, rh[3], hs, r5, F0, h);
+        const f32x16 c1 = mfma_tile<DT, 16>(X0, wa, binit, 1, j, h);
+        tile_epi<DT, true, STORE>(c0, X1, j, row0 + j, rh[0], hs, r5, F0, h);
+        const f32x16 c2 = mfma_tile<DT, 16>(X0, wa, binit, 2, j, h);
+        tile_epi<DT, true, STORE>(c1, X1, 32 + j, row0 + 32 + j, rh[0], hs, r5, F0, h);
         __syncthreads();
-        if (!(PPO_MLP_DBG & 2)) {
-            if (l == 0)
-                layer_mma<kK0, DT>(lds, xb, acc, lane);
-            else
-                layer_mma<kHid, DT>(lds, xb, acc, lane);
-        }
-        // epilogue: bias + ELU in fp32, store, and the next layer's B fragments
-        const float* bias = lbias + l * kHid;
-        // per-lane row bases: every store below is base + a compile-time offset (no per-store address)
-        uint16_t* __restrict__ hrow = l < 4 && a.h[l] ? a.h[l] + int64_t(row) * a.h_stride + 8 * h : nullptr;
-        float* __restrict__ h5row = l == 4 && a.h5 ? a.h5 + int64_t(row) * kHid + 4 * h : nullptr;
-#pragma unroll
-        for (int ot = 0; ot < kTiles; ++ot) {
-            Frag<DT> f[2];
-            float bv[16];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {  // features ot*32 + 8g + 4h + 0..3 of registers 4g..4g+3
-                const float4 q = *reinterpret_cast<const float4*>(bias + ot * 32 + 8 * g + 4 * h);
-                bv[4 * g] = q.x;
-                bv[4 * g + 1] = q.y;
-                bv[4 * g + 2] = q.z;
-                bv[4 * g + 3] = q.w;
-            }
+        const f32x16 c3 = mfma_tile<DT, 16>(X0, wa, binit, 3, j, h);
+        tile_epi<DT, true, STORE>(c2, X1, 64 + j, row0 + 64 + j, rh[0], hs, r5, F0, h);
+        tile_epi<DT, true, STORE>(c3, X1, 96 + j, row0 + 96 + j, rh[0], hs, r5, F0, h);
+    }
+    __syncthreads();
+    // ---- heads: wave w < 4 takes N-tile w; out = 16-bit(acc + 16-bit(bh)) as under autocast
+    if (wave < 4 && a.head) {
+        f32x16 hacc[4];
+        mma_rows<DT, 16, 1>(X1, wb, hacc, wave, j, h);
+        const int row = row0 + 32 * wave + j;
+        if (row < rows) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float z = acc[ot][r] + bv[r];
-                // ELU (alpha 1): exp(z) - 1 on the hardware exp; |error| ~1e-7, far below the bf16 step
-                const float y = (PPO_MLP_DBG & 4) ? z : (z > 0.f ? z : __expf(z) - 1.f);
-                acc[ot][r] = y;
-                f[r >> 3].v[r & 7] = (E)y;  // v_cvt_pk_bf16_f32 / v_cvt_f16_f32 (round to nearest even)
-            }
-            xb[ot][0] = f[0].v;
-            xb[ot][1] = f[1].v;
-            if (hrow) {
-                const uint4 c01 = pair_chunks(f[0].q[0], f[0].q[1]), c23 = pair_chunks(f[1].q[0], f[1].q[1]);
-                if (live) {
-                    *reinterpret_cast<uint4*>(hrow + ot * 32) = c01;
-                    *reinterpret_cast<uint4*>(hrow + ot * 32 + 16) = c23;
-                }
-            }
-            if (live) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    if (h5row)
-                        *reinterpret_cast<float4*>(h5row + ot * 32 + 8 * g) =
-                            make_float4(acc[ot][4 * g], acc[ot][4 * g + 1], acc[ot][4 * g + 2], acc[ot][4 * g + 3]);
-                }
+                const int o = feat(r, h);
+                if (o < a.nh) a.head[int64_t(row) * a.nh + o] = float((E)(hacc[0][r] + float((E)bhv[r])));
             }
         }
     }
-    // heads in exact f32: head[row][o] = sum_f wh[o][f] h5[f] + bh[o]
-    if (PPO_MLP_DBG & 8) return;
-    __syncthreads();
-    float* wl = reinterpret_cast<float*>(lds);
-    constexpr int kHs = kHid + 4;
-    {  // 32 x 256 fp32 head weights (rows >= nh zero): 8 independent 16-B loads per thread
-        constexpr int per = 32 * kHid / 4 / (64 * kWaves);
-        float4 v[per];
-#pragma unroll
-        for (int u = 0; u < per; ++u) {
-            const int c = u * (64 * kWaves) + threadIdx.x;
-            const int o = c / (kHid / 4), col = (c % (kHid / 4)) * 4;
-            v[u] = o < a.nh ? *reinterpret_cast<const float4*>(a.wh + o * kHid + col) : make_float4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < per; ++u) {
-            const int c = u * (64 * kWaves) + threadIdx.x;
-            *reinterpret_cast<float4*>(wl + (c / (kHid / 4)) * kHs + (c % (kHid / 4)) * 4) = v[u];
-        }
-    }
-    __syncthreads();
-    f32x16 hq[4] = {};  // four independent chains (the f32 MFMA result latency is not exposed)
-#pragma unroll
-    for (int ot = 0; ot < kTiles; ++ot) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float wv = wl[j * kHs + ot * 32 + feat(r, h)];
-            hq[r & 3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv, acc[ot][r], hq[r & 3], 0, 0, 0);
-        }
-    }
-    const f32x16 hacc = (hq[0] + hq[1]) + (hq[2] + hq[3]);
-    if (live && a.head) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int o = feat(r, h);
-            if (o < a.nh) a.head[int64_t(row) * a.nh + o] = hacc[r] + a.bh[o];
-        }
-    }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kFThreads, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
+    // training stores layers 1..5 for the backward (every pointer set); the rollout form stores none
+    if (a.h[0] && !(PPO_FWD_DBG & 4))
+        mlp_fwd_body<DT, true>(a);
+    else
+        mlp_fwd_body<DT, false>(a);
 }
 
 // ------------------------------------------------------------------------------ backward chain
@@ -435,7 +600,7 @@ extern "C" int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream) {
 
 extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
     if (!args_host || !args_host->x || args_host->nh <= 0 || args_host->nh > 32 || args_host->rows <= 0 ||
-        args_host->x_stride < kK0 || args_host->h_stride < kHid || (args_host->x_stride % 4) || (args_host->h_stride % 8) ||
+        args_host->x_stride < kK0 || args_host->h_stride < kHid || (args_host->x_stride % 8) || (args_host->h_stride % 8) ||
         (args_host->dtype != PPO_DT_BF16 && args_host->dtype != PPO_DT_F16)) {
         snprintf(g_err, sizeof(g_err), "ppo_mlp_forward: bad arguments");
         ppo_detail::set_error(g_err);
@@ -443,15 +608,15 @@ extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
     }
     static bool attr[2] = {false, false};
     const bool f16 = args_host->dtype == PPO_DT_F16;
-    const int rc = f16 ? reserve_lds(k_mlp_fwd<PPO_DT_F16>, kLdsBytes, attr[1], "ppo_mlp_forward")
-                       : reserve_lds(k_mlp_fwd<PPO_DT_BF16>, kLdsBytes, attr[0], "ppo_mlp_forward");
+    const int rc = f16 ? reserve_lds(k_mlp_fwd<PPO_DT_F16>, kFLds, attr[1], "ppo_mlp_forward")
+                       : reserve_lds(k_mlp_fwd<PPO_DT_BF16>, kFLds, attr[0], "ppo_mlp_forward");
     if (rc) return rc;
-    const int blocks = (args_host->rows + kRowsPerBlock - 1) / kRowsPerBlock;
+    const int blocks = (args_host->rows + kFRows - 1) / kFRows;
     if (f16)
-        hipLaunchKernelGGL(k_mlp_fwd<PPO_DT_F16>, dim3(blocks), dim3(64 * kWaves), kLdsBytes,
+        hipLaunchKernelGGL(k_mlp_fwd<PPO_DT_F16>, dim3(blocks), dim3(kFThreads), kFLds,
                            static_cast<hipStream_t>(stream), *args_host);
     else
-        hipLaunchKernelGGL(k_mlp_fwd<PPO_DT_BF16>, dim3(blocks), dim3(64 * kWaves), kLdsBytes,
+        hipLaunchKernelGGL(k_mlp_fwd<PPO_DT_BF16>, dim3(blocks), dim3(kFThreads), kFLds,
                            static_cast<hipStream_t>(stream), *args_host);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

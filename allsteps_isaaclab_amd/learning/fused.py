@@ -11,7 +11,8 @@ the same maths is an explicit forward / backward:
   gradients, and the weight gradients as a **split-K** batched GEMM (``bmm`` over S row chunks,
   fp32 out, summed) -- the library's single ``dz^T h`` with K = 32768 and a 256 x 256 output runs on 16
   workgroups (measured 113 us vs 29 us split, scripts/mlp_microbench.py);
-* heads (mu | value, 22 x 256) and everything after them in fp32;
+* heads (mu | value, 22 x 256) on the 16-bit layer-5 activations with fp32 accumulation and a 16-bit
+  output, as autocast runs them (MFMA trunk); the losses and everything after them in fp32;
 * ``libppo_hip.so`` (include/ppo.h) for the rest: obs normaliser update + normalise, the fused
   loss / KL / head-gradient kernel, ELU backward with bias-gradient partials, clip + Adam over the flat
   buffer (writing the fp16 / bf16 trunk mirror), adaptive LR and the device minibatch counter;
@@ -332,13 +333,14 @@ class FusedPPOUpdate:
     # ------------------------------------------------------------------ the two halves
     def _trunk(self, x, idx, rows, h, h_last_f, head) -> None:
         """Normalise rows [idx*rows, (idx+1)*rows) of x, run the trunk (16-bit mirror or fp32 weights) and
-        the fp32 heads into head = [mu | value]."""
+        the heads into head = [mu | value] (fp32 storage; with the MFMA trunk the heads run as rl_games'
+        autocast runs them: 16-bit inputs / weights / bias, fp32 accumulation, a 16-bit-rounded output)."""
         L, s, rms = self.L, self._stream(), self.rms
         _check(L.ppo_obs_normalize(_p(x), _p(idx), rows, self.obs_dim, _p(rms.running_mean), _p(rms.running_var),
                                    rms.epsilon, _p(h[0]), self.k0, h[0].stride(0), self.dt_code, s),
                "ppo_obs_normalize")
         if self.mfma_trunk:
-            # one launch: 5 x (MFMA + bias + ELU) with the activations chained in registers, fp32 heads;
+            # one launch: 5 x (MFMA + bias + ELU), weight-stationary waves, activations through LDS, 16-bit heads;
             # stores layers 1..4 (16-bit) and layer 5 (fp32) only when h has room for them (training)
             a = self._mlp_args
             a.x, a.x_stride = h[0].data_ptr(), h[0].stride(0)

@@ -137,9 +137,10 @@ int ppo_counter_add(int64_t* ctr, int64_t inc, void* stream);
  * ([mu.w | value.w]), bh: nh fp32 (nh <= 32).  Outputs (row-major, NULL = skip): h[0..3] = layers
  * 1..4 (lp, columns 0..255 of rows with stride h_stride >= 256, a multiple of 8; columns beyond are
  * not touched),
- * h5 = layer 5 in fp32 (rows x 256), head = rows x nh fp32.  Each wave keeps its 32 rows' activations
- * in registers between layers (an MFMA accumulator tile is the next layer's B operand); each layer's
- * weights are staged once per workgroup in LDS. */
+ * h5 = layer 5 in fp32 (rows x 256), head = rows x nh fp32 holding lp values: the heads run as
+ * rl_games' autocast runs them -- lp layer-5 activations, lp(wh), lp(bh), fp32 accumulation, an lp
+ * output.  x_stride is a multiple of 8.  A workgroup of 8 waves owns 128 rows; wave w keeps the weights
+ * of output features [32w, 32w + 32) in registers and the activations pass through LDS. */
 typedef struct {
     const uint16_t* x;
     const uint16_t* w[5];

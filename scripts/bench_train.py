@@ -85,7 +85,7 @@ def measure(num_envs: int = 32768, epochs: int = 3, warmup: int = 2, level: int 
         "mixed_precision": agent.mixed_precision, "grad_scaler": agent.scaler_state is not None,
         "hip_graphs": agent._play_graphs is not None,
         "precision": (("fp16" if agent.mixed_precision_dtype == torch.float16 else "bf16") if agent.mixed_precision
-                      else "fp32") + " MLP trunk on MFMA (fp32 accumulate), fp32 heads / losses / Adam / normalisers, "
+                      else "fp32") + " MLP trunk and heads on MFMA (fp32 accumulate; heads rounded to 16 bit as under autocast), fp32 losses / Adam / normalisers, "
                      "device-side GradScaler (rl_games mixed_precision=True: fp16 autocast; DESIGN.md §7)",
         "data": "synthetic (random-init policy, reference reset distribution)"}
 
