@@ -3,8 +3,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--num-envs 4096] [--level 0]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
-Protocol (after scripts/benchmarks/benchmark_non_rl.py:155-179): W untimed warm-up
-steps, then K timed ``env.step`` calls bracketed by a barrier + device synchronize on both sides;
+Protocol (after scripts/benchmarks/benchmark_non_rl.py:155-179): --preheat-ms of untimed
+env steps (GPU clocks to steady state), env.reset(), W untimed warm-up steps, then K timed
+``env.step`` calls bracketed by a barrier + device synchronize on both sides;
 fresh U(-1, 1) actions every step (pre-drawn on the device before the timed region); seed 42 + rank;
 episodes terminate and reset naturally inside the timed region.  Envs are sharded per rank (weak
 scaling, no collective in the step).  value = all ranks' env-steps / max-over-ranks wall time.
@@ -71,6 +72,9 @@ def parse():
                         "it scales, DESIGN.md §6) or the north star's all-gather of rollouts (every rank then "
                         "runs the whole update on W x the data)")
     p.add_argument("--no-c5", action="store_true", help="skip the quadruped (BASELINE C5) task measurement")
+    p.add_argument("--preheat-ms", type=float, default=250.0,
+                   help="untimed env steps before env.reset() that bring the GPU to its steady clocks (DESIGN.md §3 "
+                        "'The driver's window'); 0 disables")
     return p.parse_args()
 
 
@@ -333,6 +337,19 @@ def main():
     gen = torch.Generator(device=device).manual_seed(1000 + rank)
     K, W = args.steps, args.warmup
     actions = torch.rand(K + W, n, 21, device=device, generator=gen) * 2.0 - 1.0
+    # GPU clocks: a timed region of a few ms right after construction would run while the GPU is still
+    # clocking up from idle (measured: the 20-step driver window 0.1428 ms/step cold, 0.1317 warm,
+    # scripts/window_clock.py).  Steps of the env itself, BEFORE env.reset(), keep the part afterwards --
+    # reset, W warm-up steps, K timed steps -- exactly the protocol; they are reported on the line.
+    preheat_steps = 0
+    if args.preheat_ms > 0:
+        env.reset()
+        t_heat = time.perf_counter()
+        while time.perf_counter() - t_heat < args.preheat_ms / 1e3:
+            for _ in range(10):
+                env.step(actions[preheat_steps % (K + W)])
+                preheat_steps += 1
+            torch.cuda.synchronize(device)
     env.reset()
     for t in range(W):
         env.step(actions[K + t])
@@ -430,6 +447,9 @@ def main():
             "cpu_baseline": None,
             "resets_last_step": resets,
             # PhysX keeps every contact (simulation_cfg.py:110); this build's 30-row budget cuts these
+            "gpu_preheat": {"ms": args.preheat_ms, "env_steps": preheat_steps,
+                            "what": "untimed env steps before env.reset() (GPU clocks to steady state); then reset, "
+                                    "W warm-up steps, K timed steps"},
             "contacts_dropped": {"total": dropped, "per_step": round(dropped / K, 2),
                                  "per_env_step": round(dropped / (K * n), 6),
                                  "method": "as_step_counters word 3 summed over the timed window's K steps "
