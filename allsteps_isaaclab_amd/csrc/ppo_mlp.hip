@@ -230,6 +230,7 @@ __device__ __forceinline__ void mma_rows(const uint16_t* X, const typename Lp<DT
 #endif
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 
 // a range-checked buffer over `bytes` bytes from p (uniform kernel-argument inputs): stores past the
@@ -451,107 +452,180 @@ __global__ void __launch_bounds__(kFThreads, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
 }
 
 // ------------------------------------------------------------------------------ backward chain
+//
+// The forward's layout run backwards (weight-stationary, 8 waves, 128 rows, two LDS images): stage H
+// forms dh5 = Wh^T dhead for the wave's 32 features of layer 5 (exact-f32 `32x32x2f32` MFMAs, dhead and
+// Wh in fp32), then each stage l = 4..1 forms dh = W_l^T dz_l for the wave's 32 INPUT features of layer l
+// (the A fragments: rows of the 16-bit W_l^T mirror, in registers, loaded one stage ahead; the B
+// fragments: dz_l from LDS), and every epilogue turns dh into dz = dh * elu'(y) (y > 0 ? 1 : y + 1, the
+// output form) with y the layer's stored activations (16-bit; layer 5 in fp32), rounds it once, writes it
+// to the next stage's LDS image and to dz[l] for the weight gradients.  Same tile pipelining and barriers
+// as the forward.
+
+// y of tile rows for the wave's features F0 + feat(r, h): 16-bit activations (8 dwords) or fp32 (16 floats)
+template <bool Y32>
+struct YT;
+template <>
+struct YT<false> {
+    u32x2_t v[4];
+};
+template <>
+struct YT<true> {
+    u32x4_t v[4];
+};
+
+template <bool Y32>
+__device__ __forceinline__ YT<Y32> load_y(Rsrc ry, int row, int stride, int F0, int h) {
+    YT<Y32> y;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        if constexpr (Y32)
+            y.v[g] = __builtin_amdgcn_raw_buffer_load_b128(ry, (row * stride + F0 + 8 * g + 4 * h) * 4, 0, 0);
+        else
+            y.v[g] = __builtin_amdgcn_raw_buffer_load_b64(ry, (row * stride + F0 + 8 * g + 4 * h) * 2, 0, 0);
+    }
+    return y;
+}
+
+template <int DT, bool Y32>
+__device__ __forceinline__ float y_at(const YT<Y32>& y, int r) {
+    typedef typename Lp<DT>::e E;
+    if constexpr (Y32) {
+        return __uint_as_float(y.v[r >> 2][r & 3]);
+    } else {
+        const uint32_t d = y.v[r >> 2][(r & 3) >> 1];
+        const uint16_t u = (r & 1) ? uint16_t(d >> 16) : uint16_t(d & 0xffff);
+        return float(__builtin_bit_cast(E, u));
+    }
+}
+
+// dz of one tile: dh * elu'(y) in fp32, one rounding; into the next stage's LDS image and dz (global,
+// rows x 256, range-checked)
+template <int DT, bool Y32>
+__device__ __forceinline__ void tile_bepi(const f32x16& dh, const YT<Y32>& y, uint16_t* Xn, int rl, int row, Rsrc rdz,
+                                          int F0, int h) {
+    uint32_t dw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        float v[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int r = 2 * k + e;
+            const float yy = y_at<DT, Y32>(y, r);
+            v[e] = yy > 0.f ? dh[r] : dh[r] * (yy + 1.f);
+        }
+        dw[k] = pack2<DT>(f32x2_t{v[0], v[1]});
+    }
+    const uint4 c01 = pair_chunks(make_uint2(dw[0], dw[1]), make_uint2(dw[2], dw[3]));
+    const uint4 c23 = pair_chunks(make_uint2(dw[4], dw[5]), make_uint2(dw[6], dw[7]));
+    uint16_t* xn = Xn + rl * kXs + F0 + 8 * h;
+    *reinterpret_cast<uint4*>(xn) = c01;
+    *reinterpret_cast<uint4*>(xn + 16) = c23;
+    const int off = (row * kHid + F0 + 8 * h) * 2;
+    __builtin_amdgcn_raw_buffer_store_b128(u4(c01), rdz, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u4(c23), rdz, off + 32, 0, 0);
+}
+
+// stage l = 4..1: dh = W_l^T dz_l (Xin) for the wave's input features, epilogue against y (layer l - 1's
+// activations, ry) into Xout and dz[l - 1]; phase 0 also finishes the previous stage's tile 3 (pend,
+// against ypend, into Xin rows 96..127 and dz[l])
+template <int DT, bool YP32>
+__device__ __forceinline__ void bstage(const uint16_t* Xin, uint16_t* Xout, const typename Lp<DT>::v8 (&wa)[16],
+                                       f32x16& pend, YT<YP32>& ypend, Rsrc rdz_prev, Rsrc ry, int y_stride, Rsrc rdz,
+                                       YT<false>& ynext, int row0, int F0, int j, int h) {
+    const f32x16 zero = {};
+    YT<false> y0 = load_y<false>(ry, row0 + j, y_stride, F0, h);
+    const f32x16 c0 = mfma_tile<DT, 16>(Xin, wa, zero, 0, j, h);
+    tile_bepi<DT, YP32>(pend, ypend, const_cast<uint16_t*>(Xin), 96 + j, row0 + 96 + j, rdz_prev, F0, h);
+    YT<false> y1 = load_y<false>(ry, row0 + 32 + j, y_stride, F0, h);
+    const f32x16 c1 = mfma_tile<DT, 16>(Xin, wa, zero, 1, j, h);
+    tile_bepi<DT, false>(c0, y0, Xout, j, row0 + j, rdz, F0, h);
+    YT<false> y2 = load_y<false>(ry, row0 + 64 + j, y_stride, F0, h);
+    const f32x16 c2 = mfma_tile<DT, 16>(Xin, wa, zero, 2, j, h);
+    tile_bepi<DT, false>(c1, y1, Xout, 32 + j, row0 + 32 + j, rdz, F0, h);
+    __syncthreads();
+    ynext = load_y<false>(ry, row0 + 96 + j, y_stride, F0, h);
+    const f32x16 c3 = mfma_tile<DT, 16>(Xin, wa, zero, 3, j, h);
+    tile_bepi<DT, false>(c2, y2, Xout, 64 + j, row0 + 64 + j, rdz, F0, h);
+    pend = c3;
+    __syncthreads();
+}
 
 template <int DT>
-__global__ void __launch_bounds__(64 * kWaves, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
-    typedef typename Lp<DT>::e E;
+__global__ void __launch_bounds__(kFThreads, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
     typedef typename Lp<DT>::v8 V8;
     extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    uint16_t* X0 = lds;
+    uint16_t* X1 = lds + kFRows * kXs;
     const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
     const int j = lane & 31, h = lane >> 5, i = lane & 31;
-    const int row = blockIdx.x * kRowsPerBlock + wave * 32 + j;
-    const bool live = row < a.rows;
-    constexpr int kHs = kHid + 4;
-    // dh5 = Wh^T dhead: A[feature i][k] = wh[k][feature], B[k][batch j] = dhead[j][k]; k = 2t + h
-    float* wl = reinterpret_cast<float*>(lds);
-    {
-        constexpr int per = 32 * kHid / 4 / (64 * kWaves);
-        float4 v[per];
+    const int F0 = 32 * wave;
+    const int row0 = blockIdx.x * kFRows;
+    const int rows = a.rows, nh = a.nh, hs = a.h_stride;
+    Rsrc rdz[5], rh[4];
 #pragma unroll
-        for (int u = 0; u < per; ++u) {
-            const int c = u * (64 * kWaves) + threadIdx.x;
-            const int o = c / (kHid / 4), col = (c % (kHid / 4)) * 4;
-            v[u] = o < a.nh ? *reinterpret_cast<const float4*>(a.wh + o * kHid + col) : make_float4(0, 0, 0, 0);
-        }
+    for (int l = 0; l < 5; ++l) rdz[l] = rsrc(a.dz[l], int64_t(rows) * kHid * 2);
 #pragma unroll
-        for (int u = 0; u < per; ++u) {
-            const int c = u * (64 * kWaves) + threadIdx.x;
-            *reinterpret_cast<float4*>(wl + (c / (kHid / 4)) * kHs + (c % (kHid / 4)) * 4) = v[u];
-        }
+    for (int l = 0; l < 4; ++l) rh[l] = rsrc(a.h[l], int64_t(rows) * hs * 2);
+    const Rsrc r5 = rsrc(a.h5, int64_t(rows) * kHid * 4);
+    const Rsrc rdh = rsrc(a.dhead, int64_t(rows) * nh * 4);
+    // ---- stage H: dh5 = Wh^T dhead (f32 MFMA: A[i][k] = wh[k][F0 + i], k = 2s + h; B[k][n] = dhead[n][k])
+    float ah[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int k = 2 * s + h;
+        ah[s] = k < nh ? a.wh[k * kHid + F0 + i] : 0.f;
     }
-    float bq[16];
+    V8 wa[16], wb[16];
+    load_wa<DT, 16>(a.wt[3], kHid, F0, i, h, wa);  // W_4^T, the first 16-bit stage's slice
+    YT<true> y5[4];
+    f32x16 dh5[4];
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-        const int k = 2 * t + h;
-        bq[t] = (live && k < a.nh) ? a.dhead[int64_t(row) * a.nh + k] : 0.f;
+    for (int t = 0; t < 4; ++t) {
+        const int row = row0 + 32 * t + j;
+        y5[t] = load_y<true>(r5, row, kHid, F0, h);
+        float bq[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int k = 2 * s + h;
+            bq[s] = k < nh ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdh, (row * nh + k) * 4, 0, 0)) : 0.f;
+        }
+        f32x16 c = {};
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+            if (2 * s < nh) c = __builtin_amdgcn_mfma_f32_32x32x2f32(ah[s], bq[s], c, 0, 0, 0);  // uniform
+        dh5[t] = c;
     }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) tile_bepi<DT, true>(dh5[t], y5[t], X0, 32 * t + j, row0 + 32 * t + j, rdz[4], F0, h);
     __syncthreads();
-    f32x16 acc[kTiles];
-#pragma unroll
-    for (int ot = 0; ot < kTiles; ++ot) acc[ot] = f32x16{};
-    const int nsteps = (a.nh + 1) / 2;
-    for (int t = 0; t < nsteps; ++t) {
-        const int k = 2 * t + h;
-#pragma unroll
-        for (int ot = 0; ot < kTiles; ++ot)
-            acc[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[k * kHs + ot * 32 + i], bq[t], acc[ot], 0, 0, 0);
-    }
-    V8 xb[kTiles][2];
-    uint2 yb[kTiles][4];  // 16-bit activations of layer l - 1, loaded while layer l's MFMAs run
-    for (int l = 4; l >= 0; --l) {
-        // dz_l = dh * elu'(y_l), y_l = layer-l activations (layer 5 in fp32, the others 16-bit)
-        uint16_t* __restrict__ dzo = a.dz[l];
-#pragma unroll
-        for (int ot = 0; ot < kTiles; ++ot) {
-            float y[16];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int c = ot * 32 + 8 * g + 4 * h;
-                if (!live) {
-                    y[4 * g] = y[4 * g + 1] = y[4 * g + 2] = y[4 * g + 3] = 0.f;
-                } else if (l == 4) {
-                    const float4 q = *reinterpret_cast<const float4*>(a.h5 + int64_t(row) * kHid + c);
-                    y[4 * g] = q.x;
-                    y[4 * g + 1] = q.y;
-                    y[4 * g + 2] = q.z;
-                    y[4 * g + 3] = q.w;
-                } else {
-                    Frag<DT> ff;
-                    ff.q[0] = yb[ot][g];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) y[4 * g + e] = float(ff.v[e]);
-                }
-            }
-            Frag<DT> f[2];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float dz = y[r] > 0.f ? acc[ot][r] : acc[ot][r] * (y[r] + 1.f);
-                f[r >> 3].v[r & 7] = (E)dz;
-            }
-            xb[ot][0] = f[0].v;
-            xb[ot][1] = f[1].v;
-            const uint4 c01 = pair_chunks(f[0].q[0], f[0].q[1]), c23 = pair_chunks(f[1].q[0], f[1].q[1]);
-            if (live) {
-                uint16_t* d = dzo + int64_t(row) * kHid + ot * 32 + 8 * h;
-                *reinterpret_cast<uint4*>(d) = c01;
-                *reinterpret_cast<uint4*>(d + 16) = c23;
-            }
-        }
-        if (l == 0) break;
-        // dh of layer l's input = W_l^T dz_l
+    // ---- stages 4..1 (dz_l in the LDS image -> dz_{l-1}); the next stage's W^T slice flies under each
+    f32x16 pend = {};
+    YT<false> yp;
+    {
+        load_wa<DT, 16>(a.wt[2], kHid, F0, i, h, wb);
+        // stage 4: stage H completed all four of its tiles, so there is no pending tile to finish here
+        const f32x16 zero = {};
+        YT<false> y0 = load_y<false>(rh[3], row0 + j, hs, F0, h);
+        const f32x16 c0 = mfma_tile<DT, 16>(X0, wa, zero, 0, j, h);
+        YT<false> y1 = load_y<false>(rh[3], row0 + 32 + j, hs, F0, h);
+        const f32x16 c1 = mfma_tile<DT, 16>(X0, wa, zero, 1, j, h);
+        tile_bepi<DT, false>(c0, y0, X1, j, row0 + j, rdz[3], F0, h);
+        YT<false> y2 = load_y<false>(rh[3], row0 + 64 + j, hs, F0, h);
+        const f32x16 c2 = mfma_tile<DT, 16>(X0, wa, zero, 2, j, h);
+        tile_bepi<DT, false>(c1, y1, X1, 32 + j, row0 + 32 + j, rdz[3], F0, h);
+        yp = load_y<false>(rh[3], row0 + 96 + j, hs, F0, h);
+        const f32x16 c3 = mfma_tile<DT, 16>(X0, wa, zero, 3, j, h);
+        tile_bepi<DT, false>(c2, y2, X1, 64 + j, row0 + 64 + j, rdz[3], F0, h);
+        pend = c3;
         __syncthreads();
-        stage_w<kHid>(lds, a.wt[l - 1]);
-        __syncthreads();
-        // issued after the staging loads have been waited for, so only the MFMAs below cover them
-        if (live) {
-            const uint16_t* __restrict__ yrow = a.h[l - 1] + int64_t(row) * a.h_stride + 4 * h;
-#pragma unroll
-            for (int ot = 0; ot < kTiles; ++ot)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) yb[ot][g] = *reinterpret_cast<const uint2*>(yrow + ot * 32 + 8 * g);
-        }
-        layer_mma<kHid, DT>(lds, xb, acc, lane);
     }
+    load_wa<DT, 16>(a.wt[1], kHid, F0, i, h, wa);
+    bstage<DT, false>(X1, X0, wb, pend, yp, rdz[3], rh[2], hs, rdz[2], yp, row0, F0, j, h);
+    load_wa<DT, 16>(a.wt[0], kHid, F0, i, h, wb);
+    bstage<DT, false>(X0, X1, wa, pend, yp, rdz[2], rh[1], hs, rdz[1], yp, row0, F0, j, h);
+    bstage<DT, false>(X1, X0, wb, pend, yp, rdz[1], rh[0], hs, rdz[0], yp, row0, F0, j, h);
+    tile_bepi<DT, false>(pend, yp, X0, 96 + j, row0 + 96 + j, rdz[0], F0, h);
 }
 
 }  // namespace
@@ -579,15 +653,15 @@ extern "C" int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream) {
     }
     static bool attr[2] = {false, false};
     const bool f16 = args_host->dtype == PPO_DT_F16;
-    const int rc = f16 ? reserve_lds(k_mlp_bwd<PPO_DT_F16>, kWBytes, attr[1], "ppo_mlp_backward")
-                       : reserve_lds(k_mlp_bwd<PPO_DT_BF16>, kWBytes, attr[0], "ppo_mlp_backward");
+    const int rc = f16 ? reserve_lds(k_mlp_bwd<PPO_DT_F16>, kFLds, attr[1], "ppo_mlp_backward")
+                       : reserve_lds(k_mlp_bwd<PPO_DT_BF16>, kFLds, attr[0], "ppo_mlp_backward");
     if (rc) return rc;
-    const int blocks = (args_host->rows + kRowsPerBlock - 1) / kRowsPerBlock;
+    const int blocks = (args_host->rows + kFRows - 1) / kFRows;
     if (f16)
-        hipLaunchKernelGGL(k_mlp_bwd<PPO_DT_F16>, dim3(blocks), dim3(64 * kWaves), kWBytes,
+        hipLaunchKernelGGL(k_mlp_bwd<PPO_DT_F16>, dim3(blocks), dim3(kFThreads), kFLds,
                            static_cast<hipStream_t>(stream), *args_host);
     else
-        hipLaunchKernelGGL(k_mlp_bwd<PPO_DT_BF16>, dim3(blocks), dim3(64 * kWaves), kWBytes,
+        hipLaunchKernelGGL(k_mlp_bwd<PPO_DT_BF16>, dim3(blocks), dim3(kFThreads), kFLds,
                            static_cast<hipStream_t>(stream), *args_host);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
