@@ -372,13 +372,45 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     const int F0 = 32 * wave;                 // this wave's output features
     const int row0 = blockIdx.x * kFRows;
     const int rows = a.rows;
-    // layer-0 input rows -> X0 (16-B chunks, zero past `rows`)
+    if (a.obs) {
+        // the input normalisation fused in (ppo_obs_normalize's formula): thread -> row tid / 4, 16 columns
+        static_assert(kFRows * kK0 == 16 * kFThreads, "16 input columns per thread");
+        typedef typename Lp<DT>::e E;
+        const int r = threadIdx.x >> 2, c0 = 16 * (threadIdx.x & 3), row = row0 + r;
+        const float* src = a.obs + (int64_t(*a.mb_idx) * rows + row) * a.obs_dim;
+        uint32_t dw[8];
 #pragma unroll
-    for (int u = 0; u < kFRows * (kK0 / 8) / kFThreads; ++u) {
-        const int c = u * kFThreads + threadIdx.x, r = c / (kK0 / 8), q = c % (kK0 / 8);
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (row0 + r < rows) v = *reinterpret_cast<const uint4*>(a.x + int64_t(row0 + r) * a.x_stride + 8 * q);
-        *reinterpret_cast<uint4*>(X0 + r * kXs + 8 * q) = v;
+        for (int k = 0; k < 8; ++k) {
+            float v[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int c = c0 + 2 * k + e;
+                float y = 0.f;
+                if (c < a.obs_dim && row < rows) {
+                    const float mf = float(a.mean[c]), den = sqrtf(float(a.var[c]) + a.eps);
+                    y = fminf(fmaxf((src[c] - mf) / den, -5.f), 5.f);
+                }
+                v[e] = y;
+            }
+            dw[k] = pack2<DT>(f32x2_t{v[0], v[1]});
+        }
+        const uint4 lo = make_uint4(dw[0], dw[1], dw[2], dw[3]), hi = make_uint4(dw[4], dw[5], dw[6], dw[7]);
+        *reinterpret_cast<uint4*>(X0 + r * kXs + c0) = lo;
+        *reinterpret_cast<uint4*>(X0 + r * kXs + c0 + 8) = hi;
+        if (a.x_out && row < rows) {
+            uint16_t* d = a.x_out + int64_t(row) * a.x_stride + c0;
+            *reinterpret_cast<uint4*>(d) = lo;
+            *reinterpret_cast<uint4*>(d + 8) = hi;
+        }
+    } else {
+        // layer-0 input rows -> X0 (16-B chunks, zero past `rows`)
+#pragma unroll
+        for (int u = 0; u < kFRows * (kK0 / 8) / kFThreads; ++u) {
+            const int c = u * kFThreads + threadIdx.x, r = c / (kK0 / 8), q = c % (kK0 / 8);
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (row0 + r < rows) v = *reinterpret_cast<const uint4*>(a.x + int64_t(row0 + r) * a.x_stride + 8 * q);
+            *reinterpret_cast<uint4*>(X0 + r * kXs + 8 * q) = v;
+        }
     }
     const int hs = a.h_stride;
     Rsrc rh[4], r5;
@@ -673,7 +705,9 @@ extern "C" int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream) {
 }
 
 extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
-    if (!args_host || !args_host->x || args_host->nh <= 0 || args_host->nh > 32 || args_host->rows <= 0 ||
+    if (!args_host || (!args_host->x && !args_host->obs) || args_host->nh <= 0 || args_host->nh > 32 || args_host->rows <= 0 ||
+        (args_host->obs && (!args_host->mb_idx || !args_host->mean || !args_host->var || args_host->obs_dim <= 0 ||
+                            args_host->obs_dim > kK0)) ||
         args_host->x_stride < kK0 || args_host->h_stride < kHid || (args_host->x_stride % 8) || (args_host->h_stride % 8) ||
         (args_host->dtype != PPO_DT_BF16 && args_host->dtype != PPO_DT_F16)) {
         snprintf(g_err, sizeof(g_err), "ppo_mlp_forward: bad arguments");

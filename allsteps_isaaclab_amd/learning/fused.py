@@ -38,7 +38,7 @@ import torch.nn.functional as F
 from .._native import PPO_LIB_PATH, NativeError, check_build_id
 
 _LIB = None
-PPO_ABI_VERSION = 2
+PPO_ABI_VERSION = 3
 PPO_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 SCALER_GROWTH_INTERVAL = 2000  # torch.cuda.amp.GradScaler defaults (rl_games builds it with defaults)
 SCALER_INIT = 2.0 ** 16
@@ -60,7 +60,8 @@ class PpoMlpFwd(C.Structure):
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p * 5), ("b", C.c_void_p * 5), ("wh", C.c_void_p),
                 ("bh", C.c_void_p), ("h", C.c_void_p * 4), ("h5", C.c_void_p), ("head", C.c_void_p),
                 ("rows", C.c_int32), ("nh", C.c_int32), ("x_stride", C.c_int32), ("h_stride", C.c_int32),
-                ("dtype", C.c_int32)]
+                ("dtype", C.c_int32), ("obs", C.c_void_p), ("mb_idx", C.c_void_p), ("mean", C.c_void_p),
+                ("var", C.c_void_p), ("x_out", C.c_void_p), ("eps", C.c_float), ("obs_dim", C.c_int32)]
 
 
 class PpoMlpBwd(C.Structure):
@@ -336,13 +337,14 @@ class FusedPPOUpdate:
         the heads into head = [mu | value] (fp32 storage; with the MFMA trunk the heads run as rl_games'
         autocast runs them: 16-bit inputs / weights / bias, fp32 accumulation, a 16-bit-rounded output)."""
         L, s, rms = self.L, self._stream(), self.rms
-        _check(L.ppo_obs_normalize(_p(x), _p(idx), rows, self.obs_dim, _p(rms.running_mean), _p(rms.running_var),
-                                   rms.epsilon, _p(h[0]), self.k0, h[0].stride(0), self.dt_code, s),
-               "ppo_obs_normalize")
         if self.mfma_trunk:
-            # one launch: 5 x (MFMA + bias + ELU), weight-stationary waves, activations through LDS, 16-bit heads;
-            # stores layers 1..4 (16-bit) and layer 5 (fp32) only when h has room for them (training)
+            # one launch: the input normalisation (RunningMeanStd), 5 x (MFMA + bias + ELU) with
+            # weight-stationary waves and the activations through LDS, 16-bit heads; stores the normalised
+            # input and layers 1..4 (16-bit) and 5 (fp32) only when h has room for them (training)
             a = self._mlp_args
+            a.obs, a.mb_idx, a.obs_dim = x.data_ptr(), idx.data_ptr(), self.obs_dim
+            a.mean, a.var, a.eps = rms.running_mean.data_ptr(), rms.running_var.data_ptr(), rms.epsilon
+            a.x_out = h[0].data_ptr() if len(h) > 1 else None
             a.x, a.x_stride = h[0].data_ptr(), h[0].stride(0)
             a.h_stride = h[1].stride(0) if len(h) > 1 else 256
             for i in range(4):
@@ -351,6 +353,9 @@ class FusedPPOUpdate:
             a.head, a.rows = head.data_ptr(), rows
             _check(L.ppo_mlp_forward(C.byref(a), s), "ppo_mlp_forward")
             return
+        _check(L.ppo_obs_normalize(_p(x), _p(idx), rows, self.obs_dim, _p(rms.running_mean), _p(rms.running_var),
+                                   rms.epsilon, _p(h[0]), self.k0, h[0].stride(0), self.dt_code, s),
+               "ppo_obs_normalize")
         for i in range(len(self.linears)):  # z = h W^T + b ; h' = elu(z)
             out = h[i + 1]
             torch.addmm(self.b_lp[i], h[i], self.W_lp[i].t(), out=out)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PPO_ABI_VERSION 2
+#define PPO_ABI_VERSION 3
 /* element types of the low-precision (trunk) buffers */
 #define PPO_DT_F32 0
 #define PPO_DT_BF16 1
@@ -152,6 +152,19 @@ typedef struct {
     float* head;
     int32_t rows, nh, x_stride, h_stride;
     int32_t dtype; /* PPO_DT_BF16 or PPO_DT_F16 */
+    /* Fused input normalisation (the RunningMeanStd of the model, rl_games running_mean_std.py; replaces a
+     * ppo_obs_normalize launch): when obs != NULL the layer-0 input is formed in-kernel from the fp32
+     * observation rows [*mb_idx * rows, (*mb_idx + 1) * rows) of obs (row stride obs_dim <= 64):
+     * clamp((obs - (float)mean) / sqrtf((float)var + eps), -5, 5), zero in columns obs_dim..63, rounded
+     * to lp -- the same formula as ppo_obs_normalize -- and written to x_out (columns 0..63, row stride
+     * x_stride) when x_out != NULL (the weight gradients read it); x is then unused. */
+    const float* obs;
+    const int32_t* mb_idx;
+    const double* mean;
+    const double* var;
+    uint16_t* x_out;
+    float eps;
+    int32_t obs_dim;
 } ppo_mlp_fwd_t;
 int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream);
 

@@ -503,6 +503,58 @@ def test_fused_mlp_forward_kernel(rows, dt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rows,dt", [(32768, torch.float16), (1000, torch.bfloat16)])
+def test_fused_mlp_forward_normalises_its_input(rows, dt):
+    """ppo_mlp_forward with `obs` set forms the layer-0 input in-kernel (minibatch `*mb_idx` of the fp32
+    observations, the RunningMeanStd formula of ppo_obs_normalize): its x_out equals the separate
+    normalisation kernel's output bit for bit, and the layer outputs equal those of a forward fed that
+    output."""
+    import ctypes as C
+
+    from allsteps_isaaclab_amd.learning import fused as FU
+
+    L = FU.load()
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(5)
+    obs = torch.randn(3 * rows, 59, device=dev, generator=g) * 3
+    idx = torch.tensor([2], dtype=torch.int32, device=dev)
+    mean = torch.randn(59, device=dev, generator=g, dtype=torch.float64)
+    var = torch.rand(59, device=dev, generator=g, dtype=torch.float64) * 4
+    s = torch.cuda.current_stream().cuda_stream
+    x_ref = torch.zeros(rows, 72, device=dev, dtype=dt)
+    FU._check(L.ppo_obs_normalize(obs.data_ptr(), idx.data_ptr(), rows, 59, mean.data_ptr(), var.data_ptr(), 1e-5,
+                                  x_ref.data_ptr(), 64, 72, FU.PPO_DT[dt], s), "ppo_obs_normalize")
+    ws = [(torch.randn(256, 64 if i == 0 else 256, device=dev, generator=g) / 16).to(dt) for i in range(5)]
+    bs = [torch.randn(256, device=dev, generator=g) * 0.1 for _ in range(5)]
+    wh, bh = torch.randn(22, 256, device=dev, generator=g) / 16, torch.zeros(22, device=dev)
+    outs = []
+    for fused_in in (False, True):
+        x_out = torch.zeros(rows, 72, device=dev, dtype=dt)
+        hs = [torch.zeros(rows, 264, device=dev, dtype=dt) for _ in range(4)]
+        h5 = torch.zeros(rows, 256, device=dev)
+        head = torch.zeros(rows, 22, device=dev)
+        a = FU.PpoMlpFwd()
+        for i in range(5):
+            a.w[i], a.b[i] = ws[i].data_ptr(), bs[i].data_ptr()
+        for i in range(4):
+            a.h[i] = hs[i].data_ptr()
+        a.wh, a.bh, a.h5, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), h5.data_ptr(), head.data_ptr(), rows, 22
+        a.x_stride, a.h_stride, a.dtype = 72, 264, FU.PPO_DT[dt]
+        if fused_in:
+            a.obs, a.mb_idx, a.mean, a.var, a.eps, a.obs_dim = (obs.data_ptr(), idx.data_ptr(), mean.data_ptr(),
+                                                                var.data_ptr(), 1e-5, 59)
+            a.x_out = x_out.data_ptr()
+        else:
+            a.x = x_ref.data_ptr()
+        FU._check(L.ppo_mlp_forward(C.byref(a), s), "ppo_mlp_forward")
+        torch.cuda.synchronize()
+        outs.append((x_out.clone(), [t.clone() for t in hs], h5.clone(), head.clone()))
+    (_, h_a, h5_a, hd_a), (x_b, h_b, h5_b, hd_b) = outs
+    assert torch.equal(x_b[:, :64], x_ref[:, :64])
+    assert all(torch.equal(p, q) for p, q in zip(h_a, h_b)) and torch.equal(h5_a, h5_b) and torch.equal(hd_a, hd_b)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rows,splits,dt", [(32768, 32, torch.bfloat16), (1000, 3, torch.bfloat16),
                                             (64, 1, torch.bfloat16), (32768, 32, torch.float16),
                                             (1000, 3, torch.float16)])
