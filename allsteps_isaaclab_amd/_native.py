@@ -231,7 +231,7 @@ def hbm_copy_bandwidth(device, nbytes: int = 2 << 30, iters: int = 20) -> float:
 # code cost more register moves than they save (launch -2 %); the packed math that pays
 # (sweep, W rows) is written out as 2-vectors
 STEP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-I", INCLUDE]
-PPO_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-I", INCLUDE]
+PPO_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-I", INCLUDE]
 
 
 def build_native(verbose: bool = False) -> str:

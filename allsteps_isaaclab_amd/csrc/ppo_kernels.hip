@@ -217,94 +217,89 @@ __global__ void __launch_bounds__(kNormCols * kNormRowThreads) k_obs_normalize(
 
 // ------------------------------------------------------------------------------ PPO losses
 
-constexpr int kLossThreads = 256;
-
 // gradient of max(u1, u2) (torch.maximum: ties split the gradient in half)
 __device__ __forceinline__ float max_grad(float u1, float u2, float g1, float g2) {
     return u1 > u2 ? g1 : (u2 > u1 ? g2 : 0.5f * (g1 + g2));
 }
 
-// One row per 32-lane group: lane j < A owns action j, lane A owns the value; row sums by xor
-// shuffles inside the group.  Loads of a row's A floats are contiguous across lanes (coalesced).
-// Each lane keeps running sums for its own column over the rows its group visits.
-constexpr int kLossRowsPerGroup = 4;
+// One row per lane (round 5; the round-4 form spread a row over a 32-lane group and summed it with
+// shuffles, leaving 10 of 32 lanes idle and the row sums as chains of LDS-routed permutes): a block of
+// kLossRows lanes stages its rows of the dataset (actions, mu, sigma: A floats each) and of the heads
+// through LDS with coalesced loads, each lane then runs its row's action loop in registers, and the
+// per-row contributions to the column sums land in an LDS table that kNV threads sum down in a fixed
+// order (deterministic).  Row pitches in LDS are odd (in dwords), so the row-per-lane reads are
+// conflict-free.
+constexpr int kLossRows = 128;
 
 template <int A>
-__global__ void __launch_bounds__(kLossThreads) k_loss_grad(
+__global__ void __launch_bounds__(kLossRows) k_loss_grad(
     const float* __restrict__ head, const float* __restrict__ logstd, int mb_rows, const int32_t* __restrict__ mb_idx,
     const float* __restrict__ actions, float* __restrict__ ds_mu, float* __restrict__ ds_sigma,
     const float* __restrict__ old_nlp, const float* __restrict__ adv_, const float* __restrict__ old_v,
     const float* __restrict__ ret_, ppo_loss_cfg_t cfg, const float* __restrict__ grad_scale, float* __restrict__ dhead,
-    float* __restrict__ partials) {
-    static_assert(A + 1 <= 32, "one 32-lane group per row");
+    float* __restrict__ partials, uint16_t* __restrict__ dhead_lp, int lp_dtype) {
+    static_assert(A + 1 <= 32, "heads of at most 32 outputs");
     constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
-    constexpr int G = kLossThreads / 32;
-    __shared__ float red[G][NV];
-    const int j = threadIdx.x % 32, grp = threadIdx.x / 32;
+    constexpr int AP = A | 1, HP = (A + 1) | 1, RP = NV | 1;
+    __shared__ float s_act[kLossRows * AP], s_mu[kLossRows * AP], s_sig[kLossRows * AP], s_head[kLossRows * HP];
+    __shared__ float s_red[kLossRows * RP];
+    __shared__ float s_sg[A], s_ls[A];
+    const int tid = threadIdx.x;
+    const int r0 = blockIdx.x * kLossRows;
+    const int nr = min(kLossRows, mb_rows - r0);
+    const int64_t base = int64_t(*mb_idx) * mb_rows + r0;  // dataset row of the block's row 0
+    for (int e = tid; e < nr * A; e += kLossRows) {
+        const int r = e / A, c = e - r * A;
+        s_act[r * AP + c] = actions[base * A + e];
+        s_mu[r * AP + c] = ds_mu[base * A + e];
+        s_sig[r * AP + c] = ds_sigma[base * A + e];
+    }
+    for (int e = tid; e < nr * (A + 1); e += kLossRows) {
+        const int r = e / (A + 1), c = e - r * (A + 1);
+        s_head[r * HP + c] = head[int64_t(r0) * (A + 1) + e];
+    }
+    if (tid < A) {
+        s_ls[tid] = logstd[tid];
+        s_sg[tid] = expf(logstd[tid]);
+    }
+    __syncthreads();
     // the loss scale (a power of two, GradScaler) enters every gradient through the 1/B factor: exact
     const float inv_b = (grad_scale ? *grad_scale : 1.f) * (1.f / float(mb_rows));
-    const int64_t base = int64_t(*mb_idx) * mb_rows;
-    const bool act_lane = j < A;
-    const float ls = act_lane ? logstd[j] : 0.f;
-    const float sg = expf(ls);
-    float sum_ls = ls;
+    float sum_ls = 0.f;
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) sum_ls += __shfl_xor(sum_ls, o, 32);
+    for (int j = 0; j < A; ++j) sum_ls += s_ls[j];
     const float entropy = float(A) * (0.5f + 0.5f * kLog2Pi) + sum_ls;
-    float acc_mu = 0.f, acc_ls = 0.f, acc_v = 0.f;
-    float st_a = 0.f, st_c = 0.f, st_b = 0.f, st_e = 0.f, st_k = 0.f;
-    const int r_begin = (blockIdx.x * G + grp) * kLossRowsPerGroup;
-    // every row's inputs loaded first (one memory round trip for the group's rows, not one per row)
-    constexpr int R = kLossRowsPerGroup;
-    float hjv[R], av[R], m1v[R], s1v[R], onlp[R], advv[R], ovv[R], retv[R];
-#pragma unroll
-    for (int rr = 0; rr < R; ++rr) {
-        const int r = r_begin + rr;
-        const bool ok = r < mb_rows;  // uniform across the group
-        const int64_t row = base + (ok ? r : 0);
-        hjv[rr] = ok && j <= A ? head[int64_t(r) * (A + 1) + j] : 0.f;  // mu_j, or the value on lane A
-        av[rr] = ok && act_lane ? actions[row * A + j] : 0.f;
-        m1v[rr] = ok && act_lane ? ds_mu[row * A + j] : 0.f;
-        s1v[rr] = ok && act_lane ? ds_sigma[row * A + j] : 1.f;
-        onlp[rr] = ok ? old_nlp[row] : 0.f;
-        advv[rr] = ok ? adv_[row] : 0.f;
-        ovv[rr] = ok && j == A ? old_v[row] : 0.f;
-        retv[rr] = ok && j == A ? ret_[row] : 0.f;
-    }
-#pragma unroll
-    for (int rr = 0; rr < R; ++rr) {
-        const int r = r_begin + rr;
-        if (r >= mb_rows) break;  // uniform across the group
+    const int r = tid;
+    float* red = s_red + r * RP;
+    if (r < nr) {
         const int64_t row = base + r;
-        const float hj = hjv[rr];
-        float d = 0.f, klj = 0.f, blj = 0.f, dbj = 0.f;
-        if (act_lane) {
-            d = (av[rr] - hj) / sg;
-            const float m1 = m1v[rr], s1 = s1v[rr];
-            const float dm = m1 - hj;
-            // policy_kl(p0 = current, p1 = dataset)
-            klj = logf(s1 / sg + 1e-5f) + (sg * sg + dm * dm) / (2.f * (s1 * s1 + 1e-5f)) - 0.5f;
+        const float* hr = s_head + r * HP;
+        const float* ar = s_act + r * AP;
+        float* mr = s_mu + r * AP;
+        const float* sr = s_sig + r * AP;
+        // policy: d_j = (a_j - mu_j) / sigma_j; nlp = 0.5 sum d^2 + 0.5 log(2 pi) A + sum logstd;
+        // policy_kl(p0 = current, p1 = dataset); the bound loss
+        float d[A];
+        float q = 0.f, kl = 0.f, bl = 0.f;
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            const float hj = hr[j], sg = s_sg[j], s1 = sr[j];
+            d[j] = (ar[j] - hj) / sg;
+            q += d[j] * d[j];
+            const float dm = mr[j] - hj;
+            kl += logf(s1 / sg + 1e-5f) + (sg * sg + dm * dm) / (2.f * (s1 * s1 + 1e-5f)) - 0.5f;
             if (cfg.bound_loss == 1) {
                 const float lo = fminf(hj + cfg.soft_bound, 0.f), hi = fmaxf(hj - cfg.soft_bound, 0.f);
-                blj = lo * lo + hi * hi;
-                dbj = 2.f * (lo + hi);
+                bl += lo * lo + hi * hi;
             } else if (cfg.bound_loss == 2) {
-                blj = hj * hj;
-                dbj = 2.f * hj;
+                bl += hj * hj;
             }
         }
-        float q = d * d, kl = klj, bl = blj;
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) {
-            q += __shfl_xor(q, o, 32);
-            kl += __shfl_xor(kl, o, 32);
-            bl += __shfl_xor(bl, o, 32);
-        }
         const float nlp = 0.5f * q + 0.5f * kLog2Pi * float(A) + sum_ls;
-        const float adv = advv[rr];
+        const float adv = adv_[row];
         float a_loss, g_nlp;
         if (cfg.ppo) {
-            const float ratio = expf(onlp[rr] - nlp);
+            const float ratio = expf(old_nlp[row] - nlp);
             const float rc = fminf(fmaxf(ratio, 1.f - cfg.e_clip), 1.f + cfg.e_clip);
             const float u1 = -adv * ratio, u2 = -adv * rc;
             const bool inside = ratio >= 1.f - cfg.e_clip && ratio <= 1.f + cfg.e_clip;
@@ -316,63 +311,85 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
             g_nlp = adv;
         }
         g_nlp *= inv_b;
-        float* dh = dhead + int64_t(r) * (A + 1);
-        if (act_lane) {
-            // d nlp / d mu = -d / sigma ; d nlp / d logstd = 1 - d^2
-            const float gmu = -g_nlp * d / sg + cfg.bounds_coef * inv_b * dbj;
-            dh[j] = gmu;
-            acc_mu += gmu;
-            acc_ls += g_nlp * (1.f - d * d);
-            ds_mu[row * A + j] = hj;  // dataset.update_mu_sigma
-            ds_sigma[row * A + j] = sg;
-        } else if (j == A) {
-            const float v = hj, vp = ovv[rr], Rt = retv[rr];
-            float c_loss, g_v;
-            if (cfg.clip_value) {
-                const float dv = v - vp;
-                const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
-                const float l1 = (v - Rt) * (v - Rt), l2 = (vc - Rt) * (vc - Rt);
-                const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
-                g_v = max_grad(l1, l2, 2.f * (v - Rt), inside ? 2.f * (vc - Rt) : 0.f);
-                c_loss = fmaxf(l1, l2);
-            } else {
-                c_loss = (Rt - v) * (Rt - v);
-                g_v = 2.f * (v - Rt);
+        float gh[32];  // d loss / d head of this row, 0 past the value column
+#pragma unroll
+        for (int j = 0; j < 32; ++j) gh[j] = 0.f;
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            const float hj = hr[j], sg = s_sg[j];
+            float dbj = 0.f;
+            if (cfg.bound_loss == 1) {
+                const float lo = fminf(hj + cfg.soft_bound, 0.f), hi = fmaxf(hj - cfg.soft_bound, 0.f);
+                dbj = 2.f * (lo + hi);
+            } else if (cfg.bound_loss == 2) {
+                dbj = 2.f * hj;
             }
-            g_v *= 0.5f * cfg.critic_coef * inv_b;
-            dh[A] = g_v;
-            acc_v += g_v;
-            st_c += c_loss;
+            // d nlp / d mu = -d / sigma ; d nlp / d logstd = 1 - d^2
+            gh[j] = -g_nlp * d[j] / sg + cfg.bounds_coef * inv_b * dbj;
+            red[j] = gh[j];
+            red[A + 1 + j] = g_nlp * (1.f - d[j] * d[j]);
+            mr[j] = hj;  // dataset.update_mu_sigma (written out below, coalesced)
         }
-        if (j == 0) {
-            st_a += a_loss;
-            st_b += bl;
-            st_e += entropy;
-            st_k += kl;
+        // critic
+        const float v = hr[A], vp = old_v[row], Rt = ret_[row];
+        float c_loss, g_v;
+        if (cfg.clip_value) {
+            const float dv = v - vp;
+            const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
+            const float l1 = (v - Rt) * (v - Rt), l2 = (vc - Rt) * (vc - Rt);
+            const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
+            g_v = max_grad(l1, l2, 2.f * (v - Rt), inside ? 2.f * (vc - Rt) : 0.f);
+            c_loss = fmaxf(l1, l2);
+        } else {
+            c_loss = (Rt - v) * (Rt - v);
+            g_v = 2.f * (v - Rt);
         }
-    }
-    // block partials: column sums owned by lanes, statistics from lanes 0 / A
-    float* rg = red[grp];
-    if (act_lane) {
-        rg[j] = acc_mu;
-        rg[A + 1 + j] = acc_ls;
-    }
-    if (j == A) {
-        rg[A] = acc_v;
-        rg[2 * A + 1 + 1] = st_c;
-    }
-    if (j == 0) {
-        rg[2 * A + 1 + 0] = st_a;
-        rg[2 * A + 1 + 2] = st_b;
-        rg[2 * A + 1 + 3] = st_e;
-        rg[2 * A + 1 + 4] = st_k;
+        g_v *= 0.5f * cfg.critic_coef * inv_b;
+        gh[A] = g_v;
+        red[A] = g_v;
+        red[2 * A + 1 + 0] = a_loss;
+        red[2 * A + 1 + 1] = c_loss;
+        red[2 * A + 1 + 2] = bl;
+        red[2 * A + 1 + 3] = entropy;
+        red[2 * A + 1 + 4] = kl;
+        if (dhead) {
+            float* dh = dhead + int64_t(r0 + r) * (A + 1);
+#pragma unroll
+            for (int j = 0; j <= A; ++j) dh[j] = gh[j];
+        }
+        // the 16-bit copy (autocast: the gradient reaching the heads' fp16 Linear is fp16): 64 B per row
+        if (dhead_lp) {
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t lo = lp_dtype == PPO_DT_F16 ? f32_to_f16(gh[2 * k]) : f32_to_bf16(gh[2 * k]);
+                const uint32_t hi = lp_dtype == PPO_DT_F16 ? f32_to_f16(gh[2 * k + 1]) : f32_to_bf16(gh[2 * k + 1]);
+                w[k] = lo | (hi << 16);
+            }
+            uint4* dst = reinterpret_cast<uint4*>(dhead_lp + int64_t(r0 + r) * 32);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[k] = 0.f;
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < NV; k += kLossThreads) {
-        float t = 0.f;
+    // new mu / sigma into the dataset rows (coalesced)
+    for (int e = tid; e < nr * A; e += kLossRows) {
+        const int rr = e / A, c = e - rr * A;
+        ds_mu[base * A + e] = s_mu[rr * AP + c];
+        ds_sigma[base * A + e] = s_sg[c];
+    }
+    // block partials: column k summed over the block's rows in a fixed order (four chains)
+    if (tid < NV) {
+        float t[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+        for (int rr = 0; rr < kLossRows; rr += 4) {
 #pragma unroll
-        for (int g = 0; g < G; ++g) t += red[g][k];
-        partials[int64_t(blockIdx.x) * NV + k] = t;
+            for (int u = 0; u < 4; ++u) t[u] += s_red[(rr + u) * RP + tid];
+        }
+        partials[int64_t(blockIdx.x) * NV + tid] = (t[0] + t[1]) + (t[2] + t[3]);
     }
 }
 
@@ -657,6 +674,7 @@ __global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
 
 constexpr int kNormBlocks = 256;
 constexpr int kAdamThreads = 256;
+constexpr int kAdamBlocks = 512;  // two per CU
 
 // block partials of ||g / scale||^2 (partials[b]; NaN / inf propagate as in torch's vector_norm) and
 // of the non-finite element count (partials[gridDim.x + b]: GradScaler's found_inf, an OR over
@@ -740,24 +758,29 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     const float coef = coef_s;
     const float step_size = step_size_s;
     const float bc2_sqrt = bc2_sqrt_s;
-    const int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x;
-    if (i >= n || skip_s) return;
-    const float gi = (g[i] * inv_scale_s) * coef;
-    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    const float pi = p[i] - step_size * (mi / denom);
-    p[i] = pi;
-    if (mirror) {
-        for (int k = 0; k < segs.n; ++k) {
-            const ppo_seg_t& sg = segs.s[k];
-            if (i >= sg.off && i < sg.off + sg.len) {
-                const int64_t j = i - sg.off;
-                const int64_t r = j / sg.cols, c = j % sg.cols;
-                mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] =
-                    mirror_dtype == PPO_DT_F16 ? f32_to_f16(pi) : f32_to_bf16(pi);
+    const float inv_scale = inv_scale_s;
+    if (skip_s) return;
+    // grid-stride over the buffer: one resident block per CU pays the prologue above (the partial sums
+    // and thread 0's fp64 bias corrections) once, instead of once per 256 parameters in successive
+    // rounds of blocks
+    for (int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x; i < n; i += int64_t(gridDim.x) * kAdamThreads) {
+        const float gi = (g[i] * inv_scale) * coef;
+        const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
+        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        const float pi = p[i] - step_size * (mi / denom);
+        p[i] = pi;
+        if (mirror) {
+            for (int k = 0; k < segs.n; ++k) {
+                const ppo_seg_t& sg = segs.s[k];
+                if (i >= sg.off && i < sg.off + sg.len) {
+                    const int64_t j = i - sg.off;
+                    const int64_t r = j / sg.cols, c = j % sg.cols;
+                    mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] =
+                        mirror_dtype == PPO_DT_F16 ? f32_to_f16(pi) : f32_to_bf16(pi);
+                }
             }
         }
     }
@@ -843,21 +866,21 @@ int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, in
     return launched("k_obs_normalize");
 }
 
-int ppo_loss_blocks(int32_t mb_rows) {
-    const int rows_per_block = (kLossThreads / 32) * kLossRowsPerGroup;
-    return (mb_rows + rows_per_block - 1) / rows_per_block;
-}
+int ppo_loss_blocks(int32_t mb_rows) { return (mb_rows + kLossRows - 1) / kLossRows; }
 
 int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
                   const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
                   const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
-                  const float* grad_scale, float* dhead, float* partials, void* stream) {
-    const dim3 grid(ppo_loss_blocks(mb_rows)), block(kLossThreads);
+                  const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
+                  void* stream) {
+    if (dhead_lp && lp_dtype != PPO_DT_BF16 && lp_dtype != PPO_DT_F16)
+        return fail(-1, "ppo_loss_grad: dhead_lp needs lp_dtype PPO_DT_BF16 or PPO_DT_F16");
+    const dim3 grid(ppo_loss_blocks(mb_rows)), block(kLossRows);
 #define PPO_LOSS_CASE(AA)                                                                                        \
     case AA:                                                                                                     \
         hipLaunchKernelGGL(k_loss_grad<AA>, grid, block, 0, S(stream), head, logstd, mb_rows, mb_idx, actions, \
                            ds_mu, ds_sigma, old_neglogp, advantages, old_values, returns, cfg, grad_scale, dhead,  \
-                           partials);                                                                           \
+                           partials, dhead_lp, lp_dtype);                                                                           \
         break;
     switch (A) {
         PPO_LOSS_CASE(2)
@@ -990,7 +1013,8 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
         if (t.s[k].cols <= 0 || t.s[k].mstride < (t.s[k].trans ? rows : t.s[k].cols))
             return fail(-1, "ppo_adam: bad segment");
     }
-    hipLaunchKernelGGL(k_adam, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0, S(stream),
+    const int64_t want = (n + kAdamThreads - 1) / kAdamThreads;
+    hipLaunchKernelGGL(k_adam, dim3(unsigned(want < kAdamBlocks ? want : kAdamBlocks)), dim3(kAdamThreads), 0, S(stream),
                        p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
                        static_cast<uint16_t*>(mirror), mirror_dtype, scaler);
     return launched("k_adam");

@@ -244,8 +244,8 @@ __device__ __forceinline__ Rsrc rsrc(const void* p, int64_t bytes) {
 __device__ __forceinline__ u32x4_t u4(uint4 v) { return u32x4_t{v.x, v.y, v.z, v.w}; }
 
 // ELU (alpha 1) of one tile's fp32 values (bias already in the accumulator), one rounding to the 16-bit
-// type: the next layer's LDS image and, when STORE, the layer's global activations (and, LAST, the
-// fp32 values: h5).  Lane (j, h) holds row j, features F0 + feat(r, h).
+// type: the next layer's LDS image and, when STORE, the layer's global activations.  Lane (j, h) holds
+// row j, features F0 + feat(r, h).
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 // two fp32 values -> one dword of two 16-bit values (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32, round to
@@ -257,21 +257,23 @@ __device__ __forceinline__ uint32_t pack2(f32x2_t v) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, e2));
 }
 
-template <int DT, bool LAST, bool STORE>
-__device__ __forceinline__ void tile_epi(const f32x16& acc, uint16_t* Xn, int rl, int row, Rsrc rh, int h_stride, Rsrc r5,
-                                         int F0, int h) {
-    // ELU in pairs: one packed multiply by log2(e) and one packed add of -1 per two values around the two
-    // hardware exps (exp(z) - 1 = exp2(z log2 e) - 1, as __expf; |error| ~1e-7, far below the 16-bit step)
-    float y[16];
+template <int DT, bool STORE>
+__device__ __forceinline__ void tile_epi(const f32x16& acc, uint16_t* Xn, int rl, int row, Rsrc rh, int h_stride, int F0,
+                                         int h) {
+    // ELU(z) = med3(exp(z) - 1, z, 0): for z > 0 the three sort as 0 < z < e^z - 1, for z <= 0 as
+    // z <= e^z - 1 <= 0, so the median is z or e^z - 1 -- one v_med3_f32 instead of a compare + select
+    // (and its VCC hazard).  exp(z) - 1 = exp2(z log2 e) - 1 as __expf (|error| ~1e-7, far below the 16-bit
+    // step).  Scalar f32 ops only: packed f32 VALU costs extra issue cycles beside the MFMAs.
     uint32_t dw[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const f32x2_t z = {acc[2 * k], acc[2 * k + 1]};
-        const f32x2_t zl = z * f32x2_t{1.44269502f, 1.44269502f};
-        const f32x2_t em = f32x2_t{__builtin_amdgcn_exp2f(zl.x), __builtin_amdgcn_exp2f(zl.y)} - f32x2_t{1.f, 1.f};
-        y[2 * k] = z.x > 0.f ? z.x : em.x;
-        y[2 * k + 1] = z.y > 0.f ? z.y : em.y;
-        dw[k] = pack2<DT>(f32x2_t{y[2 * k], y[2 * k + 1]});
+        float y[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float z = acc[2 * k + e];
+            y[e] = __builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(z * 1.44269502f) - 1.f, z, 0.f);
+        }
+        dw[k] = pack2<DT>(f32x2_t{y[0], y[1]});
     }
 #if PPO_FWD_DBG & 2
 #pragma unroll
@@ -288,18 +290,9 @@ __device__ __forceinline__ void tile_epi(const f32x16& acc, uint16_t* Xn, int rl
     *reinterpret_cast<uint4*>(xn) = c01;
     *reinterpret_cast<uint4*>(xn + 16) = c23;
     if (STORE) {
-        if (!LAST) {  // layers 1..4 (16-bit); the fifth layer's values go out in fp32 only (h5)
-            const int off = (row * h_stride + F0 + 8 * h) * 2;
-            __builtin_amdgcn_raw_buffer_store_b128(u4(c01), rh, off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(u4(c23), rh, off + 32, 0, 0);
-        } else {
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    u32x4_t{__float_as_uint(y[4 * g]), __float_as_uint(y[4 * g + 1]), __float_as_uint(y[4 * g + 2]),
-                            __float_as_uint(y[4 * g + 3])},
-                    r5, (row * kHid + F0 + 8 * g + 4 * h) * 4, 0, 0);
-        }
+        const int off = (row * h_stride + F0 + 8 * h) * 2;
+        __builtin_amdgcn_raw_buffer_store_b128(u4(c01), rh, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u4(c23), rh, off + 32, 0, 0);
     }
 }
 
@@ -348,14 +341,14 @@ __device__ __forceinline__ void layer(const uint16_t* Xin, uint16_t* Xout, const
     for (int r = 0; r < 16; ++r) binit[r] = bv[r];
     const f32x16 c0 = mfma_tile<DT, NS>(Xin, wa, binit, 0, j, h);
     if (HAS_PREV)
-        tile_epi<DT, false, STORE>(pend, const_cast<uint16_t*>(Xin), 96 + j, row0 + 96 + j, rh_prev, h_stride, rh, F0, h);
+        tile_epi<DT, STORE>(pend, const_cast<uint16_t*>(Xin), 96 + j, row0 + 96 + j, rh_prev, h_stride, F0, h);
     const f32x16 c1 = mfma_tile<DT, NS>(Xin, wa, binit, 1, j, h);
-    tile_epi<DT, false, STORE>(c0, Xout, j, row0 + j, rh, h_stride, rh, F0, h);
+    tile_epi<DT, STORE>(c0, Xout, j, row0 + j, rh, h_stride, F0, h);
     const f32x16 c2 = mfma_tile<DT, NS>(Xin, wa, binit, 2, j, h);
-    tile_epi<DT, false, STORE>(c1, Xout, 32 + j, row0 + 32 + j, rh, h_stride, rh, F0, h);
+    tile_epi<DT, STORE>(c1, Xout, 32 + j, row0 + 32 + j, rh, h_stride, F0, h);
     __syncthreads();
     const f32x16 c3 = mfma_tile<DT, NS>(Xin, wa, binit, 3, j, h);
-    tile_epi<DT, false, STORE>(c2, Xout, 64 + j, row0 + 64 + j, rh, h_stride, rh, F0, h);
+    tile_epi<DT, STORE>(c2, Xout, 64 + j, row0 + 64 + j, rh, h_stride, F0, h);
     pend = c3;
     __syncthreads();
 }
@@ -413,10 +406,9 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
         }
     }
     const int hs = a.h_stride;
-    Rsrc rh[4], r5;
+    Rsrc rh[5];
 #pragma unroll
-    for (int l = 0; l < 4; ++l) rh[l] = rsrc(STORE ? a.h[l] : nullptr, STORE ? int64_t(rows) * hs * 2 : 0);
-    r5 = rsrc(STORE ? a.h5 : nullptr, STORE ? int64_t(rows) * kHid * 4 : 0);
+    for (int l = 0; l < 5; ++l) rh[l] = rsrc(STORE ? a.h[l] : nullptr, STORE ? int64_t(rows) * hs * 2 : 0);
     // Weight slices double-buffered in registers (wa / wb): layer l + 1's slice is requested at the start
     // of layer l, ahead of layer l's activation stores (a load waited for with vmcnt also waits for every
     // older store of the wave).  Bias vectors likewise one layer ahead.
@@ -438,26 +430,13 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     load_wa<DT, 16>(a.w[4], kHid, F0, i, h, wa);
     load_bias(a.b[4], F0, h, ba);
     layer<DT, 16, STORE, true>(X1, X0, wb, bb, pend, rh[2], rh[3], hs, row0, F0, j, h);
-    // the fifth layer: fp32 values too (h5); the heads' weights and biases fly under it
+    // the fifth layer; the heads' weights and biases fly under it
     if (wave < 4) load_wh<DT>(a.wh, a.nh, i, h, wb);
     float bhv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) bhv[r] = feat(r, h) < a.nh ? a.bh[feat(r, h)] : 0.f;
-    {
-        f32x16 binit;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) binit[r] = ba[r];
-        const f32x16 c0 = mfma_tile<DT, 16>(X0, wa, binit, 0, j, h);
-        tile_epi<DT, false, STORE>(pend, X0, 96 + j, row0 + 96 + j, rh[3], hs, r5, F0, h);
-        const f32x16 c1 = mfma_tile<DT, 16>(X0, wa, binit, 1, j, h);
-        tile_epi<DT, true, STORE>(c0, X1, j, row0 + j, rh[0], hs, r5, F0, h);
-        const f32x16 c2 = mfma_tile<DT, 16>(X0, wa, binit, 2, j, h);
-        tile_epi<DT, true, STORE>(c1, X1, 32 + j, row0 + 32 + j, rh[0], hs, r5, F0, h);
-        __syncthreads();
-        const f32x16 c3 = mfma_tile<DT, 16>(X0, wa, binit, 3, j, h);
-        tile_epi<DT, true, STORE>(c2, X1, 64 + j, row0 + 64 + j, rh[0], hs, r5, F0, h);
-        tile_epi<DT, true, STORE>(c3, X1, 96 + j, row0 + 96 + j, rh[0], hs, r5, F0, h);
-    }
+    layer<DT, 16, STORE, true>(X0, X1, wa, ba, pend, rh[3], rh[4], hs, row0, F0, j, h);
+    tile_epi<DT, STORE>(pend, X1, 96 + j, row0 + 96 + j, rh[4], hs, F0, h);
     __syncthreads();
     // ---- heads: wave w < 4 takes N-tile w; out = 16-bit(acc + 16-bit(bh)) as under autocast
     if (wave < 4 && a.head) {
@@ -476,7 +455,7 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
 
 template <int DT>
 __global__ void __launch_bounds__(kFThreads, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
-    // training stores layers 1..5 for the backward (every pointer set); the rollout form stores none
+    // training stores layers 1..5 for the backward (all five pointers set); the rollout form stores none
     if (a.h[0] && !(PPO_FWD_DBG & 4))
         mlp_fwd_body<DT, true>(a);
     else
@@ -486,56 +465,39 @@ __global__ void __launch_bounds__(kFThreads, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
 // ------------------------------------------------------------------------------ backward chain
 //
 // The forward's layout run backwards (weight-stationary, 8 waves, 128 rows, two LDS images): stage H
-// forms dh5 = Wh^T dhead for the wave's 32 features of layer 5 (exact-f32 `32x32x2f32` MFMAs, dhead and
-// Wh in fp32), then each stage l = 4..1 forms dh = W_l^T dz_l for the wave's 32 INPUT features of layer l
-// (the A fragments: rows of the 16-bit W_l^T mirror, in registers, loaded one stage ahead; the B
-// fragments: dz_l from LDS), and every epilogue turns dh into dz = dh * elu'(y) (y > 0 ? 1 : y + 1, the
-// output form) with y the layer's stored activations (16-bit; layer 5 in fp32), rounds it once, writes it
-// to the next stage's LDS image and to dz[l] for the weight gradients.  Same tile pipelining and barriers
-// as the forward.
+// forms dh5 = Wh^T dhead for the wave's 32 features of layer 5 (lp MFMAs with fp32 accumulation on the
+// 16-bit dhead and lp(Wh), as autocast runs the heads' Linear backward), then each stage l = 4..1 forms
+// dh = W_l^T dz_l for the wave's 32 INPUT features of layer l (the A fragments: rows of the 16-bit W_l^T
+// mirror, in registers, loaded one stage ahead; the B fragments: dz_l from LDS), and every epilogue turns
+// dh into dz = dh * elu'(y) (y > 0 ? 1 : y + 1, the output form) with y the layer's stored 16-bit
+// activations, rounds it once, writes it to the next stage's LDS image and to dz[l] for the weight
+// gradients.  Same tile pipelining and barriers as the forward.
 
-// y of tile rows for the wave's features F0 + feat(r, h): 16-bit activations (8 dwords) or fp32 (16 floats)
-template <bool Y32>
-struct YT;
-template <>
-struct YT<false> {
+// y of tile rows for the wave's features F0 + feat(r, h): 16-bit activations, 8 dwords
+struct YT {
     u32x2_t v[4];
 };
-template <>
-struct YT<true> {
-    u32x4_t v[4];
-};
 
-template <bool Y32>
-__device__ __forceinline__ YT<Y32> load_y(Rsrc ry, int row, int stride, int F0, int h) {
-    YT<Y32> y;
+__device__ __forceinline__ YT load_y(Rsrc ry, int row, int stride, int F0, int h) {
+    YT y;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        if constexpr (Y32)
-            y.v[g] = __builtin_amdgcn_raw_buffer_load_b128(ry, (row * stride + F0 + 8 * g + 4 * h) * 4, 0, 0);
-        else
-            y.v[g] = __builtin_amdgcn_raw_buffer_load_b64(ry, (row * stride + F0 + 8 * g + 4 * h) * 2, 0, 0);
-    }
+    for (int g = 0; g < 4; ++g) y.v[g] = __builtin_amdgcn_raw_buffer_load_b64(ry, (row * stride + F0 + 8 * g + 4 * h) * 2, 0, 0);
     return y;
 }
 
-template <int DT, bool Y32>
-__device__ __forceinline__ float y_at(const YT<Y32>& y, int r) {
+template <int DT>
+__device__ __forceinline__ float y_at(const YT& y, int r) {
     typedef typename Lp<DT>::e E;
-    if constexpr (Y32) {
-        return __uint_as_float(y.v[r >> 2][r & 3]);
-    } else {
-        const uint32_t d = y.v[r >> 2][(r & 3) >> 1];
-        const uint16_t u = (r & 1) ? uint16_t(d >> 16) : uint16_t(d & 0xffff);
-        return float(__builtin_bit_cast(E, u));
-    }
+    const uint32_t d = y.v[r >> 2][(r & 3) >> 1];
+    const uint16_t u = (r & 1) ? uint16_t(d >> 16) : uint16_t(d & 0xffff);
+    return float(__builtin_bit_cast(E, u));
 }
 
 // dz of one tile: dh * elu'(y) in fp32, one rounding; into the next stage's LDS image and dz (global,
 // rows x 256, range-checked)
-template <int DT, bool Y32>
-__device__ __forceinline__ void tile_bepi(const f32x16& dh, const YT<Y32>& y, uint16_t* Xn, int rl, int row, Rsrc rdz,
-                                          int F0, int h) {
+template <int DT>
+__device__ __forceinline__ void tile_bepi(const f32x16& dh, const YT& y, uint16_t* Xn, int rl, int row, Rsrc rdz, int F0,
+                                          int h) {
     uint32_t dw[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -543,8 +505,9 @@ __device__ __forceinline__ void tile_bepi(const f32x16& dh, const YT<Y32>& y, ui
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             const int r = 2 * k + e;
-            const float yy = y_at<DT, Y32>(y, r);
-            v[e] = yy > 0.f ? dh[r] : dh[r] * (yy + 1.f);
+            // elu'(y) = y > 0 ? 1 : y + 1 = min(y + 1, 1) = clamp(y + 1, 0, 1) for ELU outputs (y >= -1):
+            // one v_add_f32 with the clamp modifier; dh * 1 is dh, so the value is the select's exactly
+            v[e] = dh[r] * __builtin_amdgcn_fmed3f(y_at<DT>(y, r) + 1.f, 0.f, 1.f);
         }
         dw[k] = pack2<DT>(f32x2_t{v[0], v[1]});
     }
@@ -560,25 +523,26 @@ __device__ __forceinline__ void tile_bepi(const f32x16& dh, const YT<Y32>& y, ui
 
 // stage l = 4..1: dh = W_l^T dz_l (Xin) for the wave's input features, epilogue against y (layer l - 1's
 // activations, ry) into Xout and dz[l - 1]; phase 0 also finishes the previous stage's tile 3 (pend,
-// against ypend, into Xin rows 96..127 and dz[l])
-template <int DT, bool YP32>
+// against ypend, into Xin rows 96..127 and dz[l]); HAS_PREV = false for the first stage (stage H
+// completed all four of its tiles)
+template <int DT, bool HAS_PREV>
 __device__ __forceinline__ void bstage(const uint16_t* Xin, uint16_t* Xout, const typename Lp<DT>::v8 (&wa)[16],
-                                       f32x16& pend, YT<YP32>& ypend, Rsrc rdz_prev, Rsrc ry, int y_stride, Rsrc rdz,
-                                       YT<false>& ynext, int row0, int F0, int j, int h) {
+                                       f32x16& pend, YT& yp, Rsrc rdz_prev, Rsrc ry, int y_stride, Rsrc rdz, int row0,
+                                       int F0, int j, int h) {
     const f32x16 zero = {};
-    YT<false> y0 = load_y<false>(ry, row0 + j, y_stride, F0, h);
+    YT y0 = load_y(ry, row0 + j, y_stride, F0, h);
     const f32x16 c0 = mfma_tile<DT, 16>(Xin, wa, zero, 0, j, h);
-    tile_bepi<DT, YP32>(pend, ypend, const_cast<uint16_t*>(Xin), 96 + j, row0 + 96 + j, rdz_prev, F0, h);
-    YT<false> y1 = load_y<false>(ry, row0 + 32 + j, y_stride, F0, h);
+    if (HAS_PREV) tile_bepi<DT>(pend, yp, const_cast<uint16_t*>(Xin), 96 + j, row0 + 96 + j, rdz_prev, F0, h);
+    YT y1 = load_y(ry, row0 + 32 + j, y_stride, F0, h);
     const f32x16 c1 = mfma_tile<DT, 16>(Xin, wa, zero, 1, j, h);
-    tile_bepi<DT, false>(c0, y0, Xout, j, row0 + j, rdz, F0, h);
-    YT<false> y2 = load_y<false>(ry, row0 + 64 + j, y_stride, F0, h);
+    tile_bepi<DT>(c0, y0, Xout, j, row0 + j, rdz, F0, h);
+    YT y2 = load_y(ry, row0 + 64 + j, y_stride, F0, h);
     const f32x16 c2 = mfma_tile<DT, 16>(Xin, wa, zero, 2, j, h);
-    tile_bepi<DT, false>(c1, y1, Xout, 32 + j, row0 + 32 + j, rdz, F0, h);
-    __syncthreads();
-    ynext = load_y<false>(ry, row0 + 96 + j, y_stride, F0, h);
+    tile_bepi<DT>(c1, y1, Xout, 32 + j, row0 + 32 + j, rdz, F0, h);
+    if (HAS_PREV) __syncthreads();
+    yp = load_y(ry, row0 + 96 + j, y_stride, F0, h);
     const f32x16 c3 = mfma_tile<DT, 16>(Xin, wa, zero, 3, j, h);
-    tile_bepi<DT, false>(c2, y2, Xout, 64 + j, row0 + 64 + j, rdz, F0, h);
+    tile_bepi<DT>(c2, y2, Xout, 64 + j, row0 + 64 + j, rdz, F0, h);
     pend = c3;
     __syncthreads();
 }
@@ -586,6 +550,7 @@ __device__ __forceinline__ void bstage(const uint16_t* Xin, uint16_t* Xout, cons
 template <int DT>
 __global__ void __launch_bounds__(kFThreads, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
     typedef typename Lp<DT>::v8 V8;
+    typedef typename Lp<DT>::e E;
     extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
     uint16_t* X0 = lds;
     uint16_t* X1 = lds + kFRows * kXs;
@@ -594,70 +559,53 @@ __global__ void __launch_bounds__(kFThreads, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
     const int F0 = 32 * wave;
     const int row0 = blockIdx.x * kFRows;
     const int rows = a.rows, nh = a.nh, hs = a.h_stride;
-    Rsrc rdz[5], rh[4];
+    Rsrc rdz[5], rh[5];
 #pragma unroll
     for (int l = 0; l < 5; ++l) rdz[l] = rsrc(a.dz[l], int64_t(rows) * kHid * 2);
 #pragma unroll
-    for (int l = 0; l < 4; ++l) rh[l] = rsrc(a.h[l], int64_t(rows) * hs * 2);
-    const Rsrc r5 = rsrc(a.h5, int64_t(rows) * kHid * 4);
-    const Rsrc rdh = rsrc(a.dhead, int64_t(rows) * nh * 4);
-    // ---- stage H: dh5 = Wh^T dhead (f32 MFMA: A[i][k] = wh[k][F0 + i], k = 2s + h; B[k][n] = dhead[n][k])
-    float ah[16];
+    for (int l = 0; l < 5; ++l) rh[l] = rsrc(a.h[l], int64_t(rows) * hs * 2);
+    const Rsrc rdh = rsrc(a.dhead, int64_t(rows) * 32 * 2);
+    // ---- stage H: dh5 = Wh^T dhead (A[i][k] = lp(wh[k][F0 + i]), k = 16s + 8h + e; B[k][n] = dhead[n][k])
+    V8 ah[2];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        const int k = 2 * s + h;
-        ah[s] = k < nh ? a.wh[k * kHid + F0 + i] : 0.f;
-    }
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = 16 * s + 8 * h + e;
+            ah[s][e] = (E)(k < nh ? a.wh[k * kHid + F0 + i] : 0.f);
+        }
     V8 wa[16], wb[16];
-    load_wa<DT, 16>(a.wt[3], kHid, F0, i, h, wa);  // W_4^T, the first 16-bit stage's slice
-    YT<true> y5[4];
+    load_wa<DT, 16>(a.wt[3], kHid, F0, i, h, wa);  // W_4^T, the first hidden stage's slice
+    YT y5[4];
     f32x16 dh5[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const int row = row0 + 32 * t + j;
-        y5[t] = load_y<true>(r5, row, kHid, F0, h);
-        float bq[16];
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const int k = 2 * s + h;
-            bq[s] = k < nh ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdh, (row * nh + k) * 4, 0, 0)) : 0.f;
-        }
+        y5[t] = load_y(rh[4], row, hs, F0, h);
         f32x16 c = {};
 #pragma unroll
-        for (int s = 0; s < 16; ++s)
-            if (2 * s < nh) c = __builtin_amdgcn_mfma_f32_32x32x2f32(ah[s], bq[s], c, 0, 0, 0);  // uniform
+        for (int s = 0; s < 2; ++s) {
+            if (16 * s < nh) {  // uniform
+                const u32x4_t q = __builtin_amdgcn_raw_buffer_load_b128(rdh, (row * 32 + 16 * s + 8 * h) * 2, 0, 0);
+                c = Lp<DT>::mma(ah[s], __builtin_bit_cast(V8, q), c);
+            }
+        }
         dh5[t] = c;
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) tile_bepi<DT, true>(dh5[t], y5[t], X0, 32 * t + j, row0 + 32 * t + j, rdz[4], F0, h);
+    for (int t = 0; t < 4; ++t) tile_bepi<DT>(dh5[t], y5[t], X0, 32 * t + j, row0 + 32 * t + j, rdz[4], F0, h);
     __syncthreads();
     // ---- stages 4..1 (dz_l in the LDS image -> dz_{l-1}); the next stage's W^T slice flies under each
     f32x16 pend = {};
-    YT<false> yp;
-    {
-        load_wa<DT, 16>(a.wt[2], kHid, F0, i, h, wb);
-        // stage 4: stage H completed all four of its tiles, so there is no pending tile to finish here
-        const f32x16 zero = {};
-        YT<false> y0 = load_y<false>(rh[3], row0 + j, hs, F0, h);
-        const f32x16 c0 = mfma_tile<DT, 16>(X0, wa, zero, 0, j, h);
-        YT<false> y1 = load_y<false>(rh[3], row0 + 32 + j, hs, F0, h);
-        const f32x16 c1 = mfma_tile<DT, 16>(X0, wa, zero, 1, j, h);
-        tile_bepi<DT, false>(c0, y0, X1, j, row0 + j, rdz[3], F0, h);
-        YT<false> y2 = load_y<false>(rh[3], row0 + 64 + j, hs, F0, h);
-        const f32x16 c2 = mfma_tile<DT, 16>(X0, wa, zero, 2, j, h);
-        tile_bepi<DT, false>(c1, y1, X1, 32 + j, row0 + 32 + j, rdz[3], F0, h);
-        yp = load_y<false>(rh[3], row0 + 96 + j, hs, F0, h);
-        const f32x16 c3 = mfma_tile<DT, 16>(X0, wa, zero, 3, j, h);
-        tile_bepi<DT, false>(c2, y2, X1, 64 + j, row0 + 64 + j, rdz[3], F0, h);
-        pend = c3;
-        __syncthreads();
-    }
+    YT yp;
+    load_wa<DT, 16>(a.wt[2], kHid, F0, i, h, wb);
+    bstage<DT, false>(X0, X1, wa, pend, yp, rdz[4], rh[3], hs, rdz[3], row0, F0, j, h);
     load_wa<DT, 16>(a.wt[1], kHid, F0, i, h, wa);
-    bstage<DT, false>(X1, X0, wb, pend, yp, rdz[3], rh[2], hs, rdz[2], yp, row0, F0, j, h);
+    bstage<DT, true>(X1, X0, wb, pend, yp, rdz[3], rh[2], hs, rdz[2], row0, F0, j, h);
     load_wa<DT, 16>(a.wt[0], kHid, F0, i, h, wb);
-    bstage<DT, false>(X0, X1, wa, pend, yp, rdz[2], rh[1], hs, rdz[1], yp, row0, F0, j, h);
-    bstage<DT, false>(X1, X0, wb, pend, yp, rdz[1], rh[0], hs, rdz[0], yp, row0, F0, j, h);
-    tile_bepi<DT, false>(pend, yp, X0, 96 + j, row0 + 96 + j, rdz[0], F0, h);
+    bstage<DT, true>(X0, X1, wa, pend, yp, rdz[2], rh[1], hs, rdz[1], row0, F0, j, h);
+    bstage<DT, true>(X1, X0, wb, pend, yp, rdz[1], rh[0], hs, rdz[0], row0, F0, j, h);
+    tile_bepi<DT>(pend, yp, X0, 96 + j, row0 + 96 + j, rdz[0], F0, h);
 }
 
 }  // namespace
@@ -677,8 +625,11 @@ static int reserve_lds(F kernel, int bytes, bool& done, const char* what) {
 }
 
 extern "C" int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream) {
-    if (!args_host || !args_host->dhead || args_host->nh <= 0 || args_host->nh > 32 || args_host->rows <= 0 ||
-        args_host->h_stride < kHid || (args_host->dtype != PPO_DT_BF16 && args_host->dtype != PPO_DT_F16)) {
+    bool ok = args_host && args_host->dhead && args_host->wh && args_host->nh > 0 && args_host->nh <= 32 &&
+              args_host->rows > 0 && args_host->h_stride >= kHid && args_host->h_stride % 8 == 0 &&
+              (args_host->dtype == PPO_DT_BF16 || args_host->dtype == PPO_DT_F16);
+    for (int l = 0; ok && l < 5; ++l) ok = args_host->h[l] && args_host->dz[l] && (l == 4 || args_host->wt[l]);
+    if (!ok) {
         snprintf(g_err, sizeof(g_err), "ppo_mlp_backward: bad arguments");
         ppo_detail::set_error(g_err);
         return -1;
@@ -709,7 +660,9 @@ extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
         (args_host->obs && (!args_host->mb_idx || !args_host->mean || !args_host->var || args_host->obs_dim <= 0 ||
                             args_host->obs_dim > kK0)) ||
         args_host->x_stride < kK0 || args_host->h_stride < kHid || (args_host->x_stride % 8) || (args_host->h_stride % 8) ||
-        (args_host->dtype != PPO_DT_BF16 && args_host->dtype != PPO_DT_F16)) {
+        (args_host->dtype != PPO_DT_BF16 && args_host->dtype != PPO_DT_F16) ||
+        // the activations are stored all five or not at all (the rollout form)
+        (args_host->h[0] && !(args_host->h[1] && args_host->h[2] && args_host->h[3] && args_host->h[4]))) {
         snprintf(g_err, sizeof(g_err), "ppo_mlp_forward: bad arguments");
         ppo_detail::set_error(g_err);
         return -1;

@@ -1,19 +1,27 @@
-// ppo_wgrad.hip -- split-K weight and bias gradients of the five trunk layers in one MFMA launch
-// (include/ppo.h ppo_weight_grads).
+// ppo_wgrad.hip -- split-K weight and bias gradients of the five trunk layers and the head weights in
+// one MFMA launch (include/ppo.h ppo_weight_grads).
 //
-// For layer l, split s:  part[s][o][c] = sum_{b in rows of s} dz[b][o] * hin[b][c]   (c < kin)
-//                        part[s][o][kin] = sum_{b in rows of s} dz[b][o]             (bias column)
-// which is the (S, 256, stride) fp32 block the five torch.bmm calls produced before, so the single
-// deterministic reduce launch (ppo_reduce_rows) that sums the S partials stays as it was.
+// For job l, split s:  part[s][o][c]   = sum_{b in rows of s} dz[b][o] * hin[b][c]   (c < kin)
+//                      part[s][o][kin] = sum_{b in rows of s} dz[b][o]             (bias column, trunk)
+// the (S, nout, stride) fp32 blocks that ONE deterministic reduce launch (ppo_reduce_rows) sums.
 //
 // Both operands are batch-major ([row][feature], as the forward / backward kernels write them) while
 // the MFMA wants 8 consecutive k (= batch rows) per lane: a workgroup stages 64 rows of dz and of the
 // layer input into LDS in that same row-major form and reads the operands with ds_read_b64_tr_b16,
 // which hands every lane one feature column of a 4-row block.  Rows are padded to a pitch whose
-// 4-row blocks fall on disjoint banks, so the transposed reads are conflict-free.  One workgroup
-// (8 waves) owns the whole 256 x kin output of its row range, so every input byte is read once;
-// the register prefetch of the next 64 rows overlaps the MFMAs of the current ones (LDS double
-// buffer, one barrier per stage).
+// 4-row blocks fall on disjoint banks, so the transposed reads are conflict-free.  The register
+// prefetch of the next 64 rows overlaps the MFMAs of the current ones (LDS double buffer, one barrier
+// per stage).
+//
+// Work split (round 5).  The kernel streams ~170 MB per 32768-row minibatch (dz of five layers, their
+// inputs, the head gradient and layer 5), so it is bound by HBM / Infinity-Cache bandwidth, which a
+// chip-wide stream only reaches with every CU pulling its share (~24-33 GB/s per CU): the workgroups
+// must cover all 256 CUs.  Splitting K (rows) finer costs partials (each split writes a full 256 x 264
+// fp32 block, which the reduce reads back); so a trunk split is instead TWO workgroups, output
+// features 0..127 and 128..255, each reading its half of dz and the whole layer input -- placed 8 block
+// indices apart so that both land on the same XCD at the same time (blocks are dealt to the XCDs
+// round-robin) and the input they both stream is fetched from memory once into that XCD's L2.  The
+// head gradient (dhead, 32 columns, against layer 5) is one more job of single workgroups.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -33,16 +41,20 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int kOut = 256;                // output features of every trunk layer
+constexpr int kHeadOut = 32;             // the head job's output rows (dhead columns, nh <= 32)
+constexpr int kOG = 128;                 // output features of one trunk workgroup
 constexpr int kWaves = 8;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kKT = 64;                  // batch rows per stage
-constexpr int kPitchDz = kOut * 2 + 64;  // bytes: 576 = 144 dwords, +16 banks per row (mod 64)
-constexpr int kPitchH256 = 256 * 2 + 64;
-constexpr int kPitchH64 = 64 * 2 + 64;   // 192 B = 48 dwords: rows on banks 0, 48, 32, 16 (+16 each)
-constexpr int kStageDz = kKT * kPitchDz;
+// row pitches in bytes: +16 banks per row (mod 64), so the four rows of a transposed read are disjoint
+constexpr int kPitchD128 = kOG * 2 + 64;       // 320 B = 80 dwords
+constexpr int kPitchD32 = kHeadOut * 2;        // 64 B = 16 dwords
+constexpr int kPitchH256 = 256 * 2 + 64;       // 576 B = 144 dwords
+constexpr int kPitchH64 = 64 * 2 + 64;         // 192 B = 48 dwords: rows on banks 0, 48, 32, 16 (+16 each)
+constexpr int kStageD = kKT * kPitchD128;
 constexpr int kStageH = kKT * kPitchH256;
-constexpr int kStage = kStageDz + kStageH;
-constexpr int kLdsBytes = 2 * kStage;    // 147456 B (one workgroup per CU)
+constexpr int kStage = kStageD + kStageH;
+constexpr int kLdsBytes = 2 * kStage;    // 114688 B (one workgroup per CU)
 
 char g_err[256];
 
@@ -96,130 +108,165 @@ __device__ __forceinline__ typename Lp<DT>::v8 tr_frag(const char* img, int pitc
     return f.v;
 }
 
-// stage loads: rows [r0, r0 + kKT) of a [rows][stride] 16-bit matrix, columns [0, cols); rows past
+// stage loads: rows [r0, r0 + kKT) of a [rows][stride] 16-bit matrix, columns [c0, c0 + COLS); rows past
 // `rend` are zero (the pad rows then add nothing to the MFMA sums)
 template <int COLS>
 struct Stager {
     static constexpr int kChunksPerRow = COLS * 2 / 16;
-    static constexpr int kPer = kKT * kChunksPerRow / kThreads;
-    static_assert(kPer >= 1 && kKT * kChunksPerRow % kThreads == 0, "stage split");
+    static constexpr int kTotal = kKT * kChunksPerRow;
+    static constexpr int kPer = (kTotal + kThreads - 1) / kThreads;
     uint4 v[kPer];
-    __device__ __forceinline__ void load(const uint16_t* __restrict__ src, int stride, int r0, int rend) {
+    __device__ __forceinline__ void load(const uint16_t* __restrict__ src, int stride, int c0, int r0, int rend) {
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
             const int c = u * kThreads + threadIdx.x;
             const int r = r0 + c / kChunksPerRow;
-            v[u] = r < rend ? *reinterpret_cast<const uint4*>(src + int64_t(r) * stride + (c % kChunksPerRow) * 8)
-                            : make_uint4(0, 0, 0, 0);
+            v[u] = (kTotal % kThreads == 0 || c < kTotal) && r < rend
+                       ? *reinterpret_cast<const uint4*>(src + int64_t(r) * stride + c0 + (c % kChunksPerRow) * 8)
+                       : make_uint4(0, 0, 0, 0);
         }
     }
     __device__ __forceinline__ void store(char* img, int pitch) const {
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
             const int c = u * kThreads + threadIdx.x;
-            *reinterpret_cast<uint4*>(img + (c / kChunksPerRow) * pitch + (c % kChunksPerRow) * 16) = v[u];
+            if (kTotal % kThreads == 0 || c < kTotal)
+                *reinterpret_cast<uint4*>(img + (c / kChunksPerRow) * pitch + (c % kChunksPerRow) * 16) = v[u];
         }
     }
 };
 
-// KIN input features: 256 (trunk layers, 8 column tiles: wave = 2 o-blocks of 4 tiles x 4 c-blocks
-// of 2 tiles) or 64 (layer 0: 2 column tiles, wave = one o-tile x both c-tiles).  The bias sums of
-// o-tile obase + cblock ride along as one MFMA against an all-ones B operand.
-template <int KIN, int DT>
-__device__ __forceinline__ void wgrad_layer(const ppo_wgrad_t& a, int l, char* lds) {
+// One workgroup's output block: OG output features (o0 .. o0 + OG - 1 of the job's nout) x KIN input
+// features (+ the bias column when BIAS) over rows [r_begin, r_end).  The block is OT x CT tiles of 32 x 32;
+// wave w takes WO consecutive o-tiles x WC consecutive c-tiles (oi = w % (OT / WO), ci = w / (OT / WO)), and
+// when BIAS the waves with ci < WO also form the bias sums of o-tile oi * WO + ci as one MFMA against an
+// all-ones B operand.  Shapes: trunk 128 x 256 (2 x 2 tiles per wave), layer 0 128 x 64 (1 x 1), the
+// head 32 x 256 (1 x 1, no bias).
+template <int OG, int KIN, int WO, int WC, bool BIAS, int DT>
+__device__ __forceinline__ void wgrad_block(const uint16_t* __restrict__ dz, int dz_stride, int o0,
+                                            const uint16_t* __restrict__ hin, int hs, float* __restrict__ part,
+                                            int r_begin, int r_end, char* lds) {
     typedef typename Lp<DT>::v8 V8;
-    constexpr int NCT = KIN / 32;
-    constexpr int CBLK = NCT / 2;            // c-blocks of 2 tiles
-    constexpr int OTW = CBLK;                // o-tiles per wave (8 waves cover 8 o-tiles x NCT)
-    static_assert(OTW * (kWaves / CBLK) == kOut / 32, "wave tiling");
+    constexpr int OT = OG / 32, CT = KIN / 32;
+    constexpr int NOI = OT / WO;
+    static_assert(NOI * (CT / WC) == kWaves, "wave tiling");
+    static_assert(!BIAS || CT / WC >= WO, "bias tiles");
+    constexpr int PD = OG == 128 ? kPitchD128 : kPitchD32;
     constexpr int PH = KIN == 256 ? kPitchH256 : kPitchH64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int cb = wave % CBLK, obase = (wave / CBLK) * OTW;
-    const int S = a.splits, s = blockIdx.x;
-    const int64_t rows = a.rows;
-    const int r_begin = int(rows * s / S), r_end = int(rows * (s + 1) / S);
-    const uint16_t* __restrict__ dz = a.dz[l];
-    const uint16_t* __restrict__ hin = a.hin[l];
-    const int hs = a.hin_stride[l];
+    const int oi = wave % NOI, ci = wave / NOI;
+    const bool bias_wave = BIAS && ci < WO;
 
-    f32x16 acc[OTW][2], accb = {};
+    f32x16 acc[WO][WC], accb = {};
 #pragma unroll
-    for (int t = 0; t < OTW; ++t) acc[t][0] = acc[t][1] = f32x16{};
+    for (int t = 0; t < WO; ++t)
+#pragma unroll
+        for (int u = 0; u < WC; ++u) acc[t][u] = f32x16{};
     const V8 ones = Lp<DT>::one();
 
-    Stager<kOut> sd;
+    Stager<OG> sd;
     Stager<KIN> sh;
-    sd.load(dz, kOut, r_begin, r_end);
-    sh.load(hin, hs, r_begin, r_end);
+    sd.load(dz, dz_stride, o0, r_begin, r_end);
+    sh.load(hin, hs, 0, r_begin, r_end);
     const int nst = (r_end - r_begin + kKT - 1) / kKT;
     for (int it = 0; it < nst; ++it) {
         char* img = lds + (it & 1) * kStage;
-        sd.store(img, kPitchDz);
-        sh.store(img + kStageDz, PH);
+        sd.store(img, PD);
+        sh.store(img + kStageD, PH);
         if (it + 1 < nst) {
             const int r0 = r_begin + (it + 1) * kKT;
-            sd.load(dz, kOut, r0, r_end);
-            sh.load(hin, hs, r0, r_end);
+            sd.load(dz, dz_stride, o0, r0, r_end);
+            sh.load(hin, hs, 0, r0, r_end);
         }
         __syncthreads();
 #pragma unroll
         for (int ks = 0; ks < kKT / 16; ++ks) {
-            V8 af[OTW], bfr[2];
+            V8 af[WO], bfr[WC];
 #pragma unroll
-            for (int t = 0; t < OTW; ++t) af[t] = tr_frag<DT>(img, kPitchDz, (obase + t) * 32, ks * 16, lane);
+            for (int t = 0; t < WO; ++t) af[t] = tr_frag<DT>(img, PD, (oi * WO + t) * 32, ks * 16, lane);
 #pragma unroll
-            for (int u = 0; u < 2; ++u) bfr[u] = tr_frag<DT>(img + kStageDz, PH, (2 * cb + u) * 32, ks * 16, lane);
+            for (int u = 0; u < WC; ++u) bfr[u] = tr_frag<DT>(img + kStageD, PH, (ci * WC + u) * 32, ks * 16, lane);
 #pragma unroll
-            for (int t = 0; t < OTW; ++t)
+            for (int t = 0; t < WO; ++t)
 #pragma unroll
-                for (int u = 0; u < 2; ++u) acc[t][u] = Lp<DT>::mma(af[t], bfr[u], acc[t][u]);
-            V8 ab = af[0];  // af[cb] without a dynamically indexed register array
+                for (int u = 0; u < WC; ++u) acc[t][u] = Lp<DT>::mma(af[t], bfr[u], acc[t][u]);
+            if (bias_wave) {  // uniform per wave
+                V8 ab = af[0];  // af[ci] without a dynamically indexed register array
 #pragma unroll
-            for (int t = 1; t < OTW; ++t) ab = cb == t ? af[t] : ab;
-            accb = Lp<DT>::mma(ab, ones, accb);
+                for (int t = 1; t < WO; ++t) ab = ci == t ? af[t] : ab;
+                accb = Lp<DT>::mma(ab, ones, accb);
+            }
         }
     }
     // D[o][c]: c = lane & 31 on the lane, o = 8 (r >> 2) + 4 (lane >> 5) + (r & 3) in register r
-    float* __restrict__ part = a.part[l] + int64_t(s) * kOut * hs;
     const int j = lane & 31, h = lane >> 5;
 #pragma unroll
-    for (int t = 0; t < OTW; ++t)
+    for (int t = 0; t < WO; ++t)
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < WC; ++u)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int o = (obase + t) * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
-                part[int64_t(o) * hs + (2 * cb + u) * 32 + j] = acc[t][u][r];
+                const int o = o0 + (oi * WO + t) * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                part[int64_t(o) * hs + (ci * WC + u) * 32 + j] = acc[t][u][r];
             }
-    if (j == 0) {
+    if (bias_wave && j == 0) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int o = (obase + cb) * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+            const int o = o0 + (oi * WO + ci) * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
             part[int64_t(o) * hs + KIN] = accb[r];
         }
     }
 }
 
+// block index -> job.  Trunk pairs (layer l < 5, split s) in layer-major order, two workgroups each
+// (output halves); the pairs are dealt in groups of 8 so that the halves of a pair sit 8 block indices
+// apart (same XCD, dispatched together); the last group holds the remainder.  Then the head splits.
 template <int DT>
 __global__ void __launch_bounds__(kThreads, 1) k_wgrad(ppo_wgrad_t a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    const int l = blockIdx.y;
-    if (a.kin[l] == 64)
-        wgrad_layer<64, DT>(a, l, lds);
-    else
-        wgrad_layer<256, DT>(a, l, lds);
+    const int ntrunk = a.layers < 5 ? a.layers : 5;
+    int pairs = 0;
+    for (int l = 0; l < ntrunk; ++l) pairs += a.splits[l];
+    const int b = blockIdx.x;
+    if (b < 2 * pairs) {
+        const int q = b / 16, full = (pairs - 8 * q) >= 8 ? 8 : pairs - 8 * q;
+        const int r = b - 16 * q;
+        const int half = r / full, pair = 8 * q + r % full;
+        int l = 0, s = pair;
+        while (s >= a.splits[l]) s -= a.splits[l++];
+        const int S = a.splits[l];
+        const int r_begin = int(int64_t(a.rows) * s / S), r_end = int(int64_t(a.rows) * (s + 1) / S);
+        float* part = a.part[l] + int64_t(s) * kOut * a.hin_stride[l];
+        if (a.kin[l] == 64)
+            wgrad_block<kOG, 64, 1, 1, true, DT>(a.dz[l], kOut, half * kOG, a.hin[l], a.hin_stride[l], part,
+                                                 r_begin, r_end, lds);
+        else
+            wgrad_block<kOG, 256, 2, 2, true, DT>(a.dz[l], kOut, half * kOG, a.hin[l], a.hin_stride[l], part,
+                                                  r_begin, r_end, lds);
+    } else {
+        const int s = b - 2 * pairs, S = a.splits[5];
+        const int r_begin = int(int64_t(a.rows) * s / S), r_end = int(int64_t(a.rows) * (s + 1) / S);
+        float* part = a.part[5] + int64_t(s) * kHeadOut * a.hin_stride[5];
+        wgrad_block<kHeadOut, 256, 1, 1, false, DT>(a.dz[5], kHeadOut, 0, a.hin[5], a.hin_stride[5], part,
+                                                     r_begin, r_end, lds);
+    }
 }
 
 }  // namespace
 
 extern "C" int ppo_weight_grads(const ppo_wgrad_t* args_host, void* stream) {
     const ppo_wgrad_t* a = args_host;
-    bool ok = a && a->rows > 0 && a->splits > 0 && a->splits <= a->rows && a->layers > 0 && a->layers <= 5 &&
-              (a->dtype == PPO_DT_BF16 || a->dtype == PPO_DT_F16);
-    for (int l = 0; ok && l < a->layers; ++l)
-        ok = a->dz[l] && a->hin[l] && a->part[l] && (a->kin[l] == 64 || a->kin[l] == 256) &&
-             a->hin_stride[l] >= a->kin[l] + 1 && a->hin_stride[l] % 8 == 0 &&
+    bool ok = a && a->rows > 0 && a->layers > 0 && a->layers <= 6 && (a->dtype == PPO_DT_BF16 || a->dtype == PPO_DT_F16);
+    int blocks = 0;
+    for (int l = 0; ok && l < a->layers; ++l) {
+        const bool head = l == 5;
+        const int kin = head ? 256 : a->kin[l];
+        ok = a->dz[l] && a->hin[l] && a->part[l] && a->splits[l] > 0 && a->splits[l] <= a->rows &&
+             (head ? a->kin[l] == 256 : (kin == 64 || kin == 256) && (l == 0 || kin == 256)) &&
+             a->hin_stride[l] >= kin + (head ? 0 : 1) && a->hin_stride[l] % 8 == 0 &&
              (reinterpret_cast<uintptr_t>(a->dz[l]) | reinterpret_cast<uintptr_t>(a->hin[l])) % 16 == 0;
+        blocks += head ? a->splits[l] : 2 * a->splits[l];
+    }
     if (!ok) {
         snprintf(g_err, sizeof(g_err), "ppo_weight_grads: bad arguments");
         ppo_detail::set_error(g_err);
@@ -238,10 +285,10 @@ extern "C" int ppo_weight_grads(const ppo_wgrad_t* args_host, void* stream) {
         attr[f16] = true;
     }
     if (f16)
-        hipLaunchKernelGGL(k_wgrad<PPO_DT_F16>, dim3(a->splits, a->layers), dim3(kThreads), kLdsBytes,
+        hipLaunchKernelGGL(k_wgrad<PPO_DT_F16>, dim3(blocks), dim3(kThreads), kLdsBytes,
                            static_cast<hipStream_t>(stream), *a);
     else
-        hipLaunchKernelGGL(k_wgrad<PPO_DT_BF16>, dim3(a->splits, a->layers), dim3(kThreads), kLdsBytes,
+        hipLaunchKernelGGL(k_wgrad<PPO_DT_BF16>, dim3(blocks), dim3(kThreads), kLdsBytes,
                            static_cast<hipStream_t>(stream), *a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -38,7 +38,7 @@ import torch.nn.functional as F
 from .._native import PPO_LIB_PATH, NativeError, check_build_id
 
 _LIB = None
-PPO_ABI_VERSION = 3
+PPO_ABI_VERSION = 4
 PPO_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 SCALER_GROWTH_INTERVAL = 2000  # torch.cuda.amp.GradScaler defaults (rl_games builds it with defaults)
 SCALER_INIT = 2.0 ** 16
@@ -58,21 +58,21 @@ class PpoReduceJob(C.Structure):
 
 class PpoMlpFwd(C.Structure):
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p * 5), ("b", C.c_void_p * 5), ("wh", C.c_void_p),
-                ("bh", C.c_void_p), ("h", C.c_void_p * 4), ("h5", C.c_void_p), ("head", C.c_void_p),
+                ("bh", C.c_void_p), ("h", C.c_void_p * 5), ("head", C.c_void_p),
                 ("rows", C.c_int32), ("nh", C.c_int32), ("x_stride", C.c_int32), ("h_stride", C.c_int32),
                 ("dtype", C.c_int32), ("obs", C.c_void_p), ("mb_idx", C.c_void_p), ("mean", C.c_void_p),
                 ("var", C.c_void_p), ("x_out", C.c_void_p), ("eps", C.c_float), ("obs_dim", C.c_int32)]
 
 
 class PpoMlpBwd(C.Structure):
-    _fields_ = [("dhead", C.c_void_p), ("wh", C.c_void_p), ("wt", C.c_void_p * 4), ("h5", C.c_void_p),
-                ("h", C.c_void_p * 4), ("dz", C.c_void_p * 5), ("rows", C.c_int32), ("nh", C.c_int32),
+    _fields_ = [("dhead", C.c_void_p), ("wh", C.c_void_p), ("wt", C.c_void_p * 4),
+                ("h", C.c_void_p * 5), ("dz", C.c_void_p * 5), ("rows", C.c_int32), ("nh", C.c_int32),
                 ("h_stride", C.c_int32), ("dtype", C.c_int32)]
 
 
 class PpoWgrad(C.Structure):
-    _fields_ = [("dz", C.c_void_p * 5), ("hin", C.c_void_p * 5), ("part", C.c_void_p * 5), ("kin", C.c_int32 * 5),
-                ("hin_stride", C.c_int32 * 5), ("rows", C.c_int32), ("splits", C.c_int32), ("layers", C.c_int32),
+    _fields_ = [("dz", C.c_void_p * 6), ("hin", C.c_void_p * 6), ("part", C.c_void_p * 6), ("kin", C.c_int32 * 6),
+                ("hin_stride", C.c_int32 * 6), ("splits", C.c_int32 * 6), ("rows", C.c_int32), ("layers", C.c_int32),
                 ("dtype", C.c_int32)]
 
 
@@ -102,7 +102,7 @@ def load() -> C.CDLL:
     L.ppo_obs_stats.argtypes = [V, V, I32, I32, V, V]
     L.ppo_obs_stats_update.argtypes = [V, I32, I32, I32, V, V, V, V]
     L.ppo_obs_normalize.argtypes = [V, V, I32, I32, V, V, F32, V, I32, I32, I32, V]
-    L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V, V]
+    L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V, V, I32, V]
     L.ppo_loss_finalize.argtypes = [V, I32, I32, I32, F32, V, V, V, V, V, V, V]
     L.ppo_elu_bwd.argtypes = [V, I32, V, I32, V, I32, I32, I32, V, V]
     L.ppo_sqnorm.argtypes = [V, I64, V, V, V]
@@ -138,11 +138,24 @@ def _p(t: torch.Tensor | None) -> int | None:
 
 
 def _split(rows: int) -> int:
-    """Split-K factor for the weight-gradient GEMMs: row chunks of >= 512, at most 32 chunks."""
+    """Split-K factor of the hipBLASLt weight-gradient bmm (the non-MFMA path): row chunks of >= 512, at
+    most 32 chunks."""
     s = 1
     while s < 32 and rows % (2 * s) == 0 and rows // (2 * s) >= 512:
         s *= 2
     return s
+
+
+def wgrad_splits(rows: int) -> list[int]:
+    """Row splits of the six ppo_weight_grads jobs (trunk layers 0..4, the heads) for one chip of 256 CUs:
+    a trunk split is two workgroups (output halves), a head split one.  At 32768 rows: layer 0 16 splits
+    (its workgroups stream 384 B per row), layers 1..4 24 (768 B per row), the heads 32 (576 B per row)
+    -> 2 x (16 + 4 x 24) + 32 = 256 workgroups of about equal bytes; the trunk pair count (112) is a
+    multiple of 8, so every pair shares an XCD.  Small minibatches keep >= 128 rows per split."""
+    t = 24 if rows >= 24 * 1024 else max(1, min(24, rows // 128))
+    s0 = max(1, 2 * t // 3)
+    sh = max(1, 4 * t // 3)
+    return [s0, t, t, t, t, sh]
 
 
 class FusedPPOUpdate:
@@ -188,13 +201,15 @@ class FusedPPOUpdate:
         if self.mfma_trunk:
             # layer inputs carry a constant ones column (x: col 64 of 72, hidden: col 256 of 264), so the
             # split-K weight-gradient GEMM also yields the bias gradient (its column `in`)
+            # h[0] the normalised input, h[1..5] the five layers (16-bit, as autocast keeps them)
             self.h = [torch.zeros(B, 72, device=dev, dtype=dt)] + [torch.zeros(B, 264, device=dev, dtype=dt)
-                                                                     for _ in range(4)]
+                                                                     for _ in range(5)]
             self.h[0][:, 64] = 1.0
             for t in self.h[1:]:
                 t[:, 256] = 1.0
-            self.h_last_f = torch.empty(B, 256, device=dev)
+            self.h_last_f = None
             self.dzs = [torch.empty(B, 256, device=dev, dtype=dt) for _ in range(5)]
+            self.dhead_lp = torch.zeros(B, 32, device=dev, dtype=dt)  # d loss / d [mu | value], 16-bit
         else:
             self.h = [torch.zeros(B, w, device=dev, dtype=dt) for w in widths]
             self.h_last_f = torch.empty(B, widths[-1], device=dev) if self.lp else self.h[-1]
@@ -269,23 +284,26 @@ class FusedPPOUpdate:
             a.dtype = self.dt_code
             self._mlp_args = a
             bw = PpoMlpBwd()
-            bw.dhead, bw.wh, bw.nh = self.dhead.data_ptr(), self.Wh.data_ptr(), self.A + 1
+            bw.dhead, bw.wh, bw.nh = self.dhead_lp.data_ptr(), self.Wh.data_ptr(), self.A + 1
             for k in range(4):
                 bw.wt[k] = self.WT_lp[k].data_ptr()
-                bw.h[k] = self.h[k + 1].data_ptr()
             for k in range(5):
+                bw.h[k] = self.h[k + 1].data_ptr()
                 bw.dz[k] = self.dzs[k].data_ptr()
-            bw.h5, bw.rows, bw.h_stride = self.h_last_f.data_ptr(), B, self.h[1].stride(0)
+            bw.rows, bw.h_stride = B, self.h[1].stride(0)
             bw.dtype = self.dt_code
             self._mlp_bwd_args = bw
-            # split-K partials of the weight / bias gradients, (S, 256, 72 | 264) fp32 per layer
-            self.mfma_wgrad = bool(getattr(agent, "config", {}).get("mfma_wgrad", True))
-            self.wg_part = [torch.empty(self.S, 256, t.shape[1], device=dev) for t in self.h]
+            # split-K partials of the weight / bias gradients: (S_l, 256, 72 | 264) fp32 per trunk layer and
+            # (S_h, 32, 264) for the heads (dhead^T h5)
+            self.wg_splits = wgrad_splits(B)
+            self.wg_part = [torch.empty(self.wg_splits[k], 256 if k < 5 else 32, self.h[k].shape[1], device=dev)
+                            for k in range(6)]
             wg = PpoWgrad()
-            for k in range(5):
-                wg.dz[k], wg.hin[k], wg.part[k] = self.dzs[k].data_ptr(), self.h[k].data_ptr(), self.wg_part[k].data_ptr()
-                wg.kin[k], wg.hin_stride[k] = 64 if k == 0 else 256, self.h[k].shape[1]
-            wg.rows, wg.splits, wg.layers, wg.dtype = B, self.S, 5, self.dt_code
+            for k in range(6):
+                dz = self.dzs[k] if k < 5 else self.dhead_lp
+                wg.dz[k], wg.hin[k], wg.part[k] = dz.data_ptr(), self.h[k].data_ptr(), self.wg_part[k].data_ptr()
+                wg.kin[k], wg.hin_stride[k], wg.splits[k] = 64 if k == 0 else 256, self.h[k].shape[1], self.wg_splits[k]
+            wg.rows, wg.layers, wg.dtype = B, 6, self.dt_code
             self._wgrad_args = wg
         self.segs = (PpoSeg * max(len(segs), 1))(*segs)
         self.nseg = len(segs)
@@ -340,16 +358,15 @@ class FusedPPOUpdate:
         if self.mfma_trunk:
             # one launch: the input normalisation (RunningMeanStd), 5 x (MFMA + bias + ELU) with
             # weight-stationary waves and the activations through LDS, 16-bit heads; stores the normalised
-            # input and layers 1..4 (16-bit) and 5 (fp32) only when h has room for them (training)
+            # input and layers 1..5 (16-bit) only when h has room for them (training)
             a = self._mlp_args
             a.obs, a.mb_idx, a.obs_dim = x.data_ptr(), idx.data_ptr(), self.obs_dim
             a.mean, a.var, a.eps = rms.running_mean.data_ptr(), rms.running_var.data_ptr(), rms.epsilon
             a.x_out = h[0].data_ptr() if len(h) > 1 else None
             a.x, a.x_stride = h[0].data_ptr(), h[0].stride(0)
             a.h_stride = h[1].stride(0) if len(h) > 1 else 256
-            for i in range(4):
+            for i in range(5):
                 a.h[i] = h[i + 1].data_ptr() if len(h) > 1 else None
-            a.h5 = h_last_f.data_ptr() if h_last_f is not None else None
             a.head, a.rows = head.data_ptr(), rows
             _check(L.ppo_mlp_forward(C.byref(a), s), "ppo_mlp_forward")
             return
@@ -453,7 +470,8 @@ class FusedPPOUpdate:
         _check(L.ppo_loss_grad(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
                                _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
                                _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.scaler),
-                               _p(self.dhead), _p(self.loss_partials), s), "ppo_loss_grad")
+                               None if self.mfma_trunk else _p(self.dhead), _p(self.loss_partials),
+                               _p(self.dhead_lp) if self.mfma_trunk else None, self.dt_code, s), "ppo_loss_grad")
         _check(L.ppo_loss_finalize(_p(self.loss_partials), self.loss_partials.shape[0], A, B,
                                    self.loss_cfg.entropy_coef, _p(self.scaler), _p(self.gbh), _p(self.gls),
                                    _p(self.stats), _p(self.stat_idx), _p(self.flat.extra), s), "ppo_loss_finalize")
@@ -503,33 +521,27 @@ class FusedPPOUpdate:
         del keep
 
     def _backward_mfma(self) -> None:
-        """dz of all five layers from one MFMA launch (ppo_mlp_backward), then the weight and bias
-        gradients as split-K GEMMs against the ones-augmented layer inputs, summed by ONE reduce launch."""
-        L, s, B, A, S = self.L, self._stream(), self.mb, self.A, self.S
-        hl = self.h_last_f
-        jobs, keep = [], []
-        pw = torch.bmm(self.dhead.view(S, B // S, A + 1).transpose(1, 2), hl.view(S, B // S, 256))
-        keep.append(pw)
-        jobs.append(PpoReduceJob(pw.data_ptr(), self.gWh.data_ptr(), S, A + 1, 256, 256, 256, pw.numel() // S))
+        """dz of all five layers from one MFMA launch (ppo_mlp_backward), then the trunk weight and bias
+        gradients and the head weight gradient as split-K partials of ONE launch (ppo_weight_grads),
+        summed by ONE reduce launch (the head bias and log-sigma gradients come from ppo_loss_finalize)."""
+        L, s, A = self.L, self._stream(), self.A
+        jobs = []
         _check(L.ppo_mlp_backward(C.byref(self._mlp_bwd_args), s), "ppo_mlp_backward")
-        if self.mfma_wgrad:
-            _check(L.ppo_weight_grads(C.byref(self._wgrad_args), s), "ppo_weight_grads")
-        for i, m in enumerate(self.linears):
-            hin = self.h[i]
-            w = hin.shape[1]                     # 72 or 264: [features | 1 | 0 ...]
-            ones = 64 if i == 0 else 256
-            if self.mfma_wgrad:
-                gw = self.wg_part[i]             # (S, 256, w), bias sums in column `ones`
-            else:
-                gw = torch.bmm(self.dzs[i].view(S, B // S, 256).transpose(1, 2), hin.view(S, B // S, w),
-                               out_dtype=torch.float32)  # (S, 256, w)
-            keep.append(gw)
+        _check(L.ppo_weight_grads(C.byref(self._wgrad_args), s), "ppo_weight_grads")
+        for i in range(6):
+            w = self.h[i].shape[1]               # 72 or 264: [features | 1 | 0 ...]
+            S = self.wg_splits[i]
+            gw = self.wg_part[i]                 # (S, 256 | 32, w), trunk bias sums in column `ones`
             n_s = gw.numel() // S
+            if i == 5:
+                jobs.append(PpoReduceJob(gw.data_ptr(), self.gWh.data_ptr(), S, A + 1, w, 256, 256, n_s))
+                continue
+            m = self.linears[i]
+            ones = 64 if i == 0 else 256
             jobs.append(PpoReduceJob(gw.data_ptr(), self.gW[i].data_ptr(), S, 256, w, m.in_features, m.in_features, n_s))
             jobs.append(PpoReduceJob(gw.data_ptr() + 4 * ones, self.gb[i].data_ptr(), S, 256, w, 1, 1, n_s))
         arr = (PpoReduceJob * len(jobs))(*jobs)
         _check(L.ppo_reduce_rows(arr, len(jobs), s), "ppo_reduce_rows")
-        del keep
 
     @torch.no_grad()
     def _optimizer_step(self) -> None:

@@ -21,8 +21,8 @@
  *                                         with non-finite gradients and the scale update
  *   ppo_tail                              adaptive LR from the (rank-averaged) KL; minibatch counter
  *   ppo_mlp_forward / ppo_mlp_backward    the whole trunk forward / input-gradient chain (MFMA)
- *   ppo_weight_grads                      split-K weight + bias gradients of all trunk layers (MFMA)
- * The head weight gradient (fp32) stays a hipBLASLt split-K bmm.
+ *   ppo_weight_grads                      split-K weight + bias gradients of all trunk layers and the
+ *                                         head weights (MFMA, one launch)
  *
  * Minibatch rows are selected on the device: row r of minibatch i is dataset row i*mb_rows + r with i
  * read from `mb_idx` (int32, device), so one captured graph serves every minibatch.
@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PPO_ABI_VERSION 3
+#define PPO_ABI_VERSION 4
 /* element types of the low-precision (trunk) buffers */
 #define PPO_DT_F32 0
 #define PPO_DT_BF16 1
@@ -85,12 +85,16 @@ int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, in
  * advantages, old_values, returns (1 each).  Writes dhead (mb_rows x (A+1)) = d loss / d head,
  * new mu / sigma into the dataset rows, and per-block partials[nblk][2A+1+PPO_LOSS_NSTAT]
  * (sum over rows of dhead columns, d loss / d logstd, the five statistics); nblk = ppo_loss_blocks().
- * grad_scale (device fp32, a power of two; NULL = 1): every gradient is of scale * loss (GradScaler). */
+ * grad_scale (device fp32, a power of two; NULL = 1): every gradient is of scale * loss (GradScaler).
+ * dhead may be NULL; dhead_lp (NULL = skip) receives the same gradient rounded to lp_dtype (PPO_DT_BF16 /
+ * PPO_DT_F16) as mb_rows x 32 (columns A+1..31 zero): the 16-bit gradient autocast hands to the heads'
+ * Linear backward, read by ppo_mlp_backward and ppo_weight_grads. */
 int ppo_loss_blocks(int32_t mb_rows);
 int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
                   const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
                   const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
-                  const float* grad_scale, float* dhead, float* partials, void* stream);
+                  const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
+                  void* stream);
 /* sum the partials: bias grads of the heads -> grad_head_bias (A+1), logstd grads (+ -entropy_coef) ->
  * grad_logstd (A); the statistics (means) -> stats[stat_idx][PPO_LOSS_NSTAT] (stat_idx from device);
  * the KL also -> kl_out (the slot that rides in the gradient all-reduce); grad_scale as ppo_loss_grad */
@@ -134,10 +138,9 @@ int ppo_counter_add(int64_t* ctr, int64_t inc, void* stream);
  * v_mfma_f32_32x32x16_bf16, PPO_DT_F16 on v_mfma_f32_32x32x16_f16 -- rl_games' fp16 autocast): 5 layers
  * x 256, ELU, then the fp32 heads.  x: rows x 64 lp (normalised obs, zero-padded 59 -> 64; row stride
  * x_stride >= 64); w[0]: 256 x 64 lp, w[1..4]: 256 x 256 lp (the trunk mirror); b[l]: 256 fp32; wh: nh x 256 fp32
- * ([mu.w | value.w]), bh: nh fp32 (nh <= 32).  Outputs (row-major, NULL = skip): h[0..3] = layers
- * 1..4 (lp, columns 0..255 of rows with stride h_stride >= 256, a multiple of 8; columns beyond are
- * not touched),
- * h5 = layer 5 in fp32 (rows x 256), head = rows x nh fp32 holding lp values: the heads run as
+ * ([mu.w | value.w]), bh: nh fp32 (nh <= 32).  Outputs (row-major, NULL = skip): h[0..4] = layers
+ * 1..5 (lp, columns 0..255 of rows with stride h_stride >= 256, a multiple of 8; columns beyond are
+ * not touched), head = rows x nh fp32 holding lp values: the heads run as
  * rl_games' autocast runs them -- lp layer-5 activations, lp(wh), lp(bh), fp32 accumulation, an lp
  * output.  x_stride is a multiple of 8.  A workgroup of 8 waves owns 128 rows; wave w keeps the weights
  * of output features [32w, 32w + 32) in registers and the activations pass through LDS. */
@@ -147,8 +150,7 @@ typedef struct {
     const float* b[5];
     const float* wh;
     const float* bh;
-    uint16_t* h[4];
-    float* h5;
+    uint16_t* h[5];
     float* head;
     int32_t rows, nh, x_stride, h_stride;
     int32_t dtype; /* PPO_DT_BF16 or PPO_DT_F16 */
@@ -168,39 +170,44 @@ typedef struct {
 } ppo_mlp_fwd_t;
 int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream);
 
-/* Fused backward of the trunk's input-gradient chain (the weight gradients stay split-K GEMMs):
- *   dh5 = Wh^T dhead (exact f32 MFMA), dz4 = dh5 * elu'(h5),
+/* Fused backward of the trunk's input-gradient chain (the weight gradients are ppo_weight_grads):
+ *   dh5 = Wh^T dhead (lp MFMA, fp32 accumulation: autocast's head Linear backward), dz4 = dh5 * elu'(h5),
  *   for l = 4..1: dz_{l-1} = (W_l^T dz_l) * elu'(h_l)   (lp MFMA, W_l^T from wt[l-1])
- * with elu'(y) = 1 if y > 0 else y + 1 (output form).  dhead: rows x nh fp32; wh: nh x 256 fp32;
- * wt[k]: W_{k+1}^T (256 x 256 lp, row = input feature); h5: rows x 256 fp32; h[k]: layer k+1
- * activations (lp, row stride h_stride); outputs dz[l] (l = 0..4): rows x 256 lp.  lp = dtype. */
+ * with elu'(y) = 1 if y > 0 else y + 1 (output form), one lp rounding per dz.  dhead: rows x 32 lp
+ * (ppo_loss_grad's dhead_lp; columns nh..31 zero); wh: nh x 256 fp32 (rounded to lp in-kernel);
+ * wt[k]: W_{k+1}^T (256 x 256 lp, row = input feature); h[k]: layer k+1 activations (lp, k = 0..4, row
+ * stride h_stride); outputs dz[l] (l = 0..4): rows x 256 lp.  lp = dtype. */
 typedef struct {
-    const float* dhead;
+    const uint16_t* dhead;
     const float* wh;
     const uint16_t* wt[4];
-    const float* h5;
-    const uint16_t* h[4];
+    const uint16_t* h[5];
     uint16_t* dz[5];
     int32_t rows, nh, h_stride;
     int32_t dtype; /* PPO_DT_BF16 or PPO_DT_F16 */
 } ppo_mlp_bwd_t;
 int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream);
 
-/* Split-K weight + bias gradients of the trunk layers, all layers in one launch (the Linear weight /
- * bias gradients of loss.backward() in a2c_continuous.py calc_gradients; replaces five per-layer
- * split-K `torch.bmm(dz^T, [h | 1])` calls):
- *   part[l][s][o][c]   = sum_{b in split s} dz[l][b][o] * hin[l][b][c]   (o < 256, c < kin[l])
- *   part[l][s][o][kin] = sum_{b in split s} dz[l][b][o]                   (bias column)
- * dz[l]: rows x 256 lp; hin[l]: rows x hin_stride[l] lp (kin[l] = 64 or 256 features; lp = dtype); part[l]:
- * splits x 256 x hin_stride[l] fp32 (columns past kin[l] untouched).  Split s covers rows
- * [rows*s/splits, rows*(s+1)/splits); the partials are summed by ppo_reduce_rows. */
+/* Split-K weight + bias gradients of the trunk layers and the head weights, all in one launch (the
+ * Linear weight / bias gradients of loss.backward() in a2c_continuous.py calc_gradients):
+ *   part[l][s][o][c]   = sum_{b in split s} dz[l][b][o] * hin[l][b][c]   (o < nout[l], c < kin[l])
+ *   part[l][s][o][kin] = sum_{b in split s} dz[l][b][o]                   (bias column; trunk only)
+ * Job l < 5 is trunk layer l: dz[l] rows x 256 lp, nout 256, kin 64 (l = 0) or 256.  Job 5 (when
+ * layers == 6) is the heads: dz[5] = ppo_loss_grad's dhead_lp (rows x 32), nout 32, kin 256 (layer 5's
+ * activations), no bias column.  hin[l]: rows x hin_stride[l] lp; part[l]: splits[l] x nout x hin_stride[l]
+ * fp32 (columns past kin[l] (+1) untouched).  Split s of job l covers rows
+ * [rows*s/splits[l], rows*(s+1)/splits[l]).  A trunk split is two workgroups (output features 0..127 and
+ * 128..255) placed on one XCD so that the layer input they both stream is fetched once into its L2;
+ * the total count of trunk splits must be a multiple of 8.  The partials are summed by
+ * ppo_reduce_rows. */
 typedef struct {
-    const uint16_t* dz[5];
-    const uint16_t* hin[5];
-    float* part[5];
-    int32_t kin[5];
-    int32_t hin_stride[5];
-    int32_t rows, splits, layers;
+    const uint16_t* dz[6];
+    const uint16_t* hin[6];
+    float* part[6];
+    int32_t kin[6];
+    int32_t hin_stride[6];
+    int32_t splits[6];
+    int32_t rows, layers;
     int32_t dtype; /* PPO_DT_BF16 or PPO_DT_F16 */
 } ppo_wgrad_t;
 int ppo_weight_grads(const ppo_wgrad_t* args_host, void* stream);

@@ -19,24 +19,20 @@ bs = [torch.zeros(256, device=dev) for _ in range(5)]
 bsb = [b.to(torch.bfloat16) for b in bs]
 wh, bh = torch.randn(22, 256, device=dev) / 16, torch.zeros(22, device=dev)
 hs = [torch.empty(B, 256, device=dev, dtype=torch.bfloat16) for _ in range(5)]
-h5 = torch.empty(B, 256, device=dev)
 head = torch.empty(B, 22, device=dev)
 a = FU.PpoMlpFwd()
 a.x = x.data_ptr()
 for i in range(5):
-    a.w[i], a.b[i] = ws[i].data_ptr(), bs[i].data_ptr()
-for i in range(4):
-    a.h[i] = hs[i].data_ptr()
-a.wh, a.bh, a.h5, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), h5.data_ptr(), head.data_ptr(), B, 22
+    a.w[i], a.b[i], a.h[i] = ws[i].data_ptr(), bs[i].data_ptr(), hs[i].data_ptr()
+a.wh, a.bh, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), head.data_ptr(), B, 22
 a.x_stride, a.h_stride, a.dtype = 64, 256, 1  # bf16 (PPO_DT_BF16)
 
 
 def fused(store=True):
     if not store:
         b = FU.PpoMlpFwd.from_buffer_copy(a)
-        for i in range(4):
+        for i in range(5):
             b.h[i] = None
-        b.h5 = None
         FU._check(L.ppo_mlp_forward(C.byref(b), torch.cuda.current_stream().cuda_stream), "fwd")
         return
     FU._check(L.ppo_mlp_forward(C.byref(a), torch.cuda.current_stream().cuda_stream), "fwd")
@@ -48,8 +44,7 @@ def lib():
         torch.addmm(bsb[i], h, ws[i].t(), out=hs[i])
         F.elu(hs[i], inplace=True)
         h = hs[i]
-    h5.copy_(hs[4])
-    torch.addmm(bh, h5, wh.t(), out=head)
+    torch.addmm(bh, hs[4].float(), wh.t(), out=head)
 
 
 def t(fn, n=50):

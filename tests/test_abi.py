@@ -123,7 +123,7 @@ def test_ppo_library_exports_every_declared_symbol():
     assert set(fused.EXPORTED_SYMBOLS) == set(declared)
     assert L.ppo_abi_version() == fused.PPO_ABI_VERSION
     # block-count helpers are pure host functions
-    assert L.ppo_loss_blocks(32768) == 1024 and L.ppo_elu_bwd_blocks(32768) == 256
+    assert L.ppo_loss_blocks(32768) == 256 and L.ppo_elu_bwd_blocks(32768) == 256
 
 
 @pytest.mark.parametrize("cname,pyname", [("ppo_loss_cfg_t", "PpoLossCfg"), ("ppo_seg_t", "PpoSeg")])

@@ -449,8 +449,8 @@ def test_play_script_restores_trained_checkpoint(tmp_path):
                                      (1000, torch.float16)])
 def test_fused_mlp_forward_kernel(rows, dt):
     """ppo_mlp_forward (weight-stationary MFMA, activations through LDS) vs an fp32 torch statement of the
-    same rounding points: each hidden layer rounded to the 16-bit type once, layer 5 also kept in fp32;
-    the heads as under autocast: 16-bit layer-5 activations, weights and bias, fp32 accumulation, a
+    same rounding points: each of the five layers rounded to the 16-bit type once (as autocast keeps
+    them); the heads as under autocast: 16-bit layer-5 activations, weights and bias, fp32 accumulation, a
     16-bit output."""
     import ctypes as C
 
@@ -469,17 +469,15 @@ def test_fused_mlp_forward_kernel(rows, dt):
     bs = [torch.randn(256, device=dev, generator=g) * 0.1 for _ in range(5)]
     wh = torch.randn(22, 256, device=dev, generator=g) / 16
     bh = torch.randn(22, device=dev, generator=g) * 0.1
-    hs = [torch.empty(rows, 256, device=dev, dtype=dt) for _ in range(4)]
-    h5 = torch.empty(rows, 256, device=dev)
+    hs = [torch.empty(rows, 256, device=dev, dtype=dt) for _ in range(5)]
     head = torch.empty(rows, 22, device=dev)
     a = FU.PpoMlpFwd()
     a.x = xb.data_ptr()
     for i in range(5):
         a.w[i] = ws[i].data_ptr()
         a.b[i] = bs[i].data_ptr()
-    for i in range(4):
         a.h[i] = hs[i].data_ptr()
-    a.wh, a.bh, a.h5, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), h5.data_ptr(), head.data_ptr(), rows, 22
+    a.wh, a.bh, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), head.data_ptr(), rows, 22
     a.x_stride, a.h_stride, a.dtype = 64, 256, FU.PPO_DT[dt]
     FU._check(L.ppo_mlp_forward(C.byref(a), torch.cuda.current_stream().cuda_stream), "ppo_mlp_forward")
     torch.cuda.synchronize()
@@ -487,19 +485,16 @@ def test_fused_mlp_forward_kernel(rows, dt):
     for i in range(5):
         z = hin @ ws[i].float().t() + bs[i]
         y = torch.nn.functional.elu(z)
-        if i < 4:
-            got = hs[i].float()
-            yr = y.to(dt).float()
-            assert (got - yr).abs().max().item() < tol, i
-            frac = ((got - yr).abs() > 1e-6).float().mean().item()
-            assert frac < 0.02, (i, frac)  # only rounding-boundary flips
-            hin = got  # chain on the kernel's own rounding, as the kernel does
-        else:
-            torch.testing.assert_close(h5, y, rtol=2e-3, atol=2e-3)
-            ref_head = (h5.to(dt).float() @ wh.to(dt).float().t() + bh.to(dt).float()).to(dt).float()
-            # one 16-bit rounding step apart at most (fp32 sums in another order)
-            htol = 1e-2 if dt == torch.bfloat16 else 2e-3
-            torch.testing.assert_close(head, ref_head, rtol=htol, atol=htol)
+        got = hs[i].float()
+        yr = y.to(dt).float()
+        assert (got - yr).abs().max().item() < tol, i
+        frac = ((got - yr).abs() > 1e-6).float().mean().item()
+        assert frac < 0.02, (i, frac)  # only rounding-boundary flips
+        hin = got  # chain on the kernel's own rounding, as the kernel does
+    ref_head = (hin @ wh.to(dt).float().t() + bh.to(dt).float()).to(dt).float()
+    # one 16-bit rounding step apart at most (fp32 sums in another order)
+    htol = 1e-2 if dt == torch.bfloat16 else 2e-3
+    torch.testing.assert_close(head, ref_head, rtol=htol, atol=htol)
 
 
 @pytest.mark.gpu
@@ -530,15 +525,12 @@ def test_fused_mlp_forward_normalises_its_input(rows, dt):
     outs = []
     for fused_in in (False, True):
         x_out = torch.zeros(rows, 72, device=dev, dtype=dt)
-        hs = [torch.zeros(rows, 264, device=dev, dtype=dt) for _ in range(4)]
-        h5 = torch.zeros(rows, 256, device=dev)
+        hs = [torch.zeros(rows, 264, device=dev, dtype=dt) for _ in range(5)]
         head = torch.zeros(rows, 22, device=dev)
         a = FU.PpoMlpFwd()
         for i in range(5):
-            a.w[i], a.b[i] = ws[i].data_ptr(), bs[i].data_ptr()
-        for i in range(4):
-            a.h[i] = hs[i].data_ptr()
-        a.wh, a.bh, a.h5, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), h5.data_ptr(), head.data_ptr(), rows, 22
+            a.w[i], a.b[i], a.h[i] = ws[i].data_ptr(), bs[i].data_ptr(), hs[i].data_ptr()
+        a.wh, a.bh, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), head.data_ptr(), rows, 22
         a.x_stride, a.h_stride, a.dtype = 72, 264, FU.PPO_DT[dt]
         if fused_in:
             a.obs, a.mb_idx, a.mean, a.var, a.eps, a.obs_dim = (obs.data_ptr(), idx.data_ptr(), mean.data_ptr(),
@@ -548,48 +540,53 @@ def test_fused_mlp_forward_normalises_its_input(rows, dt):
             a.x = x_ref.data_ptr()
         FU._check(L.ppo_mlp_forward(C.byref(a), s), "ppo_mlp_forward")
         torch.cuda.synchronize()
-        outs.append((x_out.clone(), [t.clone() for t in hs], h5.clone(), head.clone()))
-    (_, h_a, h5_a, hd_a), (x_b, h_b, h5_b, hd_b) = outs
+        outs.append((x_out.clone(), [t.clone() for t in hs], head.clone()))
+    (_, h_a, hd_a), (x_b, h_b, hd_b) = outs
     assert torch.equal(x_b[:, :64], x_ref[:, :64])
-    assert all(torch.equal(p, q) for p, q in zip(h_a, h_b)) and torch.equal(h5_a, h5_b) and torch.equal(hd_a, hd_b)
+    assert all(torch.equal(p, q) for p, q in zip(h_a, h_b)) and torch.equal(hd_a, hd_b)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rows,splits,dt", [(32768, 32, torch.bfloat16), (1000, 3, torch.bfloat16),
-                                            (64, 1, torch.bfloat16), (32768, 32, torch.float16),
-                                            (1000, 3, torch.float16)])
+@pytest.mark.parametrize("rows,splits,dt", [(32768, None, torch.bfloat16), (1000, [3, 2, 5, 1, 4, 3], torch.bfloat16),
+                                            (64, [1] * 6, torch.bfloat16), (32768, None, torch.float16),
+                                            (1000, [2, 3, 3, 3, 3, 7], torch.float16)])
 def test_weight_grads_kernel(rows, splits, dt):
-    """ppo_weight_grads (MFMA, transposed LDS reads) vs fp32 torch on the same 16-bit inputs: per split
-    s, part[s] = dz[rows of s]^T [hin | 1] over columns 0..kin (the products of two bf16 or two fp16
-    values are exact in fp32; only the summation order differs).  Columns past the bias column stay
-    untouched; ragged splits (rows not a multiple of splits or of the 64-row stage) are covered."""
+    """ppo_weight_grads (MFMA, transposed LDS reads) vs fp32 torch on the same 16-bit inputs: per job l and
+    split s, part[l][s] = dz[rows of s]^T [hin | 1] over columns 0..kin for the trunk layers, dhead^T h5
+    for the heads (job 5, 32 output rows, no bias column) -- the products of two bf16 or two fp16 values
+    are exact in fp32; only the summation order differs.  Columns past the bias column stay untouched;
+    ragged splits (rows not a multiple of splits or of the 64-row stage), per-job split counts and a
+    trunk pair count that is not a multiple of 8 (the last XCD group) are covered; None = the trainer's
+    splits (fused.wgrad_splits)."""
     import ctypes as C
 
     from allsteps_isaaclab_amd.learning import fused as FU
 
     L = FU.load()
     dev = "cuda:0"
+    splits = splits or FU.wgrad_splits(rows)
     g = torch.Generator(device=dev).manual_seed(5)
-    widths = [72] + [264] * 4
-    dz = [torch.randn(rows, 256, device=dev, generator=g).to(dt) for _ in range(5)]
+    widths = [72] + [264] * 5
+    dz = [torch.randn(rows, 256 if k < 5 else 32, device=dev, generator=g).to(dt) for k in range(6)]
     hin = [torch.randn(rows, w, device=dev, generator=g).to(dt) for w in widths]
-    part = [torch.full((splits, 256, w), float("nan"), device=dev) for w in widths]
+    part = [torch.full((splits[k], 256 if k < 5 else 32, widths[k]), float("nan"), device=dev) for k in range(6)]
     a = FU.PpoWgrad()
-    for k in range(5):
+    for k in range(6):
         a.dz[k], a.hin[k], a.part[k] = dz[k].data_ptr(), hin[k].data_ptr(), part[k].data_ptr()
-        a.kin[k], a.hin_stride[k] = 64 if k == 0 else 256, widths[k]
-    a.rows, a.splits, a.layers, a.dtype = rows, splits, 5, FU.PPO_DT[dt]
+        a.kin[k], a.hin_stride[k], a.splits[k] = 64 if k == 0 else 256, widths[k], splits[k]
+    a.rows, a.layers, a.dtype = rows, 6, FU.PPO_DT[dt]
     FU._check(L.ppo_weight_grads(C.byref(a), torch.cuda.current_stream().cuda_stream), "ppo_weight_grads")
     torch.cuda.synchronize()
-    for k in range(5):
+    for k in range(6):
         kin = 64 if k == 0 else 256
-        for s in range(splits):
-            r0, r1 = rows * s // splits, rows * (s + 1) // splits
+        nb = 1 if k < 5 else 0  # bias column
+        for s in range(splits[k]):
+            r0, r1 = rows * s // splits[k], rows * (s + 1) // splits[k]
             d, h = dz[k][r0:r1].double(), hin[k][r0:r1].double()
-            ref = torch.cat([d.t() @ h[:, :kin], d.sum(0)[:, None]], 1).float()
-            got = part[k][s, :, :kin + 1]
-            torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5 * (r1 - r0) ** 0.5, msg=f"layer {k} split {s}")
-        assert torch.isnan(part[k][:, :, kin + 1:]).all(), k
+            ref = torch.cat([d.t() @ h[:, :kin], d.sum(0)[:, None]], 1).float()[:, :kin + nb]
+            got = part[k][s, :, :kin + nb]
+            torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5 * (r1 - r0) ** 0.5, msg=f"job {k} split {s}")
+        assert torch.isnan(part[k][:, :, kin + nb:]).all(), k
 
 
 def test_weight_grads_rejects_bad_arguments():
@@ -599,7 +596,8 @@ def test_weight_grads_rejects_bad_arguments():
 
     L = FU.load()
     a = FU.PpoWgrad()
-    a.rows, a.splits, a.layers = 128, 1, 1
+    a.rows, a.layers = 128, 1
+    a.splits[0] = 1
     assert L.ppo_weight_grads(C.byref(a), None) == -1  # null pointers: refused before any launch
     assert b"bad arguments" in L.ppo_last_error()
 
