@@ -713,13 +713,43 @@ struct SegTable {
     int n;
 };
 
+// the end of a minibatch step (ppo_tail): GradScaler.update, the adaptive LR from the KL, Adam's step
+// count, the device minibatch / statistics counters -- one thread
+__device__ void tail_update(const ppo_tail_args_t& t, bool skipped) {
+    if (t.scaler) {  // GradScaler.update: backoff 0.5 on a skipped step, growth 2 after growth_interval good ones
+        float* scaler = t.scaler;
+        if (skipped) {
+            scaler[0] *= 0.5f;
+            scaler[1] = 0.f;
+        } else if (scaler[1] + 1.f >= float(t.growth_interval)) {
+            scaler[0] *= 2.f;
+            scaler[1] = 0.f;
+        } else {
+            scaler[1] += 1.f;
+        }
+    }
+    if (t.kl_threshold > 0.f) {
+        const double k = double(*t.kl);
+        double cur = *t.lr, nxt = cur;
+        if (k > 2.0 * double(t.kl_threshold)) nxt = fmax(cur / 1.5, t.min_lr);
+        if (k < 0.5 * double(t.kl_threshold)) nxt = fmin(cur * 1.5, t.max_lr);
+        *t.lr = nxt;
+    }
+    if (!skipped) *t.step += 1.0;  // a skipped optimizer.step() leaves Adam's step count
+    *t.mb_idx = (*t.mb_idx + 1) % t.n_minibatches;
+    *t.stat_idx += 1;
+}
+
+// TAIL: the last block to finish (a device counter; every block reads lr / step / scaler in its prologue
+// before it counts itself done) also runs the tail, so the minibatch step ends with this one launch
+template <bool TAIL>
 __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, const float* __restrict__ g,
                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                        const float* __restrict__ np, int nnp, float max_norm,
                                                        const double* __restrict__ lr_p, const double* __restrict__ step_p,
                                                        float b1, float b2, float eps, SegTable segs,
                                                        uint16_t* __restrict__ mirror, int mirror_dtype,
-                                                       const float* __restrict__ scaler) {
+                                                       const float* __restrict__ scaler, ppo_tail_args_t tail) {
     __shared__ float red[2][kAdamThreads / kWave];
     __shared__ float coef_s, step_size_s, bc2_sqrt_s, inv_scale_s;
     __shared__ int skip_s;
@@ -759,11 +789,11 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     const float step_size = step_size_s;
     const float bc2_sqrt = bc2_sqrt_s;
     const float inv_scale = inv_scale_s;
-    if (skip_s) return;
+    const bool skip = skip_s;
     // grid-stride over the buffer: one resident block per CU pays the prologue above (the partial sums
     // and thread 0's fp64 bias corrections) once, instead of once per 256 parameters in successive
     // rounds of blocks
-    for (int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x; i < n; i += int64_t(gridDim.x) * kAdamThreads) {
+    for (int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x; !skip && i < n; i += int64_t(gridDim.x) * kAdamThreads) {
         const float gi = (g[i] * inv_scale) * coef;
         const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
         const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
@@ -784,42 +814,31 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
             }
         }
     }
+    if (TAIL) {
+        __shared__ int last_s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            last_s = atomicAdd(tail.counter, 1) == int(gridDim.x) - 1;
+        }
+        __syncthreads();
+        if (last_s && threadIdx.x == 0) {
+            __threadfence();
+            tail_update(tail, skip);
+            atomicExch(tail.counter, 0);
+        }
+    }
 }
 
-__global__ void k_tail(double* lr, const float* kl, float thr, double min_lr, double max_lr, double* step,
-                       int32_t* mb_idx, int nmb, int32_t* stat_idx, float* scaler, const float* np, int nnp,
-                       int growth_interval) {
+__global__ void k_tail(ppo_tail_args_t t, const float* np, int nnp) {
     // k_sqnorm's non-finite counts, summed by the whole wave (one thread walking the partials serially
     // was a chain of dependent global loads: 6 us of every minibatch)
     float b = 0.f;
-    if (scaler) {
+    if (t.scaler) {
         for (int k = threadIdx.x; k < nnp; k += kWave) b += np[nnp + k];
         b = wave_sum(b);
     }
-    if (threadIdx.x != 0) return;
-    bool skipped = false;
-    if (scaler) {  // GradScaler.update: backoff 0.5 on a skipped step, growth 2 after growth_interval good ones
-        skipped = b > 0.f;
-        if (skipped) {
-            scaler[0] *= 0.5f;
-            scaler[1] = 0.f;
-        } else if (scaler[1] + 1.f >= float(growth_interval)) {
-            scaler[0] *= 2.f;
-            scaler[1] = 0.f;
-        } else {
-            scaler[1] += 1.f;
-        }
-    }
-    if (thr > 0.f) {
-        const double k = double(*kl);
-        double cur = *lr, nxt = cur;
-        if (k > 2.0 * double(thr)) nxt = fmax(cur / 1.5, min_lr);
-        if (k < 0.5 * double(thr)) nxt = fmin(cur * 1.5, max_lr);
-        *lr = nxt;
-    }
-    if (!skipped) *step += 1.0;  // a skipped optimizer.step() leaves Adam's step count
-    *mb_idx = (*mb_idx + 1) % nmb;
-    *stat_idx += 1;
+    if (threadIdx.x == 0) tail_update(t, t.scaler && b > 0.f);
 }
 
 inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
@@ -998,10 +1017,10 @@ int ppo_sqnorm(const float* g, int64_t n, const float* scaler, float* partials, 
     return launched("k_sqnorm");
 }
 
-int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials, int32_t nblk_norm,
-             float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,
-             const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, const float* scaler,
-             void* stream) {
+static int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials,
+                       int32_t nblk_norm, float max_norm, const double* lr, double* step, float beta1, float beta2,
+                       float eps, const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype,
+                       const float* scaler, const ppo_tail_args_t* tail, void* stream) {
     if (nseg < 0 || nseg > PPO_MAX_SEG) return fail(-1, "ppo_adam: too many mirror segments");
     if (mirror && mirror_dtype != PPO_DT_BF16 && mirror_dtype != PPO_DT_F16)
         return fail(-1, "ppo_adam: mirror_dtype must be bf16 or fp16");
@@ -1014,19 +1033,50 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
             return fail(-1, "ppo_adam: bad segment");
     }
     const int64_t want = (n + kAdamThreads - 1) / kAdamThreads;
-    hipLaunchKernelGGL(k_adam, dim3(unsigned(want < kAdamBlocks ? want : kAdamBlocks)), dim3(kAdamThreads), 0, S(stream),
-                       p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
-                       static_cast<uint16_t*>(mirror), mirror_dtype, scaler);
+    const dim3 grid(unsigned(want < kAdamBlocks ? want : kAdamBlocks));
+    if (tail)
+        hipLaunchKernelGGL(k_adam<true>, grid, dim3(kAdamThreads), 0, S(stream), p, g, m, v, n, sqnorm_partials,
+                           nblk_norm, max_norm, lr, step, beta1, beta2, eps, t, static_cast<uint16_t*>(mirror),
+                           mirror_dtype, scaler, *tail);
+    else
+        hipLaunchKernelGGL(k_adam<false>, grid, dim3(kAdamThreads), 0, S(stream), p, g, m, v, n, sqnorm_partials,
+                           nblk_norm, max_norm, lr, step, beta1, beta2, eps, t, static_cast<uint16_t*>(mirror),
+                           mirror_dtype, scaler, ppo_tail_args_t{});
     return launched("k_adam");
+}
+
+int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials, int32_t nblk_norm,
+             float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,
+             const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, const float* scaler,
+             void* stream) {
+    return launch_adam(p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, segs_host,
+                       nseg, mirror, mirror_dtype, scaler, nullptr, stream);
+}
+
+static int check_tail(const ppo_tail_args_t& t, const float* sqnorm_partials) {
+    if (!t.lr || !t.step || !t.mb_idx || !t.stat_idx || (t.kl_threshold > 0.f && !t.kl))
+        return fail(-1, "ppo_tail: null pointer");
+    if (t.n_minibatches <= 0) return fail(-1, "ppo_tail: n_minibatches must be positive");
+    if (t.scaler && (!sqnorm_partials || t.growth_interval <= 0)) return fail(-1, "ppo_tail: the scaler needs the norm partials");
+    return 0;
+}
+
+int ppo_adam_tail(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials,
+                  int32_t nblk_norm, float max_norm, float beta1, float beta2, float eps, const ppo_seg_t* segs_host,
+                  int32_t nseg, void* mirror, int32_t mirror_dtype, const ppo_tail_args_t* tail, void* stream) {
+    if (!tail || !tail->counter) return fail(-1, "ppo_adam_tail: tail arguments with a counter required");
+    if (const int rc = check_tail(*tail, sqnorm_partials)) return rc;
+    return launch_adam(p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, tail->lr, tail->step, beta1, beta2, eps,
+                       segs_host, nseg, mirror, mirror_dtype, tail->scaler, tail, stream);
 }
 
 int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,
              int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, float* scaler, const float* sqnorm_partials,
              int32_t nblk_norm, int32_t growth_interval, void* stream) {
-    if (n_minibatches <= 0) return fail(-1, "ppo_tail: n_minibatches must be positive");
-    if (scaler && (!sqnorm_partials || growth_interval <= 0)) return fail(-1, "ppo_tail: the scaler needs the norm partials");
-    hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, S(stream), lr, kl, kl_threshold, min_lr, max_lr, step, mb_idx,
-                       n_minibatches, stat_idx, scaler, sqnorm_partials, nblk_norm, growth_interval);
+    const ppo_tail_args_t t{lr, kl, kl_threshold, min_lr, max_lr, step, mb_idx, n_minibatches, stat_idx, scaler,
+                            growth_interval, nullptr};
+    if (const int rc = check_tail(t, sqnorm_partials)) return rc;
+    hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, S(stream), t, sqnorm_partials, nblk_norm);
     return launched("k_tail");
 }
 
