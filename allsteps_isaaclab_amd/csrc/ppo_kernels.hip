@@ -231,13 +231,31 @@ __device__ __forceinline__ float max_grad(float u1, float u2, float g1, float g2
 // conflict-free.
 constexpr int kLossRows = 128;
 
+// ppo_loss_finalize's output for value k of the block-partial sums (s = the sum over blocks)
+__device__ __forceinline__ void loss_finalize_value(int k, float s, int A, int mb_rows, float entropy_coef,
+                                                    const float* __restrict__ grad_scale, float* __restrict__ g_hb,
+                                                    float* __restrict__ g_ls, float* __restrict__ stats,
+                                                    const int32_t* __restrict__ stat_idx, float* __restrict__ kl_out) {
+    if (k <= A) {
+        g_hb[k] = s;
+    } else if (k <= 2 * A) {
+        // - entropy_coef * mean(entropy): d/d logstd_j = -entropy_coef (times the loss scale)
+        g_ls[k - A - 1] = s - entropy_coef * (grad_scale ? *grad_scale : 1.f);
+    } else {
+        const int st = k - 2 * A - 1;
+        const float mean = s / float(mb_rows);
+        stats[int64_t(*stat_idx) * PPO_LOSS_NSTAT + st] = mean;
+        if (st == 4) *kl_out = mean;
+    }
+}
+
 template <int A>
 __global__ void __launch_bounds__(kLossRows) k_loss_grad(
     const float* __restrict__ head, const float* __restrict__ logstd, int mb_rows, const int32_t* __restrict__ mb_idx,
     const float* __restrict__ actions, float* __restrict__ ds_mu, float* __restrict__ ds_sigma,
     const float* __restrict__ old_nlp, const float* __restrict__ adv_, const float* __restrict__ old_v,
     const float* __restrict__ ret_, ppo_loss_cfg_t cfg, const float* __restrict__ grad_scale, float* __restrict__ dhead,
-    float* __restrict__ partials, uint16_t* __restrict__ dhead_lp, int lp_dtype) {
+    float* __restrict__ partials, uint16_t* __restrict__ dhead_lp, int lp_dtype, ppo_loss_fin_t fin) {
     static_assert(A + 1 <= 32, "heads of at most 32 outputs");
     constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
     constexpr int AP = A | 1, HP = (A + 1) | 1, RP = NV | 1;
@@ -391,6 +409,30 @@ __global__ void __launch_bounds__(kLossRows) k_loss_grad(
         }
         partials[int64_t(blockIdx.x) * NV + tid] = (t[0] + t[1]) + (t[2] + t[3]);
     }
+    if (!fin.counter) return;  // uniform
+    // fused finalize: the last block to finish sums every block's partials (thread k: value k, fixed order)
+    __shared__ int last_s;
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();
+        last_s = atomicAdd(fin.counter, 1) == int(gridDim.x) - 1;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    __threadfence();
+    if (tid < NV) {
+        const int nblk = gridDim.x;
+        float t[4] = {0.f, 0.f, 0.f, 0.f};
+        int b = 0;
+        for (; b + 4 <= nblk; b += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] += partials[int64_t(b + u) * NV + tid];
+        }
+        for (; b < nblk; ++b) t[0] += partials[int64_t(b) * NV + tid];
+        loss_finalize_value(tid, (t[0] + t[1]) + (t[2] + t[3]), A, mb_rows, fin.entropy_coef, grad_scale, fin.grad_head_bias,
+                            fin.grad_logstd, fin.stats, fin.stat_idx, fin.kl_out);
+    }
+    if (tid == 0) atomicExch(fin.counter, 0);
 }
 
 __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ partials, int nblk, int A, int mb_rows,
@@ -414,17 +456,7 @@ __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ 
     float s = (sa[0] + sa[1]) + (sa[2] + sa[3]);
     s = wave_sum(s);
     if (threadIdx.x != 0) return;
-    if (k <= A) {
-        g_hb[k] = s;
-    } else if (k <= 2 * A) {
-        // - entropy_coef * mean(entropy): d/d logstd_j = -entropy_coef (times the loss scale)
-        g_ls[k - A - 1] = s - entropy_coef * (grad_scale ? *grad_scale : 1.f);
-    } else {
-        const int st = k - 2 * A - 1;
-        const float mean = s / float(mb_rows);
-        stats[int64_t(*stat_idx) * PPO_LOSS_NSTAT + st] = mean;
-        if (st == 4) *kl_out = mean;
-    }
+    loss_finalize_value(k, s, A, mb_rows, entropy_coef, grad_scale, g_hb, g_ls, stats, stat_idx, kl_out);
 }
 
 // ------------------------------------------------------------------------------ ELU backward
@@ -887,11 +919,11 @@ int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, in
 
 int ppo_loss_blocks(int32_t mb_rows) { return (mb_rows + kLossRows - 1) / kLossRows; }
 
-int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
-                  const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
-                  const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
-                  const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
-                  void* stream) {
+static int launch_loss(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
+                       const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
+                       const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
+                       const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
+                       const ppo_loss_fin_t& fin, void* stream) {
     if (dhead_lp && lp_dtype != PPO_DT_BF16 && lp_dtype != PPO_DT_F16)
         return fail(-1, "ppo_loss_grad: dhead_lp needs lp_dtype PPO_DT_BF16 or PPO_DT_F16");
     const dim3 grid(ppo_loss_blocks(mb_rows)), block(kLossRows);
@@ -899,7 +931,7 @@ int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_
     case AA:                                                                                                     \
         hipLaunchKernelGGL(k_loss_grad<AA>, grid, block, 0, S(stream), head, logstd, mb_rows, mb_idx, actions, \
                            ds_mu, ds_sigma, old_neglogp, advantages, old_values, returns, cfg, grad_scale, dhead,  \
-                           partials, dhead_lp, lp_dtype);                                                                           \
+                           partials, dhead_lp, lp_dtype, fin);                                                  \
         break;
     switch (A) {
         PPO_LOSS_CASE(2)
@@ -910,6 +942,27 @@ int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_
     }
 #undef PPO_LOSS_CASE
     return launched("k_loss_grad");
+}
+
+int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
+                  const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
+                  const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
+                  const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
+                  void* stream) {
+    return launch_loss(head, logstd, A, mb_rows, mb_idx, actions, ds_mu, ds_sigma, old_neglogp, advantages, old_values,
+                       returns, cfg, grad_scale, dhead, partials, dhead_lp, lp_dtype, ppo_loss_fin_t{}, stream);
+}
+
+int ppo_loss_grad_fin(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
+                      const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
+                      const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
+                      const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
+                      const ppo_loss_fin_t* fin, void* stream) {
+    if (!fin || !fin->counter || !fin->grad_head_bias || !fin->grad_logstd || !fin->stats || !fin->stat_idx ||
+        !fin->kl_out)
+        return fail(-1, "ppo_loss_grad_fin: null finalize argument");
+    return launch_loss(head, logstd, A, mb_rows, mb_idx, actions, ds_mu, ds_sigma, old_neglogp, advantages, old_values,
+                       returns, cfg, grad_scale, dhead, partials, dhead_lp, lp_dtype, *fin, stream);
 }
 
 int ppo_loss_finalize(const float* partials, int32_t nblk, int32_t A, int32_t mb_rows, float entropy_coef,

@@ -76,6 +76,11 @@ class PpoWgrad(C.Structure):
                 ("dtype", C.c_int32)]
 
 
+class PpoLossFin(C.Structure):
+    _fields_ = [("entropy_coef", C.c_float), ("grad_head_bias", C.c_void_p), ("grad_logstd", C.c_void_p),
+                ("stats", C.c_void_p), ("stat_idx", C.c_void_p), ("kl_out", C.c_void_p), ("counter", C.c_void_p)]
+
+
 class PpoTailArgs(C.Structure):
     _fields_ = [("lr", C.c_void_p), ("kl", C.c_void_p), ("kl_threshold", C.c_float), ("min_lr", C.c_double),
                 ("max_lr", C.c_double), ("step", C.c_void_p), ("mb_idx", C.c_void_p), ("n_minibatches", C.c_int32),
@@ -93,7 +98,8 @@ EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
                     "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update",
-                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_adam_tail"]
+                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_adam_tail",
+                    "ppo_loss_grad_fin"]
 
 
 def load() -> C.CDLL:
@@ -111,6 +117,8 @@ def load() -> C.CDLL:
     L.ppo_obs_normalize.argtypes = [V, V, I32, I32, V, V, F32, V, I32, I32, I32, V]
     L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V, V, I32, V]
     L.ppo_loss_finalize.argtypes = [V, I32, I32, I32, F32, V, V, V, V, V, V, V]
+    L.ppo_loss_grad_fin.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V, V, I32,
+                                    C.POINTER(PpoLossFin), V]
     L.ppo_elu_bwd.argtypes = [V, I32, V, I32, V, I32, I32, I32, V, V]
     L.ppo_sqnorm.argtypes = [V, I64, V, V, V]
     L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32, V, V]
@@ -234,6 +242,8 @@ class FusedPPOUpdate:
         self.norm_partials = torch.empty(2 * L.ppo_sqnorm_blocks(), device=dev)  # norm sums | non-finite counts
         self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.tail_counter = torch.zeros(1, device=dev, dtype=torch.int32)  # ppo_adam_tail's finished-block count
+        self.loss_counter = torch.zeros(1, device=dev, dtype=torch.int32)  # ppo_loss_grad_fin's
+        self._loss_fin = PpoLossFin()
         self._tail_args = PpoTailArgs()
         self.stat_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stats = torch.zeros(agent.mini_epochs_num * self.n_mb + 1, PPO_LOSS_NSTAT, device=dev)
@@ -478,14 +488,17 @@ class FusedPPOUpdate:
         nl = len(self.linears)
         # no zero_grad: every entry of the [grads | kl] bucket is written below (loss finalize: head
         # biases, log-sigma, kl; the reduce jobs: every weight and bias gradient)
-        _check(L.ppo_loss_grad(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
-                               _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
-                               _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.scaler),
-                               None if self.mfma_trunk else _p(self.dhead), _p(self.loss_partials),
-                               _p(self.dhead_lp) if self.mfma_trunk else None, self.dt_code, s), "ppo_loss_grad")
-        _check(L.ppo_loss_finalize(_p(self.loss_partials), self.loss_partials.shape[0], A, B,
-                                   self.loss_cfg.entropy_coef, _p(self.scaler), _p(self.gbh), _p(self.gls),
-                                   _p(self.stats), _p(self.stat_idx), _p(self.flat.extra), s), "ppo_loss_finalize")
+        # losses, KL, head gradients, and (the kernel's last block) their sums over the minibatch
+        fin = self._loss_fin
+        fin.entropy_coef, fin.grad_head_bias, fin.grad_logstd = self.loss_cfg.entropy_coef, _p(self.gbh), _p(self.gls)
+        fin.stats, fin.stat_idx, fin.kl_out, fin.counter = (_p(self.stats), _p(self.stat_idx), _p(self.flat.extra),
+                                                            _p(self.loss_counter))
+        _check(L.ppo_loss_grad_fin(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
+                                   _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
+                                   _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.scaler),
+                                   None if self.mfma_trunk else _p(self.dhead), _p(self.loss_partials),
+                                   _p(self.dhead_lp) if self.mfma_trunk else None, self.dt_code, C.byref(fin), s),
+               "ppo_loss_grad_fin")
         S = self.S
         hl = self.h_last_f
         jobs, keep = [], []

@@ -647,6 +647,61 @@ def test_adam_tail_launch_equals_adam_then_tail(bad):
     assert float(lr) == pytest.approx(3e-4 / 1.5)  # kl 0.03 > 2 x 0.008
 
 
+@pytest.mark.gpu
+def test_loss_grad_fin_launch_equals_grad_then_finalize():
+    """ppo_loss_grad_fin (the finalize run by the loss kernel's last block) vs ppo_loss_grad then
+    ppo_loss_finalize on the same minibatch: per-row outputs (dhead, its 16-bit copy, the dataset's new
+    mu / sigma, the block partials) bit for bit; the sums (head-bias and log-sigma gradients, statistics,
+    KL) to fp32 rounding (another fixed summation order); the block counter back at 0."""
+    import ctypes as C
+
+    from allsteps_isaaclab_amd.learning import fused as FU
+
+    L = FU.load()
+    dev, A, B = "cuda:0", 21, 4000
+    g = torch.Generator(device=dev).manual_seed(4)
+    r = lambda *sh: torch.randn(*sh, device=dev, generator=g)  # noqa: E731
+    head = r(B, A + 1) * 0.5
+    logstd = r(A) * 0.1
+    idx = torch.tensor([1], device=dev, dtype=torch.int32)
+    ds = {"actions": r(2 * B, A), "mu": r(2 * B, A) * 0.3, "sigma": torch.exp(r(2 * B, A) * 0.1),
+          "nlp": r(2 * B).abs() * 5 + 20, "adv": r(2 * B), "v": r(2 * B), "ret": r(2 * B)}
+    cfg = FU.PpoLossCfg(0.2, 4.0, 0.0, 1e-4, 1.1, 1, 1, 1)
+    scale = torch.tensor([1024.0], device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    nblk = L.ppo_loss_blocks(B)
+    outs = []
+    for fused in (False, True):
+        d = {k: v.clone() for k, v in ds.items()}
+        dhead, dlp = torch.zeros(B, A + 1, device=dev), torch.zeros(B, 32, device=dev, dtype=torch.float16)
+        part = torch.zeros(nblk, 2 * A + 1 + 5, device=dev)
+        ghb, gls, stats = torch.zeros(A + 1, device=dev), torch.zeros(A, device=dev), torch.zeros(3, 5, device=dev)
+        sidx, kl, ctr = torch.tensor([2], device=dev, dtype=torch.int32), torch.zeros(1, device=dev), \
+            torch.zeros(1, device=dev, dtype=torch.int32)
+        args = (head.data_ptr(), logstd.data_ptr(), A, B, idx.data_ptr(), d["actions"].data_ptr(), d["mu"].data_ptr(),
+                d["sigma"].data_ptr(), d["nlp"].data_ptr(), d["adv"].data_ptr(), d["v"].data_ptr(), d["ret"].data_ptr(),
+                cfg, scale.data_ptr(), dhead.data_ptr(), part.data_ptr(), dlp.data_ptr(), FU.PPO_DT[torch.float16])
+        if fused:
+            fin = FU.PpoLossFin(0.01, ghb.data_ptr(), gls.data_ptr(), stats.data_ptr(), sidx.data_ptr(), kl.data_ptr(),
+                                ctr.data_ptr())
+            FU._check(L.ppo_loss_grad_fin(*args, C.byref(fin), s), "ppo_loss_grad_fin")
+        else:
+            FU._check(L.ppo_loss_grad(*args, s), "ppo_loss_grad")
+            FU._check(L.ppo_loss_finalize(part.data_ptr(), nblk, A, B, 0.01, scale.data_ptr(), ghb.data_ptr(),
+                                          gls.data_ptr(), stats.data_ptr(), sidx.data_ptr(), kl.data_ptr(), s),
+                      "ppo_loss_finalize")
+        torch.cuda.synchronize()
+        outs.append(([dhead, dlp, d["mu"], d["sigma"], part], [ghb, gls, stats, kl], ctr))
+    (exact_a, sums_a, _), (exact_b, sums_b, ctr) = outs
+    for a, b in zip(exact_a, exact_b):
+        assert torch.equal(a, b)
+    for a, b in zip(sums_a, sums_b):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    assert int(ctr) == 0
+    assert torch.equal(dlp[:, A + 1:], torch.zeros_like(dlp[:, A + 1:]))
+    torch.testing.assert_close(dlp[:, :A + 1].float(), exact_b[0], rtol=1e-3, atol=1e-7)
+
+
 def test_weight_grads_rejects_bad_arguments():
     import ctypes as C
 
