@@ -399,7 +399,10 @@ __global__ void __launch_bounds__(kLossRows) k_loss_grad(
         ds_mu[base * A + e] = s_mu[rr * AP + c];
         ds_sigma[base * A + e] = s_sg[c];
     }
-    // block partials: column k summed over the block's rows in a fixed order (four chains)
+    // block partials: column k summed over the block's rows in a fixed order (four chains).  With the fused
+    // finalize they are handed to the last block without fences (MI355X_MICROARCH.md, the hand-off table's
+    // first row): agent-scope (sc1) stores, each storing wave's vmcnt(0), a workgroup barrier, ONE
+    // relaxed agent-scope counter add; the block whose add returns the last count reads them with sc1 loads
     if (tid < NV) {
         float t[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
@@ -407,32 +410,33 @@ __global__ void __launch_bounds__(kLossRows) k_loss_grad(
 #pragma unroll
             for (int u = 0; u < 4; ++u) t[u] += s_red[(rr + u) * RP + tid];
         }
-        partials[int64_t(blockIdx.x) * NV + tid] = (t[0] + t[1]) + (t[2] + t[3]);
+        __hip_atomic_store(partials + int64_t(blockIdx.x) * NV + tid, (t[0] + t[1]) + (t[2] + t[3]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!fin.counter) return;  // uniform
     // fused finalize: the last block to finish sums every block's partials (thread k: value k, fixed order)
     __shared__ int last_s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-        __threadfence();
-        last_s = atomicAdd(fin.counter, 1) == int(gridDim.x) - 1;
-    }
+    if (tid == 0)
+        last_s = __hip_atomic_fetch_add(fin.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == int(gridDim.x) - 1;
     __syncthreads();
     if (!last_s) return;
-    __threadfence();
     if (tid < NV) {
         const int nblk = gridDim.x;
         float t[4] = {0.f, 0.f, 0.f, 0.f};
         int b = 0;
         for (; b + 4 <= nblk; b += 4) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) t[u] += partials[int64_t(b + u) * NV + tid];
+            for (int u = 0; u < 4; ++u)
+                t[u] += __hip_atomic_load(partials + int64_t(b + u) * NV + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        for (; b < nblk; ++b) t[0] += partials[int64_t(b) * NV + tid];
+        for (; b < nblk; ++b)
+            t[0] += __hip_atomic_load(partials + int64_t(b) * NV + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         loss_finalize_value(tid, (t[0] + t[1]) + (t[2] + t[3]), A, mb_rows, fin.entropy_coef, grad_scale, fin.grad_head_bias,
                             fin.grad_logstd, fin.stats, fin.stat_idx, fin.kl_out);
     }
-    if (tid == 0) atomicExch(fin.counter, 0);
+    if (tid == 0) __hip_atomic_store(fin.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ partials, int nblk, int A, int mb_rows,
@@ -847,17 +851,20 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
         }
     }
     if (TAIL) {
+        // no data is handed between workgroups here, only an order: every workgroup's thread 0 read lr /
+        // step / scaler (and used them) in the prologue, before its counter add below, and the tail writes
+        // them after the last add has returned; the next launch sees the writes at the kernel boundary.  So
+        // a relaxed agent-scope counter suffices -- no fences (MI355X_MICROARCH.md: an agent release
+        // writes back the XCD's L2, microseconds per workgroup)
         __shared__ int last_s;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            last_s = atomicAdd(tail.counter, 1) == int(gridDim.x) - 1;
-        }
+        if (threadIdx.x == 0)
+            last_s = __hip_atomic_fetch_add(tail.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     int(gridDim.x) - 1;
         __syncthreads();
         if (last_s && threadIdx.x == 0) {
-            __threadfence();
             tail_update(tail, skip);
-            atomicExch(tail.counter, 0);
+            __hip_atomic_store(tail.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

@@ -225,6 +225,9 @@ __device__ __forceinline__ void mma_rows(const uint16_t* X, const typename Lp<DT
     }
 }
 
+#ifndef PPO_MLP_PRIO
+#define PPO_MLP_PRIO 0  // A/B knob (scripts/mlp_ab.py): static s_setprio 1 for waves 4..7 of the trunk kernels
+#endif
 #ifndef PPO_FWD_DBG
 #define PPO_FWD_DBG 0  // timing-only builds (scripts/fwd_dbg.sh): 2 no exp, 4 no stores, 16 no MFMA, 32 no ELU / convert
 #endif
@@ -361,6 +364,9 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     uint16_t* X0 = lds;
     uint16_t* X1 = lds + kFRows * kXs;
     const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+#if PPO_MLP_PRIO
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half wins VALU arbitration
+#endif
     const int j = lane & 31, h = lane >> 5, i = lane & 31;
     const int F0 = 32 * wave;                 // this wave's output features
     const int row0 = blockIdx.x * kFRows;
@@ -555,6 +561,9 @@ __global__ void __launch_bounds__(kFThreads, 1) k_mlp_bwd(ppo_mlp_bwd_t a) {
     uint16_t* X0 = lds;
     uint16_t* X1 = lds + kFRows * kXs;
     const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+#if PPO_MLP_PRIO
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half wins VALU arbitration
+#endif
     const int j = lane & 31, h = lane >> 5, i = lane & 31;
     const int F0 = 32 * wave;
     const int row0 = blockIdx.x * kFRows;

@@ -337,7 +337,13 @@ def test_fused_train_epoch_runs_graph_replays(tmp_path):
     assert not torch.equal(p0, fus.flat.params)
     n = fus.mini_epochs_num * len(fus.dataset)
     assert int(fus.fused.stat_idx) == n and int(fus.fused.mb_idx) == 0
-    assert float(fus.optimizer.step_t) == n
+    # the synthetic dataset's random old neglogp gives some rows a ratio of ~1e4: with the 16-bit head
+    # gradient autocast hands the heads' Linear backward, such a minibatch overflows fp16 at scale 2^16 and
+    # GradScaler skips it (scale halved, Adam's step count kept) -- the reference's behaviour too
+    from allsteps_isaaclab_amd.learning.fused import SCALER_INIT
+    skips = round(math.log2(SCALER_INIT / float(fus.scaler_state[0])))
+    assert 0 <= skips < n
+    assert float(fus.optimizer.step_t) == n - skips
     assert len(fus.fused.graphs) == 3  # A (normaliser updating), A (frozen), B
     assert all(isinstance(g, torch.cuda.CUDAGraph) for g in fus.fused.graphs.values())
 
