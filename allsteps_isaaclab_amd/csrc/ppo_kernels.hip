@@ -222,14 +222,17 @@ __device__ __forceinline__ float max_grad(float u1, float u2, float g1, float g2
     return u1 > u2 ? g1 : (u2 > u1 ? g2 : 0.5f * (g1 + g2));
 }
 
-// One row per lane (round 5; the round-4 form spread a row over a 32-lane group and summed it with
-// shuffles, leaving 10 of 32 lanes idle and the row sums as chains of LDS-routed permutes): a block of
-// kLossRows lanes stages its rows of the dataset (actions, mu, sigma: A floats each) and of the heads
-// through LDS with coalesced loads, each lane then runs its row's action loop in registers, and the
-// per-row contributions to the column sums land in an LDS table that kNV threads sum down in a fixed
-// order (deterministic).  Row pitches in LDS are odd (in dwords), so the row-per-lane reads are
-// conflict-free.
-constexpr int kLossRows = 128;
+// Eight lanes per row (round 5; the round-4 form spread a row over a 32-lane group -- 10 of 32 lanes idle,
+// the row sums as chains of LDS-routed permutes; a one-row-per-lane form ran out of parallelism, 512
+// waves for a 32768-row minibatch).  Lane g of a row owns head columns NJ*g .. NJ*g + NJ - 1 (the
+// actions, then the value column A; NJ = ceil((A + 1) / 8)), so a row's loads are one contiguous run
+// across its eight lanes; the row sums (sum d^2, the KL, the bound loss) are three DPP steps inside the
+// eight lanes (bit-identical on every lane); the per-row scalar work (ratio, clipping) runs on all eight.
+// The per-row contributions to the column sums land in an LDS table that NV threads sum down in row order
+// (deterministic), one partial row per block.
+constexpr int kLossLanes = 8;
+constexpr int kLossRows = 128;                         // rows per block
+constexpr int kLossThreads = kLossRows * kLossLanes;   // 1024
 
 // ppo_loss_finalize's output for value k of the block-partial sums (s = the sum over blocks)
 __device__ __forceinline__ void loss_finalize_value(int k, float s, int A, int mb_rows, float entropy_coef,
@@ -249,157 +252,154 @@ __device__ __forceinline__ void loss_finalize_value(int k, float s, int A, int m
     }
 }
 
+// sum over the eight lanes of a row (xor 1, xor 2 by quad permutes, then the mirrored half-row): the same
+// two operands meet on every lane, so all eight hold the bit-identical sum
+__device__ __forceinline__ float sum8(float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
+    return x;
+}
+
 template <int A>
-__global__ void __launch_bounds__(kLossRows) k_loss_grad(
+__global__ void __launch_bounds__(kLossThreads) k_loss_grad(
     const float* __restrict__ head, const float* __restrict__ logstd, int mb_rows, const int32_t* __restrict__ mb_idx,
     const float* __restrict__ actions, float* __restrict__ ds_mu, float* __restrict__ ds_sigma,
     const float* __restrict__ old_nlp, const float* __restrict__ adv_, const float* __restrict__ old_v,
     const float* __restrict__ ret_, ppo_loss_cfg_t cfg, const float* __restrict__ grad_scale, float* __restrict__ dhead,
     float* __restrict__ partials, uint16_t* __restrict__ dhead_lp, int lp_dtype, ppo_loss_fin_t fin) {
     static_assert(A + 1 <= 32, "heads of at most 32 outputs");
-    constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT;
-    constexpr int AP = A | 1, HP = (A + 1) | 1, RP = NV | 1;
-    __shared__ float s_act[kLossRows * AP], s_mu[kLossRows * AP], s_sig[kLossRows * AP], s_head[kLossRows * HP];
-    __shared__ float s_red[kLossRows * RP];
-    __shared__ float s_sg[A], s_ls[A];
-    const int tid = threadIdx.x;
-    const int r0 = blockIdx.x * kLossRows;
-    const int nr = min(kLossRows, mb_rows - r0);
-    const int64_t base = int64_t(*mb_idx) * mb_rows + r0;  // dataset row of the block's row 0
-    for (int e = tid; e < nr * A; e += kLossRows) {
-        const int r = e / A, c = e - r * A;
-        s_act[r * AP + c] = actions[base * A + e];
-        s_mu[r * AP + c] = ds_mu[base * A + e];
-        s_sig[r * AP + c] = ds_sigma[base * A + e];
-    }
-    for (int e = tid; e < nr * (A + 1); e += kLossRows) {
-        const int r = e / (A + 1), c = e - r * (A + 1);
-        s_head[r * HP + c] = head[int64_t(r0) * (A + 1) + e];
-    }
-    if (tid < A) {
-        s_ls[tid] = logstd[tid];
-        s_sg[tid] = expf(logstd[tid]);
-    }
-    __syncthreads();
+    constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT, RP = NV | 1;
+    constexpr int NJ = (A + 1 + kLossLanes - 1) / kLossLanes;
+    __shared__ float s_red[2 * kLossRows * RP];  // per-row contributions; the finalize's block partials
+    __shared__ int last_s;
+    const int tid = threadIdx.x, g = tid % kLossLanes, rl = tid / kLossLanes;
+    const int r = blockIdx.x * kLossRows + rl;  // minibatch row
+    const bool ok = r < mb_rows;
+    const int64_t row = int64_t(*mb_idx) * mb_rows + (ok ? r : 0);
     // the loss scale (a power of two, GradScaler) enters every gradient through the 1/B factor: exact
     const float inv_b = (grad_scale ? *grad_scale : 1.f) * (1.f / float(mb_rows));
     float sum_ls = 0.f;
 #pragma unroll
-    for (int j = 0; j < A; ++j) sum_ls += s_ls[j];
+    for (int j = 0; j < A; ++j) sum_ls += logstd[j];
     const float entropy = float(A) * (0.5f + 0.5f * kLog2Pi) + sum_ls;
-    const int r = tid;
-    float* red = s_red + r * RP;
-    if (r < nr) {
-        const int64_t row = base + r;
-        const float* hr = s_head + r * HP;
-        const float* ar = s_act + r * AP;
-        float* mr = s_mu + r * AP;
-        const float* sr = s_sig + r * AP;
-        // policy: d_j = (a_j - mu_j) / sigma_j; nlp = 0.5 sum d^2 + 0.5 log(2 pi) A + sum logstd;
-        // policy_kl(p0 = current, p1 = dataset); the bound loss
-        float d[A];
-        float q = 0.f, kl = 0.f, bl = 0.f;
+    float hj[NJ], av[NJ], m1[NJ], s1[NJ], sg[NJ];
 #pragma unroll
-        for (int j = 0; j < A; ++j) {
-            const float hj = hr[j], sg = s_sg[j], s1 = sr[j];
-            d[j] = (ar[j] - hj) / sg;
-            q += d[j] * d[j];
-            const float dm = mr[j] - hj;
-            kl += logf(s1 / sg + 1e-5f) + (sg * sg + dm * dm) / (2.f * (s1 * s1 + 1e-5f)) - 0.5f;
+    for (int k = 0; k < NJ; ++k) {
+        const int j = NJ * g + k;
+        const bool act = ok && j < A;
+        hj[k] = ok && j <= A ? head[int64_t(r) * (A + 1) + j] : 0.f;
+        av[k] = act ? actions[row * A + j] : 0.f;
+        m1[k] = act ? ds_mu[row * A + j] : 0.f;
+        s1[k] = act ? ds_sigma[row * A + j] : 1.f;
+        sg[k] = j < A ? expf(logstd[j]) : 1.f;
+    }
+    const float onlp = ok ? old_nlp[row] : 0.f, adv = ok ? adv_[row] : 0.f;
+    const float vp = ok ? old_v[row] : 0.f, Rt = ok ? ret_[row] : 0.f;
+    // policy: d_j = (a_j - mu_j) / sigma_j; nlp = 0.5 sum d^2 + 0.5 log(2 pi) A + sum logstd;
+    // policy_kl(p0 = current, p1 = dataset); the bound loss
+    float d[NJ];
+    float q = 0.f, kl = 0.f, bl = 0.f;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+        d[k] = 0.f;
+        if (NJ * g + k < A) {
+            d[k] = (av[k] - hj[k]) / sg[k];
+            q += d[k] * d[k];
+            const float dm = m1[k] - hj[k];
+            kl += logf(s1[k] / sg[k] + 1e-5f) + (sg[k] * sg[k] + dm * dm) / (2.f * (s1[k] * s1[k] + 1e-5f)) - 0.5f;
             if (cfg.bound_loss == 1) {
-                const float lo = fminf(hj + cfg.soft_bound, 0.f), hi = fmaxf(hj - cfg.soft_bound, 0.f);
+                const float lo = fminf(hj[k] + cfg.soft_bound, 0.f), hi = fmaxf(hj[k] - cfg.soft_bound, 0.f);
                 bl += lo * lo + hi * hi;
             } else if (cfg.bound_loss == 2) {
-                bl += hj * hj;
+                bl += hj[k] * hj[k];
             }
         }
-        const float nlp = 0.5f * q + 0.5f * kLog2Pi * float(A) + sum_ls;
-        const float adv = adv_[row];
-        float a_loss, g_nlp;
-        if (cfg.ppo) {
-            const float ratio = expf(old_nlp[row] - nlp);
-            const float rc = fminf(fmaxf(ratio, 1.f - cfg.e_clip), 1.f + cfg.e_clip);
-            const float u1 = -adv * ratio, u2 = -adv * rc;
-            const bool inside = ratio >= 1.f - cfg.e_clip && ratio <= 1.f + cfg.e_clip;
-            // d(-adv * ratio)/d nlp = adv * ratio (d ratio / d nlp = -ratio); torch.maximum ties split
-            g_nlp = max_grad(u1, u2, adv * ratio, inside ? adv * ratio : 0.f);
-            a_loss = fmaxf(u1, u2);
-        } else {
-            a_loss = nlp * adv;
-            g_nlp = adv;
-        }
-        g_nlp *= inv_b;
-        float gh[32];  // d loss / d head of this row, 0 past the value column
+    }
+    q = sum8(q);
+    kl = sum8(kl);
+    bl = sum8(bl);
+    const float nlp = 0.5f * q + 0.5f * kLog2Pi * float(A) + sum_ls;
+    float a_loss, g_nlp;
+    if (cfg.ppo) {
+        const float ratio = expf(onlp - nlp);
+        const float rc = fminf(fmaxf(ratio, 1.f - cfg.e_clip), 1.f + cfg.e_clip);
+        const float u1 = -adv * ratio, u2 = -adv * rc;
+        const bool inside = ratio >= 1.f - cfg.e_clip && ratio <= 1.f + cfg.e_clip;
+        // d(-adv * ratio)/d nlp = adv * ratio (d ratio / d nlp = -ratio); torch.maximum ties split
+        g_nlp = max_grad(u1, u2, adv * ratio, inside ? adv * ratio : 0.f);
+        a_loss = fmaxf(u1, u2);
+    } else {
+        a_loss = nlp * adv;
+        g_nlp = adv;
+    }
+    g_nlp *= inv_b;
+    float* red = s_red + rl * RP;
+    float gh[NJ];  // d loss / d head for this lane's columns (0 past the value column)
 #pragma unroll
-        for (int j = 0; j < 32; ++j) gh[j] = 0.f;
-#pragma unroll
-        for (int j = 0; j < A; ++j) {
-            const float hj = hr[j], sg = s_sg[j];
+    for (int k = 0; k < NJ; ++k) {
+        const int j = NJ * g + k;
+        gh[k] = 0.f;
+        if (j < A) {
             float dbj = 0.f;
             if (cfg.bound_loss == 1) {
-                const float lo = fminf(hj + cfg.soft_bound, 0.f), hi = fmaxf(hj - cfg.soft_bound, 0.f);
+                const float lo = fminf(hj[k] + cfg.soft_bound, 0.f), hi = fmaxf(hj[k] - cfg.soft_bound, 0.f);
                 dbj = 2.f * (lo + hi);
             } else if (cfg.bound_loss == 2) {
-                dbj = 2.f * hj;
+                dbj = 2.f * hj[k];
             }
             // d nlp / d mu = -d / sigma ; d nlp / d logstd = 1 - d^2
-            gh[j] = -g_nlp * d[j] / sg + cfg.bounds_coef * inv_b * dbj;
-            red[j] = gh[j];
-            red[A + 1 + j] = g_nlp * (1.f - d[j] * d[j]);
-            mr[j] = hj;  // dataset.update_mu_sigma (written out below, coalesced)
-        }
-        // critic
-        const float v = hr[A], vp = old_v[row], Rt = ret_[row];
-        float c_loss, g_v;
-        if (cfg.clip_value) {
-            const float dv = v - vp;
-            const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
-            const float l1 = (v - Rt) * (v - Rt), l2 = (vc - Rt) * (vc - Rt);
-            const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
-            g_v = max_grad(l1, l2, 2.f * (v - Rt), inside ? 2.f * (vc - Rt) : 0.f);
-            c_loss = fmaxf(l1, l2);
-        } else {
-            c_loss = (Rt - v) * (Rt - v);
-            g_v = 2.f * (v - Rt);
-        }
-        g_v *= 0.5f * cfg.critic_coef * inv_b;
-        gh[A] = g_v;
-        red[A] = g_v;
-        red[2 * A + 1 + 0] = a_loss;
-        red[2 * A + 1 + 1] = c_loss;
-        red[2 * A + 1 + 2] = bl;
-        red[2 * A + 1 + 3] = entropy;
-        red[2 * A + 1 + 4] = kl;
-        if (dhead) {
-            float* dh = dhead + int64_t(r0 + r) * (A + 1);
-#pragma unroll
-            for (int j = 0; j <= A; ++j) dh[j] = gh[j];
-        }
-        // the 16-bit copy (autocast: the gradient reaching the heads' fp16 Linear is fp16): 64 B per row
-        if (dhead_lp) {
-            uint32_t w[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const uint32_t lo = lp_dtype == PPO_DT_F16 ? f32_to_f16(gh[2 * k]) : f32_to_bf16(gh[2 * k]);
-                const uint32_t hi = lp_dtype == PPO_DT_F16 ? f32_to_f16(gh[2 * k + 1]) : f32_to_bf16(gh[2 * k + 1]);
-                w[k] = lo | (hi << 16);
+            gh[k] = -g_nlp * d[k] / sg[k] + cfg.bounds_coef * inv_b * dbj;
+            red[j] = ok ? gh[k] : 0.f;
+            red[A + 1 + j] = ok ? g_nlp * (1.f - d[k] * d[k]) : 0.f;
+            if (ok) {
+                ds_mu[row * A + j] = hj[k];  // dataset.update_mu_sigma
+                ds_sigma[row * A + j] = sg[k];
             }
-            uint4* dst = reinterpret_cast<uint4*>(dhead_lp + int64_t(r0 + r) * 32);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        } else if (j == A) {  // critic
+            const float v = hj[k];
+            float c_loss, g_v;
+            if (cfg.clip_value) {
+                const float dv = v - vp;
+                const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
+                const float l1 = (v - Rt) * (v - Rt), l2 = (vc - Rt) * (vc - Rt);
+                const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
+                g_v = max_grad(l1, l2, 2.f * (v - Rt), inside ? 2.f * (vc - Rt) : 0.f);
+                c_loss = fmaxf(l1, l2);
+            } else {
+                c_loss = (Rt - v) * (Rt - v);
+                g_v = 2.f * (v - Rt);
+            }
+            g_v *= 0.5f * cfg.critic_coef * inv_b;
+            gh[k] = g_v;
+            red[A] = ok ? g_v : 0.f;
+            red[2 * A + 1 + 1] = ok ? c_loss : 0.f;
         }
-    } else {
+    }
+    if (g == 0) {
+        red[2 * A + 1 + 0] = ok ? a_loss : 0.f;
+        red[2 * A + 1 + 2] = ok ? bl : 0.f;
+        red[2 * A + 1 + 3] = ok ? entropy : 0.f;
+        red[2 * A + 1 + 4] = ok ? kl : 0.f;
+    }
+    if (ok) {
+        if (dhead) {
 #pragma unroll
-        for (int k = 0; k < NV; ++k) red[k] = 0.f;
+            for (int k = 0; k < NJ; ++k)
+                if (NJ * g + k <= A) dhead[int64_t(r) * (A + 1) + NJ * g + k] = gh[k];
+        }
+        // the 16-bit copy (autocast: the gradient reaching the heads' fp16 Linear is fp16), rows x 32, zero
+        // past the value column
+        if (dhead_lp) {
+            uint16_t* dl = dhead_lp + int64_t(r) * 32;
+#pragma unroll
+            for (int k = 0; k < NJ; ++k)
+                if (NJ * g + k < 32) dl[NJ * g + k] = lp_dtype == PPO_DT_F16 ? f32_to_f16(gh[k]) : f32_to_bf16(gh[k]);
+            for (int c = NJ * kLossLanes + g; c < 32; c += kLossLanes) dl[c] = 0;
+        }
     }
     __syncthreads();
-    // new mu / sigma into the dataset rows (coalesced)
-    for (int e = tid; e < nr * A; e += kLossRows) {
-        const int rr = e / A, c = e - rr * A;
-        ds_mu[base * A + e] = s_mu[rr * AP + c];
-        ds_sigma[base * A + e] = s_sg[c];
-    }
-    // block partials: column k summed over the block's rows in a fixed order (four chains).  With the fused
+    // block partials: value k summed over the block's rows in a fixed order (four chains).  With the fused
     // finalize they are handed to the last block without fences (MI355X_MICROARCH.md, the hand-off table's
     // first row): agent-scope (sc1) stores, each storing wave's vmcnt(0), a workgroup barrier, ONE
     // relaxed agent-scope counter add; the block whose add returns the last count reads them with sc1 loads
@@ -414,28 +414,31 @@ __global__ void __launch_bounds__(kLossRows) k_loss_grad(
                            __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!fin.counter) return;  // uniform
-    // fused finalize: the last block to finish sums every block's partials (thread k: value k, fixed order)
-    __shared__ int last_s;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0)
         last_s = __hip_atomic_fetch_add(fin.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == int(gridDim.x) - 1;
     __syncthreads();
     if (!last_s) return;
-    if (tid < NV) {
-        const int nblk = gridDim.x;
-        float t[4] = {0.f, 0.f, 0.f, 0.f};
-        int b = 0;
-        for (; b + 4 <= nblk; b += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                t[u] += __hip_atomic_load(partials + int64_t(b + u) * NV + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the last block: every block's partials into LDS (all lanes loading, independent sc1 loads in flight
+    // together), then value k summed over the blocks in block order
+    const int nblk = gridDim.x;
+    constexpr int kPass = 2 * kLossRows;
+    float acc = 0.f;
+    for (int b0 = 0; b0 < nblk; b0 += kPass) {
+        const int nb = min(kPass, nblk - b0);
+        __syncthreads();  // the previous pass's sums are done with s_red
+        for (int e = tid; e < nb * NV; e += kLossThreads) {
+            const int bb = e / NV, k = e - bb * NV;
+            s_red[bb * RP + k] = __hip_atomic_load(partials + int64_t(b0) * NV + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        for (; b < nblk; ++b)
-            t[0] += __hip_atomic_load(partials + int64_t(b) * NV + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        loss_finalize_value(tid, (t[0] + t[1]) + (t[2] + t[3]), A, mb_rows, fin.entropy_coef, grad_scale, fin.grad_head_bias,
-                            fin.grad_logstd, fin.stats, fin.stat_idx, fin.kl_out);
+        __syncthreads();
+        if (tid < NV)
+            for (int bb = 0; bb < nb; ++bb) acc += s_red[bb * RP + tid];
     }
+    if (tid < NV)
+        loss_finalize_value(tid, acc, A, mb_rows, fin.entropy_coef, grad_scale, fin.grad_head_bias, fin.grad_logstd,
+                            fin.stats, fin.stat_idx, fin.kl_out);
     if (tid == 0) __hip_atomic_store(fin.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -681,15 +684,16 @@ __device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int64_t 
     const int r = int(o / cols), c = int(o % cols) * V;
     const float* src = jb.src + int64_t(r) * jb.src_cols + c;
     fv s = {};
-    int q = 0;
-    for (; q + 16 <= jb.S; q += 16) {  // sixteen loads in flight, added in order (fixed summation order)
-        fv v[16];
+    // eight loads in flight per chunk, the last chunk predicated (a serial remainder loop left S = 24's last
+    // eight loads one memory round trip each), added in q order (fixed summation order)
+    for (int q = 0; q < jb.S; q += 8) {
+        fv v[8];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n);
+        for (int u = 0; u < 8; ++u) v[u] = q + u < jb.S ? *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n) : fv{};
 #pragma unroll
-        for (int u = 0; u < 16; ++u) s += v[u];
+        for (int u = 0; u < 8; ++u)
+            if (q + u < jb.S) s += v[u];
     }
-    for (; q < jb.S; ++q) s += *reinterpret_cast<const fv*>(src + int64_t(q) * jb.src_n);
     *reinterpret_cast<fv*>(jb.dst + int64_t(r) * jb.dst_stride + c) = s;
 }
 
@@ -776,16 +780,13 @@ __device__ void tail_update(const ppo_tail_args_t& t, bool skipped) {
     *t.stat_idx += 1;
 }
 
-// TAIL: the last block to finish (a device counter; every block reads lr / step / scaler in its prologue
-// before it counts itself done) also runs the tail, so the minibatch step ends with this one launch
-template <bool TAIL>
 __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, const float* __restrict__ g,
                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                        const float* __restrict__ np, int nnp, float max_norm,
                                                        const double* __restrict__ lr_p, const double* __restrict__ step_p,
                                                        float b1, float b2, float eps, SegTable segs,
                                                        uint16_t* __restrict__ mirror, int mirror_dtype,
-                                                       const float* __restrict__ scaler, ppo_tail_args_t tail) {
+                                                       const float* __restrict__ scaler) {
     __shared__ float red[2][kAdamThreads / kWave];
     __shared__ float coef_s, step_size_s, bc2_sqrt_s, inv_scale_s;
     __shared__ int skip_s;
@@ -850,23 +851,6 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
             }
         }
     }
-    if (TAIL) {
-        // no data is handed between workgroups here, only an order: every workgroup's thread 0 read lr /
-        // step / scaler (and used them) in the prologue, before its counter add below, and the tail writes
-        // them after the last add has returned; the next launch sees the writes at the kernel boundary.  So
-        // a relaxed agent-scope counter suffices -- no fences (MI355X_MICROARCH.md: an agent release
-        // writes back the XCD's L2, microseconds per workgroup)
-        __shared__ int last_s;
-        __syncthreads();
-        if (threadIdx.x == 0)
-            last_s = __hip_atomic_fetch_add(tail.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                     int(gridDim.x) - 1;
-        __syncthreads();
-        if (last_s && threadIdx.x == 0) {
-            tail_update(tail, skip);
-            __hip_atomic_store(tail.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 __global__ void k_tail(ppo_tail_args_t t, const float* np, int nnp) {
@@ -878,6 +862,116 @@ __global__ void k_tail(ppo_tail_args_t t, const float* np, int nnp) {
         b = wave_sum(b);
     }
     if (threadIdx.x == 0) tail_update(t, t.scaler && b > 0.f);
+}
+
+// ppo_adam_step (round 5): the optimizer step as two launches.  k_sqnorm_step = k_sqnorm, and its last
+// block (a relaxed agent-scope counter; the partials handed over by sc1 stores / loads as in k_loss_grad)
+// forms the step's scalars ONCE -- k_adam's prologue arithmetic, same order, same fp64 bias corrections --
+// into hp, then runs the tail (lr / step / scaler are read for hp before the tail rewrites them).
+// k_adam_hp is then a plain streaming update: no per-block prologue.
+struct SqnormStepArgs {
+    float max_norm, b1, b2;
+    ppo_tail_args_t tail;
+    float* hp;  // [coef, inv_scale, step_size, bc2_sqrt, skip]
+};
+
+__global__ void __launch_bounds__(256) k_sqnorm_step(const float* __restrict__ g, int64_t n, float* __restrict__ partials,
+                                                     SqnormStepArgs a) {
+    __shared__ float red[2][256 / kWave];
+    __shared__ int last_s;
+    const float* scaler = a.tail.scaler;
+    {
+        const float inv_scale = scaler ? 1.f / scaler[0] : 1.f;
+        float s = 0.f, bad = 0.f;
+        for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+            const float x = g[i] * inv_scale;
+            s += x * x;
+            bad += __builtin_isfinite(g[i]) ? 0.f : 1.f;
+        }
+        s = wave_sum(s);
+        bad = wave_sum(bad);
+        if (threadIdx.x % kWave == 0) {
+            red[0][threadIdx.x / kWave] = s;
+            red[1][threadIdx.x / kWave] = bad;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float t = 0.f, b = 0.f;
+            for (int w = 0; w < 256 / kWave; ++w) {
+                t += red[0][w];
+                b += red[1][w];
+            }
+            __hip_atomic_store(partials + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(partials + gridDim.x + blockIdx.x, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            last_s = __hip_atomic_fetch_add(a.tail.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     int(gridDim.x) - 1;
+        }
+        __syncthreads();
+    }
+    if (!last_s) return;
+    const int nnp = gridDim.x;
+    float s = 0.f, bad = 0.f;
+    for (int k = threadIdx.x; k < nnp; k += 256) {
+        s += __hip_atomic_load(partials + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bad += __hip_atomic_load(partials + nnp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s = wave_sum(s);
+    bad = wave_sum(bad);
+    __syncthreads();
+    if (threadIdx.x % kWave == 0) {
+        red[0][threadIdx.x / kWave] = s;
+        red[1][threadIdx.x / kWave] = bad;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    float t = 0.f, b = 0.f;
+    for (int w = 0; w < 256 / kWave; ++w) {
+        t += red[0][w];
+        b += red[1][w];
+    }
+    // k_adam's prologue, once
+    const float inv_scale = scaler ? 1.f / scaler[0] : 1.f;
+    const bool skip = scaler && b > 0.f;
+    const float c = a.max_norm / (sqrtf(t) + 1e-6f);
+    const float coef = a.max_norm > 0.f ? (c < 1.f || c != c ? c : 1.f) : 1.f;
+    const double ts = *a.tail.step + 1.0;
+    a.hp[0] = coef;
+    a.hp[1] = inv_scale;
+    a.hp[2] = float(*a.tail.lr / (1.0 - pow(double(a.b1), ts)));
+    a.hp[3] = float(sqrt(1.0 - pow(double(a.b2), ts)));
+    a.hp[4] = skip ? 1.f : 0.f;
+    tail_update(a.tail, skip);
+    __hip_atomic_store(a.tail.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(kAdamThreads) k_adam_hp(float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                          float b1, float b2, float eps, SegTable segs,
+                                                          uint16_t* __restrict__ mirror, int mirror_dtype,
+                                                          const float* __restrict__ hp) {
+    const float coef = hp[0], inv_scale = hp[1], step_size = hp[2], bc2_sqrt = hp[3];
+    const int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x;
+    if (hp[4] != 0.f || i >= n) return;
+    const float gi = (g[i] * inv_scale) * coef;
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    const float pi = p[i] - step_size * (mi / denom);
+    p[i] = pi;
+    if (mirror) {
+        for (int k = 0; k < segs.n; ++k) {
+            const ppo_seg_t& sg = segs.s[k];
+            if (i >= sg.off && i < sg.off + sg.len) {
+                const int64_t j = i - sg.off;
+                const int64_t r = j / sg.cols, c = j % sg.cols;
+                mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] =
+                    mirror_dtype == PPO_DT_F16 ? f32_to_f16(pi) : f32_to_bf16(pi);
+            }
+        }
+    }
 }
 
 inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
@@ -933,7 +1027,7 @@ static int launch_loss(const float* head, const float* logstd, int32_t A, int32_
                        const ppo_loss_fin_t& fin, void* stream) {
     if (dhead_lp && lp_dtype != PPO_DT_BF16 && lp_dtype != PPO_DT_F16)
         return fail(-1, "ppo_loss_grad: dhead_lp needs lp_dtype PPO_DT_BF16 or PPO_DT_F16");
-    const dim3 grid(ppo_loss_blocks(mb_rows)), block(kLossRows);
+    const dim3 grid(ppo_loss_blocks(mb_rows)), block(kLossThreads);
 #define PPO_LOSS_CASE(AA)                                                                                        \
     case AA:                                                                                                     \
         hipLaunchKernelGGL(k_loss_grad<AA>, grid, block, 0, S(stream), head, logstd, mb_rows, mb_idx, actions, \
@@ -1077,14 +1171,11 @@ int ppo_sqnorm(const float* g, int64_t n, const float* scaler, float* partials, 
     return launched("k_sqnorm");
 }
 
-static int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials,
-                       int32_t nblk_norm, float max_norm, const double* lr, double* step, float beta1, float beta2,
-                       float eps, const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype,
-                       const float* scaler, const ppo_tail_args_t* tail, void* stream) {
+static int seg_table(const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, SegTable& t) {
     if (nseg < 0 || nseg > PPO_MAX_SEG) return fail(-1, "ppo_adam: too many mirror segments");
     if (mirror && mirror_dtype != PPO_DT_BF16 && mirror_dtype != PPO_DT_F16)
         return fail(-1, "ppo_adam: mirror_dtype must be bf16 or fp16");
-    SegTable t{};
+    t = SegTable{};
     t.n = mirror ? nseg : 0;
     for (int k = 0; k < t.n; ++k) {
         t.s[k] = segs_host[k];
@@ -1092,25 +1183,20 @@ static int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, 
         if (t.s[k].cols <= 0 || t.s[k].mstride < (t.s[k].trans ? rows : t.s[k].cols))
             return fail(-1, "ppo_adam: bad segment");
     }
-    const int64_t want = (n + kAdamThreads - 1) / kAdamThreads;
-    const dim3 grid(unsigned(want < kAdamBlocks ? want : kAdamBlocks));
-    if (tail)
-        hipLaunchKernelGGL(k_adam<true>, grid, dim3(kAdamThreads), 0, S(stream), p, g, m, v, n, sqnorm_partials,
-                           nblk_norm, max_norm, lr, step, beta1, beta2, eps, t, static_cast<uint16_t*>(mirror),
-                           mirror_dtype, scaler, *tail);
-    else
-        hipLaunchKernelGGL(k_adam<false>, grid, dim3(kAdamThreads), 0, S(stream), p, g, m, v, n, sqnorm_partials,
-                           nblk_norm, max_norm, lr, step, beta1, beta2, eps, t, static_cast<uint16_t*>(mirror),
-                           mirror_dtype, scaler, ppo_tail_args_t{});
-    return launched("k_adam");
+    return 0;
 }
 
 int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials, int32_t nblk_norm,
              float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,
              const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, const float* scaler,
              void* stream) {
-    return launch_adam(p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, segs_host,
-                       nseg, mirror, mirror_dtype, scaler, nullptr, stream);
+    SegTable t;
+    if (const int rc = seg_table(segs_host, nseg, mirror, mirror_dtype, t)) return rc;
+    const int64_t want = (n + kAdamThreads - 1) / kAdamThreads;
+    hipLaunchKernelGGL(k_adam, dim3(unsigned(want < kAdamBlocks ? want : kAdamBlocks)), dim3(kAdamThreads), 0,
+                       S(stream), p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
+                       static_cast<uint16_t*>(mirror), mirror_dtype, scaler);
+    return launched("k_adam");
 }
 
 static int check_tail(const ppo_tail_args_t& t, const float* sqnorm_partials) {
@@ -1121,13 +1207,19 @@ static int check_tail(const ppo_tail_args_t& t, const float* sqnorm_partials) {
     return 0;
 }
 
-int ppo_adam_tail(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials,
-                  int32_t nblk_norm, float max_norm, float beta1, float beta2, float eps, const ppo_seg_t* segs_host,
-                  int32_t nseg, void* mirror, int32_t mirror_dtype, const ppo_tail_args_t* tail, void* stream) {
-    if (!tail || !tail->counter) return fail(-1, "ppo_adam_tail: tail arguments with a counter required");
+int ppo_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float* sqnorm_partials, float max_norm,
+                  float beta1, float beta2, float eps, const ppo_seg_t* segs_host, int32_t nseg, void* mirror,
+                  int32_t mirror_dtype, const ppo_tail_args_t* tail, float* hp, void* stream) {
+    if (!tail || !tail->counter || !hp || !sqnorm_partials) return fail(-1, "ppo_adam_step: null argument");
     if (const int rc = check_tail(*tail, sqnorm_partials)) return rc;
-    return launch_adam(p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, tail->lr, tail->step, beta1, beta2, eps,
-                       segs_host, nseg, mirror, mirror_dtype, tail->scaler, tail, stream);
+    SegTable t;
+    if (const int rc = seg_table(segs_host, nseg, mirror, mirror_dtype, t)) return rc;
+    const SqnormStepArgs a{max_norm, beta1, beta2, *tail, hp};
+    hipLaunchKernelGGL(k_sqnorm_step, dim3(kNormBlocks), dim3(256), 0, S(stream), g, n, sqnorm_partials, a);
+    if (const int rc = launched("k_sqnorm_step")) return rc;
+    hipLaunchKernelGGL(k_adam_hp, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0,
+                       S(stream), p, g, m, v, n, beta1, beta2, eps, t, static_cast<uint16_t*>(mirror), mirror_dtype, hp);
+    return launched("k_adam_hp");
 }
 
 int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,

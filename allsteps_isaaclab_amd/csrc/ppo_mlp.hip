@@ -226,7 +226,11 @@ __device__ __forceinline__ void mma_rows(const uint16_t* X, const typename Lp<DT
 }
 
 #ifndef PPO_MLP_PRIO
-#define PPO_MLP_PRIO 0  // A/B knob (scripts/mlp_ab.py): static s_setprio 1 for waves 4..7 of the trunk kernels
+// static s_setprio 1 for waves 4..7 of the trunk kernels (MI355X_MICROARCH.md "Two waves per SIMD" item 4:
+// the second-dispatched half otherwise loses every VALU arbitration to its SIMD partner).  A/B on one box
+// (scripts/mlp_ab.py, 32768 rows, fp16, r05i): forward 46.3 -> 45.2 us, backward 49.9 -> 45.8 us, outputs
+// bit-identical
+#define PPO_MLP_PRIO 1
 #endif
 #ifndef PPO_FWD_DBG
 #define PPO_FWD_DBG 0  // timing-only builds (scripts/fwd_dbg.sh): 2 no exp, 4 no stores, 16 no MFMA, 32 no ELU / convert

@@ -98,7 +98,7 @@ EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
                     "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update",
-                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_adam_tail",
+                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_adam_step",
                     "ppo_loss_grad_fin"]
 
 
@@ -123,8 +123,8 @@ def load() -> C.CDLL:
     L.ppo_sqnorm.argtypes = [V, I64, V, V, V]
     L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32, V, V]
     L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V, V, I32, I32, V]
-    L.ppo_adam_tail.argtypes = [V, V, V, V, I64, V, I32, F32, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32,
-                                C.POINTER(PpoTailArgs), V]
+    L.ppo_adam_step.argtypes = [V, V, V, V, I64, V, F32, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32,
+                                C.POINTER(PpoTailArgs), V, V]
     L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
     L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
     L.ppo_counter_add.argtypes = [V, I64, V]
@@ -241,7 +241,8 @@ class FusedPPOUpdate:
         self.stat_partials = torch.empty(L.ppo_obs_stats_blocks(B) * 2 * 64, device=dev, dtype=torch.float64)
         self.norm_partials = torch.empty(2 * L.ppo_sqnorm_blocks(), device=dev)  # norm sums | non-finite counts
         self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
-        self.tail_counter = torch.zeros(1, device=dev, dtype=torch.int32)  # ppo_adam_tail's finished-block count
+        self.tail_counter = torch.zeros(1, device=dev, dtype=torch.int32)  # ppo_adam_step's finished-block count
+        self.step_hp = torch.zeros(8, device=dev)  # ppo_adam_step's per-step scalars
         self.loss_counter = torch.zeros(1, device=dev, dtype=torch.int32)  # ppo_loss_grad_fin's
         self._loss_fin = PpoLossFin()
         self._tail_args = PpoTailArgs()
@@ -571,20 +572,19 @@ class FusedPPOUpdate:
     def _optimizer_step(self) -> None:
         L, s, ag, fl = self.L, self._stream(), self.agent, self.flat
         n = fl.numel
-        _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.scaler), _p(self.norm_partials), s), "ppo_sqnorm")
         opt = ag.optimizer
-        # clip + Adam, and in the same launch (its last workgroup) the tail: GradScaler.update, adaptive LR,
-        # Adam's step count, the device minibatch / statistics counters
+        # clip_grad_norm_ + Adam + the tail (GradScaler.update, adaptive LR, Adam's step count, the device
+        # minibatch / statistics counters) in two launches: the norm kernel's last workgroup forms the
+        # step's scalars once and runs the tail; the Adam launch streams the buffer
         t = self._tail_args
         t.lr, t.kl, t.kl_threshold = _p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0
         t.min_lr, t.max_lr, t.step, t.mb_idx, t.n_minibatches = self.min_lr, self.max_lr, _p(opt.step_t), _p(self.mb_idx), self.n_mb
         t.stat_idx, t.scaler, t.growth_interval, t.counter = (_p(self.stat_idx), _p(self.scaler), SCALER_GROWTH_INTERVAL,
                                                               _p(self.tail_counter))
-        _check(L.ppo_adam_tail(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
-                               _p(self.norm_partials), self.norm_partials.numel() // 2,
-                               ag.grad_norm if ag.truncate_grads else 0.0, opt.beta1, opt.beta2, opt.eps, self.segs,
-                               self.nseg, _p(self.mirror), self.dt_code if self.lp else 1, C.byref(t), s),
-               "ppo_adam_tail")
+        _check(L.ppo_adam_step(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
+                               _p(self.norm_partials), ag.grad_norm if ag.truncate_grads else 0.0, opt.beta1,
+                               opt.beta2, opt.eps, self.segs, self.nseg, _p(self.mirror),
+                               self.dt_code if self.lp else 1, C.byref(t), _p(self.step_hp), s), "ppo_adam_step")
 
     # ------------------------------------------------------------------ graphs
     def _run(self, key, fn) -> None:

@@ -20,7 +20,7 @@
  *                                         torch.cuda.amp.GradScaler) the unscale, the skip of a step
  *                                         with non-finite gradients and the scale update
  *   ppo_tail                              adaptive LR from the (rank-averaged) KL; minibatch counter
- *   ppo_adam_tail                         ppo_adam + ppo_tail in one launch
+ *   ppo_adam_step                         ppo_sqnorm + ppo_adam + ppo_tail in two launches
  *   ppo_loss_grad_fin                     ppo_loss_grad + ppo_loss_finalize in one launch
  *   ppo_mlp_forward / ppo_mlp_backward    the whole trunk forward / input-gradient chain (MFMA)
  *   ppo_weight_grads                      split-K weight + bias gradients of all trunk layers and the
@@ -266,10 +266,12 @@ int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, dou
              int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, float* scaler, const float* sqnorm_partials,
              int32_t nblk_norm, int32_t growth_interval, void* stream);
 
-/* ppo_adam followed by ppo_tail in ONE launch (round 5): the last Adam workgroup to finish -- counted on
- * `counter`, a device int32 that starts at 0 and that this call leaves at 0 -- runs the tail after every
- * workgroup has read lr / step / scaler.  Same arguments and results as the two calls (lr, step and
- * scaler come from the tail struct). */
+/* The whole optimizer half of a minibatch step (round 5): ppo_sqnorm, ppo_adam and ppo_tail in two
+ * launches.  The norm kernel's last block -- counted on tail->counter, a device int32 that starts at 0
+ * and that the call leaves at 0 -- forms the step's scalars once (clip coefficient, unscale, skip, the
+ * bias corrections from lr / step) into hp (device, 5 floats of scratch), then runs the tail; the Adam
+ * launch reads hp.  sqnorm_partials: 2 * ppo_sqnorm_blocks() floats.  Same results as the three calls
+ * (lr, step and scaler come from the tail struct). */
 typedef struct {
     double* lr;
     const float* kl;
@@ -283,9 +285,9 @@ typedef struct {
     int32_t growth_interval;
     int32_t* counter;
 } ppo_tail_args_t;
-int ppo_adam_tail(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials,
-                  int32_t nblk_norm, float max_norm, float beta1, float beta2, float eps, const ppo_seg_t* segs_host,
-                  int32_t nseg, void* mirror, int32_t mirror_dtype, const ppo_tail_args_t* tail, void* stream);
+int ppo_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float* sqnorm_partials, float max_norm,
+                  float beta1, float beta2, float eps, const ppo_seg_t* segs_host, int32_t nseg, void* mirror,
+                  int32_t mirror_dtype, const ppo_tail_args_t* tail, float* hp, void* stream);
 
 #ifdef __cplusplus
 }

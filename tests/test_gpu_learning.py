@@ -597,10 +597,11 @@ def test_weight_grads_kernel(rows, splits, dt):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("bad", [False, True])
-def test_adam_tail_launch_equals_adam_then_tail(bad):
-    """ppo_adam_tail (the tail run by the last Adam workgroup) == ppo_adam then ppo_tail, bit for bit:
-    parameters, moments, the fp16 mirror, lr / step / scaler / counters; the finished-block counter is
-    back at 0 (a graph replays it).  bad: a non-finite gradient (the scaler skips the step and backs off)."""
+def test_adam_step_equals_sqnorm_adam_tail(bad):
+    """ppo_adam_step (the norm kernel's last workgroup forms the step's scalars and runs the tail; a
+    streaming Adam launch) == ppo_sqnorm, ppo_adam, ppo_tail, bit for bit: parameters, moments, the fp16
+    mirror, lr / step / scaler / counters; the finished-block counter is back at 0 (a graph replays it).
+    bad: a non-finite gradient (the scaler skips the step and backs off)."""
     import ctypes as C
 
     from allsteps_isaaclab_amd.learning import fused as FU
@@ -614,11 +615,11 @@ def test_adam_tail_launch_equals_adam_then_tail(bad):
     if bad:
         grads[n // 3] = float("inf")
     nb = L.ppo_sqnorm_blocks()
-    partials = torch.empty(2 * nb, device=dev)
     seg = FU.PpoSeg(1000, 256 * 64, 0, 64, 72, 0)
     segs = (FU.PpoSeg * 1)(seg)
     outs = []
     for fused in (False, True):
+        partials = torch.empty(2 * nb, device=dev)
         p = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
         m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
         mirror = torch.zeros(256 * 72, device=dev, dtype=torch.float16)
@@ -627,24 +628,25 @@ def test_adam_tail_launch_equals_adam_then_tail(bad):
         scaler = torch.tensor([65536.0, 1999.0], device=dev)
         kl = torch.tensor([0.03], device=dev)
         mb, st, ctr = (torch.zeros(1, device=dev, dtype=torch.int32) for _ in range(3))
-        FU._check(L.ppo_sqnorm(grads.data_ptr(), n, scaler.data_ptr(), partials.data_ptr(), s), "sqnorm")
+        hp = torch.zeros(8, device=dev)
         if fused:
             t = FU.PpoTailArgs(lr.data_ptr(), kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4,
                                st.data_ptr(), scaler.data_ptr(), 2000, ctr.data_ptr())
-            FU._check(L.ppo_adam_tail(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, partials.data_ptr(),
-                                      nb, 1.0, 0.9, 0.999, 1e-8, segs, 1, mirror.data_ptr(), FU.PPO_DT[torch.float16],
-                                      C.byref(t), s), "ppo_adam_tail")
+            FU._check(L.ppo_adam_step(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, partials.data_ptr(),
+                                      1.0, 0.9, 0.999, 1e-8, segs, 1, mirror.data_ptr(), FU.PPO_DT[torch.float16],
+                                      C.byref(t), hp.data_ptr(), s), "ppo_adam_step")
         else:
+            FU._check(L.ppo_sqnorm(grads.data_ptr(), n, scaler.data_ptr(), partials.data_ptr(), s), "sqnorm")
             FU._check(L.ppo_adam(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, partials.data_ptr(), nb,
                                  1.0, lr.data_ptr(), step.data_ptr(), 0.9, 0.999, 1e-8, segs, 1, mirror.data_ptr(),
                                  FU.PPO_DT[torch.float16], scaler.data_ptr(), s), "ppo_adam")
             FU._check(L.ppo_tail(lr.data_ptr(), kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4,
                                  st.data_ptr(), scaler.data_ptr(), partials.data_ptr(), nb, 2000, s), "ppo_tail")
         torch.cuda.synchronize()
-        outs.append([p, m, v, mirror, lr, step, scaler, mb, st, ctr])
+        outs.append([partials, p, m, v, mirror, lr, step, scaler, mb, st, ctr])
     for a, b in zip(*outs):
         assert torch.equal(a, b), (a, b)
-    p, _, _, _, lr, step, scaler, mb, st, ctr = outs[1]
+    _, p, _, _, _, lr, step, scaler, mb, st, ctr = outs[1]
     assert int(ctr) == 0 and int(mb) == 1 and int(st) == 1
     if bad:  # skipped: step count kept, scale halved, lr still adapted from the KL
         assert float(step) == 7.0 and float(scaler[0]) == 32768.0
