@@ -433,8 +433,16 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
             s_red[bb * RP + k] = __hip_atomic_load(partials + int64_t(b0) * NV + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        if (tid < NV)
-            for (int bb = 0; bb < nb; ++bb) acc += s_red[bb * RP + tid];
+        if (tid < NV) {
+            float c4[4] = {0.f, 0.f, 0.f, 0.f};
+            int bb = 0;
+#pragma unroll 4
+            for (; bb + 4 <= nb; bb += 4)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) c4[u] += s_red[(bb + u) * RP + tid];
+            for (; bb < nb; ++bb) c4[0] += s_red[bb * RP + tid];
+            acc += (c4[0] + c4[1]) + (c4[2] + c4[3]);
+        }
     }
     if (tid < NV)
         loss_finalize_value(tid, acc, A, mb_rows, fin.entropy_coef, grad_scale, fin.grad_head_bias, fin.grad_logstd,
@@ -684,14 +692,14 @@ __device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int64_t 
     const int r = int(o / cols), c = int(o % cols) * V;
     const float* src = jb.src + int64_t(r) * jb.src_cols + c;
     fv s = {};
-    // eight loads in flight per chunk, the last chunk predicated (a serial remainder loop left S = 24's last
-    // eight loads one memory round trip each), added in q order (fixed summation order)
-    for (int q = 0; q < jb.S; q += 8) {
-        fv v[8];
+    // up to 32 loads in flight per chunk (every split of the trainer's jobs at once), the chunk predicated,
+    // added in q order (fixed summation order)
+    for (int q = 0; q < jb.S; q += 32) {
+        fv v[32];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = q + u < jb.S ? *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n) : fv{};
+        for (int u = 0; u < 32; ++u) v[u] = q + u < jb.S ? *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n) : fv{};
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < 32; ++u)
             if (q + u < jb.S) s += v[u];
     }
     *reinterpret_cast<fv*>(jb.dst + int64_t(r) * jb.dst_stride + c) = s;
@@ -754,30 +762,48 @@ struct SegTable {
 };
 
 // the end of a minibatch step (ppo_tail): GradScaler.update, the adaptive LR from the KL, Adam's step
-// count, the device minibatch / statistics counters -- one thread
-__device__ void tail_update(const ppo_tail_args_t& t, bool skipped) {
+// count, the device minibatch / statistics counters -- one thread.  The inputs are read in one go (every
+// load issued before the first use: one memory round trip, not one per field)
+struct TailVals {
+    double lr, step;
+    float kl, scale, tracker;
+    int mb, st;
+};
+
+__device__ __forceinline__ TailVals tail_load(const ppo_tail_args_t& t) {
+    TailVals v;
+    v.lr = *t.lr;
+    v.step = *t.step;
+    v.kl = t.kl_threshold > 0.f ? *t.kl : 0.f;
+    v.scale = t.scaler ? t.scaler[0] : 1.f;
+    v.tracker = t.scaler ? t.scaler[1] : 0.f;
+    v.mb = *t.mb_idx;
+    v.st = *t.stat_idx;
+    return v;
+}
+
+__device__ void tail_store(const ppo_tail_args_t& t, const TailVals& v, bool skipped) {
     if (t.scaler) {  // GradScaler.update: backoff 0.5 on a skipped step, growth 2 after growth_interval good ones
-        float* scaler = t.scaler;
         if (skipped) {
-            scaler[0] *= 0.5f;
-            scaler[1] = 0.f;
-        } else if (scaler[1] + 1.f >= float(t.growth_interval)) {
-            scaler[0] *= 2.f;
-            scaler[1] = 0.f;
+            t.scaler[0] = v.scale * 0.5f;
+            t.scaler[1] = 0.f;
+        } else if (v.tracker + 1.f >= float(t.growth_interval)) {
+            t.scaler[0] = v.scale * 2.f;
+            t.scaler[1] = 0.f;
         } else {
-            scaler[1] += 1.f;
+            t.scaler[1] = v.tracker + 1.f;
         }
     }
     if (t.kl_threshold > 0.f) {
-        const double k = double(*t.kl);
-        double cur = *t.lr, nxt = cur;
-        if (k > 2.0 * double(t.kl_threshold)) nxt = fmax(cur / 1.5, t.min_lr);
-        if (k < 0.5 * double(t.kl_threshold)) nxt = fmin(cur * 1.5, t.max_lr);
+        const double k = double(v.kl);
+        double nxt = v.lr;
+        if (k > 2.0 * double(t.kl_threshold)) nxt = fmax(v.lr / 1.5, t.min_lr);
+        if (k < 0.5 * double(t.kl_threshold)) nxt = fmin(v.lr * 1.5, t.max_lr);
         *t.lr = nxt;
     }
-    if (!skipped) *t.step += 1.0;  // a skipped optimizer.step() leaves Adam's step count
-    *t.mb_idx = (*t.mb_idx + 1) % t.n_minibatches;
-    *t.stat_idx += 1;
+    if (!skipped) *t.step = v.step + 1.0;  // a skipped optimizer.step() leaves Adam's step count
+    *t.mb_idx = (v.mb + 1) % t.n_minibatches;
+    *t.stat_idx = v.st + 1;
 }
 
 __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, const float* __restrict__ g,
@@ -861,7 +887,7 @@ __global__ void k_tail(ppo_tail_args_t t, const float* np, int nnp) {
         for (int k = threadIdx.x; k < nnp; k += kWave) b += np[nnp + k];
         b = wave_sum(b);
     }
-    if (threadIdx.x == 0) tail_update(t, t.scaler && b > 0.f);
+    if (threadIdx.x == 0) tail_store(t, tail_load(t), t.scaler && b > 0.f);
 }
 
 // ppo_adam_step (round 5): the optimizer step as two launches.  k_sqnorm_step = k_sqnorm, and its last
@@ -910,6 +936,8 @@ __global__ void __launch_bounds__(256) k_sqnorm_step(const float* __restrict__ g
         __syncthreads();
     }
     if (!last_s) return;
+    TailVals tv;
+    if (threadIdx.x == 0) tv = tail_load(a.tail);  // in flight under the partial sums
     const int nnp = gridDim.x;
     float s = 0.f, bad = 0.f;
     for (int k = threadIdx.x; k < nnp; k += 256) {
@@ -931,17 +959,17 @@ __global__ void __launch_bounds__(256) k_sqnorm_step(const float* __restrict__ g
         b += red[1][w];
     }
     // k_adam's prologue, once
-    const float inv_scale = scaler ? 1.f / scaler[0] : 1.f;
+    const float inv_scale = scaler ? 1.f / tv.scale : 1.f;
     const bool skip = scaler && b > 0.f;
     const float c = a.max_norm / (sqrtf(t) + 1e-6f);
     const float coef = a.max_norm > 0.f ? (c < 1.f || c != c ? c : 1.f) : 1.f;
-    const double ts = *a.tail.step + 1.0;
+    const double ts = tv.step + 1.0;
     a.hp[0] = coef;
     a.hp[1] = inv_scale;
-    a.hp[2] = float(*a.tail.lr / (1.0 - pow(double(a.b1), ts)));
+    a.hp[2] = float(tv.lr / (1.0 - pow(double(a.b1), ts)));
     a.hp[3] = float(sqrt(1.0 - pow(double(a.b2), ts)));
     a.hp[4] = skip ? 1.f : 0.f;
-    tail_update(a.tail, skip);
+    tail_store(a.tail, tv, skip);
     __hip_atomic_store(a.tail.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

@@ -2,7 +2,9 @@
 16-bit inputs through ppo_mlp_forward (and ppo_mlp_backward) of library A and library B; prints the
 largest differences of every output and each library's HIP-event time per launch.
 
-    python scripts/mlp_ab.py LIB_A LIB_B [rows] [dtype: f16 | bf16]
+    python scripts/mlp_ab.py LIB_A LIB_B [rows] [dtype: f16 | bf16] [obs]
+
+With `obs` the forward forms its input from fp32 observations (the trainer's fused RunningMeanStd path).
 """
 
 from __future__ import annotations
@@ -42,6 +44,7 @@ def main():
     la, lb = sys.argv[1], sys.argv[2]
     rows = int(sys.argv[3]) if len(sys.argv) > 3 else 32768
     dt = torch.float16 if (sys.argv[4] if len(sys.argv) > 4 else "f16") == "f16" else torch.bfloat16
+    use_obs = len(sys.argv) > 5 and sys.argv[5] == "obs"
     dev = "cuda:0"
     g = torch.Generator(device=dev).manual_seed(3)
     x = torch.zeros(rows, 72, device=dev)
@@ -56,6 +59,10 @@ def main():
     bh = torch.randn(22, device=dev, generator=g) * 0.1
     dhead = torch.randn(rows, 22, device=dev, generator=g) * 0.01
     out = {}
+    obs = torch.randn(2 * rows, 59, device=dev, generator=g) * 2
+    midx = torch.tensor([1], device=dev, dtype=torch.int32)
+    mean = torch.randn(59, device=dev, generator=g, dtype=torch.float64) * 0.1
+    var = torch.rand(59, device=dev, generator=g, dtype=torch.float64) + 0.5
     dh16 = torch.zeros(rows, 32, device=dev, dtype=dt)
     dh16[:, :22] = dhead.to(dt)
     for tag, path in (("A", la), ("B", lb)):
@@ -69,6 +76,11 @@ def main():
             a.w[i], a.b[i], a.h[i] = ws[i].data_ptr(), bs[i].data_ptr(), hs[i].data_ptr()
         a.wh, a.bh, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), head.data_ptr(), rows, 22
         a.x_stride, a.h_stride, a.dtype = 72, 264, FU.PPO_DT[dt]
+        if use_obs:
+            xo = torch.zeros(rows, 72, device=dev, dtype=dt)
+            a.obs, a.mb_idx, a.mean, a.var, a.eps, a.obs_dim = (obs.data_ptr(), midx.data_ptr(), mean.data_ptr(),
+                                                                var.data_ptr(), 1e-5, 59)
+            a.x_out = xo.data_ptr()
         b = FU.PpoMlpBwd()
         b.dhead, b.wh, b.nh, b.rows, b.h_stride, b.dtype = dh16.data_ptr(), wh.data_ptr(), 22, rows, 264, FU.PPO_DT[dt]
         for k in range(4):
@@ -83,7 +95,7 @@ def main():
         out[tag] = {"h": [t[:, :256].float().clone() for t in hs], "head": head.clone(),
                     "dz": [t.float().clone() for t in dzs], "fwd_us": timed(fwd), "bwd_us": timed(bwd)}
     A, B = out["A"], out["B"]
-    rep = {"rows": rows, "dtype": str(dt), "fwd_us": [A["fwd_us"], B["fwd_us"]], "bwd_us": [A["bwd_us"], B["bwd_us"]]}
+    rep = {"rows": rows, "dtype": str(dt), "obs": use_obs, "fwd_us": [A["fwd_us"], B["fwd_us"]], "bwd_us": [A["bwd_us"], B["bwd_us"]]}
     for k in ("h", "dz"):
         rep[k + "_maxdiff"] = [round(float((p - q).abs().max()), 6) for p, q in zip(A[k], B[k])]
         rep[k + "_frac_diff"] = [round(float(((p - q).abs() > 0).float().mean()), 6) for p, q in zip(A[k], B[k])]
