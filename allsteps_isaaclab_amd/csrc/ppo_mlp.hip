@@ -375,6 +375,15 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     const int F0 = 32 * wave;                 // this wave's output features
     const int row0 = blockIdx.x * kFRows;
     const int rows = a.rows;
+    // Weight slices double-buffered in registers (wa / wb): layer l + 1's slice is requested at the start
+    // of layer l, ahead of layer l's activation stores (a load waited for with vmcnt also waits for every
+    // older store of the wave).  Bias vectors likewise one layer ahead.  Layer 0's are requested first,
+    // so they fly under the input normalisation below.
+    V8 wa[16], wb[16];
+    float ba[16], bb[16];
+    f32x16 pend = {};
+    load_wa<DT, kK0 / 16>(a.w[0], kK0, F0, i, h, wa);
+    load_bias(a.b[0], F0, h, ba);
     if (a.obs) {
         // the input normalisation fused in (ppo_obs_normalize's formula): thread -> row tid / 4, 16 columns
         static_assert(kFRows * kK0 == 16 * kFThreads, "16 input columns per thread");
@@ -419,14 +428,6 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     Rsrc rh[5];
 #pragma unroll
     for (int l = 0; l < 5; ++l) rh[l] = rsrc(STORE ? a.h[l] : nullptr, STORE ? int64_t(rows) * hs * 2 : 0);
-    // Weight slices double-buffered in registers (wa / wb): layer l + 1's slice is requested at the start
-    // of layer l, ahead of layer l's activation stores (a load waited for with vmcnt also waits for every
-    // older store of the wave).  Bias vectors likewise one layer ahead.
-    V8 wa[16], wb[16];
-    float ba[16], bb[16];
-    f32x16 pend = {};
-    load_wa<DT, kK0 / 16>(a.w[0], kK0, F0, i, h, wa);
-    load_bias(a.b[0], F0, h, ba);
     __syncthreads();
     load_wa<DT, 16>(a.w[1], kHid, F0, i, h, wb);
     load_bias(a.b[1], F0, h, bb);
