@@ -267,12 +267,11 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
     const float* __restrict__ actions, float* __restrict__ ds_mu, float* __restrict__ ds_sigma,
     const float* __restrict__ old_nlp, const float* __restrict__ adv_, const float* __restrict__ old_v,
     const float* __restrict__ ret_, ppo_loss_cfg_t cfg, const float* __restrict__ grad_scale, float* __restrict__ dhead,
-    float* __restrict__ partials, uint16_t* __restrict__ dhead_lp, int lp_dtype, ppo_loss_fin_t fin) {
+    float* __restrict__ partials, uint16_t* __restrict__ dhead_lp, int lp_dtype) {
     static_assert(A + 1 <= 32, "heads of at most 32 outputs");
     constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT, RP = NV | 1;
     constexpr int NJ = (A + 1 + kLossLanes - 1) / kLossLanes;
-    __shared__ float s_red[2 * kLossRows * RP];  // per-row contributions; the finalize's block partials
-    __shared__ int last_s;
+    __shared__ float s_red[kLossRows * RP];  // per-row contributions
     const int tid = threadIdx.x, g = tid % kLossLanes, rl = tid / kLossLanes;
     const int r = blockIdx.x * kLossRows + rl;  // minibatch row
     const bool ok = r < mb_rows;
@@ -399,10 +398,10 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
         }
     }
     __syncthreads();
-    // block partials: value k summed over the block's rows in a fixed order (four chains).  With the fused
-    // finalize they are handed to the last block without fences (MI355X_MICROARCH.md, the hand-off table's
-    // first row): agent-scope (sc1) stores, each storing wave's vmcnt(0), a workgroup barrier, ONE
-    // relaxed agent-scope counter add; the block whose add returns the last count reads them with sc1 loads
+    // block partials: value k summed over the block's rows in a fixed order (four chains); ppo_loss_finalize
+    // sums them over the blocks.  (Round 5 measured the finalize folded into this kernel's last block --
+    // sc1 hand-off, relaxed agent counter -- at 16.9 us against 11.5 us for the two launches: each block's
+    // store drain and counter round trip sit on the kernel's tail, scripts/loss_bench.py.)
     if (tid < NV) {
         float t[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
@@ -410,44 +409,8 @@ __global__ void __launch_bounds__(kLossThreads) k_loss_grad(
 #pragma unroll
             for (int u = 0; u < 4; ++u) t[u] += s_red[(rr + u) * RP + tid];
         }
-        __hip_atomic_store(partials + int64_t(blockIdx.x) * NV + tid, (t[0] + t[1]) + (t[2] + t[3]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        partials[int64_t(blockIdx.x) * NV + tid] = (t[0] + t[1]) + (t[2] + t[3]);
     }
-    if (!fin.counter) return;  // uniform
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0)
-        last_s = __hip_atomic_fetch_add(fin.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == int(gridDim.x) - 1;
-    __syncthreads();
-    if (!last_s) return;
-    // the last block: every block's partials into LDS (all lanes loading, independent sc1 loads in flight
-    // together), then value k summed over the blocks in block order
-    const int nblk = gridDim.x;
-    constexpr int kPass = 2 * kLossRows;
-    float acc = 0.f;
-    for (int b0 = 0; b0 < nblk; b0 += kPass) {
-        const int nb = min(kPass, nblk - b0);
-        __syncthreads();  // the previous pass's sums are done with s_red
-        for (int e = tid; e < nb * NV; e += kLossThreads) {
-            const int bb = e / NV, k = e - bb * NV;
-            s_red[bb * RP + k] = __hip_atomic_load(partials + int64_t(b0) * NV + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        if (tid < NV) {
-            float c4[4] = {0.f, 0.f, 0.f, 0.f};
-            int bb = 0;
-#pragma unroll 4
-            for (; bb + 4 <= nb; bb += 4)
-#pragma unroll
-                for (int u = 0; u < 4; ++u) c4[u] += s_red[(bb + u) * RP + tid];
-            for (; bb < nb; ++bb) c4[0] += s_red[bb * RP + tid];
-            acc += (c4[0] + c4[1]) + (c4[2] + c4[3]);
-        }
-    }
-    if (tid < NV)
-        loss_finalize_value(tid, acc, A, mb_rows, fin.entropy_coef, grad_scale, fin.grad_head_bias, fin.grad_logstd,
-                            fin.stats, fin.stat_idx, fin.kl_out);
-    if (tid == 0) __hip_atomic_store(fin.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ partials, int nblk, int A, int mb_rows,
@@ -764,6 +727,20 @@ struct SegTable {
 // the end of a minibatch step (ppo_tail): GradScaler.update, the adaptive LR from the KL, Adam's step
 // count, the device minibatch / statistics counters -- one thread.  The inputs are read in one go (every
 // load issued before the first use: one memory round trip, not one per field)
+// ppo_tail's arguments
+struct ppo_tail_args_t {
+    double* lr;
+    const float* kl;
+    float kl_threshold;
+    double min_lr, max_lr;
+    double* step;
+    int32_t* mb_idx;
+    int32_t n_minibatches;
+    int32_t* stat_idx;
+    float* scaler;
+    int32_t growth_interval;
+};
+
 struct TailVals {
     double lr, step;
     float kl, scale, tracker;
@@ -890,118 +867,6 @@ __global__ void k_tail(ppo_tail_args_t t, const float* np, int nnp) {
     if (threadIdx.x == 0) tail_store(t, tail_load(t), t.scaler && b > 0.f);
 }
 
-// ppo_adam_step (round 5): the optimizer step as two launches.  k_sqnorm_step = k_sqnorm, and its last
-// block (a relaxed agent-scope counter; the partials handed over by sc1 stores / loads as in k_loss_grad)
-// forms the step's scalars ONCE -- k_adam's prologue arithmetic, same order, same fp64 bias corrections --
-// into hp, then runs the tail (lr / step / scaler are read for hp before the tail rewrites them).
-// k_adam_hp is then a plain streaming update: no per-block prologue.
-struct SqnormStepArgs {
-    float max_norm, b1, b2;
-    ppo_tail_args_t tail;
-    float* hp;  // [coef, inv_scale, step_size, bc2_sqrt, skip]
-};
-
-__global__ void __launch_bounds__(256) k_sqnorm_step(const float* __restrict__ g, int64_t n, float* __restrict__ partials,
-                                                     SqnormStepArgs a) {
-    __shared__ float red[2][256 / kWave];
-    __shared__ int last_s;
-    const float* scaler = a.tail.scaler;
-    {
-        const float inv_scale = scaler ? 1.f / scaler[0] : 1.f;
-        float s = 0.f, bad = 0.f;
-        for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-            const float x = g[i] * inv_scale;
-            s += x * x;
-            bad += __builtin_isfinite(g[i]) ? 0.f : 1.f;
-        }
-        s = wave_sum(s);
-        bad = wave_sum(bad);
-        if (threadIdx.x % kWave == 0) {
-            red[0][threadIdx.x / kWave] = s;
-            red[1][threadIdx.x / kWave] = bad;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            float t = 0.f, b = 0.f;
-            for (int w = 0; w < 256 / kWave; ++w) {
-                t += red[0][w];
-                b += red[1][w];
-            }
-            __hip_atomic_store(partials + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(partials + gridDim.x + blockIdx.x, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            last_s = __hip_atomic_fetch_add(a.tail.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                     int(gridDim.x) - 1;
-        }
-        __syncthreads();
-    }
-    if (!last_s) return;
-    TailVals tv;
-    if (threadIdx.x == 0) tv = tail_load(a.tail);  // in flight under the partial sums
-    const int nnp = gridDim.x;
-    float s = 0.f, bad = 0.f;
-    for (int k = threadIdx.x; k < nnp; k += 256) {
-        s += __hip_atomic_load(partials + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bad += __hip_atomic_load(partials + nnp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s = wave_sum(s);
-    bad = wave_sum(bad);
-    __syncthreads();
-    if (threadIdx.x % kWave == 0) {
-        red[0][threadIdx.x / kWave] = s;
-        red[1][threadIdx.x / kWave] = bad;
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    float t = 0.f, b = 0.f;
-    for (int w = 0; w < 256 / kWave; ++w) {
-        t += red[0][w];
-        b += red[1][w];
-    }
-    // k_adam's prologue, once
-    const float inv_scale = scaler ? 1.f / tv.scale : 1.f;
-    const bool skip = scaler && b > 0.f;
-    const float c = a.max_norm / (sqrtf(t) + 1e-6f);
-    const float coef = a.max_norm > 0.f ? (c < 1.f || c != c ? c : 1.f) : 1.f;
-    const double ts = tv.step + 1.0;
-    a.hp[0] = coef;
-    a.hp[1] = inv_scale;
-    a.hp[2] = float(tv.lr / (1.0 - pow(double(a.b1), ts)));
-    a.hp[3] = float(sqrt(1.0 - pow(double(a.b2), ts)));
-    a.hp[4] = skip ? 1.f : 0.f;
-    tail_store(a.tail, tv, skip);
-    __hip_atomic_store(a.tail.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ void __launch_bounds__(kAdamThreads) k_adam_hp(float* __restrict__ p, const float* __restrict__ g,
-                                                          float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                          float b1, float b2, float eps, SegTable segs,
-                                                          uint16_t* __restrict__ mirror, int mirror_dtype,
-                                                          const float* __restrict__ hp) {
-    const float coef = hp[0], inv_scale = hp[1], step_size = hp[2], bc2_sqrt = hp[3];
-    const int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x;
-    if (hp[4] != 0.f || i >= n) return;
-    const float gi = (g[i] * inv_scale) * coef;
-    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    const float pi = p[i] - step_size * (mi / denom);
-    p[i] = pi;
-    if (mirror) {
-        for (int k = 0; k < segs.n; ++k) {
-            const ppo_seg_t& sg = segs.s[k];
-            if (i >= sg.off && i < sg.off + sg.len) {
-                const int64_t j = i - sg.off;
-                const int64_t r = j / sg.cols, c = j % sg.cols;
-                mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] =
-                    mirror_dtype == PPO_DT_F16 ? f32_to_f16(pi) : f32_to_bf16(pi);
-            }
-        }
-    }
-}
-
 inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
 }  // namespace
@@ -1052,7 +917,7 @@ static int launch_loss(const float* head, const float* logstd, int32_t A, int32_
                        const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
                        const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
                        const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
-                       const ppo_loss_fin_t& fin, void* stream) {
+                       void* stream) {
     if (dhead_lp && lp_dtype != PPO_DT_BF16 && lp_dtype != PPO_DT_F16)
         return fail(-1, "ppo_loss_grad: dhead_lp needs lp_dtype PPO_DT_BF16 or PPO_DT_F16");
     const dim3 grid(ppo_loss_blocks(mb_rows)), block(kLossThreads);
@@ -1060,7 +925,7 @@ static int launch_loss(const float* head, const float* logstd, int32_t A, int32_
     case AA:                                                                                                     \
         hipLaunchKernelGGL(k_loss_grad<AA>, grid, block, 0, S(stream), head, logstd, mb_rows, mb_idx, actions, \
                            ds_mu, ds_sigma, old_neglogp, advantages, old_values, returns, cfg, grad_scale, dhead,  \
-                           partials, dhead_lp, lp_dtype, fin);                                                  \
+                           partials, dhead_lp, lp_dtype);                                                  \
         break;
     switch (A) {
         PPO_LOSS_CASE(2)
@@ -1079,20 +944,9 @@ int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_
                   const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
                   void* stream) {
     return launch_loss(head, logstd, A, mb_rows, mb_idx, actions, ds_mu, ds_sigma, old_neglogp, advantages, old_values,
-                       returns, cfg, grad_scale, dhead, partials, dhead_lp, lp_dtype, ppo_loss_fin_t{}, stream);
+                       returns, cfg, grad_scale, dhead, partials, dhead_lp, lp_dtype, stream);
 }
 
-int ppo_loss_grad_fin(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
-                      const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
-                      const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
-                      const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
-                      const ppo_loss_fin_t* fin, void* stream) {
-    if (!fin || !fin->counter || !fin->grad_head_bias || !fin->grad_logstd || !fin->stats || !fin->stat_idx ||
-        !fin->kl_out)
-        return fail(-1, "ppo_loss_grad_fin: null finalize argument");
-    return launch_loss(head, logstd, A, mb_rows, mb_idx, actions, ds_mu, ds_sigma, old_neglogp, advantages, old_values,
-                       returns, cfg, grad_scale, dhead, partials, dhead_lp, lp_dtype, *fin, stream);
-}
 
 int ppo_loss_finalize(const float* partials, int32_t nblk, int32_t A, int32_t mb_rows, float entropy_coef,
                       const float* grad_scale, float* grad_head_bias, float* grad_logstd, float* stats,
@@ -1235,26 +1089,11 @@ static int check_tail(const ppo_tail_args_t& t, const float* sqnorm_partials) {
     return 0;
 }
 
-int ppo_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float* sqnorm_partials, float max_norm,
-                  float beta1, float beta2, float eps, const ppo_seg_t* segs_host, int32_t nseg, void* mirror,
-                  int32_t mirror_dtype, const ppo_tail_args_t* tail, float* hp, void* stream) {
-    if (!tail || !tail->counter || !hp || !sqnorm_partials) return fail(-1, "ppo_adam_step: null argument");
-    if (const int rc = check_tail(*tail, sqnorm_partials)) return rc;
-    SegTable t;
-    if (const int rc = seg_table(segs_host, nseg, mirror, mirror_dtype, t)) return rc;
-    const SqnormStepArgs a{max_norm, beta1, beta2, *tail, hp};
-    hipLaunchKernelGGL(k_sqnorm_step, dim3(kNormBlocks), dim3(256), 0, S(stream), g, n, sqnorm_partials, a);
-    if (const int rc = launched("k_sqnorm_step")) return rc;
-    hipLaunchKernelGGL(k_adam_hp, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0,
-                       S(stream), p, g, m, v, n, beta1, beta2, eps, t, static_cast<uint16_t*>(mirror), mirror_dtype, hp);
-    return launched("k_adam_hp");
-}
-
 int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,
              int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, float* scaler, const float* sqnorm_partials,
              int32_t nblk_norm, int32_t growth_interval, void* stream) {
     const ppo_tail_args_t t{lr, kl, kl_threshold, min_lr, max_lr, step, mb_idx, n_minibatches, stat_idx, scaler,
-                            growth_interval, nullptr};
+                            growth_interval};
     if (const int rc = check_tail(t, sqnorm_partials)) return rc;
     hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, S(stream), t, sqnorm_partials, nblk_norm);
     return launched("k_tail");

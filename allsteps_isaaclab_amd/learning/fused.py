@@ -76,18 +76,6 @@ class PpoWgrad(C.Structure):
                 ("dtype", C.c_int32)]
 
 
-class PpoLossFin(C.Structure):
-    _fields_ = [("entropy_coef", C.c_float), ("grad_head_bias", C.c_void_p), ("grad_logstd", C.c_void_p),
-                ("stats", C.c_void_p), ("stat_idx", C.c_void_p), ("kl_out", C.c_void_p), ("counter", C.c_void_p)]
-
-
-class PpoTailArgs(C.Structure):
-    _fields_ = [("lr", C.c_void_p), ("kl", C.c_void_p), ("kl_threshold", C.c_float), ("min_lr", C.c_double),
-                ("max_lr", C.c_double), ("step", C.c_void_p), ("mb_idx", C.c_void_p), ("n_minibatches", C.c_int32),
-                ("stat_idx", C.c_void_p), ("scaler", C.c_void_p), ("growth_interval", C.c_int32),
-                ("counter", C.c_void_p)]
-
-
 class PpoSeg(C.Structure):
     _fields_ = [("off", C.c_int64), ("len", C.c_int64), ("moff", C.c_int64), ("cols", C.c_int32),
                 ("mstride", C.c_int32), ("trans", C.c_int32)]
@@ -98,8 +86,7 @@ EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
                     "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update",
-                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_adam_step",
-                    "ppo_loss_grad_fin"]
+                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id"]
 
 
 def load() -> C.CDLL:
@@ -117,14 +104,10 @@ def load() -> C.CDLL:
     L.ppo_obs_normalize.argtypes = [V, V, I32, I32, V, V, F32, V, I32, I32, I32, V]
     L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V, V, I32, V]
     L.ppo_loss_finalize.argtypes = [V, I32, I32, I32, F32, V, V, V, V, V, V, V]
-    L.ppo_loss_grad_fin.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V, V, I32,
-                                    C.POINTER(PpoLossFin), V]
     L.ppo_elu_bwd.argtypes = [V, I32, V, I32, V, I32, I32, I32, V, V]
     L.ppo_sqnorm.argtypes = [V, I64, V, V, V]
     L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32, V, V]
     L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V, V, I32, I32, V]
-    L.ppo_adam_step.argtypes = [V, V, V, V, I64, V, F32, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32,
-                                C.POINTER(PpoTailArgs), V, V]
     L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
     L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
     L.ppo_counter_add.argtypes = [V, I64, V]
@@ -241,11 +224,6 @@ class FusedPPOUpdate:
         self.stat_partials = torch.empty(L.ppo_obs_stats_blocks(B) * 2 * 64, device=dev, dtype=torch.float64)
         self.norm_partials = torch.empty(2 * L.ppo_sqnorm_blocks(), device=dev)  # norm sums | non-finite counts
         self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
-        self.tail_counter = torch.zeros(1, device=dev, dtype=torch.int32)  # ppo_adam_step's finished-block count
-        self.step_hp = torch.zeros(8, device=dev)  # ppo_adam_step's per-step scalars
-        self.loss_counter = torch.zeros(1, device=dev, dtype=torch.int32)  # ppo_loss_grad_fin's
-        self._loss_fin = PpoLossFin()
-        self._tail_args = PpoTailArgs()
         self.stat_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stats = torch.zeros(agent.mini_epochs_num * self.n_mb + 1, PPO_LOSS_NSTAT, device=dev)
         # grads of the trunk / heads as views of the flat bucket
@@ -489,17 +467,14 @@ class FusedPPOUpdate:
         nl = len(self.linears)
         # no zero_grad: every entry of the [grads | kl] bucket is written below (loss finalize: head
         # biases, log-sigma, kl; the reduce jobs: every weight and bias gradient)
-        # losses, KL, head gradients, and (the kernel's last block) their sums over the minibatch
-        fin = self._loss_fin
-        fin.entropy_coef, fin.grad_head_bias, fin.grad_logstd = self.loss_cfg.entropy_coef, _p(self.gbh), _p(self.gls)
-        fin.stats, fin.stat_idx, fin.kl_out, fin.counter = (_p(self.stats), _p(self.stat_idx), _p(self.flat.extra),
-                                                            _p(self.loss_counter))
-        _check(L.ppo_loss_grad_fin(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
-                                   _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
-                                   _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.scaler),
-                                   None if self.mfma_trunk else _p(self.dhead), _p(self.loss_partials),
-                                   _p(self.dhead_lp) if self.mfma_trunk else None, self.dt_code, C.byref(fin), s),
-               "ppo_loss_grad_fin")
+        _check(L.ppo_loss_grad(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
+                               _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
+                               _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.scaler),
+                               None if self.mfma_trunk else _p(self.dhead), _p(self.loss_partials),
+                               _p(self.dhead_lp) if self.mfma_trunk else None, self.dt_code, s), "ppo_loss_grad")
+        _check(L.ppo_loss_finalize(_p(self.loss_partials), self.loss_partials.shape[0], A, B,
+                                   self.loss_cfg.entropy_coef, _p(self.scaler), _p(self.gbh), _p(self.gls),
+                                   _p(self.stats), _p(self.stat_idx), _p(self.flat.extra), s), "ppo_loss_finalize")
         S = self.S
         hl = self.h_last_f
         jobs, keep = [], []
@@ -572,19 +547,16 @@ class FusedPPOUpdate:
     def _optimizer_step(self) -> None:
         L, s, ag, fl = self.L, self._stream(), self.agent, self.flat
         n = fl.numel
+        _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.scaler), _p(self.norm_partials), s), "ppo_sqnorm")
         opt = ag.optimizer
-        # clip_grad_norm_ + Adam + the tail (GradScaler.update, adaptive LR, Adam's step count, the device
-        # minibatch / statistics counters) in two launches: the norm kernel's last workgroup forms the
-        # step's scalars once and runs the tail; the Adam launch streams the buffer
-        t = self._tail_args
-        t.lr, t.kl, t.kl_threshold = _p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0
-        t.min_lr, t.max_lr, t.step, t.mb_idx, t.n_minibatches = self.min_lr, self.max_lr, _p(opt.step_t), _p(self.mb_idx), self.n_mb
-        t.stat_idx, t.scaler, t.growth_interval, t.counter = (_p(self.stat_idx), _p(self.scaler), SCALER_GROWTH_INTERVAL,
-                                                              _p(self.tail_counter))
-        _check(L.ppo_adam_step(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
-                               _p(self.norm_partials), ag.grad_norm if ag.truncate_grads else 0.0, opt.beta1,
-                               opt.beta2, opt.eps, self.segs, self.nseg, _p(self.mirror),
-                               self.dt_code if self.lp else 1, C.byref(t), _p(self.step_hp), s), "ppo_adam_step")
+        _check(L.ppo_adam(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
+                          _p(self.norm_partials), self.norm_partials.numel() // 2,
+                          ag.grad_norm if ag.truncate_grads else 0.0, _p(ag.lr), _p(opt.step_t), opt.beta1, opt.beta2,
+                          opt.eps, self.segs, self.nseg, _p(self.mirror), self.dt_code if self.lp else 1,
+                          _p(self.scaler), s), "ppo_adam")
+        _check(L.ppo_tail(_p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr, self.max_lr,
+                          _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), _p(self.scaler),
+                          _p(self.norm_partials), self.norm_partials.numel() // 2, SCALER_GROWTH_INTERVAL, s), "ppo_tail")
 
     # ------------------------------------------------------------------ graphs
     def _run(self, key, fn) -> None:

@@ -20,8 +20,6 @@
  *                                         torch.cuda.amp.GradScaler) the unscale, the skip of a step
  *                                         with non-finite gradients and the scale update
  *   ppo_tail                              adaptive LR from the (rank-averaged) KL; minibatch counter
- *   ppo_adam_step                         ppo_sqnorm + ppo_adam + ppo_tail in two launches
- *   ppo_loss_grad_fin                     ppo_loss_grad + ppo_loss_finalize in one launch
  *   ppo_mlp_forward / ppo_mlp_backward    the whole trunk forward / input-gradient chain (MFMA)
  *   ppo_weight_grads                      split-K weight + bias gradients of all trunk layers and the
  *                                         head weights (MFMA, one launch)
@@ -97,23 +95,6 @@ int ppo_loss_grad(const float* head, const float* logstd, int32_t A, int32_t mb_
                   const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
                   const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
                   void* stream);
-/* ppo_loss_grad + ppo_loss_finalize in ONE launch (round 5): the last block to finish -- counted on
- * `counter`, a device int32 that starts at 0 and that the call leaves at 0 -- sums every block's partials
- * (nblk = ppo_loss_blocks(mb_rows)) and writes what ppo_loss_finalize writes. */
-typedef struct {
-    float entropy_coef;
-    float* grad_head_bias;
-    float* grad_logstd;
-    float* stats;
-    const int32_t* stat_idx;
-    float* kl_out;
-    int32_t* counter;
-} ppo_loss_fin_t;
-int ppo_loss_grad_fin(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
-                      const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
-                      const float* advantages, const float* old_values, const float* returns, ppo_loss_cfg_t cfg,
-                      const float* grad_scale, float* dhead, float* partials, uint16_t* dhead_lp, int32_t lp_dtype,
-                      const ppo_loss_fin_t* fin, void* stream);
 /* sum the partials: bias grads of the heads -> grad_head_bias (A+1), logstd grads (+ -entropy_coef) ->
  * grad_logstd (A); the statistics (means) -> stats[stat_idx][PPO_LOSS_NSTAT] (stat_idx from device);
  * the KL also -> kl_out (the slot that rides in the gradient all-reduce); grad_scale as ppo_loss_grad */
@@ -266,28 +247,6 @@ int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, dou
              int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, float* scaler, const float* sqnorm_partials,
              int32_t nblk_norm, int32_t growth_interval, void* stream);
 
-/* The whole optimizer half of a minibatch step (round 5): ppo_sqnorm, ppo_adam and ppo_tail in two
- * launches.  The norm kernel's last block -- counted on tail->counter, a device int32 that starts at 0
- * and that the call leaves at 0 -- forms the step's scalars once (clip coefficient, unscale, skip, the
- * bias corrections from lr / step) into hp (device, 5 floats of scratch), then runs the tail; the Adam
- * launch reads hp.  sqnorm_partials: 2 * ppo_sqnorm_blocks() floats.  Same results as the three calls
- * (lr, step and scaler come from the tail struct). */
-typedef struct {
-    double* lr;
-    const float* kl;
-    float kl_threshold;
-    double min_lr, max_lr;
-    double* step;
-    int32_t* mb_idx;
-    int32_t n_minibatches;
-    int32_t* stat_idx;
-    float* scaler;
-    int32_t growth_interval;
-    int32_t* counter;
-} ppo_tail_args_t;
-int ppo_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float* sqnorm_partials, float max_norm,
-                  float beta1, float beta2, float eps, const ppo_seg_t* segs_host, int32_t nseg, void* mirror,
-                  int32_t mirror_dtype, const ppo_tail_args_t* tail, float* hp, void* stream);
 
 #ifdef __cplusplus
 }

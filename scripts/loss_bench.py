@@ -1,8 +1,7 @@
-"""HIP-event time per launch of the PPO loss kernel at a minibatch of `rows` (A = 21): ppo_loss_grad alone,
-ppo_loss_grad + ppo_loss_finalize, and ppo_loss_grad_fin (the finalize in the kernel's last block); and of
-the optimizer step: ppo_sqnorm + ppo_adam + ppo_tail vs ppo_adam_step, on a 333k-element flat buffer.
+"""HIP-event time per launch of the PPO loss kernel at a minibatch of `rows` (A = 21): ppo_loss_grad alone and
+ppo_loss_grad + ppo_loss_finalize; and of the optimizer step ppo_sqnorm + ppo_adam + ppo_tail on a
+333k-element flat buffer with a row-major and a transposed fp16 mirror segment.
     python scripts/loss_bench.py [rows]"""
-import ctypes as C
 import json
 import os
 import sys
@@ -43,18 +42,14 @@ def main():
     dlp = torch.zeros(B, 32, device=dev, dtype=torch.float16)
     part = torch.zeros(nblk, 2 * A + 1 + 5, device=dev)
     ghb, gls, stats = torch.zeros(A + 1, device=dev), torch.zeros(A, device=dev), torch.zeros(2000, 5, device=dev)
-    sidx, kl, ctr = torch.zeros(1, device=dev, dtype=torch.int32), torch.zeros(1, device=dev), \
-        torch.zeros(1, device=dev, dtype=torch.int32)
+    sidx, kl = torch.zeros(1, device=dev, dtype=torch.int32), torch.zeros(1, device=dev)
     args = (head.data_ptr(), logstd.data_ptr(), A, B, idx.data_ptr(), *[x.data_ptr() for x in ds], cfg, scale.data_ptr(),
             None, part.data_ptr(), dlp.data_ptr(), FU.PPO_DT[torch.float16])
-    fin = FU.PpoLossFin(0.01, ghb.data_ptr(), gls.data_ptr(), stats.data_ptr(), sidx.data_ptr(), kl.data_ptr(),
-                        ctr.data_ptr())
     out = {"rows": B,
            "loss_grad_us": t(lambda: L.ppo_loss_grad(*args, s)),
            "loss_grad_then_finalize_us": t(lambda: (L.ppo_loss_grad(*args, s), L.ppo_loss_finalize(
                part.data_ptr(), nblk, A, B, 0.01, scale.data_ptr(), ghb.data_ptr(), gls.data_ptr(), stats.data_ptr(),
-               sidx.data_ptr(), kl.data_ptr(), s))),
-           "loss_grad_fin_us": t(lambda: L.ppo_loss_grad_fin(*args, C.byref(fin), s))}
+               sidx.data_ptr(), kl.data_ptr(), s)))}
     n = 333_333
     grads = r(n)
     p, m, v = r(n), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
@@ -66,9 +61,6 @@ def main():
     step = torch.tensor([7.0], device=dev, dtype=torch.float64)
     scaler = torch.tensor([65536.0, 0.0], device=dev)
     mb, st = torch.zeros(1, device=dev, dtype=torch.int32), torch.zeros(1, device=dev, dtype=torch.int32)
-    hp = torch.zeros(8, device=dev)
-    tl = FU.PpoTailArgs(lr.data_ptr(), kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4,
-                        st.data_ptr(), scaler.data_ptr(), 1 << 30, ctr.data_ptr())
 
     def three():
         L.ppo_sqnorm(grads.data_ptr(), n, scaler.data_ptr(), partials.data_ptr(), s)
@@ -78,9 +70,6 @@ def main():
                    scaler.data_ptr(), partials.data_ptr(), nb, 1 << 30, s)
 
     out["sqnorm_adam_tail_us"] = t(three)
-    out["adam_step_us"] = t(lambda: L.ppo_adam_step(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n,
-                                                    partials.data_ptr(), 1.0, 0.9, 0.999, 1e-8, segs, 2,
-                                                    mirror.data_ptr(), 2, C.byref(tl), hp.data_ptr(), s))
     print(json.dumps(out), flush=True)
 
 

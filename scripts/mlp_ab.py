@@ -93,7 +93,15 @@ def main():
         assert fwd() == 0 and bwd() == 0
         torch.cuda.synchronize()
         out[tag] = {"h": [t[:, :256].float().clone() for t in hs], "head": head.clone(),
-                    "dz": [t.float().clone() for t in dzs], "fwd_us": timed(fwd), "bwd_us": timed(bwd)}
+                    "dz": [t.float().clone() for t in dzs], "fn": (fwd, bwd), "keep": (a, b, hs, head, dzs),
+                    "fwd_us": 1e9, "bwd_us": 1e9}
+    # alternate the two libraries over rounds and keep each one's best: the first timing of a process runs
+    # while the clocks ramp (the library timed first used to read 2-4 us slower whichever it was)
+    for _ in range(5):
+        for tag in ("A", "B"):
+            fwd, bwd = out[tag]["fn"]
+            out[tag]["fwd_us"] = min(out[tag]["fwd_us"], timed(fwd))
+            out[tag]["bwd_us"] = min(out[tag]["bwd_us"], timed(bwd))
     A, B = out["A"], out["B"]
     rep = {"rows": rows, "dtype": str(dt), "obs": use_obs, "fwd_us": [A["fwd_us"], B["fwd_us"]], "bwd_us": [A["bwd_us"], B["bwd_us"]]}
     for k in ("h", "dz"):

@@ -595,121 +595,6 @@ def test_weight_grads_kernel(rows, splits, dt):
         assert torch.isnan(part[k][:, :, kin + nb:]).all(), k
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("bad", [False, True])
-def test_adam_step_equals_sqnorm_adam_tail(bad):
-    """ppo_adam_step (the norm kernel's last workgroup forms the step's scalars and runs the tail; a
-    streaming Adam launch) == ppo_sqnorm, ppo_adam, ppo_tail, bit for bit: parameters, moments, the fp16
-    mirror, lr / step / scaler / counters; the finished-block counter is back at 0 (a graph replays it).
-    bad: a non-finite gradient (the scaler skips the step and backs off)."""
-    import ctypes as C
-
-    from allsteps_isaaclab_amd.learning import fused as FU
-
-    L = FU.load()
-    dev = "cuda:0"
-    g = torch.Generator(device=dev).manual_seed(9)
-    n = 333_333
-    s = torch.cuda.current_stream().cuda_stream
-    grads = torch.randn(n, device=dev, generator=g) * 100.0
-    if bad:
-        grads[n // 3] = float("inf")
-    nb = L.ppo_sqnorm_blocks()
-    seg = FU.PpoSeg(1000, 256 * 64, 0, 64, 72, 0)
-    segs = (FU.PpoSeg * 1)(seg)
-    outs = []
-    for fused in (False, True):
-        partials = torch.empty(2 * nb, device=dev)
-        p = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
-        m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
-        mirror = torch.zeros(256 * 72, device=dev, dtype=torch.float16)
-        lr = torch.tensor([3e-4], device=dev, dtype=torch.float64)
-        step = torch.tensor([7.0], device=dev, dtype=torch.float64)
-        scaler = torch.tensor([65536.0, 1999.0], device=dev)
-        kl = torch.tensor([0.03], device=dev)
-        mb, st, ctr = (torch.zeros(1, device=dev, dtype=torch.int32) for _ in range(3))
-        hp = torch.zeros(8, device=dev)
-        if fused:
-            t = FU.PpoTailArgs(lr.data_ptr(), kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4,
-                               st.data_ptr(), scaler.data_ptr(), 2000, ctr.data_ptr())
-            FU._check(L.ppo_adam_step(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, partials.data_ptr(),
-                                      1.0, 0.9, 0.999, 1e-8, segs, 1, mirror.data_ptr(), FU.PPO_DT[torch.float16],
-                                      C.byref(t), hp.data_ptr(), s), "ppo_adam_step")
-        else:
-            FU._check(L.ppo_sqnorm(grads.data_ptr(), n, scaler.data_ptr(), partials.data_ptr(), s), "sqnorm")
-            FU._check(L.ppo_adam(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, partials.data_ptr(), nb,
-                                 1.0, lr.data_ptr(), step.data_ptr(), 0.9, 0.999, 1e-8, segs, 1, mirror.data_ptr(),
-                                 FU.PPO_DT[torch.float16], scaler.data_ptr(), s), "ppo_adam")
-            FU._check(L.ppo_tail(lr.data_ptr(), kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4,
-                                 st.data_ptr(), scaler.data_ptr(), partials.data_ptr(), nb, 2000, s), "ppo_tail")
-        torch.cuda.synchronize()
-        outs.append([partials, p, m, v, mirror, lr, step, scaler, mb, st, ctr])
-    for a, b in zip(*outs):
-        assert torch.equal(a, b), (a, b)
-    _, p, _, _, _, lr, step, scaler, mb, st, ctr = outs[1]
-    assert int(ctr) == 0 and int(mb) == 1 and int(st) == 1
-    if bad:  # skipped: step count kept, scale halved, lr still adapted from the KL
-        assert float(step) == 7.0 and float(scaler[0]) == 32768.0
-    else:    # applied: step + 1, the growth interval reached -> scale doubled
-        assert float(step) == 8.0 and float(scaler[0]) == 131072.0
-    assert float(lr) == pytest.approx(3e-4 / 1.5)  # kl 0.03 > 2 x 0.008
-
-
-@pytest.mark.gpu
-def test_loss_grad_fin_launch_equals_grad_then_finalize():
-    """ppo_loss_grad_fin (the finalize run by the loss kernel's last block) vs ppo_loss_grad then
-    ppo_loss_finalize on the same minibatch: per-row outputs (dhead, its 16-bit copy, the dataset's new
-    mu / sigma, the block partials) bit for bit; the sums (head-bias and log-sigma gradients, statistics,
-    KL) to fp32 rounding (another fixed summation order); the block counter back at 0."""
-    import ctypes as C
-
-    from allsteps_isaaclab_amd.learning import fused as FU
-
-    L = FU.load()
-    dev, A, B = "cuda:0", 21, 4000
-    g = torch.Generator(device=dev).manual_seed(4)
-    r = lambda *sh: torch.randn(*sh, device=dev, generator=g)  # noqa: E731
-    head = r(B, A + 1) * 0.5
-    logstd = r(A) * 0.1
-    idx = torch.tensor([1], device=dev, dtype=torch.int32)
-    ds = {"actions": r(2 * B, A), "mu": r(2 * B, A) * 0.3, "sigma": torch.exp(r(2 * B, A) * 0.1),
-          "nlp": r(2 * B).abs() * 5 + 20, "adv": r(2 * B), "v": r(2 * B), "ret": r(2 * B)}
-    cfg = FU.PpoLossCfg(0.2, 4.0, 0.0, 1e-4, 1.1, 1, 1, 1)
-    scale = torch.tensor([1024.0], device=dev)
-    s = torch.cuda.current_stream().cuda_stream
-    nblk = L.ppo_loss_blocks(B)
-    outs = []
-    for fused in (False, True):
-        d = {k: v.clone() for k, v in ds.items()}
-        dhead, dlp = torch.zeros(B, A + 1, device=dev), torch.zeros(B, 32, device=dev, dtype=torch.float16)
-        part = torch.zeros(nblk, 2 * A + 1 + 5, device=dev)
-        ghb, gls, stats = torch.zeros(A + 1, device=dev), torch.zeros(A, device=dev), torch.zeros(3, 5, device=dev)
-        sidx, kl, ctr = torch.tensor([2], device=dev, dtype=torch.int32), torch.zeros(1, device=dev), \
-            torch.zeros(1, device=dev, dtype=torch.int32)
-        args = (head.data_ptr(), logstd.data_ptr(), A, B, idx.data_ptr(), d["actions"].data_ptr(), d["mu"].data_ptr(),
-                d["sigma"].data_ptr(), d["nlp"].data_ptr(), d["adv"].data_ptr(), d["v"].data_ptr(), d["ret"].data_ptr(),
-                cfg, scale.data_ptr(), dhead.data_ptr(), part.data_ptr(), dlp.data_ptr(), FU.PPO_DT[torch.float16])
-        if fused:
-            fin = FU.PpoLossFin(0.01, ghb.data_ptr(), gls.data_ptr(), stats.data_ptr(), sidx.data_ptr(), kl.data_ptr(),
-                                ctr.data_ptr())
-            FU._check(L.ppo_loss_grad_fin(*args, C.byref(fin), s), "ppo_loss_grad_fin")
-        else:
-            FU._check(L.ppo_loss_grad(*args, s), "ppo_loss_grad")
-            FU._check(L.ppo_loss_finalize(part.data_ptr(), nblk, A, B, 0.01, scale.data_ptr(), ghb.data_ptr(),
-                                          gls.data_ptr(), stats.data_ptr(), sidx.data_ptr(), kl.data_ptr(), s),
-                      "ppo_loss_finalize")
-        torch.cuda.synchronize()
-        outs.append(([dhead, dlp, d["mu"], d["sigma"], part], [ghb, gls, stats, kl], ctr))
-    (exact_a, sums_a, _), (exact_b, sums_b, ctr) = outs
-    for a, b in zip(exact_a, exact_b):
-        assert torch.equal(a, b)
-    for a, b in zip(sums_a, sums_b):
-        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
-    assert int(ctr) == 0
-    assert torch.equal(dlp[:, A + 1:], torch.zeros_like(dlp[:, A + 1:]))
-    torch.testing.assert_close(dlp[:, :A + 1].float(), exact_b[0], rtol=1e-3, atol=1e-7)
-
-
 def test_weight_grads_rejects_bad_arguments():
     import ctypes as C
 
