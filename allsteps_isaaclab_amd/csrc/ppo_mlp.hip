@@ -226,11 +226,10 @@ __device__ __forceinline__ void mma_rows(const uint16_t* X, const typename Lp<DT
 }
 
 #ifndef PPO_MLP_PRIO
-// static s_setprio 1 for waves 4..7 of the trunk kernels (MI355X_MICROARCH.md "Two waves per SIMD" item 4:
-// the second-dispatched half otherwise loses every VALU arbitration to its SIMD partner).  A/B on one box
-// (scripts/mlp_ab.py, 32768 rows, fp16, r05i): forward 46.3 -> 45.2 us, backward 49.9 -> 45.8 us, outputs
-// bit-identical
-#define PPO_MLP_PRIO 1
+// A/B knob: static s_setprio 1 for waves 4..7 of the trunk kernels (MI355X_MICROARCH.md "Two waves per
+// SIMD" item 4).  Measured with the libraries alternated over rounds (scripts/mlp_ab.py, r05l): forward
+// 55.3 / 55.7 us, backward 44.8 / 44.5 us with / without -- no effect, so off
+#define PPO_MLP_PRIO 0
 #endif
 #ifndef PPO_FWD_DBG
 #define PPO_FWD_DBG 0  // timing-only builds (scripts/fwd_dbg.sh): 2 no exp, 4 no stores, 16 no MFMA, 32 no ELU / convert
@@ -375,21 +374,26 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     const int F0 = 32 * wave;                 // this wave's output features
     const int row0 = blockIdx.x * kFRows;
     const int rows = a.rows;
-    // Weight slices double-buffered in registers (wa / wb): layer l + 1's slice is requested at the start
-    // of layer l, ahead of layer l's activation stores (a load waited for with vmcnt also waits for every
-    // older store of the wave).  Bias vectors likewise one layer ahead.  Layer 0's are requested first,
-    // so they fly under the input normalisation below.
-    V8 wa[16], wb[16];
-    float ba[16], bb[16];
-    f32x16 pend = {};
-    load_wa<DT, kK0 / 16>(a.w[0], kK0, F0, i, h, wa);
-    load_bias(a.b[0], F0, h, ba);
     if (a.obs) {
-        // the input normalisation fused in (ppo_obs_normalize's formula): thread -> row tid / 4, 16 columns
+        // the input normalisation fused in (ppo_obs_normalize's formula): the column constants (float(mean),
+        // sqrtf(float(var) + eps)) formed once per workgroup into scratch at the head of X1 (layer 0 writes
+        // X1 only after the barriers below), then thread -> row tid / 4, 16 columns, its 16 loads issued
+        // together (after the barrier: held across it they pushed the kernel past 256 VGPRs)
         static_assert(kFRows * kK0 == 16 * kFThreads, "16 input columns per thread");
-        typedef typename Lp<DT>::e E;
+        float* nm = reinterpret_cast<float*>(X1);
+        float* nd = nm + kK0;
+        if (threadIdx.x < kK0) {
+            const int c = threadIdx.x;
+            const bool in = c < a.obs_dim;
+            nm[c] = in ? float(a.mean[c]) : 0.f;
+            nd[c] = in ? sqrtf(float(a.var[c]) + a.eps) : 1.f;
+        }
+        __syncthreads();
         const int r = threadIdx.x >> 2, c0 = 16 * (threadIdx.x & 3), row = row0 + r;
         const float* src = a.obs + (int64_t(*a.mb_idx) * rows + row) * a.obs_dim;
+        float x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = c0 + k < a.obs_dim && row < rows ? src[c0 + k] : 0.f;
         uint32_t dw[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -397,12 +401,7 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int c = c0 + 2 * k + e;
-                float y = 0.f;
-                if (c < a.obs_dim && row < rows) {
-                    const float mf = float(a.mean[c]), den = sqrtf(float(a.var[c]) + a.eps);
-                    y = fminf(fmaxf((src[c] - mf) / den, -5.f), 5.f);
-                }
-                v[e] = y;
+                v[e] = c < a.obs_dim && row < rows ? fminf(fmaxf((x[2 * k + e] - nm[c]) / nd[c], -5.f), 5.f) : 0.f;
             }
             dw[k] = pack2<DT>(f32x2_t{v[0], v[1]});
         }
@@ -424,6 +423,14 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
             *reinterpret_cast<uint4*>(X0 + r * kXs + 8 * q) = v;
         }
     }
+    // Weight slices double-buffered in registers (wa / wb): layer l + 1's slice is requested at the start
+    // of layer l, ahead of layer l's activation stores (a load waited for with vmcnt also waits for every
+    // older store of the wave).  Bias vectors likewise one layer ahead.
+    V8 wa[16], wb[16];
+    float ba[16], bb[16];
+    f32x16 pend = {};
+    load_wa<DT, kK0 / 16>(a.w[0], kK0, F0, i, h, wa);
+    load_bias(a.b[0], F0, h, ba);
     const int hs = a.h_stride;
     Rsrc rh[5];
 #pragma unroll
