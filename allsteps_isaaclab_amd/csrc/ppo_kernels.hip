@@ -643,16 +643,17 @@ __global__ void __launch_bounds__(64) k_meter_update(const float* __restrict__ p
 
 struct JobTable {
     ppo_reduce_job_t j[PPO_MAX_JOBS];
-    int64_t start[PPO_MAX_JOBS + 1];  // first thread of each job
-    int vec[PPO_MAX_JOBS];            // columns per thread: 4 (float4 path) or 1
+    int32_t count[PPO_MAX_JOBS];          // threads of each job
+    int32_t blk_start[PPO_MAX_JOBS + 1];  // first block of each job (blocks never straddle two jobs)
+    int vec[PPO_MAX_JOBS];                // columns per thread: 4 (float4 path) or 1
     int n;
 };
 
 template <int V>
-__device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int64_t o) {
+__device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int o) {
     typedef float fv __attribute__((ext_vector_type(V)));
     const int cols = jb.dst_cols / V;
-    const int r = int(o / cols), c = int(o % cols) * V;
+    const int r = o / cols, c = (o - r * cols) * V;
     const float* src = jb.src + int64_t(r) * jb.src_cols + c;
     fv s = {};
     // up to 32 loads in flight per chunk (every split of the trainer's jobs at once), the chunk predicated,
@@ -669,16 +670,19 @@ __device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int64_t 
 }
 
 // dst[r][c] = sum_q src[q][r][c] in q order; one thread per output element, or per 4 consecutive
-// elements when the job's strides and pointers allow 16-B accesses (the same per-element sums)
+// elements when the job's strides and pointers allow 16-B accesses (the same per-element sums).  Each
+// block belongs to one job, found by a block-uniform (scalar) search: a per-thread search over the job
+// table was a chain of dependent vector loads ahead of every thread's first partial load.
 __global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
-    const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= t.start[t.n]) return;
+    const int b = blockIdx.x;
     int k = 0;
-    while (e >= t.start[k + 1]) ++k;
+    while (b >= t.blk_start[k + 1]) ++k;
+    const int o = (b - t.blk_start[k]) * 256 + threadIdx.x;
+    if (o >= t.count[k]) return;
     if (t.vec[k] == 4)
-        reduce_cols<4>(t.j[k], e - t.start[k]);
+        reduce_cols<4>(t.j[k], o);
     else
-        reduce_cols<1>(t.j[k], e - t.start[k]);
+        reduce_cols<1>(t.j[k], o);
 }
 
 // ------------------------------------------------------------------------------ clip + Adam
@@ -986,7 +990,7 @@ int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stre
     if (njobs <= 0 || njobs > PPO_MAX_JOBS) return fail(-1, "ppo_reduce_rows: 1..16 jobs");
     JobTable t{};
     t.n = njobs;
-    t.start[0] = 0;
+    t.blk_start[0] = 0;
     for (int k = 0; k < njobs; ++k) {
         const ppo_reduce_job_t& j = jobs_host[k];
         if (j.S <= 0 || j.dst_cols <= 0 || j.src_cols < j.dst_cols || j.dst_stride < j.dst_cols || !j.src || !j.dst)
@@ -995,10 +999,13 @@ int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stre
         const bool v4 = j.dst_cols % 4 == 0 && j.src_cols % 4 == 0 && j.dst_stride % 4 == 0 && j.src_n % 4 == 0 &&
                         (reinterpret_cast<uintptr_t>(j.src) | reinterpret_cast<uintptr_t>(j.dst)) % 16 == 0;
         t.vec[k] = v4 ? 4 : 1;
-        t.start[k + 1] = t.start[k] + int64_t(j.out_rows) * j.dst_cols / t.vec[k];
+        const int64_t cnt = int64_t(j.out_rows) * j.dst_cols / t.vec[k];
+        if (cnt > (int64_t(1) << 30)) return fail(-1, "ppo_reduce_rows: job too large");
+        t.count[k] = int32_t(cnt);
+        t.blk_start[k + 1] = t.blk_start[k] + int32_t((cnt + 255) / 256);
     }
-    const int64_t n = t.start[njobs];
-    hipLaunchKernelGGL(k_reduce_rows, dim3(unsigned((n + 255) / 256)), dim3(256), 0, S(stream), t);
+    for (int k = njobs; k < PPO_MAX_JOBS; ++k) t.blk_start[k + 1] = t.blk_start[njobs];
+    hipLaunchKernelGGL(k_reduce_rows, dim3(unsigned(t.blk_start[njobs])), dim3(256), 0, S(stream), t);
     return launched("k_reduce_rows");
 }
 
