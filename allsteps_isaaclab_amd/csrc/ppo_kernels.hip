@@ -14,6 +14,7 @@
 #include <stdio.h>
 
 #include "ppo.h"
+#include "ppo_loss.h"
 
 namespace {
 
@@ -234,24 +235,6 @@ constexpr int kLossLanes = 8;
 constexpr int kLossRows = 128;                         // rows per block
 constexpr int kLossThreads = kLossRows * kLossLanes;   // 1024
 
-// ppo_loss_finalize's output for value k of the block-partial sums (s = the sum over blocks)
-__device__ __forceinline__ void loss_finalize_value(int k, float s, int A, int mb_rows, float entropy_coef,
-                                                    const float* __restrict__ grad_scale, float* __restrict__ g_hb,
-                                                    float* __restrict__ g_ls, float* __restrict__ stats,
-                                                    const int32_t* __restrict__ stat_idx, float* __restrict__ kl_out) {
-    if (k <= A) {
-        g_hb[k] = s;
-    } else if (k <= 2 * A) {
-        // - entropy_coef * mean(entropy): d/d logstd_j = -entropy_coef (times the loss scale)
-        g_ls[k - A - 1] = s - entropy_coef * (grad_scale ? *grad_scale : 1.f);
-    } else {
-        const int st = k - 2 * A - 1;
-        const float mean = s / float(mb_rows);
-        stats[int64_t(*stat_idx) * PPO_LOSS_NSTAT + st] = mean;
-        if (st == 4) *kl_out = mean;
-    }
-}
-
 // sum over the eight lanes of a row (xor 1, xor 2 by quad permutes, then the mirrored half-row): the same
 // two operands meet on every lane, so all eight hold the bit-identical sum
 __device__ __forceinline__ float sum8(float x) {
@@ -434,7 +417,7 @@ __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ 
     float s = (sa[0] + sa[1]) + (sa[2] + sa[3]);
     s = wave_sum(s);
     if (threadIdx.x != 0) return;
-    loss_finalize_value(k, s, A, mb_rows, entropy_coef, grad_scale, g_hb, g_ls, stats, stat_idx, kl_out);
+    ppo_detail::loss_finalize_value(k, s, A, mb_rows, entropy_coef, grad_scale, g_hb, g_ls, stats, stat_idx, kl_out);
 }
 
 // ------------------------------------------------------------------------------ ELU backward

@@ -27,6 +27,7 @@
 #include <stdio.h>
 
 #include "ppo.h"
+#include "ppo_loss.h"
 
 namespace ppo_detail {
 void set_error(const char* msg);
@@ -218,6 +219,32 @@ __device__ __forceinline__ void wgrad_block(const uint16_t* __restrict__ dz, int
     }
 }
 
+// ppo_loss_finalize's work (include/ppo.h ppo_wgrad_t.loss): value k of the loss kernel's block partials
+// summed over the blocks in block order, the partials staged through LDS by all threads in passes
+__device__ void loss_finalize_side(const ppo_loss_side_t& f, float* sm) {
+    const int NV = 2 * f.A + 1 + PPO_LOSS_NSTAT;
+    const int chunk = (kLdsBytes / 4) / NV;
+    float acc = 0.f;
+    for (int b0 = 0; b0 < f.nblk; b0 += chunk) {
+        const int nb = min(chunk, f.nblk - b0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < nb * NV; e += kThreads) sm[e] = f.partials[int64_t(b0) * NV + e];
+        __syncthreads();
+        if (int(threadIdx.x) < NV) {
+            float c4[4] = {0.f, 0.f, 0.f, 0.f};
+            int bb = 0;
+            for (; bb + 4 <= nb; bb += 4)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) c4[u] += sm[(bb + u) * NV + threadIdx.x];
+            for (; bb < nb; ++bb) c4[0] += sm[bb * NV + threadIdx.x];
+            acc += (c4[0] + c4[1]) + (c4[2] + c4[3]);
+        }
+    }
+    if (int(threadIdx.x) < NV)
+        ppo_detail::loss_finalize_value(threadIdx.x, acc, f.A, f.mb_rows, f.entropy_coef, f.grad_scale, f.grad_head_bias,
+                                        f.grad_logstd, f.stats, f.stat_idx, f.kl_out);
+}
+
 // block index -> job.  Trunk pairs (layer l < 5, split s) in layer-major order, two workgroups each
 // (output halves); the pairs are dealt in groups of 8 so that the halves of a pair sit 8 block indices
 // apart (same XCD, dispatched together); the last group holds the remainder.  Then the head splits.
@@ -249,6 +276,12 @@ __global__ void __launch_bounds__(kThreads, 1) k_wgrad(ppo_wgrad_t a) {
         float* part = a.part[5] + int64_t(s) * kHeadOut * a.hin_stride[5];
         wgrad_block<kHeadOut, 256, 1, 1, false, DT>(a.dz[5], kHeadOut, 0, a.hin[5], a.hin_stride[5], part,
                                                      r_begin, r_end, lds);
+        // the side job on the last head workgroup (a head split streams ~0.6 of a trunk split's bytes, so
+        // this one finishes early even with the finalize added)
+        if (s == S - 1 && a.loss.partials) {
+            __syncthreads();  // the block's LDS stages are done with
+            loss_finalize_side(a.loss, reinterpret_cast<float*>(lds));
+        }
     }
 }
 
@@ -267,6 +300,9 @@ extern "C" int ppo_weight_grads(const ppo_wgrad_t* args_host, void* stream) {
              (reinterpret_cast<uintptr_t>(a->dz[l]) | reinterpret_cast<uintptr_t>(a->hin[l])) % 16 == 0;
         blocks += head ? a->splits[l] : 2 * a->splits[l];
     }
+    if (ok && a->loss.partials)  // the side job runs on the head job's last workgroup
+        ok = a->layers == 6 && a->loss.nblk > 0 && a->loss.A > 0 && a->loss.A <= PPO_MAX_ACT && a->loss.mb_rows > 0 &&
+             a->loss.grad_head_bias && a->loss.grad_logstd && a->loss.stats && a->loss.stat_idx && a->loss.kl_out;
     if (!ok) {
         snprintf(g_err, sizeof(g_err), "ppo_weight_grads: bad arguments");
         ppo_detail::set_error(g_err);

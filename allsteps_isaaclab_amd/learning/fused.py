@@ -70,10 +70,16 @@ class PpoMlpBwd(C.Structure):
                 ("h_stride", C.c_int32), ("dtype", C.c_int32)]
 
 
+class PpoLossSide(C.Structure):
+    _fields_ = [("partials", C.c_void_p), ("nblk", C.c_int32), ("A", C.c_int32), ("mb_rows", C.c_int32),
+                ("entropy_coef", C.c_float), ("grad_scale", C.c_void_p), ("grad_head_bias", C.c_void_p),
+                ("grad_logstd", C.c_void_p), ("stats", C.c_void_p), ("stat_idx", C.c_void_p), ("kl_out", C.c_void_p)]
+
+
 class PpoWgrad(C.Structure):
     _fields_ = [("dz", C.c_void_p * 6), ("hin", C.c_void_p * 6), ("part", C.c_void_p * 6), ("kin", C.c_int32 * 6),
                 ("hin_stride", C.c_int32 * 6), ("splits", C.c_int32 * 6), ("rows", C.c_int32), ("layers", C.c_int32),
-                ("dtype", C.c_int32)]
+                ("dtype", C.c_int32), ("loss", PpoLossSide)]
 
 
 class PpoSeg(C.Structure):
@@ -472,9 +478,10 @@ class FusedPPOUpdate:
                                _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.scaler),
                                None if self.mfma_trunk else _p(self.dhead), _p(self.loss_partials),
                                _p(self.dhead_lp) if self.mfma_trunk else None, self.dt_code, s), "ppo_loss_grad")
-        _check(L.ppo_loss_finalize(_p(self.loss_partials), self.loss_partials.shape[0], A, B,
-                                   self.loss_cfg.entropy_coef, _p(self.scaler), _p(self.gbh), _p(self.gls),
-                                   _p(self.stats), _p(self.stat_idx), _p(self.flat.extra), s), "ppo_loss_finalize")
+        if not self.mfma_trunk:  # (the MFMA path runs the finalize as a side job of ppo_weight_grads)
+            _check(L.ppo_loss_finalize(_p(self.loss_partials), self.loss_partials.shape[0], A, B,
+                                       self.loss_cfg.entropy_coef, _p(self.scaler), _p(self.gbh), _p(self.gls),
+                                       _p(self.stats), _p(self.stat_idx), _p(self.flat.extra), s), "ppo_loss_finalize")
         S = self.S
         hl = self.h_last_f
         jobs, keep = [], []
@@ -527,6 +534,13 @@ class FusedPPOUpdate:
         L, s, A = self.L, self._stream(), self.A
         jobs = []
         _check(L.ppo_mlp_backward(C.byref(self._mlp_bwd_args), s), "ppo_mlp_backward")
+        # + ppo_loss_finalize's work as the launch's side job (the head-bias / log-sigma gradients, the
+        # statistics, the KL)
+        f = self._wgrad_args.loss
+        f.partials, f.nblk, f.A, f.mb_rows = _p(self.loss_partials), self.loss_partials.shape[0], A, self.mb
+        f.entropy_coef, f.grad_scale, f.grad_head_bias, f.grad_logstd = (self.loss_cfg.entropy_coef, _p(self.scaler),
+                                                                          _p(self.gbh), _p(self.gls))
+        f.stats, f.stat_idx, f.kl_out = _p(self.stats), _p(self.stat_idx), _p(self.flat.extra)
         _check(L.ppo_weight_grads(C.byref(self._wgrad_args), s), "ppo_weight_grads")
         for i in range(6):
             w = self.h[i].shape[1]               # 72 or 264: [features | 1 | 0 ...]

@@ -200,6 +200,18 @@ int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream);
  * 128..255) placed on one XCD so that the layer input they both stream is fetched once into its L2;
  * the total count of trunk splits must be a multiple of 8.  The partials are summed by
  * ppo_reduce_rows. */
+/* ppo_loss_finalize's arguments, for running that work as a side job (below) */
+typedef struct {
+    const float* partials; /* ppo_loss_grad's block partials, nblk x (2A+1+PPO_LOSS_NSTAT); NULL = no side job */
+    int32_t nblk, A, mb_rows;
+    float entropy_coef;
+    const float* grad_scale;
+    float* grad_head_bias;
+    float* grad_logstd;
+    float* stats;
+    const int32_t* stat_idx;
+    float* kl_out;
+} ppo_loss_side_t;
 typedef struct {
     const uint16_t* dz[6];
     const uint16_t* hin[6];
@@ -209,6 +221,11 @@ typedef struct {
     int32_t splits[6];
     int32_t rows, layers;
     int32_t dtype; /* PPO_DT_BF16 or PPO_DT_F16 */
+    /* Side job (round 5): with loss.partials set (and layers == 6), the head job's last workgroup also does
+     * ppo_loss_finalize's work -- a head split streams about 0.6 of a trunk split's bytes, so that
+     * workgroup has the slack, and the minibatch step saves a launch.  Same outputs as ppo_loss_finalize
+     * (the sums over the blocks in block order: equal to its to fp32 rounding). */
+    ppo_loss_side_t loss;
 } ppo_wgrad_t;
 int ppo_weight_grads(const ppo_wgrad_t* args_host, void* stream);
 

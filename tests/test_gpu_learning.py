@@ -595,6 +595,58 @@ def test_weight_grads_kernel(rows, splits, dt):
         assert torch.isnan(part[k][:, :, kin + nb:]).all(), k
 
 
+@pytest.mark.gpu
+def test_weight_grads_side_job_equals_loss_finalize():
+    """ppo_weight_grads with the loss side job (ppo_wgrad_t.loss) writes what ppo_loss_finalize writes from
+    the same loss-kernel partials -- head-bias and log-sigma gradients, the statistics row, the KL -- to fp32
+    rounding (the blocks summed in another fixed order), and the weight-gradient partials are unchanged."""
+    import ctypes as C
+
+    from allsteps_isaaclab_amd.learning import fused as FU
+
+    L = FU.load()
+    dev, A, rows = "cuda:0", 21, 4096
+    g = torch.Generator(device=dev).manual_seed(8)
+    nblk = L.ppo_loss_blocks(rows)
+    partials = torch.randn(nblk, 2 * A + 1 + 5, device=dev, generator=g)
+    scale = torch.tensor([256.0], device=dev)
+    sidx = torch.tensor([1], device=dev, dtype=torch.int32)
+    s = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for side in (False, True):
+        ghb, gls, stats, kl = (torch.zeros(A + 1, device=dev), torch.zeros(A, device=dev), torch.zeros(3, 5, device=dev),
+                               torch.zeros(1, device=dev))
+        splits = FU.wgrad_splits(rows)
+        widths = [72] + [264] * 5
+        gg = torch.Generator(device=dev).manual_seed(2)
+        dz = [torch.randn(rows, 256 if k < 5 else 32, device=dev, generator=gg).half() for k in range(6)]
+        hin = [torch.randn(rows, w, device=dev, generator=gg).half() for w in widths]
+        part = [torch.zeros(splits[k], 256 if k < 5 else 32, widths[k], device=dev) for k in range(6)]
+        a = FU.PpoWgrad()
+        for k in range(6):
+            a.dz[k], a.hin[k], a.part[k] = dz[k].data_ptr(), hin[k].data_ptr(), part[k].data_ptr()
+            a.kin[k], a.hin_stride[k], a.splits[k] = 64 if k == 0 else 256, widths[k], splits[k]
+        a.rows, a.layers, a.dtype = rows, 6, FU.PPO_DT[torch.float16]
+        if side:
+            f = a.loss
+            f.partials, f.nblk, f.A, f.mb_rows, f.entropy_coef = partials.data_ptr(), nblk, A, rows, 0.01
+            f.grad_scale, f.grad_head_bias, f.grad_logstd = scale.data_ptr(), ghb.data_ptr(), gls.data_ptr()
+            f.stats, f.stat_idx, f.kl_out = stats.data_ptr(), sidx.data_ptr(), kl.data_ptr()
+        else:
+            FU._check(L.ppo_loss_finalize(partials.data_ptr(), nblk, A, rows, 0.01, scale.data_ptr(), ghb.data_ptr(),
+                                          gls.data_ptr(), stats.data_ptr(), sidx.data_ptr(), kl.data_ptr(), s),
+                      "ppo_loss_finalize")
+        FU._check(L.ppo_weight_grads(C.byref(a), s), "ppo_weight_grads")
+        torch.cuda.synchronize()
+        outs.append(([ghb, gls, stats, kl], part))
+    (sa, pa), (sb, pb) = outs
+    for x, y in zip(sa, sb):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-5)
+    assert float(sb[2][1].abs().sum()) > 0 and float(sb[2][0].abs().sum()) == 0  # the stat_idx row only
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+
+
 def test_weight_grads_rejects_bad_arguments():
     import ctypes as C
 
