@@ -218,182 +218,11 @@ __global__ void __launch_bounds__(kNormCols * kNormRowThreads) k_obs_normalize(
 
 // ------------------------------------------------------------------------------ PPO losses
 
-// gradient of max(u1, u2) (torch.maximum: ties split the gradient in half)
-__device__ __forceinline__ float max_grad(float u1, float u2, float g1, float g2) {
-    return u1 > u2 ? g1 : (u2 > u1 ? g2 : 0.5f * (g1 + g2));
-}
-
-// Eight lanes per row (round 5; the round-4 form spread a row over a 32-lane group -- 10 of 32 lanes idle,
-// the row sums as chains of LDS-routed permutes; a one-row-per-lane form ran out of parallelism, 512
-// waves for a 32768-row minibatch).  Lane g of a row owns head columns NJ*g .. NJ*g + NJ - 1 (the
-// actions, then the value column A; NJ = ceil((A + 1) / 8)), so a row's loads are one contiguous run
-// across its eight lanes; the row sums (sum d^2, the KL, the bound loss) are three DPP steps inside the
-// eight lanes (bit-identical on every lane); the per-row scalar work (ratio, clipping) runs on all eight.
-// The per-row contributions to the column sums land in an LDS table that NV threads sum down in row order
-// (deterministic), one partial row per block.
-constexpr int kLossLanes = 8;
-constexpr int kLossRows = 128;                         // rows per block
-constexpr int kLossThreads = kLossRows * kLossLanes;   // 1024
-
-// sum over the eight lanes of a row (xor 1, xor 2 by quad permutes, then the mirrored half-row): the same
-// two operands meet on every lane, so all eight hold the bit-identical sum
-__device__ __forceinline__ float sum8(float x) {
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
-    return x;
-}
 
 template <int A>
-__global__ void __launch_bounds__(kLossThreads) k_loss_grad(
-    const float* __restrict__ head, const float* __restrict__ logstd, int mb_rows, const int32_t* __restrict__ mb_idx,
-    const float* __restrict__ actions, float* __restrict__ ds_mu, float* __restrict__ ds_sigma,
-    const float* __restrict__ old_nlp, const float* __restrict__ adv_, const float* __restrict__ old_v,
-    const float* __restrict__ ret_, ppo_loss_cfg_t cfg, const float* __restrict__ grad_scale, float* __restrict__ dhead,
-    float* __restrict__ partials, uint16_t* __restrict__ dhead_lp, int lp_dtype) {
-    static_assert(A + 1 <= 32, "heads of at most 32 outputs");
-    constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT, RP = NV | 1;
-    constexpr int NJ = (A + 1 + kLossLanes - 1) / kLossLanes;
-    __shared__ float s_red[kLossRows * RP];  // per-row contributions
-    const int tid = threadIdx.x, g = tid % kLossLanes, rl = tid / kLossLanes;
-    const int r = blockIdx.x * kLossRows + rl;  // minibatch row
-    const bool ok = r < mb_rows;
-    const int64_t row = int64_t(*mb_idx) * mb_rows + (ok ? r : 0);
-    // the loss scale (a power of two, GradScaler) enters every gradient through the 1/B factor: exact
-    const float inv_b = (grad_scale ? *grad_scale : 1.f) * (1.f / float(mb_rows));
-    float sum_ls = 0.f;
-#pragma unroll
-    for (int j = 0; j < A; ++j) sum_ls += logstd[j];
-    const float entropy = float(A) * (0.5f + 0.5f * kLog2Pi) + sum_ls;
-    float hj[NJ], av[NJ], m1[NJ], s1[NJ], sg[NJ];
-#pragma unroll
-    for (int k = 0; k < NJ; ++k) {
-        const int j = NJ * g + k;
-        const bool act = ok && j < A;
-        hj[k] = ok && j <= A ? head[int64_t(r) * (A + 1) + j] : 0.f;
-        av[k] = act ? actions[row * A + j] : 0.f;
-        m1[k] = act ? ds_mu[row * A + j] : 0.f;
-        s1[k] = act ? ds_sigma[row * A + j] : 1.f;
-        sg[k] = j < A ? expf(logstd[j]) : 1.f;
-    }
-    const float onlp = ok ? old_nlp[row] : 0.f, adv = ok ? adv_[row] : 0.f;
-    const float vp = ok ? old_v[row] : 0.f, Rt = ok ? ret_[row] : 0.f;
-    // policy: d_j = (a_j - mu_j) / sigma_j; nlp = 0.5 sum d^2 + 0.5 log(2 pi) A + sum logstd;
-    // policy_kl(p0 = current, p1 = dataset); the bound loss
-    float d[NJ];
-    float q = 0.f, kl = 0.f, bl = 0.f;
-#pragma unroll
-    for (int k = 0; k < NJ; ++k) {
-        d[k] = 0.f;
-        if (NJ * g + k < A) {
-            d[k] = (av[k] - hj[k]) / sg[k];
-            q += d[k] * d[k];
-            const float dm = m1[k] - hj[k];
-            kl += logf(s1[k] / sg[k] + 1e-5f) + (sg[k] * sg[k] + dm * dm) / (2.f * (s1[k] * s1[k] + 1e-5f)) - 0.5f;
-            if (cfg.bound_loss == 1) {
-                const float lo = fminf(hj[k] + cfg.soft_bound, 0.f), hi = fmaxf(hj[k] - cfg.soft_bound, 0.f);
-                bl += lo * lo + hi * hi;
-            } else if (cfg.bound_loss == 2) {
-                bl += hj[k] * hj[k];
-            }
-        }
-    }
-    q = sum8(q);
-    kl = sum8(kl);
-    bl = sum8(bl);
-    const float nlp = 0.5f * q + 0.5f * kLog2Pi * float(A) + sum_ls;
-    float a_loss, g_nlp;
-    if (cfg.ppo) {
-        const float ratio = expf(onlp - nlp);
-        const float rc = fminf(fmaxf(ratio, 1.f - cfg.e_clip), 1.f + cfg.e_clip);
-        const float u1 = -adv * ratio, u2 = -adv * rc;
-        const bool inside = ratio >= 1.f - cfg.e_clip && ratio <= 1.f + cfg.e_clip;
-        // d(-adv * ratio)/d nlp = adv * ratio (d ratio / d nlp = -ratio); torch.maximum ties split
-        g_nlp = max_grad(u1, u2, adv * ratio, inside ? adv * ratio : 0.f);
-        a_loss = fmaxf(u1, u2);
-    } else {
-        a_loss = nlp * adv;
-        g_nlp = adv;
-    }
-    g_nlp *= inv_b;
-    float* red = s_red + rl * RP;
-    float gh[NJ];  // d loss / d head for this lane's columns (0 past the value column)
-#pragma unroll
-    for (int k = 0; k < NJ; ++k) {
-        const int j = NJ * g + k;
-        gh[k] = 0.f;
-        if (j < A) {
-            float dbj = 0.f;
-            if (cfg.bound_loss == 1) {
-                const float lo = fminf(hj[k] + cfg.soft_bound, 0.f), hi = fmaxf(hj[k] - cfg.soft_bound, 0.f);
-                dbj = 2.f * (lo + hi);
-            } else if (cfg.bound_loss == 2) {
-                dbj = 2.f * hj[k];
-            }
-            // d nlp / d mu = -d / sigma ; d nlp / d logstd = 1 - d^2
-            gh[k] = -g_nlp * d[k] / sg[k] + cfg.bounds_coef * inv_b * dbj;
-            red[j] = ok ? gh[k] : 0.f;
-            red[A + 1 + j] = ok ? g_nlp * (1.f - d[k] * d[k]) : 0.f;
-            if (ok) {
-                ds_mu[row * A + j] = hj[k];  // dataset.update_mu_sigma
-                ds_sigma[row * A + j] = sg[k];
-            }
-        } else if (j == A) {  // critic
-            const float v = hj[k];
-            float c_loss, g_v;
-            if (cfg.clip_value) {
-                const float dv = v - vp;
-                const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
-                const float l1 = (v - Rt) * (v - Rt), l2 = (vc - Rt) * (vc - Rt);
-                const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
-                g_v = max_grad(l1, l2, 2.f * (v - Rt), inside ? 2.f * (vc - Rt) : 0.f);
-                c_loss = fmaxf(l1, l2);
-            } else {
-                c_loss = (Rt - v) * (Rt - v);
-                g_v = 2.f * (v - Rt);
-            }
-            g_v *= 0.5f * cfg.critic_coef * inv_b;
-            gh[k] = g_v;
-            red[A] = ok ? g_v : 0.f;
-            red[2 * A + 1 + 1] = ok ? c_loss : 0.f;
-        }
-    }
-    if (g == 0) {
-        red[2 * A + 1 + 0] = ok ? a_loss : 0.f;
-        red[2 * A + 1 + 2] = ok ? bl : 0.f;
-        red[2 * A + 1 + 3] = ok ? entropy : 0.f;
-        red[2 * A + 1 + 4] = ok ? kl : 0.f;
-    }
-    if (ok) {
-        if (dhead) {
-#pragma unroll
-            for (int k = 0; k < NJ; ++k)
-                if (NJ * g + k <= A) dhead[int64_t(r) * (A + 1) + NJ * g + k] = gh[k];
-        }
-        // the 16-bit copy (autocast: the gradient reaching the heads' fp16 Linear is fp16), rows x 32, zero
-        // past the value column
-        if (dhead_lp) {
-            uint16_t* dl = dhead_lp + int64_t(r) * 32;
-#pragma unroll
-            for (int k = 0; k < NJ; ++k)
-                if (NJ * g + k < 32) dl[NJ * g + k] = lp_dtype == PPO_DT_F16 ? f32_to_f16(gh[k]) : f32_to_bf16(gh[k]);
-            for (int c = NJ * kLossLanes + g; c < 32; c += kLossLanes) dl[c] = 0;
-        }
-    }
-    __syncthreads();
-    // block partials: value k summed over the block's rows in a fixed order (four chains); ppo_loss_finalize
-    // sums them over the blocks.  (Round 5 measured the finalize folded into this kernel's last block --
-    // sc1 hand-off, relaxed agent counter -- at 16.9 us against 11.5 us for the two launches: each block's
-    // store drain and counter round trip sit on the kernel's tail, scripts/loss_bench.py.)
-    if (tid < NV) {
-        float t[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-        for (int rr = 0; rr < kLossRows; rr += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) t[u] += s_red[(rr + u) * RP + tid];
-        }
-        partials[int64_t(blockIdx.x) * NV + tid] = (t[0] + t[1]) + (t[2] + t[3]);
-    }
+__global__ void __launch_bounds__(ppo_detail::kLossThreads) k_loss_grad(ppo_detail::LossRowArgs p) {
+    __shared__ float s_red[ppo_detail::kLossRows * ppo_detail::loss_rp(A)];
+    ppo_detail::loss_block<A, ppo_detail::kLossThreads>(p, blockIdx.x, s_red);
 }
 
 __global__ void __launch_bounds__(64) k_loss_finalize(const float* __restrict__ partials, int nblk, int A, int mb_rows,
@@ -896,7 +725,7 @@ int ppo_obs_normalize(const float* x, const int32_t* mb_idx, int32_t mb_rows, in
     return launched("k_obs_normalize");
 }
 
-int ppo_loss_blocks(int32_t mb_rows) { return (mb_rows + kLossRows - 1) / kLossRows; }
+int ppo_loss_blocks(int32_t mb_rows) { return (mb_rows + ppo_detail::kLossRows - 1) / ppo_detail::kLossRows; }
 
 static int launch_loss(const float* head, const float* logstd, int32_t A, int32_t mb_rows, const int32_t* mb_idx,
                        const float* actions, float* ds_mu, float* ds_sigma, const float* old_neglogp,
@@ -905,12 +734,30 @@ static int launch_loss(const float* head, const float* logstd, int32_t A, int32_
                        void* stream) {
     if (dhead_lp && lp_dtype != PPO_DT_BF16 && lp_dtype != PPO_DT_F16)
         return fail(-1, "ppo_loss_grad: dhead_lp needs lp_dtype PPO_DT_BF16 or PPO_DT_F16");
-    const dim3 grid(ppo_loss_blocks(mb_rows)), block(kLossThreads);
-#define PPO_LOSS_CASE(AA)                                                                                        \
-    case AA:                                                                                                     \
-        hipLaunchKernelGGL(k_loss_grad<AA>, grid, block, 0, S(stream), head, logstd, mb_rows, mb_idx, actions, \
-                           ds_mu, ds_sigma, old_neglogp, advantages, old_values, returns, cfg, grad_scale, dhead,  \
-                           partials, dhead_lp, lp_dtype);                                                  \
+    const dim3 grid(ppo_loss_blocks(mb_rows)), block(ppo_detail::kLossThreads);
+    ppo_detail::LossRowArgs p{};
+    p.head = head;
+    p.head_stride = A + 1;
+    p.head_block_rows = true;
+    p.logstd = logstd;
+    p.mb_rows = mb_rows;
+    p.mb_idx = mb_idx;
+    p.actions = actions;
+    p.ds_mu = ds_mu;
+    p.ds_sigma = ds_sigma;
+    p.old_nlp = old_neglogp;
+    p.adv = advantages;
+    p.old_v = old_values;
+    p.ret = returns;
+    p.cfg = cfg;
+    p.grad_scale = grad_scale;
+    p.dhead = dhead;
+    p.dhead_lp = dhead_lp;
+    p.lp_dtype = lp_dtype;
+    p.partials = partials;
+#define PPO_LOSS_CASE(AA)                                                                          \
+    case AA:                                                                                       \
+        hipLaunchKernelGGL(k_loss_grad<AA>, grid, block, 0, S(stream), p);                         \
         break;
     switch (A) {
         PPO_LOSS_CASE(2)

@@ -1,6 +1,7 @@
-// ppo_loss.h -- the per-value output rule of the PPO loss finalize (ppo_loss_finalize), shared by the
-// finalize kernel (ppo_kernels.hip) and the same work run as a side job of the weight-gradient launch
-// (ppo_wgrad.hip).  Value k of the loss-kernel block partials, summed over the blocks (s):
+// ppo_loss.h -- the PPO loss block (ppo_loss_grad's per-row losses and head gradients for 128 minibatch
+// rows) and the per-value output rule of the loss finalize (ppo_loss_finalize), shared by the standalone
+// kernels (ppo_kernels.hip), the trunk forward that runs the loss block in its epilogue (ppo_mlp.hip) and
+// the weight-gradient launch that runs the finalize as a side job (ppo_wgrad.hip).  Value k of the loss-kernel block partials, summed over the blocks (s):
 //   k <= A: head-bias gradient; A < k <= 2A: log-sigma gradient minus entropy_coef (times the loss scale);
 //   k > 2A: statistic k - 2A - 1, as its mean over the minibatch (the KL also into kl_out).
 #pragma once
@@ -26,5 +27,222 @@ __device__ __forceinline__ void loss_finalize_value(int k, float s, int A, int m
         if (st == 4) *kl_out = mean;
     }
 }
+
+
+// one block's worth of ppo_loss_grad (include/ppo.h): rows [blk * kLossRows, +kLossRows) of the minibatch
+struct LossRowArgs {
+    const float* head;     // rows x head_stride fp32 ([mu | value]); global, or an LDS table of the block's rows
+    int head_stride;
+    bool head_block_rows;  // true: head row = minibatch row r; false: row r - blk * kLossRows (a block table)
+    const float* logstd;
+    int mb_rows;
+    const int32_t* mb_idx;
+    const float* actions;
+    float* ds_mu;
+    float* ds_sigma;
+    const float* old_nlp;
+    const float* adv;
+    const float* old_v;
+    const float* ret;
+    ppo_loss_cfg_t cfg;
+    const float* grad_scale;
+    float* dhead;          // rows x (A + 1) fp32, or NULL
+    uint16_t* dhead_lp;    // rows x 32 lp, or NULL
+    int lp_dtype;
+    float* partials;       // nblk x (2A + 1 + PPO_LOSS_NSTAT)
+};
+
+__device__ __forceinline__ uint16_t loss_bf16(float f) {  // round to nearest even
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7f800000u) == 0x7f800000u) return uint16_t((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return uint16_t(u >> 16);
+}
+__device__ __forceinline__ uint16_t loss_f16(float f) { return __builtin_bit_cast(uint16_t, static_cast<_Float16>(f)); }
+
+// gradient of max(u1, u2) (torch.maximum: ties split the gradient in half)
+__device__ __forceinline__ float loss_max_grad(float u1, float u2, float g1, float g2) {
+    return u1 > u2 ? g1 : (u2 > u1 ? g2 : 0.5f * (g1 + g2));
+}
+
+// Eight lanes per row (round 5; the round-4 form spread a row over a 32-lane group -- 10 of 32 lanes idle,
+// the row sums as chains of LDS-routed permutes; a one-row-per-lane form ran out of parallelism, 512
+// waves for a 32768-row minibatch).  Lane g of a row owns head columns NJ*g .. NJ*g + NJ - 1 (the
+// actions, then the value column A; NJ = ceil((A + 1) / 8)), so a row's loads are one contiguous run
+// across its eight lanes; the row sums (sum d^2, the KL, the bound loss) are three DPP steps inside the
+// eight lanes (bit-identical on every lane); the per-row scalar work (ratio, clipping) runs on all eight.
+// The per-row contributions to the column sums land in an LDS table that NV threads sum down in row order
+// (deterministic), one partial row per block.
+constexpr int kLossLanes = 8;
+constexpr int kLossRows = 128;                         // rows per block
+constexpr int kLossThreads = kLossRows * kLossLanes;   // 1024 (the standalone kernel: one pass)
+constexpr float kLog2PiL = 1.8378770664093453f;
+__host__ __device__ constexpr int loss_rp(int A) { return (2 * A + 1 + PPO_LOSS_NSTAT) | 1; }  // LDS row pitch
+
+// sum over the eight lanes of a row (xor 1, xor 2 by quad permutes, then the mirrored half-row): the same
+// two operands meet on every lane, so all eight hold the bit-identical sum
+__device__ __forceinline__ float sum8(float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
+    return x;
+}
+
+
+// NT threads (a multiple of 8) cover the block's 128 rows in 128 / (NT / 8) passes; s_red: kLossRows x
+// loss_rp(A) floats of LDS
+template <int A, int NT>
+__device__ void loss_block(const LossRowArgs& p, int blk, float* __restrict__ s_red) {
+    static_assert(A + 1 <= 32, "heads of at most 32 outputs");
+    static_assert(NT % kLossLanes == 0 && kLossRows % (NT / kLossLanes) == 0, "whole passes of rows");
+    constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT, RP = loss_rp(A);
+    constexpr int NJ = (A + 1 + kLossLanes - 1) / kLossLanes;
+    const ppo_loss_cfg_t cfg = p.cfg;
+    const int mb_rows = p.mb_rows;
+    const int tid = threadIdx.x, g = tid % kLossLanes;
+    // the loss scale (a power of two, GradScaler) enters every gradient through the 1/B factor: exact
+    const float inv_b = (p.grad_scale ? *p.grad_scale : 1.f) * (1.f / float(mb_rows));
+    float sum_ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < A; ++j) sum_ls += p.logstd[j];
+    const float entropy = float(A) * (0.5f + 0.5f * kLog2PiL) + sum_ls;
+    for (int pass = 0; pass < kLossRows / (NT / kLossLanes); ++pass) {
+    const int rl = pass * (NT / kLossLanes) + tid / kLossLanes;
+    const int r = blk * kLossRows + rl;  // minibatch row
+    const bool ok = r < mb_rows;
+    const int64_t row = int64_t(*p.mb_idx) * mb_rows + (ok ? r : 0);
+    const float* hrow = p.head + int64_t(p.head_block_rows ? r : rl) * p.head_stride;
+    float hj[NJ], av[NJ], m1[NJ], s1[NJ], sg[NJ];
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+        const int j = NJ * g + k;
+        const bool act = ok && j < A;
+        hj[k] = ok && j <= A ? hrow[j] : 0.f;
+        av[k] = act ? p.actions[row * A + j] : 0.f;
+        m1[k] = act ? p.ds_mu[row * A + j] : 0.f;
+        s1[k] = act ? p.ds_sigma[row * A + j] : 1.f;
+        sg[k] = j < A ? expf(p.logstd[j]) : 1.f;
+    }
+    const float onlp = ok ? p.old_nlp[row] : 0.f, adv = ok ? p.adv[row] : 0.f;
+    const float vp = ok ? p.old_v[row] : 0.f, Rt = ok ? p.ret[row] : 0.f;
+    // policy: d_j = (a_j - mu_j) / sigma_j; nlp = 0.5 sum d^2 + 0.5 log(2 pi) A + sum logstd;
+    // policy_kl(p0 = current, p1 = dataset); the bound loss
+    float d[NJ];
+    float q = 0.f, kl = 0.f, bl = 0.f;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+        d[k] = 0.f;
+        if (NJ * g + k < A) {
+            d[k] = (av[k] - hj[k]) / sg[k];
+            q += d[k] * d[k];
+            const float dm = m1[k] - hj[k];
+            kl += logf(s1[k] / sg[k] + 1e-5f) + (sg[k] * sg[k] + dm * dm) / (2.f * (s1[k] * s1[k] + 1e-5f)) - 0.5f;
+            if (cfg.bound_loss == 1) {
+                const float lo = fminf(hj[k] + cfg.soft_bound, 0.f), hi = fmaxf(hj[k] - cfg.soft_bound, 0.f);
+                bl += lo * lo + hi * hi;
+            } else if (cfg.bound_loss == 2) {
+                bl += hj[k] * hj[k];
+            }
+        }
+    }
+    q = sum8(q);
+    kl = sum8(kl);
+    bl = sum8(bl);
+    const float nlp = 0.5f * q + 0.5f * kLog2PiL * float(A) + sum_ls;
+    float a_loss, g_nlp;
+    if (cfg.ppo) {
+        const float ratio = expf(onlp - nlp);
+        const float rc = fminf(fmaxf(ratio, 1.f - cfg.e_clip), 1.f + cfg.e_clip);
+        const float u1 = -adv * ratio, u2 = -adv * rc;
+        const bool inside = ratio >= 1.f - cfg.e_clip && ratio <= 1.f + cfg.e_clip;
+        // d(-adv * ratio)/d nlp = adv * ratio (d ratio / d nlp = -ratio); torch.maximum ties split
+        g_nlp = loss_max_grad(u1, u2, adv * ratio, inside ? adv * ratio : 0.f);
+        a_loss = fmaxf(u1, u2);
+    } else {
+        a_loss = nlp * adv;
+        g_nlp = adv;
+    }
+    g_nlp *= inv_b;
+    float* red = s_red + rl * RP;
+    float gh[NJ];  // d loss / d head for this lane's columns (0 past the value column)
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+        const int j = NJ * g + k;
+        gh[k] = 0.f;
+        if (j < A) {
+            float dbj = 0.f;
+            if (cfg.bound_loss == 1) {
+                const float lo = fminf(hj[k] + cfg.soft_bound, 0.f), hi = fmaxf(hj[k] - cfg.soft_bound, 0.f);
+                dbj = 2.f * (lo + hi);
+            } else if (cfg.bound_loss == 2) {
+                dbj = 2.f * hj[k];
+            }
+            // d nlp / d mu = -d / sigma ; d nlp / d logstd = 1 - d^2
+            gh[k] = -g_nlp * d[k] / sg[k] + cfg.bounds_coef * inv_b * dbj;
+            red[j] = ok ? gh[k] : 0.f;
+            red[A + 1 + j] = ok ? g_nlp * (1.f - d[k] * d[k]) : 0.f;
+            if (ok) {
+                p.ds_mu[row * A + j] = hj[k];  // dataset.update_mu_sigma
+                p.ds_sigma[row * A + j] = sg[k];
+            }
+        } else if (j == A) {  // critic
+            const float v = hj[k];
+            float c_loss, g_v;
+            if (cfg.clip_value) {
+                const float dv = v - vp;
+                const float vc = vp + fminf(fmaxf(dv, -cfg.e_clip), cfg.e_clip);
+                const float l1 = (v - Rt) * (v - Rt), l2 = (vc - Rt) * (vc - Rt);
+                const bool inside = dv >= -cfg.e_clip && dv <= cfg.e_clip;
+                g_v = loss_max_grad(l1, l2, 2.f * (v - Rt), inside ? 2.f * (vc - Rt) : 0.f);
+                c_loss = fmaxf(l1, l2);
+            } else {
+                c_loss = (Rt - v) * (Rt - v);
+                g_v = 2.f * (v - Rt);
+            }
+            g_v *= 0.5f * cfg.critic_coef * inv_b;
+            gh[k] = g_v;
+            red[A] = ok ? g_v : 0.f;
+            red[2 * A + 1 + 1] = ok ? c_loss : 0.f;
+        }
+    }
+    if (g == 0) {
+        red[2 * A + 1 + 0] = ok ? a_loss : 0.f;
+        red[2 * A + 1 + 2] = ok ? bl : 0.f;
+        red[2 * A + 1 + 3] = ok ? entropy : 0.f;
+        red[2 * A + 1 + 4] = ok ? kl : 0.f;
+    }
+    if (ok) {
+        if (p.dhead) {
+#pragma unroll
+            for (int k = 0; k < NJ; ++k)
+                if (NJ * g + k <= A) p.dhead[int64_t(r) * (A + 1) + NJ * g + k] = gh[k];
+        }
+        // the 16-bit copy (autocast: the gradient reaching the heads' fp16 Linear is fp16), rows x 32, zero
+        // past the value column
+        if (p.dhead_lp) {
+            uint16_t* dl = p.dhead_lp + int64_t(r) * 32;
+#pragma unroll
+            for (int k = 0; k < NJ; ++k)
+                if (NJ * g + k < 32) dl[NJ * g + k] = p.lp_dtype == PPO_DT_F16 ? loss_f16(gh[k]) : loss_bf16(gh[k]);
+            for (int c = NJ * kLossLanes + g; c < 32; c += kLossLanes) dl[c] = 0;
+        }
+    }
+    }  // pass
+    __syncthreads();
+    // block partials: value k summed over the block's rows in a fixed order (four chains); ppo_loss_finalize
+    // sums them over the blocks.  (Round 5 measured the finalize folded into this kernel's last block --
+    // sc1 hand-off, relaxed agent counter -- at 16.9 us against 11.5 us for the two launches: each block's
+    // store drain and counter round trip sit on the kernel's tail, scripts/loss_bench.py.)
+    if (tid < NV) {
+        float t[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+        for (int rr = 0; rr < kLossRows; rr += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] += s_red[(rr + u) * RP + tid];
+        }
+        p.partials[int64_t(blk) * NV + tid] = (t[0] + t[1]) + (t[2] + t[3]);
+    }
+}
+
 
 }  // namespace ppo_detail

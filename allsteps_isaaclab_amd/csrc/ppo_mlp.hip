@@ -15,6 +15,7 @@
 #include <stdio.h>
 
 #include "ppo.h"
+#include "ppo_loss.h"
 
 namespace ppo_detail {
 void set_error(const char* msg);
@@ -359,7 +360,7 @@ __device__ __forceinline__ void layer(const uint16_t* Xin, uint16_t* Xout, const
     __syncthreads();
 }
 
-template <int DT, bool STORE>
+template <int DT, bool STORE, int LA>
 __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     typedef typename Lp<DT>::e E;
     typedef typename Lp<DT>::v8 V8;
@@ -456,28 +457,63 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     layer<DT, 16, STORE, true>(X0, X1, wa, ba, pend, rh[3], rh[4], hs, row0, F0, j, h);
     tile_epi<DT, STORE>(pend, X1, 96 + j, row0 + 96 + j, rh[4], hs, F0, h);
     __syncthreads();
-    // ---- heads: wave w < 4 takes N-tile w; out = 16-bit(acc + 16-bit(bh)) as under autocast
+    // ---- heads: wave w < 4 takes N-tile w; out = 16-bit(acc + 16-bit(bh)) as under autocast.  With the
+    // fused losses (LA > 0) the values also go to a table of the block's rows at the head of X0 (free: layer
+    // 5 has read it), the losses' input
+    constexpr int kHS = (LA + 1) | 1;
+    float* sh = reinterpret_cast<float*>(X0);
     if (wave < 4 && a.head) {
         f32x16 hacc[4];
         mma_rows<DT, 16, 1>(X1, wb, hacc, wave, j, h);
-        const int row = row0 + 32 * wave + j;
-        if (row < rows) {
+        const int rl = 32 * wave + j, row = row0 + rl;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int o = feat(r, h);
-                if (o < a.nh) a.head[int64_t(row) * a.nh + o] = float((E)(hacc[0][r] + float((E)bhv[r])));
-            }
+        for (int r = 0; r < 16; ++r) {
+            const int o = feat(r, h);
+            const float v = float((E)(hacc[0][r] + float((E)bhv[r])));
+            if (o < a.nh && row < rows) a.head[int64_t(row) * a.nh + o] = v;
+            if (LA > 0 && o <= LA) sh[rl * kHS + o] = v;
         }
+    }
+    if constexpr (LA > 0) {
+        // ppo_loss_grad's work for the block's rows (ppo_loss.h), eight lanes per row in two passes; the
+        // per-row table in X1 (the heads' MFMAs have read it)
+        __syncthreads();
+        ppo_detail::LossRowArgs p{};
+        p.head = sh;
+        p.head_stride = kHS;
+        p.head_block_rows = false;
+        p.logstd = a.loss.logstd;
+        p.mb_rows = rows;
+        p.mb_idx = a.mb_idx;
+        p.actions = a.loss.actions;
+        p.ds_mu = a.loss.ds_mu;
+        p.ds_sigma = a.loss.ds_sigma;
+        p.old_nlp = a.loss.old_neglogp;
+        p.adv = a.loss.advantages;
+        p.old_v = a.loss.old_values;
+        p.ret = a.loss.returns;
+        p.cfg = a.loss.cfg;
+        p.grad_scale = a.loss.grad_scale;
+        p.dhead = nullptr;
+        p.dhead_lp = a.loss.dhead_lp;
+        p.lp_dtype = DT;
+        p.partials = a.loss.partials;
+        static_assert(kFRows == ppo_detail::kLossRows, "one loss block per workgroup");
+        ppo_detail::loss_block<LA, kFThreads>(p, blockIdx.x, reinterpret_cast<float*>(X1));
     }
 }
 
-template <int DT>
+template <int DT, int LA>
 __global__ void __launch_bounds__(kFThreads, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
     // training stores layers 1..5 for the backward (all five pointers set); the rollout form stores none
-    if (a.h[0] && !(PPO_FWD_DBG & 4))
-        mlp_fwd_body<DT, true>(a);
-    else
-        mlp_fwd_body<DT, false>(a);
+    if constexpr (LA > 0) {
+        mlp_fwd_body<DT, true, LA>(a);
+    } else {
+        if (a.h[0] && !(PPO_FWD_DBG & 4))
+            mlp_fwd_body<DT, true, 0>(a);
+        else
+            mlp_fwd_body<DT, false, 0>(a);
+    }
 }
 
 // ------------------------------------------------------------------------------ backward chain
@@ -676,30 +712,12 @@ extern "C" int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream) {
     return 0;
 }
 
-extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
-    if (!args_host || (!args_host->x && !args_host->obs) || args_host->nh <= 0 || args_host->nh > 32 || args_host->rows <= 0 ||
-        (args_host->obs && (!args_host->mb_idx || !args_host->mean || !args_host->var || args_host->obs_dim <= 0 ||
-                            args_host->obs_dim > kK0)) ||
-        args_host->x_stride < kK0 || args_host->h_stride < kHid || (args_host->x_stride % 8) || (args_host->h_stride % 8) ||
-        (args_host->dtype != PPO_DT_BF16 && args_host->dtype != PPO_DT_F16) ||
-        // the activations are stored all five or not at all (the rollout form)
-        (args_host->h[0] && !(args_host->h[1] && args_host->h[2] && args_host->h[3] && args_host->h[4]))) {
-        snprintf(g_err, sizeof(g_err), "ppo_mlp_forward: bad arguments");
-        ppo_detail::set_error(g_err);
-        return -1;
-    }
-    static bool attr[2] = {false, false};
-    const bool f16 = args_host->dtype == PPO_DT_F16;
-    const int rc = f16 ? reserve_lds(k_mlp_fwd<PPO_DT_F16>, kFLds, attr[1], "ppo_mlp_forward")
-                       : reserve_lds(k_mlp_fwd<PPO_DT_BF16>, kFLds, attr[0], "ppo_mlp_forward");
-    if (rc) return rc;
-    const int blocks = (args_host->rows + kFRows - 1) / kFRows;
-    if (f16)
-        hipLaunchKernelGGL(k_mlp_fwd<PPO_DT_F16>, dim3(blocks), dim3(kFThreads), kFLds,
-                           static_cast<hipStream_t>(stream), *args_host);
-    else
-        hipLaunchKernelGGL(k_mlp_fwd<PPO_DT_BF16>, dim3(blocks), dim3(kFThreads), kFLds,
-                           static_cast<hipStream_t>(stream), *args_host);
+template <int DT, int LA>
+static int launch_fwd(const ppo_mlp_fwd_t* a, void* stream) {
+    static bool attr = false;
+    if (const int rc = reserve_lds(k_mlp_fwd<DT, LA>, kFLds, attr, "ppo_mlp_forward")) return rc;
+    const int blocks = (a->rows + kFRows - 1) / kFRows;
+    hipLaunchKernelGGL((k_mlp_fwd<DT, LA>), dim3(blocks), dim3(kFThreads), kFLds, static_cast<hipStream_t>(stream), *a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         snprintf(g_err, sizeof(g_err), "k_mlp_fwd: %s", hipGetErrorString(e));
@@ -707,4 +725,28 @@ extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
         return -2;
     }
     return 0;
+}
+
+extern "C" int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream) {
+    const ppo_mlp_fwd_t* a = args_host;
+    bool ok = a && (a->x || a->obs) && a->nh > 0 && a->nh <= 32 && a->rows > 0 &&
+              !(a->obs && (!a->mb_idx || !a->mean || !a->var || a->obs_dim <= 0 || a->obs_dim > kK0)) &&
+              a->x_stride >= kK0 && a->h_stride >= kHid && !(a->x_stride % 8) && !(a->h_stride % 8) &&
+              (a->dtype == PPO_DT_BF16 || a->dtype == PPO_DT_F16) &&
+              // the activations are stored all five or not at all (the rollout form)
+              !(a->h[0] && !(a->h[1] && a->h[2] && a->h[3] && a->h[4]));
+    const int LA = ok ? a->loss.A : 0;
+    if (ok && LA)  // the fused losses: training form, every dataset pointer, the heads' width A + 1
+        ok = (LA == 12 || LA == 21) && a->nh == LA + 1 && a->h[0] && a->head && a->mb_idx && a->loss.logstd &&
+             a->loss.actions && a->loss.ds_mu && a->loss.ds_sigma && a->loss.old_neglogp && a->loss.advantages &&
+             a->loss.old_values && a->loss.returns && a->loss.dhead_lp && a->loss.partials;
+    if (!ok) {
+        snprintf(g_err, sizeof(g_err), "ppo_mlp_forward: bad arguments");
+        ppo_detail::set_error(g_err);
+        return -1;
+    }
+    const bool f16 = a->dtype == PPO_DT_F16;
+    if (LA == 21) return f16 ? launch_fwd<PPO_DT_F16, 21>(a, stream) : launch_fwd<PPO_DT_BF16, 21>(a, stream);
+    if (LA == 12) return f16 ? launch_fwd<PPO_DT_F16, 12>(a, stream) : launch_fwd<PPO_DT_BF16, 12>(a, stream);
+    return f16 ? launch_fwd<PPO_DT_F16, 0>(a, stream) : launch_fwd<PPO_DT_BF16, 0>(a, stream);
 }

@@ -56,12 +56,20 @@ class PpoReduceJob(C.Structure):
                 ("src_cols", C.c_int32), ("dst_cols", C.c_int32), ("dst_stride", C.c_int32), ("src_n", C.c_int64)]
 
 
+class PpoFwdLoss(C.Structure):
+    _fields_ = [("A", C.c_int32), ("logstd", C.c_void_p), ("actions", C.c_void_p), ("ds_mu", C.c_void_p),
+                ("ds_sigma", C.c_void_p), ("old_neglogp", C.c_void_p), ("advantages", C.c_void_p),
+                ("old_values", C.c_void_p), ("returns", C.c_void_p), ("cfg", PpoLossCfg), ("grad_scale", C.c_void_p),
+                ("dhead_lp", C.c_void_p), ("partials", C.c_void_p)]
+
+
 class PpoMlpFwd(C.Structure):
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p * 5), ("b", C.c_void_p * 5), ("wh", C.c_void_p),
                 ("bh", C.c_void_p), ("h", C.c_void_p * 5), ("head", C.c_void_p),
                 ("rows", C.c_int32), ("nh", C.c_int32), ("x_stride", C.c_int32), ("h_stride", C.c_int32),
                 ("dtype", C.c_int32), ("obs", C.c_void_p), ("mb_idx", C.c_void_p), ("mean", C.c_void_p),
-                ("var", C.c_void_p), ("x_out", C.c_void_p), ("eps", C.c_float), ("obs_dim", C.c_int32)]
+                ("var", C.c_void_p), ("x_out", C.c_void_p), ("eps", C.c_float), ("obs_dim", C.c_int32),
+                ("loss", PpoFwdLoss)]
 
 
 class PpoMlpBwd(C.Structure):
@@ -356,7 +364,7 @@ class FusedPPOUpdate:
         return torch.cuda.current_stream(self.dev).cuda_stream
 
     # ------------------------------------------------------------------ the two halves
-    def _trunk(self, x, idx, rows, h, h_last_f, head) -> None:
+    def _trunk(self, x, idx, rows, h, h_last_f, head, fused_loss: bool = False) -> None:
         """Normalise rows [idx*rows, (idx+1)*rows) of x, run the trunk (16-bit mirror or fp32 weights) and
         the heads into head = [mu | value] (fp32 storage; with the MFMA trunk the heads run as rl_games'
         autocast runs them: 16-bit inputs / weights / bias, fp32 accumulation, a 16-bit-rounded output)."""
@@ -374,6 +382,14 @@ class FusedPPOUpdate:
             for i in range(5):
                 a.h[i] = h[i + 1].data_ptr() if len(h) > 1 else None
             a.head, a.rows = head.data_ptr(), rows
+            a.loss.A = 0
+            if fused_loss:  # the losses in the forward's epilogue (ppo_mlp_fwd_t.loss)
+                ds, fl = self.ds, a.loss
+                fl.A, fl.logstd, fl.actions = self.A, _p(self.logstd), _p(ds["actions"])
+                fl.ds_mu, fl.ds_sigma, fl.old_neglogp = _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"])
+                fl.advantages, fl.old_values, fl.returns = _p(ds["advantages"]), _p(ds["old_values"]), _p(ds["returns"])
+                fl.cfg, fl.grad_scale = self.loss_cfg, _p(self.scaler)
+                fl.dhead_lp, fl.partials = _p(self.dhead_lp), _p(self.loss_partials)
             _check(L.ppo_mlp_forward(C.byref(a), s), "ppo_mlp_forward")
             return
         _check(L.ppo_obs_normalize(_p(x), _p(idx), rows, self.obs_dim, _p(rms.running_mean), _p(rms.running_var),
@@ -469,15 +485,17 @@ class FusedPPOUpdate:
             _check(L.ppo_obs_stats_update(_p(self.stat_partials), L.ppo_obs_stats_blocks(B), self.obs_dim, B,
                                           _p(rms.running_mean), _p(rms.running_var), _p(rms.count), s),
                    "ppo_obs_stats_update")
-        self._trunk(ds["obs"], self.mb_idx, B, self.h, self.h_last_f, self.head)
+        fused_loss = self.mfma_trunk and A in (12, 21)  # the forward runs ppo_loss_grad's work too
+        self._trunk(ds["obs"], self.mb_idx, B, self.h, self.h_last_f, self.head, fused_loss)
         nl = len(self.linears)
         # no zero_grad: every entry of the [grads | kl] bucket is written below (loss finalize: head
         # biases, log-sigma, kl; the reduce jobs: every weight and bias gradient)
-        _check(L.ppo_loss_grad(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
-                               _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
-                               _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.scaler),
-                               None if self.mfma_trunk else _p(self.dhead), _p(self.loss_partials),
-                               _p(self.dhead_lp) if self.mfma_trunk else None, self.dt_code, s), "ppo_loss_grad")
+        if not fused_loss:
+            _check(L.ppo_loss_grad(_p(self.head), _p(self.logstd), A, B, _p(self.mb_idx), _p(ds["actions"]),
+                                   _p(ds["mu"]), _p(ds["sigma"]), _p(ds["old_logp_actions"]), _p(ds["advantages"]),
+                                   _p(ds["old_values"]), _p(ds["returns"]), self.loss_cfg, _p(self.scaler),
+                                   None if self.mfma_trunk else _p(self.dhead), _p(self.loss_partials),
+                                   _p(self.dhead_lp) if self.mfma_trunk else None, self.dt_code, s), "ppo_loss_grad")
         if not self.mfma_trunk:  # (the MFMA path runs the finalize as a side job of ppo_weight_grads)
             _check(L.ppo_loss_finalize(_p(self.loss_partials), self.loss_partials.shape[0], A, B,
                                        self.loss_cfg.entropy_coef, _p(self.scaler), _p(self.gbh), _p(self.gls),

@@ -167,6 +167,27 @@ typedef struct {
     uint16_t* x_out;
     float eps;
     int32_t obs_dim;
+    /* Fused losses (round 5): with loss.A > 0 (12 or 21; training form, every h[] set, obs set) the
+     * workgroup runs ppo_loss_grad's work for its 128 rows right after the heads, from the head values
+     * it holds (the minibatch is rows [*mb_idx * rows, ...) of the dataset tensors): the dataset's mu /
+     * sigma rows updated, the 16-bit head gradient into loss.dhead_lp (rows x 32, the trunk's dtype), one
+     * row of block partials per workgroup into loss.partials (ppo_loss_blocks(rows) rows) -- bit-identical
+     * to ppo_loss_grad, one launch fewer per minibatch. */
+    struct {
+        int32_t A;
+        const float* logstd;
+        const float* actions;
+        float* ds_mu;
+        float* ds_sigma;
+        const float* old_neglogp;
+        const float* advantages;
+        const float* old_values;
+        const float* returns;
+        ppo_loss_cfg_t cfg;
+        const float* grad_scale;
+        uint16_t* dhead_lp;
+        float* partials;
+    } loss;
 } ppo_mlp_fwd_t;
 int ppo_mlp_forward(const ppo_mlp_fwd_t* args_host, void* stream);
 

@@ -553,6 +553,69 @@ def test_fused_mlp_forward_normalises_its_input(rows, dt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rows,A,dt", [(32768, 21, torch.float16), (1000, 12, torch.bfloat16)])
+def test_fused_mlp_forward_runs_the_losses(rows, A, dt):
+    """ppo_mlp_forward with loss.A set runs ppo_loss_grad's work in its epilogue: the 16-bit head gradient,
+    the block partials and the dataset's updated mu / sigma equal a forward followed by ppo_loss_grad bit for
+    bit (the same loss block, ppo_loss.h, on the same head values), and the activations are unchanged."""
+    import ctypes as C
+
+    from allsteps_isaaclab_amd.learning import fused as FU
+
+    L = FU.load()
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(12)
+    r = lambda *sh: torch.randn(*sh, device=dev, generator=g)  # noqa: E731
+    obs = r(2 * rows, 59) * 2
+    idx = torch.tensor([1], dtype=torch.int32, device=dev)
+    mean, var = r(59).double() * 0.1, torch.rand(59, device=dev, generator=g, dtype=torch.float64) + 0.5
+    ws = [(r(256, 64 if i == 0 else 256) / 16).to(dt) for i in range(5)]
+    bs = [r(256) * 0.1 for _ in range(5)]
+    wh, bh = r(A + 1, 256) / 16, r(A + 1) * 0.1
+    logstd = r(A) * 0.1
+    ds0 = {"actions": r(2 * rows, A), "mu": r(2 * rows, A) * 0.3, "sigma": torch.exp(r(2 * rows, A) * 0.1),
+           "nlp": r(2 * rows).abs() * 2 + 25, "adv": r(2 * rows), "v": r(2 * rows), "ret": r(2 * rows)}
+    cfg = FU.PpoLossCfg(0.2, 4.0, 0.0, 1e-4, 1.1, 1, 1, 1)
+    scale = torch.tensor([1024.0], device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    nblk = L.ppo_loss_blocks(rows)
+    outs = []
+    for fused in (False, True):
+        ds = {k: v.clone() for k, v in ds0.items()}
+        x_out = torch.zeros(rows, 72, device=dev, dtype=dt)
+        hs = [torch.zeros(rows, 264, device=dev, dtype=dt) for _ in range(5)]
+        head = torch.zeros(rows, A + 1, device=dev)
+        dlp = torch.full((rows, 32), 7.0, device=dev, dtype=dt)
+        part = torch.zeros(nblk, 2 * A + 1 + 5, device=dev)
+        a = FU.PpoMlpFwd()
+        for i in range(5):
+            a.w[i], a.b[i], a.h[i] = ws[i].data_ptr(), bs[i].data_ptr(), hs[i].data_ptr()
+        a.wh, a.bh, a.head, a.rows, a.nh = wh.data_ptr(), bh.data_ptr(), head.data_ptr(), rows, A + 1
+        a.x_stride, a.h_stride, a.dtype = 72, 264, FU.PPO_DT[dt]
+        a.obs, a.mb_idx, a.mean, a.var, a.eps, a.obs_dim = (obs.data_ptr(), idx.data_ptr(), mean.data_ptr(),
+                                                            var.data_ptr(), 1e-5, 59)
+        a.x_out = x_out.data_ptr()
+        if fused:
+            fl = a.loss
+            fl.A, fl.logstd, fl.actions, fl.ds_mu, fl.ds_sigma = (A, logstd.data_ptr(), ds["actions"].data_ptr(),
+                                                                  ds["mu"].data_ptr(), ds["sigma"].data_ptr())
+            fl.old_neglogp, fl.advantages, fl.old_values, fl.returns = (ds["nlp"].data_ptr(), ds["adv"].data_ptr(),
+                                                                        ds["v"].data_ptr(), ds["ret"].data_ptr())
+            fl.cfg, fl.grad_scale, fl.dhead_lp, fl.partials = cfg, scale.data_ptr(), dlp.data_ptr(), part.data_ptr()
+        FU._check(L.ppo_mlp_forward(C.byref(a), s), "ppo_mlp_forward")
+        if not fused:
+            FU._check(L.ppo_loss_grad(head.data_ptr(), logstd.data_ptr(), A, rows, idx.data_ptr(),
+                                      ds["actions"].data_ptr(), ds["mu"].data_ptr(), ds["sigma"].data_ptr(),
+                                      ds["nlp"].data_ptr(), ds["adv"].data_ptr(), ds["v"].data_ptr(),
+                                      ds["ret"].data_ptr(), cfg, scale.data_ptr(), None, part.data_ptr(),
+                                      dlp.data_ptr(), FU.PPO_DT[dt], s), "ppo_loss_grad")
+        torch.cuda.synchronize()
+        outs.append([x_out, *hs, head, dlp, part, ds["mu"], ds["sigma"]])
+    for i, (p, q) in enumerate(zip(*outs)):
+        assert torch.equal(p, q), i
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rows,splits,dt", [(32768, None, torch.bfloat16), (1000, [3, 2, 5, 1, 4, 3], torch.bfloat16),
                                             (64, [1] * 6, torch.bfloat16), (32768, None, torch.float16),
                                             (1000, [2, 3, 3, 3, 3, 7], torch.float16)])
