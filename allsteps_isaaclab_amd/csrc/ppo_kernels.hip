@@ -459,10 +459,15 @@ struct JobTable {
     int32_t blk_start[PPO_MAX_JOBS + 1];  // first block of each job (blocks never straddle two jobs)
     int vec[PPO_MAX_JOBS];                // columns per thread: 4 (float4 path) or 1
     int n;
+    // ppo_reduce_rows_norm: k_sqnorm's partials of the values written (+ one block for the extra arrays)
+    float* norm;                          // [nblk sums of (v / scale)^2 | nblk non-finite counts], or NULL
+    const float* scaler;
+    const float* extra[2];
+    int32_t extra_n[2];
 };
 
 template <int V>
-__device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int o) {
+__device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int o, float inv_scale, float& sq, float& bad) {
     typedef float fv __attribute__((ext_vector_type(V)));
     const int cols = jb.dst_cols / V;
     const int r = o / cols, c = (o - r * cols) * V;
@@ -479,22 +484,62 @@ __device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int o) {
             if (q + u < jb.S) s += v[u];
     }
     *reinterpret_cast<fv*>(jb.dst + int64_t(r) * jb.dst_stride + c) = s;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+        const float x = s[e] * inv_scale;
+        sq += x * x;
+        bad += __builtin_isfinite(s[e]) ? 0.f : 1.f;
+    }
 }
 
 // dst[r][c] = sum_q src[q][r][c] in q order; one thread per output element, or per 4 consecutive
 // elements when the job's strides and pointers allow 16-B accesses (the same per-element sums).  Each
 // block belongs to one job, found by a block-uniform (scalar) search: a per-thread search over the job
-// table was a chain of dependent vector loads ahead of every thread's first partial load.
+// table was a chain of dependent vector loads ahead of every thread's first partial load.  With t.norm the
+// blocks also leave k_sqnorm's partials of what they wrote (one gradient pass fewer; a last block covers
+// the extra arrays -- the gradients other kernels wrote)
 __global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
     const int b = blockIdx.x;
-    int k = 0;
-    while (b >= t.blk_start[k + 1]) ++k;
-    const int o = (b - t.blk_start[k]) * 256 + threadIdx.x;
-    if (o >= t.count[k]) return;
-    if (t.vec[k] == 4)
-        reduce_cols<4>(t.j[k], o);
-    else
-        reduce_cols<1>(t.j[k], o);
+    const int nb = t.blk_start[t.n];
+    const float inv_scale = t.norm && t.scaler ? 1.f / t.scaler[0] : 1.f;
+    float sq = 0.f, bad = 0.f;
+    if (b < nb) {
+        int k = 0;
+        while (b >= t.blk_start[k + 1]) ++k;
+        const int o = (b - t.blk_start[k]) * 256 + threadIdx.x;
+        if (o < t.count[k]) {
+            if (t.vec[k] == 4)
+                reduce_cols<4>(t.j[k], o, inv_scale, sq, bad);
+            else
+                reduce_cols<1>(t.j[k], o, inv_scale, sq, bad);
+        }
+    } else {
+        for (int a = 0; a < 2; ++a)
+            for (int i = threadIdx.x; i < t.extra_n[a]; i += 256) {
+                const float v = t.extra[a][i];
+                const float x = v * inv_scale;
+                sq += x * x;
+                bad += __builtin_isfinite(v) ? 0.f : 1.f;
+            }
+    }
+    if (!t.norm) return;  // uniform
+    __shared__ float red[2][256 / kWave];
+    sq = wave_sum(sq);
+    bad = wave_sum(bad);
+    if (threadIdx.x % kWave == 0) {
+        red[0][threadIdx.x / kWave] = sq;
+        red[1][threadIdx.x / kWave] = bad;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a = 0.f, c = 0.f;
+        for (int w = 0; w < 256 / kWave; ++w) {
+            a += red[0][w];
+            c += red[1][w];
+        }
+        t.norm[b] = a;
+        t.norm[gridDim.x + b] = c;
+    }
 }
 
 // ------------------------------------------------------------------------------ clip + Adam
@@ -816,9 +861,9 @@ int ppo_elu_bwd(const void* dh, int32_t dh_dtype, const void* h, int32_t h_dtype
     return launched("k_elu_bwd");
 }
 
-int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stream) {
+static int reduce_table(const ppo_reduce_job_t* jobs_host, int32_t njobs, JobTable& t) {
     if (njobs <= 0 || njobs > PPO_MAX_JOBS) return fail(-1, "ppo_reduce_rows: 1..16 jobs");
-    JobTable t{};
+    t = JobTable{};
     t.n = njobs;
     t.blk_start[0] = 0;
     for (int k = 0; k < njobs; ++k) {
@@ -835,7 +880,33 @@ int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stre
         t.blk_start[k + 1] = t.blk_start[k] + int32_t((cnt + 255) / 256);
     }
     for (int k = njobs; k < PPO_MAX_JOBS; ++k) t.blk_start[k + 1] = t.blk_start[njobs];
+    return 0;
+}
+
+int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stream) {
+    JobTable t;
+    if (const int rc = reduce_table(jobs_host, njobs, t)) return rc;
     hipLaunchKernelGGL(k_reduce_rows, dim3(unsigned(t.blk_start[njobs])), dim3(256), 0, S(stream), t);
+    return launched("k_reduce_rows");
+}
+
+int ppo_reduce_rows_norm(const ppo_reduce_job_t* jobs_host, int32_t njobs, const float* scaler, const float* extra0,
+                         int32_t extra0_n, const float* extra1, int32_t extra1_n, float* norm_partials,
+                         int32_t max_blocks, int32_t* nblk_out, void* stream) {
+    JobTable t;
+    if (const int rc = reduce_table(jobs_host, njobs, t)) return rc;
+    const int nblk = t.blk_start[njobs] + 1;
+    if (!norm_partials || !nblk_out || nblk > max_blocks || extra0_n < 0 || extra1_n < 0 ||
+        (extra0_n && !extra0) || (extra1_n && !extra1))
+        return fail(-1, "ppo_reduce_rows_norm: bad norm arguments");
+    t.norm = norm_partials;
+    t.scaler = scaler;
+    t.extra[0] = extra0;
+    t.extra[1] = extra1;
+    t.extra_n[0] = extra0_n;
+    t.extra_n[1] = extra1_n;
+    *nblk_out = nblk;
+    hipLaunchKernelGGL(k_reduce_rows, dim3(unsigned(nblk)), dim3(256), 0, S(stream), t);
     return launched("k_reduce_rows");
 }
 

@@ -100,7 +100,7 @@ EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
                     "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update",
-                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id"]
+                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_reduce_rows_norm"]
 
 
 def load() -> C.CDLL:
@@ -123,6 +123,7 @@ def load() -> C.CDLL:
     L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32, V, V]
     L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V, V, I32, I32, V]
     L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
+    L.ppo_reduce_rows_norm.argtypes = [C.POINTER(PpoReduceJob), I32, V, V, I32, V, I32, V, I32, C.POINTER(I32), V]
     L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
     L.ppo_counter_add.argtypes = [V, I64, V]
     L.ppo_mlp_forward.argtypes = [C.POINTER(PpoMlpFwd), V]
@@ -237,6 +238,13 @@ class FusedPPOUpdate:
         self.loss_partials = torch.empty(L.ppo_loss_blocks(B), 2 * self.A + 1 + PPO_LOSS_NSTAT, device=dev)
         self.stat_partials = torch.empty(L.ppo_obs_stats_blocks(B) * 2 * 64, device=dev, dtype=torch.float64)
         self.norm_partials = torch.empty(2 * L.ppo_sqnorm_blocks(), device=dev)  # norm sums | non-finite counts
+        # the gradient norm's partials left by the reduce launch itself (no all-reduce between the two graphs:
+        # one gradient pass, k_sqnorm, fewer per minibatch); `fuse_norm` False keeps the separate pass
+        self.fuse_norm = bool(getattr(agent, "config", {}).get("fuse_norm", True)) and not (
+            getattr(agent, "multi_gpu", False) and getattr(agent, "multi_gpu_mode", "") == "allreduce"
+            and getattr(agent, "world_size", 1) > 1)
+        self.red_norm = torch.empty(2 * 4096, device=dev)
+        self._red_nblk = C.c_int32(0)
         self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stat_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stats = torch.zeros(agent.mini_epochs_num * self.n_mb + 1, PPO_LOSS_NSTAT, device=dev)
@@ -359,6 +367,16 @@ class FusedPPOUpdate:
         if self.ds is None or key != self._ds_key:
             self.graphs.clear()
         self.ds, self._ds_key = ds, key
+
+    def _reduce(self, jobs, s) -> None:
+        arr = (PpoReduceJob * len(jobs))(*jobs)
+        if not self.fuse_norm:
+            _check(self.L.ppo_reduce_rows(arr, len(jobs), s), "ppo_reduce_rows")
+            return
+        _check(self.L.ppo_reduce_rows_norm(arr, len(jobs), _p(self.scaler), _p(self.gbh), self.gbh.numel(),
+                                           _p(self.gls), self.gls.numel(), _p(self.red_norm),
+                                           self.red_norm.numel() // 2, C.byref(self._red_nblk), s),
+               "ppo_reduce_rows_norm")
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.dev).cuda_stream
@@ -541,8 +559,7 @@ class FusedPPOUpdate:
                 dhi = self.dh[:, :kin]
                 torch.mm(dz, self.W_lp[i], out=dhi)
                 dh, dh_t = dhi, dt_code
-        arr = (PpoReduceJob * len(jobs))(*jobs)
-        _check(L.ppo_reduce_rows(arr, len(jobs), s), "ppo_reduce_rows")
+        self._reduce(jobs, s)
         del keep
 
     def _backward_mfma(self) -> None:
@@ -572,23 +589,28 @@ class FusedPPOUpdate:
             ones = 64 if i == 0 else 256
             jobs.append(PpoReduceJob(gw.data_ptr(), self.gW[i].data_ptr(), S, 256, w, m.in_features, m.in_features, n_s))
             jobs.append(PpoReduceJob(gw.data_ptr() + 4 * ones, self.gb[i].data_ptr(), S, 256, w, 1, 1, n_s))
-        arr = (PpoReduceJob * len(jobs))(*jobs)
-        _check(L.ppo_reduce_rows(arr, len(jobs), s), "ppo_reduce_rows")
+        self._reduce(jobs, s)
 
     @torch.no_grad()
     def _optimizer_step(self) -> None:
         L, s, ag, fl = self.L, self._stream(), self.agent, self.flat
         n = fl.numel
-        _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.scaler), _p(self.norm_partials), s), "ppo_sqnorm")
+        if self.fuse_norm:  # the reduce launch of graph A left the norm partials
+            npart, nnp = self.red_norm, self._red_nblk.value
+            if nnp <= 0:
+                raise NativeError("fused gradient norm: step_b before step_a")
+        else:
+            _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.scaler), _p(self.norm_partials), s), "ppo_sqnorm")
+            npart, nnp = self.norm_partials, self.norm_partials.numel() // 2
         opt = ag.optimizer
         _check(L.ppo_adam(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
-                          _p(self.norm_partials), self.norm_partials.numel() // 2,
+                          _p(npart), nnp,
                           ag.grad_norm if ag.truncate_grads else 0.0, _p(ag.lr), _p(opt.step_t), opt.beta1, opt.beta2,
                           opt.eps, self.segs, self.nseg, _p(self.mirror), self.dt_code if self.lp else 1,
                           _p(self.scaler), s), "ppo_adam")
         _check(L.ppo_tail(_p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr, self.max_lr,
                           _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), _p(self.scaler),
-                          _p(self.norm_partials), self.norm_partials.numel() // 2, SCALER_GROWTH_INTERVAL, s), "ppo_tail")
+                          _p(npart), nnp, SCALER_GROWTH_INTERVAL, s), "ppo_tail")
 
     # ------------------------------------------------------------------ graphs
     def _run(self, key, fn) -> None:

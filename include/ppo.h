@@ -121,6 +121,14 @@ typedef struct {
 } ppo_reduce_job_t;
 #define PPO_MAX_JOBS 16
 int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stream);
+/* ppo_reduce_rows + ppo_sqnorm's work over the values it writes (round 5, one gradient pass fewer when no
+ * all-reduce sits between the two): norm_partials receives [nblk sums of (v / scale)^2 | nblk non-finite
+ * counts] (scaler: as ppo_sqnorm) over every dst element written plus the extra arrays (the gradients
+ * other kernels wrote: head biases, log-sigma); *nblk_out = nblk (<= max_blocks) is the count to pass to
+ * ppo_adam / ppo_tail as nblk_norm. */
+int ppo_reduce_rows_norm(const ppo_reduce_job_t* jobs_host, int32_t njobs, const float* scaler, const float* extra0,
+                         int32_t extra0_n, const float* extra1, int32_t extra1_n, float* norm_partials,
+                         int32_t max_blocks, int32_t* nblk_out, void* stream);
 
 /* Rollout policy head (graph-safe sampling): head = [mu | value] (rows x (A+1), fp32), logstd (A).
  * actions = mu + exp(logstd) * N(0, 1) with the normals from Philox4x32-10 keyed by `seed` and

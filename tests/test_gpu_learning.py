@@ -141,6 +141,7 @@ def _grads(agent):
 @pytest.mark.parametrize("graphs", [False, True])
 def test_fused_minibatch_step_matches_autograd_fp32(tmp_path, graphs):
     ref, fus = _agents_and_batch(256, mixed=False, tmp=tmp_path)
+    fus.fused.fuse_norm = False  # this test writes the gradients between step_a and step_b
     fus.fused.use_graphs = graphs
     ref.truncate_grads = False  # compare raw gradients (the fused clip happens inside the Adam kernel)
     saved = ref.optimizer.step
@@ -229,6 +230,7 @@ def test_fused_loss_scaler_skips_and_grows(tmp_path):
     from allsteps_isaaclab_amd.learning.fused import SCALER_GROWTH_INTERVAL
 
     _, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path)
+    fus.fused.fuse_norm = False  # this test writes the gradients between step_a and step_b
     fus.fused.use_graphs = False
     fus.fused.begin_epoch()
     fus.fused.step_a(True)
@@ -273,6 +275,7 @@ def test_fused_loss_scaler_clips_finite_overflowing_norm(tmp_path):
     squared sum overflows fp32 (||g|| * scale > 1.8e19) are unscaled, clipped and applied like
     torch's GradScaler + clip_grad_norm_ would, and the scale keeps growing (no skip)."""
     _, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path)
+    fus.fused.fuse_norm = False  # this test writes the gradients between step_a and step_b
     fus.fused.use_graphs = False
     fus.fused.begin_epoch()
     fus.fused.step_a(True)
@@ -312,6 +315,7 @@ def test_fused_unscaled_nan_gradient_poisons_the_step_like_torch(tmp_path):
     clip coefficient, so torch turns every parameter NaN; the fused path does the same instead of
     clipping the finite elements to zero."""
     _, fus = _agents_and_batch(256, mixed=False, tmp=tmp_path)
+    fus.fused.fuse_norm = False  # this test writes the gradients between step_a and step_b
     if not fus.truncate_grads:
         pytest.skip("agent config without grad clipping")
     fus.fused.use_graphs = False
@@ -322,6 +326,28 @@ def test_fused_unscaled_nan_gradient_poisons_the_step_like_torch(tmp_path):
     fus.fused.step_b()
     torch.cuda.synchronize()
     assert torch.isnan(fus.flat.params).all()
+
+
+@pytest.mark.gpu
+def test_fused_gradient_norm_from_the_reduce_launch(tmp_path):
+    """One GPU, no all-reduce: the reduce launch leaves the gradient-norm partials (ppo_reduce_rows_norm)
+    and step B skips the separate norm pass.  Against the separate pass on the same minibatch: the same
+    gradients bit for bit, the norm's partial count is the reduce's block count + 1, and the clipped Adam
+    step agrees to fp32 rounding (the squares summed in another fixed order)."""
+    outs = []
+    for fuse in (False, True):
+        _, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path / str(fuse))
+        fus.fused.fuse_norm = fuse
+        fus.fused.begin_epoch()
+        fus.fused.step_a(True)
+        g = fus.flat.grads.clone()
+        fus.fused.step_b()
+        torch.cuda.synchronize()
+        outs.append((g, fus.flat.params.clone(), fus.scaler_state.clone(), fus.fused._red_nblk.value))
+    (ga, pa, sa, _), (gb, pb, sb, nb) = outs
+    assert torch.equal(ga, gb) and torch.equal(sa, sb)
+    assert nb > 1
+    torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-7)
 
 
 @pytest.mark.gpu
