@@ -643,20 +643,13 @@ __device__ void tail_store(const ppo_tail_args_t& t, const TailVals& v, bool ski
     *t.stat_idx = v.st + 1;
 }
 
-// TAIL (ppo_adam_tail): the minibatch's tail runs in this launch.  Its writes (lr, step, scaler, the
-// counters) must follow every block's prologue reads of lr / step / scaler, and nothing else orders them:
-// thread 0 of each block adds 1 to a relaxed agent-scope counter right after its prologue -- whose loads
-// have been consumed by then -- and the block whose add returns the last count runs the tail and resets
-// the counter, while every block streams its elements.  No data passes between blocks, so no fences.
-template <bool TAIL>
 __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, const float* __restrict__ g,
                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                        const float* __restrict__ np, int nnp, float max_norm,
                                                        const double* __restrict__ lr_p, const double* __restrict__ step_p,
                                                        float b1, float b2, float eps, SegTable segs,
                                                        uint16_t* __restrict__ mirror, int mirror_dtype,
-                                                       const float* __restrict__ scaler, ppo_tail_args_t tail,
-                                                       int32_t* __restrict__ counter) {
+                                                       const float* __restrict__ scaler) {
     __shared__ float red[2][kAdamThreads / kWave];
     __shared__ float coef_s, step_size_s, bc2_sqrt_s, inv_scale_s;
     __shared__ int skip_s;
@@ -690,10 +683,6 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
         const double ts = *step_p + 1.0;
         step_size_s = float(*lr_p / (1.0 - pow(double(b1), ts)));
         bc2_sqrt_s = float(sqrt(1.0 - pow(double(b2), ts)));
-        if (TAIL && __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == int(gridDim.x) - 1) {
-            tail_store(tail, tail_load(tail), skip_s);
-            __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
     __syncthreads();
     const float coef = coef_s;
@@ -991,9 +980,9 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
              void* stream) {
     SegTable t;
     if (const int rc = seg_table(segs_host, nseg, mirror, mirror_dtype, t)) return rc;
-    hipLaunchKernelGGL(k_adam<false>, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0,
+    hipLaunchKernelGGL(k_adam, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0,
                        S(stream), p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
-                       static_cast<uint16_t*>(mirror), mirror_dtype, scaler, ppo_tail_args_t{}, nullptr);
+                       static_cast<uint16_t*>(mirror), mirror_dtype, scaler);
     return launched("k_adam");
 }
 
@@ -1003,23 +992,6 @@ static int check_tail(const ppo_tail_args_t& t, const float* sqnorm_partials) {
     if (t.n_minibatches <= 0) return fail(-1, "ppo_tail: n_minibatches must be positive");
     if (t.scaler && (!sqnorm_partials || t.growth_interval <= 0)) return fail(-1, "ppo_tail: the scaler needs the norm partials");
     return 0;
-}
-
-int ppo_adam_tail(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials,
-                  int32_t nblk_norm, float max_norm, double* lr, double* step, float beta1, float beta2, float eps,
-                  const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, float* scaler,
-                  const float* kl, float kl_threshold, double min_lr, double max_lr, int32_t* mb_idx,
-                  int32_t n_minibatches, int32_t* stat_idx, int32_t growth_interval, int32_t* counter, void* stream) {
-    const ppo_tail_args_t ta{lr, kl, kl_threshold, min_lr, max_lr, step, mb_idx, n_minibatches, stat_idx, scaler,
-                             growth_interval};
-    if (const int rc = check_tail(ta, sqnorm_partials)) return rc;
-    if (!counter) return fail(-1, "ppo_adam_tail: counter required");
-    SegTable t;
-    if (const int rc = seg_table(segs_host, nseg, mirror, mirror_dtype, t)) return rc;
-    hipLaunchKernelGGL(k_adam<true>, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0,
-                       S(stream), p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
-                       static_cast<uint16_t*>(mirror), mirror_dtype, scaler, ta, counter);
-    return launched("k_adam");
 }
 
 int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,

@@ -100,8 +100,7 @@ EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
                     "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update",
-                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_reduce_rows_norm",
-                    "ppo_adam_tail"]
+                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_reduce_rows_norm"]
 
 
 def load() -> C.CDLL:
@@ -123,8 +122,6 @@ def load() -> C.CDLL:
     L.ppo_sqnorm.argtypes = [V, I64, V, V, V]
     L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32, V, V]
     L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V, V, I32, I32, V]
-    L.ppo_adam_tail.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32, V,
-                                V, F32, F64, F64, V, I32, V, I32, V, V]
     L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
     L.ppo_reduce_rows_norm.argtypes = [C.POINTER(PpoReduceJob), I32, V, V, I32, V, I32, V, I32, C.POINTER(I32), V]
     L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
@@ -247,7 +244,6 @@ class FusedPPOUpdate:
             getattr(agent, "multi_gpu", False) and getattr(agent, "multi_gpu_mode", "") == "allreduce"
             and getattr(agent, "world_size", 1) > 1)
         self.red_norm = torch.empty(2 * 4096, device=dev)
-        self.tail_counter = torch.zeros(1, device=dev, dtype=torch.int32)  # ppo_adam_tail's block count
         self._red_nblk = C.c_int32(0)
         self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stat_idx = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -607,14 +603,14 @@ class FusedPPOUpdate:
             _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.scaler), _p(self.norm_partials), s), "ppo_sqnorm")
             npart, nnp = self.norm_partials, self.norm_partials.numel() // 2
         opt = ag.optimizer
-        # clip + Adam, and in the same launch the tail (GradScaler.update, adaptive LR, Adam's step count,
-        # the device minibatch / statistics counters)
-        _check(L.ppo_adam_tail(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n, _p(npart), nnp,
-                               ag.grad_norm if ag.truncate_grads else 0.0, _p(ag.lr), _p(opt.step_t), opt.beta1,
-                               opt.beta2, opt.eps, self.segs, self.nseg, _p(self.mirror), self.dt_code if self.lp else 1,
-                               _p(self.scaler), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr,
-                               self.max_lr, _p(self.mb_idx), self.n_mb, _p(self.stat_idx), SCALER_GROWTH_INTERVAL,
-                               _p(self.tail_counter), s), "ppo_adam_tail")
+        _check(L.ppo_adam(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
+                          _p(npart), nnp,
+                          ag.grad_norm if ag.truncate_grads else 0.0, _p(ag.lr), _p(opt.step_t), opt.beta1, opt.beta2,
+                          opt.eps, self.segs, self.nseg, _p(self.mirror), self.dt_code if self.lp else 1,
+                          _p(self.scaler), s), "ppo_adam")
+        _check(L.ppo_tail(_p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr, self.max_lr,
+                          _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), _p(self.scaler),
+                          _p(npart), nnp, SCALER_GROWTH_INTERVAL, s), "ppo_tail")
 
     # ------------------------------------------------------------------ graphs
     def _run(self, key, fn) -> None:

@@ -292,14 +292,6 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
 int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,
              int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, float* scaler, const float* sqnorm_partials,
              int32_t nblk_norm, int32_t growth_interval, void* stream);
-/* ppo_adam then ppo_tail in ONE launch (round 5): the tail runs in the workgroup that is the last to pass
- * its prologue reads of lr / step / scaler (counted on `counter`, a device int32 that starts at 0 and
- * that the call leaves at 0), overlapped with the streaming update.  Same results as the two calls. */
-int ppo_adam_tail(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials,
-                  int32_t nblk_norm, float max_norm, double* lr, double* step, float beta1, float beta2, float eps,
-                  const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, float* scaler,
-                  const float* kl, float kl_threshold, double min_lr, double max_lr, int32_t* mb_idx,
-                  int32_t n_minibatches, int32_t* stat_idx, int32_t growth_interval, int32_t* counter, void* stream);
 
 
 #ifdef __cplusplus

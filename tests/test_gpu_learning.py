@@ -736,63 +736,6 @@ def test_weight_grads_side_job_equals_loss_finalize():
         assert torch.equal(x, y)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("bad", [False, True])
-def test_adam_tail_launch_equals_adam_then_tail(bad):
-    """ppo_adam_tail (the tail run by the last block past its prologue) == ppo_adam then ppo_tail, bit for
-    bit: parameters, moments, the fp16 mirror (a row-major and a transposed segment), lr / step / scaler /
-    counters; the block counter is back at 0 (a graph replays it).  bad: a non-finite gradient (the scaler
-    skips the step and backs off)."""
-    from allsteps_isaaclab_amd.learning import fused as FU
-
-    L = FU.load()
-    dev = "cuda:0"
-    g = torch.Generator(device=dev).manual_seed(9)
-    n = 333_333
-    s = torch.cuda.current_stream().cuda_stream
-    grads = torch.randn(n, device=dev, generator=g) * 100.0
-    if bad:
-        grads[n // 3] = float("inf")
-    nb = L.ppo_sqnorm_blocks()
-    partials = torch.empty(2 * nb, device=dev)
-    segs = (FU.PpoSeg * 2)(FU.PpoSeg(1000, 256 * 64, 0, 64, 72, 0), FU.PpoSeg(70000, 256 * 256, 256 * 72, 256, 256, 1))
-    FU._check(L.ppo_sqnorm(grads.data_ptr(), n, None, partials.data_ptr(), s), "sqnorm")
-    outs = []
-    for fused in (False, True):
-        p = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
-        m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
-        mirror = torch.zeros(256 * 72 + 256 * 256, device=dev, dtype=torch.float16)
-        lr = torch.tensor([3e-4], device=dev, dtype=torch.float64)
-        step = torch.tensor([7.0], device=dev, dtype=torch.float64)
-        scaler = torch.tensor([65536.0, 1999.0], device=dev)
-        kl = torch.tensor([0.03], device=dev)
-        mb, st, ctr = (torch.zeros(1, device=dev, dtype=torch.int32) for _ in range(3))
-        FU._check(L.ppo_sqnorm(grads.data_ptr(), n, scaler.data_ptr(), partials.data_ptr(), s), "sqnorm")
-        if fused:
-            FU._check(L.ppo_adam_tail(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, partials.data_ptr(),
-                                      nb, 1.0, lr.data_ptr(), step.data_ptr(), 0.9, 0.999, 1e-8, segs, 2,
-                                      mirror.data_ptr(), FU.PPO_DT[torch.float16], scaler.data_ptr(), kl.data_ptr(),
-                                      0.008, 1e-6, 1e-2, mb.data_ptr(), 4, st.data_ptr(), 2000, ctr.data_ptr(), s),
-                      "ppo_adam_tail")
-        else:
-            FU._check(L.ppo_adam(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, partials.data_ptr(), nb,
-                                 1.0, lr.data_ptr(), step.data_ptr(), 0.9, 0.999, 1e-8, segs, 2, mirror.data_ptr(),
-                                 FU.PPO_DT[torch.float16], scaler.data_ptr(), s), "ppo_adam")
-            FU._check(L.ppo_tail(lr.data_ptr(), kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4,
-                                 st.data_ptr(), scaler.data_ptr(), partials.data_ptr(), nb, 2000, s), "ppo_tail")
-        torch.cuda.synchronize()
-        outs.append([p, m, v, mirror, lr, step, scaler, mb, st, ctr])
-    for a, b in zip(*outs):
-        assert torch.equal(a, b), (a, b)
-    _, _, _, _, lr, step, scaler, mb, st, ctr = outs[1]
-    assert int(ctr) == 0 and int(mb) == 1 and int(st) == 1
-    if bad:  # skipped: step count kept, scale halved, lr still adapted from the KL
-        assert float(step) == 7.0 and float(scaler[0]) == 32768.0
-    else:    # applied: step + 1, the growth interval reached -> scale doubled
-        assert float(step) == 8.0 and float(scaler[0]) == 131072.0
-    assert float(lr) == pytest.approx(3e-4 / 1.5)  # kl 0.03 > 2 x 0.008
-
-
 def test_weight_grads_rejects_bad_arguments():
     import ctypes as C
 
