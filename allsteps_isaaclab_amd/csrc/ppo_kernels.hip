@@ -466,23 +466,42 @@ struct JobTable {
     int32_t extra_n[2];
 };
 
+// The splits of one output are summed by TWO threads -- the block's threads t and t + 128 take the
+// first and the second half of q -- and combined through LDS, (first half) + (second half), a fixed order:
+// twice the loads in flight per CU of the one-thread form, which left the chip at ~1.3 waves per SIMD
+// and latency-bound (2 TB/s).
+constexpr int kRedOut = 128;  // outputs (or float4 columns) per block
+
 template <int V>
-__device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int o, float inv_scale, float& sq, float& bad) {
+__device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int o, bool active, float inv_scale, float& sq,
+                                            float& bad) {
     typedef float fv __attribute__((ext_vector_type(V)));
+    __shared__ float hi_s[kRedOut * 4];
+    const int half = threadIdx.x / kRedOut;
     const int cols = jb.dst_cols / V;
     const int r = o / cols, c = (o - r * cols) * V;
     const float* src = jb.src + int64_t(r) * jb.src_cols + c;
+    const int q0 = half ? (jb.S + 1) / 2 : 0, q1 = half ? jb.S : (jb.S + 1) / 2;
     fv s = {};
-    // up to 32 loads in flight per chunk (every split of the trainer's jobs at once), the chunk predicated,
-    // added in q order (fixed summation order)
-    for (int q = 0; q < jb.S; q += 32) {
-        fv v[32];
+    if (active) {
+        // up to 16 loads in flight per chunk, the chunk predicated, added in q order
+        for (int q = q0; q < q1; q += 16) {
+            fv v[16];
 #pragma unroll
-        for (int u = 0; u < 32; ++u) v[u] = q + u < jb.S ? *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n) : fv{};
+            for (int u = 0; u < 16; ++u) v[u] = q + u < q1 ? *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n) : fv{};
 #pragma unroll
-        for (int u = 0; u < 32; ++u)
-            if (q + u < jb.S) s += v[u];
+            for (int u = 0; u < 16; ++u)
+                if (q + u < q1) s += v[u];
+        }
     }
+    if (half) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) hi_s[(threadIdx.x - kRedOut) * V + e] = s[e];
+    }
+    __syncthreads();
+    if (half || !active) return;
+#pragma unroll
+    for (int e = 0; e < V; ++e) s[e] += hi_s[threadIdx.x * V + e];
     *reinterpret_cast<fv*>(jb.dst + int64_t(r) * jb.dst_stride + c) = s;
 #pragma unroll
     for (int e = 0; e < V; ++e) {
@@ -492,12 +511,12 @@ __device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int o, f
     }
 }
 
-// dst[r][c] = sum_q src[q][r][c] in q order; one thread per output element, or per 4 consecutive
-// elements when the job's strides and pointers allow 16-B accesses (the same per-element sums).  Each
-// block belongs to one job, found by a block-uniform (scalar) search: a per-thread search over the job
-// table was a chain of dependent vector loads ahead of every thread's first partial load.  With t.norm the
-// blocks also leave k_sqnorm's partials of what they wrote (one gradient pass fewer; a last block covers
-// the extra arrays -- the gradients other kernels wrote)
+// dst[r][c] = sum_q src[q][r][c]; one output element per thread pair, or 4 consecutive elements when the
+// job's strides and pointers allow 16-B accesses (the same per-element sums).  Each block belongs to one
+// job, found by a block-uniform (scalar) search: a per-thread search over the job table was a chain of
+// dependent vector loads ahead of every thread's first partial load.  With t.norm the blocks also leave
+// k_sqnorm's partials of what they wrote (one gradient pass fewer; a last block covers the extra arrays --
+// the gradients other kernels wrote)
 __global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
     const int b = blockIdx.x;
     const int nb = t.blk_start[t.n];
@@ -506,13 +525,12 @@ __global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
     if (b < nb) {
         int k = 0;
         while (b >= t.blk_start[k + 1]) ++k;
-        const int o = (b - t.blk_start[k]) * 256 + threadIdx.x;
-        if (o < t.count[k]) {
-            if (t.vec[k] == 4)
-                reduce_cols<4>(t.j[k], o, inv_scale, sq, bad);
-            else
-                reduce_cols<1>(t.j[k], o, inv_scale, sq, bad);
-        }
+        const int o = (b - t.blk_start[k]) * kRedOut + threadIdx.x % kRedOut;
+        const bool active = o < t.count[k];
+        if (t.vec[k] == 4)
+            reduce_cols<4>(t.j[k], o, active, inv_scale, sq, bad);
+        else
+            reduce_cols<1>(t.j[k], o, active, inv_scale, sq, bad);
     } else {
         for (int a = 0; a < 2; ++a)
             for (int i = threadIdx.x; i < t.extra_n[a]; i += 256) {
@@ -877,7 +895,7 @@ static int reduce_table(const ppo_reduce_job_t* jobs_host, int32_t njobs, JobTab
         const int64_t cnt = int64_t(j.out_rows) * j.dst_cols / t.vec[k];
         if (cnt > (int64_t(1) << 30)) return fail(-1, "ppo_reduce_rows: job too large");
         t.count[k] = int32_t(cnt);
-        t.blk_start[k + 1] = t.blk_start[k] + int32_t((cnt + 255) / 256);
+        t.blk_start[k + 1] = t.blk_start[k] + int32_t((cnt + kRedOut - 1) / kRedOut);
     }
     for (int k = njobs; k < PPO_MAX_JOBS; ++k) t.blk_start[k + 1] = t.blk_start[njobs];
     return 0;
