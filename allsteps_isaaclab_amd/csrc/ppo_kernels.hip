@@ -466,42 +466,46 @@ struct JobTable {
     int32_t extra_n[2];
 };
 
-// The splits of one output are summed by TWO threads -- the block's threads t and t + 128 take the
-// first and the second half of q -- and combined through LDS, (first half) + (second half), a fixed order:
-// twice the loads in flight per CU of the one-thread form, which left the chip at ~1.3 waves per SIMD
-// and latency-bound (2 TB/s).
-constexpr int kRedOut = 128;  // outputs (or float4 columns) per block
+// The splits of one output are summed by kRedT threads -- the block's threads t + kRedOut * i take the
+// i-th part of q -- and combined through LDS in part order, a fixed order: more loads in flight per CU than
+// one thread per output, which left the chip at ~1.3 waves per SIMD and latency-bound (2 TB/s; two threads
+// per output measured 13.8 -> 10.3 us in the trainer).
+constexpr int kRedT = 4;                  // threads per output
+constexpr int kRedOut = 256 / kRedT;      // outputs (or float4 columns) per block
 
 template <int V>
 __device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int o, bool active, float inv_scale, float& sq,
                                             float& bad) {
     typedef float fv __attribute__((ext_vector_type(V)));
-    __shared__ float hi_s[kRedOut * 4];
-    const int half = threadIdx.x / kRedOut;
+    __shared__ float part_s[kRedT - 1][kRedOut * 4];
+    const int part = threadIdx.x / kRedOut, lo = threadIdx.x % kRedOut;
     const int cols = jb.dst_cols / V;
     const int r = o / cols, c = (o - r * cols) * V;
     const float* src = jb.src + int64_t(r) * jb.src_cols + c;
-    const int q0 = half ? (jb.S + 1) / 2 : 0, q1 = half ? jb.S : (jb.S + 1) / 2;
+    const int per = (jb.S + kRedT - 1) / kRedT;
+    const int q0 = min(jb.S, part * per), q1 = min(jb.S, q0 + per);
     fv s = {};
     if (active) {
-        // up to 16 loads in flight per chunk, the chunk predicated, added in q order
-        for (int q = q0; q < q1; q += 16) {
-            fv v[16];
+        // up to 8 loads in flight per chunk, the chunk predicated, added in q order
+        for (int q = q0; q < q1; q += 8) {
+            fv v[8];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = q + u < q1 ? *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n) : fv{};
+            for (int u = 0; u < 8; ++u) v[u] = q + u < q1 ? *reinterpret_cast<const fv*>(src + int64_t(q + u) * jb.src_n) : fv{};
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
+            for (int u = 0; u < 8; ++u)
                 if (q + u < q1) s += v[u];
         }
     }
-    if (half) {
+    if (part) {
 #pragma unroll
-        for (int e = 0; e < V; ++e) hi_s[(threadIdx.x - kRedOut) * V + e] = s[e];
+        for (int e = 0; e < V; ++e) part_s[part - 1][lo * V + e] = s[e];
     }
     __syncthreads();
-    if (half || !active) return;
+    if (part || !active) return;
 #pragma unroll
-    for (int e = 0; e < V; ++e) s[e] += hi_s[threadIdx.x * V + e];
+    for (int i = 0; i < kRedT - 1; ++i)
+#pragma unroll
+        for (int e = 0; e < V; ++e) s[e] += part_s[i][lo * V + e];
     *reinterpret_cast<fv*>(jb.dst + int64_t(r) * jb.dst_stride + c) = s;
 #pragma unroll
     for (int e = 0; e < V; ++e) {
@@ -511,7 +515,7 @@ __device__ __forceinline__ void reduce_cols(const ppo_reduce_job_t& jb, int o, b
     }
 }
 
-// dst[r][c] = sum_q src[q][r][c]; one output element per thread pair, or 4 consecutive elements when the
+// dst[r][c] = sum_q src[q][r][c]; one output element per kRedT threads, or 4 consecutive elements when the
 // job's strides and pointers allow 16-B accesses (the same per-element sums).  Each block belongs to one
 // job, found by a block-uniform (scalar) search: a per-thread search over the job table was a chain of
 // dependent vector loads ahead of every thread's first partial load.  With t.norm the blocks also leave
