@@ -228,9 +228,12 @@ __device__ __forceinline__ void mma_rows(const uint16_t* X, const typename Lp<DT
 
 #ifndef PPO_MLP_PRIO
 // A/B knob: static s_setprio 1 for waves 4..7 of the trunk kernels (MI355X_MICROARCH.md "Two waves per
-// SIMD" item 4).  Measured with the libraries alternated over rounds (scripts/mlp_ab.py, r05l): forward
-// 55.3 / 55.7 us, backward 44.8 / 44.5 us with / without -- no effect, so off
+// SIMD" item 4).  Measured with each library in its own processes (scripts/mlp_ab.py, r05t): forward 46.7 /
+// 46.9 us, backward 43.3 / 43.7 us without / with -- no gain, so off
 #define PPO_MLP_PRIO 0
+#endif
+#ifndef PPO_FWD_SINGLE_W
+#define PPO_FWD_SINGLE_W 0
 #endif
 #ifndef PPO_FWD_DBG
 #define PPO_FWD_DBG 0  // timing-only builds (scripts/fwd_dbg.sh): 2 no exp, 4 no stores, 16 no MFMA, 32 no ELU / convert
@@ -424,18 +427,47 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
             *reinterpret_cast<uint4*>(X0 + r * kXs + 8 * q) = v;
         }
     }
+    const int hs = a.h_stride;
+    Rsrc rh[5];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) rh[l] = rsrc(STORE ? a.h[l] : nullptr, STORE ? int64_t(rows) * hs * 2 : 0);
+    f32x16 pend = {};
+    float bhv[16];
+#if PPO_FWD_SINGLE_W
+    // timing variant: ONE register set of weights, each layer's slice loaded after the previous layer's
+    // MFMAs (64 VGPRs freed for the B-fragment prefetch; the load latency exposed once per layer).
+    // Measured (r05t): 48.0 -> 55.4 us -- the compiler fills the freed registers and spills
+    V8 wa[16];
+    float ba[16];
+    load_wa<DT, kK0 / 16>(a.w[0], kK0, F0, i, h, wa);
+    load_bias(a.b[0], F0, h, ba);
+    __syncthreads();
+    layer<DT, kK0 / 16, STORE, false>(X0, X1, wa, ba, pend, rh[0], rh[0], hs, row0, F0, j, h);
+    load_wa<DT, 16>(a.w[1], kHid, F0, i, h, wa);
+    load_bias(a.b[1], F0, h, ba);
+    layer<DT, 16, STORE, true>(X1, X0, wa, ba, pend, rh[0], rh[1], hs, row0, F0, j, h);
+    load_wa<DT, 16>(a.w[2], kHid, F0, i, h, wa);
+    load_bias(a.b[2], F0, h, ba);
+    layer<DT, 16, STORE, true>(X0, X1, wa, ba, pend, rh[1], rh[2], hs, row0, F0, j, h);
+    load_wa<DT, 16>(a.w[3], kHid, F0, i, h, wa);
+    load_bias(a.b[3], F0, h, ba);
+    layer<DT, 16, STORE, true>(X1, X0, wa, ba, pend, rh[2], rh[3], hs, row0, F0, j, h);
+    load_wa<DT, 16>(a.w[4], kHid, F0, i, h, wa);
+    load_bias(a.b[4], F0, h, ba);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bhv[r] = feat(r, h) < a.nh ? a.bh[feat(r, h)] : 0.f;
+    layer<DT, 16, STORE, true>(X0, X1, wa, ba, pend, rh[3], rh[4], hs, row0, F0, j, h);
+    tile_epi<DT, STORE>(pend, X1, 96 + j, row0 + 96 + j, rh[4], hs, F0, h);
+    if (wave < 4) load_wh<DT>(a.wh, a.nh, i, h, wa);
+    V8 (&whf)[16] = wa;
+#else
     // Weight slices double-buffered in registers (wa / wb): layer l + 1's slice is requested at the start
     // of layer l, ahead of layer l's activation stores (a load waited for with vmcnt also waits for every
     // older store of the wave).  Bias vectors likewise one layer ahead.
     V8 wa[16], wb[16];
     float ba[16], bb[16];
-    f32x16 pend = {};
     load_wa<DT, kK0 / 16>(a.w[0], kK0, F0, i, h, wa);
     load_bias(a.b[0], F0, h, ba);
-    const int hs = a.h_stride;
-    Rsrc rh[5];
-#pragma unroll
-    for (int l = 0; l < 5; ++l) rh[l] = rsrc(STORE ? a.h[l] : nullptr, STORE ? int64_t(rows) * hs * 2 : 0);
     __syncthreads();
     load_wa<DT, 16>(a.w[1], kHid, F0, i, h, wb);
     load_bias(a.b[1], F0, h, bb);
@@ -451,11 +483,12 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     layer<DT, 16, STORE, true>(X1, X0, wb, bb, pend, rh[2], rh[3], hs, row0, F0, j, h);
     // the fifth layer; the heads' weights and biases fly under it
     if (wave < 4) load_wh<DT>(a.wh, a.nh, i, h, wb);
-    float bhv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) bhv[r] = feat(r, h) < a.nh ? a.bh[feat(r, h)] : 0.f;
     layer<DT, 16, STORE, true>(X0, X1, wa, ba, pend, rh[3], rh[4], hs, row0, F0, j, h);
     tile_epi<DT, STORE>(pend, X1, 96 + j, row0 + 96 + j, rh[4], hs, F0, h);
+    V8 (&whf)[16] = wb;
+#endif
     __syncthreads();
     // ---- heads: wave w < 4 takes N-tile w; out = 16-bit(acc + 16-bit(bh)) as under autocast.  With the
     // fused losses (LA > 0) the values also go to a table of the block's rows at the head of X0 (free: layer
@@ -464,7 +497,7 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     float* sh = reinterpret_cast<float*>(X0);
     if (wave < 4 && a.head) {
         f32x16 hacc[4];
-        mma_rows<DT, 16, 1>(X1, wb, hacc, wave, j, h);
+        mma_rows<DT, 16, 1>(X1, whf, hacc, wave, j, h);
         const int rl = 32 * wave + j, row = row0 + rl;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
