@@ -232,6 +232,12 @@ __device__ __forceinline__ void mma_rows(const uint16_t* X, const typename Lp<DT
 // 46.9 us, backward 43.3 / 43.7 us without / with -- no gain, so off
 #define PPO_MLP_PRIO 0
 #endif
+#ifndef PPO_MMA_PD
+#define PPO_MMA_PD 4  // B-fragment reads issued this many k-steps ahead of their MFMA (A/B knob)
+#endif
+#ifndef PPO_MMA_SCHED
+#define PPO_MMA_SCHED 1  // the sched_barriers that keep the reads and MFMAs in order (A/B knob)
+#endif
 #ifndef PPO_FWD_SINGLE_W
 #define PPO_FWD_SINGLE_W 0
 #endif
@@ -314,7 +320,7 @@ template <int DT, int NS>
 __device__ __forceinline__ f32x16 mfma_tile(const uint16_t* X, const typename Lp<DT>::v8 (&wa)[16], f32x16 c, int t,
                                             int j, int h) {
     typedef typename Lp<DT>::v8 V8;
-    constexpr int PD = NS < 4 ? NS : 4;
+    constexpr int PD = NS < PPO_MMA_PD ? NS : PPO_MMA_PD;
     constexpr int kFloat = 0x1 | 0x2 | 0x4 | 0x40 | 0x200;
     const uint16_t* xr = X + (32 * t + j) * kXs + 8 * h;
     V8 b[NS];
@@ -323,13 +329,17 @@ __device__ __forceinline__ f32x16 mfma_tile(const uint16_t* X, const typename Lp
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         if (s + PD < NS) b[s + PD] = *reinterpret_cast<const V8*>(xr + 16 * (s + PD));
+#if PPO_MMA_SCHED
         __builtin_amdgcn_sched_barrier(kFloat);
+#endif
 #if PPO_FWD_DBG & 16
         c[s & 15] += __builtin_bit_cast(float, uint32_t(b[s][0] != b[s][1]));
 #else
         c = Lp<DT>::mma(wa[s], b[s], c);
 #endif
+#if PPO_MMA_SCHED
         __builtin_amdgcn_sched_barrier(kFloat);
+#endif
     }
     return c;
 }
