@@ -675,10 +675,59 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     __shared__ float red[2][kAdamThreads / kWave];
     __shared__ float coef_s, step_size_s, bc2_sqrt_s, inv_scale_s;
     __shared__ int skip_s;
+    // one element per thread (the grid covers n; a grid-stride form with one prologue per resident block
+    // measured slower in the trainer, 9.7 -> 12.0 us: fewer waves in flight for the streaming part).  The
+    // element's four operands and thread 0's scalars are loaded before the prologue's reductions, so their
+    // memory round trip overlaps the norm partials' instead of following it
+    const int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x;
+    float g0 = 0.f, m0 = 0.f, v0 = 0.f, p0 = 0.f;
+    if (i < n) {
+        g0 = g[i];
+        m0 = m[i];
+        v0 = v[i];
+        p0 = p[i];
+    }
+    // the norm partials (k_reduce_rows leaves one pair per block, ~1.2 k at the trainer's size) in chunks
+    // of 8 loads per thread, all in flight together: the plain loop waited one round trip per iteration
+    // (the partials come from other XCDs' writes, so every round trip reaches past L2).  Added in k order,
+    // the same sums as the plain loop
+    constexpr int kU = 8;
     float s = 0.f, bad = 0.f;
-    for (int k = threadIdx.x; k < nnp; k += kAdamThreads) {
-        s += np[k];
-        bad += np[nnp + k];
+    float ps[kU], pb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {  // clamped, unpredicated loads (nnp >= 1): no branch to wait inside
+        const int k = min(int(threadIdx.x) + u * kAdamThreads, nnp - 1);
+        ps[u] = np[k];
+        pb[u] = np[nnp + k];
+    }
+    // thread 0: the bias corrections (fp64 pow / sqrt are long instruction sequences) while those loads
+    // are in flight
+    float scale0 = 1.f, step_size0 = 0.f, bc2_sqrt0 = 0.f;
+    if (threadIdx.x == 0) {
+        if (scaler) scale0 = scaler[0];
+        const double ts = *step_p + 1.0;
+        step_size0 = float(*lr_p / (1.0 - pow(double(b1), ts)));
+        bc2_sqrt0 = float(sqrt(1.0 - pow(double(b2), ts)));
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const bool in = int(threadIdx.x) + u * kAdamThreads < nnp;
+        s += in ? ps[u] : 0.f;
+        bad += in ? pb[u] : 0.f;
+    }
+    for (int k0 = threadIdx.x + kU * kAdamThreads; k0 < nnp; k0 += kU * kAdamThreads) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int k = min(k0 + u * kAdamThreads, nnp - 1);
+            ps[u] = np[k];
+            pb[u] = np[nnp + k];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const bool in = k0 + u * kAdamThreads < nnp;
+            s += in ? ps[u] : 0.f;
+            bad += in ? pb[u] : 0.f;
+        }
     }
     s = wave_sum(s);
     bad = wave_sum(bad);
@@ -695,16 +744,14 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
         }
         // GradScaler: grads carry the loss scale (a power of two); a non-finite element skips the step
         // (scaler.step's found_inf), otherwise they are unscaled exactly before the clip (unscale_)
-        inv_scale_s = scaler ? 1.f / scaler[0] : 1.f;
+        inv_scale_s = 1.f / scale0;
         skip_s = scaler && b > 0.f;
         // torch.nn.utils.clip_grad_norm_: coef = clamp(max_norm / (total_norm + 1e-6), max=1); the
         // norm is of the unscaled grads (k_sqnorm); a NaN norm makes coef NaN (clamp keeps NaN)
         const float c = max_norm / (sqrtf(t) + 1e-6f);
         coef_s = max_norm > 0.f ? (c < 1.f || c != c ? c : 1.f) : 1.f;
-        // bias corrections once per block (fp64 pow / sqrt are long instruction sequences)
-        const double ts = *step_p + 1.0;
-        step_size_s = float(*lr_p / (1.0 - pow(double(b1), ts)));
-        bc2_sqrt_s = float(sqrt(1.0 - pow(double(b2), ts)));
+        step_size_s = step_size0;
+        bc2_sqrt_s = bc2_sqrt0;
     }
     __syncthreads();
     const float coef = coef_s;
@@ -712,23 +759,22 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     const float bc2_sqrt = bc2_sqrt_s;
     const float inv_scale = inv_scale_s;
     const bool skip = skip_s;
-    // one element per thread (a grid-stride form with one prologue per resident block measured slower in
-    // the trainer, 9.7 -> 12.0 us: fewer waves in flight for the streaming part)
-    for (int64_t i = int64_t(blockIdx.x) * kAdamThreads + threadIdx.x; !skip && i < n; i += int64_t(gridDim.x) * kAdamThreads) {
-        const float gi = (g[i] * inv_scale) * coef;
-        const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
-        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    if (!skip && i < n) {
+        const float gi = (g0 * inv_scale) * coef;
+        const float mi = m0 + (1.f - b1) * (gi - m0);  // exp_avg.lerp_(grad, 1 - beta1)
+        const float vi = v0 * b2 + (1.f - b2) * gi * gi;
         m[i] = mi;
         v[i] = vi;
         const float denom = sqrtf(vi) / bc2_sqrt + eps;
-        const float pi = p[i] - step_size * (mi / denom);
+        const float pi = p0 - step_size * (mi / denom);
         p[i] = pi;
         if (mirror) {
             for (int k = 0; k < segs.n; ++k) {
                 const ppo_seg_t& sg = segs.s[k];
                 if (i >= sg.off && i < sg.off + sg.len) {
-                    const int64_t j = i - sg.off;
-                    const int64_t r = j / sg.cols, c = j % sg.cols;
+                    // 32-bit division: seg_table holds every segment below 2^31 elements
+                    const uint32_t j = uint32_t(i - sg.off), cols = uint32_t(sg.cols);
+                    const int64_t r = j / cols, c = j % cols;
                     mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] =
                         mirror_dtype == PPO_DT_F16 ? f32_to_f16(pi) : f32_to_bf16(pi);
                 }
@@ -737,15 +783,32 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     }
 }
 
-__global__ void k_tail(ppo_tail_args_t t, const float* np, int nnp) {
-    // k_sqnorm's non-finite counts, summed by the whole wave (one thread walking the partials serially
-    // was a chain of dependent global loads: 6 us of every minibatch)
+constexpr int kTailThreads = 256;
+
+__global__ void __launch_bounds__(kTailThreads) k_tail(ppo_tail_args_t t, const float* np, int nnp) {
+    // the norm partials' non-finite counts, 8 clamped loads per thread all in flight at once, issued with
+    // thread 0's tail_load (one thread walking the partials serially was a chain of dependent global loads,
+    // 6 us of every minibatch; one wave with a plain loop still waited one round trip per 64 partials)
+    constexpr int kU = 8;
+    __shared__ float red[kTailThreads / kWave];
+    TailVals v{};
+    if (threadIdx.x == 0) v = tail_load(t);
     float b = 0.f;
-    if (t.scaler) {
-        for (int k = threadIdx.x; k < nnp; k += kWave) b += np[nnp + k];
+    if (t.scaler) {  // uniform
+        for (int k0 = threadIdx.x; k0 < nnp; k0 += kU * kTailThreads) {
+            float x[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) x[u] = np[nnp + min(k0 + u * kTailThreads, nnp - 1)];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) b += k0 + u * kTailThreads < nnp ? x[u] : 0.f;
+        }
         b = wave_sum(b);
+        if (threadIdx.x % kWave == 0) red[threadIdx.x / kWave] = b;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int w = 1; w < kTailThreads / kWave; ++w) b += red[w];
     }
-    if (threadIdx.x == 0) tail_store(t, tail_load(t), t.scaler && b > 0.f);
+    if (threadIdx.x == 0) tail_store(t, v, t.scaler && b > 0.f);
 }
 
 inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
@@ -990,7 +1053,8 @@ static int seg_table(const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int
     for (int k = 0; k < t.n; ++k) {
         t.s[k] = segs_host[k];
         const int64_t rows = t.s[k].cols > 0 ? t.s[k].len / t.s[k].cols : 0;
-        if (t.s[k].cols <= 0 || t.s[k].mstride < (t.s[k].trans ? rows : t.s[k].cols))
+        if (t.s[k].cols <= 0 || t.s[k].len < 0 || t.s[k].len > INT32_MAX ||
+            t.s[k].mstride < (t.s[k].trans ? rows : t.s[k].cols))
             return fail(-1, "ppo_adam: bad segment");
     }
     return 0;
@@ -1002,17 +1066,18 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
              void* stream) {
     SegTable t;
     if (const int rc = seg_table(segs_host, nseg, mirror, mirror_dtype, t)) return rc;
+    if (nblk_norm < 1) return fail(-1, "ppo_adam: need nblk_norm >= 1");
     hipLaunchKernelGGL(k_adam, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0,
                        S(stream), p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
                        static_cast<uint16_t*>(mirror), mirror_dtype, scaler);
     return launched("k_adam");
 }
 
-static int check_tail(const ppo_tail_args_t& t, const float* sqnorm_partials) {
+static int check_tail(const ppo_tail_args_t& t, const float* sqnorm_partials, int32_t nblk_norm) {
     if (!t.lr || !t.step || !t.mb_idx || !t.stat_idx || (t.kl_threshold > 0.f && !t.kl))
         return fail(-1, "ppo_tail: null pointer");
     if (t.n_minibatches <= 0) return fail(-1, "ppo_tail: n_minibatches must be positive");
-    if (t.scaler && (!sqnorm_partials || t.growth_interval <= 0)) return fail(-1, "ppo_tail: the scaler needs the norm partials");
+    if (t.scaler && (!sqnorm_partials || nblk_norm < 1 || t.growth_interval <= 0)) return fail(-1, "ppo_tail: the scaler needs the norm partials");
     return 0;
 }
 
@@ -1021,8 +1086,8 @@ int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, dou
              int32_t nblk_norm, int32_t growth_interval, void* stream) {
     const ppo_tail_args_t t{lr, kl, kl_threshold, min_lr, max_lr, step, mb_idx, n_minibatches, stat_idx, scaler,
                             growth_interval};
-    if (const int rc = check_tail(t, sqnorm_partials)) return rc;
-    hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, S(stream), t, sqnorm_partials, nblk_norm);
+    if (const int rc = check_tail(t, sqnorm_partials, nblk_norm)) return rc;
+    hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTailThreads), 0, S(stream), t, sqnorm_partials, nblk_norm);
     return launched("k_tail");
 }
 

@@ -712,12 +712,16 @@ class A2CAgent:
         f = self.fused
         f.begin_epoch()
         n_mb = len(self.dataset)
+        exchange = self.multi_gpu and self.multi_gpu_mode == "allreduce" and self.world_size > 1
         for ep in range(self.mini_epochs_num):
             rms_train = self.normalize_input and ep == 0
-            for _ in range(n_mb):
-                f.step_a(rms_train)
-                self._exchange_grads()
-                f.step_b()
+            if not exchange:  # nothing between A and B: the whole mini-epoch is one graph
+                f.run_minibatches(n_mb, rms_train)
+            else:
+                for _ in range(n_mb):
+                    f.step_a(rms_train)
+                    self._exchange_grads()
+                    f.step_b()
             if self.schedule_type == "standard":
                 s0 = ep * n_mb
                 self.scheduler.update_(self.lr, f.stats[s0:s0 + n_mb, 4].mean())

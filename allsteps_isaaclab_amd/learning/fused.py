@@ -23,6 +23,8 @@ the same maths is an explicit forward / backward:
   graph B = clip + Adam + LR; in multi-GPU ``allreduce`` mode the RCCL all-reduce of the bucket runs
   between them.  Minibatch rows are addressed through a device counter, so one graph serves every
   minibatch; two variants of A exist (obs normaliser updating: first mini-epoch; frozen: the rest).
+  With nothing between A and B (one GPU, or the rollout all-gather mode) a whole mini-epoch's A, B,
+  A, B, ... is captured as ONE graph (``run_minibatches``), one launch per mini-epoch.
 
 ``compute_dtype=torch.float32`` runs the same schedule in fp32 (tests compare it with autograd).
 """
@@ -643,3 +645,19 @@ class FusedPPOUpdate:
             self._run(("b",), self._optimizer_step)
         else:
             self._optimizer_step()
+
+    def run_minibatches(self, n: int, rms_train: bool) -> None:
+        """n consecutive minibatch steps (graph A's then graph B's work, n times) as ONE graph, for a
+        mini-epoch with nothing between A and B (no bucket all-reduce): the rows, the statistics slot and
+        the LR are device counters, so the same n-step sequence serves every mini-epoch.  One graph launch
+        per mini-epoch instead of 2 n: each launch boundary left ~5 us of idle GPU (r05w: update_s 54.1 ms
+        against 50.5 ms of kernels)."""
+        def body() -> None:
+            for _ in range(n):
+                self._forward_backward(rms_train)
+                self._optimizer_step()
+
+        if self.use_graphs:
+            self._run(("mb", n, rms_train), body)
+        else:
+            body()

@@ -280,7 +280,8 @@ int ppo_sqnorm(const float* g, int64_t n, const float* scaler, float* partials, 
  * weight_decay 0) with device lr / step (fp64); writes the mirror (mirror_dtype PPO_DT_BF16 / PPO_DT_F16)
  * of the listed segments.  scaler (device fp32 [scale, growth tracker], NULL = none): the gradients
  * carry the loss scale -- a non-finite element skips the whole update (GradScaler.step), otherwise
- * g / scale (exact: a power of two) is what is clipped and applied (GradScaler.unscale_) */
+ * g / scale (exact: a power of two) is what is clipped and applied (GradScaler.unscale_).
+ * nblk_norm >= 1 (the partials' pair count); segments hold fewer than 2^31 elements each */
 int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* sqnorm_partials, int32_t nblk_norm,
              float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,
              const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, const float* scaler,
@@ -288,7 +289,8 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
 /* adaptive LR (rl_games AdaptiveScheduler; kl_threshold <= 0: identity) from kl (device fp32), then
  * step += 1 (Adam's count; ppo_adam used step + 1) unless the scaler skipped the step,
  * mb_idx = (mb_idx + 1) % n_minibatches, stat_idx += 1; with a scaler, GradScaler.update from the same
- * norm partials: scale *= 0.5 after a skipped step, *= 2 after growth_interval good ones in a row */
+ * norm partials (nblk_norm >= 1): scale *= 0.5 after a skipped step, *= 2 after growth_interval good ones
+ * in a row */
 int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,
              int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, float* scaler, const float* sqnorm_partials,
              int32_t nblk_norm, int32_t growth_interval, void* stream);

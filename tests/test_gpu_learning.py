@@ -370,8 +370,46 @@ def test_fused_train_epoch_runs_graph_replays(tmp_path):
     skips = round(math.log2(SCALER_INIT / float(fus.scaler_state[0])))
     assert 0 <= skips < n
     assert float(fus.optimizer.step_t) == n - skips
-    assert len(fus.fused.graphs) == 3  # A (normaliser updating), A (frozen), B
-    assert all(isinstance(g, torch.cuda.CUDAGraph) for g in fus.fused.graphs.values())
+    # one graph per mini-epoch: the normaliser-updating first mini-epoch ran once (eagerly, the warm-up
+    # of its variant), the frozen ones ran eagerly, then were captured and replayed
+    n_mb = len(fus.dataset)
+    g = fus.fused.graphs
+    assert set(g) == {("mb", n_mb, True), ("mb", n_mb, False)}
+    assert g[("mb", n_mb, True)] == "warm" and isinstance(g[("mb", n_mb, False)], torch.cuda.CUDAGraph)
+    fus._train_epoch_fused(0.0, 0.0, 0.0)
+    assert all(isinstance(v, torch.cuda.CUDAGraph) for v in g.values())
+    assert int(fus.fused.stat_idx) == n and int(fus.fused.mb_idx) == 0
+
+
+@pytest.mark.gpu
+def test_mini_epoch_graph_equals_per_minibatch_graphs(tmp_path):
+    """run_minibatches (a mini-epoch's n minibatch steps as one graph) against the step_a / step_b graph
+    pair per minibatch, over three mini-epochs (eager warm-up, capture + replay, replay): the same kernels
+    in the same order, so parameters, Adam moments and count, scaler, LR, normaliser, statistics and the
+    device counters agree bit for bit."""
+    outs = []
+    for whole in (False, True):
+        _, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path / str(whole))
+        f = fus.fused
+        n_mb = len(fus.dataset)
+        f.begin_epoch()
+        for ep in range(3):
+            if whole:
+                f.run_minibatches(n_mb, ep == 0)
+            else:
+                for _ in range(n_mb):
+                    f.step_a(ep == 0)
+                    f.step_b()
+        torch.cuda.synchronize()
+        rms = fus.model.running_mean_std
+        outs.append([t.clone() for t in (fus.flat.params, fus.optimizer.exp_avg, fus.optimizer.exp_avg_sq,
+                                         fus.optimizer.step_t, fus.scaler_state, fus.lr, f.stats, f.mb_idx,
+                                         f.stat_idx, rms.running_mean, rms.running_var, rms.count)])
+        if whole:
+            assert isinstance(f.graphs[("mb", n_mb, False)], torch.cuda.CUDAGraph)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert int(outs[1][8]) == 3 * n_mb
 
 
 @pytest.mark.gpu
