@@ -470,7 +470,7 @@ struct JobTable {
 // i-th part of q -- and combined through LDS in part order, a fixed order: more loads in flight per CU than
 // one thread per output, which left the chip at ~1.3 waves per SIMD and latency-bound (2 TB/s; two threads
 // per output measured 13.8 -> 10.3 us in the trainer).
-constexpr int kRedT = 4;                  // threads per output
+constexpr int kRedT = 4;                  // threads per output (2 / 8 measured no better in the trainer)
 constexpr int kRedOut = 256 / kRedT;      // outputs (or float4 columns) per block
 
 template <int V>
