@@ -89,14 +89,54 @@ __device__ __forceinline__ float sum8(float x) {
 }
 
 
-// NT threads (a multiple of 8) cover the block's 128 rows in 128 / (NT / 8) passes; s_red: kLossRows x
-// loss_rp(A) floats of LDS
+template <int A>
+constexpr int loss_nj() { return (A + 1 + kLossLanes - 1) / kLossLanes; }
+template <int NT>
+constexpr int loss_passes() { return kLossRows / (NT / kLossLanes); }
+
+// a lane's minibatch inputs for one pass (its row's dataset values; the head values come later)
+template <int A>
+struct LossIn {
+    float av[loss_nj<A>()], m1[loss_nj<A>()], s1[loss_nj<A>()];
+    float onlp, adv, vp, Rt;
+};
+
+// the dataset loads of every pass, issued together (no dependence on the head values: the trunk forward
+// issues them before its heads, so their round trip overlaps the heads' MFMAs and barriers)
 template <int A, int NT>
-__device__ void loss_block(const LossRowArgs& p, int blk, float* __restrict__ s_red) {
+__device__ __forceinline__ void loss_prefetch(const LossRowArgs& p, int blk, LossIn<A> (&in)[loss_passes<NT>()]) {
+    constexpr int NJ = loss_nj<A>();
+    const int tid = threadIdx.x, g = tid % kLossLanes;
+    const int64_t base = int64_t(*p.mb_idx) * p.mb_rows;
+#pragma unroll
+    for (int pass = 0; pass < loss_passes<NT>(); ++pass) {
+        const int r = blk * kLossRows + pass * (NT / kLossLanes) + tid / kLossLanes;
+        const bool ok = r < p.mb_rows;
+        const int64_t row = base + (ok ? r : 0);
+#pragma unroll
+        for (int k = 0; k < NJ; ++k) {
+            const bool act = ok && NJ * g + k < A;
+            in[pass].av[k] = act ? p.actions[row * A + NJ * g + k] : 0.f;
+            in[pass].m1[k] = act ? p.ds_mu[row * A + NJ * g + k] : 0.f;
+            in[pass].s1[k] = act ? p.ds_sigma[row * A + NJ * g + k] : 1.f;
+        }
+        in[pass].onlp = ok ? p.old_nlp[row] : 0.f;
+        in[pass].adv = ok ? p.adv[row] : 0.f;
+        in[pass].vp = ok ? p.old_v[row] : 0.f;
+        in[pass].Rt = ok ? p.ret[row] : 0.f;
+    }
+}
+
+// NT threads (a multiple of 8) cover the block's 128 rows in 128 / (NT / 8) passes; s_red: kLossRows x
+// loss_rp(A) floats of LDS; `in`: loss_prefetch's loads (this thread's own rows: ds_mu / ds_sigma are read
+// there before this thread rewrites them here)
+template <int A, int NT>
+__device__ void loss_block(const LossRowArgs& p, int blk, float* __restrict__ s_red,
+                           const LossIn<A> (&in)[loss_passes<NT>()]) {
     static_assert(A + 1 <= 32, "heads of at most 32 outputs");
     static_assert(NT % kLossLanes == 0 && kLossRows % (NT / kLossLanes) == 0, "whole passes of rows");
     constexpr int NV = 2 * A + 1 + PPO_LOSS_NSTAT, RP = loss_rp(A);
-    constexpr int NJ = (A + 1 + kLossLanes - 1) / kLossLanes;
+    constexpr int NJ = loss_nj<A>();
     const ppo_loss_cfg_t cfg = p.cfg;
     const int mb_rows = p.mb_rows;
     const int tid = threadIdx.x, g = tid % kLossLanes;
@@ -106,25 +146,26 @@ __device__ void loss_block(const LossRowArgs& p, int blk, float* __restrict__ s_
 #pragma unroll
     for (int j = 0; j < A; ++j) sum_ls += p.logstd[j];
     const float entropy = float(A) * (0.5f + 0.5f * kLog2PiL) + sum_ls;
-    for (int pass = 0; pass < kLossRows / (NT / kLossLanes); ++pass) {
+    const int64_t base = int64_t(*p.mb_idx) * mb_rows;
+#pragma unroll
+    for (int pass = 0; pass < loss_passes<NT>(); ++pass) {
     const int rl = pass * (NT / kLossLanes) + tid / kLossLanes;
     const int r = blk * kLossRows + rl;  // minibatch row
     const bool ok = r < mb_rows;
-    const int64_t row = int64_t(*p.mb_idx) * mb_rows + (ok ? r : 0);
+    const int64_t row = base + (ok ? r : 0);
     const float* hrow = p.head + int64_t(p.head_block_rows ? r : rl) * p.head_stride;
-    float hj[NJ], av[NJ], m1[NJ], s1[NJ], sg[NJ];
+    float hj[NJ], sg[NJ];
+    const float* av = in[pass].av;
+    const float* m1 = in[pass].m1;
+    const float* s1 = in[pass].s1;
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
         const int j = NJ * g + k;
-        const bool act = ok && j < A;
         hj[k] = ok && j <= A ? hrow[j] : 0.f;
-        av[k] = act ? p.actions[row * A + j] : 0.f;
-        m1[k] = act ? p.ds_mu[row * A + j] : 0.f;
-        s1[k] = act ? p.ds_sigma[row * A + j] : 1.f;
         sg[k] = j < A ? expf(p.logstd[j]) : 1.f;
     }
-    const float onlp = ok ? p.old_nlp[row] : 0.f, adv = ok ? p.adv[row] : 0.f;
-    const float vp = ok ? p.old_v[row] : 0.f, Rt = ok ? p.ret[row] : 0.f;
+    const float onlp = in[pass].onlp, adv = in[pass].adv;
+    const float vp = in[pass].vp, Rt = in[pass].Rt;
     // policy: d_j = (a_j - mu_j) / sigma_j; nlp = 0.5 sum d^2 + 0.5 log(2 pi) A + sum logstd;
     // policy_kl(p0 = current, p1 = dataset); the bound loss
     float d[NJ];
@@ -242,6 +283,13 @@ __device__ void loss_block(const LossRowArgs& p, int blk, float* __restrict__ s_
         }
         p.partials[int64_t(blk) * NV + tid] = (t[0] + t[1]) + (t[2] + t[3]);
     }
+}
+
+template <int A, int NT>
+__device__ __forceinline__ void loss_block(const LossRowArgs& p, int blk, float* __restrict__ s_red) {
+    LossIn<A> in[loss_passes<NT>()];
+    loss_prefetch<A, NT>(p, blk, in);
+    loss_block<A, NT>(p, blk, s_red, in);
 }
 
 

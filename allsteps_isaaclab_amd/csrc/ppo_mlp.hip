@@ -499,29 +499,14 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     tile_epi<DT, STORE>(pend, X1, 96 + j, row0 + 96 + j, rh[4], hs, F0, h);
     V8 (&whf)[16] = wb;
 #endif
-    __syncthreads();
-    // ---- heads: wave w < 4 takes N-tile w; out = 16-bit(acc + 16-bit(bh)) as under autocast.  With the
-    // fused losses (LA > 0) the values also go to a table of the block's rows at the head of X0 (free: layer
-    // 5 has read it), the losses' input
+    // ---- fused losses (LA > 0): ppo_loss_grad's work for the block's rows (ppo_loss.h), eight lanes per row
+    // in two passes.  Their dataset loads are issued here, ahead of the heads, so the round trip overlaps the
+    // heads' MFMAs and the two barriers (layer 5's weights are dead: the registers are free)
     constexpr int kHS = (LA + 1) | 1;
     float* sh = reinterpret_cast<float*>(X0);
-    if (wave < 4 && a.head) {
-        f32x16 hacc[4];
-        mma_rows<DT, 16, 1>(X1, whf, hacc, wave, j, h);
-        const int rl = 32 * wave + j, row = row0 + rl;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int o = feat(r, h);
-            const float v = float((E)(hacc[0][r] + float((E)bhv[r])));
-            if (o < a.nh && row < rows) a.head[int64_t(row) * a.nh + o] = v;
-            if (LA > 0 && o <= LA) sh[rl * kHS + o] = v;
-        }
-    }
+    ppo_detail::LossRowArgs p{};
+    ppo_detail::LossIn<LA> lin[LA > 0 ? ppo_detail::loss_passes<kFThreads>() : 1];
     if constexpr (LA > 0) {
-        // ppo_loss_grad's work for the block's rows (ppo_loss.h), eight lanes per row in two passes; the
-        // per-row table in X1 (the heads' MFMAs have read it)
-        __syncthreads();
-        ppo_detail::LossRowArgs p{};
         p.head = sh;
         p.head_stride = kHS;
         p.head_block_rows = false;
@@ -542,7 +527,28 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
         p.lp_dtype = DT;
         p.partials = a.loss.partials;
         static_assert(kFRows == ppo_detail::kLossRows, "one loss block per workgroup");
-        ppo_detail::loss_block<LA, kFThreads>(p, blockIdx.x, reinterpret_cast<float*>(X1));
+        ppo_detail::loss_prefetch<LA, kFThreads>(p, blockIdx.x, lin);
+    }
+    __syncthreads();
+    // ---- heads: wave w < 4 takes N-tile w; out = 16-bit(acc + 16-bit(bh)) as under autocast.  With the
+    // fused losses (LA > 0) the values also go to a table of the block's rows at the head of X0 (free: layer
+    // 5 has read it), the losses' input
+    if (wave < 4 && a.head) {
+        f32x16 hacc[4];
+        mma_rows<DT, 16, 1>(X1, whf, hacc, wave, j, h);
+        const int rl = 32 * wave + j, row = row0 + rl;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int o = feat(r, h);
+            const float v = float((E)(hacc[0][r] + float((E)bhv[r])));
+            if (o < a.nh && row < rows) a.head[int64_t(row) * a.nh + o] = v;
+            if (LA > 0 && o <= LA) sh[rl * kHS + o] = v;
+        }
+    }
+    if constexpr (LA > 0) {
+        // the losses' per-row table in X1 (the heads' MFMAs have read it)
+        __syncthreads();
+        ppo_detail::loss_block<LA, kFThreads>(p, blockIdx.x, reinterpret_cast<float*>(X1), lin);
     }
 }
 
