@@ -453,6 +453,17 @@ __global__ void __launch_bounds__(64) k_meter_update(const float* __restrict__ p
 
 // ------------------------------------------------------------------------------ partial-row reductions
 
+// ppo_opt_snap_t: Adam's step inputs as this launch found them (ppo_adam_step reads them instead of the
+// originals its first block rewrites)
+__device__ __forceinline__ void write_snap(ppo_opt_snap_t* snap, const double* lr, const double* step,
+                                           const float* scaler) {
+    ppo_opt_snap_t s{};
+    s.lr = *lr;
+    s.step = *step;
+    s.scale = scaler ? scaler[0] : 1.f;
+    *snap = s;
+}
+
 struct JobTable {
     ppo_reduce_job_t j[PPO_MAX_JOBS];
     int32_t count[PPO_MAX_JOBS];          // threads of each job
@@ -464,6 +475,9 @@ struct JobTable {
     const float* scaler;
     const float* extra[2];
     int32_t extra_n[2];
+    const double* lr;  // the optimizer snapshot (NULL: none), written by the extra block
+    const double* step;
+    ppo_opt_snap_t* snap;
 };
 
 // The splits of one output are summed by kRedT threads -- the block's threads t + kRedOut * i take the
@@ -536,6 +550,7 @@ __global__ void __launch_bounds__(256) k_reduce_rows(JobTable t) {
         else
             reduce_cols<1>(t.j[k], o, active, inv_scale, sq, bad);
     } else {
+        if (t.snap && threadIdx.x == 0) write_snap(t.snap, t.lr, t.step, t.scaler);
         for (int a = 0; a < 2; ++a)
             for (int i = threadIdx.x; i < t.extra_n[a]; i += 256) {
                 const float v = t.extra[a][i];
@@ -574,8 +589,10 @@ constexpr int kAdamThreads = 256;
 // isfinite(g[i]) -- kept apart from the norm so a finite gradient whose square sum overflows is
 // clipped, not skipped).  The scale is a power of two, so g / scale is exact.
 __global__ void __launch_bounds__(256) k_sqnorm(const float* __restrict__ g, int64_t n, const float* __restrict__ scaler,
-                                                float* __restrict__ partials) {
+                                                float* __restrict__ partials, const double* lr, const double* step,
+                                                ppo_opt_snap_t* snap) {
     __shared__ float red[2][256 / kWave];
+    if (snap && blockIdx.x == 0 && threadIdx.x == 0) write_snap(snap, lr, step, scaler);
     const float inv_scale = scaler ? 1.f / scaler[0] : 1.f;
     float s = 0.f, bad = 0.f;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
@@ -665,13 +682,38 @@ __device__ void tail_store(const ppo_tail_args_t& t, const TailVals& v, bool ski
     *t.stat_idx = v.st + 1;
 }
 
-__global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, const float* __restrict__ g,
-                                                       float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                       const float* __restrict__ np, int nnp, float max_norm,
-                                                       const double* __restrict__ lr_p, const double* __restrict__ step_p,
-                                                       float b1, float b2, float eps, SegTable segs,
-                                                       uint16_t* __restrict__ mirror, int mirror_dtype,
-                                                       const float* __restrict__ scaler) {
+struct AdamArgs {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    int64_t n;
+    const float* np;  // norm partials [nnp sums | nnp non-finite counts]
+    int nnp;
+    float max_norm;
+    const double* lr_p;  // !TAIL: Adam's lr / step / the scaler read here
+    const double* step_p;
+    const float* scaler;  // the scaler (NULL: none; with TAIL only tested for NULL, the scale is in snap)
+    float b1, b2, eps;
+    SegTable segs;
+    uint16_t* mirror;
+    int mirror_dtype;
+    const ppo_opt_snap_t* snap;  // TAIL: lr / step / scale from the norm launch's snapshot
+    ppo_tail_args_t tail;        // TAIL: run by block 0 on the originals
+};
+
+// clip + Adam (ppo_adam); with TAIL also ppo_tail's work, by block 0 (ppo_adam_step): the other blocks read
+// lr / step / scale from the snapshot, never the originals the tail rewrites, so no block waits for another
+template <bool TAIL>
+__global__ void __launch_bounds__(kAdamThreads) k_adam(AdamArgs a) {
+    float* __restrict__ p = a.p;
+    const float* __restrict__ g = a.g;
+    float* __restrict__ m = a.m;
+    float* __restrict__ v = a.v;
+    const float* __restrict__ np = a.np;
+    const int64_t n = a.n;
+    const int nnp = a.nnp;
+    const float b1 = a.b1, b2 = a.b2, eps = a.eps;
     __shared__ float red[2][kAdamThreads / kWave];
     __shared__ float coef_s, step_size_s, bc2_sqrt_s, inv_scale_s;
     __shared__ int skip_s;
@@ -703,10 +745,21 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
     // thread 0: the bias corrections (fp64 pow / sqrt are long instruction sequences) while those loads
     // are in flight
     float scale0 = 1.f, step_size0 = 0.f, bc2_sqrt0 = 0.f;
+    TailVals tv{};
     if (threadIdx.x == 0) {
-        if (scaler) scale0 = scaler[0];
-        const double ts = *step_p + 1.0;
-        step_size0 = float(*lr_p / (1.0 - pow(double(b1), ts)));
+        double lr, st;
+        if constexpr (TAIL) {
+            if (blockIdx.x == 0) tv = tail_load(a.tail);  // in flight with the partials
+            lr = a.snap->lr;
+            st = a.snap->step;
+            scale0 = a.snap->scale;
+        } else {
+            lr = *a.lr_p;
+            st = *a.step_p;
+            if (a.scaler) scale0 = a.scaler[0];
+        }
+        const double ts = st + 1.0;
+        step_size0 = float(lr / (1.0 - pow(double(b1), ts)));
         bc2_sqrt0 = float(sqrt(1.0 - pow(double(b2), ts)));
     }
 #pragma unroll
@@ -745,13 +798,17 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
         // GradScaler: grads carry the loss scale (a power of two); a non-finite element skips the step
         // (scaler.step's found_inf), otherwise they are unscaled exactly before the clip (unscale_)
         inv_scale_s = 1.f / scale0;
-        skip_s = scaler && b > 0.f;
+        const bool skip = a.scaler && b > 0.f;
+        skip_s = skip;
         // torch.nn.utils.clip_grad_norm_: coef = clamp(max_norm / (total_norm + 1e-6), max=1); the
         // norm is of the unscaled grads (k_sqnorm); a NaN norm makes coef NaN (clamp keeps NaN)
-        const float c = max_norm / (sqrtf(t) + 1e-6f);
-        coef_s = max_norm > 0.f ? (c < 1.f || c != c ? c : 1.f) : 1.f;
+        const float c = a.max_norm / (sqrtf(t) + 1e-6f);
+        coef_s = a.max_norm > 0.f ? (c < 1.f || c != c ? c : 1.f) : 1.f;
         step_size_s = step_size0;
         bc2_sqrt_s = bc2_sqrt0;
+        if constexpr (TAIL) {
+            if (blockIdx.x == 0) tail_store(a.tail, tv, skip);  // the same decision k_tail makes
+        }
     }
     __syncthreads();
     const float coef = coef_s;
@@ -768,15 +825,15 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(float* __restrict__ p, co
         const float denom = sqrtf(vi) / bc2_sqrt + eps;
         const float pi = p0 - step_size * (mi / denom);
         p[i] = pi;
-        if (mirror) {
-            for (int k = 0; k < segs.n; ++k) {
-                const ppo_seg_t& sg = segs.s[k];
+        if (a.mirror) {
+            for (int k = 0; k < a.segs.n; ++k) {
+                const ppo_seg_t& sg = a.segs.s[k];
                 if (i >= sg.off && i < sg.off + sg.len) {
                     // 32-bit division: seg_table holds every segment below 2^31 elements
                     const uint32_t j = uint32_t(i - sg.off), cols = uint32_t(sg.cols);
                     const int64_t r = j / cols, c = j % cols;
-                    mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] =
-                        mirror_dtype == PPO_DT_F16 ? f32_to_f16(pi) : f32_to_bf16(pi);
+                    a.mirror[sg.moff + (sg.trans ? c * sg.mstride + r : r * sg.mstride + c)] =
+                        a.mirror_dtype == PPO_DT_F16 ? f32_to_f16(pi) : f32_to_bf16(pi);
                 }
             }
         }
@@ -977,13 +1034,18 @@ int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stre
 
 int ppo_reduce_rows_norm(const ppo_reduce_job_t* jobs_host, int32_t njobs, const float* scaler, const float* extra0,
                          int32_t extra0_n, const float* extra1, int32_t extra1_n, float* norm_partials,
-                         int32_t max_blocks, int32_t* nblk_out, void* stream) {
+                         int32_t max_blocks, int32_t* nblk_out, const double* lr, const double* step,
+                         ppo_opt_snap_t* snap, void* stream) {
     JobTable t;
     if (const int rc = reduce_table(jobs_host, njobs, t)) return rc;
     const int nblk = t.blk_start[njobs] + 1;
     if (!norm_partials || !nblk_out || nblk > max_blocks || extra0_n < 0 || extra1_n < 0 ||
         (extra0_n && !extra0) || (extra1_n && !extra1))
         return fail(-1, "ppo_reduce_rows_norm: bad norm arguments");
+    if (snap && (!lr || !step)) return fail(-1, "ppo_reduce_rows_norm: the snapshot needs lr and step");
+    t.lr = lr;
+    t.step = step;
+    t.snap = snap;
     t.norm = norm_partials;
     t.scaler = scaler;
     t.extra[0] = extra0;
@@ -1039,8 +1101,10 @@ int ppo_meter_update(const float* partials, int32_t nblk, float max_size, float*
 
 int ppo_sqnorm_blocks(void) { return kNormBlocks; }
 
-int ppo_sqnorm(const float* g, int64_t n, const float* scaler, float* partials, void* stream) {
-    hipLaunchKernelGGL(k_sqnorm, dim3(kNormBlocks), dim3(256), 0, S(stream), g, n, scaler, partials);
+int ppo_sqnorm(const float* g, int64_t n, const float* scaler, float* partials, const double* lr, const double* step,
+               ppo_opt_snap_t* snap, void* stream) {
+    if (snap && (!lr || !step)) return fail(-1, "ppo_sqnorm: the snapshot needs lr and step");
+    hipLaunchKernelGGL(k_sqnorm, dim3(kNormBlocks), dim3(256), 0, S(stream), g, n, scaler, partials, lr, step, snap);
     return launched("k_sqnorm");
 }
 
@@ -1064,12 +1128,29 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
              float max_norm, const double* lr, double* step, float beta1, float beta2, float eps,
              const ppo_seg_t* segs_host, int32_t nseg, void* mirror, int32_t mirror_dtype, const float* scaler,
              void* stream) {
-    SegTable t;
-    if (const int rc = seg_table(segs_host, nseg, mirror, mirror_dtype, t)) return rc;
+    AdamArgs a{};
+    if (const int rc = seg_table(segs_host, nseg, mirror, mirror_dtype, a.segs)) return rc;
     if (nblk_norm < 1) return fail(-1, "ppo_adam: need nblk_norm >= 1");
-    hipLaunchKernelGGL(k_adam, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0,
-                       S(stream), p, g, m, v, n, sqnorm_partials, nblk_norm, max_norm, lr, step, beta1, beta2, eps, t,
-                       static_cast<uint16_t*>(mirror), mirror_dtype, scaler);
+    if (n < 0 || !lr || !step) return fail(-1, "ppo_adam: bad arguments");
+    a.p = p;
+    a.g = g;
+    a.m = m;
+    a.v = v;
+    a.n = n;
+    a.np = sqnorm_partials;
+    a.nnp = nblk_norm;
+    a.max_norm = max_norm;
+    a.lr_p = lr;
+    a.step_p = step;
+    a.scaler = scaler;
+    a.b1 = beta1;
+    a.b2 = beta2;
+    a.eps = eps;
+    a.mirror = static_cast<uint16_t*>(mirror);
+    a.mirror_dtype = mirror_dtype;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_adam<false>, dim3(unsigned((n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0,
+                       S(stream), a);
     return launched("k_adam");
 }
 
@@ -1089,6 +1170,35 @@ int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, dou
     if (const int rc = check_tail(t, sqnorm_partials, nblk_norm)) return rc;
     hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTailThreads), 0, S(stream), t, sqnorm_partials, nblk_norm);
     return launched("k_tail");
+}
+
+int ppo_adam_step(const ppo_adam_step_t* s, void* stream) {
+    if (!s) return fail(-1, "ppo_adam_step: null arguments");
+    AdamArgs a{};
+    if (const int rc = seg_table(s->segs_host, s->nseg, s->mirror, s->mirror_dtype, a.segs)) return rc;
+    if (s->nblk_norm < 1 || !s->norm_partials) return fail(-1, "ppo_adam_step: need the norm partials (nblk_norm >= 1)");
+    if (s->n <= 0 || !s->snap) return fail(-1, "ppo_adam_step: need n > 0 and the snapshot");
+    a.tail = ppo_tail_args_t{s->lr, s->kl, s->kl_threshold, s->min_lr, s->max_lr, s->step, s->mb_idx,
+                             s->n_minibatches, s->stat_idx, s->scaler, s->growth_interval};
+    if (const int rc = check_tail(a.tail, s->norm_partials, s->nblk_norm)) return rc;
+    a.p = s->p;
+    a.g = s->g;
+    a.m = s->m;
+    a.v = s->v;
+    a.n = s->n;
+    a.np = s->norm_partials;
+    a.nnp = s->nblk_norm;
+    a.max_norm = s->max_norm;
+    a.scaler = s->scaler;
+    a.b1 = s->beta1;
+    a.b2 = s->beta2;
+    a.eps = s->eps;
+    a.mirror = static_cast<uint16_t*>(s->mirror);
+    a.mirror_dtype = s->mirror_dtype;
+    a.snap = s->snap;
+    hipLaunchKernelGGL(k_adam<true>, dim3(unsigned((s->n + kAdamThreads - 1) / kAdamThreads)), dim3(kAdamThreads), 0,
+                       S(stream), a);
+    return launched("k_adam_step");
 }
 
 }  // extern "C"

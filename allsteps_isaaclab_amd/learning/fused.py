@@ -40,7 +40,7 @@ import torch.nn.functional as F
 from .._native import PPO_LIB_PATH, NativeError, check_build_id
 
 _LIB = None
-PPO_ABI_VERSION = 4
+PPO_ABI_VERSION = 5
 PPO_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 SCALER_GROWTH_INTERVAL = 2000  # torch.cuda.amp.GradScaler defaults (rl_games builds it with defaults)
 SCALER_INIT = 2.0 ** 16
@@ -97,12 +97,22 @@ class PpoSeg(C.Structure):
                 ("mstride", C.c_int32), ("trans", C.c_int32)]
 
 
+class PpoAdamStep(C.Structure):
+    _fields_ = [("p", C.c_void_p), ("g", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p), ("n", C.c_int64),
+                ("norm_partials", C.c_void_p), ("nblk_norm", C.c_int32), ("max_norm", C.c_float),
+                ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("segs_host", C.POINTER(PpoSeg)),
+                ("nseg", C.c_int32), ("mirror", C.c_void_p), ("mirror_dtype", C.c_int32), ("snap", C.c_void_p),
+                ("lr", C.c_void_p), ("kl", C.c_void_p), ("kl_threshold", C.c_float), ("min_lr", C.c_double),
+                ("max_lr", C.c_double), ("step", C.c_void_p), ("mb_idx", C.c_void_p), ("n_minibatches", C.c_int32),
+                ("stat_idx", C.c_void_p), ("scaler", C.c_void_p), ("growth_interval", C.c_int32)]
+
+
 EXPORTED_SYMBOLS = ["ppo_abi_version", "ppo_last_error", "ppo_obs_stats_blocks", "ppo_obs_stats",
                     "ppo_obs_stats_update", "ppo_obs_normalize", "ppo_loss_blocks", "ppo_loss_grad",
                     "ppo_loss_finalize", "ppo_elu_bwd_blocks", "ppo_elu_bwd", "ppo_sqnorm_blocks", "ppo_sqnorm",
                     "ppo_adam", "ppo_tail", "ppo_reduce_rows", "ppo_policy_sample", "ppo_counter_add",
                     "ppo_mlp_forward", "ppo_rollout_post_blocks", "ppo_rollout_post", "ppo_meter_update",
-                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_reduce_rows_norm"]
+                    "ppo_mlp_backward", "ppo_weight_grads", "ppo_build_id", "ppo_reduce_rows_norm", "ppo_adam_step"]
 
 
 def load() -> C.CDLL:
@@ -121,11 +131,13 @@ def load() -> C.CDLL:
     L.ppo_loss_grad.argtypes = [V, V, I32, I32, V, V, V, V, V, V, V, V, PpoLossCfg, V, V, V, V, I32, V]
     L.ppo_loss_finalize.argtypes = [V, I32, I32, I32, F32, V, V, V, V, V, V, V]
     L.ppo_elu_bwd.argtypes = [V, I32, V, I32, V, I32, I32, I32, V, V]
-    L.ppo_sqnorm.argtypes = [V, I64, V, V, V]
+    L.ppo_sqnorm.argtypes = [V, I64, V, V, V, V, V, V]
     L.ppo_adam.argtypes = [V, V, V, V, I64, V, I32, F32, V, V, F32, F32, F32, C.POINTER(PpoSeg), I32, V, I32, V, V]
     L.ppo_tail.argtypes = [V, V, F32, F64, F64, V, V, I32, V, V, V, I32, I32, V]
     L.ppo_reduce_rows.argtypes = [C.POINTER(PpoReduceJob), I32, V]
-    L.ppo_reduce_rows_norm.argtypes = [C.POINTER(PpoReduceJob), I32, V, V, I32, V, I32, V, I32, C.POINTER(I32), V]
+    L.ppo_reduce_rows_norm.argtypes = [C.POINTER(PpoReduceJob), I32, V, V, I32, V, I32, V, I32, C.POINTER(I32), V, V,
+                                       V, V]
+    L.ppo_adam_step.argtypes = [C.POINTER(PpoAdamStep), V]
     L.ppo_policy_sample.argtypes = [V, V, I32, I32, C.c_uint64, V, V, V, F32, V, V, V, V, V, V]
     L.ppo_counter_add.argtypes = [V, I64, V]
     L.ppo_mlp_forward.argtypes = [C.POINTER(PpoMlpFwd), V]
@@ -247,6 +259,11 @@ class FusedPPOUpdate:
             and getattr(agent, "world_size", 1) > 1)
         self.red_norm = torch.empty(2 * 4096, device=dev)
         self._red_nblk = C.c_int32(0)
+        # ppo_opt_snap_t (lr, step, scale): taken by the norm launch, read by ppo_adam_step, whose first
+        # block runs the tail on the originals
+        self.opt_snap = torch.zeros(4, dtype=torch.float64, device=dev)
+        # A/B knob: PPO_SEPARATE_TAIL=1 runs ppo_adam + ppo_tail as two launches (the round-5 form)
+        self.fuse_tail = os.environ.get("PPO_SEPARATE_TAIL", "0") != "1"
         self.mb_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stat_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stats = torch.zeros(agent.mini_epochs_num * self.n_mb + 1, PPO_LOSS_NSTAT, device=dev)
@@ -377,7 +394,8 @@ class FusedPPOUpdate:
             return
         _check(self.L.ppo_reduce_rows_norm(arr, len(jobs), _p(self.scaler), _p(self.gbh), self.gbh.numel(),
                                            _p(self.gls), self.gls.numel(), _p(self.red_norm),
-                                           self.red_norm.numel() // 2, C.byref(self._red_nblk), s),
+                                           self.red_norm.numel() // 2, C.byref(self._red_nblk), _p(self.agent.lr),
+                                           _p(self.agent.optimizer.step_t), _p(self.opt_snap), s),
                "ppo_reduce_rows_norm")
 
     def _stream(self) -> int:
@@ -602,17 +620,27 @@ class FusedPPOUpdate:
             if nnp <= 0:
                 raise NativeError("fused gradient norm: step_b before step_a")
         else:
-            _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.scaler), _p(self.norm_partials), s), "ppo_sqnorm")
+            _check(L.ppo_sqnorm(_p(fl.grads), n, _p(self.scaler), _p(self.norm_partials), _p(ag.lr),
+                                _p(ag.optimizer.step_t), _p(self.opt_snap), s), "ppo_sqnorm")
             npart, nnp = self.norm_partials, self.norm_partials.numel() // 2
         opt = ag.optimizer
-        _check(L.ppo_adam(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n,
-                          _p(npart), nnp,
-                          ag.grad_norm if ag.truncate_grads else 0.0, _p(ag.lr), _p(opt.step_t), opt.beta1, opt.beta2,
-                          opt.eps, self.segs, self.nseg, _p(self.mirror), self.dt_code if self.lp else 1,
-                          _p(self.scaler), s), "ppo_adam")
-        _check(L.ppo_tail(_p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr, self.max_lr,
-                          _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), _p(self.scaler),
-                          _p(npart), nnp, SCALER_GROWTH_INTERVAL, s), "ppo_tail")
+        if not self.fuse_tail:
+            _check(L.ppo_adam(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n, _p(npart), nnp,
+                              ag.grad_norm if ag.truncate_grads else 0.0, _p(ag.lr), _p(opt.step_t), opt.beta1,
+                              opt.beta2, opt.eps, self.segs, self.nseg, _p(self.mirror), self.dt_code if self.lp else 1,
+                              _p(self.scaler), s), "ppo_adam")
+            _check(L.ppo_tail(_p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr, self.max_lr,
+                              _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), _p(self.scaler),
+                              _p(npart), nnp, SCALER_GROWTH_INTERVAL, s), "ppo_tail")
+            return
+        # clip + Adam + the tail (adaptive LR, GradScaler update, counters) in one launch
+        a = PpoAdamStep(_p(fl.params), _p(fl.grads), _p(opt.exp_avg), _p(opt.exp_avg_sq), n, _p(npart), nnp,
+                        ag.grad_norm if ag.truncate_grads else 0.0, opt.beta1, opt.beta2, opt.eps, self.segs,
+                        self.nseg, _p(self.mirror), self.dt_code if self.lp else 1, _p(self.opt_snap),
+                        _p(ag.lr), _p(fl.extra), self.kl_thr if self.legacy else 0.0, self.min_lr, self.max_lr,
+                        _p(opt.step_t), _p(self.mb_idx), self.n_mb, _p(self.stat_idx), _p(self.scaler),
+                        SCALER_GROWTH_INTERVAL)
+        _check(L.ppo_adam_step(C.byref(a), s), "ppo_adam_step")
 
     # ------------------------------------------------------------------ graphs
     def _run(self, key, fn) -> None:

@@ -20,6 +20,10 @@
  *                                         torch.cuda.amp.GradScaler) the unscale, the skip of a step
  *                                         with non-finite gradients and the scale update
  *   ppo_tail                              adaptive LR from the (rank-averaged) KL; minibatch counter
+ *   ppo_adam_step                         ppo_adam + ppo_tail in ONE launch (round 5): Adam reads its
+ *                                         lr / step / scale from the snapshot the norm launch took
+ *                                         (ppo_opt_snap_t), so the first block may run the tail on the
+ *                                         originals while the others still read
  *   ppo_mlp_forward / ppo_mlp_backward    the whole trunk forward / input-gradient chain (MFMA)
  *   ppo_weight_grads                      split-K weight + bias gradients of all trunk layers and the
  *                                         head weights (MFMA, one launch)
@@ -38,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PPO_ABI_VERSION 4
+#define PPO_ABI_VERSION 5
 /* element types of the low-precision (trunk) buffers */
 #define PPO_DT_F32 0
 #define PPO_DT_BF16 1
@@ -126,9 +130,21 @@ int ppo_reduce_rows(const ppo_reduce_job_t* jobs_host, int32_t njobs, void* stre
  * counts] (scaler: as ppo_sqnorm) over every dst element written plus the extra arrays (the gradients
  * other kernels wrote: head biases, log-sigma); *nblk_out = nblk (<= max_blocks) is the count to pass to
  * ppo_adam / ppo_tail as nblk_norm. */
+/* Adam's step inputs as a launch ahead of the optimizer found them: lr, step (the count before this step),
+ * scale (the loss scale; 1 without a scaler).  Written by ppo_sqnorm / ppo_reduce_rows_norm when given a
+ * snapshot pointer (one thread, after nothing of theirs depends on it), read by ppo_adam_step. */
+typedef struct {
+    double lr;
+    double step;
+    float scale;
+    float pad_;
+} ppo_opt_snap_t;
+
+/* ... + snap (NULL = none): the snapshot of *lr, *step and the scale (lr / step non-NULL with it) */
 int ppo_reduce_rows_norm(const ppo_reduce_job_t* jobs_host, int32_t njobs, const float* scaler, const float* extra0,
                          int32_t extra0_n, const float* extra1, int32_t extra1_n, float* norm_partials,
-                         int32_t max_blocks, int32_t* nblk_out, void* stream);
+                         int32_t max_blocks, int32_t* nblk_out, const double* lr, const double* step,
+                         ppo_opt_snap_t* snap, void* stream);
 
 /* Rollout policy head (graph-safe sampling): head = [mu | value] (rows x (A+1), fp32), logstd (A).
  * actions = mu + exp(logstd) * N(0, 1) with the normals from Philox4x32-10 keyed by `seed` and
@@ -275,7 +291,9 @@ int ppo_meter_update(const float* partials, int32_t nblk, float max_size, float*
  * NULL: scale 1; NaN / inf propagate into the norm as in torch), [nblk, 2 nblk) block counts of
  * non-finite g (GradScaler's found_inf: an OR over isfinite, separate from the norm) */
 int ppo_sqnorm_blocks(void);
-int ppo_sqnorm(const float* g, int64_t n, const float* scaler, float* partials, void* stream);
+/* snap (NULL = none): as ppo_reduce_rows_norm */
+int ppo_sqnorm(const float* g, int64_t n, const float* scaler, float* partials, const double* lr, const double* step,
+               ppo_opt_snap_t* snap, void* stream);
 /* clip (max_norm > 0: g *= min(1, max_norm / (||g|| + 1e-6))) + Adam (torch.optim.Adam, amsgrad off,
  * weight_decay 0) with device lr / step (fp64); writes the mirror (mirror_dtype PPO_DT_BF16 / PPO_DT_F16)
  * of the listed segments.  scaler (device fp32 [scale, growth tracker], NULL = none): the gradients
@@ -294,6 +312,38 @@ int ppo_adam(float* p, const float* g, float* m, float* v, int64_t n, const floa
 int ppo_tail(double* lr, const float* kl, float kl_threshold, double min_lr, double max_lr, double* step,
              int32_t* mb_idx, int32_t n_minibatches, int32_t* stat_idx, float* scaler, const float* sqnorm_partials,
              int32_t nblk_norm, int32_t growth_interval, void* stream);
+
+/* ppo_adam then ppo_tail as ONE launch: the clip + Adam of ppo_adam with lr, step and the scale read from
+ * `snap` (taken this minibatch by ppo_sqnorm / ppo_reduce_rows_norm), and ppo_tail's update of the
+ * originals (lr, step, mb_idx, stat_idx, scaler) run by the launch's first block -- no other block reads
+ * them, so no hand-off is needed.  Same arguments and results as the two calls. */
+typedef struct {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    int64_t n;
+    const float* norm_partials;
+    int32_t nblk_norm;
+    float max_norm, beta1, beta2, eps;
+    const ppo_seg_t* segs_host;
+    int32_t nseg;
+    void* mirror;
+    int32_t mirror_dtype;
+    const ppo_opt_snap_t* snap;
+    /* the tail (ppo_tail's arguments) */
+    double* lr;
+    const float* kl;
+    float kl_threshold;
+    double min_lr, max_lr;
+    double* step;
+    int32_t* mb_idx;
+    int32_t n_minibatches;
+    int32_t* stat_idx;
+    float* scaler;
+    int32_t growth_interval;
+} ppo_adam_step_t;
+int ppo_adam_step(const ppo_adam_step_t* a, void* stream);
 
 
 #ifdef __cplusplus

@@ -2,6 +2,7 @@
 ppo_loss_grad + ppo_loss_finalize; and of the optimizer step ppo_sqnorm + ppo_adam + ppo_tail on a
 333k-element flat buffer with a row-major and a transposed fp16 mirror segment.
     python scripts/loss_bench.py [rows]"""
+import ctypes as C
 import json
 import os
 import sys
@@ -62,14 +63,27 @@ def main():
     scaler = torch.tensor([65536.0, 0.0], device=dev)
     mb, st = torch.zeros(1, device=dev, dtype=torch.int32), torch.zeros(1, device=dev, dtype=torch.int32)
 
+    snap = torch.zeros(4, device=dev, dtype=torch.float64)
+
     def three():
-        L.ppo_sqnorm(grads.data_ptr(), n, scaler.data_ptr(), partials.data_ptr(), s)
+        L.ppo_sqnorm(grads.data_ptr(), n, scaler.data_ptr(), partials.data_ptr(), None, None, None, s)
         L.ppo_adam(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, partials.data_ptr(), nb, 1.0,
                    lr.data_ptr(), step.data_ptr(), 0.9, 0.999, 1e-8, segs, 2, mirror.data_ptr(), 2, scaler.data_ptr(), s)
         L.ppo_tail(lr.data_ptr(), kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4, st.data_ptr(),
                    scaler.data_ptr(), partials.data_ptr(), nb, 1 << 30, s)
 
     out["sqnorm_adam_tail_us"] = t(three)
+
+    def two():  # the norm launch taking the snapshot, then Adam + tail in one launch (ppo_adam_step)
+        L.ppo_sqnorm(grads.data_ptr(), n, scaler.data_ptr(), partials.data_ptr(), lr.data_ptr(), step.data_ptr(),
+                     snap.data_ptr(), s)
+        a = FU.PpoAdamStep(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, partials.data_ptr(), nb,
+                           1.0, 0.9, 0.999, 1e-8, segs, 2, mirror.data_ptr(), 2, snap.data_ptr(), lr.data_ptr(),
+                           kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4, st.data_ptr(),
+                           scaler.data_ptr(), 1 << 30)
+        L.ppo_adam_step(C.byref(a), s)
+
+    out["sqnorm_adam_step_us"] = t(two)
     print(json.dumps(out), flush=True)
 
 

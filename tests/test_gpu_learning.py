@@ -774,6 +774,77 @@ def test_weight_grads_side_job_equals_loss_finalize():
         assert torch.equal(x, y)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["good_growth", "skip", "no_scaler"])
+def test_adam_step_equals_adam_then_tail(case):
+    """ppo_adam_step (Adam reading the norm launch's snapshot, the tail run by its first block) against
+    ppo_sqnorm + ppo_adam + ppo_tail on the same inputs: parameters, moments, the 16-bit mirror, lr, step,
+    the scaler and the counters bit for bit -- a good step that ends a growth interval (scale x2, KL above
+    2x the threshold: lr / 1.5), a step skipped on a non-finite gradient (scale x0.5, step kept), and no
+    scaler at all."""
+    import ctypes as C
+
+    from allsteps_isaaclab_amd.learning import fused as FU
+
+    L = FU.load()
+    dev = "cuda:0"
+    gen = torch.Generator(device=dev).manual_seed(3)
+    n = 300_001
+    grads = torch.randn(n, device=dev, generator=gen) * 1e3
+    if case == "skip":
+        grads[12345] = float("inf")
+    p0 = torch.randn(n, device=dev, generator=gen)
+    m0 = torch.randn(n, device=dev, generator=gen) * 0.01
+    v0 = torch.rand(n, device=dev, generator=gen) * 0.01
+    segs = (FU.PpoSeg * 2)(FU.PpoSeg(0, 65536, 0, 256, 256, 0), FU.PpoSeg(65536, 65536, 65536, 256, 256, 1))
+    nb = L.ppo_sqnorm_blocks()
+    outs = []
+    for fused in (False, True):
+        p, m, v = p0.clone(), m0.clone(), v0.clone()
+        mirror = torch.zeros(2 * 65536, device=dev, dtype=torch.float16)
+        lr = torch.tensor([3e-4], device=dev, dtype=torch.float64)
+        step = torch.tensor([7.0], device=dev, dtype=torch.float64)
+        scaler = None if case == "no_scaler" else torch.tensor([65536.0, 1999.0], device=dev)
+        kl = torch.tensor([0.02], device=dev)
+        mb = torch.tensor([3], device=dev, dtype=torch.int32)
+        st = torch.tensor([5], device=dev, dtype=torch.int32)
+        part = torch.zeros(2 * nb, device=dev)
+        snap = torch.zeros(4, device=dev, dtype=torch.float64)
+        sp = None if scaler is None else scaler.data_ptr()
+        if not fused:
+            assert L.ppo_sqnorm(grads.data_ptr(), n, sp, part.data_ptr(), None, None, None, None) == 0
+            assert L.ppo_adam(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, part.data_ptr(), nb,
+                              1.0, lr.data_ptr(), step.data_ptr(), 0.9, 0.999, 1e-8, segs, 2, mirror.data_ptr(), 2,
+                              sp, None) == 0
+            assert L.ppo_tail(lr.data_ptr(), kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4,
+                              st.data_ptr(), sp, part.data_ptr(), nb, 2000, None) == 0
+        else:
+            assert L.ppo_sqnorm(grads.data_ptr(), n, sp, part.data_ptr(), lr.data_ptr(), step.data_ptr(),
+                                snap.data_ptr(), None) == 0
+            a = FU.PpoAdamStep(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), n, part.data_ptr(), nb,
+                               1.0, 0.9, 0.999, 1e-8, segs, 2, mirror.data_ptr(), 2, snap.data_ptr(), lr.data_ptr(),
+                               kl.data_ptr(), 0.008, 1e-6, 1e-2, step.data_ptr(), mb.data_ptr(), 4, st.data_ptr(), sp,
+                               2000)
+            assert L.ppo_adam_step(C.byref(a), None) == 0
+        torch.cuda.synchronize()
+        outs.append([p, m, v, mirror, lr, step, kl, mb, st] + ([] if scaler is None else [scaler]))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    p, _, _, _, lr, step = outs[1][:6]
+    assert int(outs[1][7]) == 0 and int(outs[1][8]) == 6  # mb_idx (3 + 1) % 4, stat_idx + 1
+    if case == "skip":
+        assert torch.equal(p, p0) and float(step) == 7.0 and float(outs[1][-1][0]) == 32768.0
+    else:
+        assert not torch.equal(p, p0) and float(step) == 8.0
+        assert float(lr) == pytest.approx(3e-4 / 1.5)
+        if case == "good_growth":
+            assert float(outs[1][-1][0]) == 131072.0 and float(outs[1][-1][1]) == 0.0
+    # without the snapshot pointer the step refuses to run
+    a.snap = None
+    assert L.ppo_adam_step(C.byref(a), None) != 0
+
+
+
 def test_weight_grads_rejects_bad_arguments():
     import ctypes as C
 
