@@ -14,6 +14,7 @@ from typing import Any
 
 import torch
 
+from .scene import SceneView
 from .spaces import Box, Dict, batch_box
 
 
@@ -31,6 +32,7 @@ class DirectRLEnv:
             cfg.seed = self.seed(cfg.seed)
         self._device = torch.device(cfg.sim.device)
         self.num_envs = int(cfg.scene.num_envs)
+        self.scene = SceneView(cfg.scene, self._device)  # env_origins: the reference's world offsets
         self.common_step_counter = 0
         self._sim_step_counter = 0
         self.extras: dict = {}
