@@ -83,17 +83,19 @@ def _describe(gs, st, n, bad):
     return "\n".join(lines)
 
 
-def _run(orc, capsys, n, level, steps, warm, seed=42):
+def _run(orc, capsys, n, level, steps, warm, seed=42, near_timeout=False):
     env = _env(n, level, seed)
     env.reset()
     gen = torch.Generator(device="cuda").manual_seed(seed + warm)
     for _ in range(warm):  # GPU alone: reach a contact-rich, mid-episode state
         env.step(torch.rand(n, 21, device="cuda", generator=gen) * 2.4 - 1.2)
+    if near_timeout:  # episode counters 890..898: every env meets the 899-step time-out inside the window
+        env.set_state({"ep_len": (890 + torch.arange(n, device="cuda") % 9).to(torch.int32).reshape(1, n)})
     torch.cuda.synchronize()
     st = orc.state(n)
     _to_oracle(env, st)
     rng = np.random.default_rng(1000 + n + level + warm)
-    resets = contacts = dropped = 0
+    resets = contacts = dropped = truncs = 0
     for t in range(steps):
         act = rng.uniform(-1.2, 1.2, (n, 21)).astype(np.float32)
         o_g, r_g, t_g, tr_g, _ = env.step(torch.from_numpy(act).cuda())
@@ -113,6 +115,7 @@ def _run(orc, capsys, n, level, steps, warm, seed=42):
         assert d_g == orc.last_dropped, (t, d_g, orc.last_dropped)
         dropped += d_g
         resets += int((t_c | tr_c).sum())
+        truncs += int(tr_c.sum())
         contacts += int((st["contact_mask"] != 0).any(0).sum())
         with capsys.disabled():
             print(f"[exact n={n} level={level} warm={warm}] step {t}: {nbad} of {n} envs mismatched "
@@ -122,7 +125,7 @@ def _run(orc, capsys, n, level, steps, warm, seed=42):
             "\n".join(f"  {k}: {len(v)} envs" for k, v in bad.items() if len(v) and k in ("terminated", "truncated",
                                                                                           "obs", "reward"))
     env.close()
-    return resets, contacts, dropped
+    return resets, contacts, dropped, truncs
 
 
 @pytest.mark.parametrize("n,level,steps,warm", [
@@ -134,10 +137,22 @@ def _run(orc, capsys, n, level, steps, warm, seed=42):
     (1024, 0, 400, 0),      # long horizon: 400 consecutive steps, every env through falls and resets
 ])
 def test_trajectory_bit_exact(orc, capsys, n, level, steps, warm):
-    resets, contacts, dropped = _run(orc, capsys, n, level, steps, warm)
+    resets, contacts, dropped, _ = _run(orc, capsys, n, level, steps, warm)
     if n >= 4096:
         assert contacts > 0, "no env ever touched a stone: the trajectory did not exercise the contact path"
     if n == 32768 and warm:
         assert dropped > 0, "the C3 warm trajectory never hit the constraint budget: the drop count is untested"
     if warm:
         assert resets > 0, "no env reset during the compared steps"
+
+
+@pytest.mark.parametrize("n,level", [(4096, 0), (32768, 9)])
+def test_time_out_path_bit_exact(orc, capsys, n, level):
+    """Full steps (physics + task) across the 899-step time-out (allsteps_env.py:399 with direct_rl_env.py:248-250, truncated =
+    episode_length_buf >= max_episode_length - 1): episode counters preset to 890..898 after a warm-up,
+    then 12 steps in lock-step with the oracle -- every env that has not fallen is truncated and reset
+    inside the window (the random-action trajectories above fall long before 899 steps)."""
+    resets, contacts, dropped, truncs = _run(orc, capsys, n, level, 12, 60, near_timeout=True)
+    assert truncs > 0, "no time-out inside the window"
+    with capsys.disabled():
+        print(f"[time-out n={n}] {truncs} time-outs, {resets} resets, {dropped} contacts dropped in 12 steps")
