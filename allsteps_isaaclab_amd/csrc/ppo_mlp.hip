@@ -242,7 +242,8 @@ __device__ __forceinline__ void mma_rows(const uint16_t* X, const typename Lp<DT
 #define PPO_FWD_SINGLE_W 0
 #endif
 #ifndef PPO_FWD_DBG
-#define PPO_FWD_DBG 0  // timing-only builds (scripts/fwd_dbg.sh): 2 no exp, 4 no stores, 16 no MFMA, 32 no ELU / convert
+#define PPO_FWD_DBG 0  // timing-only builds (scripts/fwd_dbg.sh): 2 no exp, 4 no stores, 16 no MFMA, 32 no ELU / convert,
+                       // 64 no loss block, 128 no heads
 #endif
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -533,7 +534,7 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     // ---- heads: wave w < 4 takes N-tile w; out = 16-bit(acc + 16-bit(bh)) as under autocast.  With the
     // fused losses (LA > 0) the values also go to a table of the block's rows at the head of X0 (free: layer
     // 5 has read it), the losses' input
-    if (wave < 4 && a.head) {
+    if (wave < 4 && a.head && !(PPO_FWD_DBG & 128)) {
         f32x16 hacc[4];
         mma_rows<DT, 16, 1>(X1, whf, hacc, wave, j, h);
         const int rl = 32 * wave + j, row = row0 + rl;
@@ -548,7 +549,7 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     if constexpr (LA > 0) {
         // the losses' per-row table in X1 (the heads' MFMAs have read it)
         __syncthreads();
-        ppo_detail::loss_block<LA, kFThreads>(p, blockIdx.x, reinterpret_cast<float*>(X1), lin);
+        if (!(PPO_FWD_DBG & 64)) ppo_detail::loss_block<LA, kFThreads>(p, blockIdx.x, reinterpret_cast<float*>(X1), lin);
     }
 }
 
@@ -556,7 +557,7 @@ template <int DT, int LA>
 __global__ void __launch_bounds__(kFThreads, 1) k_mlp_fwd(ppo_mlp_fwd_t a) {
     // training stores layers 1..5 for the backward (all five pointers set); the rollout form stores none
     if constexpr (LA > 0) {
-        mlp_fwd_body<DT, true, LA>(a);
+        mlp_fwd_body<DT, !(PPO_FWD_DBG & 4), LA>(a);
     } else {
         if (a.h[0] && !(PPO_FWD_DBG & 4))
             mlp_fwd_body<DT, true, 0>(a);
