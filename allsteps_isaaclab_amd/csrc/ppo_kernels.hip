@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(kNormCols * kNormRowThreads) k_obs_normalize(
 
 template <int A>
 __global__ void __launch_bounds__(ppo_detail::kLossThreads) k_loss_grad(ppo_detail::LossRowArgs p) {
-    __shared__ float s_red[ppo_detail::kLossRows * ppo_detail::loss_rp(A)];
+    __shared__ float s_red[ppo_detail::loss_lds_floats(A)];
     ppo_detail::loss_block<A, ppo_detail::kLossThreads>(p, blockIdx.x, s_red);
 }
 

@@ -78,6 +78,11 @@ constexpr int kLossRows = 128;                         // rows per block
 constexpr int kLossThreads = kLossRows * kLossLanes;   // 1024 (the standalone kernel: one pass)
 constexpr float kLog2PiL = 1.8378770664093453f;
 __host__ __device__ constexpr int loss_rp(int A) { return (2 * A + 1 + PPO_LOSS_NSTAT) | 1; }  // LDS row pitch
+constexpr int kLossColGroups = 8;  // the column sums: 8 row groups of 16, then the 8 group sums in order
+// LDS floats loss_block needs: the per-row table + the group sums
+__host__ __device__ constexpr int loss_lds_floats(int A) {
+    return kLossRows * loss_rp(A) + kLossColGroups * (2 * A + 1 + PPO_LOSS_NSTAT);
+}
 
 // sum over the eight lanes of a row (xor 1, xor 2 by quad permutes, then the mirrored half-row): the same
 // two operands meet on every lane, so all eight hold the bit-identical sum
@@ -280,18 +285,32 @@ __device__ void loss_block(const LossRowArgs& p, int blk, float* __restrict__ s_
     }
     }  // pass
     __syncthreads();
-    // block partials: value k summed over the block's rows in a fixed order (four chains); ppo_loss_finalize
-    // sums them over the blocks.  (Round 5 measured the finalize folded into this kernel's last block --
-    // sc1 hand-off, relaxed agent counter -- at 16.9 us against 11.5 us for the two launches: each block's
-    // store drain and counter round trip sit on the kernel's tail, scripts/loss_bench.py.)
-    if (tid < NV) {
-        float t[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-        for (int rr = 0; rr < kLossRows; rr += 4) {
+    // block partials: value k summed over the block's rows in a fixed order -- eight groups of 16 rows on
+    // 8 x NV threads (two chains each), then the eight group sums in group order (one 48-thread pass over
+    // all 128 rows left seven of the forward's eight waves idle); ppo_loss_finalize sums them over the
+    // blocks.  (Round 5 measured the finalize folded into this kernel's last block -- sc1 hand-off, relaxed
+    // agent counter -- at 16.9 us against 11.5 us for the two launches: each block's store drain and
+    // counter round trip sit on the kernel's tail, scripts/loss_bench.py.)
+    constexpr int kRG = kLossRows / kLossColGroups;
+    static_assert(NT >= kLossColGroups * NV, "one thread per (group, value)");
+    float* s_grp = s_red + kLossRows * RP;
+    if (tid < kLossColGroups * NV) {
+        const int c = tid % NV, gi = tid / NV;
+        const float* col = s_red + gi * kRG * RP + c;
+        float t0 = 0.f, t1 = 0.f;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) t[u] += s_red[(rr + u) * RP + tid];
+        for (int rr = 0; rr < kRG; rr += 2) {
+            t0 += col[rr * RP];
+            t1 += col[(rr + 1) * RP];
         }
-        p.partials[int64_t(blk) * NV + tid] = (t[0] + t[1]) + (t[2] + t[3]);
+        s_grp[gi * NV + c] = t0 + t1;
+    }
+    __syncthreads();
+    if (tid < NV) {
+        float t = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < kLossColGroups; ++gi) t += s_grp[gi * NV + tid];
+        p.partials[int64_t(blk) * NV + tid] = t;
     }
 }
 

@@ -528,6 +528,7 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
         p.lp_dtype = DT;
         p.partials = a.loss.partials;
         static_assert(kFRows == ppo_detail::kLossRows, "one loss block per workgroup");
+        static_assert(ppo_detail::loss_lds_floats(LA) * 4 <= kXBytes, "the loss tables fit the free image");
         ppo_detail::loss_prefetch<LA, kFThreads>(p, blockIdx.x, lin);
     }
     __syncthreads();
