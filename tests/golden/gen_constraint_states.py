@@ -1,7 +1,13 @@
 """Generate tests/golden/constraint_states.npz: walker states that exercise the constraint budget.
 
 The fixtures are states of OUR oracle (not reference outputs -- PhysX is absent), found
-by search and committed so that the CPU and GPU constraint tests start from the same bytes:
+by a seeded search and committed so that the CPU and GPU constraint tests start from the same bytes.
+The committed bytes ARE the fixture: the search was run on the round-2 oracle, and the oracle's
+arithmetic has changed since (round 4: FK by pointer jumping), so a regeneration on a later oracle
+finds other states -- equally valid ones, meeting the same acceptance predicates below.  Those
+predicates (`self_arm_ok`, `crowded_ok`, `fallen_ok`) are what the fixture promises; they are checked
+on the committed states on HEAD's oracle by tests/test_oracle_constraints.py::test_fixture_claims, and
+`python tests/golden/gen_constraint_states.py --check` runs the same check.
 
   self_arm    -- the robot high in the air (no stone within reach), right arm folded so that the
                  forearm / hand penetrates the torso: exactly one contact, a self-contact between
@@ -13,7 +19,8 @@ by search and committed so that the CPU and GPU constraint tests start from the 
   fallen      -- a natural rollout state with more contacts than the budget AND several active
                  joint-limit rows (all of which must be kept).
 
-    python tests/golden/gen_constraint_states.py
+    python tests/golden/gen_constraint_states.py            # search and (re)write the fixture
+    python tests/golden/gen_constraint_states.py --check    # the committed states meet the predicates
 """
 
 from __future__ import annotations
@@ -46,6 +53,33 @@ def level0(st):
         st["stones"][3 * k + 2][:] = 0.0
 
 
+def self_arm_ok(orc, p) -> bool:
+    """Exactly one contact, a self-contact between the root link and the right forearm, penetrating."""
+    m = orc.m
+    elbow = m["cfg_dof_link"][m["dof_names"].index("right_elbow")]
+    return bool(p["ncontact"] == 1 and p["link2"][0] >= 0 and p["sep"][0] < -0.01
+                and {int(p["link"][0]), int(p["link2"][0])} == {0, elbow})
+
+
+def crowded_ok(p) -> bool:
+    """More contacts found than the budget keeps, and a kept foot contact on a higher-index stone than
+    some kept non-foot stone contact, pushing (lam_n > 0): the state in which a stone-major emission
+    order would have let other bodies crowd out the foot."""
+    if p["nfound"] <= p["ncap"]:
+        return False
+    feet = p["foot"] >= 0
+    others = ~feet & (p["stone"] >= 0)
+    if not feet.any() or not others.any():
+        return False
+    hi_foot = p["stone"][feet].max()
+    return bool(hi_foot > p["stone"][others].min() and (p["lam_n"][feet & (p["stone"] == hi_foot)] > 0).any())
+
+
+def fallen_ok(p) -> bool:
+    """More contacts found than the budget keeps AND at least three active joint-limit rows."""
+    return bool(p["nfound"] > p["ncap"] and p["nlim"] >= 3)
+
+
 def find_self_arm(orc) -> dict:
     m = orc.m
     names = m["dof_names"]
@@ -61,9 +95,7 @@ def find_self_arm(orc) -> dict:
             lo, hi = lim[nm]
             st["q"][names.index(nm), 0] = rng.uniform(lo + 0.05, hi - 0.05)
         st["root_pos"][:, 0] = [0.0, 0.0, 5.0]
-        p = orc.probe(st, 0)
-        if (p["ncontact"] == 1 and p["link2"][0] >= 0 and p["sep"][0] < -0.01
-                and {p["link"][0], p["link2"][0]} == {0, link_of["right_elbow"]}):
+        if self_arm_ok(orc, orc.probe(st, 0)):
             return snapshot(st, 0)
     raise RuntimeError("no self-contact pose found")
 
@@ -78,24 +110,39 @@ def find_rollout_states(orc, n=512, steps=400) -> tuple[dict, dict]:
         orc.env_step(st, rng.uniform(-1, 1, (n, 21)).astype(np.float32))
         for e in range(n):
             p = orc.probe(st, e)
-            if p["nfound"] <= p["ncap"]:
-                continue
-            feet = p["foot"] >= 0
-            if crowded is None and feet.any() and (~feet & (p["stone"] >= 0)).any():
-                hi_foot = p["stone"][feet].max()
-                lo_other = p["stone"][~feet & (p["stone"] >= 0)].min()
-                if hi_foot > lo_other and (p["lam_n"][feet & (p["stone"] == hi_foot)] > 0).any():
-                    crowded = snapshot(st, e)
-            if fallen is None and p["nlim"] >= 3:
+            if crowded is None and crowded_ok(p):
+                crowded = snapshot(st, e)
+            if fallen is None and fallen_ok(p):
                 fallen = snapshot(st, e)
         if crowded is not None and fallen is not None:
             return crowded, fallen
     raise RuntimeError(f"not found: crowded {crowded is not None}, fallen {fallen is not None}")
 
 
+def check(orc, path=None) -> dict:
+    """Each committed state against its acceptance predicate on this oracle: {name: bool}."""
+    z = np.load(path or os.path.join(HERE, "constraint_states.npz"), allow_pickle=False)
+    out = {}
+    for name, ok in (("self_arm", lambda p: self_arm_ok(orc, p)), ("crowded", crowded_ok), ("fallen", fallen_ok)):
+        st = orc.state(1)
+        for k in z.files:
+            if k.startswith(name + "/"):
+                a, v = st[k.split("/", 1)[1]], z[k]
+                if a.ndim > 1:
+                    a[:, 0] = v
+                else:
+                    a[0] = v[0]
+        out[name] = ok(orc.probe(st, 0))
+    return out
+
+
 def main():
     O.build()
     orc = O.Oracle()
+    if "--check" in sys.argv:
+        res = check(orc)
+        print(res)
+        sys.exit(0 if all(res.values()) else 1)
     out = {}
     for name, snap in [("self_arm", find_self_arm(orc)), *zip(("crowded", "fallen"), find_rollout_states(orc))]:
         for k, v in snap.items():

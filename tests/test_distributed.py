@@ -56,8 +56,12 @@ def _worker(rank: int, world: int, port: int, q):
         dist.destroy_process_group()
 
 
-def test_rollout_gather_world2():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_rollout_gather_world2(world):
+    """Both layouts at world 2, 3 (odd) and 4: every rank receives the rank-major
+    concatenation, i.e. global env order, with rank r's shard at [r N, (r+1) N); receive buffers are
+    reused across gathers."""
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -78,8 +82,9 @@ def test_rollout_gather_world2():
             assert res[k].dtype == v.dtype and res[k].shape == v.shape, k
             torch.testing.assert_close(res[k], v, rtol=0, atol=0)
         # global env ids come out in order: rank r's shard is [r N, (r+1) N)
-        assert torch.equal(res["env_ids"][0], torch.arange(12))
-        assert mean == pytest.approx((1 + 4) / 2)
+        assert torch.equal(res["env_ids"][0], torch.arange(6 * world))
+        assert torch.equal(res["flat/env_ids"][::4], torch.arange(6 * world))  # env-major rows, H = 4 each
+        assert mean == pytest.approx(sum(1 + 3 * r for r in range(world)) / world)
 
 
 def test_single_process_gather_is_identity():

@@ -289,23 +289,109 @@ def _dist_worker(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("mode", ["allreduce", "allgather"])
-def test_multi_gpu_modes_keep_ranks_identical(mode):
+def test_multi_gpu_modes_keep_ranks_identical(mode, world):
+    """Both exchange modes at world 2 and 3 (odd): parameters and LR identical on
+    every rank after 3 epochs, the allgather batch / minibatch scaled by the world size, frames counting
+    every rank's env steps (the allreduce step's arithmetic: test_allreduce_minibatch_step_equals_mean_gradient_step)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, p0, lr0, bs0, mb0, fr0), (_, p1, lr1, bs1, mb1, fr1) = res
-    assert np.array_equal(p0, p1), f"{mode}: parameters diverged across ranks"
-    assert lr0 == lr1
+    _, p0, lr0, bs0, mb0, fr0 = res[0]
+    for rank, p1, lr1, bs1, mb1, fr1 in res[1:]:
+        assert np.array_equal(p0, p1), f"{mode}: rank {rank} diverged from rank 0"
+        assert (lr1, bs1, mb1, fr1) == (lr0, bs0, mb0, fr0)
     if mode == "allgather":
-        assert (bs0, mb0) == (2 * 16 * 16, 2 * 16 * 4)  # global batch, world-scaled minibatch
+        assert (bs0, mb0) == (world * 16 * 16, world * 16 * 4)  # global batch, world-scaled minibatch
     else:
         assert (bs0, mb0) == (16 * 16, 16 * 4)
-    assert fr0 == 3 * 2 * 16 * 16  # frames count every rank's env steps
+    assert fr0 == 3 * world * 16 * 16  # frames count every rank's env steps
+
+
+# ------------------------------ the allreduce exchange vs a single-process step on the mean gradient
+
+def _mb_batch(rank: int, B: int, device: str = "cpu") -> dict:
+    g = torch.Generator(device=device).manual_seed(500 + rank)
+    r = lambda *s: torch.randn(*s, device=device, generator=g)  # noqa: E731
+    return {"obses": r(B, 5) * 2 + 0.5, "actions": r(B, 2), "neglogpacs": r(B).abs() * 2 + 3,
+            "values": r(B, 1), "returns": r(B, 1) * 2, "mus": r(B, 2) * 0.3,
+            "sigmas": torch.exp(r(B, 2) * 0.1), "dones": torch.zeros(B, dtype=torch.uint8, device=device)}
+
+
+def _mb_agent(multi_gpu: bool):
+    params = agent_params(16, multi_gpu=multi_gpu, multi_gpu_mode="allreduce", minibatch_size=16 * 16)
+    params["config"]["vec_env"] = ToyReachEnv(16, seed=0)
+    torch.manual_seed(3)  # identical initial parameters on every rank and in the reference
+    ag = A.A2CAgent("run", params)
+    ag.init_tensors()
+    ag.model.train()
+    return ag
+
+
+def _allreduce_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ag = _mb_agent(True)
+        ag.prepare_dataset(_mb_batch(rank, ag.batch_size))
+        out = ag.calc_gradients(ag.dataset[0])  # backward, [grads | kl] all-reduce (mean), clip, Adam
+        q.put((rank, ag.flat.params.detach().numpy().copy(), float(out[3]), ag.flat.grads.detach().numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allreduce_minibatch_step_equals_mean_gradient_step(world):
+    """one all-reduced minibatch step on W ranks (gloo; identical parameters,
+    different minibatches) equals a single-process step whose [grads | kl] bucket is the mean of the W
+    ranks' own buckets -- the clip (grad_norm 1.0, on the averaged gradient) and Adam included.  Two
+    ranks applying the same WRONG gradient (an exchange at the wrong point, a bucket that misses a
+    parameter, the KL left un-averaged) would pass "ranks stay identical" but fail this."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_allreduce_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    class _Stop(Exception):
+        pass
+
+    # the single-process statement: each rank's own bucket (backward only), then one step on their mean
+    buckets = []
+    for r in range(world):
+        ag = _mb_agent(False)
+        ag.prepare_dataset(_mb_batch(r, ag.batch_size))
+
+        def grab(ag=ag):
+            buckets.append(ag._bucket.clone())
+            raise _Stop
+
+        ag._exchange_grads = grab
+        with pytest.raises(_Stop):
+            ag.calc_gradients(ag.dataset[0])
+    mean = torch.stack(buckets).sum(0) / world
+    ref = _mb_agent(False)
+    ref.prepare_dataset(_mb_batch(0, ref.batch_size))
+    ref._exchange_grads = lambda: ref._bucket.copy_(mean)
+    out = ref.calc_gradients(ref.dataset[0])
+    p_ref = ref.flat.params.detach().numpy()
+    assert float(torch.linalg.vector_norm(mean[:-1])) > ref.grad_norm  # the clip is active in this step
+    for rank, p, kl, grads in res:
+        assert np.array_equal(p, res[0][1]), f"rank {rank} diverged"
+        np.testing.assert_allclose(p, p_ref, rtol=1e-6, atol=1e-7, err_msg=f"rank {rank} vs mean-gradient step")
+        assert kl == pytest.approx(float(out[3]), rel=1e-6)  # the KL slot is averaged with the gradients
+        np.testing.assert_allclose(grads, ref.flat.grads.detach().numpy(), rtol=1e-6, atol=1e-9)

@@ -138,3 +138,22 @@ def test_dropped_contacts_counted(orc, name):
     st3["next"][:] = 2
     orc.env_step(st3, act)
     assert orc.last_dropped == drop
+
+
+def test_fixture_claims(orc):
+    """the committed constraint states are a search result of an earlier oracle
+    (tests/golden/gen_constraint_states.py cannot regenerate the same bytes on HEAD's oracle), so the
+    generator's acceptance predicates -- the promises of its docstring -- are checked here on the
+    committed bytes with HEAD's oracle: the arm penetrates the torso as the only contact; the crowded
+    state finds more contacts than the budget and keeps a pushing foot contact on a higher stone than a
+    kept non-foot contact; the fallen state finds more contacts than the budget with >= 3 limit rows
+    (every one kept: test_budget_keeps_every_limit_row)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import gen_constraint_states as G
+
+    assert G.check(orc) == {"self_arm": True, "crowded": True, "fallen": True}
+    p = orc.probe(_state(orc, "crowded"))
+    assert p["ncontact"] == p["ncap"] and p["nfound"] > p["ncap"]  # contacts beyond the budget are cut
