@@ -105,6 +105,12 @@ class RolloutGather:
     ``all_gather_into_tensor`` (RCCL) -- no send-side packing and no copy after the collective; the
     payloads are MB-sized, so the per-collective latency is negligible against the per-link
     bandwidth.  For another env axis ([H, N, ...]) the parts are concatenated along it (one copy).
+
+    The returned tensors are this object's cached receive buffers (or views of them), keyed by
+    (key, dtype, shape, device): they stay valid until the next ``gather`` with the same keys and shapes,
+    which overwrites them in place.  A caller that keeps an earlier result across gathers passes
+    ``copy=True`` (fresh tensors) or clones what it keeps; the trainer consumes each gathered batch
+    (prepare_dataset copies it into the update's static buffers) before the next epoch's gather.
     """
 
     def __init__(self, group=None, env_axis: int = 0):
@@ -124,10 +130,10 @@ class RolloutGather:
             self._recv[k] = buf
         return buf
 
-    def gather(self, tensors: dict[str, torch.Tensor]) -> dict[str, torch.Tensor]:
+    def gather(self, tensors: dict[str, torch.Tensor], copy: bool = False) -> dict[str, torch.Tensor]:
         world = self._world()
         if world == 1:
-            return dict(tensors)
+            return {k: v.clone() for k, v in tensors.items()} if copy else dict(tensors)
         backend = dist.get_backend(self.group)
         out: dict[str, torch.Tensor] = {}
         for k, t in tensors.items():
@@ -141,4 +147,6 @@ class RolloutGather:
             else:  # gloo (CPU tests, the shared-GPU rehearsal): views of the same buffer, no extra copy
                 dist.all_gather(list(wire_buf.chunk(world)), wire_src, group=self.group)
             out[k] = buf if self.env_axis == 0 else buf.movedim(0, self.env_axis)
+            if copy:
+                out[k] = out[k].clone()
         return out

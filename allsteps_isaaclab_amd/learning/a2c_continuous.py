@@ -712,7 +712,11 @@ class A2CAgent:
         f = self.fused
         f.begin_epoch()
         n_mb = len(self.dataset)
-        exchange = self.multi_gpu and self.multi_gpu_mode == "allreduce" and self.world_size > 1
+        # `exchange_schedule` (agent config, diagnostic): run the allreduce mode's schedule -- per-minibatch
+        # graphs A / exchange / B, the separate norm pass -- at world 1 too, so its one-GPU cost is measured
+        # (scripts/price_exchange.sh); the exchange itself is then a no-op
+        exchange = (self.multi_gpu and self.multi_gpu_mode == "allreduce" and self.world_size > 1) or bool(
+            self.config.get("exchange_schedule", False))
         for ep in range(self.mini_epochs_num):
             rms_train = self.normalize_input and ep == 0
             if not exchange:  # nothing between A and B: the whole mini-epoch is one graph

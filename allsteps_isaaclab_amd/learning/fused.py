@@ -256,7 +256,8 @@ class FusedPPOUpdate:
         # one gradient pass, k_sqnorm, fewer per minibatch); `fuse_norm` False keeps the separate pass
         self.fuse_norm = bool(getattr(agent, "config", {}).get("fuse_norm", True)) and not (
             getattr(agent, "multi_gpu", False) and getattr(agent, "multi_gpu_mode", "") == "allreduce"
-            and getattr(agent, "world_size", 1) > 1)
+            and getattr(agent, "world_size", 1) > 1) and not bool(getattr(agent, "config", {}).get(
+                "exchange_schedule", False))
         self.red_norm = torch.empty(2 * 4096, device=dev)
         self._red_nblk = C.c_int32(0)
         # ppo_opt_snap_t (lr, step, scale): taken by the norm launch, read by ppo_adam_step, whose first

@@ -203,6 +203,9 @@ def cpu_baseline(num_envs: int, level: int, threads: int | None, warm_steps: int
         total_s += el
     med = float(np.median(rates))
     return {"value": round(med, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "kind_detail": "bit-exact serial restatement of the HIP step (oracle/: the kernel's lane trees, "
+                           "MFMA fmaf chains and two-partial sums restated serially, -ffp-contract=off), not a "
+                           "tuned CPU simulator; the reference's PhysX CPU pipeline cannot run here",
             "samples": [round(r, 1) for r in rates], "spread": round((max(rates) - min(rates)) / med, 4),
             "threads_from": why, "host": host,
             "sample": f"oracle/ C port, {n} envs, {samples} samples, {total_steps} steps in {total_s:.2f} s wall "
@@ -341,6 +344,29 @@ def main():
     # clocking up from idle (measured: the 20-step driver window 0.1428 ms/step cold, 0.1317 warm,
     # scripts/window_clock.py).  Steps of the env itself, BEFORE env.reset(), keep the part afterwards --
     # reset, W warm-up steps, K timed steps -- exactly the protocol; they are reported on the line.
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    # the protocol without the pre-heat, first, on the GPU as it comes (benchmark_non_rl.py:145-166 starts
+    # timing right after env.reset()): reported beside the line's value, never as it
+    cold = None
+    if args.preheat_ms > 0:
+        env.reset()
+        for t in range(W):
+            env.step(actions[K + t])
+        env._native.profile(0)
+        barrier()
+        t0 = time.perf_counter()
+        for t in range(K):
+            env.step(actions[t])
+        barrier()
+        cold = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([cold], device=device if backend == "nccl" else "cpu", dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            cold = float(tt.item())
     preheat_steps = 0
     if args.preheat_ms > 0:
         env.reset()
@@ -356,11 +382,6 @@ def main():
     torch.cuda.synchronize(device)
     env._native.profile(0)  # no HIP events inside the timed loop (each adds a launch gap to its step)
     s_start = env.get_state()  # the timed window's start state: replayed below for the kernel timings
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(device)
 
     barrier()
     t0 = time.perf_counter()
@@ -450,6 +471,11 @@ def main():
             "gpu_preheat": {"ms": args.preheat_ms, "env_steps": preheat_steps,
                             "what": "untimed env steps before env.reset() (GPU clocks to steady state); then reset, "
                                     "W warm-up steps, K timed steps"},
+            "no_preheat": None if cold is None else {
+                "value": round(n * world * K / cold, 1), "ms_per_step": round(cold / K * 1e3, 4),
+                "what": "the same protocol (reset, W warm-up steps, K timed steps, same actions) run first, before "
+                        "the pre-heat, on the GPU as it comes: the reference protocol's number "
+                        "(benchmark_non_rl.py:145-166); beside `value`, never as it"},
             "contacts_dropped": {"total": dropped, "per_step": round(dropped / K, 2),
                                  "per_env_step": round(dropped / (K * n), 6),
                                  "method": "as_step_counters word 3 summed over the timed window's K steps "
@@ -467,6 +493,12 @@ def main():
             line["train"] = train
         elif "error" in train:
             print(f"bench rank {rank}: train leg failed: {train['error']}", file=sys.stderr, flush=True)
+        if world > 1:  # both exchange modes on the line: the other one beside the default
+            other = "allgather" if args.multi_gpu_mode == "allreduce" else "allreduce"
+            train2 = train_leg(argparse.Namespace(**{**vars(args), "multi_gpu_mode": other}), world, rank, backend,
+                               device)
+            if rank == 0:
+                line["train_" + other] = train2
     if rank == 0:
         if world == 1 and not args.no_c5:
             sys.path.insert(0, os.path.join(ROOT, "scripts"))

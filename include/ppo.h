@@ -242,8 +242,10 @@ int ppo_mlp_backward(const ppo_mlp_bwd_t* args_host, void* stream);
  * activations), no bias column.  hin[l]: rows x hin_stride[l] lp; part[l]: splits[l] x nout x hin_stride[l]
  * fp32 (columns past kin[l] (+1) untouched).  Split s of job l covers rows
  * [rows*s/splits[l], rows*(s+1)/splits[l]).  A trunk split is two workgroups (output features 0..127 and
- * 128..255) placed on one XCD so that the layer input they both stream is fetched once into its L2;
- * the total count of trunk splits must be a multiple of 8.  The partials are summed by
+ * 128..255), placed 8 block indices apart so that, in every full group of 8 pairs, the two halves run on
+ * one XCD and the layer input they both stream is fetched once into its L2 (a performance placement,
+ * not a requirement: a last group of fewer than 8 pairs -- any split total that is not a multiple of 8,
+ * e.g. small minibatches -- is handled and only loses the co-location).  The partials are summed by
  * ppo_reduce_rows. */
 /* ppo_loss_finalize's arguments, for running that work as a side job (below) */
 typedef struct {

@@ -46,6 +46,12 @@ def _worker(rank: int, world: int, port: int, q):
         for it in range(2):  # second call reuses the cached receive buffers
             res = gather.gather(_rank_rollout(rank))
             flat = flat_gather.gather({k: _flat(v) for k, v in _rank_rollout(rank).items()})
+        # the results are the cached buffers: a later gather overwrites them in place; copy=True does not
+        kept = flat_gather.gather({"obs": _flat(_rank_rollout(rank)["obs"])}, copy=True)["obs"]
+        again = flat_gather.gather({"obs": torch.zeros_like(_flat(_rank_rollout(rank)["obs"]))})["obs"]
+        assert again.data_ptr() == flat["obs"].data_ptr() and float(flat["obs"].abs().sum()) == 0.0
+        assert float(kept.abs().sum()) > 0.0
+        flat["obs"] = kept
         res.update({"flat/" + k: v for k, v in flat.items()})
         fake_env = types.SimpleNamespace(curr_target_index=torch.full((6,), 1 + 3 * rank, dtype=torch.int32))
         mean = global_curriculum_mean(fake_env)

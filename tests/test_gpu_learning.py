@@ -1001,3 +1001,90 @@ def test_training_is_deterministic(tmp_path):
     assert torch.equal(out[0][0], out[1][0])
     for key in ("q", "qd", "root_pos", "idx", "episode"):
         assert torch.equal(out[0][1][key], out[1][1][key]), key
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mp_dtype,tol", [("float16", 4e-3), ("bfloat16", 3.5e-2)])  # r06c measured: 9.4e-4 / 8.9e-3
+def test_rollout_heads_lowp_bounded_and_equal_to_training_forward(tmp_path, mp_dtype, tol):
+    """with mixed_precision the rollout policy runs the same 16-bit trunk AND heads as
+    the training forward (16-bit layer-5 activations and head weights, fp32 accumulation, a 16-bit
+    rounded output: autocast's Linear).  rl_games' play_steps runs its policy in fp32 (no autocast), so
+    the rollout's mu / value deviate from the fp32 policy by the 16-bit rounding: bounded here against the
+    fp32 torch forward of the same parameters (max error over 2048 rows relative to the largest entry;
+    the measured figure is printed).  In exchange the rollout's mu equals the training forward's mu bit
+    for bit (the same kernel, the same rounding points), so the PPO ratio of an unchanged policy is
+    exactly 1 -- under rl_games' fp32 rollout / fp16 training it carries the 16-bit noise instead."""
+    _, fus = _agents_and_batch(256, mixed=True, tmp=tmp_path, mp_dtype=mp_dtype)
+    f = fus.fused
+    n = f.mb  # one minibatch of rows: the training forward's minibatch 0 is the same rows
+    f.init_rollout(n, seed=1)
+    obs = fus.dataset.values_dict["obs"][:n].contiguous()
+    out = {k: torch.empty(n, 21, device="cuda:0") for k in ("actions", "mus", "sigmas")}
+    out["neglogpacs"] = torch.empty(n, device="cuda:0")
+    out["values"] = torch.empty(n, 1, device="cuda:0")
+    f.policy_act(obs, out)
+    v_norm = f.head_r[:, 21:].clone()
+    fus.model.eval()
+    with torch.no_grad():
+        ref = fus.model({"is_train": False, "prev_actions": None, "obs": obs})  # fp32 torch forward
+        net = fus.model.a2c_network
+        x = fus.model.norm_obs(obs)
+        h = x
+        for m in net.actor_mlp:
+            h = m(h)
+        v_ref = net.value(h)  # normalised value head (what the training loss reads)
+    emu = ((out["mus"] - ref["mus"]).abs().max() / ref["mus"].abs().max()).item()
+    ev = ((out["values"] - ref["values"]).abs().max() / ref["values"].abs().max()).item()
+    evn = ((v_norm - v_ref).abs().max() / v_ref.abs().max()).item()
+    print(f"{mp_dtype}: rollout vs fp32 policy, max rel. error mu {emu:.2e}, value {ev:.2e}, normalised value {evn:.2e}")
+    assert emu < tol and ev < tol and evn < tol
+    # the training forward on the same rows: the same mu and value bits
+    f.begin_epoch()
+    f.use_graphs = False
+    f.fuse_norm = False
+    f.step_a(False)
+    torch.cuda.synchronize()
+    assert torch.equal(f.head[:, :21], out["mus"])
+    assert torch.equal(f.head[:, 21:], v_norm)
+
+
+@pytest.mark.gpu
+def test_loss_head_gradient_vs_fp32_autograd(tmp_path):
+    """the loss block multiplies by a correctly rounded 1/sigma where torch divides by
+    sigma, so d loss / d [mu | value] (the head gradient that seeds the whole backward) and the loss
+    statistics are within a few ulp of torch autograd, not bit-equal.  Pinned here on the fp32 path
+    (ppo_loss_grad's fp32 dhead) against autograd of rl_games' loss (actor_loss, critic_loss, bound_loss,
+    entropy) through the same head values; the measured error is printed and the bound is ~4x it."""
+    from allsteps_isaaclab_amd.learning import a2c_continuous as AC
+    from allsteps_isaaclab_amd.learning.models import neglogp
+
+    _, fus = _agents_and_batch(256, mixed=False, tmp=tmp_path)
+    f = fus.fused
+    f.use_graphs = False
+    f.fuse_norm = False
+    mb = {k: v.clone() for k, v in fus.dataset[0].items() if torch.is_tensor(v)}
+    f.begin_epoch()
+    f.step_a(False)
+    torch.cuda.synchronize()
+    head, dhead = f.head.clone(), f.dhead.clone()
+    A, B = 21, head.shape[0]
+    mu = head[:, :A].clone().requires_grad_(True)
+    value = head[:, A:].clone().requires_grad_(True)
+    logstd = fus.model.a2c_network.sigma.detach().clone()
+    sigma = torch.exp(logstd).expand_as(mu)
+    nlp = neglogp(mb["actions"], mu, sigma, logstd.expand_as(mu))
+    ent = (0.5 + 0.5 * math.log(2 * math.pi) + torch.log(sigma)).sum(dim=-1)
+    a_loss = AC.actor_loss(mb["old_logp_actions"], nlp, mb["advantages"], fus.ppo, fus.e_clip).mean()
+    c_loss = AC.critic_loss(mb["old_values"], value, fus.e_clip, mb["returns"], fus.clip_value).mean()
+    b_loss = AC.bound_loss(mu).mean() if fus.bound_loss_type == "bound" else torch.zeros((), device=mu.device)
+    loss = (a_loss + 0.5 * c_loss * fus.critic_coef - ent.mean() * fus.entropy_coef
+            + b_loss * float(fus.bounds_loss_coef or 0.0))
+    loss.backward()
+    ref = torch.cat([mu.grad, value.grad], dim=1)
+    err = ((dhead - ref).abs().max() / ref.abs().max()).item()
+    st = f.stats[0]
+    e_a = abs(st[0].item() - a_loss.item()) / max(abs(a_loss.item()), 1e-12)
+    e_c = abs(st[1].item() - c_loss.item()) / max(abs(c_loss.item()), 1e-12)
+    print(f"dhead max rel. error {err:.2e} (B = {B}); a_loss {e_a:.2e}, c_loss {e_c:.2e}")
+    assert err < 2.5e-6, err  # r06c measured 6.5e-7 (B = 2048)
+    assert e_a < 2e-6 and e_c < 2e-6  # r06c measured 4.0e-7 / 0
