@@ -18,19 +18,39 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 
 MAXL, MAXG, MAXSP = 32, 32, 256
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 EXPORTED_SYMBOLS = [
     "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
     "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask", "as_set_graph_safe",
     "as_profile_sampled", "as_hbm_copy", "as_set_actuator", "as_set_quad_task", "as_quad_step", "as_quad_reset_all",
-    "as_build_id", "as_step_counters_host",
+    "as_build_id", "as_step_counters_host", "as_body_state",
 ]
+MAXB = 32  # AS_MAX_BODIES
+BODY_STATE_ROWS = 16  # AS_BODY_STATE_ROWS: pos 3 | quat 4 | frame lin vel 3 | ang vel 3 | COM lin vel 3
 
 
 class NativeError(RuntimeError):
     pass
+
+
+class AsBodyTable(C.Structure):
+    """as_body_table_t (include/allsteps.h): the model's bodies for as_body_state."""
+    _fields_ = [("num_bodies", C.c_int32), ("link", C.c_int32 * MAXB), ("offset_pos", (C.c_float * 3) * MAXB),
+                ("offset_quat", (C.c_float * 4) * MAXB), ("com", (C.c_float * 3) * MAXB)]
+
+
+def make_body_table(m: dict) -> AsBodyTable:
+    t = AsBodyTable()
+    nb = int(m["num_bodies"])
+    t.num_bodies = nb
+    for k in range(nb):
+        t.link[k] = int(m["body_link"][k])
+        t.offset_pos[k][:] = [float(x) for x in m["body_offset_pos"][k]]
+        t.offset_quat[k][:] = [float(x) for x in m["body_offset_quat"][k]]
+        t.com[k][:] = [float(x) for x in m["body_com"][k]]
+    return t
 
 
 class AsModel(C.Structure):
@@ -179,6 +199,7 @@ def load() -> C.CDLL:
     L.as_set_quad_task.argtypes = [V, V]
     L.as_quad_step.argtypes = [V, V, V, V, V, V, V]
     L.as_quad_reset_all.argtypes = [V, V, V]
+    L.as_body_state.argtypes = [V, V, V, V]
     L.as_last_error.restype = C.c_char_p
     L.as_build_id.restype = C.c_char_p
     for name in EXPORTED_SYMBOLS:
@@ -368,6 +389,10 @@ class NativeEnv:
 
     def physics_step(self, actions, stream=None):
         check(self.L.as_physics_step(self.h, actions.data_ptr(), stream), "as_physics_step")
+
+    def body_state(self, table: "AsBodyTable", out, stream=None):
+        """as_body_state: out [BODY_STATE_ROWS][num_bodies][n] fp32 on the device (ring-2 body views)."""
+        check(self.L.as_body_state(self.h, C.byref(table), out.data_ptr(), stream), "as_body_state")
 
     def set_actuator(self, mode: int, action_scale: float = 0.0, default_q=(), stiffness: float = 0.0,
                      damping: float = 0.0, saturation_effort: float = 0.0, effort_limit: float = 0.0,

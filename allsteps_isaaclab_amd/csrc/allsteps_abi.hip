@@ -452,6 +452,24 @@ int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* s
   return AS_OK;
 }
 
+int as_body_state(as_env_t* env, const as_body_table_t* bodies_host, float* out, void* stream) {
+  if (!env || !bodies_host || !out) return fail(AS_ERR_INVALID, "as_body_state: null argument");
+  const as_body_table_t& b = *bodies_host;
+  if (b.num_bodies < 1 || b.num_bodies > AS_MAX_BODIES)
+    return fail(AS_ERR_INVALID, "as_body_state: num_bodies out of range [1, AS_MAX_BODIES]");
+  for (int i = 0; i < b.num_bodies; ++i)
+    if (b.link[i] < 0 || b.link[i] >= env->host.model.num_links)
+      return fail(AS_ERR_INVALID, "as_body_state: body link out of range");
+  as::BodyArgs a{};
+  a.consts = env->consts_dev;
+  a.st = env->st;
+  a.n = env->n;
+  a.out = out;
+  a.bodies = b;
+  HIP_TRY(as::launch_body_state(a, reinterpret_cast<hipStream_t>(stream)));
+  return AS_OK;
+}
+
 int as_set_graph_safe(as_env_t* env, int32_t on) {
   if (!env) return fail(AS_ERR_INVALID, "as_set_graph_safe: null handle");
   env->graph_safe = on != 0;

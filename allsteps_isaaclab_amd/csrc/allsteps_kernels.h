@@ -121,7 +121,18 @@ struct StonesArgs {
   int64_t env_offset;
 };
 
+// k_body_state (ring-2 views, as_body_state): the step kernel's FK of the current state, then every
+// body's pose and velocities
+struct BodyArgs {
+  const Consts* consts;
+  as_state_t st;
+  int32_t n;
+  float* out;                  // [AS_BODY_STATE_ROWS][nb][n]
+  as_body_table_t bodies;
+};
+
 bool step_supported_nv(int nv);
+hipError_t launch_body_state(const BodyArgs& a, hipStream_t stream);
 hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream);
 hipError_t launch_obs(const ObsArgs& a, hipStream_t stream);
 hipError_t launch_stones(const StonesArgs& a, hipStream_t stream);

@@ -2556,6 +2556,131 @@ hipError_t launch_obs(const ObsArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// Ring-2 views (as_body_state, include/allsteps.h): the ArticulationData body poses and velocities of
+// every model body, from the state as it stands.  Off the hot path (launched when a view is read); the
+// launch shape is k_step's (two envs per one-wave workgroup) so the FK is k_step's own fk<false>.
+__device__ void mat_to_quat(const float* R, float* q) {  // (w, x, y, z), w >= 0
+  const float t = R[0] + R[4] + R[8];
+  float w, x, y, z;
+  if (t > 0.f) {
+    const float r = 2.f * sqrtf(t + 1.f);
+    w = 0.25f * r; x = (R[7] - R[5]) / r; y = (R[2] - R[6]) / r; z = (R[3] - R[1]) / r;
+  } else if (R[0] >= R[4] && R[0] >= R[8]) {
+    const float r = 2.f * sqrtf(1.f + R[0] - R[4] - R[8]);
+    w = (R[7] - R[5]) / r; x = 0.25f * r; y = (R[1] + R[3]) / r; z = (R[2] + R[6]) / r;
+  } else if (R[4] >= R[8]) {
+    const float r = 2.f * sqrtf(1.f + R[4] - R[0] - R[8]);
+    w = (R[2] - R[6]) / r; x = (R[1] + R[3]) / r; y = 0.25f * r; z = (R[5] + R[7]) / r;
+  } else {
+    const float r = 2.f * sqrtf(1.f + R[8] - R[0] - R[4]);
+    w = (R[3] - R[1]) / r; x = (R[2] + R[6]) / r; y = (R[5] + R[7]) / r; z = 0.25f * r;
+  }
+  const float sg = w < 0.f ? -1.f : 1.f, nn = sg / sqrtf(w * w + x * x + y * y + z * z);
+  q[0] = w * nn; q[1] = x * nn; q[2] = y * nn; q[3] = z * nn;
+}
+
+__global__ __launch_bounds__(kStepThreads) void k_body_state(BodyArgs P) {
+  __shared__ Smem sm;
+  const Consts& K = *(const Consts*)(CK*)P.consts;
+  const int el = threadIdx.x >> 5, lane = threadIdx.x & 31;
+  const int n = P.n;
+  const int e_raw = blockIdx.x * EPB + el;
+  const bool valid = e_raw < n;
+  const int e = valid ? e_raw : n - 1;
+  EnvS& s = sm.env[el];
+  const as_state_t& st = P.st;
+  const as_model_t& m = K.model;
+  const int nh = m.num_hinges, nl = m.num_links;
+  if (el == 0) sm.topo[lane] = load_topo(K, lane);
+  if (lane < 3) s.root_pos[lane] = st.root_pos[lane * n + e];
+  if (lane < 4) s.root_quat[lane] = st.root_quat[lane * n + e];
+  if (lane < nh) {
+    const int i = m.cfg_dof_link[lane] - 1;
+    s.qi[i] = st.q[lane * n + e];
+    s.u[6 + i] = st.qd[lane * n + e];
+  }
+  float v0[3], w0[3];  // the root COM's linear velocity (root_lin) and the angular velocity
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    v0[k] = st.root_lin[k * n + e];
+    w0[k] = st.root_ang[k * n + e];
+  }
+  __syncthreads();
+  const LinkC lc = load_link(K, lane);
+  fk<false>(K, s, lane, sm.topo[lane], lc, K.max_path);
+  // lane i >= 1: its hinge's world axis and anchor (relative to the root origin) and qd, into the
+  // dynamics scratch (free after fk<false>)
+  DynScratch& d = s.x.d;
+  if (lane >= 1 && lane < nl) {
+    float a[3], o[3];
+    matvec3(s.R[lane], lc.ax, a);
+    matvec3(s.R[lane], lc.an, o);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      d.c[lane][k] = a[k];
+      d.Sq[lane][k] = o[k] + s.p[lane][k];
+    }
+    d.Sq[lane][3] = s.u[6 + lane - 1];
+  }
+  __syncthreads();
+  const int nb = P.bodies.num_bodies;
+  if (lane < nb && valid) {
+    const int b = lane, L = P.bodies.link[b];
+    float R0[9], c0[3];
+    quat_to_mat(s.root_quat, R0);
+    matvec3(R0, m.com[0], c0);
+    // the root origin's velocity: v_O = v_com0 - w0 x c0
+    float vO[3], t[3];
+    cross3(w0, c0, t);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) vO[k] = v0[k] - t[k];
+    const float* RL = s.R[L];
+    float po[3], pb[3];
+    matvec3(RL, P.bodies.offset_pos[b], po);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pb[k] = s.p[L][k] + po[k];
+    float w[3] = {w0[0], w0[1], w0[2]}, v[3];
+    cross3(w0, pb, t);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) v[k] = vO[k] + t[k];
+    uint32_t path = sm.topo[L].lpath & ~1u;  // hinges on the path root..L (link j >= 1 carries hinge j - 1)
+    while (path) {
+      const int j = __builtin_ctz(path);
+      path &= path - 1u;
+      const float nj[3] = {d.c[j][0], d.c[j][1], d.c[j][2]};
+      const float qd = d.Sq[j][3];
+      const float r[3] = {pb[0] - d.Sq[j][0], pb[1] - d.Sq[j][1], pb[2] - d.Sq[j][2]};
+      cross3(nj, r, t);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        w[k] += nj[k] * qd;
+        v[k] += t[k] * qd;
+      }
+    }
+    float Ro[9], Rb[9], q[4];
+    quat_to_mat(P.bodies.offset_quat[b], Ro);
+    matmul3(RL, Ro, Rb);
+    mat_to_quat(Rb, q);
+    float cw[3], vc[3];
+    matvec3(Rb, P.bodies.com[b], cw);
+    cross3(w, cw, t);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) vc[k] = v[k] + t[k];
+    const float row[AS_BODY_STATE_ROWS] = {s.root_pos[0] + pb[0], s.root_pos[1] + pb[1], s.root_pos[2] + pb[2],
+                                           q[0], q[1], q[2], q[3], v[0], v[1], v[2], w[0], w[1], w[2],
+                                           vc[0], vc[1], vc[2]};
+#pragma unroll
+    for (int r = 0; r < AS_BODY_STATE_ROWS; ++r) P.out[((size_t)r * nb + b) * n + e] = row[r];
+  }
+}
+
+hipError_t launch_body_state(const BodyArgs& a, hipStream_t stream) {
+  const int blocks = (a.n + EPB - 1) / EPB;
+  hipLaunchKernelGGL(k_body_state, dim3(blocks), dim3(kStepThreads), 0, stream, a);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_zero(int32_t* p, int n) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0;
 }

@@ -29,15 +29,21 @@ _INT_FIELDS = [(n, r) for n, r, t in _native.STATE_LAYOUT if t == "i"]
 
 
 class _RobotData:
-    """The ``ArticulationData`` views the task reads (articulation_data.py:364-601), as zero-copy
-    (N, k) views of the SoA state (k-major storage, so rows are strided)."""
+    """The ``ArticulationData`` views (articulation_data.py:364-601).  Ring 1 -- what the task reads --
+    as zero-copy (N, k) views of the SoA state (k-major storage, so rows are strided).  Ring 2 -- the
+    body views of every MJCF body (``body_names``: the walker's 17, document order) -- computed on demand
+    by the ``as_body_state`` HIP kernel (the step kernel's own FK of the state as it stands) each time one
+    is read; the step never computes them (include/allsteps.h)."""
 
     def __init__(self, env: "AllstepsEnv"):
         self._env = env
         s = env.state
         n = env.num_envs
         self.joint_names = list(env.model["dof_names"])
-        self.body_names = ["torso", "right_foot", "left_foot"]
+        self.body_names = list(env.model["body_names"])
+        self.num_bodies = len(self.body_names)
+        self._body_table = _native.make_body_table(env.model)
+        self._body_out = None
         lim = torch.as_tensor(joint_limits_cfg(env.model), device=env._device)
         self.joint_pos_limits = lim.unsqueeze(0).expand(n, -1, -1)
         self.default_joint_pos = torch.zeros(n, 21, device=env._device)
@@ -59,10 +65,112 @@ class _RobotData:
         s = self._s
         return torch.cat([s["root_pos"], s["root_quat"], s["root_lin"], s["root_ang"]], 0).T.contiguous()
 
+    def _bodies(self) -> torch.Tensor:
+        """(16, B, N) as_body_state rows of the current state: pos 3 | quat 4 | frame lin vel 3 | ang vel 3 |
+        COM lin vel 3 (one launch on the env's stream)."""
+        env = self._env
+        if self._body_out is None:
+            self._body_out = torch.empty(_native.BODY_STATE_ROWS, self.num_bodies, env.num_envs, device=env._device)
+        env._native.body_state(self._body_table, self._body_out, stream=env._stream())
+        return self._body_out
+
+    def _rows(self, lo: int, hi: int) -> torch.Tensor:
+        return self._bodies()[lo:hi].permute(2, 1, 0).contiguous()
+
     @property
     def body_pos_w(self) -> torch.Tensor:
-        """(N, 3, 3): torso, right_foot, left_foot link-frame positions (FK after the last substep)."""
-        return self._s["body_pos"].view(3, 3, -1).permute(2, 0, 1)
+        """(N, B, 3) body (link-frame) positions, all bodies; rows torso / right_foot / left_foot equal the
+        state's body_pos (the step's FK after the last substep) bit for bit."""
+        return self._rows(0, 3)
+
+    @property
+    def body_quat_w(self) -> torch.Tensor:
+        """(N, B, 4) body orientations (w, x, y, z)."""
+        return self._rows(3, 7)
+
+    @property
+    def body_lin_vel_w(self) -> torch.Tensor:
+        """(N, B, 3) linear velocities of the bodies' centres of mass (PhysX link velocities)."""
+        return self._rows(13, 16)
+
+    @property
+    def body_ang_vel_w(self) -> torch.Tensor:
+        return self._rows(10, 13)
+
+    @property
+    def body_state_w(self) -> torch.Tensor:
+        """(N, B, 13) [pos, quat, lin_vel, ang_vel]: link-frame pose, centre-of-mass velocity
+        (articulation_data.py:430-447)."""
+        b = self._bodies()
+        return torch.cat([b[0:7], b[13:16], b[10:13]], 0).permute(2, 1, 0).contiguous()
+
+    @property
+    def body_link_state_w(self) -> torch.Tensor:
+        """(N, B, 13) link-frame pose and the link frame's own velocity (articulation_data.py:449-470)."""
+        return self._rows(0, 13)
+
+    @property
+    def body_link_pos_w(self) -> torch.Tensor:
+        return self._rows(0, 3)
+
+    @property
+    def body_link_vel_w(self) -> torch.Tensor:
+        return self._rows(7, 13)
+
+    @property
+    def body_com_pos_w(self) -> torch.Tensor:
+        """(N, B, 3) the bodies' own centres of mass (as_body_table_t.com, from the MJCF geoms)."""
+        b = self._bodies()
+        q = b[3:7].permute(2, 1, 0)
+        com = torch.as_tensor(self._env.model["body_com"][: self.num_bodies], device=b.device)
+        w, v = q[..., :1], q[..., 1:]
+        c = com.expand_as(v)
+        t = 2.0 * torch.linalg.cross(v, c, dim=-1)
+        return b[0:3].permute(2, 1, 0) + c + w * t + torch.linalg.cross(v, t, dim=-1)
+
+
+class _SensorData:
+    def __init__(self, sensor: "_FootSensor"):
+        self._sensor = sensor
+
+    @property
+    def force_matrix_w(self) -> torch.Tensor | None:
+        """(N, B, 20, 3) FLAG-VALUED force matrix of the stones (filter_prim_paths_expr = the 20 steps):
+        (0, 0, 1) N where the foot pushed on that stone with |F| > 1e-4 N in the env step's last
+        substep (contact_sensor.py:341 with the contact solve's impulse / dt), 0 elsewhere.  The force
+        itself is not kept by the step (only the flag the task reads: allsteps_env.py:421-425 tests
+        ``vector_norm(force_matrix_w) > EPSILON``, which this view answers exactly).  None for the
+        unfiltered two-foot sensor, as in the reference."""
+        return self._sensor._force_matrix()
+
+    @property
+    def net_forces_w(self):
+        raise _native.NativeError(
+            "ContactSensor.data.net_forces_w is not available: the MI355X step keeps the per-stone contact "
+            "flags of each foot (force_matrix_w, flag-valued), not net contact forces (INTEGRATION.md §C3)")
+
+
+class _FootSensor:
+    """The reference's foot ContactSensors (allsteps_env_cfg.py:119-130; contact_sensor.py:320-343):
+    ``sensor_right`` / ``sensor_left`` (one foot, filtered by the 20 stones) and ``sensor`` (both feet,
+    unfiltered), over the state's per-foot stone bitmasks (contact_mask)."""
+
+    def __init__(self, env: "AllstepsEnv", feet: list, names: list, filtered: bool):
+        self._env, self._feet, self._filtered = env, feet, filtered
+        self.body_names = list(names)
+        self.num_bodies = len(feet)
+        self.data = _SensorData(self)
+
+    def _force_matrix(self):
+        if not self._filtered:
+            return None
+        env = self._env
+        m = env.state["contact_mask"]  # (2, N) int32, bit s = stone s
+        bits = torch.arange(env.num_steps, device=m.device, dtype=torch.int32)
+        f = torch.zeros(env.num_envs, self.num_bodies, env.num_steps, 3, device=m.device)
+        for k, foot in enumerate(self._feet):
+            f[:, k, :, 2] = ((m[foot].unsqueeze(1) >> bits) & 1).float()
+        return f
 
 
 class _RobotView:
@@ -149,6 +257,10 @@ class AllstepsEnv(DirectRLEnv):
                                                        device=dev)
         self.joint_gears = torch.tensor(cfg.joint_gears, dtype=torch.float32, device=dev)
         self.robot = _RobotView(self)
+        # foot contact sensors (allsteps_env.py:224-226): right = sensor foot 0, left = 1
+        self.sensor_right = _FootSensor(self, [0], ["right_foot"], True)
+        self.sensor_left = _FootSensor(self, [1], ["left_foot"], True)
+        self.sensor = _FootSensor(self, [0, 1], ["right_foot", "left_foot"], False)
         jn = self.robot.data.joint_names
         self.foot_names = list(cfg.foot_names)
         self.foot_indices = [self.robot.data.body_names.index(x) for x in self.foot_names]

@@ -18,6 +18,7 @@ import numpy as np
 MAX_LINKS = 32
 MAX_GEOMS = 32
 MAX_SELF_PAIRS = 256  # include/allsteps.h AS_MAX_SELF_PAIRS
+MAX_BODIES = 32  # include/allsteps.h AS_MAX_BODIES
 HERE = os.path.dirname(os.path.abspath(__file__))
 WALKER_JSON = os.path.join(HERE, "walker3d.json")
 ANYMAL_C_JSON = os.path.join(HERE, "anymal_c.json")  # BASELINE C5 quadruped (authored approximation)
@@ -108,6 +109,24 @@ def load_model(path: str = WALKER_JSON) -> dict:
     m["foot_link"] = np.array(foot_link[:2], np.int32)  # body_pos FK slots (as_model_t.foot_link[2])
     m["sensor_links"] = list(foot_link)
     m["link_names"] = [L["name"] for L in links]
+    # the MJCF bodies (document order) for the ArticulationData body views (ring 2, as_body_state):
+    # the link whose frame carries each body, the body frame in it, the body's own COM (body frame)
+    bodies = j.get("bodies") or [{"name": b, "link": li, "offset_pos": [0.0] * 3, "offset_quat": [1.0, 0.0, 0.0, 0.0],
+                                   "mass": 0.0, "com": [0.0] * 3} for b, li in bl.items()]
+    if len(bodies) > MAX_BODIES:
+        raise ValueError(f"model has {len(bodies)} bodies > {MAX_BODIES}")
+    m["body_names"] = [b["name"] for b in bodies]
+    m["num_bodies"] = len(bodies)
+    m["body_link"] = np.zeros(MAX_BODIES, np.int32)
+    m["body_offset_pos"] = np.zeros((MAX_BODIES, 3), np.float32)
+    m["body_offset_quat"] = np.zeros((MAX_BODIES, 4), np.float32)
+    m["body_offset_quat"][:, 0] = 1.0
+    m["body_com"] = np.zeros((MAX_BODIES, 3), np.float32)
+    for k, b in enumerate(bodies):
+        m["body_link"][k] = b["link"]
+        m["body_offset_pos"][k] = b["offset_pos"]
+        m["body_offset_quat"][k] = b["offset_quat"]
+        m["body_com"][k] = b["com"]
     m["dof_names"] = list(j["cfg_dof_order"])
     m["total_mass"] = float(j["total_mass"])
     return m

@@ -79,6 +79,27 @@ def quat_to_mat(q) -> np.ndarray:
     ])
 
 
+def mat_to_quat(R) -> list[float]:
+    """(w, x, y, z) of a rotation matrix, w >= 0 (Shepperd's branch on the largest diagonal term)."""
+    R = np.asarray(R, float)
+    t = np.trace(R)
+    if t > 0:
+        s = math.sqrt(t + 1.0) * 2
+        q = [0.25 * s, (R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s]
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = math.sqrt(1.0 + R[i, i] - R[j, j] - R[k, k]) * 2
+        q = [0.0] * 4
+        q[0] = (R[k, j] - R[j, k]) / s
+        q[1 + i] = 0.25 * s
+        q[1 + j] = (R[j, i] + R[i, j]) / s
+        q[1 + k] = (R[k, i] + R[i, k]) / s
+    q = np.array(q)
+    q = q / np.linalg.norm(q)
+    return (q if q[0] >= 0 else -q).tolist()
+
+
 def _frame_from_z(d: np.ndarray) -> np.ndarray:
     """Rotation whose third column is the unit vector d."""
     z = d / np.linalg.norm(d)
@@ -160,6 +181,15 @@ def compile_mjcf(path: str, opts: dict | None = None) -> dict:
     base = world.find("body")
 
     links: list[dict] = []
+    # every MJCF body in document order: the link whose frame carries it, its frame in that link's frame,
+    # and the mass / COM of its own geoms (body frame) -- the ArticulationData body views (ring 2)
+    bodies: list[dict] = []
+
+    def add_body_entry(body: ET.Element, link: int, R_b: np.ndarray, p_b: np.ndarray) -> None:
+        parts = [geom_mass_inertia(g) for g in parse_geoms(body, np.eye(3), np.zeros(3))]
+        m, c, _ = combine(parts) if parts else (0.0, np.zeros(3), np.zeros((3, 3)))
+        bodies.append({"name": body.get("name"), "link": link, "offset_pos": np.asarray(p_b, float).tolist(),
+                       "offset_quat": mat_to_quat(R_b), "mass": float(m), "com": np.asarray(c, float).tolist()})
 
     def parse_geoms(body: ET.Element, R_off: np.ndarray, p_off: np.ndarray) -> list[dict]:
         """Geoms of `body`, expressed in a frame where body-frame point x maps to R_off x + p_off."""
@@ -197,6 +227,7 @@ def compile_mjcf(path: str, opts: dict | None = None) -> dict:
             # fixed body: merge geoms into parent_link, recurse with accumulated transform
             R_b = R_acc @ quat_to_mat(quat)
             p_b = R_acc @ pos + p_acc
+            add_body_entry(body, parent_link, R_b, p_b)
             links[parent_link]["geoms"].extend(parse_geoms(body, R_b, p_b))
             links[parent_link]["merged"].append(body.get("name"))
             for child in body.findall("body"):
@@ -235,6 +266,7 @@ def compile_mjcf(path: str, opts: dict | None = None) -> dict:
             }
             links.append(link)
             prev = len(links) - 1
+        add_body_entry(body, prev, np.eye(3), np.zeros(3))
         links[prev]["geoms"].extend(parse_geoms(body, np.eye(3), np.zeros(3)))
         for child in body.findall("body"):
             add_body(child, prev, np.eye(3), np.zeros(3))
@@ -246,6 +278,7 @@ def compile_mjcf(path: str, opts: dict | None = None) -> dict:
     links.append({"name": "root", "body": base.get("name"), "parent": -1,
                   "offset_pos": [0.0, 0.0, 0.0], "offset_quat": [1.0, 0.0, 0.0, 0.0],
                   "joint": None, "geoms": [], "merged": [], "is_body_frame": True})
+    add_body_entry(base, 0, np.eye(3), np.zeros(3))
     links[0]["geoms"].extend(parse_geoms(base, np.eye(3), np.zeros(3)))
     for child in base.findall("body"):
         add_body(child, 0, np.eye(3), np.zeros(3))
@@ -280,6 +313,7 @@ def compile_mjcf(path: str, opts: dict | None = None) -> dict:
         "gears": list(opts["gears"]),
         "mjcf_base_pos": pos.tolist(),
         "total_mass": float(sum(L["mass"] for L in links)),
+        "bodies": bodies,
     }
     if opts is not WALKER:  # the walker's json predates these keys; load_model defaults to them
         out.update(torso=opts["torso"], sensor_feet=opts["sensor_feet"], contact_first=opts["contact_first"])

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define AS_ABI_VERSION 3
+#define AS_ABI_VERSION 4
 #define AS_MAX_LINKS 32
 #define AS_MAX_GEOMS 32
 #define AS_MAX_SELF_PAIRS 256
@@ -269,6 +269,29 @@ int as_quad_reset_all(as_env_t* env, float* obs, void* stream);
 /* _generate_foot_steps_allsteps (allsteps_env.py:125-174) on the device at curriculum `level`;
  * draws: [5][n][20] U[0,1) (NULL = Philox stream (seed, env, 0xF007)). Writes state->stones. */
 int as_generate_stones(as_env_t* env, int32_t level, const float* draws, void* stream);
+
+/* Ring-2 views, off the hot path (round 6).  The reference's ArticulationData body views
+ * (articulation_data.py:430-447 body_state_w -- link-frame pose, COM velocity -- and body_link_state_w --
+ * link-frame pose and velocity; body_pos_w = body_state_w[..., :3]) for EVERY body of the model (the
+ * walker's 17 MJCF bodies), computed on demand from the SoA state as it stands: root pose / velocity
+ * (root_lin is the root COM's velocity, as in the state), q, qd.  FK with the step kernel's own
+ * arithmetic, so rows of bodies whose frame is the torso / a foot link equal state->body_pos bit for bit;
+ * then per body b, with L = link[b]:
+ *   pos  = root_pos + p_L + R_L offset_pos[b]             rot = R_L R(offset_quat[b])  (quat w, x, y, z)
+ *   w    = root angular velocity + sum over the hinges j on the path of L of axis_j(world) * qd_j
+ *   vfrm = velocity of the body frame's origin             vcom = velocity of the body's own COM (com[b])
+ * out: device [AS_BODY_STATE_ROWS][num_bodies][n] fp32 = pos 3 | quat 4 | vfrm 3 | w 3 | vcom 3.
+ * as_step never runs it; the caller launches it when a view is read (envs/allsteps_env.py). */
+#define AS_MAX_BODIES 32
+#define AS_BODY_STATE_ROWS 16
+typedef struct {
+  int32_t num_bodies;
+  int32_t link[AS_MAX_BODIES];          /* the link whose frame carries the body (model body_link) */
+  float offset_pos[AS_MAX_BODIES][3];   /* body frame in that link's frame */
+  float offset_quat[AS_MAX_BODIES][4];  /* (w, x, y, z) */
+  float com[AS_MAX_BODIES][3];          /* the body's own centre of mass, body frame */
+} as_body_table_t;
+int as_body_state(as_env_t* env, const as_body_table_t* bodies_host, float* out, void* stream);
 
 /* Per-launch timing: record HIP events around the step kernel (k_step) and the observation
  * kernel (k_obs) of the next `max_launches` calls on their own stream; as_profile_read
