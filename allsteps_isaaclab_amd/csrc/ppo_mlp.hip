@@ -241,9 +241,21 @@ __device__ __forceinline__ void mma_rows(const uint16_t* X, const typename Lp<DT
 #ifndef PPO_FWD_SINGLE_W
 #define PPO_FWD_SINGLE_W 0
 #endif
+#ifndef PPO_FWD_COPY
+// A/B knob.  1: the layers' activation stores leave through full-row copies of the LDS image (every wave
+// store 1 KB contiguous: two whole rows) once a tile row block is complete, instead of each wave storing its
+// own 32 features (32-B runs per row) from its epilogue -- the same bytes and values (bit-identical, r06f).
+// Measured (DESIGN §7 "Round 6"): the standalone forward 44.1 -> 43.0 us, but the training forward with the
+// fused losses slower (update_s 0.0513 -> 0.0520 s): off.  (A timing-only build with the stores made
+// contiguous in a wrong layout, PPO_FWD_DBG 256, put the row pattern's share of the store cost at 4.4 of
+// ~10 us; the copies' extra LDS reads and the tail copies give most of it back.)
+#define PPO_FWD_COPY 0
+#endif
 #ifndef PPO_FWD_DBG
 #define PPO_FWD_DBG 0  // timing-only builds (scripts/fwd_dbg.sh): 2 no exp, 4 no stores, 16 no MFMA, 32 no ELU / convert,
-                       // 64 no loss block, 128 no heads
+                       // 64 no loss block, 128 no heads, 256 the activation stores as contiguous 1-KB wave stores
+                       // (wrong layout: is the 32-B-run row pattern what the stores cost?); backward: 512 dz
+                       // stores contiguous, 1024 y loads contiguous, 2048 no y loads, 4096 no dz stores
 #endif
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -306,10 +318,32 @@ __device__ __forceinline__ void tile_epi(const f32x16& acc, uint16_t* Xn, int rl
     uint16_t* xn = Xn + rl * kXs + F0 + 8 * h;
     *reinterpret_cast<uint4*>(xn) = c01;
     *reinterpret_cast<uint4*>(xn + 16) = c23;
-    if (STORE) {
+    if (STORE && !PPO_FWD_COPY) {
+#if PPO_FWD_DBG & 256
+        // timing-only: the same bytes as fully contiguous 1-KB wave stores (wrong layout)
+        const int tb = (row - (threadIdx.x & 31)) * h_stride * 2 + (F0 / 32) * 2 * 2048 + 16 * int(threadIdx.x & 63);
+        __builtin_amdgcn_raw_buffer_store_b128(u4(c01), rh, tb, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u4(c23), rh, tb + 1024, 0, 0);
+#else
         const int off = (row * h_stride + F0 + 8 * h) * 2;
         __builtin_amdgcn_raw_buffer_store_b128(u4(c01), rh, off, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(u4(c23), rh, off + 32, 0, 0);
+#endif
+    }
+}
+
+// Rows [r0, r0 + NR) of the LDS activation image X (features 0..255) to global rows row0 + r0.. of rh (range-
+// checked): 16-B chunks, 32 per row, consecutive threads on consecutive chunks, so every wave store covers two
+// whole 512-B rows.  The constant ones column (256) of the global rows is left alone.
+template <int NR>
+__device__ __forceinline__ void copy_rows(const uint16_t* X, int r0, Rsrc rh, int h_stride, int row0) {
+    constexpr int kChunks = NR * (kHid / 8);
+    static_assert(kChunks % kFThreads == 0, "whole chunks per thread");
+#pragma unroll
+    for (int u = 0; u < kChunks / kFThreads; ++u) {
+        const int c = u * kFThreads + int(threadIdx.x), r = r0 + c / (kHid / 8), q = c % (kHid / 8);
+        const uint4 v = *reinterpret_cast<const uint4*>(X + r * kXs + 8 * q);
+        __builtin_amdgcn_raw_buffer_store_b128(u4(v), rh, ((row0 + r) * h_stride + 8 * q) * 2, 0, 0);
     }
 }
 
@@ -363,11 +397,16 @@ __device__ __forceinline__ void layer(const uint16_t* Xin, uint16_t* Xout, const
     const f32x16 c0 = mfma_tile<DT, NS>(Xin, wa, binit, 0, j, h);
     if (HAS_PREV)
         tile_epi<DT, STORE>(pend, const_cast<uint16_t*>(Xin), 96 + j, row0 + 96 + j, rh_prev, h_stride, F0, h);
+    // the previous layer's output (this layer's input image) leaves by row copies: rows 0..95 (complete since
+    // the previous layer's last barrier) beside tiles 1 and 2, rows 96..127 beside tile 3
+    if (STORE && PPO_FWD_COPY && HAS_PREV) copy_rows<48>(Xin, 0, rh_prev, h_stride, row0);
     const f32x16 c1 = mfma_tile<DT, NS>(Xin, wa, binit, 1, j, h);
     tile_epi<DT, STORE>(c0, Xout, j, row0 + j, rh, h_stride, F0, h);
+    if (STORE && PPO_FWD_COPY && HAS_PREV) copy_rows<48>(Xin, 48, rh_prev, h_stride, row0);
     const f32x16 c2 = mfma_tile<DT, NS>(Xin, wa, binit, 2, j, h);
     tile_epi<DT, STORE>(c1, Xout, 32 + j, row0 + 32 + j, rh, h_stride, F0, h);
     __syncthreads();
+    if (STORE && PPO_FWD_COPY && HAS_PREV) copy_rows<32>(Xin, 96, rh_prev, h_stride, row0);
     const f32x16 c3 = mfma_tile<DT, NS>(Xin, wa, binit, 3, j, h);
     tile_epi<DT, STORE>(c2, Xout, 64 + j, row0 + 64 + j, rh, h_stride, F0, h);
     pend = c3;
@@ -498,6 +537,7 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
     for (int r = 0; r < 16; ++r) bhv[r] = feat(r, h) < a.nh ? a.bh[feat(r, h)] : 0.f;
     layer<DT, 16, STORE, true>(X0, X1, wa, ba, pend, rh[3], rh[4], hs, row0, F0, j, h);
     tile_epi<DT, STORE>(pend, X1, 96 + j, row0 + 96 + j, rh[4], hs, F0, h);
+    if (STORE && PPO_FWD_COPY) copy_rows<96>(X1, 0, rh[4], hs, row0);  // layer 5's rows 0..95 (complete)
     V8 (&whf)[16] = wb;
 #endif
     // ---- fused losses (LA > 0): ppo_loss_grad's work for the block's rows (ppo_loss.h), eight lanes per row
@@ -532,6 +572,7 @@ __device__ __forceinline__ void mlp_fwd_body(const ppo_mlp_fwd_t& a) {
         ppo_detail::loss_prefetch<LA, kFThreads>(p, blockIdx.x, lin);
     }
     __syncthreads();
+    if (STORE && PPO_FWD_COPY) copy_rows<32>(X1, 96, rh[4], hs, row0);  // layer 5's rows 96..127
     // ---- heads: wave w < 4 takes N-tile w; out = 16-bit(acc + 16-bit(bh)) as under autocast.  With the
     // fused losses (LA > 0) the values also go to a table of the block's rows at the head of X0 (free: layer
     // 5 has read it), the losses' input
@@ -586,7 +627,16 @@ struct YT {
 __device__ __forceinline__ YT load_y(Rsrc ry, int row, int stride, int F0, int h) {
     YT y;
 #pragma unroll
+#if PPO_FWD_DBG & 2048
+    for (int g = 0; g < 4; ++g) y.v[g] = u32x2_t{0u, 0u};  // timing-only: no y loads
+#elif PPO_FWD_DBG & 1024
+    // timing-only: the same bytes as contiguous 512-B wave loads (wrong values)
+    for (int g = 0; g < 4; ++g)
+        y.v[g] = __builtin_amdgcn_raw_buffer_load_b64(ry, (row - int(threadIdx.x & 31)) * stride * 2 + F0 * 64 + 512 * g +
+                                                               8 * int(threadIdx.x & 63), 0, 0);
+#else
     for (int g = 0; g < 4; ++g) y.v[g] = __builtin_amdgcn_raw_buffer_load_b64(ry, (row * stride + F0 + 8 * g + 4 * h) * 2, 0, 0);
+#endif
     return y;
 }
 
@@ -621,9 +671,18 @@ __device__ __forceinline__ void tile_bepi(const f32x16& dh, const YT& y, uint16_
     uint16_t* xn = Xn + rl * kXs + F0 + 8 * h;
     *reinterpret_cast<uint4*>(xn) = c01;
     *reinterpret_cast<uint4*>(xn + 16) = c23;
+#if PPO_FWD_DBG & 4096
+    (void)row; (void)rdz;  // timing-only: no dz stores
+#elif PPO_FWD_DBG & 512
+    // timing-only: the same bytes as contiguous 1-KB wave stores (wrong layout)
+    const int tb = (row - int(threadIdx.x & 31)) * kHid * 2 + F0 * 128 + 16 * int(threadIdx.x & 63);
+    __builtin_amdgcn_raw_buffer_store_b128(u4(c01), rdz, tb, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u4(c23), rdz, tb + 1024, 0, 0);
+#else
     const int off = (row * kHid + F0 + 8 * h) * 2;
     __builtin_amdgcn_raw_buffer_store_b128(u4(c01), rdz, off, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(u4(c23), rdz, off + 32, 0, 0);
+#endif
 }
 
 // stage l = 4..1: dh = W_l^T dz_l (Xin) for the wave's input features, epilogue against y (layer l - 1's
