@@ -424,7 +424,7 @@ def test_bench_two_ranks_one_gpu():
            "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20",
            "--warmup", "3", "--num-envs", "256", "--no-cpu-baseline", "--no-c5", "--train-envs", "1024",
            "--multi-gpu-mode", "allgather"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -452,7 +452,7 @@ def test_bench_gpus_flag_launches_ranks_itself():
     env["ALLSTEPS_DIST_BACKEND"] = "gloo"
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "3",
            "--num-envs", "256", "--no-cpu-baseline", "--no-c5", "--train-envs", "1024"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -461,6 +461,10 @@ def test_bench_gpus_flag_launches_ranks_itself():
     tr = line["train"]
     assert "error" not in tr, (tr, r.stderr[-2000:])
     assert tr["n_gpus"] == 2 and tr["multi_gpu_mode"] == "allreduce"  # bench default
+    tg = line["train_allgather"]  # the north star's exchange, reported beside the default
+    assert "error" not in tg, (tg, r.stderr[-2000:])
+    assert tg["n_gpus"] == 2 and tg["multi_gpu_mode"] == "allgather"
+    assert line["no_preheat"]["value"] > 0
     # the kernel timings come from a bit-exact replay of each rank's timed window, >= 200 launches
     km = line["kernels_ms"]
     assert km["replay_exact"] and km["sampled_launches"] >= 200
