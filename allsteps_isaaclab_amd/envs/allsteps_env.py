@@ -44,12 +44,16 @@ class _RobotData:
         self.num_bodies = len(self.body_names)
         self._body_table = _native.make_body_table(env.model)
         self._body_out = None
+        nd = self._nd = int(env.model["num_hinges"])
         lim = torch.as_tensor(joint_limits_cfg(env.model), device=env._device)
         self.joint_pos_limits = lim.unsqueeze(0).expand(n, -1, -1)
-        self.default_joint_pos = torch.zeros(n, 21, device=env._device)
-        self.default_joint_vel = torch.zeros(n, 21, device=env._device)
+        djp = getattr(env, "default_joint_pos", None)  # the quadruped's stand pose; the walker's is zero
+        self.default_joint_pos = (djp.reshape(1, nd).expand(n, nd).clone() if torch.is_tensor(djp)
+                                  else torch.zeros(n, nd, device=env._device))
+        self.default_joint_vel = torch.zeros(n, nd, device=env._device)
         self.default_root_state = torch.zeros(n, 13, device=env._device)
-        self.default_root_state[:, :3] = torch.tensor(env.cfg.init_root_pos, device=env._device)
+        if getattr(env.cfg, "init_root_pos", None) is not None:
+            self.default_root_state[:, :3] = torch.tensor(env.cfg.init_root_pos, device=env._device)
         self.default_root_state[:, 3] = 1.0
         self._s = s
 
@@ -57,8 +61,8 @@ class _RobotData:
     root_quat_w = property(lambda self: self._s["root_quat"].T)
     root_lin_vel_w = property(lambda self: self._s["root_lin"].T)
     root_ang_vel_w = property(lambda self: self._s["root_ang"].T)
-    joint_pos = property(lambda self: self._s["q"].T)
-    joint_vel = property(lambda self: self._s["qd"].T)
+    joint_pos = property(lambda self: self._s["q"][: self._nd].T)  # the state's rows past the model's hinges unused
+    joint_vel = property(lambda self: self._s["qd"][: self._nd].T)
 
     @property
     def root_state_w(self) -> torch.Tensor:

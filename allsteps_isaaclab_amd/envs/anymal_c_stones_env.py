@@ -94,6 +94,11 @@ class AnymalCStonesEnv(DirectRLEnv):
         self._reset_buf_stale = False
         self.extras = {}
         self._native.quad_reset_all(self.obs_buf, stream=self._stream())
+        # the ArticulationData views (ring 1 zero-copy, ring 2 -- the 13 MJCF bodies -- by as_body_state on
+        # demand), as the walker's env serves them (envs/allsteps_env.py)
+        from .allsteps_env import _RobotView
+
+        self.robot = _RobotView(self)
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self._device).cuda_stream

@@ -164,3 +164,29 @@ def test_foot_sensor_force_matrix_is_the_task_flag(env):
     assert env.sensor.data.force_matrix_w is None
     with pytest.raises(_native.NativeError):
         env.sensor_left.data.net_forces_w
+
+
+def test_quadruped_body_views_match_float64_fk():
+    """The C5 env serves the same views for its 13 bodies (AnymalCStonesEnv.robot.data)."""
+    from allsteps_isaaclab_amd.envs.anymal_c_stones_env import AnymalCStonesEnv
+    from allsteps_isaaclab_amd.envs.anymal_c_stones_env_cfg import AnymalCStonesEnvCfg
+
+    cfg = AnymalCStonesEnvCfg()
+    cfg.scene.num_envs = 128
+    cfg.sim.device = "cuda:0"
+    env = AnymalCStonesEnv(cfg)
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    for _ in range(20):
+        env.step(torch.rand(128, 12, device="cuda:0", generator=g) * 2 - 1)
+    torch.cuda.synchronize()
+    d, m = env.robot.data, env.model
+    assert d.body_names[0] == "base" and len(d.body_names) == 13
+    assert d.body_pos_w.shape == (128, 13, 3) and d.joint_pos.shape == (128, 12)
+    assert torch.equal(d.default_joint_pos[0], env.default_joint_pos)
+    pos = d.body_pos_w.cpu().numpy()
+    st = {k: env.state[k].cpu().numpy() for k in ("root_pos", "root_quat", "q")}
+    for e in range(0, 128, 13):
+        p_ref, _ = _fk_bodies(m, st["root_pos"][:, e], st["root_quat"][:, e], st["q"][:, e])
+        np.testing.assert_allclose(pos[e], p_ref, atol=2e-5)
+    env.close()
