@@ -3,7 +3,8 @@ config, N envs, E epochs; prints per-epoch mean episode reward / length / curric
 JSON lines (the evidence that physics + task + trainer learn together).
 
     python scripts/train_curve.py [num_envs] [epochs] [every] [task] [env.<k>=<v> | agent.<k>=<v> ...]
-    (task: Allsteps-v0 or Allsteps-AnymalC-v0, the C5 quadruped behind the same env surface)"""
+    (task: Allsteps-v0 or Allsteps-AnymalC-v0, the C5 quadruped behind the same env surface; the seed is 42
+    unless CURVE_SEED is set)"""
 import json
 import os
 import sys
@@ -47,5 +48,5 @@ with open(os.devnull, "w") as dn:
     with contextlib.redirect_stdout(sys.stderr):
         pass
 # past the four positional arguments: hydra-style overrides (env.<path>=<value>, agent.<path>=<value>)
-train.main(["--task", TASK, "--num_envs", str(N), "--max_iterations", str(E), "--seed", "42",
+train.main(["--task", TASK, "--num_envs", str(N), "--max_iterations", str(E), "--seed", os.environ.get("CURVE_SEED", "42"),
             "--log_root", "/tmp/curve_logs", *sys.argv[5:]])
