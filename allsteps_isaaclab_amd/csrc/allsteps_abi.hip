@@ -94,6 +94,9 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   if (!out || !model || !sim || !task || !state) return fail(AS_ERR_INVALID, "as_create: null argument");
   *out = nullptr;
   if (num_envs <= 0) return fail(AS_ERR_INVALID, "as_create: num_envs must be > 0");
+  if (num_envs > AS_MAX_ENVS)
+    return fail(AS_ERR_INVALID, "as_create: num_envs > AS_MAX_ENVS (" + std::to_string(AS_MAX_ENVS) +
+                                    "): the kernels' state offsets are 32-bit; shard the envs over more handles");
   if (model->num_links < 1 || model->num_links > as::kMaxLinks)
     return fail(AS_ERR_INVALID, "as_create: num_links out of range (1.." + std::to_string(as::kMaxLinks) + ")");
   if (model->num_hinges != model->num_links - 1 || model->num_hinges > AS_ACT_DIM)

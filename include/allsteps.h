@@ -33,6 +33,9 @@ extern "C" {
 #define AS_MAX_LINKS 32
 #define AS_MAX_GEOMS 32
 #define AS_MAX_SELF_PAIRS 256
+/* envs per handle: the kernels index the field-major state and the [5][n][20] draw tables with 32-bit
+ * offsets (row * n + env, < 2^31); 2^24 envs is ~22 GB of state, far past one GPU's useful launch */
+#define AS_MAX_ENVS (1 << 24)
 #define AS_NUM_STONES 20
 /* Constraint budget per env and substep: every active joint-limit row is kept (a walker has at most
  * 21, one side per hinge); contacts fill the remaining rows three at a time up to AS_MAX_CONTACTS, in

@@ -186,6 +186,22 @@ def test_create_rejects_malformed_model(field, mutate, msg):
     assert msg in L.as_last_error(), L.as_last_error()
 
 
+def test_create_rejects_more_envs_than_32_bit_offsets_reach():
+    """num_envs above AS_MAX_ENVS (2^24: the kernels' field-major offsets are 32-bit) is refused before any
+    device call, with a message naming the limit; 2^24 itself passes validation."""
+    import torch
+
+    from allsteps_isaaclab_amd import _native
+
+    L = _native.load()
+    M, S, T, st, _buf = _valid_args()
+    h = C.c_void_p()
+    assert L.as_create((1 << 24) + 1, C.byref(M), C.byref(S), C.byref(T), C.byref(st), 0, 0, 0, C.byref(h)) == -1
+    assert b"AS_MAX_ENVS" in L.as_last_error()
+    if not torch.cuda.is_available():  # validation passes; the error is the missing device's
+        assert L.as_create(1 << 24, C.byref(M), C.byref(S), C.byref(T), C.byref(st), 0, 0, 0, C.byref(h)) == -3
+
+
 def test_create_accepts_the_walker_model_up_to_the_device():
     """The unmodified walker passes validation: without a device the error is the device's."""
     import torch
