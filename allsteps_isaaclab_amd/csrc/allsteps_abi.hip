@@ -56,6 +56,7 @@ struct as_env {
   int32_t bank = 0, last_bank = 0;
   int32_t graph_safe = 0;  // as_set_graph_safe: fixed bank 0 + memset per call
   uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_obs
+  int32_t* wave_map_dev = nullptr;  // [n] cost-balanced placement (kMapEnvs), or null: xcd_block
   int32_t num_steps;
   int32_t nv;
   as::Consts host;        // host copy of consts_dev (as_set_actuator / as_set_quad_task re-upload it)
@@ -210,6 +211,21 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   }
   HIP_TRY(hipMemcpy(env->consts_dev, &h, sizeof(as::Consts), hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(env->counters_dev, 0, 2 * as::kCntBank * sizeof(int32_t)));
+  HIP_TRY(hipMemset(env->side_dev, 0, (size_t)as::kSideWords * num_envs * sizeof(uint32_t)));
+  // cost-balanced placement (placement only: results are the same under any map); ALLSTEPS_WAVE_MAP=0
+  // keeps the fixed XCD-contiguous placement (A/B timing)
+  const char* wm = std::getenv("ALLSTEPS_WAVE_MAP");
+  if (as::wave_map_fits(num_envs) && !(wm && std::strcmp(wm, "0") == 0)) {
+    std::vector<int32_t> map((size_t)num_envs);  // the map k_obs builds from all-zero row counts (2 envs per workgroup)
+    for (int w = 0; w < num_envs / as::kMapEnvs; ++w)
+      for (int t = 0; t < as::kMapEnvs; ++t)
+        map[(size_t)2 * as::wave_map_block(w, t >> 1, num_envs) + (t & 1)] = w * as::kMapEnvs + t;
+    if (hipMalloc(&env->wave_map_dev, map.size() * sizeof(int32_t)) != hipSuccess) {
+      (void)as_destroy(env);
+      return fail(AS_ERR_HIP, "as_create: hipMalloc failed");
+    }
+    HIP_TRY(hipMemcpy(env->wave_map_dev, map.data(), map.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   *out = env;
   return AS_OK;
 }
@@ -221,6 +237,7 @@ int as_destroy(as_env_t* env) {
   (void)hipFree(env->consts_dev);
   (void)hipFree(env->counters_dev);
   (void)hipFree(env->side_dev);
+  (void)hipFree(env->wave_map_dev);
   delete env;
   return AS_OK;
 }
@@ -254,6 +271,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   a.stamps = env->stamps;
   a.obs = mode == as::kModePhysics ? nullptr : obs;
   a.side = env->side_dev;
+  a.wave_map = env->wave_map_dev;
   const bool prof = env->prof_n < env->prof_cap && (env->prof_calls++ % env->prof_stride) == 0;
   if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n], s));
   HIP_TRY(as::launch_step(a, env->nv, s));
@@ -277,6 +295,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   o.side = env->side_dev;
   o.seed = env->seed;
   o.env_offset = env->env_offset;
+  o.wave_map = env->wave_map_dev;
   HIP_TRY(as::launch_obs(o, s));
   if (prof) {
     HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 2], s));

@@ -56,6 +56,7 @@ struct StepArgs {
   uint64_t seed;
   int64_t env_offset;
   unsigned long long* stamps;  // diagnostic phase timing (s_memtime deltas summed over waves) or null
+  const int32_t* wave_map;     // [2 * blocks] env of each workgroup half (see kMapEnvs) or null: xcd_block
 };
 
 // phase ids of the diagnostic stamps (as_debug_stamps)
@@ -80,7 +81,24 @@ constexpr int kCntBank = kCntStride * (1 + kCntSlots);
 constexpr int kSideState = 9;
 constexpr int kSideObs = 11;
 constexpr int kSideRegen = kSideState + kSideObs;  // 1 = reset env due new stones (regen_footsteps)
-constexpr int kSideWords = kSideRegen + 1;
+constexpr int kSideCost = kSideRegen + 1;   // constraint rows of the env over this launch's substeps
+constexpr int kSideWords = kSideCost + 1;
+
+// Cost-balanced wave placement (k_obs -> the next k_step; placement only, never results).  With n a
+// multiple of kMapEnvs * 8 the k_step workgroups b and b + n/4 share a SIMD (two one-wave workgroups per
+// SIMD when the grid fills the chip; measured, scripts/simd_mates.py), and a wave's cycles grow with its
+// PARTNER's constraint rows more than with its own (the heavier wave takes issue priority).  So k_obs
+// ranks each workgroup-chunk of kMapEnvs envs by the rows they had in this launch, puts the two heaviest
+// envs in one wave, the next two in the next ..., and gives the heaviest wave the lightest as SIMD
+// partner: wave_map[2 b + h] = the env that workgroup b's half h steps in the next launch.
+constexpr int kMapEnvs = 64;
+__host__ __device__ inline bool wave_map_fits(int n) { return n > 0 && n % (8 * kMapEnvs) == 0; }
+// the workgroup of rank-pair p (0 = heaviest) of env chunk w, n / 4 workgroups per half of the grid:
+// chunk w's 16 heaviest pairs on XCD w % 8 in the first half, the 16 lightest on their SIMD partners
+__host__ __device__ inline int wave_map_block(int w, int p, int n) {
+  const int x = w & 7, j = w >> 3, half = n >> 2;
+  return p < kMapEnvs / 4 ? x + 8 * ((kMapEnvs / 4) * j + p) : x + 8 * ((kMapEnvs / 4) * j + (kMapEnvs / 2 - 1 - p)) + half;
+}
 constexpr int kCntLevel = 2;  // counter-bank word: the curriculum level k_step saw (k_obs regen level)
 constexpr int kCntDropped = 3;  // counter-bank word: contacts found past the row budget (as_step_counters [3])
 
@@ -109,6 +127,7 @@ struct ObsArgs {
   const uint32_t* side;
   uint64_t seed;
   int64_t env_offset;
+  int32_t* wave_map;       // null, or rebuilt here for the next k_step from the side buffer's row counts
 };
 
 struct StonesArgs {

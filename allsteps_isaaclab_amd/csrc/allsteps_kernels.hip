@@ -156,6 +156,7 @@ struct EnvS {
   int cand[NST];
   uint32_t mask[4];     // contact sensors 0..3 (2, 3: a quadruped's hind feet)
   int ndrop;            // contacts cut by the row budget over this launch's substeps (counters[kCntDropped])
+  int nrows;            // constraint rows over this launch's substeps (the next launch's placement cost)
 };
 
 struct Smem {
@@ -1565,6 +1566,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   }
   const int nrow = crow + nlim;  // uniform over the env's half-wave
   ts.count(nrow, nc);
+  if (lane == 0) s.nrows += nrow;  // (the last substep's rows, or the peak, predict no better: r06j)
   const int maxrow = max(__builtin_amdgcn_readlane(nrow, 0), __builtin_amdgcn_readlane(nrow, 32));
   __syncthreads();  // the row metadata above, for the J build
   // Issue priority by constraint load: the two waves of a SIMD are arbitrated by priority, then
@@ -1832,7 +1834,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2,
   const Consts& K = *(const Consts*)(CK*)P.consts;
   const int el = threadIdx.x >> 5, lane = threadIdx.x & 31;
   const int n = P.n;
-  const int e_raw = xcd_block(blockIdx.x, gridDim.x) * EPB + el;
+  const int e_raw = P.wave_map ? P.wave_map[EPB * blockIdx.x + el] : xcd_block(blockIdx.x, gridDim.x) * EPB + el;
   const bool valid = e_raw < n;
   const int e = valid ? e_raw : n - 1;
   EnvS& s = sm.env[el];
@@ -1852,7 +1854,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2,
     s.u[3 + lane] = st.root_ang[lane * n + e];
   }
   if (lane < 4) s.root_quat[lane] = st.root_quat[lane * n + e];
-  if (lane == 0) s.ndrop = 0;
+  if (lane == 0) { s.ndrop = 0; s.nrows = 0; }
   const int cur = st.curriculum[0];
   const float gain = T.gain_curriculum[cur];
   if (lane < nh) {
@@ -2146,6 +2148,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2,
       st.body_pos[lane * n + e] = v;
     }
     if (lane == 0) {
+      P.side[kSideCost * n + e] = (uint32_t)s.nrows;
       st.contact_mask[e] = s.mask[0];
       st.contact_mask[n + e] = s.mask[1];
       if (st.contact_mask_hind) {
@@ -2178,6 +2181,25 @@ __global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
   const int n = P.n;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int any_reset = P.counters[0];
+  if (P.wave_map) {
+    // the next k_step's placement (kMapEnvs): this workgroup's 64 envs ranked by their constraint rows
+    // in this launch (a bitonic sort of (rows, lane) keys across the wave, unique keys: deterministic),
+    // rank q -> pair q / 2, half q % 2 (rows is at most substeps x 30: 16 bits hold it)
+    static_assert(kMapEnvs == 64, "one wave per env chunk");
+    const int t = threadIdx.x;
+    const uint32_t rows = min(P.side[kSideCost * n + e], 0xFFFFu);
+    uint32_t key = rows << 6 | (uint32_t)(63 - t);  // descending rows, ascending env on ties
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)key, j);
+        const bool desc = (t & k) == 0, first = (t & j) == 0;  // descending overall
+        key = first == desc ? max(key, o) : min(key, o);
+      }
+    const int src = blockIdx.x * kMapEnvs + 63 - (int)(key & 63u);
+    P.wave_map[EPB * wave_map_block(blockIdx.x, t >> 1, n) + (t & 1)] = src;
+  }
   if (blockIdx.x == 0) {
     // the gate's inputs in one memory round trip: lane i < kCntSlots reads partial sum i, lane
     // kCntSlots the curriculum level (all issued before any store: the stores below may alias them)
