@@ -443,6 +443,8 @@ static int quad(as_env_t* env, int reset_all, const float* actions, float* obs, 
   a.truncated = trunc;
   a.seed = env->seed;
   a.env_offset = env->env_offset;
+  a.side = env->side_dev;
+  a.wave_map = env->wave_map_dev;
   HIP_TRY(as::launch_quad(a, s));
   return AS_OK;
 }

@@ -115,6 +115,8 @@ struct QuadArgs {
   uint8_t* truncated;
   uint64_t seed;
   int64_t env_offset;
+  const uint32_t* side;        // k_step's side buffer (the row counts of the placement)
+  int32_t* wave_map;           // null, or rebuilt here for the next k_step (kMapEnvs)
 };
 
 struct ObsArgs {

@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from stamps import NP, simd_key, wave_records  # noqa: E402
+from stamps import NP, PHASES, simd_key, wave_records  # noqa: E402
 from allsteps_isaaclab_amd.envs.allsteps_env import AllstepsEnv  # noqa: E402
 from allsteps_isaaclab_amd.envs.allsteps_env_cfg import AllstepsEnvCfg  # noqa: E402
 
@@ -70,20 +70,29 @@ def main(n=4096, steps=30, warm=20):
     X = np.stack([np.ones(L * nb), own.ravel(), mate_rows.ravel()], axis=1)
     coef, *_ = np.linalg.lstsq(X, tot.ravel(), rcond=None)
     # env rows launch to launch (env id of block b, half h)
-    eid = np.array([[xcd_block(b, nb) * 2 + h for h in range(2)] for b in range(nb)])
-    er = np.zeros((L, n))
-    er[:, eid.ravel()] = rows.reshape(L, -1)
-    c1 = float(np.corrcoef(er[:-1].ravel(), er[1:].ravel())[0, 1])
+    # (only with the fixed placement: under the cost-balanced wave map the env of a block moves)
+    c1 = None
+    if os.environ.get("ALLSTEPS_WAVE_MAP") == "0":
+        eid = np.array([[xcd_block(b, nb) * 2 + h for h in range(2)] for b in range(nb)])
+        er = np.zeros((L, n))
+        er[:, eid.ravel()] = rows.reshape(L, -1)
+        c1 = round(float(np.corrcoef(er[:-1].ravel(), er[1:].ravel())[0, 1]), 3)
     worst = np.argmax(tot, axis=1)
     d = {"n": n, "launches": L, "waves_per_simd_hist": waves_per_simd[0],
          "mates_same_as_launch0": round(same / max((L - 1) * nb, 1), 3),
          "mate_block_distance_top": [[int(k), int(v)] for k, v in sorted(zip(*np.unique(dist, return_counts=True)), key=lambda kv: -kv[1])[:10]],
          "fit_cycles": {"const": round(coef[0]), "per_own_row": round(coef[1], 1), "per_mate_row": round(coef[2], 1)},
          "rows_mean": round(float(own.mean()), 2), "rows_p99": float(np.percentile(own, 99)),
-         "env_rows_corr_next_launch": round(c1, 3),
+         "env_rows_corr_next_launch": c1,
+         "pairs_own_mate_rows_corr": round(float(np.corrcoef(own.ravel(), mate_rows.ravel())[0, 1]), 3),
          "slowest": [{"tot": int(tot[li, w]), "own": int(own[li, w]), "mate": int(mate_rows[li, w]),
                       "mate_tot": int(mate_tot[li, w])} for li, w in enumerate(worst)][:10],
-         "mean_tot": int(tot.mean()), "max_tot_mean": int(tot.max(axis=1).mean())}
+         "mean_tot": int(tot.mean()), "max_tot_mean": int(tot.max(axis=1).mean()),
+         "top_waves_by_launch": [[[int(tot[li, w]), int(own[li, w]), int(mate_rows[li, w])] for w in np.argsort(-tot[li])[:8]]
+                                 for li in range(3)],
+         "mean_phases": {PHASES[k]: int(R[:, :, k].mean()) for k in range(NP)},
+         "slowest_phases": [{PHASES[k]: int(R[li, w, k]) for k in range(NP)} for li, w in enumerate(worst)][:6],
+         "slowest_cons": [[int(R[li, w, NP + 7]), int(R[li, w, NP + 8])] for li, w in enumerate(worst)][:10]}
     # counterfactual from the fit: the slowest wave if its partner were the lightest
     print(json.dumps(d))
     env.close()
