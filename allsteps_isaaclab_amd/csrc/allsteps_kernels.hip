@@ -1841,6 +1841,12 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2,
   const as_state_t& st = P.st;
   Stamp ts{P.stamps, sm.stamp_acc, 0ull};
   ts.start();
+  // Under the wave map the second half of the grid holds the predicted-light waves, each the SIMD
+  // partner of a heavy one.  The light wave starts with issue priority, until the first substep's row
+  // count sets the rule below: with the heavy wave ahead from the first instruction the light partner
+  // finished last (a wave's cycles grow more with its partner's rows than with its own, r06j), and
+  // light-first for the opening phases only (not every substep's, nor the first two) measured best (r06k).
+  if (P.wave_map && blockIdx.x >= (gridDim.x >> 1)) __builtin_amdgcn_s_setprio(1);
   __syncthreads();
   const as_model_t& m = K.model;
   const int nh = m.num_hinges;
