@@ -57,6 +57,7 @@ struct as_env {
   int32_t graph_safe = 0;  // as_set_graph_safe: fixed bank 0 + memset per call
   uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_obs
   int32_t* wave_map_dev = nullptr;  // [n] cost-balanced placement (kMapEnvs), or null: xcd_block
+  int32_t map_streamed = 0;         // k_step's grid is larger than the chip's workgroup slots
   int32_t num_steps;
   int32_t nv;
   as::Consts host;        // host copy of consts_dev (as_set_actuator / as_set_quad_task re-upload it)
@@ -216,10 +217,13 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   // keeps the fixed XCD-contiguous placement (A/B timing)
   const char* wm = std::getenv("ALLSTEPS_WAVE_MAP");
   if (as::wave_map_fits(num_envs) && !(wm && std::strcmp(wm, "0") == 0)) {
+    // k_step: one-wave workgroups of 2 envs, 8 per CU (LDS-bound, tests/kernel_budget.json)
+    // (ALLSTEPS_WAVE_MAP=resident keeps the resident layout on a streamed grid: A/B timing)
+    env->map_streamed = num_envs / 2 > 8 * prop.multiProcessorCount && !(wm && std::strcmp(wm, "resident") == 0);
     std::vector<int32_t> map((size_t)num_envs);  // the map k_obs builds from all-zero row counts (2 envs per workgroup)
     for (int w = 0; w < num_envs / as::kMapEnvs; ++w)
       for (int t = 0; t < as::kMapEnvs; ++t)
-        map[(size_t)2 * as::wave_map_block(w, t >> 1, num_envs) + (t & 1)] = w * as::kMapEnvs + t;
+        map[(size_t)2 * as::wave_map_block(w, t >> 1, num_envs, env->map_streamed) + (t & 1)] = w * as::kMapEnvs + t;
     if (hipMalloc(&env->wave_map_dev, map.size() * sizeof(int32_t)) != hipSuccess) {
       (void)as_destroy(env);
       return fail(AS_ERR_HIP, "as_create: hipMalloc failed");
@@ -296,6 +300,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   o.seed = env->seed;
   o.env_offset = env->env_offset;
   o.wave_map = env->wave_map_dev;
+  o.map_streamed = env->map_streamed;
   HIP_TRY(as::launch_obs(o, s));
   if (prof) {
     HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 2], s));
@@ -445,6 +450,7 @@ static int quad(as_env_t* env, int reset_all, const float* actions, float* obs, 
   a.env_offset = env->env_offset;
   a.side = env->side_dev;
   a.wave_map = env->wave_map_dev;
+  a.map_streamed = env->map_streamed;
   HIP_TRY(as::launch_quad(a, s));
   return AS_OK;
 }

@@ -84,20 +84,23 @@ constexpr int kSideRegen = kSideState + kSideObs;  // 1 = reset env due new ston
 constexpr int kSideCost = kSideRegen + 1;   // constraint rows of the env over this launch's substeps
 constexpr int kSideWords = kSideCost + 1;
 
-// Cost-balanced wave placement (k_obs -> the next k_step; placement only, never results).  With n a
-// multiple of kMapEnvs * 8 the k_step workgroups b and b + n/4 share a SIMD (two one-wave workgroups per
-// SIMD when the grid fills the chip; measured, scripts/simd_mates.py), and a wave's cycles grow with its
-// PARTNER's constraint rows more than with its own (the heavier wave takes issue priority).  So k_obs
-// ranks each workgroup-chunk of kMapEnvs envs by the rows they had in this launch, puts the two heaviest
-// envs in one wave, the next two in the next ..., and gives the heaviest wave the lightest as SIMD
-// partner: wave_map[2 b + h] = the env that workgroup b's half h steps in the next launch.
+// Cost-balanced wave placement (k_obs / k_quad -> the next k_step; placement only, never results).
+// k_obs ranks each chunk of kMapEnvs consecutive envs by the constraint rows they had in this launch,
+// puts ranks 2p and 2p + 1 in one wave (pair p, 0 = heaviest) and places pair p of chunk w at workgroup
+//   resident grid (the whole grid fits the chip, 8 one-wave workgroups per CU):
+//     p < 16: p C + w,   p >= 16: n / 4 + (31 - p) C + w        (C = n / 64 chunks)
+//   -- workgroups b and b + n / 4 share a SIMD (measured, scripts/simd_mates.py), and a wave's cycles
+//   grow with its PARTNER's rows more than with its own, so the heaviest wave gets the lightest partner;
+//   streamed grid (more workgroups than slots): p C + w, so the dispatcher starts the heaviest pairs of
+//   every chunk first and the lightest last (longest-processing-time-first order).
+// Either way workgroup b runs on XCD b % 8 = w % 8 (C is a multiple of 8): a chunk's envs stay in one
+// XCD's L2.  wave_map[2 b + h] = the env of workgroup b's half h.
 constexpr int kMapEnvs = 64;
 __host__ __device__ inline bool wave_map_fits(int n) { return n > 0 && n % (8 * kMapEnvs) == 0; }
-// the workgroup of rank-pair p (0 = heaviest) of env chunk w, n / 4 workgroups per half of the grid:
-// chunk w's 16 heaviest pairs on XCD w % 8 in the first half, the 16 lightest on their SIMD partners
-__host__ __device__ inline int wave_map_block(int w, int p, int n) {
-  const int x = w & 7, j = w >> 3, half = n >> 2;
-  return p < kMapEnvs / 4 ? x + 8 * ((kMapEnvs / 4) * j + p) : x + 8 * ((kMapEnvs / 4) * j + (kMapEnvs / 2 - 1 - p)) + half;
+__host__ __device__ inline int wave_map_block(int w, int p, int n, bool streamed) {
+  const int C = n / kMapEnvs;
+  if (streamed || p < kMapEnvs / 4) return p * C + w;
+  return (n >> 2) + (kMapEnvs / 2 - 1 - p) * C + w;
 }
 constexpr int kCntLevel = 2;  // counter-bank word: the curriculum level k_step saw (k_obs regen level)
 constexpr int kCntDropped = 3;  // counter-bank word: contacts found past the row budget (as_step_counters [3])
@@ -117,6 +120,7 @@ struct QuadArgs {
   int64_t env_offset;
   const uint32_t* side;        // k_step's side buffer (the row counts of the placement)
   int32_t* wave_map;           // null, or rebuilt here for the next k_step (kMapEnvs)
+  int32_t map_streamed;        // wave_map_block
 };
 
 struct ObsArgs {
@@ -130,6 +134,7 @@ struct ObsArgs {
   uint64_t seed;
   int64_t env_offset;
   int32_t* wave_map;       // null, or rebuilt here for the next k_step from the side buffer's row counts
+  int32_t map_streamed;    // wave_map_block: the grid streams through the chip (LPT order)
 };
 
 struct StonesArgs {

@@ -2184,7 +2184,8 @@ __device__ void gen_stones(const as_task_t& T, int level, uint64_t seed, uint32_
 // The next k_step's placement (kMapEnvs), by one wave (t = lane): env chunk w's 64 envs ranked by their
 // constraint rows in this launch (a bitonic sort of (rows, lane) keys across the wave, unique keys:
 // deterministic), rank q -> pair q / 2, half q % 2 (rows is at most substeps x 30: 16 bits hold it).
-__device__ __forceinline__ void build_wave_map(const uint32_t* side, int32_t* wave_map, int n, int w, int t) {
+__device__ __forceinline__ void build_wave_map(const uint32_t* side, int32_t* wave_map, int n, bool streamed, int w,
+                                               int t) {
   static_assert(kMapEnvs == 64, "one wave per env chunk");
   const uint32_t rows = min(side[kSideCost * n + w * kMapEnvs + t], 0xFFFFu);
   uint32_t key = rows << 6 | (uint32_t)(63 - t);  // descending rows, ascending env on ties
@@ -2196,7 +2197,7 @@ __device__ __forceinline__ void build_wave_map(const uint32_t* side, int32_t* wa
       const bool desc = (t & k) == 0, first = (t & j) == 0;  // descending overall
       key = first == desc ? max(key, o) : min(key, o);
     }
-  wave_map[EPB * wave_map_block(w, t >> 1, n) + (t & 1)] = w * kMapEnvs + 63 - (int)(key & 63u);
+  wave_map[EPB * wave_map_block(w, t >> 1, n, streamed) + (t & 1)] = w * kMapEnvs + 63 - (int)(key & 63u);
 }
 
 __global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
@@ -2205,7 +2206,7 @@ __global__ __launch_bounds__(64) void k_obs(ObsArgs P) {
   const int n = P.n;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int any_reset = P.counters[0];
-  if (P.wave_map) build_wave_map(P.side, P.wave_map, n, blockIdx.x, threadIdx.x);
+  if (P.wave_map) build_wave_map(P.side, P.wave_map, n, P.map_streamed != 0, blockIdx.x, threadIdx.x);
   if (blockIdx.x == 0) {
     // the gate's inputs in one memory round trip: lane i < kCntSlots reads partial sum i, lane
     // kCntSlots the curriculum level (all issued before any store: the stores below may alias them)
@@ -2339,7 +2340,7 @@ __global__ __launch_bounds__(4 * kQuadEnvs) void k_quad(QuadArgs P) {
   const int n = P.n, nh = m.num_hinges, N = K.task.num_steps;
   const as_state_t& st = P.st;
   static_assert(kQuadEnvs == kMapEnvs, "a workgroup's envs are one placement chunk");
-  if (P.wave_map && tid < kMapEnvs) build_wave_map(P.side, P.wave_map, n, blockIdx.x, tid);  // (wave 0)
+  if (P.wave_map && tid < kMapEnvs) build_wave_map(P.side, P.wave_map, n, P.map_streamed != 0, blockIdx.x, tid);  // (wave 0)
   // ---- the model tables of the feet's chains, once per workgroup
   if (tid == 0) as_link_dof_map(m.cfg_dof_link, nh, AS_MAX_LINKS, qs.link_dof);
   if (tid < AS_MAX_LINKS) {
