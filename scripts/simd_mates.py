@@ -69,6 +69,18 @@ def main(n=4096, steps=30, warm=20):
             same += int(np.sum(mates == mates0))
     X = np.stack([np.ones(L * nb), own.ravel(), mate_rows.ravel()], axis=1)
     coef, *_ = np.linalg.lstsq(X, tot.ravel(), rcond=None)
+    # CU level: the rows of the other waves on the same CU (other SIMDs), and the block -> CU pattern
+    cu_rows = np.zeros((L, nb))
+    cu_of = []
+    for li in range(L):
+        ck = simd_key(R[li]) // 4
+        cu_of.append(ck)
+        sums = np.bincount(ck, weights=own[li], minlength=ck.max() + 1)
+        cu_rows[li] = sums[ck] - own[li] - mate_rows[li]
+    X2 = np.stack([np.ones(L * nb), own.ravel(), mate_rows.ravel(), cu_rows.ravel()], axis=1)
+    coef2, *_ = np.linalg.lstsq(X2, tot.ravel(), rcond=None)
+    ck0 = cu_of[0]
+    cu_blocks = [sorted(np.flatnonzero(ck0 == c).tolist()) for c in np.unique(ck0)[:3]]
     # env rows launch to launch (env id of block b, half h)
     # (only with the fixed placement: under the cost-balanced wave map the env of a block moves)
     c1 = None
@@ -82,6 +94,10 @@ def main(n=4096, steps=30, warm=20):
          "mates_same_as_launch0": round(same / max((L - 1) * nb, 1), 3),
          "mate_block_distance_top": [[int(k), int(v)] for k, v in sorted(zip(*np.unique(dist, return_counts=True)), key=lambda kv: -kv[1])[:10]],
          "fit_cycles": {"const": round(coef[0]), "per_own_row": round(coef[1], 1), "per_mate_row": round(coef[2], 1)},
+         "fit_cycles_cu": {"const": round(coef2[0]), "per_own_row": round(coef2[1], 1), "per_mate_row": round(coef2[2], 1),
+                           "per_cu_other_row": round(coef2[3], 1)},
+         "cu_same_as_launch0": round(float(np.mean([np.mean(c == ck0) for c in cu_of[1:]])), 3),
+         "cu_blocks_example": cu_blocks,
          "rows_mean": round(float(own.mean()), 2), "rows_p99": float(np.percentile(own, 99)),
          "env_rows_corr_next_launch": c1,
          "pairs_own_mate_rows_corr": round(float(np.corrcoef(own.ravel(), mate_rows.ravel())[0, 1]), 3),
