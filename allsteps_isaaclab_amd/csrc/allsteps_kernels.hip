@@ -2154,7 +2154,9 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2,
       st.body_pos[lane * n + e] = v;
     }
     if (lane == 0) {
-      P.side[kSideCost * n + e] = (uint32_t)s.nrows;
+      // an env reset in this launch starts the next one from the spawn pose in the air: no rows
+      // (its fallen-state rows predicted a heavy wave that was not; C3 +1 %, r06q)
+      P.side[kSideCost * n + e] = done ? 0u : (uint32_t)s.nrows;
       st.contact_mask[e] = s.mask[0];
       st.contact_mask[n + e] = s.mask[1];
       if (st.contact_mask_hind) {
