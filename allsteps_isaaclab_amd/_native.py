@@ -18,14 +18,14 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 
 MAXL, MAXG, MAXSP = 32, 32, 256
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 EXPORTED_SYMBOLS = [
     "as_create", "as_destroy", "as_reset_all", "as_step", "as_physics_step", "as_generate_stones",
     "as_step_counters", "as_get_curriculum_host", "as_abi_version", "as_last_error", "as_task_step",
     "as_set_seed", "as_profile", "as_profile_read", "as_debug_stamps", "as_reset_mask", "as_set_graph_safe",
     "as_profile_sampled", "as_hbm_copy", "as_set_actuator", "as_set_quad_task", "as_quad_step", "as_quad_reset_all",
-    "as_build_id", "as_step_counters_host", "as_body_state",
+    "as_build_id", "as_step_counters_host", "as_body_state", "as_sweep_plan",
 ]
 MAXB = 32  # AS_MAX_BODIES
 BODY_STATE_ROWS = 16  # AS_BODY_STATE_ROWS: pos 3 | quat 4 | frame lin vel 3 | ang vel 3 | COM lin vel 3
@@ -200,6 +200,7 @@ def load() -> C.CDLL:
     L.as_quad_step.argtypes = [V, V, V, V, V, V, V]
     L.as_quad_reset_all.argtypes = [V, V, V]
     L.as_body_state.argtypes = [V, V, V, V]
+    L.as_sweep_plan.argtypes = [V, C.POINTER(C.c_uint64)]
     L.as_last_error.restype = C.c_char_p
     L.as_build_id.restype = C.c_char_p
     for name in EXPORTED_SYMBOLS:
@@ -278,6 +279,18 @@ def build_native(verbose: bool = False) -> str:
 
 
 # ------------------------------------------------------------------------------------------ structs
+
+def sweep_plan(m: dict) -> tuple[int, int]:
+    """as_sweep_plan: (1 if the step kernel's compiled sweep skips hold for model `m`, else 0; the mask of
+    column quads that are exactly zero for it).  Host-only (no device)."""
+    L = load()
+    M = make_model(m)
+    mask = C.c_uint64(0)
+    rc = L.as_sweep_plan(C.byref(M), C.byref(mask))
+    if rc < 0:
+        raise NativeError(L.as_last_error().decode())
+    return rc, int(mask.value)
+
 
 def make_model(m: dict) -> AsModel:
     M = AsModel()

@@ -58,6 +58,7 @@ struct as_env {
   uint32_t* side_dev = nullptr;  // [kSideWords][n] k_step -> k_obs
   int32_t* wave_map_dev = nullptr;  // [n] cost-balanced placement (kMapEnvs), or null: xcd_block
   int32_t map_streamed = 0;         // k_step's grid is larger than the chip's workgroup slots
+  bool sweep_skip = false;          // the model admits the compiled sweep skips (as_sweep_plan)
   int32_t num_steps;
   int32_t nv;
   as::Consts host;        // host copy of consts_dev (as_set_actuator / as_set_quad_task re-upload it)
@@ -90,6 +91,19 @@ int as_hbm_copy(void* dst, const void* src, int64_t n16, void* stream) {
 }
 
 const char* as_last_error(void) { return g_err.c_str(); }
+
+int as_sweep_plan(const as_model_t* model, uint64_t* skip_mask) {
+  if (!model) return fail(AS_ERR_INVALID, "as_sweep_plan: null model");
+  const int nv = 6 + model->num_hinges;
+  if (!as::step_supported_nv(nv) || model->num_links < 1 || model->num_links > as::kMaxLinks)
+    return fail(AS_ERR_INVALID, "as_sweep_plan: no k_step instantiation for this model");
+  for (int i = 1; i < model->num_links; ++i)
+    if (model->parent[i] < 0 || model->parent[i] >= i) return fail(AS_ERR_INVALID, "as_sweep_plan: parent not topological");
+  const uint64_t valid = as::sweep_skip_mask(*model);
+  const uint64_t compiled = nv == 27 ? as::kSweepSkip27 : as::kSweepSkip18;
+  if (skip_mask) *skip_mask = valid;
+  return (compiled & ~valid) == 0ull ? 1 : 0;
+}
 
 int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, const as_task_t* task,
               const as_state_t* state, uint64_t seed, int32_t device, int64_t env_id_offset, as_env_t** out) {
@@ -202,6 +216,7 @@ int as_create(int32_t num_envs, const as_model_t* model, const as_sim_t* sim, co
   env->num_steps = task->num_steps;
   env->nv = h.nv;
   env->host = h;
+  env->sweep_skip = as_sweep_plan(model, nullptr) == 1;
   if (hipMalloc(&env->consts_dev, sizeof(as::Consts)) != hipSuccess ||
       hipMalloc(&env->counters_dev, 2 * as::kCntBank * sizeof(int32_t)) != hipSuccess ||
       hipMalloc(&env->side_dev, (size_t)as::kSideWords * num_envs * sizeof(uint32_t)) != hipSuccess) {
@@ -278,7 +293,7 @@ static int run(as_env_t* env, int mode, const float* actions, float* obs, float*
   a.wave_map = env->wave_map_dev;
   const bool prof = env->prof_n < env->prof_cap && (env->prof_calls++ % env->prof_stride) == 0;
   if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n], s));
-  HIP_TRY(as::launch_step(a, env->nv, s));
+  HIP_TRY(as::launch_step(a, env->nv, env->sweep_skip, s));
   if (prof) HIP_TRY(hipEventRecord(env->ev[3 * env->prof_n + 1], s));
   if (mode == as::kModePhysics) {
     if (prof) {

@@ -157,9 +157,18 @@ struct BodyArgs {
   as_body_table_t bodies;
 };
 
+// The H^-1 sweep's skipped column quads (allsteps_kernels.hip sweep_inverse; bit r (NB - 1) + jb: round
+// r, quad jb of the rotated row), compiled for the Allsteps walker (27 dofs) and the C5 quadruped (18):
+// the quads in which the pivot rows are structurally zero for those trees.  as_create runs the
+// structural sweep for the model it is given (sweep_skip_mask) and launches the skipping kernel only if
+// every compiled bit is also set for that model.
+constexpr uint64_t kSweepSkip27 = 207817167ull;  // 14 of the walker's 42 quad updates
+constexpr uint64_t kSweepSkip18 = 3219ull;       // 6 of the quadruped's 20
+uint64_t sweep_skip_mask(const as_model_t& m);  // the model's exactly-zero quads (host)
+
 bool step_supported_nv(int nv);
 hipError_t launch_body_state(const BodyArgs& a, hipStream_t stream);
-hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream);
+hipError_t launch_step(const StepArgs& a, int nv, bool sweep_skip, hipStream_t stream);
 hipError_t launch_obs(const ObsArgs& a, hipStream_t stream);
 hipError_t launch_stones(const StonesArgs& a, hipStream_t stream);
 hipError_t launch_quad(const QuadArgs& a, hipStream_t stream);

@@ -830,45 +830,70 @@ __device__ __forceinline__ void block_inverse(float (&M)[B][B]) {  // M <- M^-1 
   }
 }
 
+// The sweep's layout (include/as_detmath.h AS_SWEEP_PAD): the NV dofs padded to NP with identity rows /
+// columns at padded index PAD, the NB = NP / 4 pivot blocks swept LAST block first (the limbs before the
+// root).  A lane keeps ITS dof's row (lane k < NV: dof k, padded row padded(k); lane NV + q: pad row
+// PAD + q), so no row moves between lanes; the columns start in the round-0 rotated order -- blocks
+// NB - 1, NB - 2, ..., 0, natural order inside a block -- which the rotation below returns to after the
+// last round.  SKIP bit r (NB - 1) + jb: in round r the pivot rows are exactly zero in column quad jb
+// (as_create's structural check, sweep_skip_mask): that quad's update is the identity and is not issued
+// (the pivot rows' zeros are +0 and stay +0, so every skipped fmaf would have returned its addend bit for
+// bit; the oracle performs them).
+template <int NV>
+struct SweepLayout {
+  static constexpr int NP = (NV + kSweepB - 1) / kSweepB * kSweepB;
+  static constexpr int NB = NP / kSweepB;
+  static constexpr int NQ = NB - 1;
+  static constexpr int PAD = AS_SWEEP_PAD(NV);
+  static constexpr int padded(int k) { return k < PAD ? k : k + (NP - NV); }
+  static constexpr int pos(int P) { return (NB - 1 - P / kSweepB) * kSweepB + P % kSweepB; }  // round-0 register
+};
+
 // Software-pipelined and branch-free.  Every lane publishes its whole rotated row each round (no
 // pivot-lane branch: the sweep is one basic block, so the scheduler can interleave across rounds), and
 // its new leading quad -- the next round's pivot columns -- first: right after that store every lane
 // reads the next pivot block back and inverts it, and the 4x4 inverse's division chain overlaps the
 // round's remaining column updates instead of heading the next round.  Per element the operations
 // and their order are those of oracle/physics.c sweep_inverse: only the issue order changes.
-template <int NP, int B>
-__device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
-  static_assert(NP % B == 0, "padded order");
+template <int NV, uint64_t SKIP>
+__device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[SweepLayout<NV>::NP]) {
+  typedef SweepLayout<NV> L;
+  constexpr int NP = L::NP, NB = L::NB, NQ = L::NQ, B = kSweepB;
   static_assert(B == 4, "16-B pivot rows");
   static_assert(NP <= 28, "row buffer stride");
+  static_assert(NQ * NB <= 64, "skip mask bits");
+  // this lane's padded row
+  const int prow = lane < NV ? (lane < L::PAD ? lane : lane + (NP - NV)) : (lane < NP ? L::PAD + (lane - NV) : lane);
   // LDS operations of a wave complete in issue order: a round's stores cannot overtake the previous
   // round's reads of the same rows.  Explicit 16-B accesses on a native 4-vector type (float4 is a
   // struct whose copies SROA splits into b96 + b32 pairs)
   float(*Rw)[28] = s.x.sw.rows;
-  v4f* own = reinterpret_cast<v4f*>(Rw[lane]);
+  v4f* own = reinterpret_cast<v4f*>(Rw[prow]);
 #pragma unroll
   for (int j = 0; j < NP; j += 4) own[j / 4] = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
   __syncthreads();
   float D[B][B];
 #pragma unroll
   for (int a = 0; a < B; ++a) {
-    const v4f d = *reinterpret_cast<const v4f*>(Rw[a]);
+    const v4f d = *reinterpret_cast<const v4f*>(Rw[(NB - 1) * B + a]);
     D[a][0] = d.x; D[a][1] = d.y; D[a][2] = d.z; D[a][3] = d.w;
   }
   block_inverse<B>(D);
-  // unrolled over the 7 rounds: the column rotation is then register renaming and the pivot lanes /
-  // padding are known per round
+  // unrolled over the rounds: the column rotation is then register renaming and the pivot lanes /
+  // padding / skipped quads are known per round
 #pragma unroll
-  for (int p = 0; p < NP; p += B) {
-    const int t = lane - p;
+  for (int r = 0; r < NB; ++r) {
+    const int p = (NB - 1 - r) * B;  // the pivot block's padded rows
+    const int t = prow - p;
     const bool piv = (unsigned)t < (unsigned)B;
-    constexpr int NQ = NP / 4 - 1;  // column quads past the pivot columns
-    // the pivot rows' other columns (stored last round, or above for p = 0)
+    // the pivot rows' other columns (stored last round, or above for r = 0); a skipped quad's are
+    // never read
     v4f x[NQ][B];
 #pragma unroll
     for (int jb = 0; jb < NQ; ++jb)
 #pragma unroll
-      for (int c = 0; c < B; ++c) x[jb][c] = *reinterpret_cast<const v4f*>(&Rw[p + c][B + 4 * jb]);
+      for (int c = 0; c < B; ++c)
+        if (!((SKIP >> (r * NQ + jb)) & 1ull)) x[jb][c] = *reinterpret_cast<const v4f*>(&Rw[p + c][B + 4 * jb]);
     // packed pairs written out (the file is built without the SLP vectorizer, which elsewhere paid
     // for its pairs with register moves); per element the same operations in the same order
     float alpha = 1.f, beta[B];
@@ -891,20 +916,30 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
 #pragma unroll
     for (int jb = 0; jb < NQ; ++jb) {
       const int j = B + 4 * jb;
-      v2f lo = v2f{alpha, alpha} * v2f{Hr[j], Hr[j + 1]}, hi = v2f{alpha, alpha} * v2f{Hr[j + 2], Hr[j + 3]};
+      v2f lo, hi;
+      if ((SKIP >> (r * NQ + jb)) & 1ull) {
+        // the pivot rows are +0 in this quad: alpha a - sum (+-0) = a, for the pivot lanes too (their
+        // own entries here are those +0)
+        lo = v2f{Hr[j], Hr[j + 1]};
+        hi = v2f{Hr[j + 2], Hr[j + 3]};
+      } else {
+        lo = v2f{alpha, alpha} * v2f{Hr[j], Hr[j + 1]};
+        hi = v2f{alpha, alpha} * v2f{Hr[j + 2], Hr[j + 3]};
 #pragma unroll
-      for (int c = 0; c < B; ++c) {
-        lo = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[jb][c].xy, lo);
-        hi = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[jb][c].zw, hi);
+        for (int c = 0; c < B; ++c) {
+          lo = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[jb][c].xy, lo);
+          hi = __builtin_elementwise_fma(v2f{-beta[c], -beta[c]}, x[jb][c].zw, hi);
+        }
       }
       Hr[j - B] = lo.x; Hr[j + 1 - B] = lo.y; Hr[j + 2 - B] = hi.x; Hr[j + 3 - B] = hi.y;
-      if (jb == 0 && p + B < NP) {
-        // the next round's pivot block: published, read back and inverted under the rest of the round
+      if (jb == 0 && r + 1 < NB) {
+        // the next round's pivot block (padded rows p - B ..): published, read back and inverted under
+        // the rest of the round
         own[0] = v4f{lo.x, lo.y, hi.x, hi.y};
         __builtin_amdgcn_wave_barrier();  // one wave: the store above reaches LDS before these reads
 #pragma unroll
         for (int a = 0; a < B; ++a) {
-          const v4f d = *reinterpret_cast<const v4f*>(Rw[p + B + a]);
+          const v4f d = *reinterpret_cast<const v4f*>(Rw[p - B + a]);
           Dn[a][0] = d.x; Dn[a][1] = d.y; Dn[a][2] = d.z; Dn[a][3] = d.w;
         }
         block_inverse<B>(Dn);
@@ -912,7 +947,7 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[NP]) {
     }
 #pragma unroll
     for (int c = 0; c < B; ++c) Hr[NP - B + c] = beta[c];
-    if (p + B < NP) {
+    if (r + 1 < NB) {
 #pragma unroll
       for (int j = B; j < NP; j += 4) own[j / 4] = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
       __builtin_amdgcn_wave_barrier();
@@ -1455,7 +1490,7 @@ __device__ __forceinline__ void pgs_sweeps(const EnvS& s, int iters, float& uj, 
   }
 }
 
-template <int NV>
+template <int NV, uint64_t SKIP>
 __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const Topo& tp0, const GeomC& gc,
                         const LinkC& lc, uint32_t (&mask_out)[4], Stamp& ts) {
   // Opaque copies of the constants pointer and the lane id: everything derived from them below
@@ -1486,15 +1521,25 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   float Sj[6], Fj[6];  // dof lane j: S_j and Ic_link(j) S_j for the H rows
   dynamics(K, s, lane, tp, K.sim.gravity, Sj, Fj, smp);
   ts.mark(kStLinkQ);
-  constexpr int NP = (NV + kSweepB - 1) / kSweepB * kSweepB;  // sweep order, padded with identity
+  typedef SweepLayout<NV> SL;
+  constexpr int NP = SL::NP;
   float Hr[NP];
   h_row<NV>(s, lane, tp, gc.anc, Sj, Fj, *reinterpret_cast<float(*)[NV]>(Hr));
-#pragma unroll
-  for (int j = NV; j < NP; ++j) Hr[j] = lane == j ? 1.f : 0.f;
   ts.mark(kStDyn);
-  sweep_inverse<NP, kSweepB>(s, lane, Hr);  // Hr <- row `lane` of -H^-1
+  {
+    // into the sweep's round-0 column order with the identity pad rows / columns (register renaming),
+    // the sweep, and back: row `lane` of H^-1 in dof order
+    float Hs[NP];
 #pragma unroll
-  for (int j = 0; j < NV; ++j) Hr[j] = lane < NV ? -Hr[j] : 0.f;
+    for (int k = 0; k < NV; ++k) Hs[SL::pos(SL::padded(k))] = Hr[k];
+#pragma unroll
+    for (int q = 0; q < NP - NV; ++q) Hs[SL::pos(SL::PAD + q)] = lane == NV + q ? 1.f : 0.f;
+    sweep_inverse<NV, SKIP>(s, lane, Hs);  // Hs <- this lane's row of -H^-1
+#pragma unroll
+    for (int k = 0; k < NV; ++k) Hr[k] = lane < NV ? -Hs[SL::pos(SL::padded(k))] : 0.f;
+#pragma unroll
+    for (int k = NV; k < NP; ++k) Hr[k] = 0.f;
+  }
   ts.mark(kStChol);
   // u* = u + dt H^-1 b   (b broadcast from LDS)
   float uj = 0.f;
@@ -1826,7 +1871,7 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
 constexpr int kStepThreads = 64;
 static_assert(kStepThreads == 64, "k_step assumes a one-wave (wave64) workgroup: see the FK rounds");
 
-template <int NV>
+template <int NV, uint64_t SKIP>
 __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_step(StepArgs P) {
   __shared__ Smem sm;
   // model / plan constants stay in global memory (5.7 KB, L1/K$-resident): LDS is the occupancy
@@ -1883,7 +1928,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(2,
   // ---- physics
   if (do_physics) {
     const GeomC gc = load_geom(K, lane);
-    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV>(K, sm, s, lane, tp, gc, lc, mask, ts);
+    for (int sub = 0; sub < K.sim.substeps; ++sub) substep<NV, SKIP>(K, sm, s, lane, tp, gc, lc, mask, ts);
   }
   // This lane's reset constants (joint `lane` in cfg order: its link and limits, the start pose plain and
   // mirrored), loaded ahead of the final FK so that their global loads (L2 round trips) run under it
@@ -2570,12 +2615,62 @@ hipError_t launch_quad(const QuadArgs& a, hipStream_t stream) {
 // (model/anymal_c.xml, 6 + 12 hinges), stepped through as_physics_step.
 bool step_supported_nv(int nv) { return nv == 27 || nv == 18; }
 
-hipError_t launch_step(const StepArgs& a, int nv, hipStream_t stream) {
+// The structural sweep (host): which column quads of which rounds the pivot rows are exactly zero in,
+// for this model's tree under the sweep's layout and round order (SweepLayout).  H_ij is nonzero only
+// when the links of dofs i and j are on one root path (h_row writes +0 elsewhere); a round on block P
+// leaves (i, j) zero unless it was nonzero or both a_iP and a_Pj have a nonzero entry, sets the pivot
+// columns where a_iP has one and the pivot rows where a_Pj has one -- a zero stays +0 through every such
+// update (its products all have a +0 factor and start from +0), which is what makes a skipped quad exact.
+uint64_t sweep_skip_mask(const as_model_t& m) {
+  const int nl = m.num_links, nv = 6 + m.num_hinges;
+  const int NP = (nv + kSweepB - 1) / kSweepB * kSweepB, NB = NP / kSweepB, NQ = NB - 1, PAD = AS_SWEEP_PAD(nv);
+  if (NP > 32 || NQ * NB > 64 || nl < 1 || nl > kMaxLinks) return 0ull;
+  auto padded = [&](int k) { return k < PAD ? k : k + (NP - nv); };
+  auto link = [](int d) { return d < 6 ? 0 : d - 5; };
+  auto on_path = [&](int a, int l) {  // a is l or one of its ancestors
+    for (int x = l; x >= 0; x = x > 0 ? m.parent[x] : -1)
+      if (x == a) return true;
+    return false;
+  };
+  bool S[32][32] = {};
+  for (int i = 0; i < nv; ++i)
+    for (int j = 0; j < nv; ++j)
+      S[padded(i)][padded(j)] = on_path(link(i), link(j)) || on_path(link(j), link(i));
+  for (int q = 0; q < NP - nv; ++q) S[PAD + q][PAD + q] = true;
+  uint64_t mask = 0ull;
+  for (int r = 0; r < NB; ++r) {
+    const int b = NB - 1 - r, p = kSweepB * b;
+    bool colany[32] = {}, rowany[32] = {};
+    for (int c = 0; c < kSweepB; ++c)
+      for (int k = 0; k < NP; ++k) {
+        colany[k] = colany[k] || S[p + c][k];
+        rowany[k] = rowany[k] || S[k][p + c];
+      }
+    for (int jb = 0; jb < NQ; ++jb) {
+      const int bb = ((b - 1 - jb) % NB + NB) % NB;
+      bool any = false;
+      for (int c = 0; c < kSweepB; ++c) any = any || colany[kSweepB * bb + c];
+      if (!any) mask |= 1ull << (r * NQ + jb);
+    }
+    for (int i = 0; i < NP; ++i)
+      for (int j = 0; j < NP; ++j) {
+        const bool pi = i >= p && i < p + kSweepB, pj = j >= p && j < p + kSweepB;
+        S[i][j] = pi && pj ? true : pj ? rowany[i] : pi ? colany[j] : (S[i][j] || (rowany[i] && colany[j]));
+      }
+  }
+  return mask;
+}
+
+hipError_t launch_step(const StepArgs& a, int nv, bool sweep_skip, hipStream_t stream) {
   int blocks = (a.n + EPB - 1) / EPB;
-  if (nv == 27)
-    hipLaunchKernelGGL(k_step<27>, dim3(blocks), dim3(kStepThreads), 0, stream, a);
+  if (nv == 27 && sweep_skip)
+    hipLaunchKernelGGL((k_step<27, kSweepSkip27>), dim3(blocks), dim3(kStepThreads), 0, stream, a);
+  else if (nv == 27)
+    hipLaunchKernelGGL((k_step<27, 0ull>), dim3(blocks), dim3(kStepThreads), 0, stream, a);
+  else if (nv == 18 && sweep_skip)
+    hipLaunchKernelGGL((k_step<18, kSweepSkip18>), dim3(blocks), dim3(kStepThreads), 0, stream, a);
   else if (nv == 18)
-    hipLaunchKernelGGL(k_step<18>, dim3(blocks), dim3(kStepThreads), 0, stream, a);
+    hipLaunchKernelGGL((k_step<18, 0ull>), dim3(blocks), dim3(kStepThreads), 0, stream, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

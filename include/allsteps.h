@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define AS_ABI_VERSION 4
+#define AS_ABI_VERSION 5
 #define AS_MAX_LINKS 32
 #define AS_MAX_GEOMS 32
 #define AS_MAX_SELF_PAIRS 256
@@ -295,6 +295,15 @@ typedef struct {
   float com[AS_MAX_BODIES][3];          /* the body's own centre of mass, body frame */
 } as_body_table_t;
 int as_body_state(as_env_t* env, const as_body_table_t* bodies_host, float* out, void* stream);
+
+/* The H^-1 sweep plan for a model (round 6, ABI 5; no device needed).  The step kernel sweeps the
+ * padded joint-space inertia last block first and, for the trees it is compiled for (the walker, the
+ * C5 quadruped), skips the column quads in which the pivot rows are structurally zero -- an exact
+ * identity, so results do not depend on it.  Returns 1 when the compiled skips hold for `model` (as_create
+ * then launches the skipping kernel), 0 when they do not (the full sweep runs), <0 on an invalid model;
+ * *skip_mask (if not NULL) receives the quads that are zero for this model (bit r (NB-1) + q: round r,
+ * quad q).  Replaces nothing in the reference: PhysX factors the articulation internally. */
+int as_sweep_plan(const as_model_t* model, uint64_t* skip_mask);
 
 /* Per-launch timing: record HIP events around the step kernel (k_step) and the observation
  * kernel (k_obs) of the next `max_launches` calls on their own stream; as_profile_read

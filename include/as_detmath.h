@@ -28,6 +28,14 @@
 #define AS_HD static inline
 #endif
 
+/* The H^-1 sweep's layout (csrc/allsteps_kernels.hip sweep_inverse, oracle/physics.c sweep_inverse):
+ * the nv dofs are padded to a multiple of 4 with identity rows / columns inserted at padded index
+ * AS_SWEEP_PAD(nv) (dof k < pad -> k, else k + the pad count), and the 4 x 4 pivot blocks are swept
+ * LAST block first -- the limbs (the high dof indices of a topological order) before the root, so the
+ * columns of the other limbs stay exactly zero through the first rounds.  The pad position aligns the
+ * walker's arms (dofs 19-22, 23-26) and the quadruped's last leg to whole blocks. */
+#define AS_SWEEP_PAD(nv) ((nv) == 27 ? 19 : (nv) == 18 ? 15 : (nv))
+
 /* dot products: fmaf chain from the first product, ascending index */
 AS_HD float as_dot3(const float* a, const float* b) { return fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0])); }
 

@@ -302,7 +302,8 @@ static void rnea_bias(const or_model_t* m, const kin_t* K, const float* u, float
 /* Inverse of the SPD joint-space inertia by the block sweep operator on SWEEP_B x SWEEP_B pivot
  * blocks (no pivoting needed for SPD), in the arithmetic of the HIP kernel (sweep_inverse /
  * block_inverse in csrc/allsteps_kernels.hip).  The matrix is padded to a multiple of SWEEP_B with
- * identity rows/columns.  Round on P = {p..p+B-1}: D = (a_PP)^-1 by 2x2-block Schur complement;
+ * identity rows/columns at AS_SWEEP_PAD(n), and the blocks are swept last block first (the limbs
+ * before the root).  Round on P = {p..p+B-1}: D = (a_PP)^-1 by 2x2-block Schur complement;
  * row'_j = alpha a_ij - sum_c beta_c a_Pc,j for j not in P, row'_P = beta, where
  * (alpha, beta) = (1, a_iP D) for i not in P and (0, -D_t) for pivot row t.  After all rounds
  * a = -H^-1; the result is negated. */
@@ -343,13 +344,19 @@ static void block_inverse(float M[SWEEP_B][SWEEP_B]) {
     }
 }
 
+/* dof k's row / column in the padded order (AS_SWEEP_PAD, include/as_detmath.h) */
+static int sweep_padded(int k, int n, int np) { return k < AS_SWEEP_PAD(n) ? k : k + (np - n); }
+
 static void sweep_inverse(float* h, int n) {
   const int np = (n + SWEEP_B - 1) / SWEEP_B * SWEEP_B;
   float a[NV_MAX + SWEEP_B][NV_MAX + SWEEP_B];
   float out[NV_MAX + SWEEP_B];
   for (int i = 0; i < np; ++i)
-    for (int j = 0; j < np; ++j) a[i][j] = (i < n && j < n) ? h[i * n + j] : (i == j ? 1.f : 0.f);
-  for (int p = 0; p < np; p += SWEEP_B) {
+    for (int j = 0; j < np; ++j) a[i][j] = i == j ? 1.f : 0.f;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) a[sweep_padded(i, n, np)][sweep_padded(j, n, np)] = h[i * n + j];
+  /* the last pivot block first (the kernel's round order) */
+  for (int p = np - SWEEP_B; p >= 0; p -= SWEEP_B) {
     float D[SWEEP_B][SWEEP_B], Q[SWEEP_B][NV_MAX + SWEEP_B];
     for (int x = 0; x < SWEEP_B; ++x)
       for (int c = 0; c < SWEEP_B; ++c) D[x][c] = a[p + x][p + c];
@@ -378,7 +385,7 @@ static void sweep_inverse(float* h, int n) {
     }
   }
   for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) h[i * n + j] = -a[i][j];
+    for (int j = 0; j < n; ++j) h[i * n + j] = -a[sweep_padded(i, n, np)][sweep_padded(j, n, np)];
 }
 
 /* x = A b (row-major, fmaf chain ascending in k) */

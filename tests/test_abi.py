@@ -262,3 +262,68 @@ def test_loader_refuses_a_library_built_from_other_sources(monkeypatch):
     monkeypatch.setenv("ALLSTEPS_HIP_LIB", _native.LIB_PATH)
     monkeypatch.setenv("PPO_HIP_LIB", _native.PPO_LIB_PATH)
     assert _native.load() is not None and fused.load() is not None
+
+
+def _structural_skip_mask(m: dict) -> int:
+    """Python restatement of the kernel's structural sweep (csrc/allsteps_kernels.hip sweep_skip_mask):
+    padded layout AS_SWEEP_PAD, last block first, a quad skippable when the pivot rows are zero there."""
+    import numpy as np
+
+    nl, nv = int(m["num_links"]), 6 + int(m["num_hinges"])
+    parent = [int(x) for x in m["parent"][:nl]]
+    NP = (nv + 3) // 4 * 4
+    NB, PAD = NP // 4, {27: 19, 18: 15}.get(nv, nv)
+    NQ = NB - 1
+
+    def on_path(a, l):
+        while l >= 0:
+            if l == a:
+                return True
+            l = parent[l] if l > 0 else -1
+        return False
+
+    link = lambda d: 0 if d < 6 else d - 5  # noqa: E731
+    padded = lambda k: k if k < PAD else k + (NP - nv)  # noqa: E731
+    S = np.zeros((NP, NP), bool)
+    for i in range(nv):
+        for j in range(nv):
+            S[padded(i), padded(j)] = on_path(link(i), link(j)) or on_path(link(j), link(i))
+    for q in range(NP - nv):
+        S[PAD + q, PAD + q] = True
+    mask = 0
+    for r in range(NB):
+        b = NB - 1 - r
+        P = list(range(4 * b, 4 * b + 4))
+        colany, rowany = S[P, :].any(0), S[:, P].any(1)
+        for jb in range(NQ):
+            bb = (b - 1 - jb) % NB
+            if not colany[4 * bb: 4 * bb + 4].any():
+                mask |= 1 << (r * NQ + jb)
+        S = S | np.outer(rowany, colany)
+        S[:, P] = rowany[:, None]
+        S[P, :] = colany[None, :]
+        S[np.ix_(P, P)] = True
+    return mask
+
+
+def test_sweep_plan_skips_only_structural_zeros():
+    """as_sweep_plan (no device): the walker and the C5 quadruped take the compiled sweep skips (their
+    structurally-zero quads include every compiled one: 14 of the walker's 42 quad updates, 6 of the
+    quadruped's 20), the C++ structural sweep equals its Python restatement, and a tree whose zeros do not
+    cover the compiled skips (a chain: every dof on one root path) falls back to the full sweep."""
+    from allsteps_isaaclab_amd import _native
+    from allsteps_isaaclab_amd.model import ANYMAL_C_JSON, load_model
+
+    walker, quad = load_model(), load_model(ANYMAL_C_JSON)
+    for m, compiled, n in ((walker, 207817167, 14), (quad, 3219, 6)):
+        use, mask = _native.sweep_plan(m)
+        assert use == 1 and mask & compiled == compiled and bin(compiled).count("1") == n
+        assert mask == _structural_skip_mask(m)
+    chain = dict(walker)
+    chain["parent"] = [-1] + list(range(walker["num_links"] - 1)) + [0] * (len(walker["parent"]) - walker["num_links"])
+    use, mask = _native.sweep_plan(chain)
+    assert use == 0 and mask == _structural_skip_mask(chain) == 0
+    bad = dict(walker)
+    bad["parent"] = [-1, 3] + list(walker["parent"][2:])
+    with pytest.raises(_native.NativeError, match="topological"):
+        _native.sweep_plan(bad)
