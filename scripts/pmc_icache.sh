@@ -22,7 +22,7 @@ import csv, glob, sys
 per = {}
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith("void as::k_step<27>"):
+        if r["Kernel_Name"].startswith(("void as::k_step<27>", "void as::k_step<27, ")):
             k = (r["Dispatch_Id"], r["Counter_Name"])
             per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
 tot = {}

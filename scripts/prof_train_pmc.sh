@@ -14,7 +14,7 @@ done
 python3 - "$O" <<'PY'
 import collections, csv, glob, json, sys
 o = sys.argv[1]
-keys = ("k_mlp_fwd<2, 21>", "k_mlp_bwd<2>", "k_wgrad<2>", "k_reduce_rows", "k_adam<true>", "k_step<27>")
+keys = ("k_mlp_fwd<2, 21>", "k_mlp_bwd<2>", "k_wgrad<2>", "k_reduce_rows", "k_adam<true>", "k_step<27")
 res = collections.defaultdict(dict)
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
