@@ -760,14 +760,18 @@ __device__ __forceinline__ void h_row(EnvS& s, int lane, const Topo& tp, uint32_
       *reinterpret_cast<v4f*>(&M[lane][4 * q]) = v4f{e[0], e[1], e[2], e[3]};
     }
   }
+  // the root's six dofs are on every dof's path (ancmask bits 0-5, as_create), so their entries are
+  // never taken from the transpose: those reads and selects are not issued (lanes >= NV keep the +0 of
+  // the select above, as before)
+  constexpr int kRootDofs = 6;
   const int jj = lane < NV ? lane : NV;
   float t[NV];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) t[k] = M[k][jj];
+  for (int k = kRootDofs; k < NV; ++k) t[k] = M[k][jj];
   // (a register value, not a load: a select between two loads becomes a load from a selected
   // address, which puts Hr in scratch)
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
+  for (int k = kRootDofs; k < NV; ++k) {
     asm volatile("" : "+v"(t[k]));
     Hr[k] = (on >> k) & 1u ? Hr[k] : t[k];
   }
