@@ -873,8 +873,11 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[SweepLayout<NV>::NP
   // struct whose copies SROA splits into b96 + b32 pairs)
   float(*Rw)[28] = s.x.sw.rows;
   v4f* own = reinterpret_cast<v4f*>(Rw[prow]);
+  // a row quad is stored only if the next round reads it: round r reads quad jb of its pivot rows
+  // unless SKIP says those are +0 (the rows are LDS scratch, dead after the sweep)
 #pragma unroll
-  for (int j = 0; j < NP; j += 4) own[j / 4] = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
+  for (int j = 0; j < NP; j += 4)
+    if (j == 0 || !((SKIP >> (j / 4 - 1)) & 1ull)) own[j / 4] = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
   __syncthreads();
   float D[B][B];
 #pragma unroll
@@ -953,7 +956,8 @@ __device__ void sweep_inverse(EnvS& s, int lane, float (&Hr)[SweepLayout<NV>::NP
     for (int c = 0; c < B; ++c) Hr[NP - B + c] = beta[c];
     if (r + 1 < NB) {
 #pragma unroll
-      for (int j = B; j < NP; j += 4) own[j / 4] = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
+      for (int j = B; j < NP; j += 4)
+        if (!((SKIP >> ((r + 1) * NQ + j / 4 - 1)) & 1ull)) own[j / 4] = v4f{Hr[j], Hr[j + 1], Hr[j + 2], Hr[j + 3]};
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int a = 0; a < B; ++a)
