@@ -589,6 +589,7 @@ __device__ __forceinline__ void mfma_columns(const f32x32& acc, float (&col)[32]
 // steps, an fmaf chain over l ascending from +0 for every (quantity, link) -- the root's row is the
 // whole tree (oracle/physics.c subtree_sums restates the chain).  Then per dof j: C_j = S_j . F_link(j),
 // b_j = tau_j - C_j (returned, also in LDS), Fh_j = Ic_link(j) S_j.
+template <int NV>
 __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, const Topo& tp, float gravity,
                                           float (&Sj)[6], float (&Fj)[6], int max_path) {
   const as_model_t& m = K.model;
@@ -675,8 +676,13 @@ __device__ __forceinline__ float dynamics(const Consts& K, EnvS& s, int lane, co
     }
     typedef float f32x16 __attribute__((ext_vector_type(16)));
     f32x16 acc = {};
+    // only the instructions that hold a link: num_links = NV - 5 (as_create: one hinge per non-root
+    // link), and a slot past it adds +0 products to an accumulator that started at +0 -- the same bits
+    // (the walker's 22 links use 11 of the 12 steps, the quadruped's 13 links 7)
+    constexpr int kSubSteps = (NV - 5 + 1) / 2;
+    static_assert(kSubSteps <= LMAX / 2, "link slots");
 #pragma unroll
-    for (int t = 0; t < LMAX / 2; ++t)
+    for (int t = 0; t < kSubSteps; ++t)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[t], (float)((sub >> (2 * t)) & 1u), acc, 0, 0, 0);
     float col[16];
 #pragma unroll
@@ -1530,7 +1536,7 @@ __device__ void substep(const Consts& K0, Smem& sm, EnvS& s, int lane0, const To
   fk<true>(K, s, lane, tp, lc, smp);  // (its first barrier publishes tau before the dynamics read it)
   ts.mark(kStFK);
   float Sj[6], Fj[6];  // dof lane j: S_j and Ic_link(j) S_j for the H rows
-  dynamics(K, s, lane, tp, K.sim.gravity, Sj, Fj, smp);
+  dynamics<NV>(K, s, lane, tp, K.sim.gravity, Sj, Fj, smp);
   ts.mark(kStLinkQ);
   typedef SweepLayout<NV> SL;
   constexpr int NP = SL::NP;
