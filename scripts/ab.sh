@@ -13,7 +13,7 @@ import json,sys
 d=json.loads(sys.stdin.read()); L=d['roofline']['latency']
 print('$1 N=$2', 'value %.4g' % d['value'], 'k_step', d['kernels_ms']['k_step_ms'], 'period', d['kernels_ms']['k_step_period_ms'], 'k_obs', d['kernels_ms']['k_obs_ms'], 'ms', d['ms_per_step'],
       'crit', {k: L['critical_path_phases'][k] for k in ('collide','pgs','sweep','wsolve','rows')},
-      'meanpgs', L['mean_phases']['pgs'], 'meansweep', L['mean_phases']['sweep'], 'max', L['max_wave_cycles'], 'avg', L['avg_wave_cycles'])" | tee -a $OUT
+      'meancollide', L['mean_phases']['collide'], 'meanpgs', L['mean_phases']['pgs'], 'meansweep', L['mean_phases']['sweep'], 'max', L['max_wave_cycles'], 'avg', L['avg_wave_cycles'])" | tee -a $OUT
 }
 for rep in 1 2; do
   for lib in base "$@"; do
