@@ -1085,8 +1085,11 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   // appends the surviving (stone, geom) pairs to a list in LDS, in emission order.  (B) lane = pair,
   // in chunks of kPairsPerChunk: the exact test (capsules: slope bisection for the segment's closest
   // point) and the contacts, emitted in list order by a prefix sum.  A chunk is flushed as soon as
-  // kPairsPerChunk pairs are pending, so the list never exceeds 32 + 22 entries; the search runs over
-  // every pair even past ncap contacts (the surplus is counted, not emitted).
+  // either env of the wave has kPairsPerChunk pairs pending, by both envs together (the other one
+  // flushes its partial list: chunk boundaries change neither the contacts nor their order, and one
+  // flush for the wave replaces one per env under divergence), so the list never exceeds 32 + 22
+  // entries; the search runs over every pair even past ncap contacts (the surplus is counted, not
+  // emitted).
   {
     float* gs = s.x.col.g[lane];  // staging of this lane's geom for pass B and the self pairs
     if (gv) {
@@ -1103,7 +1106,7 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
     int cnt = 0, plink = 0, pst = 0, pfoot = -1;
     float P0[3], N0[3], P1[3], N1[3], P2[3], N2[3], SEP0 = 0.f, SEP1 = 0.f, SEP2 = 0.f, pr = 0.f;
     const bool act = lane < npairs;
-    const int e = pl[act ? lane : 0];
+    const int e = act ? pl[lane] : 0;  // (an env with nothing pending flushes too: stone 0, geom 0)
     const int gi = e & 0xff;
     pst = e >> 8;
     const float* gq = s.x.col.g[gi];
@@ -1116,9 +1119,10 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
     float c[3];
     for (int k = 0; k < 3; ++k) c[k] = s.stones[3 * pst + k] - s.root_pos[k];
     // capsule: minimum of the (convex) signed distance along the segment by bisection on the sign
-    // of its slope.  Runs for every lane (the result is only used by capsule pairs).
+    // of its slope.  Runs for every lane (the result is only used by capsule pairs); unrolled by 4
+    // (by 2: +0.6 % step time, profiles/r06z7_ab_flush_unroll.log).
     float lo = 0.f, hi = 1.f;
-#pragma unroll 2
+#pragma unroll 4
     for (int it = 0; it < kBisectIters; ++it) {
       const float t = 0.5f * (lo + hi);
       const bool up = sd_box_slope(A, Bb, t, c, h) > 0.f;
@@ -1126,17 +1130,17 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
       lo = up ? lo : t;
     }
     if (act) {
-      float nr[3];
+      // the segment's first point: the sphere's test and the capsule's t = 0 end are the same value
+      float n0[3];
+      const float s0 = sd_box(A, c, h, n0) - pr;
       if (pty == 0) {
-        float sd = sd_box(A, c, h, nr) - pr;
-        if (sd < margin) {
-          for (int k = 0; k < 3; ++k) { P0[k] = A[k]; N0[k] = nr[k]; }
-          SEP0 = sd;
+        if (s0 < margin) {
+          for (int k = 0; k < 3; ++k) { P0[k] = A[k]; N0[k] = n0[k]; }
+          SEP0 = s0;
           cnt = 1;
         }
       } else {
-        float n0[3], n1[3];
-        float s0 = sd_box(A, c, h, n0) - pr;
+        float n1[3];
         float s1 = sd_box(Bb, c, h, n1) - pr;
         float ts = 0.5f * (lo + hi), Ps[3], ns[3];
         for (int k = 0; k < 3; ++k) Ps[k] = A[k] + ts * (Bb[k] - A[k]);
@@ -1193,14 +1197,17 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   }
   __syncthreads();
   const uint32_t primask = npri >= 32 ? ~0u : (1u << npri) - 1u;
+  const int wcand = max(__builtin_amdgcn_readlane(ncand, 0), __builtin_amdgcn_readlane(ncand, 32));
 #pragma unroll 1
   for (int cls = 0; cls < 2; ++cls) {
 #pragma unroll 1
-    for (int ci = 0; ci < ncand; ++ci) {
-      const uint32_t bl = cneed[ci] & (cls == 0 ? primask : ~primask);
+    for (int ci = 0; ci < wcand; ++ci) {
+      const uint32_t bl = ci < ncand ? cneed[ci] & (cls == 0 ? primask : ~primask) : 0u;
       if ((bl >> lane) & 1u) pl[pend + __popc(bl & ((1u << lane) - 1u))] = (s.cand[ci] << 8) | lane;
       pend += __popc(bl);  // no barrier: the single wave's LDS operations complete in issue order
-      if (pend >= kPairsPerChunk) flush(kPairsPerChunk);
+      // wave-uniform flush decision (see above); the candidate loop runs to the wave's larger count
+      if (max(__builtin_amdgcn_readlane(pend, 0), __builtin_amdgcn_readlane(pend, 32)) >= kPairsPerChunk)
+        flush(pend < kPairsPerChunk ? pend : kPairsPerChunk);
     }
   }
   if (pend > 0) flush(pend);
