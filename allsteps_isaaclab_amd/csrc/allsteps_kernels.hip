@@ -1013,6 +1013,52 @@ __device__ __forceinline__ GeomC load_geom(const Consts& K, int lane) {
   return c;
 }
 
+// as_capsule_contact (include/as_detmath.h) without branches: every lane forms the three quotients of
+// the main path (s, then t, then the clamped-end s) and selects; the degenerate cases (a sphere: a or e
+// <= eps) reuse the same quotients with their own numerators.  The values selected are the same
+// operations on the same operands as the branchy form, so the same bits; a wave whose pairs take
+// different branches runs three divisions instead of up to six.
+__device__ __forceinline__ float capsule_contact_sel(const float* a1, const float* b1, float r1, const float* a2,
+                                                     const float* b2, float r2, float* P, float* n) {
+  float d1[3], d2[3], r[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    d1[k] = b1[k] - a1[k];
+    d2[k] = b2[k] - a2[k];
+    r[k] = a1[k] - a2[k];
+  }
+  const float a = as_dot3(d1, d1), e = as_dot3(d2, d2), f = as_dot3(d2, r);
+  const float eps = 1e-12f;
+  const bool pa = a <= eps, pe = e <= eps, gen = !pa && !pe;
+  const float c = as_dot3(d1, r);
+  const float b = as_dot3(d1, d2);
+  const float den = fmaf(a, e, -(b * b));
+  const float sm = den > 0.f ? as_clamp01(fmaf(b, f, -(c * e)) / den) : 0.f;
+  const float tq = (pa ? f : fmaf(b, sm, f)) / e;
+  const bool lo = gen && tq < 0.f, hi = gen && tq > 1.f;
+  const float sq = as_clamp01((hi ? b - c : -c) / a);
+  const float s = pa ? 0.f : (pe || lo || hi) ? sq : sm;
+  const float t = pa ? (pe ? 0.f : as_clamp01(tq)) : pe ? 0.f : lo ? 0.f : hi ? 1.f : tq;
+  float c1[3], c2[3], w[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    c1[k] = fmaf(s, d1[k], a1[k]);
+    c2[k] = fmaf(t, d2[k], a2[k]);
+    w[k] = c1[k] - c2[k];
+  }
+  const float dist = sqrtf(as_dot3(w, w));
+  const bool nz = dist > 1e-9f;
+  const float inv = 1.0f / dist;
+  n[0] = nz ? w[0] * inv : 0.f;
+  n[1] = nz ? w[1] * inv : 0.f;
+  n[2] = nz ? w[2] * inv : 1.f;
+  const float sep = dist - r1 - r2;
+  const float off = fmaf(0.5f, sep, r2);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) P[k] = fmaf(off, n[k], c2[k]);
+  return sep;
+}
+
 // At most ncap contacts, in priority order (oracle/physics.c collide() emits the same list); every
 // pair is still tested past the cap, and the contacts found beyond it are counted in s.ndrop:
 //   1. the priority geoms (the feet: geoms [0, num_priority_geoms)) against the candidate stones,
@@ -1213,7 +1259,8 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
   if (pend > 0) flush(pend);
   // self-contacts.  (A) lane = pair: the bounding-sphere filter; the surviving pairs are appended to
   // the pending list in table order.  (B) lane = pending pair, in chunks of G: the capsule-capsule
-  // closest points (include/as_detmath.h, shared with the oracle), emitted in list order.
+  // closest points (capsule_contact_sel: as_detmath.h's as_capsule_contact, which the oracle runs, in
+  // selects), emitted in list order.
   pend = 0;
   auto flush_self = [&](int npairs) {
     const bool act = lane < npairs;
@@ -1224,7 +1271,7 @@ __device__ __forceinline__ int collide(const Consts& K, EnvS& s, int lane, int n
     if (act) {
       const float* q1 = s.x.col.g[g1];
       const float* q2 = s.x.col.g[g2];
-      sep = as_capsule_contact(q1, q1 + 3, q1[6], q2, q2 + 3, q2[6], P, n);
+      sep = capsule_contact_sel(q1, q1 + 3, q1[6], q2, q2 + 3, q2[6], P, n);
       cnt = sep < margin;
       l1 = __float_as_int(q1[7]) >> 8;
       l2 = __float_as_int(q2[7]) >> 8;
